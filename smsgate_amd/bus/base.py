@@ -1,0 +1,285 @@
+"""Transport-agnostic durable pub/sub contract.
+
+The reference talks to NATS JetStream (libs/nats_utils.py):
+one stream ``SMS`` over five subjects, file storage, LIMITS retention with a
+3-day ``max_age``, durable consumers with explicit ack and server-default
+ack-wait redelivery, and ``consumer_info`` stats (``num_pending``,
+``num_ack_pending``).  This module defines the same semantics as an abstract
+:class:`Bus` with three implementations:
+
+* :class:`smsgate_amd.bus.memory.MemoryBus` — in-process (tests, benchmarks,
+  single-process deployments);
+* :class:`smsgate_amd.bus.server.BusServer` + :class:`smsgate_amd.bus.client.RemoteBus`
+  — a broker process with a crash-safe segment log (``smsgate_amd.bus.filelog``)
+  that any number of service processes reach over TCP/UDS;
+* ``nats://`` DSNs map to an optional NATS adapter when ``nats-py`` exists.
+
+Semantics (all backends):
+
+* every consumer is *durable* and *competing*: each stored message matching
+  its filter is handed to exactly one of the subscribers bound to that durable
+  name (the reference's intended ``--group`` scaling, worker.py:199-202, which
+  nats-py push consumers did not actually provide — SURVEY.md §2.10);
+* delivery is at-least-once: a message not acked within ``ack_wait`` is
+  redelivered; ``nak`` redelivers now (or after a delay); ``term`` drops it;
+  ``max_deliver`` bounds attempts (``-1`` = unbounded);
+* ``ensure_stream`` *creates* a missing stream (fixes D3) and updates subjects.
+"""
+from __future__ import annotations
+
+import abc
+import enum
+import time
+from dataclasses import dataclass
+from typing import AsyncIterator, Dict, List, Optional, Sequence, Tuple
+
+__all__ = [
+    "SUBJECT_RAW",
+    "SUBJECT_PARSED",
+    "SUBJECT_PROCESSING",
+    "SUBJECT_FAILED",
+    "SUBJECT_CATEGORIZED",
+    "STREAM_NAME",
+    "ALL_SUBJECTS",
+    "DeliverPolicy",
+    "StreamConfig",
+    "ConsumerConfig",
+    "PubAck",
+    "StreamInfo",
+    "ConsumerInfo",
+    "Msg",
+    "MsgMetadata",
+    "Acker",
+    "Subscription",
+    "Bus",
+    "BusError",
+    "subject_matches",
+    "default_stream_config",
+]
+
+# Subjects and stream of the reference (nats_utils.py:25-29, :64).
+SUBJECT_RAW = "sms.raw"
+SUBJECT_PARSED = "sms.parsed"
+SUBJECT_PROCESSING = "sms.processing"
+SUBJECT_FAILED = "sms.failed"
+SUBJECT_CATEGORIZED = "sms.categorized"
+STREAM_NAME = "SMS"
+ALL_SUBJECTS = (SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_FAILED, SUBJECT_PROCESSING, SUBJECT_CATEGORIZED)
+
+
+class BusError(RuntimeError):
+    pass
+
+
+class DeliverPolicy(str, enum.Enum):
+    ALL = "all"
+    NEW = "new"
+    LAST = "last"
+
+
+@dataclass
+class StreamConfig:
+    name: str
+    subjects: List[str]
+    max_age: float = 0.0  # seconds; 0 = unlimited
+    max_msgs: int = -1
+    max_bytes: int = -1
+    storage: str = "file"  # "file" | "memory" (memory bus ignores it)
+
+
+@dataclass
+class ConsumerConfig:
+    durable: str
+    filter_subject: str = ">"
+    ack_wait: float = 30.0
+    max_deliver: int = -1
+    deliver_policy: DeliverPolicy = DeliverPolicy.ALL
+    max_ack_pending: int = 65536
+
+    def __post_init__(self) -> None:
+        self.deliver_policy = DeliverPolicy(self.deliver_policy)
+
+
+@dataclass
+class PubAck:
+    stream: str
+    seq: int
+    duplicate: bool = False
+
+
+@dataclass
+class StreamInfo:
+    config: StreamConfig
+    messages: int
+    bytes: int
+    first_seq: int
+    last_seq: int
+    consumers: int
+
+
+@dataclass
+class ConsumerInfo:
+    stream: str
+    name: str
+    num_pending: int  # stored, matching, never delivered
+    num_ack_pending: int  # delivered, not yet acked
+    num_redelivered: int
+    delivered_seq: int
+    ack_floor: int
+    num_waiting: int = 0
+
+
+def subject_matches(pattern: str, subject: str) -> bool:
+    """NATS-style matching: ``*`` = one token, ``>`` = one or more trailing tokens."""
+    if pattern == subject or pattern == ">":
+        return True
+    pt = pattern.split(".")
+    st = subject.split(".")
+    for i, tok in enumerate(pt):
+        if tok == ">":
+            return len(st) > i
+        if i >= len(st):
+            return False
+        if tok != "*" and tok != st[i]:
+            return False
+    return len(pt) == len(st)
+
+
+def default_stream_config(max_age: float = 3 * 24 * 3600.0) -> StreamConfig:
+    """The reference's ``SMS`` stream (nats_utils.py:64-76): LIMITS, 3-day max_age."""
+    return StreamConfig(name=STREAM_NAME, subjects=list(ALL_SUBJECTS), max_age=max_age)
+
+
+@dataclass
+class MsgMetadata:
+    sequence: int
+    num_delivered: int
+    timestamp: float
+    stream: str
+    consumer: str
+
+
+class Msg:
+    """One delivered message.  ``data`` is bytes; ack/nak/term are idempotent."""
+
+    __slots__ = ("subject", "data", "headers", "metadata", "_acker", "_done")
+
+    def __init__(self, subject: str, data: bytes, metadata: MsgMetadata, acker: "Acker",
+                 headers: Optional[Dict[str, str]] = None) -> None:
+        self.subject = subject
+        self.data = data
+        self.headers = headers or {}
+        self.metadata = metadata
+        self._acker = acker
+        self._done = False
+
+    @property
+    def seq(self) -> int:
+        return self.metadata.sequence
+
+    async def ack(self) -> None:
+        if not self._done:
+            self._done = True
+            await self._acker.ack(self.metadata.stream, self.metadata.consumer, self.metadata.sequence)
+
+    async def nak(self, delay: float = 0.0) -> None:
+        if not self._done:
+            self._done = True
+            await self._acker.nak(self.metadata.stream, self.metadata.consumer, self.metadata.sequence, delay)
+
+    async def term(self) -> None:
+        if not self._done:
+            self._done = True
+            await self._acker.term(self.metadata.stream, self.metadata.consumer, self.metadata.sequence)
+
+    async def in_progress(self) -> None:
+        if not self._done:
+            await self._acker.touch(self.metadata.stream, self.metadata.consumer, self.metadata.sequence)
+
+    def json(self):
+        import json
+
+        return json.loads(self.data)
+
+    def __repr__(self) -> str:  # pragma: no cover
+        return f"Msg(subject={self.subject!r}, seq={self.seq}, len={len(self.data)})"
+
+
+class Acker(abc.ABC):
+    @abc.abstractmethod
+    async def ack(self, stream: str, consumer: str, seq: int) -> None: ...
+
+    @abc.abstractmethod
+    async def nak(self, stream: str, consumer: str, seq: int, delay: float) -> None: ...
+
+    @abc.abstractmethod
+    async def term(self, stream: str, consumer: str, seq: int) -> None: ...
+
+    @abc.abstractmethod
+    async def touch(self, stream: str, consumer: str, seq: int) -> None: ...
+
+
+class Subscription(abc.ABC):
+    """A binding to a durable consumer.  Several may share one durable."""
+
+    consumer: str
+
+    @abc.abstractmethod
+    async def fetch(self, batch: int = 1, timeout: Optional[float] = None) -> List[Msg]:
+        """Wait up to ``timeout`` (None = forever) for >=1 message, return <= batch."""
+
+    async def next_msg(self, timeout: Optional[float] = None) -> Optional[Msg]:
+        got = await self.fetch(1, timeout)
+        return got[0] if got else None
+
+    @property
+    def messages(self) -> AsyncIterator[Msg]:
+        return self._iter()
+
+    async def _iter(self) -> AsyncIterator[Msg]:
+        while True:
+            for m in await self.fetch(64, None):
+                yield m
+
+    @abc.abstractmethod
+    async def unsubscribe(self) -> None: ...
+
+
+class Bus(abc.ABC):
+    """Durable subject bus (the NATS JetStream role)."""
+
+    @abc.abstractmethod
+    async def ensure_stream(self, config: Optional[StreamConfig] = None) -> StreamInfo: ...
+
+    @abc.abstractmethod
+    async def publish(self, subject: str, data: bytes, headers: Optional[Dict[str, str]] = None) -> PubAck: ...
+
+    async def publish_many(self, items: Sequence[Tuple[str, bytes]]) -> List[PubAck]:
+        return [await self.publish(s, d) for s, d in items]
+
+    @abc.abstractmethod
+    async def subscribe(self, subject: str, durable: str, **consumer_opts) -> Subscription: ...
+
+    @abc.abstractmethod
+    async def consumer_info(self, stream: str, durable: str) -> ConsumerInfo: ...
+
+    @abc.abstractmethod
+    async def stream_info(self, stream: str) -> StreamInfo: ...
+
+    @abc.abstractmethod
+    async def ping(self) -> bool: ...
+
+    async def drain(self) -> None:
+        await self.close()
+
+    @abc.abstractmethod
+    async def close(self) -> None: ...
+
+    @property
+    def is_connected(self) -> bool:
+        return True
+
+
+def now() -> float:
+    return time.time()
+

@@ -1,0 +1,122 @@
+"""Wire-level domain objects shared by every stage of the pipeline.
+
+These are byte-compatible with the reference's JSON contracts
+(``libs/models.py:35-109``, ``libs/llm_core.py:9-19``):
+
+* :class:`RawSMS` travels on ``sms.raw``;
+* :class:`ParsedSMS` travels on ``sms.parsed`` / ``sms.processing``
+  (naive ISO dates, ``Decimal`` serialised as a string, upper-cased currency,
+  exactly-4-char card);
+* :class:`ParsedSmsCore` is the mini-schema an extraction backend must fill.
+
+Message identities keep the reference's two quirks (D9): the HTTP gateway uses
+``md5(message)`` (api_gateway/main.py:113) and the XML importer uses
+``sha1(body)`` (watcher.py:45).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import hashlib
+from decimal import Decimal
+from enum import Enum
+from typing import Literal, Optional
+
+from pydantic import BaseModel, Field, field_serializer, field_validator
+
+__all__ = [
+    "TxnType",
+    "RawSMS",
+    "ParsedSMS",
+    "ParsedSmsCore",
+    "get_md5_hash",
+    "get_sha1_hash",
+    "PARSER_VERSION_LLM",
+    "CORE_FIELDS",
+]
+
+PARSER_VERSION_LLM = "llm-0.2.0"  # gemini_parser.py:267
+
+
+class TxnType(str, Enum):
+    """Transaction class an SMS is mapped to."""
+
+    DEBIT = "debit"
+    CREDIT = "credit"
+    OTP = "otp"
+    UNKNOWN = "unknown"
+
+
+class RawSMS(BaseModel):
+    """An ingested, not-yet-understood SMS (``sms.raw`` payload)."""
+
+    msg_id: str
+    sender: str = Field(..., min_length=1)
+    body: str = Field(..., min_length=1)
+    date: str
+    device_id: Optional[str] = None
+    source: Literal["device", "xml"] = "device"
+
+
+class ParsedSMS(BaseModel):
+    """A fully normalised transaction (``sms.parsed`` payload)."""
+
+    msg_id: str
+    device_id: Optional[str]
+    sender: str
+    date: _dt.datetime
+    raw_body: str
+
+    txn_type: TxnType
+    amount: Optional[Decimal] = None
+    currency: Optional[str] = None
+    card: Optional[str] = Field(None, min_length=4, max_length=4)
+
+    merchant: Optional[str] = None
+    city: Optional[str] = None
+    address: Optional[str] = None
+
+    balance: Optional[Decimal] = None
+
+    parser_version: str = "0.1.0"
+
+    @field_validator("currency")
+    @classmethod
+    def _currency_upper(cls, v: Optional[str]) -> Optional[str]:
+        return v.upper() if v else v
+
+    @field_serializer("amount", "balance", when_used="json")
+    def _dec_str(self, v: Optional[Decimal]) -> Optional[str]:
+        return None if v is None else str(v)
+
+    @field_serializer("date", when_used="json")
+    def _iso(self, v: _dt.datetime) -> str:
+        return v.isoformat()
+
+
+class ParsedSmsCore(BaseModel):
+    """The extraction schema (what an LLM backend must produce)."""
+
+    txn_type: TxnType
+    date: _dt.datetime
+    amount: Optional[Decimal] = Field(None, ge=0)
+    currency: Optional[str]
+    card: Optional[str]
+    merchant: Optional[str]
+    city: Optional[str]
+    address: Optional[str]
+    balance: Optional[Decimal]
+
+
+#: Field order of the extraction schema — shared by prompts, FSM decoding and
+#: the Gemini response schema (gemini_parser.py:46-61).
+CORE_FIELDS = tuple(ParsedSmsCore.model_fields)
+
+
+def get_md5_hash(text: str) -> str:
+    """Gateway message id: hex md5 of the UTF-8 body (libs/models.py:97-109)."""
+    return hashlib.md5(text.encode("utf-8")).hexdigest()
+
+
+def get_sha1_hash(text: str) -> str:
+    """XML-import message id: hex sha1 of the UTF-8 body (watcher.py:45)."""
+    return hashlib.sha1(text.encode("utf-8")).hexdigest()

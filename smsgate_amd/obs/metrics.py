@@ -1,0 +1,110 @@
+"""Prometheus metrics of every service, under the reference's metric names.
+
+Parser worker (services/parser_worker/metrics.py:27-59) — served on
+``PARSER_METRICS_PORT`` (default 9102; the reference read ``METRICS_PORT``
+instead, metrics.py:109, and ``METRICS_PORT`` is still honoured):
+``sms_parsed_ok_total``, ``sms_parsed_fail_total``, ``sms_parsed_skip_total``,
+``sms_parser_stream_lag`` (now actually set from ``num_pending``),
+``sms_parser_processing_seconds`` (1 ms…5 s buckets), ``sms_parser_gemini_seconds``
+(the backend-call latency, whatever the backend), ``sms_parser_ack_pending``.
+
+Writer (services/pb_writer/writer.py:35-39, port 9103):
+``pb_writer_parsed_ok_total``, ``pb_writer_parsed_fail_total``, ``pb_writer_stream_lag``.
+
+Gateway (new — README.md:37 promised port 9101 but nothing was exported, D12):
+``api_gateway_requests_total{endpoint,status}``, ``api_gateway_publish_seconds``.
+
+Local LLM backend (new): ``llm_batch_size``, ``llm_step_seconds``,
+``llm_tokens_total{phase}``.
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+import os
+import threading
+from typing import Optional
+
+from prometheus_client import (
+    REGISTRY,
+    CollectorRegistry,
+    Counter,
+    Gauge,
+    Histogram,
+    Summary,
+    generate_latest,
+    start_http_server,
+)
+
+__all__ = [
+    "PARSED_OK",
+    "PARSED_FAIL",
+    "PARSED_SKIP",
+    "STREAM_LAG",
+    "PROCESSING_TIME",
+    "GEMINI_LATENCY",
+    "ACK_PENDING",
+    "WRITER_OK",
+    "WRITER_FAIL",
+    "WRITER_LAG",
+    "GATEWAY_REQUESTS",
+    "GATEWAY_PUBLISH_TIME",
+    "LLM_BATCH",
+    "LLM_STEP_TIME",
+    "LLM_TOKENS",
+    "start_metrics_server",
+    "render_latest",
+]
+
+log = logging.getLogger(__name__)
+
+PARSED_OK = Counter("sms_parsed_ok_total", "SMS successfully parsed (or skipped as non-transaction)")
+PARSED_FAIL = Counter("sms_parsed_fail_total", "SMS sent to the DLQ by the parser")
+PARSED_SKIP = Counter("sms_parsed_skip_total", "SMS skipped as broken (no card)")
+STREAM_LAG = Gauge("sms_parser_stream_lag", "Messages waiting for the parser consumer group")
+PROCESSING_TIME = Histogram(
+    "sms_parser_processing_seconds",
+    "Seconds spent parsing one message",
+    buckets=(0.001, 0.01, 0.05, 0.1, 0.25, 0.5, 1, 2, 5),
+)
+GEMINI_LATENCY = Summary("sms_parser_gemini_seconds", "Seconds spent in the extraction backend call")
+ACK_PENDING = Gauge("sms_parser_ack_pending", "Delivered-but-unacked messages of the parser consumer")
+
+WRITER_OK = Counter("pb_writer_parsed_ok_total", "Records saved by the writer")
+WRITER_FAIL = Counter("pb_writer_parsed_fail_total", "Records the writer failed to save")
+WRITER_LAG = Gauge("pb_writer_stream_lag", "sms.parsed consumer lag (messages)")
+
+GATEWAY_REQUESTS = Counter("api_gateway_requests_total", "HTTP requests", ["endpoint", "status"])
+GATEWAY_PUBLISH_TIME = Histogram("api_gateway_publish_seconds", "Seconds to publish one SMS to the bus")
+
+LLM_BATCH = Histogram("llm_batch_size", "Sequences per extraction batch", buckets=(1, 8, 32, 64, 128, 256, 512, 1024, 2048))
+LLM_STEP_TIME = Histogram("llm_step_seconds", "Seconds per engine step", ["phase"],
+                          buckets=(1e-4, 3e-4, 1e-3, 3e-3, 1e-2, 3e-2, 0.1, 0.3, 1.0))
+LLM_TOKENS = Counter("llm_tokens_total", "Tokens processed by the local extractor", ["phase"])
+
+_started: set[int] = set()
+_lock = threading.Lock()
+
+
+def start_metrics_server(port: Optional[int] = None, *, env_var: str = "METRICS_PORT",
+                         default: int = 9102, registry: CollectorRegistry = REGISTRY) -> Optional[int]:
+    """Serve ``/metrics`` from a daemon thread; idempotent per port.
+
+    Returns the port, or ``None`` if it could not be bound (the reference also
+    swallowed ``OSError`` here, metrics.py:110).
+    """
+    if port is None:
+        port = int(os.getenv(env_var, default))
+    with _lock:
+        if port in _started:
+            return port
+        with contextlib.suppress(OSError):
+            start_http_server(port, registry=registry)
+            _started.add(port)
+            log.info("Prometheus metrics on :%s/metrics", port)
+            return port
+    return None
+
+
+def render_latest(registry: CollectorRegistry = REGISTRY) -> bytes:
+    return generate_latest(registry)

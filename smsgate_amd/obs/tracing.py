@@ -1,0 +1,86 @@
+"""Lightweight transaction/span tracing.
+
+The reference wraps each parsed message in a Sentry transaction
+``task/process_parsing`` with spans ``check_stream``, ``validate``,
+``parsing``, ``validate_parsed``, ``publish`` (worker.py:33-55, :80-171).
+Here spans are recorded by an in-process :class:`Tracer` (per-span count and
+total/max duration, cheap enough for the hot path) and forwarded to Sentry when
+the SDK is active.  ``SMSGATE_TRACE=0`` disables recording entirely.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import threading
+import time
+from dataclasses import dataclass
+from typing import Dict, Iterator, Optional
+
+from . import errors
+
+__all__ = ["Tracer", "tracer", "start_transaction", "start_span", "SpanStats"]
+
+
+@dataclass
+class SpanStats:
+    count: int = 0
+    total_s: float = 0.0
+    max_s: float = 0.0
+
+    @property
+    def mean_s(self) -> float:
+        return self.total_s / self.count if self.count else 0.0
+
+
+class Tracer:
+    def __init__(self, enabled: bool = True) -> None:
+        self.enabled = enabled
+        self._stats: Dict[str, SpanStats] = {}
+        self._lock = threading.Lock()
+
+    def record(self, name: str, dt: float) -> None:
+        with self._lock:
+            s = self._stats.get(name)
+            if s is None:
+                s = self._stats[name] = SpanStats()
+            s.count += 1
+            s.total_s += dt
+            if dt > s.max_s:
+                s.max_s = dt
+
+    @contextlib.contextmanager
+    def span(self, name: str) -> Iterator[None]:
+        if not self.enabled:
+            yield
+            return
+        t0 = time.perf_counter()
+        sdk = errors._sdk
+        cm = sdk.start_span(name=name) if sdk is not None else contextlib.nullcontext()
+        try:
+            with cm:
+                yield
+        finally:
+            self.record(name, time.perf_counter() - t0)
+
+    def snapshot(self) -> Dict[str, SpanStats]:
+        with self._lock:
+            return {k: SpanStats(v.count, v.total_s, v.max_s) for k, v in self._stats.items()}
+
+    def reset(self) -> None:
+        with self._lock:
+            self._stats.clear()
+
+
+tracer = Tracer(enabled=os.getenv("SMSGATE_TRACE", "1") != "0")
+
+
+@contextlib.contextmanager
+def start_transaction(op: str, name: str) -> Iterator[None]:
+    sdk = errors._sdk
+    cm = sdk.start_transaction(op=op, name=name) if sdk is not None else contextlib.nullcontext()
+    with cm, tracer.span(f"{op}/{name}"):
+        yield
+
+
+def start_span(name: str, t: Optional[Tracer] = None):
+    return (t or tracer).span(name)

@@ -1,0 +1,77 @@
+"""Date/time normalisation chain of the parse pipeline.
+
+Behaviour-compatible with the reference helpers (golden-tested):
+
+* :func:`parse_custom_datetime` — ``'%d.%m.%y %H:%M'`` first, then a free-form
+  ``dateutil`` parse (gemini_parser.py:106-119).
+* :func:`parse_unix_timestamp` — seconds vs milliseconds auto-detection
+  (< 1e11 s, < 1e14 ms), conversion into an IANA zone, optionally naive
+  (gemini_parser.py:139-188).
+* :func:`fix_broken_datetime` — the first ``dd.mm.yyyy`` (else ``dd.mm.yy``)
+  date found in the SMS body overrides the *date part* of the LLM's answer
+  while its time of day is kept (gemini_parser.py:67-104). This repairs
+  day/month swaps made by the model.
+"""
+from __future__ import annotations
+
+import re
+import zoneinfo
+from datetime import datetime, timezone
+from typing import Union
+
+from dateutil.parser import parse as _du_parse
+
+__all__ = [
+    "parse_custom_datetime",
+    "parse_unix_timestamp",
+    "fix_broken_datetime",
+    "TimestampParseError",
+]
+
+_BODY_DATE_PATTERNS = (
+    (re.compile(r"\d{2}\.\d{2}\.\d{4}"), "%d.%m.%Y"),
+    (re.compile(r"\d{2}\.\d{2}\.\d{2}"), "%d.%m.%y"),
+)
+
+
+class TimestampParseError(ValueError):
+    """Raised for values that cannot be a Unix timestamp."""
+
+
+def parse_custom_datetime(text: str) -> datetime:
+    try:
+        return datetime.strptime(text, "%d.%m.%y %H:%M")
+    except Exception:
+        return _du_parse(text)
+
+
+def parse_unix_timestamp(ts: Union[int, float, str], tz: str = "UTC", aware: bool = True) -> datetime:
+    try:
+        num = float(ts)
+    except (TypeError, ValueError):
+        raise TimestampParseError(f"unsupported timestamp {ts!r}") from None
+    if num < 0:
+        raise TimestampParseError("negative timestamps are not supported")
+    if num < 1e11:
+        seconds = num
+    elif num < 1e14:
+        seconds = num / 1000.0
+    else:
+        raise TimestampParseError("value does not look like a Unix timestamp in s or ms")
+    local = datetime.fromtimestamp(seconds, tz=timezone.utc).astimezone(zoneinfo.ZoneInfo(tz))
+    return local if aware else local.replace(tzinfo=None)
+
+
+def fix_broken_datetime(body: str, current: datetime) -> datetime:
+    for rx, fmt in _BODY_DATE_PATTERNS:
+        m = rx.search(body)
+        if m is None:
+            continue
+        try:
+            day = datetime.strptime(m.group(0), fmt)
+        except ValueError:
+            continue
+        # ``time()`` drops tzinfo, exactly like the reference: a repaired date
+        # is naive local time.
+        return datetime.combine(day.date(), current.time())
+    return current

@@ -1,0 +1,185 @@
+"""Batched parse pipeline: pre-filter → normalise → cache → extract → post-process.
+
+Behaviour per message matches ``parse_sms_llm`` (gemini_parser.py:193-271):
+
+1. case-sensitive OTP pre-filter → ``UNMATCHED`` (the worker routes it to the
+   DLQ as ``{"reason": "unmatched"}``);
+2. body normalisation + card masking; cache key = sha256 of that body;
+3. extraction (cache hit or backend call; backend answers are cached *raw*,
+   so post-processing fixes apply on replay — SURVEY.md §5.4, D7);
+   a backend exception → ``ERROR`` (DLQ shape b);
+4. post-processing chain: date (strptime → dateutil → on "String does not
+   contain a date" the message timestamp in Asia/Yerevan → body-date repair),
+   card (strip ``*``/blanks, first 4), amount/balance via
+   :func:`parse_ambiguous_decimal` of ``str(value)`` (so ``None`` fails — D6,
+   kept as a contract), :class:`ParsedSmsCore` validation; any failure →
+   ``UNMATCHED`` (error captured unless ``txn_type == 'otp'``);
+5. ``address == "null"`` → ``""``; a card shorter than 4 chars → ``BROKEN``;
+6. build :class:`ParsedSMS` with ``parser_version = "llm-0.2.0"``.
+
+What is different is the execution model: a whole batch of messages is
+prepared, looked up in the cache with one query, the misses go to the backend
+in one :meth:`ParserBackend.extract_batch` call, and post-processing runs on
+the results — the reference did one synchronous HTTPS call per message.
+"""
+from __future__ import annotations
+
+import enum
+import time
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..models.domain import PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
+from ..obs.errors import sentry_capture
+from ..obs.metrics import GEMINI_LATENCY
+from .backends.base import BackendError, ParserBackend
+from .cache import MemoryKV, ResponseCache, cache_key
+from .dates import fix_broken_datetime, parse_custom_datetime, parse_unix_timestamp
+from .numeric import parse_ambiguous_decimal
+from .text import llm_should_skip, normalize_body
+
+__all__ = ["Outcome", "ParseResult", "ParsePipeline", "BrokenMessage", "postprocess_answer"]
+
+DEFAULT_TZ = "Asia/Yerevan"  # gemini_parser.py:229, Dockerfile TZ
+
+
+class BrokenMessage(Exception):
+    """The SMS parsed but carries no usable card number (gemini_parser.py:20-22)."""
+
+
+class Outcome(str, enum.Enum):
+    PARSED = "parsed"
+    UNMATCHED = "unmatched"
+    BROKEN = "broken"
+    ERROR = "error"
+
+
+@dataclass
+class ParseResult:
+    outcome: Outcome
+    parsed: Optional[ParsedSMS] = None
+    error: Optional[BaseException] = None
+    cached: bool = False
+
+
+def postprocess_answer(raw: RawSMS, fixed_body: str, answer: Dict[str, Any], tz: str = DEFAULT_TZ) -> ParseResult:
+    """Turn one raw extraction answer into a :class:`ParseResult`."""
+    resp = dict(answer)
+    try:
+        try:
+            resp["date"] = parse_custom_datetime(resp["date"])
+        except Exception as exc:
+            if "String does not contain a date" in str(exc):
+                resp["date"] = parse_unix_timestamp(int(raw.date), tz=tz, aware=False)
+        resp["date"] = fix_broken_datetime(raw.body, resp["date"])
+        card = resp["card"].replace("*", "").replace(" ", "")
+        resp["card"] = card[:4] if len(card) > 4 else card
+        resp["amount"] = parse_ambiguous_decimal(str(resp["amount"]))
+        resp["balance"] = parse_ambiguous_decimal(str(resp["balance"]))
+        core = ParsedSmsCore.model_validate(resp)
+    except Exception as exc:
+        if resp.get("txn_type") != "otp":
+            sentry_capture(exc, extras={"raw_body": raw.body[:4096]})
+        return ParseResult(Outcome.UNMATCHED, error=exc)
+
+    address = "" if core.address == "null" else core.address
+    if len(str(core.card)) < 4:
+        return ParseResult(Outcome.BROKEN, error=BrokenMessage("no card number in message"))
+    try:
+        parsed = ParsedSMS(
+            msg_id=raw.msg_id,
+            device_id=raw.device_id,
+            sender=raw.sender,
+            date=core.date,
+            raw_body=fixed_body,
+            txn_type=core.txn_type,
+            amount=core.amount,
+            currency=core.currency,
+            card=core.card,
+            merchant=core.merchant,
+            city=core.city,
+            address=address,
+            balance=core.balance,
+            parser_version=PARSER_VERSION_LLM,
+        )
+    except Exception as exc:  # e.g. a 5+ char card can't happen, but stay total
+        return ParseResult(Outcome.ERROR, error=exc)
+    return ParseResult(Outcome.PARSED, parsed=parsed)
+
+
+class ParsePipeline:
+    """Stateless-per-message, batched parse engine around one backend."""
+
+    def __init__(self, backend: ParserBackend, cache: Optional[ResponseCache] = None,
+                 tz: str = DEFAULT_TZ) -> None:
+        self.backend = backend
+        self.cache = cache if cache is not None else MemoryKV()
+        self.tz = tz
+        self.backend_calls = 0
+        self.backend_seconds = 0.0
+
+    async def parse(self, raw: RawSMS) -> ParseResult:
+        return (await self.parse_batch([raw]))[0]
+
+    async def parse_batch(self, raws: Sequence[RawSMS]) -> List[ParseResult]:
+        n = len(raws)
+        results: List[Optional[ParseResult]] = [None] * n
+        bodies: List[Optional[str]] = [None] * n
+        keys: List[Optional[str]] = [None] * n
+        todo: List[int] = []
+        for i, raw in enumerate(raws):
+            if llm_should_skip(raw.body):
+                results[i] = ParseResult(Outcome.UNMATCHED)
+                continue
+            fb = normalize_body(raw.body)
+            bodies[i] = fb
+            keys[i] = cache_key(fb)
+            todo.append(i)
+
+        answers: Dict[int, Any] = {}
+        cached: set = set()
+        if todo:
+            hits = self.cache.get_many([keys[i] for i in todo])  # type: ignore[misc]
+            miss: List[int] = []
+            for i, h in zip(todo, hits):
+                if h is None:
+                    miss.append(i)
+                else:
+                    answers[i] = h
+                    cached.add(i)
+            if miss:
+                # One backend call per unique body (duplicates in a batch share it).
+                uniq: Dict[str, List[int]] = {}
+                for i in miss:
+                    uniq.setdefault(bodies[i], []).append(i)  # type: ignore[arg-type]
+                ubodies = list(uniq)
+                t0 = time.perf_counter()
+                try:
+                    got = await self.backend.extract_batch(ubodies)
+                except Exception as exc:  # whole-batch failure
+                    got = [exc] * len(ubodies)
+                dt = time.perf_counter() - t0
+                self.backend_calls += 1
+                self.backend_seconds += dt
+                GEMINI_LATENCY.observe(dt / max(1, len(ubodies)))
+                to_cache = []
+                for b, r in zip(ubodies, got):
+                    if not isinstance(r, BaseException) and not isinstance(r, dict):
+                        r = BackendError(f"backend returned {type(r).__name__}, not a JSON object")
+                    for i in uniq[b]:
+                        answers[i] = r
+                    if isinstance(r, dict):
+                        to_cache.append((keys[uniq[b][0]], r))
+                if to_cache:
+                    self.cache.put_many(to_cache)
+
+        for i in todo:
+            ans = answers[i]
+            if isinstance(ans, BaseException):
+                sentry_capture(ans, extras={"raw_body": raws[i].body[:4096]})
+                results[i] = ParseResult(Outcome.ERROR, error=ans)
+            else:
+                r = postprocess_answer(raws[i], bodies[i], ans, self.tz)  # type: ignore[arg-type]
+                r.cached = i in cached
+                results[i] = r
+        return results  # type: ignore[return-value]

@@ -1,0 +1,72 @@
+"""Text-level steps of the parse pipeline: pre-filters, normalisation, JSON salvage.
+
+* :data:`WORKER_SKIP_KEYWORDS` / :func:`worker_should_skip` — the parser
+  worker's non-transaction filter (worker.py:112-121). Case-insensitive except
+  ``'Daily limit exceeded'``, which the reference matches case-sensitively.
+* :data:`LLM_SKIP_KEYWORDS` / :func:`llm_should_skip` — the parser's own OTP
+  pre-filter, case-sensitive (gemini_parser.py:198-199).
+* :func:`normalize_body` — NBSP→space, bullet→``*``, then
+  :func:`mask_card_number_with_prefix` (gemini_parser.py:202-203, 121-137).
+* :func:`extract_json` — greedy first-``{`` to last-``}`` salvage of a model
+  answer (gemini_parser.py:63-65).
+"""
+from __future__ import annotations
+
+import json
+import re
+from typing import Any, Optional
+
+__all__ = [
+    "WORKER_SKIP_KEYWORDS",
+    "LLM_SKIP_KEYWORDS",
+    "worker_should_skip",
+    "llm_should_skip",
+    "normalize_body",
+    "mask_card_number_with_prefix",
+    "extract_json",
+]
+
+#: Upper-cased substrings that make the worker ack-and-skip a message.
+WORKER_SKIP_KEYWORDS = (
+    "OTP",
+    "CODE:",
+    "NOT ENOUGH FUNDS",
+    "INSUFFICIENT FUNDS",
+    "CREDIT PAYMENT",
+    "C2C RECEIVED",
+    "PASS:",
+    "PASS=",
+    "PERSON TO PERSON",
+)
+_WORKER_SKIP_CASE_SENSITIVE = ("Daily limit exceeded",)
+
+#: Case-sensitive substrings for which the parser returns ``None`` (-> DLQ).
+LLM_SKIP_KEYWORDS = ("OTP", "CODE:", "PASS:", "PASS=", "Daily limit exceeded:")
+
+_CARD_RE = re.compile(r"\d{4}\*{3}(\d{4})")
+_JSON_RE = re.compile(r"\{.*\}", re.S)
+
+
+def worker_should_skip(body: str) -> bool:
+    up = body.upper()
+    return any(k in up for k in WORKER_SKIP_KEYWORDS) or any(
+        k in body for k in _WORKER_SKIP_CASE_SENSITIVE
+    )
+
+
+def llm_should_skip(body: str) -> bool:
+    return any(k in body for k in LLM_SKIP_KEYWORDS)
+
+
+def mask_card_number_with_prefix(text: str) -> str:
+    """``'4083***7538'`` → ``'CARD:7538'`` (every occurrence)."""
+    return _CARD_RE.sub(r"CARD:\1", text)
+
+
+def normalize_body(body: str) -> str:
+    return mask_card_number_with_prefix(body.replace("\u00a0", " ").replace("\u2022", "*"))
+
+
+def extract_json(text: str) -> Optional[Any]:
+    m = _JSON_RE.search(text)
+    return json.loads(m.group(0)) if m else None

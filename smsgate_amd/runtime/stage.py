@@ -1,0 +1,169 @@
+"""The consume → handle → ack runtime shared by every worker service.
+
+The reference copy-pastes one serial loop per service
+(``async for msg in sub.messages: await _process_one(...)`` — worker.py:206,
+writer.py:108, dlq_worker.py:89) and an exception escaping ``_process_one``
+silently kills that loop while the process stays up (D1/D2).  :class:`Stage`
+is the one loop, written once:
+
+* pulls *batches* from a durable competing consumer (``batch`` ≤ backend max);
+* runs up to ``concurrency`` batch handlers at once (I/O-bound handlers such as
+  a remote LLM or a database get overlap; a GPU handler gets a full batch);
+* never dies on a handler exception: the batch's un-acked messages are
+  ``nak``-ed with a backoff delay (redelivered later) and the error captured;
+* exports lag/ack-pending gauges from ``consumer_info`` on a timer;
+* drains in-flight batches on stop (graceful shutdown, worker.py:241-263).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+from typing import Awaitable, Callable, List, Optional, Sequence
+
+from ..bus.base import Bus, Msg, Subscription
+from ..obs.errors import sentry_capture
+
+__all__ = ["Stage", "BatchHandler"]
+
+log = logging.getLogger(__name__)
+
+BatchHandler = Callable[[Sequence[Msg]], Awaitable[None]]
+
+
+class Stage:
+    def __init__(
+        self,
+        bus: Bus,
+        subject: str,
+        durable: str,
+        handler: BatchHandler,
+        *,
+        batch: int = 64,
+        concurrency: int = 1,
+        fetch_timeout: float = 0.5,
+        ack_wait: float = 30.0,
+        max_deliver: int = -1,
+        nak_delay: float = 1.0,
+        stats_interval: float = 5.0,
+        on_stats: Optional[Callable[[int, int], None]] = None,
+        name: Optional[str] = None,
+    ) -> None:
+        self.bus = bus
+        self.subject = subject
+        self.durable = durable
+        self.handler = handler
+        self.batch = max(1, batch)
+        self.concurrency = max(1, concurrency)
+        self.fetch_timeout = fetch_timeout
+        self.ack_wait = ack_wait
+        self.max_deliver = max_deliver
+        self.nak_delay = nak_delay
+        self.stats_interval = stats_interval
+        self.on_stats = on_stats
+        self.name = name or durable
+        self.sub: Optional[Subscription] = None
+        self.processed = 0
+        self.batches = 0
+        self.handler_errors = 0
+        self._stop = asyncio.Event()
+        self._tasks: List[asyncio.Task] = []
+
+    async def open(self) -> Subscription:
+        if self.sub is None:
+            self.sub = await self.bus.subscribe(
+                self.subject, self.durable, ack_wait=self.ack_wait, max_deliver=self.max_deliver
+            )
+        return self.sub
+
+    async def _worker(self, wid: int) -> None:
+        sub = await self.open()
+        while not self._stop.is_set():
+            try:
+                msgs = await sub.fetch(self.batch, self.fetch_timeout)
+            except asyncio.CancelledError:
+                raise
+            except Exception as exc:  # bus hiccup: back off, keep running
+                log.warning("%s: fetch failed: %s", self.name, exc)
+                sentry_capture(exc, extras={"stage": self.name})
+                await asyncio.sleep(0.5)
+                continue
+            if not msgs:
+                continue
+            await self._run_batch(msgs)
+
+    async def _run_batch(self, msgs: Sequence[Msg]) -> None:
+        try:
+            await self.handler(msgs)
+        except asyncio.CancelledError:
+            raise
+        except Exception as exc:
+            self.handler_errors += 1
+            log.exception("%s: handler failed on a batch of %d", self.name, len(msgs))
+            sentry_capture(exc, extras={"stage": self.name, "batch": len(msgs)})
+            for m in msgs:
+                try:
+                    await m.nak(self.nak_delay)
+                except Exception:  # pragma: no cover
+                    pass
+        self.processed += len(msgs)
+        self.batches += 1
+
+    async def _stats(self) -> None:
+        while not self._stop.is_set():
+            try:
+                stream = getattr(self.sub, "stream", None) or "SMS"
+                info = await self.bus.consumer_info(stream, self.durable)
+                if self.on_stats is not None:
+                    self.on_stats(info.num_pending, info.num_ack_pending)
+            except Exception as exc:  # noqa: BLE001
+                log.debug("%s: stats failed: %s", self.name, exc)
+            try:
+                await asyncio.wait_for(self._stop.wait(), self.stats_interval)
+            except asyncio.TimeoutError:
+                pass
+
+    async def start(self) -> None:
+        await self.open()
+        self._stop.clear()
+        self._tasks = [asyncio.create_task(self._worker(i), name=f"{self.name}-w{i}")
+                       for i in range(self.concurrency)]
+        if self.on_stats is not None and self.stats_interval > 0:
+            self._tasks.append(asyncio.create_task(self._stats(), name=f"{self.name}-stats"))
+
+    async def stop(self, timeout: float = 10.0) -> None:
+        """Stop fetching, let in-flight batches finish (bounded), then cancel."""
+        self._stop.set()
+        if not self._tasks:
+            return
+        done, pending = await asyncio.wait(self._tasks, timeout=timeout)
+        for t in pending:
+            t.cancel()
+        for t in pending:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+        self._tasks = []
+
+    async def run(self, stop: Optional[asyncio.Event] = None) -> None:
+        await self.start()
+        try:
+            if stop is None:
+                await asyncio.gather(*self._tasks)
+            else:
+                await stop.wait()
+        finally:
+            await self.stop()
+
+    async def run_until_idle(self, idle_s: float = 0.2, max_s: float = 60.0) -> int:
+        """Test/benchmark helper: process until no message arrives for ``idle_s``."""
+        sub = await self.open()
+        t_end = time.monotonic() + max_s
+        n0 = self.processed
+        while time.monotonic() < t_end:
+            msgs = await sub.fetch(self.batch, idle_s)
+            if not msgs:
+                break
+            await self._run_batch(msgs)
+        return self.processed - n0

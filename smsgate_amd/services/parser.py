@@ -1,0 +1,192 @@
+"""Parser worker: ``sms.raw`` → parse → ``sms.parsed`` + ``sms.processing`` | ``sms.failed``.
+
+Routing is exactly the reference's ``_process_one`` (worker.py:74-189;
+SURVEY.md §3.2, envelope shapes §2.12), per message:
+
+====================================  ==============================================  =========
+condition                             published                                       metric
+====================================  ==============================================  =========
+payload not JSON / not a RawSMS       ``{"err", "entry": <payload str>}`` (a)         FAIL
+worker keyword skip (OTP, C2C …)      nothing                                         OK (D11)
+card missing (BrokenMessage)          nothing                                         SKIP
+backend raised                        ``{"err", "entry": RawSMS dict}`` (b)           FAIL
+unmatched / post-processing failed    ``{"reason": "unmatched", "raw": RawSMS}`` (c)  FAIL
+ParsedSMS re-validation failed        ``{"err", "entry": <payload str>}`` (d)         FAIL
+date in the future                    ``{"err": "Дата больше чем сегодня", …}`` (e)   FAIL
+parsed                                ParsedSMS JSON on parsed *and* processing      OK
+====================================  ==============================================  =========
+
+Every branch acks (after its publish), so poison messages never loop.
+A DLQ envelope carrying ``raw`` is unwrapped, so ``sms.failed`` entries can be
+re-fed (dlq ``--reparse``).
+
+Fixed defects: D1 (a malformed payload or future date no longer kills the
+loop: the decoded text is kept separately from the bytes), D2 (tz-aware dates
+are compared with an aware "now"), R4 (the backend is awaited — blocking
+backends run in threads, GPU backends batch), D3 (the stream is ensured once
+at start, not per message).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+from datetime import datetime, timezone
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_RAW, Bus, Msg
+from ..models.domain import ParsedSMS, RawSMS
+from ..obs import metrics as M
+from ..obs.errors import sentry_capture
+from ..obs.tracing import start_span, start_transaction
+from ..parse.pipeline import Outcome, ParsePipeline
+from ..parse.text import worker_should_skip
+from ..runtime.stage import Stage
+
+__all__ = ["ParserWorker", "FUTURE_DATE_ERR", "route_batch"]
+
+log = logging.getLogger("parser_worker")
+
+FUTURE_DATE_ERR = "Дата больше чем сегодня"
+
+
+def _is_future(dt: datetime) -> bool:
+    if dt.tzinfo is None:
+        return dt > datetime.now()
+    return dt > datetime.now(timezone.utc)
+
+
+def _dump(obj: Dict[str, Any]) -> bytes:
+    return json.dumps(obj).encode()
+
+
+async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[List[Tuple[str, bytes]], Dict[str, int]]:
+    """Decide every message's output. Returns ``(publishes, counters)``."""
+    out: List[Tuple[str, bytes]] = []
+    counts = {"ok": 0, "fail": 0, "skip": 0}
+    texts: List[str] = []
+    raws: List[RawSMS] = []
+    raw_idx: List[int] = []
+
+    with start_span("validate"):
+        for i, m in enumerate(msgs):
+            text = m.data.decode(errors="ignore") if isinstance(m.data, (bytes, bytearray)) else str(m.data)
+            texts.append(text)
+            try:
+                payload = json.loads(text)
+                if isinstance(payload, dict) and "raw" in payload:
+                    payload = payload["raw"]
+                raw = RawSMS(**payload)
+            except Exception as err:
+                out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))
+                counts["fail"] += 1
+                sentry_capture(err, extras={"raw_data": text})
+                continue
+            if worker_should_skip(raw.body):
+                counts["ok"] += 1
+                continue
+            raws.append(raw)
+            raw_idx.append(i)
+
+    if raws:
+        t0 = time.perf_counter()
+        with start_span("parsing"):
+            results = await pipeline.parse_batch(raws)
+        per_msg = (time.perf_counter() - t0) / len(raws)
+        for _ in raws:
+            M.PROCESSING_TIME.observe(per_msg)
+
+        with start_span("validate_parsed"):
+            for raw, i, res in zip(raws, raw_idx, results):
+                text = texts[i]
+                if res.outcome is Outcome.BROKEN:
+                    counts["skip"] += 1
+                    continue
+                if res.outcome is Outcome.ERROR:
+                    out.append((SUBJECT_FAILED, _dump({"err": str(res.error), "entry": raw.model_dump()})))
+                    counts["fail"] += 1
+                    continue
+                if res.outcome is Outcome.UNMATCHED or res.parsed is None:
+                    out.append((SUBJECT_FAILED, _dump({"reason": "unmatched", "raw": raw.model_dump()})))
+                    counts["fail"] += 1
+                    continue
+                try:
+                    parsed = ParsedSMS(**res.parsed.model_dump())
+                except Exception as err:
+                    sentry_capture(err, extras={"raw_data": text})
+                    out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))
+                    counts["fail"] += 1
+                    continue
+                if _is_future(parsed.date):
+                    sentry_capture(ValueError(FUTURE_DATE_ERR), extras={"raw_data": text})
+                    out.append((SUBJECT_FAILED, _dump({"err": FUTURE_DATE_ERR, "entry": text})))
+                    counts["fail"] += 1
+                    continue
+                payload = parsed.model_dump_json().encode()
+                out.append((SUBJECT_PARSED, payload))
+                out.append((SUBJECT_PROCESSING, payload))
+                counts["ok"] += 1
+    return out, counts
+
+
+class ParserWorker:
+    """The parser service: one :class:`Stage` over ``sms.raw`` + a :class:`ParsePipeline`."""
+
+    def __init__(self, bus: Bus, pipeline: ParsePipeline, *, group: str = "parser_worker",
+                 batch: Optional[int] = None, concurrency: int = 1, ack_wait: float = 30.0,
+                 stats_interval: float = 5.0) -> None:
+        self.bus = bus
+        self.pipeline = pipeline
+        self.group = group
+        self.counts = {"ok": 0, "fail": 0, "skip": 0}
+        self.stage = Stage(
+            bus,
+            SUBJECT_RAW,
+            group,
+            self.handle_batch,
+            batch=batch or pipeline.backend.max_batch,
+            concurrency=concurrency,
+            ack_wait=ack_wait,
+            stats_interval=stats_interval,
+            on_stats=self._on_stats,
+            name="parser_worker",
+        )
+
+    @staticmethod
+    def _on_stats(num_pending: int, num_ack_pending: int) -> None:
+        M.STREAM_LAG.set(num_pending)
+        M.ACK_PENDING.set(num_ack_pending)
+
+    async def handle_batch(self, msgs: Sequence[Msg]) -> None:
+        with start_transaction("task", "process_parsing"):
+            publishes, counts = await route_batch(self.pipeline, msgs)
+            with start_span("publish"):
+                if publishes:
+                    await self.bus.publish_many(publishes)
+                for m in msgs:
+                    await m.ack()
+        if counts["ok"]:
+            M.PARSED_OK.inc(counts["ok"])
+        if counts["fail"]:
+            M.PARSED_FAIL.inc(counts["fail"])
+        if counts["skip"]:
+            M.PARSED_SKIP.inc(counts["skip"])
+        for k, v in counts.items():
+            self.counts[k] += v
+
+    async def start(self) -> None:
+        await self.bus.ensure_stream()
+        await self.pipeline.backend.start()
+        await self.stage.start()
+
+    async def stop(self) -> None:
+        await self.stage.stop()
+        await self.pipeline.backend.close()
+
+    async def run(self, stop: Optional[asyncio.Event] = None) -> None:
+        await self.start()
+        try:
+            await (stop.wait() if stop is not None else asyncio.Event().wait())
+        finally:
+            await self.stop()

@@ -1,0 +1,106 @@
+"""SQL sink: ``INSERT … ON CONFLICT (msg_id) DO UPDATE`` (pb_writer/upsert.py:7-33).
+
+The reference used SQLAlchemy's async engine over asyncpg; neither asyncpg nor
+aiosqlite is on the image, so this sink drives a *synchronous* SQLAlchemy
+engine from a worker thread (``asyncio.to_thread``) — same SQL, no event-loop
+blocking.  Works for PostgreSQL and SQLite URLs.  A whole batch is one
+statement and one transaction.  Errors propagate (the reference swallowed them
+into Sentry, so "OK" could mean "only PocketBase written" — D4).
+"""
+from __future__ import annotations
+
+import asyncio
+from typing import Any, Dict, List, Optional, Sequence
+
+from sqlalchemy import create_engine, delete, select, update
+from sqlalchemy.engine import Engine
+
+from ..db import migrations
+from ..db.schema import UPSERT_EXCLUDED, parsed_to_row, sms_data
+from ..models.domain import ParsedSMS
+from .base import Sink
+
+__all__ = ["SqlSink", "make_engine"]
+
+
+def make_engine(url: str, **kw: Any) -> Engine:
+    if url.startswith("sqlite"):
+        kw.setdefault("connect_args", {"check_same_thread": False})
+    else:
+        kw.setdefault("pool_size", 10)  # db/session.py:9
+    return create_engine(url, **kw)
+
+
+def _insert_for(engine: Engine):
+    if engine.dialect.name == "postgresql":
+        from sqlalchemy.dialects.postgresql import insert
+    elif engine.dialect.name == "sqlite":
+        from sqlalchemy.dialects.sqlite import insert
+    else:  # pragma: no cover
+        raise NotImplementedError(f"upsert not implemented for {engine.dialect.name}")
+    return insert
+
+
+class SqlSink(Sink):
+    name = "sql"
+
+    def __init__(self, url: str, *, migrate: bool = True, engine: Optional[Engine] = None) -> None:
+        self.url = url
+        self.engine = engine or make_engine(url)
+        self._insert = _insert_for(self.engine)
+        if migrate:
+            migrations.upgrade(self.engine)
+
+    # -- sync core (runs in a thread) ------------------------------------------------
+    def upsert_rows_sync(self, rows: List[Dict[str, Any]]) -> None:
+        if not rows:
+            return
+        # Deduplicate inside one statement (ON CONFLICT can't touch a row twice).
+        by_id: Dict[Any, Dict[str, Any]] = {}
+        for r in rows:
+            by_id[r["msg_id"]] = r
+        stmt = self._insert(sms_data).values(list(by_id.values()))
+        stmt = stmt.on_conflict_do_update(
+            index_elements=["msg_id"],
+            set_={c.name: stmt.excluded[c.name] for c in sms_data.columns if c.name not in UPSERT_EXCLUDED},
+        )
+        with self.engine.begin() as conn:
+            conn.execute(stmt)
+
+    async def upsert_many(self, records: Sequence[ParsedSMS]) -> None:
+        rows = [parsed_to_row(r) for r in records]
+        await asyncio.to_thread(self.upsert_rows_sync, rows)
+
+    async def upsert_dict(self, parsed: Dict[str, Any]) -> None:
+        """``upsert_parsed_sms(dict)`` of the reference (takes a ParsedSMS dump)."""
+        await self.upsert_many([ParsedSMS.model_validate(parsed)])
+
+    # -- query helpers used by the MCP tools ------------------------------------------
+    def get_by_id(self, record_id: int) -> Optional[Dict[str, Any]]:
+        with self.engine.connect() as c:
+            row = c.execute(select(sms_data).where(sms_data.c.id == record_id)).mappings().first()
+            return dict(row) if row else None
+
+    def find(self, conditions: List[Any]) -> List[Dict[str, Any]]:
+        q = select(sms_data)
+        if conditions:
+            q = q.where(*conditions)
+        with self.engine.connect() as c:
+            return [dict(r) for r in c.execute(q.order_by(sms_data.c.id)).mappings()]
+
+    def update_by_id(self, record_id: int, values: Dict[str, Any]) -> int:
+        with self.engine.begin() as c:
+            return c.execute(update(sms_data).where(sms_data.c.id == record_id).values(**values)).rowcount
+
+    def delete_by_id(self, record_id: int) -> int:
+        with self.engine.begin() as c:
+            return c.execute(delete(sms_data).where(sms_data.c.id == record_id)).rowcount
+
+    def count(self) -> int:
+        from sqlalchemy import func
+
+        with self.engine.connect() as c:
+            return int(c.execute(select(func.count()).select_from(sms_data)).scalar())
+
+    async def close(self) -> None:
+        self.engine.dispose()

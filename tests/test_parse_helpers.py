@@ -1,0 +1,133 @@
+"""Golden behaviours captured from the reference's helpers.
+
+Each value here was produced by executing the reference code (gemini_parser.py,
+decimal_utils.py, models.py); quirks are contracts and pinned as such.
+"""
+from datetime import datetime, timezone
+from decimal import Decimal
+
+import pytest
+from pydantic import ValidationError
+
+from smsgate_amd.models import ParsedSMS, RawSMS, get_md5_hash, get_sha1_hash
+from smsgate_amd.parse import (
+    extract_json,
+    fix_broken_datetime,
+    llm_should_skip,
+    mask_card_number_with_prefix,
+    normalize_body,
+    parse_ambiguous_decimal,
+    parse_custom_datetime,
+    parse_unix_timestamp,
+    worker_should_skip,
+)
+
+
+@pytest.mark.parametrize(
+    "text, expected",
+    [
+        ("79,825.89", "79825.89"),
+        ("79.825,89", "79825.89"),
+        ("79 825,89", "79825.89"),
+        ("1,234,567.89", "1234567.89"),
+        ("1.234.567,89", "1234567.89"),
+        ("123456", "123456"),
+        ("123.45", "123.45"),
+        ("1,23", "1.23"),
+        ("1,000", "1.000"),  # quirk: a single comma is a decimal mark
+        ("999,999", "999.999"),
+        ("1.234.567", "1234.567"),  # quirk: the comment at decimal_utils.py:50 claims 1234567
+        ("", "0.0"),
+        ("52.00 USD", "52.00"),
+        ("-5,5", "-5.5"),
+    ],
+)
+def test_parse_ambiguous_decimal_golden(text, expected):
+    got = parse_ambiguous_decimal(text)
+    assert got == Decimal(expected)
+    assert str(got) == expected
+
+
+def test_parse_ambiguous_decimal_rejects_none_string():
+    # D6: str(None) == 'None' -> ValueError, so null amounts go to the DLQ.
+    with pytest.raises(ValueError):
+        parse_ambiguous_decimal("None")
+
+
+def test_parse_ambiguous_decimal_non_string():
+    assert parse_ambiguous_decimal(5) == Decimal(5)
+
+
+def test_mask_card_number():
+    assert mask_card_number_with_prefix("DEBIT 4083***7538, x 1234***5678") == "DEBIT CARD:7538, x CARD:5678"
+    assert mask_card_number_with_prefix("card ***0018.") == "card ***0018."
+
+
+def test_normalize_body():
+    assert normalize_body("A B •••1234 4083***7538") == "A B ***1234 CARD:7538"
+
+
+def test_parse_custom_datetime():
+    assert parse_custom_datetime("06.05.25 14:23") == datetime(2025, 5, 6, 14, 23)
+    assert parse_custom_datetime("2025-06-10 20:51") == datetime(2025, 6, 10, 20, 51)
+
+
+def test_fix_broken_datetime():
+    assert fix_broken_datetime("foo 10.06.2025 20:51", datetime(2025, 10, 6, 20, 51)) == datetime(2025, 6, 10, 20, 51)
+    assert fix_broken_datetime("no date here", datetime(2025, 10, 6, 20, 51)) == datetime(2025, 10, 6, 20, 51)
+    # two-digit year form
+    assert fix_broken_datetime("x 06.05.25 14:23", datetime(2025, 6, 5, 14, 23)) == datetime(2025, 5, 6, 14, 23)
+
+
+def test_parse_unix_timestamp():
+    assert parse_unix_timestamp(1749808562, tz="Asia/Yerevan", aware=False) == datetime(2025, 6, 13, 13, 56, 2)
+    ms = parse_unix_timestamp("1749808562123")
+    assert ms == datetime(2025, 6, 13, 9, 56, 2, 123000, tzinfo=timezone.utc)
+    with pytest.raises(ValueError):
+        parse_unix_timestamp(-1)
+    with pytest.raises(ValueError):
+        parse_unix_timestamp(1e15)
+    with pytest.raises(ValueError):
+        parse_unix_timestamp("abc")
+
+
+def test_extract_json():
+    assert extract_json('```json\n{"a":1}\n``` trailing') == {"a": 1}
+    assert extract_json("no json") is None
+
+
+def test_skip_filters():
+    assert worker_should_skip("your otp is 1234")  # upper-cased match
+    assert worker_should_skip("C2C received 100 AMD")
+    assert worker_should_skip("Daily limit exceeded")
+    assert not worker_should_skip("daily limit exceeded")  # case-sensitive in the reference
+    assert not worker_should_skip("APPROVED PURCHASE DB SALE: X")
+    assert llm_should_skip("Your OTP: 1")
+    assert not llm_should_skip("your otp: 1")  # the parser's filter is case-sensitive
+
+
+def test_md5_sha1_ids():
+    assert get_md5_hash("APPROVED PURCHASE DB SALE: …") == "ba20eeee04a7b49c06131ff1403e8fa4"
+    assert get_sha1_hash("abc") == "a9993e364706816aba3e25717850c26c9cd0d89d"
+
+
+def test_rawsms_validation_contracts():
+    with pytest.raises(ValidationError):
+        RawSMS(msg_id="x", sender="", body="b", date="1")
+    with pytest.raises(ValidationError):
+        RawSMS(msg_id="x", sender="s", body="b", date="1", source=None)
+    r = RawSMS(msg_id="x", sender="s", body="b", date="1")
+    assert r.source == "device" and r.device_id is None
+
+
+def test_parsedsms_contracts():
+    with pytest.raises(ValidationError):
+        ParsedSMS(msg_id="m", device_id=None, sender="s", date=datetime(2025, 1, 1), raw_body="b",
+                  txn_type="debit", card="018")
+    p = ParsedSMS(msg_id="m", device_id=None, sender="s", date=datetime(2025, 5, 6, 14, 23), raw_body="b",
+                  txn_type="debit", amount=Decimal("52.00"), currency="usd", card="0018", parser_version="llm-0.2.0")
+    js = p.model_dump_json()
+    assert '"date":"2025-05-06T14:23:00"' in js
+    assert '"amount":"52.00"' in js
+    assert '"currency":"USD"' in js
+    assert ParsedSMS.model_validate_json(js) == p

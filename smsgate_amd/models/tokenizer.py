@@ -1,0 +1,110 @@
+"""Byte-level BPE tokenizer of the local extractor.
+
+No pretrained tokenizer files exist on the box, so the extractor's tokenizer is
+trained in-repo (``python -m smsgate_amd.models.tokenizer --train``) with the
+Rust ``tokenizers`` library on the synthetic SMS corpus
+(:mod:`smsgate_amd.utils.synth`) plus the system prompt, and committed as
+``assets/extractor_tokenizer.json``.  Byte-level BPE never fails on unseen
+text (Cyrillic, emoji…): unknown strings fall back to byte tokens.
+
+Special tokens: ``<pad> <bos> <eos> <sep> <sms> <ans>``.  The prompt of one
+extraction is ``<bos> SYSTEM_INSTRUCTION`` (shared prefix, cached once on
+the GPU) + ``<sms> body <ans>`` (per message); the answer is the nine field
+values in schema order, each terminated by ``<sep>``.
+"""
+from __future__ import annotations
+
+import functools
+from pathlib import Path
+from typing import List, Sequence
+
+__all__ = ["ExtractorTokenizer", "SPECIALS", "load_tokenizer", "train_tokenizer", "ASSET"]
+
+ASSET = Path(__file__).resolve().parent / "assets" / "extractor_tokenizer.json"
+SPECIALS = ["<pad>", "<bos>", "<eos>", "<sep>", "<sms>", "<ans>"]
+DEFAULT_VOCAB = 8192
+
+
+def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: int = 60000, seed: int = 1234):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    from ..parse.schema import SYSTEM_INSTRUCTION
+    from ..utils.synth import iter_corpus
+
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    trainer = trainers.BpeTrainer(
+        vocab_size=vocab_size,
+        special_tokens=SPECIALS,
+        initial_alphabet=pre_tokenizers.ByteLevel.alphabet(),
+        show_progress=False,
+    )
+
+    def corpus():
+        for _ in range(50):
+            yield SYSTEM_INSTRUCTION
+        yield from iter_corpus(n_sms, seed)
+
+    tok.train_from_iterator(corpus(), trainer=trainer)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    tok.save(str(path))
+    return tok
+
+
+class ExtractorTokenizer:
+    def __init__(self, path: Path = ASSET) -> None:
+        from tokenizers import Tokenizer
+
+        if not Path(path).exists():
+            train_tokenizer(Path(path))
+        self.tk = Tokenizer.from_file(str(path))
+        self.vocab_size = self.tk.get_vocab_size()
+        ids = {s: self.tk.token_to_id(s) for s in SPECIALS}
+        self.pad, self.bos, self.eos, self.sep, self.sms, self.ans = (ids[s] for s in SPECIALS)
+
+    def encode(self, text: str) -> List[int]:
+        return self.tk.encode(text, add_special_tokens=False).ids
+
+    def encode_batch(self, texts: Sequence[str]) -> List[List[int]]:
+        return [e.ids for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
+
+    def decode(self, ids: Sequence[int]) -> str:
+        return self.tk.decode(list(ids), skip_special_tokens=True)
+
+    @functools.cached_property
+    def token_strings(self) -> List[str]:
+        """Decoded text of every id (specials → their literal)."""
+        out = []
+        for i in range(self.vocab_size):
+            s = self.tk.id_to_token(i)
+            out.append(s if s in SPECIALS else self.tk.decode([i], skip_special_tokens=False))
+        return out
+
+    def prefix_ids(self, system: str) -> List[int]:
+        return [self.bos] + self.encode(system)
+
+    def message_ids(self, bodies: Sequence[str], max_body: int) -> List[List[int]]:
+        enc = self.encode_batch(bodies)
+        return [[self.sms] + e[:max_body] + [self.ans] for e in enc]
+
+
+@functools.lru_cache(maxsize=4)
+def load_tokenizer(path: str = str(ASSET)) -> ExtractorTokenizer:
+    return ExtractorTokenizer(Path(path))
+
+
+if __name__ == "__main__":
+    import sys
+    import time
+
+    if "--train" in sys.argv:
+        t0 = time.time()
+        tk = train_tokenizer()
+        print(f"trained vocab={tk.get_vocab_size()} in {time.time() - t0:.1f}s -> {ASSET}")
+    t = load_tokenizer()
+    from ..utils.synth import reference_cases
+
+    for b in reference_cases():
+        ids = t.encode(b)
+        print(len(b), "chars ->", len(ids), "tokens")

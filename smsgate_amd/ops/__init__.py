@@ -1,0 +1,240 @@
+"""HIP/CDNA4 kernels of the local extractor LM, exposed to PyTorch.
+
+The kernels live in ``csrc/llm_kernels.hip`` and are built in-tree for gfx950
+(``smsgate_amd.ops.build``).  Each wrapper here validates shapes/dtypes on the
+host *before* launching (a mis-shaped launch on the GPU box can fault the
+device), then launches on ``torch.cuda.current_stream()`` — so the calls are
+captured by ``torch.cuda.CUDAGraph``.
+
+There is deliberately **no silent fallback**: on a GPU, a missing library is
+an error (``SMSGATE_ALLOW_TORCH_OPS=1`` opts into the slow PyTorch reference
+path, for debugging only).  The ``ref_*`` functions are the fp32 PyTorch
+references the numerics tests compare against.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Optional
+
+import torch
+
+from . import build as _build
+
+__all__ = [
+    "load_library",
+    "have_kernels",
+    "rmsnorm_residual",
+    "silu_mul",
+    "rope_qkv_cache",
+    "attn_prefill",
+    "attn_decode",
+    "fsm_sample",
+    "rope_table",
+    "ref_rmsnorm",
+    "ref_silu_mul",
+    "ref_rope",
+    "ref_attention",
+]
+
+_lib: Optional[ctypes.CDLL] = None
+_c_int = ctypes.c_int
+_c_float = ctypes.c_float
+_vp = ctypes.c_void_p
+_ip = ctypes.c_void_p  # int32 device pointers travel as void*
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    lib.sg_rmsnorm_residual.argtypes = [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_float, _vp]
+    lib.sg_silu_mul.argtypes = [_vp, _vp, _c_int, _c_int, _vp]
+    lib.sg_rope_qkv_cache.argtypes = [_vp, _ip, _ip, _vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp]
+    lib.sg_attn_prefill.argtypes = [_vp, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
+                                    _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
+    lib.sg_attn_decode.argtypes = [_vp, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
+                                   _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
+    lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
+                                  _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
+                                  ctypes.c_uint, _vp]
+    for f in ("sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
+              "sg_fsm_sample", "sg_version"):
+        getattr(lib, f).restype = _c_int
+
+
+def load_library(build_if_missing: bool = True) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if build_if_missing and _build.needs_build():
+        _build.build()
+    if not path.exists():
+        raise RuntimeError(f"HIP kernel library missing: {path} (run python -m smsgate_amd.ops.build)")
+    lib = ctypes.CDLL(str(path))
+    _declare(lib)
+    _lib = lib
+    return lib
+
+
+def have_kernels() -> bool:
+    try:
+        load_library()
+        return True
+    except Exception:
+        return False
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (rc={rc})")
+
+
+def _req(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+
+
+# ---------------------------------------------------------------------------- ops
+def rmsnorm_residual(residual: torch.Tensor, weight: torch.Tensor, eps: float,
+                     x: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``residual += x`` (in place, if given); returns ``rmsnorm(residual) * weight``."""
+    T, H = residual.shape
+    _req(residual, torch.bfloat16, "residual")
+    _req(weight, torch.bfloat16, "weight")
+    if x is not None:
+        _req(x, torch.bfloat16, "x")
+        assert x.shape == residual.shape
+    if out is None:
+        out = torch.empty_like(residual)
+    assert weight.numel() == H and out.shape == residual.shape
+    _check(load_library().sg_rmsnorm_residual(_p(x), _p(residual), _p(weight), _p(out), T, H, eps, _stream()),
+           "rmsnorm_residual")
+    return out
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    T, I2 = gu.shape
+    _req(gu, torch.bfloat16, "gu")
+    I = I2 // 2
+    if out is None:
+        out = gu.new_empty((T, I))
+    assert out.shape == (T, I)
+    _check(load_library().sg_silu_mul(_p(gu), _p(out), T, I, _stream()), "silu_mul")
+    return out
+
+
+def rope_table(max_pos: int, head_dim: int, theta: float, device) -> torch.Tensor:
+    """``[max_pos, head_dim/2, 2]`` fp32 (cos, sin) — computed once on the host side (Appendix B)."""
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    ang = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).to(torch.float32).contiguous().to(device)
+
+
+def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor,
+                   q_out: torch.Tensor, k_cache: torch.Tensor, vt_cache: torch.Tensor,
+                   nh: int, nkv: int, head_dim: int, p0: int) -> None:
+    T = qkv.shape[0]
+    _req(qkv, torch.bfloat16, "qkv")
+    _req(pos, torch.int32, "pos")
+    _req(slot, torch.int32, "slot")
+    _req(cos_sin, torch.float32, "cos_sin")
+    S, nkv_, Lmax, D = k_cache.shape
+    assert qkv.shape[1] == (nh + 2 * nkv) * head_dim and D == head_dim and nkv_ == nkv
+    assert vt_cache.shape == (S, nkv, D, Lmax)
+    assert q_out.shape[0] >= T and q_out.numel() >= T * nh * D
+    assert pos.numel() == T and slot.numel() == T
+    _check(load_library().sg_rope_qkv_cache(_p(qkv), _p(pos), _p(slot), _p(cos_sin), _p(q_out), _p(k_cache),
+                                            _p(vt_cache), T, nh, nkv, D, Lmax, p0, _stream()), "rope_qkv_cache")
+
+
+def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slot: torch.Tensor, max_q: int,
+                 k_cache: torch.Tensor, vt_cache: torch.Tensor, pk: torch.Tensor, pvt: torch.Tensor, P0: int,
+                 out: torch.Tensor, scale: float) -> torch.Tensor:
+    """Causal varlen attention. ``q``: [T, nh, D]; sequence ``b`` owns rows
+    ``cu_q[b]:cu_q[b+1]`` whose own offsets start at ``q_start[b]``; keys are the
+    shared prefix (``pk``/``pvt``, ``P0`` valid of ``P0pad``) followed by the slot's own keys."""
+    T, nh, D = q.shape
+    S, nkv, Lmax, _ = k_cache.shape
+    P0pad = pk.shape[1]
+    nseq = cu_q.numel() - 1
+    assert pk.shape == (nkv, P0pad, D) and pvt.shape == (nkv, D, P0pad)
+    assert slot.numel() == nseq and q_start.numel() == nseq and P0 <= P0pad
+    _check(load_library().sg_attn_prefill(_p(q), _p(cu_q), _p(q_start), _p(slot), _p(k_cache), _p(vt_cache),
+                                          _p(pk), _p(pvt), P0, P0pad, _p(out), nseq, max_q, nh, nkv, D, Lmax,
+                                          scale, _stream()), "attn_prefill")
+    return out
+
+
+def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache: torch.Tensor,
+                vt_cache: torch.Tensor, pk: torch.Tensor, pvt: torch.Tensor, P0: int, out: torch.Tensor,
+                scale: float) -> torch.Tensor:
+    B, nh, D = q.shape
+    S, nkv, Lmax, _ = k_cache.shape
+    P0pad = pk.shape[1]
+    assert pos.numel() == B and slot.numel() == B
+    _check(load_library().sg_attn_decode(_p(q), _p(pos), _p(slot), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt),
+                                         P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, _stream()), "attn_decode")
+    return out
+
+
+def fsm_sample(logits: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tensor, out_buf: torch.Tensor,
+               out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, slot_id: torch.Tensor,
+               temperature: float, seed: int, row_map: Optional[torch.Tensor] = None) -> None:
+    """Masked argmax/Gumbel sampling + FSM transition for ``B = logits.shape[0]`` rows.
+
+    Logits row ``i`` updates state row ``row_map[i]`` (or ``i``)."""
+    B, V = logits.shape
+    ldl = logits.stride(0)
+    assert logits.dtype == torch.bfloat16 and logits.stride(1) == 1
+    max_out = out_buf.shape[1]
+    inv_t = 0.0 if temperature <= 0 else 1.0 / temperature
+    _check(load_library().sg_fsm_sample(
+        _p(logits), ldl, _p(fsm.masks), _p(fsm.state_mask), _p(state), _p(fsm.next_sep_t), _p(fsm.next_tok_t),
+        _p(fsm.enum_tok_t), _p(fsm.enum_next_t), fsm.E, fsm.sep_token, fsm.done_state, _p(tok_io), _p(out_buf),
+        _p(out_len), _p(done), _p(pos), _p(slot_id), _p(row_map), max_out, V, B, inv_t, seed & 0xFFFFFFFF,
+        _stream()),
+        "fsm_sample")
+
+
+# ------------------------------------------------------------------ references
+def ref_rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+
+
+def ref_silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    g, u = gu.float().chunk(2, dim=-1)
+    return torch.nn.functional.silu(g) * u
+
+
+def ref_rope(x: torch.Tensor, positions: torch.Tensor, theta: float) -> torch.Tensor:
+    """rotate-half RoPE in fp32; ``x``: [T, H, D], ``positions``: [T]."""
+    D = x.shape[-1]
+    inv = 1.0 / (theta ** (torch.arange(0, D, 2, dtype=torch.float64, device=x.device) / D))
+    ang = positions.double()[:, None] * inv[None, :]
+    cos, sin = ang.cos().float()[:, None, :], ang.sin().float()[:, None, :]
+    x1, x2 = x.float()[..., : D // 2], x.float()[..., D // 2:]
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+
+
+def ref_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: torch.Tensor, scale: float) -> torch.Tensor:
+    """fp32 attention. q [nq, D], k/v [nk, D], mask [nq, nk] bool (True = attend)."""
+    s = (q.float() @ k.float().t()) * scale
+    s = s.masked_fill(~mask, float("-inf"))
+    return torch.softmax(s, dim=-1) @ v.float()
+
+
+def default_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim)

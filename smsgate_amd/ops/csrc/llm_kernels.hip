@@ -1,0 +1,609 @@
+// smsgate_amd — HIP/CDNA4 (gfx950) kernels for the local extraction LM.
+//
+// Plain C ABI (extern "C"), launched on a caller-supplied hipStream_t so every
+// launch is capturable into a hipGraph by torch.cuda.CUDAGraph; no allocation,
+// no synchronisation inside a launch function (cdna_hip_programming.md G9).
+//
+// Kernels (all bf16 storage, fp32 math):
+//   sg_rmsnorm_residual  residual += x (optional); out = rmsnorm(residual) * w
+//   sg_silu_mul          out = silu(gu[:, :I]) * gu[:, I:]
+//   sg_rope_qkv_cache    RoPE(q,k) + write K rows / V^T columns into the KV cache
+//   sg_attn_prefill      varlen causal attention over [shared prefix | own keys],
+//                        MFMA 16x16x32 bf16, one wave per 16 query rows
+//   sg_attn_decode       one query token per sequence, GQA group per workgroup
+//   sg_fsm_sample        schema-FSM masked argmax / Gumbel sampling + FSM step
+//
+// KV layout (memory sized for 288 GB HBM: every slot owns its rows, no paging):
+//   K   [slots][nkv][Lmax][D]   (a key row is 128 contiguous bytes at D = 64)
+//   V^T [slots][nkv][D][Lmax]   (transposed so 8 consecutive keys of one dim are
+//                                one 16-byte load: the MFMA B operand of P·V)
+// Key index space of a sequence = [prefix keys 0..P0pad) ++ [own keys]:
+// the shared system-prompt prefix lives once in pk/pvt (zero padded to a
+// multiple of 32 keys), own keys live in the slot, RoPE position = P0 + own offset.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define WAVE 64
+
+static __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+static __device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 on gfx950: RNE, NaN stays NaN
+  return __builtin_bit_cast(uint16_t, b);
+}
+static __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+static __device__ __forceinline__ uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+static __device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, WAVE));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// RMSNorm (+ residual add). One wave per row, 4 rows per 256-thread block.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rmsnorm_residual_kernel(const uint16_t* __restrict__ x_in,
+                                                               uint16_t* __restrict__ residual,
+                                                               const uint16_t* __restrict__ w,
+                                                               uint16_t* __restrict__ out, int T, int H,
+                                                               float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= T) return;
+  const int nvec = H >> 3;
+  uint4* r4 = reinterpret_cast<uint4*>(residual + (size_t)row * H);
+  const uint4* x4 = x_in ? reinterpret_cast<const uint4*>(x_in + (size_t)row * H) : nullptr;
+  float ss = 0.f;
+  for (int c = lane; c < nvec; c += WAVE) {
+    float a[8];
+    unpack8(r4[c], a);
+    if (x4) {
+      float b[8];
+      unpack8(x4[c], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = bf2f(f2bf(a[j] + b[j]));  // residual stream stays bf16
+      r4[c] = pack8(a);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)H + eps);
+  const uint4* w4 = reinterpret_cast<const uint4*>(w);
+  uint4* o4 = reinterpret_cast<uint4*>(out + (size_t)row * H);
+  for (int c = lane; c < nvec; c += WAVE) {
+    float a[8], g[8];
+    unpack8(r4[c], a);
+    unpack8(w4[c], g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = a[j] * r * g[j];
+    o4[c] = pack8(a);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SwiGLU activation: out[t, i] = silu(gu[t, i]) * gu[t, I + i]; 8 elements/thread.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                       int T, int I) {
+  const int nv = I >> 3;
+  const long total = (long)T * nv;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const long t = idx / nv;
+    const int c = (int)(idx - t * nv);
+    const uint4* row = reinterpret_cast<const uint4*>(gu + (size_t)t * 2 * I);
+    float g[8], u[8];
+    unpack8(row[c], g);
+    unpack8(row[nv + c], u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
+    reinterpret_cast<uint4*>(out + (size_t)t * I)[c] = pack8(g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// RoPE on q and k (rotate-half convention) + KV-cache write. One block/token.
+//   qkv    [T][(nh + 2 nkv) D]    (GEMM output)
+//   pos    [T] own offset of the token; RoPE position = p0 + pos
+//   slot   [T] cache slot
+//   cs     [max_pos][D/2] float2 (cos, sin)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rope_qkv_cache_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ pos,
+                                                             const int* __restrict__ slot, const float2* __restrict__ cs,
+                                                             uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
+                                                             uint16_t* __restrict__ vt_cache, int nh, int nkv, int D,
+                                                             int Lmax, int p0) {
+  const int t = blockIdx.x;
+  const int half = D >> 1;
+  const int p = pos[t];
+  const int s = slot[t];
+  const float2* cst = cs + (size_t)(p0 + p) * half;
+  const uint16_t* src = qkv + (size_t)t * (nh + 2 * nkv) * D;
+  const int nrot = (nh + nkv) * half;
+  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
+    const int h = it / half;
+    const int i = it - h * half;
+    const float2 c = cst[i];
+    const float x1 = bf2f(src[h * D + i]);
+    const float x2 = bf2f(src[h * D + i + half]);
+    const float y1 = x1 * c.x - x2 * c.y;
+    const float y2 = x2 * c.x + x1 * c.y;
+    if (h < nh) {
+      uint16_t* q = q_out + ((size_t)t * nh + h) * D;
+      q[i] = f2bf(y1);
+      q[i + half] = f2bf(y2);
+    } else {
+      const int kh = h - nh;
+      uint16_t* k = k_cache + (((size_t)s * nkv + kh) * Lmax + p) * D;
+      k[i] = f2bf(y1);
+      k[i + half] = f2bf(y2);
+    }
+  }
+  const uint16_t* v = src + (nh + nkv) * D;
+  for (int it = threadIdx.x; it < nkv * D; it += blockDim.x) {
+    const int kh = it / D;
+    const int d = it - kh * D;
+    vt_cache[(((size_t)s * nkv + kh) * D + d) * Lmax + p] = v[it];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Prefill attention (varlen, causal), D = 64, MFMA 16x16x32 bf16.
+// grid = (ceil(max_q / 16), nseq, nh); block = one wave.
+//   S = Q K^T   : A = Q (lane: row l&15, dims 8(l>>4)+j+32s), B = K^T (lane: key l&15)
+//                 acc: S[q = 4(l>>4)+i][key = l&15]
+//   O += P V    : A = P (via LDS, lane: row l&15, keys 8(l>>4)+j),
+//                 B = V (lane: keys 8(l>>4)+j, dim l&15 (+16n)) = one 16-B load of V^T
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) attn_prefill_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
+    const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out,
+    int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int tile = blockIdx.x, b = blockIdx.y, h = blockIdx.z;
+  const int l = threadIdx.x;
+  const int qbeg = cu_q[b];
+  const int qlen = cu_q[b + 1] - qbeg;
+  if (tile * 16 >= qlen) return;
+  const int G = nh / nkv;
+  const int kh = h / G;
+  const int g4 = l >> 4, r16 = l & 15;
+  const int qs = q_start[b];
+  const int sl = slot[b];
+
+  __shared__ __attribute__((aligned(16))) uint16_t P_lds[16 * 32];
+
+  // Q fragments (two k-steps of 32 dims)
+  bf16x8 qa[2];
+  {
+    const int row = tile * 16 + r16;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < qlen) v = *reinterpret_cast<const uint4*>(q + ((size_t)(qbeg + row) * nh + h) * D + 8 * g4 + 32 * s);
+      qa[s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  // own offsets of the 4 query rows this lane accumulates (S/O layout)
+  int qoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qoff[i] = qs + tile * 16 + 4 * g4 + i;
+  const int last_row = min(tile * 16 + 15, qlen - 1);
+  const int own_keys = qs + last_row + 1;  // own keys needed by this tile
+  const int nkeys = P0pad + own_keys;
+
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[4], lsum[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m[i] = -INFINITY; lsum[i] = 0.f; }
+
+  for (int kt = 0; kt < nkeys; kt += 32) {
+    const bool pre = kt < P0pad;  // tiles never straddle: P0pad % 32 == 0
+    f32x4 sacc[2];
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const int key = kt + 16 * hs + r16;
+      sacc[hs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint4 kv = make_uint4(0, 0, 0, 0);
+        if (key < nkeys) {
+          const uint16_t* krow = pre ? (kpre + (size_t)key * D) : (kself + (size_t)(key - P0pad) * D);
+          kv = *reinterpret_cast<const uint4*>(krow + 8 * g4 + 32 * s);
+        }
+        sacc[hs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], __builtin_bit_cast(bf16x8, kv), sacc[hs], 0, 0, 0);
+      }
+    }
+    // mask + scale, tile row max
+    float sv[2][4];
+    float tmax[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tmax[i] = -INFINITY;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const int key = kt + 16 * hs + r16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool ok;
+        if (pre) ok = key < P0;
+        else ok = (key - P0pad) <= qoff[i];
+        const float v = ok ? sacc[hs][i] * scale_log2 : -INFINITY;
+        sv[hs][i] = v;
+        tmax[i] = fmaxf(tmax[i], v);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o2 = 8; o2 > 0; o2 >>= 1) tmax[i] = fmaxf(tmax[i], __shfl_xor(tmax[i], o2, WAVE));
+    }
+    float alpha[4], rs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float mn = fmaxf(m[i], tmax[i]);
+      alpha[i] = (mn == -INFINITY) ? 1.f : exp2f(m[i] - mn);
+      m[i] = mn;
+      rs[i] = 0.f;
+    }
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = (m[i] == -INFINITY) ? 0.f : exp2f(sv[hs][i] - m[i]);
+        rs[i] += p;
+        P_lds[(4 * g4 + i) * 32 + 16 * hs + r16] = f2bf(p);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o2 = 8; o2 > 0; o2 >>= 1) rs[i] += __shfl_xor(rs[i], o2, WAVE);
+      lsum[i] = lsum[i] * alpha[i] + rs[i];
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[n][i] *= alpha[i];
+    }
+    __syncthreads();
+    const bf16x8 pa = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&P_lds[r16 * 32 + 8 * g4]));
+    const int kk = kt + 8 * g4;  // first of this lane's 8 keys
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int d = 16 * n + r16;
+      uint4 vv = make_uint4(0, 0, 0, 0);
+      if (kk < nkeys) {
+        const uint16_t* vrow = pre ? (vpre + (size_t)d * P0pad + kk) : (vself + (size_t)d * Lmax + (kk - P0pad));
+        vv = *reinterpret_cast<const uint4*>(vrow);
+      }
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vv), o[n], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = tile * 16 + 4 * g4 + i;
+    if (row >= qlen) continue;
+    const float inv = lsum[i] > 0.f ? 1.f / lsum[i] : 0.f;
+    uint16_t* orow = out + ((size_t)(qbeg + row) * nh + h) * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) orow[16 * n + r16] = f2bf(o[n][i] * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Decode attention: one query token per sequence. grid = (B, nkv), block 256.
+// Phase 1: scores of the G = nh/nkv heads for every key (8 lanes per key row).
+// Phase 2: softmax. Phase 3: P·V with lane = dim, 4 contiguous key ranges.
+// ---------------------------------------------------------------------------
+#define DEC_MAXCTX 1024
+#define DEC_MAXG 4
+__global__ void __launch_bounds__(256) attn_decode_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache, const uint16_t* __restrict__ pk,
+    const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out, int nh, int nkv, int Lmax,
+    float scale_log2) {
+  constexpr int D = 64;
+  const int b = blockIdx.x, kh = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = nh / nkv;
+  const int own = pos[b] + 1;  // own keys 0..pos inclusive
+  const int sl = slot[b];
+  const int nk = P0 + own;     // logical keys: prefix [0,P0) then own
+  __shared__ float sc[DEC_MAXG][DEC_MAXCTX];
+  __shared__ float red[4][DEC_MAXG][D];
+  __shared__ float stat[2][DEC_MAXG];
+
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+
+  // phase 1 ------------------------------------------------------------------
+  const int dc = lane & 7;
+  float qf[DEC_MAXG][8];
+#pragma unroll
+  for (int g = 0; g < DEC_MAXG; ++g) {
+    if (g < G) {
+      uint4 v = *reinterpret_cast<const uint4*>(q + ((size_t)b * nh + kh * G + g) * D + 8 * dc);
+      unpack8(v, qf[g]);
+    }
+  }
+  for (int k = wid * 8 + (lane >> 3); k < nk; k += 32) {
+    const uint16_t* krow = (k < P0) ? (kpre + (size_t)k * D) : (kself + (size_t)(k - P0) * D);
+    float kf[8];
+    unpack8(*reinterpret_cast<const uint4*>(krow + 8 * dc), kf);
+#pragma unroll
+    for (int g = 0; g < DEC_MAXG; ++g) {
+      if (g < G) {
+        float acc = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += qf[g][j] * kf[j];
+        acc += __shfl_xor(acc, 1, WAVE);
+        acc += __shfl_xor(acc, 2, WAVE);
+        acc += __shfl_xor(acc, 4, WAVE);
+        if (dc == 0) sc[g][k] = acc * scale_log2;
+      }
+    }
+  }
+  __syncthreads();
+  // phase 2 ------------------------------------------------------------------
+  for (int g = 0; g < G; ++g) {
+    float mx = -INFINITY;
+    for (int k = tid; k < nk; k += 256) mx = fmaxf(mx, sc[g][k]);
+    mx = wave_max(mx);
+    if (lane == 0) red[wid][g][0] = mx;
+  }
+  __syncthreads();
+  if (tid < G) stat[0][tid] = fmaxf(fmaxf(red[0][tid][0], red[1][tid][0]), fmaxf(red[2][tid][0], red[3][tid][0]));
+  __syncthreads();
+  for (int g = 0; g < G; ++g) {
+    const float mx = stat[0][g];
+    float sm = 0.f;
+    for (int k = tid; k < nk; k += 256) {
+      const float p = exp2f(sc[g][k] - mx);
+      sc[g][k] = p;
+      sm += p;
+    }
+    sm = wave_sum(sm);
+    if (lane == 0) red[wid][g][1] = sm;
+  }
+  __syncthreads();
+  if (tid < G) stat[1][tid] = red[0][tid][1] + red[1][tid][1] + red[2][tid][1] + red[3][tid][1];
+  __syncthreads();
+  // phase 3 ------------------------------------------------------------------
+  const int d = lane;
+  float acc[DEC_MAXG];
+#pragma unroll
+  for (int g = 0; g < DEC_MAXG; ++g) acc[g] = 0.f;
+  // prefix keys [0, P0): chunked by 8, split over the 4 waves
+  {
+    const int nch = (P0 + 7) >> 3;
+    for (int c = wid; c < nch; c += 4) {
+      float vf[8];
+      unpack8(*reinterpret_cast<const uint4*>(vpre + (size_t)d * P0pad + 8 * c), vf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * c + j;
+        if (k < P0) {
+#pragma unroll
+          for (int g = 0; g < DEC_MAXG; ++g)
+            if (g < G) acc[g] += sc[g][k] * vf[j];
+        }
+      }
+    }
+    const int nch2 = (own + 7) >> 3;
+    for (int c = wid; c < nch2; c += 4) {
+      float vf[8];
+      unpack8(*reinterpret_cast<const uint4*>(vself + (size_t)d * Lmax + 8 * c), vf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * c + j;
+        if (k < own) {
+#pragma unroll
+          for (int g = 0; g < DEC_MAXG; ++g)
+            if (g < G) acc[g] += sc[g][P0 + k] * vf[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < DEC_MAXG; ++g)
+    if (g < G) red[wid][g][d] = acc[g];
+  __syncthreads();
+  if (wid == 0) {
+    for (int g = 0; g < G; ++g) {
+      const float v = red[0][g][d] + red[1][g][d] + red[2][g][d] + red[3][g][d];
+      out[((size_t)b * nh + kh * G + g) * D + d] = f2bf(v / stat[1][g]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schema-FSM constrained sampling + FSM transition, fully on the GPU (so many
+// decode steps can be replayed from one captured graph without a host sync).
+// One 256-thread block per sequence row.
+// ---------------------------------------------------------------------------
+static __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u ^ (c + 0x165667B1u) * 0xC2B2AE3Du;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+
+__global__ void __launch_bounds__(256) fsm_sample_kernel(
+    const uint16_t* __restrict__ logits, int ldl, const uint32_t* __restrict__ masks, const int* __restrict__ state_mask,
+    int* __restrict__ state, const int* __restrict__ next_sep, const int* __restrict__ next_tok,
+    const int* __restrict__ enum_tok, const int* __restrict__ enum_next, int E, int sep_token, int done_state,
+    int* __restrict__ tok_io, int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done,
+    int* __restrict__ pos, const int* __restrict__ slot_id, const int* __restrict__ row_map, int max_out, int V,
+    float inv_temp, uint32_t seed) {
+  const int lr = blockIdx.x;                      // logits row
+  const int b = row_map ? row_map[lr] : lr;       // state row
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  if (done[b]) return;  // block-uniform
+  const int s = state[b];
+  const uint32_t* mrow = masks + (size_t)state_mask[s] * (V >> 5);
+  const uint16_t* lrow = logits + (size_t)lr * ldl;
+  const uint32_t rseed = hash3(seed, (uint32_t)slot_id[b], (uint32_t)out_len[b]);
+  float best = -INFINITY;
+  int besti = 0x7fffffff;
+  const int nvec = V >> 3;
+  for (int c = tid; c < nvec; c += 256) {
+    const uint32_t bits = (mrow[c >> 2] >> ((c & 3) * 8)) & 0xffu;
+    if (!bits) continue;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(lrow + 8 * c), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (bits & (1u << j)) {
+        const int idx = 8 * c + j;
+        float v = f[j];
+        if (inv_temp > 0.f) {
+          const uint32_t hsh = hash3(rseed, (uint32_t)idx, 0x51ED270Bu);
+          const float u = ((hsh >> 8) + 0.5f) * (1.0f / 16777216.0f);
+          v = v * inv_temp - __logf(-__logf(u));
+        }
+        if (v > best || (v == best && idx < besti)) { best = v; besti = idx; }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, WAVE);
+    const int oi = __shfl_xor(besti, o, WAVE);
+    if (ov > best || (ov == best && oi < besti)) { best = ov; besti = oi; }
+  }
+  if (lane == 0) { bv[wid] = best; bi[wid] = besti; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w)
+      if (bv[w] > best || (bv[w] == best && bi[w] < besti)) { best = bv[w]; besti = bi[w]; }
+    int tok = (besti == 0x7fffffff) ? sep_token : besti;
+    int ns;
+    if (tok == sep_token) {
+      ns = next_sep[s];
+    } else {
+      ns = next_tok[s];
+      if (E > 0 && ns == -2) {  // enum/trie state: sparse transition list
+        ns = -1;
+        for (int e = 0; e < E; ++e)
+          if (enum_tok[s * E + e] == tok) { ns = enum_next[s * E + e]; break; }
+      }
+    }
+    const int len = out_len[b];
+    out_buf[(size_t)b * max_out + len] = tok;
+    out_len[b] = len + 1;
+    tok_io[b] = tok;
+    state[b] = ns < 0 ? done_state : ns;
+    if (ns < 0 || ns == done_state || len + 1 >= max_out) {
+      done[b] = 1;
+    } else {
+      pos[b] = pos[b] + 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int sg_rmsnorm_residual(const void* x_in, void* residual, const void* w, void* out, int T, int H, float eps,
+                        hipStream_t stream) {
+  if (H % 8) return -1;
+  if (T == 0) return 0;
+  dim3 grid((T + 3) / 4);
+  hipLaunchKernelGGL(rmsnorm_residual_kernel, grid, dim3(256), 0, stream, (const uint16_t*)x_in, (uint16_t*)residual,
+                     (const uint16_t*)w, (uint16_t*)out, T, H, eps);
+  return (int)hipGetLastError();
+}
+
+int sg_silu_mul(const void* gu, void* out, int T, int I, hipStream_t stream) {
+  if (I % 8) return -1;
+  if (T == 0) return 0;
+  long total = (long)T * (I / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)out, T, I);
+  return (int)hipGetLastError();
+}
+
+int sg_rope_qkv_cache(const void* qkv, const int* pos, const int* slot, const void* cos_sin, void* q_out,
+                      void* k_cache, void* vt_cache, int T, int nh, int nkv, int D, int Lmax, int p0,
+                      hipStream_t stream) {
+  if (D % 2) return -1;
+  if (T == 0) return 0;
+  hipLaunchKernelGGL(rope_qkv_cache_kernel, dim3(T), dim3(256), 0, stream, (const uint16_t*)qkv, pos, slot,
+                     (const float2*)cos_sin, (uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)vt_cache, nh, nkv, D,
+                     Lmax, p0);
+  return (int)hipGetLastError();
+}
+
+int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const int* slot, const void* k_cache,
+                    const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int nseq,
+                    int max_q, int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || (P0pad % 32) || (Lmax % 8) || nh % nkv) return -1;
+  if (nseq == 0 || max_q == 0) return 0;
+  dim3 grid((max_q + 15) / 16, nseq, nh);
+  hipLaunchKernelGGL(attn_prefill_kernel, grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, slot,
+                     (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt,
+                     P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+int sg_attn_decode(const void* q, const int* pos, const int* slot, const void* k_cache, const void* vt_cache,
+                   const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh, int nkv, int D,
+                   int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > DEC_MAXG || P0 + Lmax > DEC_MAXCTX || (P0pad % 8) || (Lmax % 8)) return -1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(attn_decode_kernel, dim3(B, nkv), dim3(256), 0, stream, (const uint16_t*)q, pos, slot,
+                     (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt, P0,
+                     P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+int sg_fsm_sample(const void* logits, int ldl, const void* masks, const int* state_mask, int* state,
+                  const int* next_sep, const int* next_tok, const int* enum_tok, const int* enum_next, int E,
+                  int sep_token, int done_state, int* tok_io, int* out_buf, int* out_len, int* done, int* pos,
+                  const int* slot_id, const int* row_map, int max_out, int V, int B, float inv_temp,
+                  unsigned int seed, hipStream_t stream) {
+  if (V % 32 || ldl % 8) return -1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(fsm_sample_kernel, dim3(B), dim3(256), 0, stream, (const uint16_t*)logits, ldl,
+                     (const uint32_t*)masks, state_mask, state, next_sep, next_tok, enum_tok, enum_next, E, sep_token,
+                     done_state, tok_io, out_buf, out_len, done, pos, slot_id, row_map, max_out, V, inv_temp, seed);
+  return (int)hipGetLastError();
+}
+
+int sg_version() { return 1; }
+
+}  // extern "C"

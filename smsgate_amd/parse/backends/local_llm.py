@@ -1,0 +1,91 @@
+"""``local_llm`` backend: the extraction LM served on this process's MI355X.
+
+Replaces the remote ``call_gemini`` (gemini_parser.py:273-292) behind the same
+boundary.  Answers have the Gemini JSON shape (nine string fields) so the
+post-processing chain is unchanged.  One backend instance = one GPU = one
+engine thread; under ``torchrun`` every rank builds its own (data-parallel
+replicas consuming ``sms.raw`` as one competing consumer group —
+:mod:`smsgate_amd.parallel`).
+
+Weights: ``LLM_CHECKPOINT`` (safetensors, serving layout) or random-init of
+the named architecture (``LLM_MODEL``, default ``smollm-135m``) — the box has
+no pretrained checkpoint, so random-init output values are schema-valid but
+semantically meaningless and post-processing routes them to the DLQ.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, List, Optional, Sequence
+
+from .base import BackendError, ExtractResult, ParserBackend
+
+__all__ = ["LocalLLMBackend", "build_engine"]
+
+
+def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
+                 seed: int = 0, **engine_kw: Any):
+    import torch
+
+    from ...models.extractor import CONFIGS, ExtractorWeights
+    from ...models.tokenizer import load_tokenizer
+    from ...serving.engine import EngineConfig, ExtractionEngine
+
+    cfg = CONFIGS[model]
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    if checkpoint:
+        w = ExtractorWeights.load(checkpoint, cfg, device=dev)
+    else:
+        w = ExtractorWeights(cfg, device=dev, seed=seed)
+    w.requires_grad_(False)
+    return ExtractionEngine(w, load_tokenizer(), EngineConfig(**engine_kw))
+
+
+class LocalLLMBackend(ParserBackend):
+    name = "local_llm"
+
+    def __init__(self, model: Optional[str] = None, checkpoint: Optional[str] = None, device: Optional[str] = None,
+                 max_slots: int = 1024, max_batch: Optional[int] = None, **engine_kw: Any) -> None:
+        self.model = model or os.getenv("LLM_MODEL", "smollm-135m")
+        self.checkpoint = checkpoint or os.getenv("LLM_CHECKPOINT") or None
+        self.device = device or os.getenv("LLM_DEVICE", "cuda")
+        self.engine_kw = dict(max_slots=max_slots, **engine_kw)
+        self.max_batch = max_batch or max_slots
+        self._worker = None
+
+    async def start(self) -> None:
+        if self._worker is not None:
+            return
+        import asyncio
+
+        from ...serving.worker import EngineWorker
+
+        w = EngineWorker(lambda: build_engine(self.model, self.checkpoint, self.device, **self.engine_kw))
+        await asyncio.to_thread(w.start)
+        self._worker = w
+
+    async def close(self) -> None:
+        if self._worker is not None:
+            import asyncio
+
+            await asyncio.to_thread(self._worker.stop)
+            self._worker = None
+
+    @property
+    def engine(self):
+        return None if self._worker is None else self._worker.engine
+
+    async def extract_batch(self, bodies: Sequence[str]) -> List[ExtractResult]:
+        if self._worker is None:
+            await self.start()
+        res = await self._worker.extract(bodies)  # type: ignore[union-attr]
+        out: List[ExtractResult] = []
+        for r in res:
+            if isinstance(r, BaseException):
+                out.append(r)
+            elif r is None:
+                out.append(BackendError("local LLM produced no answer"))
+            else:
+                out.append(dict(r))
+        return out

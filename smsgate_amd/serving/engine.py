@@ -1,0 +1,387 @@
+"""GPU extraction engine: continuous batching over a slot-resident KV cache.
+
+One engine = one MI355X = one data-parallel replica (``smsgate_amd.parallel``).
+
+Per engine:
+
+* **weights** in serving layout (270 MB bf16 for the 135M extractor);
+* **KV cache** ``K[L][slots][nkv][Lmax][D]`` and ``V^T[L][slots][nkv][D][Lmax]``,
+  zero-initialised, one fixed region per slot — at ~4.6 MB/slot (135M model,
+  ``Lmax`` 200) thousands of concurrent sequences fit in 288 GB, so there is no
+  paging/block-table indirection in the attention kernels;
+* **shared prefix**: the system prompt (``<bos> SYSTEM_INSTRUCTION``) is run
+  once at start-up into ``pk``/``pvt``; every sequence attends to it without
+  recomputing or copying it (and its K/V stay L2-resident across the batch);
+* **per-row device state** (token, position, FSM state, done flag, output
+  buffer) so the *whole* decode step — embedding → 30 layers → lm_head →
+  FSM-masked sampling → state update — runs on the GPU without host
+  round-trips, and ``steps_per_graph`` consecutive steps are captured into one
+  hipGraph per batch-size bucket;
+* **scheduler**: admit waiting requests into free rows (prefill packs many
+  sequences into one varlen batch), replay decode graphs, harvest finished rows.
+
+Hot ops are the HIP kernels of :mod:`smsgate_amd.ops`; the projections are
+plain library GEMMs (hipBLASLt through ``torch.nn.functional.linear``).
+"""
+from __future__ import annotations
+
+import heapq
+import math
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Any, Deque, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..models.extractor import ExtractorConfig, ExtractorWeights
+from ..models.tokenizer import ExtractorTokenizer
+from ..parse.schema import SYSTEM_INSTRUCTION
+from .fsm import DEFAULT_FIELDS, FieldSpec, SchemaFSM, build_fsm
+
+__all__ = ["EngineConfig", "ExtractionEngine", "EngineStats"]
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class EngineConfig:
+    max_slots: int = 1024
+    max_body_tokens: int = 128
+    temperature: float = 0.0
+    seed: int = 0
+    steps_per_graph: int = 8
+    use_graphs: bool = True
+    prefill_max_tokens: int = 32768
+    admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
+    buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
+
+
+@dataclass
+class EngineStats:
+    prefill_tokens: int = 0
+    prefill_seqs: int = 0
+    prefill_s: float = 0.0
+    decode_steps: int = 0
+    decode_row_steps: int = 0
+    decode_s: float = 0.0
+    harvest_s: float = 0.0
+    completed: int = 0
+
+    def as_dict(self) -> Dict[str, float]:
+        return dict(self.__dict__)
+
+
+@dataclass
+class _Pending:
+    key: Any
+    ids: List[int]
+
+
+class ExtractionEngine:
+    def __init__(self, weights: ExtractorWeights, tokenizer: ExtractorTokenizer,
+                 cfg: Optional[EngineConfig] = None, fields: Sequence[FieldSpec] = DEFAULT_FIELDS,
+                 system_prompt: str = SYSTEM_INSTRUCTION) -> None:
+        self.cfg = cfg or EngineConfig()
+        self.w = weights
+        self.mc: ExtractorConfig = weights.cfg
+        self.tok = tokenizer
+        self.device = weights.embed.device
+        if self.device.type != "cuda":
+            raise RuntimeError("ExtractionEngine needs a GPU (the HIP kernels have no CPU path)")
+        ops.load_library()
+        mc, ec = self.mc, self.cfg
+        if mc.head_dim != 64:
+            raise ValueError("kernels are specialised for head_dim 64")
+        self.fsm: SchemaFSM = build_fsm(tokenizer, mc.vocab, fields).to_device(self.device)
+        self.max_out = self.fsm.max_steps()
+        self.prefix_ids = tokenizer.prefix_ids(system_prompt)
+        self.P0 = len(self.prefix_ids)
+        self.P0pad = _round_up(self.P0, 32)
+        self.Lmax = _round_up(ec.max_body_tokens + 2 + self.max_out, 8)
+        if self.P0 + self.Lmax > 1024:
+            raise ValueError("prefix + Lmax exceeds the decode kernel's context limit (1024)")
+        S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
+        dev, bf = self.device, torch.bfloat16
+        self.k_cache = torch.zeros(L, S, nkv, self.Lmax, D, dtype=bf, device=dev)
+        self.vt_cache = torch.zeros(L, S, nkv, D, self.Lmax, dtype=bf, device=dev)
+        self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
+        self.pvt = torch.zeros(L, nkv, D, self.P0pad, dtype=bf, device=dev)
+        self.cos_sin = ops.rope_table(self.P0 + self.Lmax + 1, D, mc.rope_theta, dev)
+        self.scale = 1.0 / math.sqrt(D)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.tok_buf = torch.zeros(S, **i32)
+        self.pos = torch.zeros(S, **i32)
+        self.state = torch.full((S,), self.fsm.done_state, **i32)
+        self.done = torch.ones(S, **i32)
+        self.out_len = torch.zeros(S, **i32)
+        self.out_buf = torch.zeros(S, self.max_out, **i32)
+        self.slot_id = torch.arange(S, **i32)
+        self.free_rows: List[int] = list(range(S))
+        heapq.heapify(self.free_rows)
+        self.active: Dict[int, Any] = {}
+        self.waiting: Deque[_Pending] = deque()
+        self.stats = EngineStats()
+        self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self._pool = None
+        self._compute_prefix()
+        if ec.use_graphs:
+            self._capture_graphs()
+
+    # ------------------------------------------------------------------ model
+    def _layers(self, x: torch.Tensor, *, pos_tok: torch.Tensor, slot_tok: torch.Tensor, attn, k_cache,
+                vt_cache, p0: int) -> torch.Tensor:
+        """Run all decoder layers on packed tokens; returns the final-normed hidden."""
+        mc, w = self.mc, self.w
+        T = x.shape[0]
+        resid = x
+        y: Optional[torch.Tensor] = None
+        q = torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=x.device)
+        a = torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)
+        for i in range(mc.layers):
+            h = ops.rmsnorm_residual(resid, w.ln1[i], mc.eps, x=y)
+            qkv = F.linear(h, w.qkv[i])
+            ops.rope_qkv_cache(qkv, pos_tok, slot_tok, self.cos_sin, q, k_cache(i), vt_cache(i), mc.heads,
+                               mc.kv_heads, mc.head_dim, p0)
+            attn(i, q, a)
+            y = F.linear(a, w.o[i])
+            h = ops.rmsnorm_residual(resid, w.ln2[i], mc.eps, x=y)
+            act = ops.silu_mul(F.linear(h, w.gate_up[i]))
+            y = F.linear(act, w.down[i])
+        return ops.rmsnorm_residual(resid, w.ln_f, mc.eps, x=y)
+
+    def _compute_prefix(self) -> None:
+        ids = torch.tensor(self.prefix_ids, dtype=torch.int32, device=self.device)
+        T = ids.numel()
+        x = F.embedding(ids.long(), self.w.embed).contiguous()
+        pos = torch.arange(T, dtype=torch.int32, device=self.device)
+        slot = torch.zeros(T, dtype=torch.int32, device=self.device)
+        cu = torch.tensor([0, T], dtype=torch.int32, device=self.device)
+        qs = torch.zeros(1, dtype=torch.int32, device=self.device)
+        s1 = torch.zeros(1, dtype=torch.int32, device=self.device)
+        empty_k = torch.zeros(self.mc.kv_heads, 0, self.mc.head_dim, dtype=torch.bfloat16, device=self.device)
+        empty_v = torch.zeros(self.mc.kv_heads, self.mc.head_dim, 0, dtype=torch.bfloat16, device=self.device)
+
+        def kc(i):
+            return self.pk[i].unsqueeze(0)
+
+        def vc(i):
+            return self.pvt[i].unsqueeze(0)
+
+        def attn(i, q, out):
+            ops.attn_prefill(q, cu, qs, s1, T, kc(i), vc(i), empty_k, empty_v, 0, out, self.scale)
+
+        self._layers(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=0)
+        torch.cuda.synchronize(self.device)
+
+    # ---------------------------------------------------------------- prefill
+    def _prefill(self, rows: List[int], items: List[_Pending], sample: bool = True) -> torch.Tensor:
+        t0 = time.perf_counter()
+        lens = [len(it.ids) for it in items]
+        T = sum(lens)
+        dev = self.device
+        flat = torch.tensor([t for it in items for t in it.ids], dtype=torch.int64)
+        pos_h = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens])
+        slot_h = torch.repeat_interleave(torch.tensor(rows, dtype=torch.int32), torch.tensor(lens))
+        cu_h = torch.zeros(len(items) + 1, dtype=torch.int32)
+        cu_h[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int32), 0)
+        rows_h = torch.tensor(rows, dtype=torch.int32)
+        # one pinned staging copy for all small index arrays
+        meta = torch.cat([pos_h, slot_h, cu_h, rows_h, torch.tensor(lens, dtype=torch.int32) - 1]).pin_memory()
+        meta_d = meta.to(dev, non_blocking=True)
+        o = 0
+        pos_d = meta_d[o:o + T]; o += T
+        slot_d = meta_d[o:o + T]; o += T
+        cu_d = meta_d[o:o + len(items) + 1]; o += len(items) + 1
+        rows_d = meta_d[o:o + len(items)]; o += len(items)
+        last_pos_d = meta_d[o:o + len(items)]
+        qstart = torch.zeros(len(items), dtype=torch.int32, device=dev)
+        x = F.embedding(flat.pin_memory().to(dev, non_blocking=True), self.w.embed).contiguous()
+        max_q = max(lens)
+
+        def kc(i):
+            return self.k_cache[i]
+
+        def vc(i):
+            return self.vt_cache[i]
+
+        def attn(i, q, out):
+            ops.attn_prefill(q, cu_d, qstart, rows_d, max_q, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
+                             self.scale)
+
+        h = self._layers(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        last = h.index_select(0, (cu_d[1:] - 1).long())
+        logits = F.linear(last, self.w.embed)
+        if not sample:
+            return logits
+        # reset the admitted rows, then sample their first answer token
+        rl = rows_d.long()
+        self.done.index_fill_(0, rl, 0)
+        self.out_len.index_fill_(0, rl, 0)
+        self.state.index_fill_(0, rl, self.fsm.start_state)
+        self.pos.index_copy_(0, rl, last_pos_d)
+        ops.fsm_sample(logits, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done, self.pos,
+                       self.slot_id, self.cfg.temperature, self.cfg.seed, row_map=rows_d)
+        self.stats.prefill_tokens += T
+        self.stats.prefill_seqs += len(items)
+        self.stats.prefill_s += time.perf_counter() - t0
+        return logits
+
+    # ----------------------------------------------------------------- decode
+    def _decode_step(self, B: int, sample: bool = True) -> torch.Tensor:
+        tok = self.tok_buf[:B]
+        pos = self.pos[:B]
+        slot = self.slot_id[:B]
+        x = F.embedding(tok.long(), self.w.embed)
+
+        def kc(i):
+            return self.k_cache[i]
+
+        def vc(i):
+            return self.vt_cache[i]
+
+        def attn(i, q, out):
+            ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale)
+
+        h = self._layers(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        logits = F.linear(h, self.w.embed)
+        if sample:
+            ops.fsm_sample(logits, self.fsm, self.state[:B], tok, self.out_buf[:B], self.out_len[:B],
+                           self.done[:B], pos, slot, self.cfg.temperature, self.cfg.seed)
+        return logits
+
+    # ------------------------------------------------------------ debugging
+    def debug_logits(self, bodies: Sequence[str], forced: Sequence[Sequence[int]] = ()) -> List[torch.Tensor]:
+        """Logits of the HIP path for validation: the prefill's last position,
+        then one decode step per forced token (rows 0..n-1; engine must be idle)."""
+        assert not self.active
+        items = [_Pending(i, ids) for i, ids in enumerate(self.tok.message_ids(list(bodies), self.cfg.max_body_tokens))]
+        n = len(items)
+        rows = list(range(n))
+        outs = [self._prefill(rows, items, sample=False).float()]
+        lens = torch.tensor([len(it.ids) for it in items], dtype=torch.int32, device=self.device)
+        self.pos[:n] = lens - 1
+        for step in range(len(forced[0]) if forced else 0):
+            self.tok_buf[:n] = torch.tensor([f[step] for f in forced], dtype=torch.int32, device=self.device)
+            self.pos[:n] += 1
+            outs.append(self._decode_step(n, sample=False).float())
+        return outs
+
+    def _bucket(self, n: int) -> int:
+        for b in self.cfg.buckets:
+            if b >= n and b <= self.cfg.max_slots:
+                return b
+        return self.cfg.max_slots
+
+    def _capture_graphs(self) -> None:
+        """Capture ``steps_per_graph`` decode steps per bucket (all rows idle/done)."""
+        sizes = sorted({self._bucket(b) for b in self.cfg.buckets if b <= self.cfg.max_slots} | {self.cfg.max_slots})
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for B in sizes:  # warm-up: hipBLASLt heuristics/workspaces before capture
+                self._decode_step(B)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._pool = torch.cuda.graph_pool_handle()
+        for B in sorted(sizes, reverse=True):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._pool):
+                for _ in range(self.cfg.steps_per_graph):
+                    self._decode_step(B)
+            self.graphs[B] = g
+        torch.cuda.synchronize(self.device)
+
+    def _run_decode(self, B: int) -> None:
+        t0 = time.perf_counter()
+        g = self.graphs.get(B)
+        if g is not None:
+            g.replay()
+            n = self.cfg.steps_per_graph
+        else:
+            self._decode_step(B)
+            n = 1
+        self.stats.decode_steps += n
+        self.stats.decode_row_steps += n * B
+        self.stats.decode_s += time.perf_counter() - t0
+
+    # -------------------------------------------------------------- scheduler
+    def submit(self, key: Any, body: str) -> None:
+        ids = self.tok.message_ids([body], self.cfg.max_body_tokens)[0]
+        self.waiting.append(_Pending(key, ids))
+
+    def submit_many(self, items: Sequence[Tuple[Any, str]]) -> None:
+        if not items:
+            return
+        enc = self.tok.message_ids([b for _, b in items], self.cfg.max_body_tokens)
+        for (k, _), ids in zip(items, enc):
+            self.waiting.append(_Pending(k, ids))
+
+    def busy(self) -> bool:
+        return bool(self.waiting or self.active)
+
+    def _admit(self) -> None:
+        S = self.cfg.max_slots
+        if not self.waiting or not self.free_rows:
+            return
+        if self.active and len(self.free_rows) < max(1, int(S * self.cfg.admit_min_fraction)) \
+                and len(self.free_rows) < len(self.waiting):
+            return
+        while self.waiting and self.free_rows:
+            rows, items, ntok = [], [], 0
+            while self.waiting and self.free_rows:
+                it = self.waiting[0]
+                if items and ntok + len(it.ids) > self.cfg.prefill_max_tokens:
+                    break
+                self.waiting.popleft()
+                r = heapq.heappop(self.free_rows)
+                rows.append(r)
+                items.append(it)
+                ntok += len(it.ids)
+                self.active[r] = it.key
+            self._prefill(rows, items)
+
+    def _decode_answer(self, toks: List[int]) -> Dict[str, Optional[str]]:
+        vals = self.fsm.split_fields(toks)
+        out: Dict[str, Optional[str]] = {}
+        for i, f in enumerate(self.fsm.fields):
+            out[f.name] = self.tok.decode(vals[i]).strip() if i < len(vals) else None
+        return out
+
+    def _harvest(self, B: int) -> List[Tuple[Any, Dict[str, Optional[str]]]]:
+        t0 = time.perf_counter()
+        done_h = self.done[:B].cpu()
+        fin = [r for r in self.active if r < B and done_h[r]]
+        res: List[Tuple[Any, Dict[str, Optional[str]]]] = []
+        if fin:
+            idx = torch.tensor(fin, dtype=torch.long, device=self.device)
+            bufs = self.out_buf.index_select(0, idx).cpu().tolist()
+            lens = self.out_len.index_select(0, idx).cpu().tolist()
+            for r, buf, n in zip(fin, bufs, lens):
+                res.append((self.active.pop(r), self._decode_answer(buf[:n])))
+                heapq.heappush(self.free_rows, r)
+        self.stats.completed += len(res)
+        self.stats.harvest_s += time.perf_counter() - t0
+        return res
+
+    def step(self) -> List[Tuple[Any, Dict[str, Optional[str]]]]:
+        """Admit → one decode chunk → harvest. Returns finished ``(key, answer)``."""
+        self._admit()
+        if not self.active:
+            return []
+        B = self._bucket(max(self.active) + 1)
+        self._run_decode(B)
+        return self._harvest(B)
+
+    def run(self, bodies: Sequence[str]) -> List[Dict[str, Optional[str]]]:
+        """Synchronous batch extraction (tests, benchmarks)."""
+        self.submit_many(list(enumerate(bodies)))
+        out: List[Optional[Dict[str, Optional[str]]]] = [None] * len(bodies)
+        while self.busy():
+            for k, ans in self.step():
+                out[k] = ans
+        return out  # type: ignore[return-value]

@@ -1,0 +1,248 @@
+"""Schema finite-state machine for constrained extraction decoding.
+
+The reference asks Gemini for JSON matching a 9-key schema
+(gemini_parser.py:46-61, ``response_mime_type=application/json``). The local
+extractor instead emits the nine values in schema order, each terminated by
+``<sep>`` — the JSON scaffolding (keys, quotes, braces) is implied by the
+schema, so no decode step is spent on it. Every step is constrained by this
+FSM, compiled into GPU tables and applied inside ``sg_fsm_sample``:
+
+* a **value state** ``(field, k)`` allows the field's token class plus
+  ``<sep>``; at the field's token cap only ``<sep>`` is allowed, so every
+  sequence terminates within ``sum(caps) + 9`` steps;
+* ``txn_type`` is an **enum** compiled to a token trie over the tokenizer's
+  encodings of ``debit | credit | otp | unknown``;
+* token classes are derived from each token's decoded text (digits/dots for
+  dates, digits/separators for amounts, capitals for currencies, …).
+
+Tables (``int32``/``uint32`` on the device): ``masks[S, V/32]`` allowed-token
+bitmasks, ``next_sep[S]``, ``next_tok[S]`` (``-2`` = look up the sparse enum
+table ``enum_tok/enum_next[S, E]``), plus ``done_state``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..models.domain import CORE_FIELDS
+from ..parse.schema import TXN_TYPES
+
+__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm"]
+
+
+@dataclass(frozen=True)
+class FieldSpec:
+    name: str
+    kind: str  # text | date | number | currency | card | enum
+    cap: int
+    choices: Tuple[str, ...] = ()
+
+
+DEFAULT_FIELDS: Tuple[FieldSpec, ...] = (
+    FieldSpec("txn_type", "enum", 1, TXN_TYPES),
+    FieldSpec("date", "date", 10),
+    FieldSpec("amount", "number", 6),
+    FieldSpec("currency", "currency", 2),
+    FieldSpec("card", "card", 3),
+    FieldSpec("merchant", "text", 6),
+    FieldSpec("city", "text", 4),
+    FieldSpec("address", "text", 12),
+    FieldSpec("balance", "number", 6),
+)
+assert tuple(f.name for f in DEFAULT_FIELDS) == CORE_FIELDS
+
+_CLASS_CHARS = {
+    "date": set("0123456789.:/- "),
+    "number": set("0123456789.,- "),
+    "currency": set("ABCDEFGHIJKLMNOPQRSTUVWXYZ "),
+    "card": set("0123456789* "),
+}
+
+
+def _token_class_sets(token_strings: Sequence[str], specials: Sequence[int]) -> Dict[str, np.ndarray]:
+    V = len(token_strings)
+    spec = set(specials)
+    out = {k: np.zeros(V, dtype=bool) for k in ("text", "date", "number", "currency", "card")}
+    for i, s in enumerate(token_strings):
+        if i in spec or not s:
+            continue
+        out["text"][i] = True
+        if not s.strip():
+            continue  # pure-whitespace tokens only count as free text
+        cs = set(s)
+        for k, allowed in _CLASS_CHARS.items():
+            if cs <= allowed:
+                out[k][i] = True
+    return out
+
+
+@dataclass
+class SchemaFSM:
+    fields: Tuple[FieldSpec, ...]
+    vocab: int  # model vocab (≥ tokenizer vocab; extra ids never allowed)
+    sep_token: int
+    allowed: np.ndarray  # [S, vocab] bool
+    next_sep: np.ndarray  # [S]
+    next_tok: np.ndarray  # [S] (-2 = enum lookup)
+    enum_tok: np.ndarray  # [S, E]
+    enum_next: np.ndarray  # [S, E]
+    done_state: int
+    start_state: int = 0
+    field_of_state: List[int] = field(default_factory=list)
+    # device copies (filled by to_device; consumed by ops.fsm_sample)
+    masks: object = None
+    state_mask: object = None
+    next_sep_t: object = None
+    next_tok_t: object = None
+    enum_tok_t: object = None
+    enum_next_t: object = None
+
+    @property
+    def E(self) -> int:
+        return int(self.enum_tok.shape[1])
+
+    @property
+    def num_states(self) -> int:
+        return int(self.allowed.shape[0])
+
+    def max_steps(self) -> int:
+        return sum(f.cap for f in self.fields) + len(self.fields)
+
+    def packed_masks(self) -> np.ndarray:
+        """[S, vocab/32] uint32, bit j of word w = token 32w+j allowed."""
+        S, V = self.allowed.shape
+        bits = self.allowed.reshape(S, V // 32, 32).astype(np.uint64)
+        weights = (np.uint64(1) << np.arange(32, dtype=np.uint64))
+        return (bits * weights).sum(-1).astype(np.uint32)
+
+    def to_device(self, device) -> "SchemaFSM":
+        import torch
+
+        self.masks = torch.from_numpy(self.packed_masks().view(np.int32)).to(device)
+        self.state_mask = torch.arange(self.num_states, dtype=torch.int32, device=device)
+        # kernel-facing names
+        self.next_sep_t = torch.from_numpy(self.next_sep.astype(np.int32)).to(device)
+        self.next_tok_t = torch.from_numpy(self.next_tok.astype(np.int32)).to(device)
+        self.enum_tok_t = torch.from_numpy(self.enum_tok.astype(np.int32)).to(device)
+        self.enum_next_t = torch.from_numpy(self.enum_next.astype(np.int32)).to(device)
+        return self
+
+    def step_host(self, state: int, tok: int) -> int:
+        """Reference transition (host side, for tests)."""
+        if not self.allowed[state, tok]:
+            return -1
+        if tok == self.sep_token:
+            return int(self.next_sep[state])
+        nt = int(self.next_tok[state])
+        if nt != -2:
+            return nt
+        for t, n in zip(self.enum_tok[state], self.enum_next[state]):
+            if int(t) == tok:
+                return int(n)
+        return -1
+
+    def split_fields(self, tokens: Sequence[int]) -> List[List[int]]:
+        vals: List[List[int]] = [[]]
+        for t in tokens:
+            if t == self.sep_token:
+                vals.append([])
+            else:
+                vals[-1].append(t)
+        return vals[: len(self.fields)]
+
+
+def build_fsm(tokenizer, vocab: int, fields: Sequence[FieldSpec] = DEFAULT_FIELDS) -> SchemaFSM:
+    strings = tokenizer.token_strings
+    V_tok = len(strings)
+    specials = [tokenizer.pad, tokenizer.bos, tokenizer.eos, tokenizer.sep, tokenizer.sms, tokenizer.ans]
+    classes = _token_class_sets(strings, specials)
+    sep = tokenizer.sep
+
+    states_allowed: List[np.ndarray] = []
+    next_sep: List[int] = []
+    next_tok: List[int] = []
+    enum_lists: List[List[Tuple[int, int]]] = []
+    field_of: List[int] = []
+
+    def new_state(allowed: np.ndarray, fidx: int) -> int:
+        states_allowed.append(allowed)
+        next_sep.append(-1)
+        next_tok.append(-1)
+        enum_lists.append([])
+        field_of.append(fidx)
+        return len(states_allowed) - 1
+
+    def pad(mask: np.ndarray) -> np.ndarray:
+        full = np.zeros(vocab, dtype=bool)
+        full[:V_tok] = mask
+        return full
+
+    only_sep = np.zeros(vocab, dtype=bool)
+    only_sep[sep] = True
+
+    field_starts: List[int] = []
+    field_ends: List[List[int]] = []  # states whose <sep> leaves the field
+    for fi, f in enumerate(fields):
+        if f.kind == "enum":
+            enc = [tokenizer.encode(c) for c in f.choices]
+            # trie over token sequences
+            root = new_state(np.zeros(vocab, dtype=bool), fi)
+            field_starts.append(root)
+            ends: List[int] = []
+            nodes: Dict[Tuple[int, ...], int] = {(): root}
+            for seq in enc:
+                for depth in range(len(seq)):
+                    pre = tuple(seq[:depth])
+                    cur = nodes[pre]
+                    nxt_key = tuple(seq[: depth + 1])
+                    if nxt_key not in nodes:
+                        nodes[nxt_key] = new_state(np.zeros(vocab, dtype=bool), fi)
+                    states_allowed[cur][seq[depth]] = True
+                    if (seq[depth], nodes[nxt_key]) not in enum_lists[cur]:
+                        enum_lists[cur].append((seq[depth], nodes[nxt_key]))
+                    next_tok[cur] = -2
+                leaf = nodes[tuple(seq)]
+                states_allowed[leaf][sep] = True
+                ends.append(leaf)
+            field_ends.append(ends)
+        else:
+            cls = pad(classes[f.kind])
+            allow = cls.copy()
+            allow[sep] = True
+            st = [new_state(allow.copy(), fi) for _ in range(f.cap)]
+            last = new_state(only_sep.copy(), fi)
+            chain = st + [last]
+            for a, b in zip(chain[:-1], chain[1:]):
+                next_tok[a] = b
+            field_starts.append(chain[0])
+            field_ends.append(chain)
+    done = new_state(only_sep.copy(), len(fields))
+    next_sep[done] = done
+    for fi in range(len(fields)):
+        tgt = field_starts[fi + 1] if fi + 1 < len(fields) else done
+        for s in field_ends[fi]:
+            next_sep[s] = tgt
+
+    S = len(states_allowed)
+    E = max(1, max(len(e) for e in enum_lists))
+    enum_tok = np.full((S, E), -1, dtype=np.int32)
+    enum_next = np.full((S, E), -1, dtype=np.int32)
+    for s, lst in enumerate(enum_lists):
+        for j, (t, n) in enumerate(lst):
+            enum_tok[s, j] = t
+            enum_next[s, j] = n
+    return SchemaFSM(
+        fields=tuple(fields),
+        vocab=vocab,
+        sep_token=sep,
+        allowed=np.stack(states_allowed),
+        next_sep=np.asarray(next_sep, dtype=np.int32),
+        next_tok=np.asarray(next_tok, dtype=np.int32),
+        enum_tok=enum_tok,
+        enum_next=enum_next,
+        done_state=done,
+        start_state=field_starts[0],
+        field_of_state=field_of,
+    )

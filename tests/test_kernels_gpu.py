@@ -1,0 +1,183 @@
+"""Numerics of the HIP kernels vs plain PyTorch fp32 references (MI355X only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")]
+
+from smsgate_amd import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def _bf(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(DEV)
+
+
+def test_library_loads_from_tree():
+    lib = ops.load_library()
+    assert lib.sg_version() == 1
+    assert "smsgate_amd/ops/_lib" in lib._name
+
+
+@pytest.mark.parametrize("T,H", [(1, 576), (7, 576), (300, 576), (33, 1024)])
+def test_rmsnorm_residual(T, H):
+    res = _bf(T, H, seed=1)
+    x = _bf(T, H, seed=2)
+    w = _bf(H, seed=3) + 1
+    res0 = res.clone()
+    out = ops.rmsnorm_residual(res, w, 1e-5, x=x)
+    new_res = (res0.float() + x.float()).to(torch.bfloat16)
+    assert torch.equal(res, new_res)
+    ref = ops.ref_rmsnorm(new_res, w, 1e-5)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    out2 = ops.rmsnorm_residual(res0.clone(), w, 1e-5)
+    torch.testing.assert_close(out2.float(), ops.ref_rmsnorm(res0, w, 1e-5), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("T,I", [(1, 1536), (129, 1536), (5, 64)])
+def test_silu_mul(T, I):
+    gu = _bf(T, 2 * I, scale=3.0)
+    out = ops.silu_mul(gu)
+    torch.testing.assert_close(out.float(), ops.ref_silu_mul(gu), atol=3e-2, rtol=2e-2)
+
+
+def test_rope_qkv_cache():
+    T, nh, nkv, D, S, Lmax, p0 = 37, 9, 3, 64, 5, 64, 11
+    qkv = _bf(T, (nh + 2 * nkv) * D)
+    pos = torch.randint(0, Lmax, (T,), dtype=torch.int32, device=DEV)
+    slot = torch.randint(0, S, (T,), dtype=torch.int32, device=DEV)
+    # unique (slot, pos) pairs so writes don't collide
+    pairs = torch.randperm(S * Lmax)[:T]
+    slot = (pairs // Lmax).to(torch.int32).to(DEV)
+    pos = (pairs % Lmax).to(torch.int32).to(DEV)
+    cs = ops.rope_table(p0 + Lmax + 1, D, 1e5, DEV)
+    q = torch.empty(T, nh, D, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
+    vt = torch.zeros(S, nkv, D, Lmax, dtype=torch.bfloat16, device=DEV)
+    ops.rope_qkv_cache(qkv, pos, slot, cs, q, kc, vt, nh, nkv, D, p0)
+    qf, kf, vf = qkv.float().split([nh * D, nkv * D, nkv * D], -1)
+    absp = (pos + p0).long()
+    qr = ops.ref_rope(qf.view(T, nh, D), absp, 1e5)
+    kr = ops.ref_rope(kf.view(T, nkv, D), absp, 1e5)
+    torch.testing.assert_close(q.float(), qr, atol=2e-2, rtol=2e-2)
+    sl, ps = slot.long(), pos.long()
+    torch.testing.assert_close(kc[sl, :, ps, :].float(), kr, atol=2e-2, rtol=2e-2)
+    got_v = vt[sl, :, :, ps]  # [T, nkv, D]
+    assert torch.equal(got_v.float(), vf.view(T, nkv, D))
+
+
+def _ref_seq_attention(qb, own_k, own_v, pk, pv, P0, q_off, scale):
+    """qb [nq, nh, D]; own_k/v [nown, nkv, D]; pk/pv [P0, nkv, D]; q_off[i] = own offset of query i."""
+    nq, nh, D = qb.shape
+    nkv = own_k.shape[1]
+    G = nh // nkv
+    out = torch.empty(nq, nh, D, device=qb.device)
+    nown = own_k.shape[0]
+    keys_k = torch.cat([pk, own_k], 0)
+    keys_v = torch.cat([pv, own_v], 0)
+    kidx = torch.arange(P0 + nown, device=qb.device)
+    mask = (kidx[None, :] < P0) | ((kidx[None, :] - P0) <= torch.as_tensor(q_off, device=qb.device)[:, None])
+    for h in range(nh):
+        kh = h // G
+        out[:, h] = ops.ref_attention(qb[:, h], keys_k[:, kh], keys_v[:, kh], mask, scale)
+    return out
+
+
+@pytest.mark.parametrize("P0", [0, 75])
+def test_attn_prefill(P0):
+    nh, nkv, D, S, Lmax = 9, 3, 64, 6, 200
+    P0pad = (P0 + 31) // 32 * 32
+    lens = [1, 17, 40, 63, 5]
+    starts = [0, 0, 3, 0, 30]  # own offset of each chunk's first query (chunked prefill)
+    rows = [4, 0, 2, 5, 1]
+    T = sum(lens)
+    q = _bf(T, nh, D, seed=4)
+    kc = _bf(S, nkv, Lmax, D, seed=5)
+    vt = _bf(S, nkv, D, Lmax, seed=6)
+    pk = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
+    pvt = torch.zeros(nkv, D, P0pad, dtype=torch.bfloat16, device=DEV)
+    if P0:
+        pk[:, :P0] = _bf(nkv, P0, D, seed=7)
+        pvt[:, :, :P0] = _bf(nkv, D, P0, seed=8)
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32, device=DEV)
+    qs = torch.tensor(starts, dtype=torch.int32, device=DEV)
+    sl = torch.tensor(rows, dtype=torch.int32, device=DEV)
+    out = torch.empty(T, nh * D, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / math.sqrt(D)
+    ops.attn_prefill(q, cu, qs, sl, max(lens), kc, vt, pk, pvt, P0, out, scale)
+    o = 0
+    for n, st, r in zip(lens, starts, rows):
+        nown = st + n
+        own_k = kc[r, :, :nown].permute(1, 0, 2).float()
+        own_v = vt[r, :, :, :nown].permute(2, 0, 1).float()
+        ref = _ref_seq_attention(q[o:o + n].float(), own_k, own_v, pk[:, :P0].permute(1, 0, 2).float(),
+                                 pvt[:, :, :P0].permute(2, 0, 1).float(), P0, list(range(st, st + n)), scale)
+        torch.testing.assert_close(out[o:o + n].float().view(n, nh, D), ref, atol=3e-2, rtol=3e-2)
+        o += n
+
+
+@pytest.mark.parametrize("P0", [0, 75])
+def test_attn_decode(P0):
+    nh, nkv, D, S, Lmax = 9, 3, 64, 8, 200
+    P0pad = (P0 + 31) // 32 * 32
+    B = 6
+    q = _bf(B, nh, D, seed=9)
+    kc = _bf(S, nkv, Lmax, D, seed=10)
+    vt = _bf(S, nkv, D, Lmax, seed=11)
+    pk = torch.zeros(nkv, max(P0pad, 0), D, dtype=torch.bfloat16, device=DEV)
+    pvt = torch.zeros(nkv, D, max(P0pad, 0), dtype=torch.bfloat16, device=DEV)
+    if P0:
+        pk[:, :P0] = _bf(nkv, P0, D, seed=12)
+        pvt[:, :, :P0] = _bf(nkv, D, P0, seed=13)
+    pos = torch.tensor([0, 1, 7, 8, 100, 199], dtype=torch.int32, device=DEV)
+    slot = torch.tensor([3, 0, 7, 1, 2, 5], dtype=torch.int32, device=DEV)
+    out = torch.empty(B, nh * D, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / math.sqrt(D)
+    ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, scale)
+    for b in range(B):
+        p, r = int(pos[b]), int(slot[b])
+        own_k = kc[r, :, : p + 1].permute(1, 0, 2).float()
+        own_v = vt[r, :, :, : p + 1].permute(2, 0, 1).float()
+        ref = _ref_seq_attention(q[b:b + 1].float(), own_k, own_v, pk[:, :P0].permute(1, 0, 2).float(),
+                                 pvt[:, :, :P0].permute(2, 0, 1).float(), P0, [p], scale)
+        torch.testing.assert_close(out[b].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_fsm_sample_greedy_and_transitions():
+    from smsgate_amd.models.tokenizer import load_tokenizer
+    from smsgate_amd.serving.fsm import build_fsm
+
+    tk = load_tokenizer()
+    V = 49152
+    fsm = build_fsm(tk, V).to_device(DEV)
+    B = 64
+    logits = _bf(B, V, scale=3.0, seed=14)
+    states_h = torch.randint(0, fsm.num_states - 1, (B,))
+    state = states_h.to(torch.int32).to(DEV)
+    tok = torch.zeros(B, dtype=torch.int32, device=DEV)
+    out_buf = torch.zeros(B, 8, dtype=torch.int32, device=DEV)
+    out_len = torch.zeros(B, dtype=torch.int32, device=DEV)
+    done = torch.zeros(B, dtype=torch.int32, device=DEV)
+    done[0] = 1
+    pos = torch.zeros(B, dtype=torch.int32, device=DEV)
+    slot = torch.arange(B, dtype=torch.int32, device=DEV)
+    ops.fsm_sample(logits, fsm, state, tok, out_buf, out_len, done, pos, slot, 0.0, 0)
+    allowed = torch.from_numpy(fsm.allowed)
+    lf = logits.float().cpu()
+    for b in range(1, B):
+        s = int(states_h[b])
+        masked = lf[b].masked_fill(~allowed[s], float("-inf"))
+        exp_tok = int(masked.argmax())
+        assert int(tok[b]) == exp_tok and int(out_buf[b, 0]) == exp_tok and int(out_len[b]) == 1
+        ns = fsm.step_host(s, exp_tok)
+        assert int(state[b]) == (ns if ns >= 0 else fsm.done_state)
+    assert int(out_len[0]) == 0  # done rows untouched
+    # temperature sampling stays inside the mask
+    state2 = states_h.to(torch.int32).to(DEV)
+    done.zero_()
+    ops.fsm_sample(logits, fsm, state2, tok, out_buf, out_len.zero_(), done, pos, slot, 1.0, 123)
+    for b in range(B):
+        assert allowed[int(states_h[b]), int(tok[b])]

@@ -32,6 +32,9 @@ __all__ = [
     "attn_decode",
     "fsm_sample",
     "rope_table",
+    "vt_shape",
+    "vt_to_rows",
+    "rows_to_vt",
     "ref_rmsnorm",
     "ref_silu_mul",
     "ref_rope",
@@ -48,10 +51,10 @@ _ip = ctypes.c_void_p  # int32 device pointers travel as void*
 def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_rmsnorm_residual.argtypes = [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_float, _vp]
     lib.sg_silu_mul.argtypes = [_vp, _vp, _c_int, _c_int, _vp]
-    lib.sg_rope_qkv_cache.argtypes = [_vp, _ip, _ip, _vp, _vp, _vp, _vp] + [_c_int] * 7 + [_vp]
+    lib.sg_rope_qkv_cache.argtypes = [_vp, _ip, _ip, _vp, _vp, _vp, _vp] + [_c_int] * 6 + [_vp]
     lib.sg_attn_prefill.argtypes = [_vp, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
                                     _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
-    lib.sg_attn_decode.argtypes = [_vp, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
+    lib.sg_attn_decode.argtypes = [_vp, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
                                    _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
@@ -152,7 +155,7 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos
     _req(cos_sin, torch.float32, "cos_sin")
     S, nkv_, Lmax, D = k_cache.shape
     assert qkv.shape[1] == (nh + 2 * nkv) * head_dim and D == head_dim and nkv_ == nkv
-    assert vt_cache.shape == (S, nkv, D, Lmax)
+    assert vt_cache.shape == vt_shape(S, nkv, D, Lmax), (vt_cache.shape, vt_shape(S, nkv, D, Lmax))
     assert q_out.shape[0] >= T and q_out.numel() >= T * nh * D
     assert pos.numel() == T and slot.numel() == T
     _check(load_library().sg_rope_qkv_cache(_p(qkv), _p(pos), _p(slot), _p(cos_sin), _p(q_out), _p(k_cache),
@@ -169,7 +172,8 @@ def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slo
     S, nkv, Lmax, _ = k_cache.shape
     P0pad = pk.shape[1]
     nseq = cu_q.numel() - 1
-    assert pk.shape == (nkv, P0pad, D) and pvt.shape == (nkv, D, P0pad)
+    assert pk.shape == (nkv, P0pad, D) and pvt.shape == vt_shape(1, nkv, D, P0pad)[1:]
+    assert vt_cache.shape == vt_shape(S, nkv, D, Lmax)
     assert slot.numel() == nseq and q_start.numel() == nseq and P0 <= P0pad
     _check(load_library().sg_attn_prefill(_p(q), _p(cu_q), _p(q_start), _p(slot), _p(k_cache), _p(vt_cache),
                                           _p(pk), _p(pvt), P0, P0pad, _p(out), nseq, max_q, nh, nkv, D, Lmax,
@@ -179,13 +183,16 @@ def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slo
 
 def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache: torch.Tensor,
                 vt_cache: torch.Tensor, pk: torch.Tensor, pvt: torch.Tensor, P0: int, out: torch.Tensor,
-                scale: float) -> torch.Tensor:
+                scale: float, done: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One query token per row; rows with ``done[b] != 0`` are skipped (output untouched)."""
     B, nh, D = q.shape
     S, nkv, Lmax, _ = k_cache.shape
     P0pad = pk.shape[1]
-    assert pos.numel() == B and slot.numel() == B
-    _check(load_library().sg_attn_decode(_p(q), _p(pos), _p(slot), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt),
-                                         P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, _stream()), "attn_decode")
+    assert pos.numel() == B and slot.numel() == B and (done is None or done.numel() >= B)
+    assert vt_cache.shape == vt_shape(S, nkv, D, Lmax) and pvt.shape == vt_shape(1, nkv, D, P0pad)[1:]
+    _check(load_library().sg_attn_decode(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk),
+                                         _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, _stream()),
+           "attn_decode")
     return out
 
 
@@ -206,6 +213,24 @@ def fsm_sample(logits: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Ten
         _p(out_len), _p(done), _p(pos), _p(slot_id), _p(row_map), max_out, V, B, inv_t, seed & 0xFFFFFFFF,
         _stream()),
         "fsm_sample")
+
+
+def vt_shape(S: int, nkv: int, D: int, L: int):
+    """Blocked V^T cache layout ``[S][nkv][L/8][D][8]`` (8 keys of one dim = 16 bytes)."""
+    assert L % 8 == 0
+    return (S, nkv, L // 8, D, 8)
+
+
+def vt_to_rows(vt: torch.Tensor) -> torch.Tensor:
+    """Blocked ``[..., L/8, D, 8]`` → plain rows ``[..., L, D]`` (tests/debugging)."""
+    *lead, nb, D, eight = vt.shape
+    return vt.transpose(-1, -2).reshape(*lead, nb * eight, D)
+
+
+def rows_to_vt(v: torch.Tensor) -> torch.Tensor:
+    """Plain rows ``[..., L, D]`` → blocked ``[..., L/8, D, 8]``."""
+    *lead, L, D = v.shape
+    return v.reshape(*lead, L // 8, 8, D).transpose(-1, -2).contiguous()
 
 
 # ------------------------------------------------------------------ references

@@ -66,37 +66,56 @@ __global__ void __launch_bounds__(256) rmsnorm_residual_kernel(const uint16_t* _
                                                                const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ out, int T, int H,
                                                                float eps) {
+  // The row stays in registers (<= RMS_MAXV chunks of 8 per lane, H <= 2048):
+  // one read of residual/x, one write of residual and out — no second pass.
+  constexpr int RMS_MAXV = 4;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= T) return;
   const int nvec = H >> 3;
   uint4* r4 = reinterpret_cast<uint4*>(residual + (size_t)row * H);
   const uint4* x4 = x_in ? reinterpret_cast<const uint4*>(x_in + (size_t)row * H) : nullptr;
-  float ss = 0.f;
-  for (int c = lane; c < nvec; c += WAVE) {
-    float a[8];
-    unpack8(r4[c], a);
-    if (x4) {
-      float b[8];
-      unpack8(x4[c], b);
+  uint4 rv[RMS_MAXV], xv[RMS_MAXV];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = bf2f(f2bf(a[j] + b[j]));  // residual stream stays bf16
-      r4[c] = pack8(a);
+  for (int k = 0; k < RMS_MAXV; ++k) {
+    const int c = lane + k * WAVE;
+    if (c < nvec) {
+      rv[k] = r4[c];
+      if (x4) xv[k] = x4[c];
     }
+  }
+  float ss = 0.f;
+  float a[RMS_MAXV][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ss += a[j] * a[j];
+  for (int k = 0; k < RMS_MAXV; ++k) {
+    const int c = lane + k * WAVE;
+    if (c < nvec) {
+      unpack8(rv[k], a[k]);
+      if (x4) {
+        float b[8];
+        unpack8(xv[k], b);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[k][j] = bf2f(f2bf(a[k][j] + b[j]));  // residual stream stays bf16
+        r4[c] = pack8(a[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += a[k][j] * a[k][j];
+    }
   }
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)H + eps);
   const uint4* w4 = reinterpret_cast<const uint4*>(w);
   uint4* o4 = reinterpret_cast<uint4*>(out + (size_t)row * H);
-  for (int c = lane; c < nvec; c += WAVE) {
-    float a[8], g[8];
-    unpack8(r4[c], a);
-    unpack8(w4[c], g);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a[j] = a[j] * r * g[j];
-    o4[c] = pack8(a);
+  for (int k = 0; k < RMS_MAXV; ++k) {
+    const int c = lane + k * WAVE;
+    if (c < nvec) {
+      float g[8];
+      unpack8(w4[c], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = a[k][j] * r * g[j];
+      o4[c] = pack8(g);
+    }
   }
 }
 
@@ -127,19 +146,25 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restric
 //   slot   [T] cache slot
 //   cs     [max_pos][D/2] float2 (cos, sin)
 // ---------------------------------------------------------------------------
+// One wave per token, 4 tokens per block. V goes to the *blocked* V^T layout
+// [slot][kvh][Lmax/8][D][8]: one token's 64 values land in one 1 KiB block (8
+// cache lines) instead of 64 rows, and a P·V reader gets 8 keys of one dim as
+// one 16-byte load with the 64 lanes of a wave reading 1 KiB contiguously.
 __global__ void __launch_bounds__(256) rope_qkv_cache_kernel(const uint16_t* __restrict__ qkv, const int* __restrict__ pos,
                                                              const int* __restrict__ slot, const float2* __restrict__ cs,
                                                              uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache,
-                                                             uint16_t* __restrict__ vt_cache, int nh, int nkv, int D,
-                                                             int Lmax, int p0) {
-  const int t = blockIdx.x;
+                                                             uint16_t* __restrict__ vt_cache, int T, int nh, int nkv,
+                                                             int D, int Lmax, int p0) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= T) return;
   const int half = D >> 1;
   const int p = pos[t];
   const int s = slot[t];
   const float2* cst = cs + (size_t)(p0 + p) * half;
   const uint16_t* src = qkv + (size_t)t * (nh + 2 * nkv) * D;
   const int nrot = (nh + nkv) * half;
-  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
+  for (int it = lane; it < nrot; it += WAVE) {
     const int h = it / half;
     const int i = it - h * half;
     const float2 c = cst[i];
@@ -159,10 +184,11 @@ __global__ void __launch_bounds__(256) rope_qkv_cache_kernel(const uint16_t* __r
     }
   }
   const uint16_t* v = src + (nh + nkv) * D;
-  for (int it = threadIdx.x; it < nkv * D; it += blockDim.x) {
+  const int nb = Lmax >> 3;
+  for (int it = lane; it < nkv * D; it += WAVE) {
     const int kh = it / D;
     const int d = it - kh * D;
-    vt_cache[(((size_t)s * nkv + kh) * D + d) * Lmax + p] = v[it];
+    vt_cache[((((size_t)s * nkv + kh) * nb + (p >> 3)) * D + d) * 8 + (p & 7)] = v[it];
   }
 }
 
@@ -300,7 +326,9 @@ __global__ void __launch_bounds__(64) attn_prefill_kernel(
       const int d = 16 * n + r16;
       uint4 vv = make_uint4(0, 0, 0, 0);
       if (kk < nkeys) {
-        const uint16_t* vrow = pre ? (vpre + (size_t)d * P0pad + kk) : (vself + (size_t)d * Lmax + (kk - P0pad));
+        // blocked V^T: 8 keys of dim d = one 16-byte chunk at ((key/8) * D + d) * 8
+        const uint16_t* vrow = pre ? (vpre + ((size_t)(kk >> 3) * D + d) * 8)
+                                   : (vself + ((size_t)((kk - P0pad) >> 3) * D + d) * 8);
         vv = *reinterpret_cast<const uint4*>(vrow);
       }
       o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vv), o[n], 0, 0, 0);
@@ -319,27 +347,32 @@ __global__ void __launch_bounds__(64) attn_prefill_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Decode attention: one query token per sequence. grid = (B, nkv), block 256.
-// Phase 1: scores of the G = nh/nkv heads for every key (8 lanes per key row).
-// Phase 2: softmax. Phase 3: P·V with lane = dim, 4 contiguous key ranges.
+// Decode attention: one query token per sequence; grid = (B, nkv), ONE wave per
+// (sequence, kv head) computing its G = nh/nkv query heads, so every K/V byte is
+// read once per GQA group. Finished rows exit immediately (done[b] != 0).
+// Score index space: [prefix 0..P0pad) ++ [own 0..own8) with padding p = 0.
+//   phase 1  8 lanes per key row (16 B each), 16 keys in flight per iteration
+//   phase 2  softmax per head (lane-strided over the scores in LDS)
+//   phase 3  lane = dim; blocked V^T gives 8 keys of the lane's dim per 16-B
+//            load, the wave reading 1 KiB contiguously per chunk
 // ---------------------------------------------------------------------------
-#define DEC_MAXCTX 1024
+#define DEC_MAXCTX 512
 #define DEC_MAXG 4
-__global__ void __launch_bounds__(256) attn_decode_kernel(
+__global__ void __launch_bounds__(64) attn_decode_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
-    const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache, const uint16_t* __restrict__ pk,
-    const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out, int nh, int nkv, int Lmax,
-    float scale_log2) {
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
+    uint16_t* __restrict__ out, int nh, int nkv, int Lmax, float scale_log2) {
   constexpr int D = 64;
   const int b = blockIdx.x, kh = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int lane = threadIdx.x;
+  if (done != nullptr && done[b]) return;
   const int G = nh / nkv;
-  const int own = pos[b] + 1;  // own keys 0..pos inclusive
+  const int own = pos[b] + 1;              // own keys 0..pos inclusive
+  const int own8 = (own + 7) & ~7;
   const int sl = slot[b];
-  const int nk = P0 + own;     // logical keys: prefix [0,P0) then own
-  __shared__ float sc[DEC_MAXG][DEC_MAXCTX];
-  __shared__ float red[4][DEC_MAXG][D];
-  __shared__ float stat[2][DEC_MAXG];
+  const int ns = P0pad + own8;             // padded score count
+  __shared__ __attribute__((aligned(16))) float sc[DEC_MAXG][DEC_MAXCTX];
 
   const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
   const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
@@ -347,103 +380,87 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(
   const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
 
   // phase 1 ------------------------------------------------------------------
-  const int dc = lane & 7;
+  const int dc = lane & 7, kr = lane >> 3;
   float qf[DEC_MAXG][8];
 #pragma unroll
   for (int g = 0; g < DEC_MAXG; ++g) {
-    if (g < G) {
-      uint4 v = *reinterpret_cast<const uint4*>(q + ((size_t)b * nh + kh * G + g) * D + 8 * dc);
-      unpack8(v, qf[g]);
-    }
+    if (g < G) unpack8(*reinterpret_cast<const uint4*>(q + ((size_t)b * nh + kh * G + g) * D + 8 * dc), qf[g]);
   }
-  for (int k = wid * 8 + (lane >> 3); k < nk; k += 32) {
-    const uint16_t* krow = (k < P0) ? (kpre + (size_t)k * D) : (kself + (size_t)(k - P0) * D);
-    float kf[8];
-    unpack8(*reinterpret_cast<const uint4*>(krow + 8 * dc), kf);
+  auto score_rows = [&](const uint16_t* base, int nkeys, int sbase) {
+    for (int k0 = 0; k0 < nkeys; k0 += 16) {
+      const int ka = k0 + kr, kb = k0 + 8 + kr;
+      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+      if (ka < nkeys) va = *reinterpret_cast<const uint4*>(base + (size_t)ka * D + 8 * dc);
+      if (kb < nkeys) vb = *reinterpret_cast<const uint4*>(base + (size_t)kb * D + 8 * dc);
+      float fa[8], fb[8];
+      unpack8(va, fa);
+      unpack8(vb, fb);
 #pragma unroll
-    for (int g = 0; g < DEC_MAXG; ++g) {
-      if (g < G) {
-        float acc = 0.f;
+      for (int g = 0; g < DEC_MAXG; ++g) {
+        if (g < G) {
+          float sa = 0.f, sb = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc += qf[g][j] * kf[j];
-        acc += __shfl_xor(acc, 1, WAVE);
-        acc += __shfl_xor(acc, 2, WAVE);
-        acc += __shfl_xor(acc, 4, WAVE);
-        if (dc == 0) sc[g][k] = acc * scale_log2;
+          for (int j = 0; j < 8; ++j) { sa += qf[g][j] * fa[j]; sb += qf[g][j] * fb[j]; }
+#pragma unroll
+          for (int o = 1; o < 8; o <<= 1) { sa += __shfl_xor(sa, o, WAVE); sb += __shfl_xor(sb, o, WAVE); }
+          if (dc == 0) {
+            if (ka < nkeys) sc[g][sbase + ka] = sa * scale_log2;
+            if (kb < nkeys) sc[g][sbase + kb] = sb * scale_log2;
+          }
+        }
       }
     }
-  }
+  };
+  score_rows(kpre, P0, 0);
+  score_rows(kself, own, P0pad);
   __syncthreads();
   // phase 2 ------------------------------------------------------------------
-  for (int g = 0; g < G; ++g) {
+  float inv_sum[DEC_MAXG];
+#pragma unroll
+  for (int g = 0; g < DEC_MAXG; ++g) {
+    inv_sum[g] = 0.f;
+    if (g >= G) continue;
     float mx = -INFINITY;
-    for (int k = tid; k < nk; k += 256) mx = fmaxf(mx, sc[g][k]);
+    for (int i = lane; i < ns; i += WAVE) {
+      const bool ok = (i < P0) || (i >= P0pad && i - P0pad < own);
+      if (ok) mx = fmaxf(mx, sc[g][i]);
+    }
     mx = wave_max(mx);
-    if (lane == 0) red[wid][g][0] = mx;
-  }
-  __syncthreads();
-  if (tid < G) stat[0][tid] = fmaxf(fmaxf(red[0][tid][0], red[1][tid][0]), fmaxf(red[2][tid][0], red[3][tid][0]));
-  __syncthreads();
-  for (int g = 0; g < G; ++g) {
-    const float mx = stat[0][g];
     float sm = 0.f;
-    for (int k = tid; k < nk; k += 256) {
-      const float p = exp2f(sc[g][k] - mx);
-      sc[g][k] = p;
+    for (int i = lane; i < ns; i += WAVE) {
+      const bool ok = (i < P0) || (i >= P0pad && i - P0pad < own);
+      const float p = ok ? exp2f(sc[g][i] - mx) : 0.f;
+      sc[g][i] = p;
       sm += p;
     }
-    sm = wave_sum(sm);
-    if (lane == 0) red[wid][g][1] = sm;
+    inv_sum[g] = 1.f / wave_sum(sm);
   }
-  __syncthreads();
-  if (tid < G) stat[1][tid] = red[0][tid][1] + red[1][tid][1] + red[2][tid][1] + red[3][tid][1];
   __syncthreads();
   // phase 3 ------------------------------------------------------------------
   const int d = lane;
   float acc[DEC_MAXG];
 #pragma unroll
   for (int g = 0; g < DEC_MAXG; ++g) acc[g] = 0.f;
-  // prefix keys [0, P0): chunked by 8, split over the 4 waves
-  {
-    const int nch = (P0 + 7) >> 3;
-    for (int c = wid; c < nch; c += 4) {
+  auto pv_chunks = [&](const uint16_t* vbase, int nchunks, int sbase) {
+    for (int c = 0; c < nchunks; ++c) {
       float vf[8];
-      unpack8(*reinterpret_cast<const uint4*>(vpre + (size_t)d * P0pad + 8 * c), vf);
+      unpack8(*reinterpret_cast<const uint4*>(vbase + ((size_t)c * D + d) * 8), vf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * c + j;
-        if (k < P0) {
-#pragma unroll
-          for (int g = 0; g < DEC_MAXG; ++g)
-            if (g < G) acc[g] += sc[g][k] * vf[j];
+      for (int g = 0; g < DEC_MAXG; ++g) {
+        if (g < G) {
+          const float4 p0 = *reinterpret_cast<const float4*>(&sc[g][sbase + 8 * c]);
+          const float4 p1 = *reinterpret_cast<const float4*>(&sc[g][sbase + 8 * c + 4]);
+          acc[g] += p0.x * vf[0] + p0.y * vf[1] + p0.z * vf[2] + p0.w * vf[3] +
+                    p1.x * vf[4] + p1.y * vf[5] + p1.z * vf[6] + p1.w * vf[7];
         }
       }
     }
-    const int nch2 = (own + 7) >> 3;
-    for (int c = wid; c < nch2; c += 4) {
-      float vf[8];
-      unpack8(*reinterpret_cast<const uint4*>(vself + (size_t)d * Lmax + 8 * c), vf);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * c + j;
-        if (k < own) {
-#pragma unroll
-          for (int g = 0; g < DEC_MAXG; ++g)
-            if (g < G) acc[g] += sc[g][P0 + k] * vf[j];
-        }
-      }
-    }
-  }
+  };
+  pv_chunks(vpre, P0pad >> 3, 0);
+  pv_chunks(vself, own8 >> 3, P0pad);
 #pragma unroll
   for (int g = 0; g < DEC_MAXG; ++g)
-    if (g < G) red[wid][g][d] = acc[g];
-  __syncthreads();
-  if (wid == 0) {
-    for (int g = 0; g < G; ++g) {
-      const float v = red[0][g][d] + red[1][g][d] + red[2][g][d] + red[3][g][d];
-      out[((size_t)b * nh + kh * G + g) * D + d] = f2bf(v / stat[1][g]);
-    }
-  }
+    if (g < G) out[((size_t)b * nh + kh * G + g) * D + d] = f2bf(acc[g] * inv_sum[g]);
 }
 
 // ---------------------------------------------------------------------------
@@ -539,7 +556,7 @@ extern "C" {
 
 int sg_rmsnorm_residual(const void* x_in, void* residual, const void* w, void* out, int T, int H, float eps,
                         hipStream_t stream) {
-  if (H % 8) return -1;
+  if (H % 8 || H > 2048) return -1;
   if (T == 0) return 0;
   dim3 grid((T + 3) / 4);
   hipLaunchKernelGGL(rmsnorm_residual_kernel, grid, dim3(256), 0, stream, (const uint16_t*)x_in, (uint16_t*)residual,
@@ -562,9 +579,10 @@ int sg_rope_qkv_cache(const void* qkv, const int* pos, const int* slot, const vo
                       hipStream_t stream) {
   if (D % 2) return -1;
   if (T == 0) return 0;
-  hipLaunchKernelGGL(rope_qkv_cache_kernel, dim3(T), dim3(256), 0, stream, (const uint16_t*)qkv, pos, slot,
-                     (const float2*)cos_sin, (uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)vt_cache, nh, nkv, D,
-                     Lmax, p0);
+  if (Lmax % 8) return -1;
+  hipLaunchKernelGGL(rope_qkv_cache_kernel, dim3((T + 3) / 4), dim3(256), 0, stream, (const uint16_t*)qkv, pos, slot,
+                     (const float2*)cos_sin, (uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)vt_cache, T, nh, nkv,
+                     D, Lmax, p0);
   return (int)hipGetLastError();
 }
 
@@ -580,12 +598,14 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   return (int)hipGetLastError();
 }
 
-int sg_attn_decode(const void* q, const int* pos, const int* slot, const void* k_cache, const void* vt_cache,
-                   const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh, int nkv, int D,
-                   int Lmax, float scale, hipStream_t stream) {
-  if (D != 64 || nh % nkv || nh / nkv > DEC_MAXG || P0 + Lmax > DEC_MAXCTX || (P0pad % 8) || (Lmax % 8)) return -1;
+int sg_attn_decode(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                   const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh,
+                   int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > DEC_MAXG || P0pad + Lmax > DEC_MAXCTX || (P0pad % 8) || (Lmax % 8) ||
+      P0 > P0pad)
+    return -1;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(attn_decode_kernel, dim3(B, nkv), dim3(256), 0, stream, (const uint16_t*)q, pos, slot,
+  hipLaunchKernelGGL(attn_decode_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, pos, slot, done,
                      (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt, P0,
                      P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
   return (int)hipGetLastError();

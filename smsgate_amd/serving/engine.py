@@ -5,7 +5,7 @@ One engine = one MI355X = one data-parallel replica (``smsgate_amd.parallel``).
 Per engine:
 
 * **weights** in serving layout (270 MB bf16 for the 135M extractor);
-* **KV cache** ``K[L][slots][nkv][Lmax][D]`` and ``V^T[L][slots][nkv][D][Lmax]``,
+* **KV cache** ``K[L][slots][nkv][Lmax][D]`` and blocked ``V^T[L][slots][nkv][Lmax/8][D][8]``,
   zero-initialised, one fixed region per slot — at ~4.6 MB/slot (135M model,
   ``Lmax`` 200) thousands of concurrent sequences fit in 288 GB, so there is no
   paging/block-table indirection in the attention kernels;
@@ -82,6 +82,14 @@ class _Pending:
     ids: List[int]
 
 
+@dataclass
+class _Snapshot:
+    B: int
+    event: Any
+    bufs: Dict[str, torch.Tensor]
+    active: Dict[int, Any]  # row -> key at snapshot time (guards against re-admitted rows)
+
+
 class ExtractionEngine:
     def __init__(self, weights: ExtractorWeights, tokenizer: ExtractorTokenizer,
                  cfg: Optional[EngineConfig] = None, fields: Sequence[FieldSpec] = DEFAULT_FIELDS,
@@ -103,14 +111,14 @@ class ExtractionEngine:
         self.P0 = len(self.prefix_ids)
         self.P0pad = _round_up(self.P0, 32)
         self.Lmax = _round_up(ec.max_body_tokens + 2 + self.max_out, 8)
-        if self.P0 + self.Lmax > 1024:
-            raise ValueError("prefix + Lmax exceeds the decode kernel's context limit (1024)")
+        if self.P0pad + self.Lmax > 512:
+            raise ValueError("prefix + Lmax exceeds the decode kernel's context limit (512)")
         S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
         dev, bf = self.device, torch.bfloat16
         self.k_cache = torch.zeros(L, S, nkv, self.Lmax, D, dtype=bf, device=dev)
-        self.vt_cache = torch.zeros(L, S, nkv, D, self.Lmax, dtype=bf, device=dev)
+        self.vt_cache = torch.zeros(L, *ops.vt_shape(S, nkv, D, self.Lmax), dtype=bf, device=dev)
         self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
-        self.pvt = torch.zeros(L, nkv, D, self.P0pad, dtype=bf, device=dev)
+        self.pvt = torch.zeros(L, *ops.vt_shape(1, nkv, D, self.P0pad)[1:], dtype=bf, device=dev)
         self.cos_sin = ops.rope_table(self.P0 + self.Lmax + 1, D, mc.rope_theta, dev)
         self.scale = 1.0 / math.sqrt(D)
         i32 = dict(dtype=torch.int32, device=dev)
@@ -128,6 +136,15 @@ class ExtractionEngine:
         self.stats = EngineStats()
         self.graphs: Dict[int, torch.cuda.CUDAGraph] = {}
         self._pool = None
+        # double-buffered pinned host snapshots of the row state (see step())
+        self._host_bufs = [
+            {"done": torch.zeros(S, dtype=torch.int32).pin_memory(),
+             "len": torch.zeros(S, dtype=torch.int32).pin_memory(),
+             "buf": torch.zeros(S, self.max_out, dtype=torch.int32).pin_memory()}
+            for _ in range(2)
+        ]
+        self._snap_flip = 0
+        self._pending: Optional[_Snapshot] = None
         self._compute_prefix()
         if ec.use_graphs:
             self._capture_graphs()
@@ -164,7 +181,7 @@ class ExtractionEngine:
         qs = torch.zeros(1, dtype=torch.int32, device=self.device)
         s1 = torch.zeros(1, dtype=torch.int32, device=self.device)
         empty_k = torch.zeros(self.mc.kv_heads, 0, self.mc.head_dim, dtype=torch.bfloat16, device=self.device)
-        empty_v = torch.zeros(self.mc.kv_heads, self.mc.head_dim, 0, dtype=torch.bfloat16, device=self.device)
+        empty_v = torch.zeros(self.mc.kv_heads, 0, self.mc.head_dim, 8, dtype=torch.bfloat16, device=self.device)
 
         def kc(i):
             return self.pk[i].unsqueeze(0)
@@ -245,7 +262,8 @@ class ExtractionEngine:
             return self.vt_cache[i]
 
         def attn(i, q, out):
-            ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale)
+            ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
+                            done=self.done)
 
         h = self._layers(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
         logits = F.linear(h, self.w.embed)
@@ -322,7 +340,7 @@ class ExtractionEngine:
             self.waiting.append(_Pending(k, ids))
 
     def busy(self) -> bool:
-        return bool(self.waiting or self.active)
+        return bool(self.waiting or self.active or self._pending is not None)
 
     def _admit(self) -> None:
         S = self.cfg.max_slots
@@ -352,30 +370,45 @@ class ExtractionEngine:
             out[f.name] = self.tok.decode(vals[i]).strip() if i < len(vals) else None
         return out
 
-    def _harvest(self, B: int) -> List[Tuple[Any, Dict[str, Optional[str]]]]:
+    def _snapshot(self, B: int) -> "_Snapshot":
+        """Queue an async D2H copy of the row state after the chunk just launched."""
+        i = self._snap_flip
+        self._snap_flip ^= 1
+        hb = self._host_bufs[i]
+        hb["done"][:B].copy_(self.done[:B], non_blocking=True)
+        hb["len"][:B].copy_(self.out_len[:B], non_blocking=True)
+        hb["buf"][:B].copy_(self.out_buf[:B], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return _Snapshot(B, ev, hb, dict(self.active))
+
+    def _harvest(self, snap: "_Snapshot") -> List[Tuple[Any, Dict[str, Optional[str]]]]:
         t0 = time.perf_counter()
-        done_h = self.done[:B].cpu()
-        fin = [r for r in self.active if r < B and done_h[r]]
+        snap.event.synchronize()
+        done_h = snap.bufs["done"][: snap.B].numpy()
         res: List[Tuple[Any, Dict[str, Optional[str]]]] = []
-        if fin:
-            idx = torch.tensor(fin, dtype=torch.long, device=self.device)
-            bufs = self.out_buf.index_select(0, idx).cpu().tolist()
-            lens = self.out_len.index_select(0, idx).cpu().tolist()
-            for r, buf, n in zip(fin, bufs, lens):
-                res.append((self.active.pop(r), self._decode_answer(buf[:n])))
+        lens = snap.bufs["len"]
+        bufs = snap.bufs["buf"]
+        for r, key in snap.active.items():
+            if r < snap.B and done_h[r] and self.active.get(r) is key:
+                n = int(lens[r])
+                res.append((self.active.pop(r), self._decode_answer(bufs[r, :n].tolist())))
                 heapq.heappush(self.free_rows, r)
         self.stats.completed += len(res)
         self.stats.harvest_s += time.perf_counter() - t0
         return res
 
     def step(self) -> List[Tuple[Any, Dict[str, Optional[str]]]]:
-        """Admit → one decode chunk → harvest. Returns finished ``(key, answer)``."""
+        """Admit → launch one decode chunk → harvest the *previous* chunk's snapshot
+        (the GPU runs chunk k while the host decodes chunk k-1's finished rows).
+        Returns finished ``(key, answer)``."""
         self._admit()
-        if not self.active:
-            return []
-        B = self._bucket(max(self.active) + 1)
-        self._run_decode(B)
-        return self._harvest(B)
+        prev, self._pending = self._pending, None
+        if self.active:
+            B = self._bucket(max(self.active) + 1)
+            self._run_decode(B)
+            self._pending = self._snapshot(B)
+        return self._harvest(prev) if prev is not None else []
 
     def run(self, bodies: Sequence[str]) -> List[Dict[str, Optional[str]]]:
         """Synchronous batch extraction (tests, benchmarks)."""

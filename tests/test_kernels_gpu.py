@@ -56,7 +56,7 @@ def test_rope_qkv_cache():
     cs = ops.rope_table(p0 + Lmax + 1, D, 1e5, DEV)
     q = torch.empty(T, nh, D, dtype=torch.bfloat16, device=DEV)
     kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
-    vt = torch.zeros(S, nkv, D, Lmax, dtype=torch.bfloat16, device=DEV)
+    vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=DEV)
     ops.rope_qkv_cache(qkv, pos, slot, cs, q, kc, vt, nh, nkv, D, p0)
     qf, kf, vf = qkv.float().split([nh * D, nkv * D, nkv * D], -1)
     absp = (pos + p0).long()
@@ -65,7 +65,7 @@ def test_rope_qkv_cache():
     torch.testing.assert_close(q.float(), qr, atol=2e-2, rtol=2e-2)
     sl, ps = slot.long(), pos.long()
     torch.testing.assert_close(kc[sl, :, ps, :].float(), kr, atol=2e-2, rtol=2e-2)
-    got_v = vt[sl, :, :, ps]  # [T, nkv, D]
+    got_v = ops.vt_to_rows(vt)[sl, :, ps, :]  # [T, nkv, D]
     assert torch.equal(got_v.float(), vf.view(T, nkv, D))
 
 
@@ -96,12 +96,14 @@ def test_attn_prefill(P0):
     T = sum(lens)
     q = _bf(T, nh, D, seed=4)
     kc = _bf(S, nkv, Lmax, D, seed=5)
-    vt = _bf(S, nkv, D, Lmax, seed=6)
+    vrows = _bf(S, nkv, Lmax, D, seed=6)
+    vt = ops.rows_to_vt(vrows)
     pk = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
-    pvt = torch.zeros(nkv, D, P0pad, dtype=torch.bfloat16, device=DEV)
+    pvrows = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
     if P0:
         pk[:, :P0] = _bf(nkv, P0, D, seed=7)
-        pvt[:, :, :P0] = _bf(nkv, D, P0, seed=8)
+        pvrows[:, :P0] = _bf(nkv, P0, D, seed=8)
+    pvt = ops.rows_to_vt(pvrows)
     cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32, device=DEV)
     qs = torch.tensor(starts, dtype=torch.int32, device=DEV)
     sl = torch.tensor(rows, dtype=torch.int32, device=DEV)
@@ -112,9 +114,9 @@ def test_attn_prefill(P0):
     for n, st, r in zip(lens, starts, rows):
         nown = st + n
         own_k = kc[r, :, :nown].permute(1, 0, 2).float()
-        own_v = vt[r, :, :, :nown].permute(2, 0, 1).float()
+        own_v = vrows[r, :, :nown].permute(1, 0, 2).float()
         ref = _ref_seq_attention(q[o:o + n].float(), own_k, own_v, pk[:, :P0].permute(1, 0, 2).float(),
-                                 pvt[:, :, :P0].permute(2, 0, 1).float(), P0, list(range(st, st + n)), scale)
+                                 pvrows[:, :P0].permute(1, 0, 2).float(), P0, list(range(st, st + n)), scale)
         torch.testing.assert_close(out[o:o + n].float().view(n, nh, D), ref, atol=3e-2, rtol=3e-2)
         o += n
 
@@ -126,23 +128,30 @@ def test_attn_decode(P0):
     B = 6
     q = _bf(B, nh, D, seed=9)
     kc = _bf(S, nkv, Lmax, D, seed=10)
-    vt = _bf(S, nkv, D, Lmax, seed=11)
-    pk = torch.zeros(nkv, max(P0pad, 0), D, dtype=torch.bfloat16, device=DEV)
-    pvt = torch.zeros(nkv, D, max(P0pad, 0), dtype=torch.bfloat16, device=DEV)
+    vrows = _bf(S, nkv, Lmax, D, seed=11)
+    vt = ops.rows_to_vt(vrows)
+    pk = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
+    pvrows = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
     if P0:
         pk[:, :P0] = _bf(nkv, P0, D, seed=12)
-        pvt[:, :, :P0] = _bf(nkv, D, P0, seed=13)
+        pvrows[:, :P0] = _bf(nkv, P0, D, seed=13)
+    pvt = ops.rows_to_vt(pvrows)
     pos = torch.tensor([0, 1, 7, 8, 100, 199], dtype=torch.int32, device=DEV)
     slot = torch.tensor([3, 0, 7, 1, 2, 5], dtype=torch.int32, device=DEV)
-    out = torch.empty(B, nh * D, dtype=torch.bfloat16, device=DEV)
+    out = torch.full((B, nh * D), 7.0, dtype=torch.bfloat16, device=DEV)
     scale = 1 / math.sqrt(D)
-    ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, scale)
+    done = torch.zeros(B, dtype=torch.int32, device=DEV)
+    done[2] = 1  # finished rows are skipped
+    ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, scale, done=done)
     for b in range(B):
+        if b == 2:
+            assert torch.all(out[b] == 7.0)
+            continue
         p, r = int(pos[b]), int(slot[b])
         own_k = kc[r, :, : p + 1].permute(1, 0, 2).float()
-        own_v = vt[r, :, :, : p + 1].permute(2, 0, 1).float()
+        own_v = vrows[r, :, : p + 1].permute(1, 0, 2).float()
         ref = _ref_seq_attention(q[b:b + 1].float(), own_k, own_v, pk[:, :P0].permute(1, 0, 2).float(),
-                                 pvt[:, :, :P0].permute(2, 0, 1).float(), P0, [p], scale)
+                                 pvrows[:, :P0].permute(1, 0, 2).float(), P0, [p], scale)
         torch.testing.assert_close(out[b].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)
 
 

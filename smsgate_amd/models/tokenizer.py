@@ -72,6 +72,9 @@ class ExtractorTokenizer:
     def decode(self, ids: Sequence[int]) -> str:
         return self.tk.decode(list(ids), skip_special_tokens=True)
 
+    def decode_batch(self, seqs: Sequence[Sequence[int]]) -> List[str]:
+        return self.tk.decode_batch([list(s) for s in seqs], skip_special_tokens=True)
+
     @functools.cached_property
     def token_strings(self) -> List[str]:
         """Decoded text of every id (specials → their literal)."""

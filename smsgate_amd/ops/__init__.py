@@ -56,6 +56,8 @@ def _declare(lib: ctypes.CDLL) -> None:
                                     _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
     lib.sg_attn_decode.argtypes = [_vp, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
                                    _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
+    lib.sg_attn_decode_valu.argtypes = lib.sg_attn_decode.argtypes
+    lib.sg_attn_decode_valu.restype = _c_int
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
                                   ctypes.c_uint, _vp]
@@ -183,16 +185,20 @@ def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slo
 
 def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache: torch.Tensor,
                 vt_cache: torch.Tensor, pk: torch.Tensor, pvt: torch.Tensor, P0: int, out: torch.Tensor,
-                scale: float, done: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """One query token per row; rows with ``done[b] != 0`` are skipped (output untouched)."""
+                scale: float, done: Optional[torch.Tensor] = None, impl: str = "mfma") -> torch.Tensor:
+    """One query token per row; rows with ``done[b] != 0`` are skipped (output untouched).
+
+    ``impl="mfma"`` (default) packs the GQA heads of a KV head into one MFMA tile;
+    ``impl="valu"`` is the vector-ALU variant kept for A/B measurement."""
     B, nh, D = q.shape
     S, nkv, Lmax, _ = k_cache.shape
     P0pad = pk.shape[1]
     assert pos.numel() == B and slot.numel() == B and (done is None or done.numel() >= B)
     assert vt_cache.shape == vt_shape(S, nkv, D, Lmax) and pvt.shape == vt_shape(1, nkv, D, P0pad)[1:]
-    _check(load_library().sg_attn_decode(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk),
-                                         _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, _stream()),
-           "attn_decode")
+    lib = load_library()
+    fn = lib.sg_attn_decode if impl == "mfma" else lib.sg_attn_decode_valu
+    _check(fn(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B,
+              nh, nkv, D, Lmax, scale, _stream()), f"attn_decode[{impl}]")
     return out
 
 

@@ -386,26 +386,31 @@ __global__ void __launch_bounds__(64) attn_decode_kernel(
   for (int g = 0; g < DEC_MAXG; ++g) {
     if (g < G) unpack8(*reinterpret_cast<const uint4*>(q + ((size_t)b * nh + kh * G + g) * D + 8 * dc), qf[g]);
   }
+  // Latency, not bandwidth, bounds this kernel (~140 keys per wave): every
+  // round issues DEC_UNR independent 16-B loads per lane before consuming any.
+  constexpr int DEC_UNR = 4;
   auto score_rows = [&](const uint16_t* base, int nkeys, int sbase) {
-    for (int k0 = 0; k0 < nkeys; k0 += 16) {
-      const int ka = k0 + kr, kb = k0 + 8 + kr;
-      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-      if (ka < nkeys) va = *reinterpret_cast<const uint4*>(base + (size_t)ka * D + 8 * dc);
-      if (kb < nkeys) vb = *reinterpret_cast<const uint4*>(base + (size_t)kb * D + 8 * dc);
-      float fa[8], fb[8];
-      unpack8(va, fa);
-      unpack8(vb, fb);
+    for (int k0 = 0; k0 < nkeys; k0 += 8 * DEC_UNR) {
+      uint4 kv[DEC_UNR];
 #pragma unroll
-      for (int g = 0; g < DEC_MAXG; ++g) {
-        if (g < G) {
-          float sa = 0.f, sb = 0.f;
+      for (int u = 0; u < DEC_UNR; ++u) {
+        const int k = k0 + 8 * u + kr;
+        kv[u] = (k < nkeys) ? *reinterpret_cast<const uint4*>(base + (size_t)k * D + 8 * dc) : make_uint4(0, 0, 0, 0);
+      }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { sa += qf[g][j] * fa[j]; sb += qf[g][j] * fb[j]; }
+      for (int u = 0; u < DEC_UNR; ++u) {
+        const int k = k0 + 8 * u + kr;
+        float f[8];
+        unpack8(kv[u], f);
 #pragma unroll
-          for (int o = 1; o < 8; o <<= 1) { sa += __shfl_xor(sa, o, WAVE); sb += __shfl_xor(sb, o, WAVE); }
-          if (dc == 0) {
-            if (ka < nkeys) sc[g][sbase + ka] = sa * scale_log2;
-            if (kb < nkeys) sc[g][sbase + kb] = sb * scale_log2;
+        for (int g = 0; g < DEC_MAXG; ++g) {
+          if (g < G) {
+            float sa = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sa += qf[g][j] * f[j];
+#pragma unroll
+            for (int o = 1; o < 8; o <<= 1) sa += __shfl_xor(sa, o, WAVE);
+            if (dc == 0 && k < nkeys) sc[g][sbase + k] = sa * scale_log2;
           }
         }
       }
@@ -442,16 +447,26 @@ __global__ void __launch_bounds__(64) attn_decode_kernel(
 #pragma unroll
   for (int g = 0; g < DEC_MAXG; ++g) acc[g] = 0.f;
   auto pv_chunks = [&](const uint16_t* vbase, int nchunks, int sbase) {
-    for (int c = 0; c < nchunks; ++c) {
-      float vf[8];
-      unpack8(*reinterpret_cast<const uint4*>(vbase + ((size_t)c * D + d) * 8), vf);
+    for (int c0 = 0; c0 < nchunks; c0 += DEC_UNR) {
+      uint4 vv[DEC_UNR];
 #pragma unroll
-      for (int g = 0; g < DEC_MAXG; ++g) {
-        if (g < G) {
-          const float4 p0 = *reinterpret_cast<const float4*>(&sc[g][sbase + 8 * c]);
-          const float4 p1 = *reinterpret_cast<const float4*>(&sc[g][sbase + 8 * c + 4]);
-          acc[g] += p0.x * vf[0] + p0.y * vf[1] + p0.z * vf[2] + p0.w * vf[3] +
-                    p1.x * vf[4] + p1.y * vf[5] + p1.z * vf[6] + p1.w * vf[7];
+      for (int u = 0; u < DEC_UNR; ++u)
+        vv[u] = (c0 + u < nchunks) ? *reinterpret_cast<const uint4*>(vbase + ((size_t)(c0 + u) * D + d) * 8)
+                                   : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < DEC_UNR; ++u) {
+        const int c = c0 + u;
+        if (c >= nchunks) break;
+        float vf[8];
+        unpack8(vv[u], vf);
+#pragma unroll
+        for (int g = 0; g < DEC_MAXG; ++g) {
+          if (g < G) {
+            const float4 p0 = *reinterpret_cast<const float4*>(&sc[g][sbase + 8 * c]);
+            const float4 p1 = *reinterpret_cast<const float4*>(&sc[g][sbase + 8 * c + 4]);
+            acc[g] += p0.x * vf[0] + p0.y * vf[1] + p0.z * vf[2] + p0.w * vf[3] +
+                      p1.x * vf[4] + p1.y * vf[5] + p1.z * vf[6] + p1.w * vf[7];
+          }
         }
       }
     }
@@ -461,6 +476,158 @@ __global__ void __launch_bounds__(64) attn_decode_kernel(
 #pragma unroll
   for (int g = 0; g < DEC_MAXG; ++g)
     if (g < G) out[((size_t)b * nh + kh * G + g) * D + d] = f2bf(acc[g] * inv_sum[g]);
+}
+
+// ---------------------------------------------------------------------------
+// MFMA decode attention (the production decode path). grid = (B, nkv), one wave.
+// The G query heads that share a KV head are the rows of one 16-row MFMA tile
+// (rows >= G carry q = 0 and are never stored), so S = Q·K^T and O += P·V are
+// two and four mfma_f32_16x16x32_bf16 per 32-key tile — the arithmetic is free
+// and the kernel reduces to streaming K/V once per GQA group. Tile t+1's K/V
+// (8 × 16-B loads per lane) is issued before tile t is consumed, and finished
+// rows exit at once. Layouts and the prefix/own key spaces as in prefill.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) attn_decode_mfma_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
+    uint16_t* __restrict__ out, int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int b = blockIdx.x, kh = blockIdx.y, l = threadIdx.x;
+  if (done != nullptr && done[b]) return;
+  const int G = nh / nkv;
+  const int g4 = l >> 4, r16 = l & 15;
+  const int own = pos[b] + 1;
+  const int sl = slot[b];
+  __shared__ __attribute__((aligned(16))) uint16_t P_lds[16 * 32];
+
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+
+  bf16x8 qa[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r16 < G) v = *reinterpret_cast<const uint4*>(q + ((size_t)b * nh + kh * G + r16) * D + 8 * g4 + 32 * s);
+    qa[s] = __builtin_bit_cast(bf16x8, v);
+  }
+  const int npre = P0pad >> 5;
+  const int ntiles = npre + ((own + 31) >> 5);
+
+  auto load_tile = [&](int t, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
+    const bool pre = t < npre;
+    const int kt = pre ? t * 32 : (t - npre) * 32;
+    const int nval = pre ? P0 : own;
+    const uint16_t* kb = pre ? kpre : kself;
+    const uint16_t* vb = pre ? vpre : vself;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const int key = kt + 16 * hs + r16;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        kv[hs][s] = key < nval ? *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 8 * g4 + 32 * s)
+                               : make_uint4(0, 0, 0, 0);
+    }
+    const int kk = kt + 8 * g4;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      vv[n] = kk < nval ? *reinterpret_cast<const uint4*>(vb + ((size_t)(kk >> 3) * D + 16 * n + r16) * 8)
+                        : make_uint4(0, 0, 0, 0);
+  };
+
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[4], lsum[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m[i] = -INFINITY; lsum[i] = 0.f; }
+
+  uint4 kc[2][2], vc[4], kn[2][2], vn[4];
+  load_tile(0, kc, vc);
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) load_tile(t + 1, kn, vn);
+    const bool pre = t < npre;
+    const int kt = pre ? t * 32 : (t - npre) * 32;
+    const int nval = pre ? P0 : own;
+    f32x4 sacc[2];
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      sacc[hs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        sacc[hs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], __builtin_bit_cast(bf16x8, kc[hs][s]), sacc[hs],
+                                                           0, 0, 0);
+    }
+    float sv[2][4], tmax[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tmax[i] = -INFINITY;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const bool ok = (kt + 16 * hs + r16) < nval;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v = ok ? sacc[hs][i] * scale_log2 : -INFINITY;
+        sv[hs][i] = v;
+        tmax[i] = fmaxf(tmax[i], v);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o2 = 8; o2 > 0; o2 >>= 1) tmax[i] = fmaxf(tmax[i], __shfl_xor(tmax[i], o2, WAVE));
+    }
+    float alpha[4], rs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float mn = fmaxf(m[i], tmax[i]);
+      alpha[i] = (mn == -INFINITY) ? 1.f : exp2f(m[i] - mn);
+      m[i] = mn;
+      rs[i] = 0.f;
+    }
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = (m[i] == -INFINITY) ? 0.f : exp2f(sv[hs][i] - m[i]);
+        rs[i] += p;
+        P_lds[(4 * g4 + i) * 32 + 16 * hs + r16] = f2bf(p);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o2 = 8; o2 > 0; o2 >>= 1) rs[i] += __shfl_xor(rs[i], o2, WAVE);
+      lsum[i] = lsum[i] * alpha[i] + rs[i];
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[n][i] *= alpha[i];
+    }
+    __syncthreads();
+    const bf16x8 pa = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&P_lds[r16 * 32 + 8 * g4]));
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vc[n]), o[n], 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) kc[hs][s] = kn[hs][s];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) vc[n] = vn[n];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 4 * g4 + i;
+    if (row >= G) continue;
+    const float inv = 1.f / lsum[i];
+    uint16_t* orow = out + ((size_t)b * nh + kh * G + row) * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) orow[16 * n + r16] = f2bf(o[n][i] * inv);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -601,6 +768,18 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
 int sg_attn_decode(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
                    const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh,
                    int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 8) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(attn_decode_mfma_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, pos, slot, done,
+                     (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt, P0,
+                     P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// VALU reference implementation (kept for A/B measurement: scripts/kbench.py).
+int sg_attn_decode_valu(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                        const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B,
+                        int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
   if (D != 64 || nh % nkv || nh / nkv > DEC_MAXG || P0pad + Lmax > DEC_MAXCTX || (P0pad % 8) || (Lmax % 8) ||
       P0 > P0pad)
     return -1;

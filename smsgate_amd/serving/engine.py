@@ -283,10 +283,12 @@ class ExtractionEngine:
         outs = [self._prefill(rows, items, sample=False).float()]
         lens = torch.tensor([len(it.ids) for it in items], dtype=torch.int32, device=self.device)
         self.pos[:n] = lens - 1
+        self.done[:n] = 0  # attention skips finished rows
         for step in range(len(forced[0]) if forced else 0):
             self.tok_buf[:n] = torch.tensor([f[step] for f in forced], dtype=torch.int32, device=self.device)
             self.pos[:n] += 1
             outs.append(self._decode_step(n, sample=False).float())
+        self.done[:n] = 1
         return outs
 
     def _bucket(self, n: int) -> int:
@@ -389,10 +391,22 @@ class ExtractionEngine:
         res: List[Tuple[Any, Dict[str, Optional[str]]]] = []
         lens = snap.bufs["len"]
         bufs = snap.bufs["buf"]
-        for r, key in snap.active.items():
-            if r < snap.B and done_h[r] and self.active.get(r) is key:
-                n = int(lens[r])
-                res.append((self.active.pop(r), self._decode_answer(bufs[r, :n].tolist())))
+        fin = [r for r, key in snap.active.items()
+               if r < snap.B and done_h[r] and self.active.get(r) is key]
+        if fin:
+            # one batched detokenisation (Rust, parallel) for every field of every finished row
+            nf = len(self.fsm.fields)
+            lens_l = lens[fin].tolist()
+            rows_l = bufs[fin].tolist()
+            pieces: List[List[int]] = []
+            for toks, n in zip(rows_l, lens_l):
+                vals = self.fsm.split_fields(toks[:n])
+                vals += [[]] * (nf - len(vals))
+                pieces.extend(vals)
+            texts = self.tok.decode_batch(pieces)
+            for j, r in enumerate(fin):
+                ans = {f.name: texts[j * nf + i].strip() for i, f in enumerate(self.fsm.fields)}
+                res.append((self.active.pop(r), ans))
                 heapq.heappush(self.free_rows, r)
         self.stats.completed += len(res)
         self.stats.harvest_s += time.perf_counter() - t0

@@ -121,8 +121,9 @@ def test_attn_prefill(P0):
         o += n
 
 
+@pytest.mark.parametrize("impl", ["mfma", "valu"])
 @pytest.mark.parametrize("P0", [0, 75])
-def test_attn_decode(P0):
+def test_attn_decode(P0, impl):
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 200
     P0pad = (P0 + 31) // 32 * 32
     B = 6
@@ -142,7 +143,7 @@ def test_attn_decode(P0):
     scale = 1 / math.sqrt(D)
     done = torch.zeros(B, dtype=torch.int32, device=DEV)
     done[2] = 1  # finished rows are skipped
-    ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, scale, done=done)
+    ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, scale, done=done, impl=impl)
     for b in range(B):
         if b == 2:
             assert torch.all(out[b] == 7.0)

@@ -131,3 +131,33 @@ def test_parsedsms_contracts():
     assert '"amount":"52.00"' in js
     assert '"currency":"USD"' in js
     assert ParsedSMS.model_validate_json(js) == p
+
+
+def _strptime_or_exc(s, fmt):
+    try:
+        return datetime.strptime(s, fmt)
+    except Exception as e:  # noqa: BLE001
+        return type(e)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_fast_date_paths_equal_strptime(seed):
+    """The integer fast paths of dates.py must agree with strptime everywhere."""
+    import random
+
+    from smsgate_amd.parse import dates
+
+    r = random.Random(seed)
+    for _ in range(3000):
+        d, m, y, hh, mm = (r.randint(0, 39), r.randint(0, 19), r.randint(0, 99), r.randint(0, 29), r.randint(0, 69))
+        s = f"{d:02d}.{m:02d}.{y:02d} {hh:02d}:{mm:02d}"
+        ref = _strptime_or_exc(s, "%d.%m.%y %H:%M")
+        if isinstance(ref, datetime):
+            assert dates.parse_custom_datetime(s) == ref
+        body_short, body_long = f"x {d:02d}.{m:02d}.{y:02d} y", f"x {d:02d}.{m:02d}.{2000 + y} y"
+        for body, fmt, txt in ((body_short, "%d.%m.%y", f"{d:02d}.{m:02d}.{y:02d}"),
+                               (body_long, "%d.%m.%Y", f"{d:02d}.{m:02d}.{2000 + y}")):
+            exp = _strptime_or_exc(txt, fmt)
+            got = dates.fix_broken_datetime(body, datetime(2020, 1, 1, 7, 8))
+            if isinstance(exp, datetime):
+                assert got == datetime.combine(exp.date(), datetime(2020, 1, 1, 7, 8).time())

@@ -5,21 +5,23 @@ Metric (BASELINE.json): the reference's own metric, "SMS msgs/sec through
 parser_worker", on config #1 — ``POST /sms/raw`` payload → bus ``sms.raw`` →
 parser → ``sms.parsed``/``sms.processing``/DLQ → ack.  The reference measured
 ~10.4 k msgs/s on one CPU core **with Gemini stubbed out (zero-cost LLM)** and
-its own stack stubbed.
+its broker stubbed.
 
-Here every message does strictly more work: the extraction runs on a *real*
-LLM — the 134.5 M-parameter SmolLM2-135M-architecture extractor (random-init
-weights: no checkpoint exists on the box) served on the MI355X with the HIP
-kernels of ``smsgate_amd.ops``, schema-FSM-constrained decoding, continuous
-batching and hipGraph-captured decode.  ``--backend fake`` reproduces the
-reference's stubbed-LLM config on the CPU for a like-for-like comparison.
+Here every message does strictly more work: extraction runs on a *real* LLM —
+the 134.5 M-parameter SmolLM2-135M-architecture extractor (random-init weights:
+no checkpoint exists on the box) on the MI355X through the HIP kernels of
+``smsgate_amd.ops``, schema-FSM-constrained decoding, continuous batching and
+hipGraph-captured decode.  ``--backend fake`` reproduces the reference's
+stubbed-LLM configuration on the CPU for a like-for-like comparison.
 
-One "step" = ``--msgs-per-step`` unique synthetic SMS per GPU (built with the
-gateway's payload→RawSMS mapping and published to the bus inside the timed
-region) fully processed and acked.  Under ``torchrun`` each rank is one
-data-parallel replica (its own GPU, bus partition and engine; weak scaling);
-timing uses barrier + ``torch.cuda.synchronize`` on both sides and the max
-over ranks; rank 0 prints one JSON line.
+Layout (``smsgate_amd.parallel.replica``): each rank = one GPU = one
+data-parallel replica; the rank process runs only the engine, and
+``--cpu-workers`` parser processes (spawned before the GPU is touched) each run
+a full parser stage on their own bus partition.  One "step" =
+``--msgs-per-step`` unique synthetic SMS per GPU, mapped to RawSMS and
+published to the bus *inside* the timed region, parsed, routed and acked.
+Timing: barrier + ``torch.cuda.synchronize`` on both sides, max over ranks
+(RCCL all-reduce); rank 0 prints one JSON line.  Weak scaling.
 """
 from __future__ import annotations
 
@@ -40,120 +42,123 @@ def _args(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--backend", default="local_llm", choices=["local_llm", "fake", "regex"])
     p.add_argument("--model", default="smollm-135m")
-    p.add_argument("--msgs-per-step", type=int, default=4096)
-    p.add_argument("--max-slots", type=int, default=2048)
+    p.add_argument("--msgs-per-step", type=int, default=8192)
+    p.add_argument("--max-slots", type=int, default=4096)
     p.add_argument("--steps-per-graph", type=int, default=8)
+    p.add_argument("--cpu-workers", type=int, default=8)
     p.add_argument("--concurrency", type=int, default=4)
-    p.add_argument("--batch", type=int, default=1024)
+    p.add_argument("--batch", type=int, default=512)
     p.add_argument("--verbose", action="store_true")
     return p.parse_args(argv)
 
 
-def _dist_setup(n: int):
-    if n <= 1 or "RANK" not in os.environ:
-        return 0, 1, 0, None
-    import torch
-    import torch.distributed as dist
+def _rank_env():
+    if "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), int(os.environ.get("LOCAL_RANK", "0"))
+    return 0, 1, 0
 
-    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", rank))
+
+# ------------------------------------------------------------------ GPU replica
+def run_replica(args, rank: int, world: int, local: int):
+    from smsgate_amd.parallel.replica import Coordinator, spawn_parser_workers
+
+    W = max(1, args.cpu_workers)
+    if args.msgs_per_step % W:
+        raise SystemExit("--msgs-per-step must be divisible by --cpu-workers")
+    cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128}
+    # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
+    procs, conns = spawn_parser_workers(W, rank, cfg)
+
+    # 2) GPU: device, RCCL group, engine
+    import torch
+
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, local, dist
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from smsgate_amd.parse.backends.local_llm import build_engine
+
+    t_init = time.perf_counter()
+    engine = build_engine(args.model, device=f"cuda:{local}", max_slots=args.max_slots,
+                          steps_per_graph=args.steps_per_graph)
+    init_s = time.perf_counter() - t_init
+    coord = Coordinator(engine, conns)
+    coord.wait_all("ready")
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    per_w = args.msgs_per_step // W
+
+    def seeds(first, n):
+        return [[1_000_003 * (rank + 1) + 7919 * w + s for s in range(first, first + n)] for w in range(W)]
+
+    if args.warmup:
+        coord.run_phase(seeds(0, args.warmup), per_w)
+    engine.stats.__init__()
+    dt, counts = coord.run_phase(seeds(args.warmup, args.steps), per_w, sync=sync)
+    coord.shutdown(procs)
+    estats = engine.stats.as_dict()
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.destroy_process_group()
+    return dt, counts, init_s, estats
 
 
-def _payloads(n: int, seed: int):
-    from smsgate_amd.services.gateway import RawSMSPayload
-    from smsgate_amd.utils.synth import generate
-
-    return [RawSMSPayload(device_id="bench", message=s.body, sender="BANK", timestamp=s.timestamp, source="device")
-            for s in generate(n, seed=seed)]
-
-
-async def _run(args, rank, world, local, dist):
-    import torch
-
+# ------------------------------------------------------------- CPU (stubbed LLM)
+async def _run_cpu(args):
     from smsgate_amd.bus import SUBJECT_RAW, MemoryBus
-    from smsgate_amd.obs.tracing import tracer
+    from smsgate_amd.parallel.replica import _payload_bytes
     from smsgate_amd.parse.backends import create_backend
     from smsgate_amd.parse.pipeline import ParsePipeline
     from smsgate_amd.services.gateway import payload_to_raw
     from smsgate_amd.services.parser import ParserWorker
 
-    use_gpu = args.backend == "local_llm"
-    if use_gpu:
-        kw = dict(model=args.model, device=f"cuda:{local}", max_slots=args.max_slots,
-                  steps_per_graph=args.steps_per_graph, max_batch=args.batch)
-        backend = create_backend("local_llm", **kw)
-    else:
-        backend = create_backend(args.backend) if args.backend != "fake" else create_backend("fake", max_batch=args.batch)
+    backend = create_backend("fake", max_batch=args.batch) if args.backend == "fake" else create_backend(args.backend)
     bus = MemoryBus()
     worker = ParserWorker(bus, ParsePipeline(backend), batch=args.batch, concurrency=args.concurrency,
                           stats_interval=0)
-    t_init = time.perf_counter()
     await worker.start()
-    init_s = time.perf_counter() - t_init
+    sets = [_payload_bytes(args.msgs_per_step, 1_000_003 + s) for s in range(args.warmup + args.steps)]
 
-    def sync():
-        if use_gpu:
-            torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    # Synthetic payloads are generated outside the timed region (they stand in
-    # for phones posting); mapping them to RawSMS and publishing is timed.
-    payload_sets = [_payloads(args.msgs_per_step, seed=1_000_003 * (rank + 1) + s)
-                    for s in range(args.warmup + args.steps)]
-
-    async def publish(step: int) -> None:
-        items = [(SUBJECT_RAW, payload_to_raw(p).model_dump_json().encode("utf-8")) for p in payload_sets[step]]
-        await bus.publish_many(items)
-
-    async def run_steps(first: int, n: int) -> None:
-        # Ingestion runs one step ahead of parsing (a continuous inflow): step
-        # s+1 is on the bus while step s is still being parsed.
+    async def run(first, n):
         base = worker.stage.processed
-        await publish(first)
+        pub = lambda i: bus.publish_many(  # noqa: E731
+            [(SUBJECT_RAW, payload_to_raw(p).model_dump_json().encode()) for p in sets[i]])
+        await pub(first)
         for i in range(n):
             if i + 1 < n:
-                await publish(first + i + 1)
-            target = base + (i + 1) * args.msgs_per_step
-            while worker.stage.processed < target:
+                await pub(first + i + 1)
+            while worker.stage.processed < base + (i + 1) * args.msgs_per_step:
                 await asyncio.sleep(0.0005)
 
-    await run_steps(0, args.warmup)
-    tracer.reset()
+    await run(0, args.warmup)
     c0 = dict(worker.counts)
-    sync()
     t0 = time.perf_counter()
-    await run_steps(args.warmup, args.steps)
-    sync()
+    await run(args.warmup, args.steps)
     dt = time.perf_counter() - t0
-    counts = {k: worker.counts[k] - c0[k] for k in c0}
-    eng = getattr(backend, "engine", None)
-    estats = eng.stats.as_dict() if eng is not None else {}
     await worker.stop()
-
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    return dt, counts, init_s, estats
+    return dt, {k: worker.counts[k] - c0[k] for k in c0}, 0.0, {}
 
 
 def main(argv=None) -> int:
     args = _args(argv)
-    rank, world, local, dist = _dist_setup(args.gpus)
+    rank, world, local = _rank_env()
     if args.backend == "local_llm":
-        import torch
-
-        if not torch.cuda.is_available():
-            print("local_llm backend needs a GPU; use --backend fake on CPU", file=sys.stderr)
-            return 2
-    dt, counts, init_s, estats = asyncio.run(_run(args, rank, world, local, dist))
+        dt, counts, init_s, estats = run_replica(args, rank, world, local)
+    else:
+        dt, counts, init_s, estats = asyncio.run(_run_cpu(args))
+        world = 1
     total = args.msgs_per_step * args.steps * world
     value = total / dt
     if rank == 0:
+        gpu = args.backend == "local_llm"
         out = {
             "metric": "sms_msgs_per_sec",
             "value": round(value, 1),
@@ -166,16 +171,16 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_MSGS_PER_S, 3),
             "dtype": "bf16",
-            "data": "synthetic (unique bank-SMS bodies, random-init extractor weights)",
+            "data": "synthetic (unique bank-SMS bodies; random-init extractor weights)",
             "config": {
-                "model": f"{args.model} extractor (local LLM replacing the Gemini call)" if args.backend == "local_llm"
-                else f"{args.backend} backend (CPU, stubbed LLM)",
+                "model": (f"{args.model} extractor LLM (134.5M params, replaces the Gemini call)" if gpu
+                          else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
                 "pipeline": "payload->RawSMS->bus sms.raw->parser_worker->sms.parsed/processing|DLQ->ack",
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
-                "seq_len": "prefix 75 + ~40 prompt + <=59 constrained output tokens",
-                "parallelism": f"dp{world}",
-                "backend": args.backend,
+                "seq_len": "prefix 75 + ~40 prompt + <=59 schema-constrained output tokens",
+                "parallelism": f"dp{world}" if gpu else "cpu",
+                "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
                 "max_slots": args.max_slots,
                 "baseline_msgs_per_s": BASELINE_MSGS_PER_S,
             },
@@ -185,8 +190,6 @@ def main(argv=None) -> int:
         if args.verbose and estats:
             out["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in estats.items()}
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
     return 0
 
 

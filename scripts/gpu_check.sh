@@ -9,5 +9,5 @@ timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpur
 rc=$?; tail -30 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1
 rc=$?; tail -5 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 900 python bench.py --steps 3 --warmup 1 --msgs-per-step 2048 --verbose > gpurun_out/bench.log 2>&1
+timeout -k 10 900 python bench.py --steps 3 --warmup 1 --verbose > gpurun_out/bench.log 2>&1
 rc=$?; tail -5 gpurun_out/bench.log; exit $rc

@@ -1,0 +1,176 @@
+"""One data-parallel replica per MI355X: a GPU engine process + K CPU parser processes.
+
+The reference scales by running more ``parser_worker`` containers in one
+durable consumer group (worker.py:199-202). Here one replica per GPU is the
+unit of scale-out; inside a replica the work is split by resource:
+
+* the **rank process** (one per GPU under torchrun) owns the GPU — the
+  extraction engine with its hipGraph-captured decode — and serves token-id
+  batches to its workers (:class:`~smsgate_amd.serving.remote.EngineServer`);
+  across ranks it joins a ``torch.distributed`` group over RCCL for barriers
+  and metric reductions (no per-message collectives: replicas are independent
+  competing consumers, the right call for a model that fits one GPU —
+  SURVEY.md §5.8);
+* **K parser processes** run the CPU side of the parser stage (bus I/O,
+  JSON, validation, tokenisation, post-processing, DLQ routing), each with its
+  own interpreter so no GIL is shared with the GPU feeder.
+
+Parser processes are spawned *before* the rank process touches the GPU.
+"""
+from __future__ import annotations
+
+import asyncio
+import multiprocessing as mp
+import os
+import time
+from multiprocessing.connection import Connection
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+__all__ = ["spawn_parser_workers", "parser_worker_main", "Coordinator"]
+
+
+def spawn_parser_workers(n: int, rank: int, cfg: Dict[str, Any]) -> Tuple[List[Any], List[Connection]]:
+    """Start ``n`` parser processes (spawn context, GPU hidden); returns (procs, conns)."""
+    ctx = mp.get_context("spawn")
+    procs, conns = [], []
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")}
+    try:
+        # parser processes never touch the GPU; hide it so an accidental CUDA call fails fast
+        os.environ["HIP_VISIBLE_DEVICES"] = ""
+        os.environ["CUDA_VISIBLE_DEVICES"] = ""
+        for w in range(n):
+            a, b = ctx.Pipe(duplex=True)
+            p = ctx.Process(target=parser_worker_main, args=(b, rank, w, cfg), name=f"parser-r{rank}-w{w}",
+                            daemon=True)
+            p.start()
+            b.close()
+            procs.append(p)
+            conns.append(a)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return procs, conns
+
+
+def _payload_bytes(n: int, seed: int) -> List[bytes]:
+    """Synthetic phone posts → RawSMS JSON, exactly as the gateway maps them."""
+    from ..services.gateway import RawSMSPayload, payload_to_raw
+    from ..utils.synth import generate
+
+    out = []
+    for s in generate(n, seed=seed):
+        p = RawSMSPayload(device_id="bench", message=s.body, sender="BANK", timestamp=s.timestamp, source="device")
+        out.append(p)
+    return out  # type: ignore[return-value]
+
+
+def parser_worker_main(conn: Connection, rank: int, widx: int, cfg: Dict[str, Any]) -> None:
+    """Entry point of a parser process (bench/serving harness)."""
+    asyncio.run(_worker_async(conn, rank, widx, cfg))
+
+
+async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, Any]) -> None:
+    from ..bus import SUBJECT_RAW, MemoryBus
+    from ..parse.backends.local_llm import RemoteLLMBackend
+    from ..parse.pipeline import ParsePipeline
+    from ..serving.remote import RemoteEngineClient
+    from ..services.gateway import payload_to_raw
+    from ..services.parser import ParserWorker
+
+    client = RemoteEngineClient(conn, max_body_tokens=cfg.get("max_body_tokens", 128))
+    bus = MemoryBus()
+    backend = RemoteLLMBackend(client, max_batch=cfg.get("batch", 512))
+    worker = ParserWorker(bus, ParsePipeline(backend), batch=cfg.get("batch", 512),
+                          concurrency=cfg.get("concurrency", 4), stats_interval=0)
+    await worker.start()
+    client.send_control({"event": "ready", "w": widx})
+    prepared: List[List[Any]] = []
+    while True:
+        cmd = await asyncio.to_thread(client.control.get)
+        if cmd is None or cmd.get("cmd") == "quit":
+            break
+        if cmd["cmd"] == "prepare":
+            n = int(cmd["n"])
+            prepared = [_payload_bytes(n, seed) for seed in cmd["seeds"]]
+            client.send_control({"event": "prepared", "w": widx})
+        elif cmd["cmd"] == "go":
+            c0 = dict(worker.counts)
+            t0 = time.perf_counter()
+            base = worker.stage.processed
+
+            async def publish(i: int) -> None:
+                items = [(SUBJECT_RAW, payload_to_raw(p).model_dump_json().encode("utf-8")) for p in prepared[i]]
+                await bus.publish_many(items)
+
+            nsteps = len(prepared)
+            if nsteps:
+                await publish(0)
+            done_msgs = 0
+            for i in range(nsteps):
+                if i + 1 < nsteps:
+                    await publish(i + 1)  # ingestion runs one step ahead of parsing
+                done_msgs += len(prepared[i])
+                while worker.stage.processed < base + done_msgs:
+                    await asyncio.sleep(0.0005)
+            counts = {k: worker.counts[k] - c0[k] for k in c0}
+            client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
+    await worker.stop()
+
+
+class Coordinator:
+    """Rank-side driver: serves the engine while steering the parser processes."""
+
+    def __init__(self, engine, conns: Sequence[Connection]) -> None:
+        from ..serving.remote import EngineServer
+
+        self.events: Dict[str, Dict[int, Any]] = {}
+        self.server = EngineServer(engine, conns, on_control=self._on_control)
+        self.n = len(conns)
+
+    def _on_control(self, idx: int, obj: Any) -> None:
+        self.events.setdefault(obj.get("event", "?"), {})[idx] = obj
+
+    def wait_all(self, event: str, timeout: float = 1800.0) -> Dict[int, Any]:
+        t_end = time.time() + timeout
+        self.server.serve_until(lambda: len(self.events.get(event, {})) >= self.n or time.time() > t_end)
+        got = self.events.pop(event, {})
+        if len(got) < self.n:
+            raise TimeoutError(f"only {len(got)}/{self.n} parser workers reported {event!r}")
+        return got
+
+    def broadcast(self, obj: Any) -> None:
+        for i in range(self.n):
+            self.server.send_control(i, obj)
+
+    def run_phase(self, seeds_per_worker: Sequence[Sequence[int]], n_per_step: int,
+                  sync=None) -> Tuple[float, Dict[str, int]]:
+        """Prepare (untimed), then time ``go`` → all ``done``. Returns (seconds, routing counts)."""
+        for i in range(self.n):
+            self.server.send_control(i, {"cmd": "prepare", "n": n_per_step, "seeds": list(seeds_per_worker[i])})
+        self.wait_all("prepared")
+        if sync is not None:
+            sync()
+        t0 = time.perf_counter()
+        self.broadcast({"cmd": "go"})
+        done = self.wait_all("done")
+        if sync is not None:
+            sync()
+        dt = time.perf_counter() - t0
+        counts: Dict[str, int] = {}
+        for d in done.values():
+            for k, v in d["counts"].items():
+                counts[k] = counts.get(k, 0) + v
+        return dt, counts
+
+    def shutdown(self, procs: Sequence[Any]) -> None:
+        try:
+            self.broadcast({"cmd": "quit"})
+        except Exception:
+            pass
+        for p in procs:
+            p.join(timeout=20)
+            if p.is_alive():
+                p.terminate()

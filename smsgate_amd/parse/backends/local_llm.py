@@ -19,7 +19,7 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from .base import BackendError, ExtractResult, ParserBackend
 
-__all__ = ["LocalLLMBackend", "build_engine"]
+__all__ = ["LocalLLMBackend", "RemoteLLMBackend", "build_engine"]
 
 
 def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
@@ -89,3 +89,21 @@ class LocalLLMBackend(ParserBackend):
             else:
                 out.append(dict(r))
         return out
+
+
+class RemoteLLMBackend(ParserBackend):
+    """The same extractor, served by an engine process on the GPU
+    (:class:`~smsgate_amd.serving.remote.EngineServer`); this process only
+    tokenises, ships ids and detokenises — the multi-process replica layout."""
+
+    name = "local_llm"
+
+    def __init__(self, client, max_batch: int = 512) -> None:
+        self.client = client
+        self.max_batch = max_batch
+
+    async def extract_batch(self, bodies: Sequence[str]) -> List[ExtractResult]:
+        try:
+            return list(await self.client.extract(bodies))
+        except Exception as exc:  # noqa: BLE001 — every message of the batch fails loudly
+            return [exc] * len(bodies)

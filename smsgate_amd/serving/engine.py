@@ -384,16 +384,23 @@ class ExtractionEngine:
         ev.record()
         return _Snapshot(B, ev, hb, dict(self.active))
 
-    def _harvest(self, snap: "_Snapshot") -> List[Tuple[Any, Dict[str, Optional[str]]]]:
+    def _harvest(self, snap: "_Snapshot", raw: bool = False) -> List[Tuple[Any, Any]]:
         t0 = time.perf_counter()
         snap.event.synchronize()
         done_h = snap.bufs["done"][: snap.B].numpy()
-        res: List[Tuple[Any, Dict[str, Optional[str]]]] = []
+        res: List[Tuple[Any, Any]] = []
         lens = snap.bufs["len"]
         bufs = snap.bufs["buf"]
         fin = [r for r, key in snap.active.items()
                if r < snap.B and done_h[r] and self.active.get(r) is key]
-        if fin:
+        if fin and raw:
+            # token ids only (a remote client detokenises): numpy row slices
+            lens_n = lens.numpy()
+            bufs_n = bufs.numpy()
+            for r in fin:
+                res.append((self.active.pop(r), bufs_n[r, : lens_n[r]].copy()))
+                heapq.heappush(self.free_rows, r)
+        elif fin:
             # one batched detokenisation (Rust, parallel) for every field of every finished row
             nf = len(self.fsm.fields)
             lens_l = lens[fin].tolist()
@@ -412,17 +419,27 @@ class ExtractionEngine:
         self.stats.harvest_s += time.perf_counter() - t0
         return res
 
-    def step(self) -> List[Tuple[Any, Dict[str, Optional[str]]]]:
+    def step(self, raw: bool = False) -> List[Tuple[Any, Any]]:
         """Admit → launch one decode chunk → harvest the *previous* chunk's snapshot
         (the GPU runs chunk k while the host decodes chunk k-1's finished rows).
-        Returns finished ``(key, answer)``."""
+        Returns finished ``(key, answer dict)`` — or ``(key, int32 token array)``
+        with ``raw=True`` (the remote-client path)."""
         self._admit()
         prev, self._pending = self._pending, None
         if self.active:
             B = self._bucket(max(self.active) + 1)
             self._run_decode(B)
             self._pending = self._snapshot(B)
-        return self._harvest(prev) if prev is not None else []
+        return self._harvest(prev, raw) if prev is not None else []
+
+    def submit_ids(self, items: Sequence[Tuple[Any, Sequence[int]]]) -> None:
+        """Queue pre-tokenised prompts (``<sms> body <ans>`` ids, see the tokenizer)."""
+        cap = self.cfg.max_body_tokens + 2
+        for k, ids in items:
+            ids = list(ids)
+            if len(ids) > cap:
+                ids = ids[: cap - 1] + [ids[-1]]
+            self.waiting.append(_Pending(k, ids))
 
     def run(self, bodies: Sequence[str]) -> List[Dict[str, Optional[str]]]:
         """Synchronous batch extraction (tests, benchmarks)."""

@@ -1,0 +1,69 @@
+"""Binary wire format between parser processes and a GPU engine server.
+
+Requests and responses are token-id batches, packed with numpy (no pickle):
+
+``request``  = ``b"Q"`` | req_id:u64 | n:u32 | lens:u16[n] | ids:i32[sum(lens)]
+``response`` = ``b"R"`` | req_id:u64 | n:u32 | lens:u16[n] | ids:i32[sum(lens)]
+``error``    = ``b"E"`` | req_id:u64 | utf-8 message
+``control``  = ``b"C"`` | utf-8 JSON (used by the benchmark harness)
+
+Tokenisation and detokenisation happen on the client side, so the GPU
+process does only scheduling: its Python work per message is a few slices.
+"""
+from __future__ import annotations
+
+import json
+import struct
+from typing import Any, List, Sequence, Tuple
+
+import numpy as np
+
+__all__ = ["pack_ids", "unpack_ids", "pack_error", "pack_control", "kind"]
+
+_HDR = struct.Struct("<cQI")
+
+
+def pack_ids(tag: bytes, req_id: int, seqs: Sequence[Sequence[int]]) -> bytes:
+    n = len(seqs)
+    lens = np.fromiter((len(s) for s in seqs), dtype=np.uint16, count=n)
+    flat = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(lens.sum()))
+    return _HDR.pack(tag, req_id, n) + lens.tobytes() + flat.tobytes()
+
+
+def pack_arrays(tag: bytes, req_id: int, lens: np.ndarray, flat: np.ndarray) -> bytes:
+    return _HDR.pack(tag, req_id, len(lens)) + lens.astype(np.uint16).tobytes() + flat.astype(np.int32).tobytes()
+
+
+def unpack_ids(buf: bytes) -> Tuple[bytes, int, List[List[int]]]:
+    tag, req_id, n = _HDR.unpack_from(buf, 0)
+    off = _HDR.size
+    lens = np.frombuffer(buf, dtype=np.uint16, count=n, offset=off)
+    off += 2 * n
+    flat = np.frombuffer(buf, dtype=np.int32, count=int(lens.sum()), offset=off).tolist()
+    out: List[List[int]] = []
+    p = 0
+    for ln in lens.tolist():
+        out.append(flat[p:p + ln])
+        p += ln
+    return tag, req_id, out
+
+
+def pack_error(req_id: int, msg: str) -> bytes:
+    return _HDR.pack(b"E", req_id, 0) + msg.encode()
+
+
+def unpack_error(buf: bytes) -> Tuple[int, str]:
+    _, req_id, _ = _HDR.unpack_from(buf, 0)
+    return req_id, buf[_HDR.size:].decode(errors="replace")
+
+
+def pack_control(obj: Any) -> bytes:
+    return b"C" + json.dumps(obj).encode()
+
+
+def unpack_control(buf: bytes) -> Any:
+    return json.loads(buf[1:].decode())
+
+
+def kind(buf: bytes) -> bytes:
+    return buf[:1]

@@ -1,0 +1,215 @@
+"""Engine server (GPU process) and client (parser processes).
+
+Topology per MI355X (see ``bench.py`` and ``python -m smsgate_amd engine-server``):
+
+    parser worker 1 ─┐                       ┌──────────────────────────────┐
+    parser worker 2 ─┼── pipes / unix socket ─► EngineServer (GPU process)  │
+    parser worker K ─┘   token ids ⇄ ids     │  continuous batching engine  │
+                                             └──────────────────────────────┘
+
+The GPU process does nothing but schedule the engine: its Python work per
+message is a few array slices, so the decode graphs are replayed back to back
+while the CPU-heavy work — tokenisation, detokenisation, post-processing,
+validation, bus I/O — runs in K parser processes with their own interpreters
+(no shared GIL). Parser workers must be started before the GPU process
+initialises the GPU (no exec after GPU init on this platform).
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from multiprocessing.connection import Connection, wait
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import protocol as P
+
+__all__ = ["EngineServer", "RemoteEngineClient"]
+
+
+@dataclass
+class _Req:
+    conn_idx: int
+    req_id: int
+    out: List[Any]
+    left: int
+
+
+class EngineServer:
+    def __init__(self, engine, conns: Sequence[Connection] = (),
+                 on_control: Optional[Callable[[int, Any], None]] = None) -> None:
+        self.engine = engine
+        self.conns: List[Optional[Connection]] = list(conns)
+        self.on_control = on_control
+        self.reqs: Dict[tuple, _Req] = {}
+        self.served = 0
+
+    def add_connection(self, conn: Connection) -> int:
+        self.conns.append(conn)
+        return len(self.conns) - 1
+
+    def send_control(self, idx: int, obj: Any) -> None:
+        c = self.conns[idx]
+        if c is not None:
+            c.send_bytes(P.pack_control(obj))
+
+    def _live(self) -> List[Connection]:
+        return [c for c in self.conns if c is not None]
+
+    def poll(self, timeout: Optional[float]) -> None:
+        live = self._live()
+        if not live:
+            if timeout:
+                time.sleep(min(timeout, 0.01))
+            return
+        for c in wait(live, timeout):
+            idx = self.conns.index(c)
+            while True:
+                try:
+                    buf = c.recv_bytes()
+                except (EOFError, OSError):
+                    self.conns[idx] = None
+                    break
+                k = P.kind(buf)
+                if k == b"Q":
+                    _, rid, seqs = P.unpack_ids(buf)
+                    if not seqs:
+                        c.send_bytes(P.pack_ids(b"R", rid, []))
+                    else:
+                        self.reqs[(idx, rid)] = _Req(idx, rid, [None] * len(seqs), len(seqs))
+                        self.engine.submit_ids([((idx, rid, i), s) for i, s in enumerate(seqs)])
+                elif k == b"C" and self.on_control is not None:
+                    self.on_control(idx, P.unpack_control(buf))
+                if not c.poll():
+                    break
+
+    def step(self) -> None:
+        try:
+            finished = self.engine.step(raw=True)
+        except Exception as exc:  # fail every waiting request loudly
+            for (idx, rid), _ in list(self.reqs.items()):
+                c = self.conns[idx]
+                if c is not None:
+                    c.send_bytes(P.pack_error(rid, repr(exc)))
+            self.reqs.clear()
+            self.engine.waiting.clear()
+            self.engine.active.clear()
+            self.engine._pending = None
+            raise
+        for (idx, rid, i), toks in finished:
+            r = self.reqs.get((idx, rid))
+            if r is None:
+                continue
+            r.out[i] = toks
+            r.left -= 1
+            if r.left == 0:
+                del self.reqs[(idx, rid)]
+                c = self.conns[idx]
+                if c is not None:
+                    lens = np.fromiter((len(t) for t in r.out), dtype=np.uint16, count=len(r.out))
+                    flat = np.concatenate(r.out) if r.out else np.zeros(0, np.int32)
+                    c.send_bytes(P.pack_arrays(b"R", rid, lens, flat))
+                self.served += len(r.out)
+
+    def serve_until(self, pred: Callable[[], bool]) -> None:
+        while not pred():
+            self.poll(0 if self.engine.busy() else 0.002)
+            if self.engine.busy():
+                self.step()
+
+    def serve_forever(self) -> None:
+        self.serve_until(lambda: not self._live() and not self.engine.busy())
+
+
+class RemoteEngineClient:
+    """Async client: tokenises, ships ids, awaits ids, detokenises into answers."""
+
+    def __init__(self, conn: Connection, tokenizer=None, max_body_tokens: int = 128) -> None:
+        from ..models.tokenizer import load_tokenizer
+        from .fsm import DEFAULT_FIELDS
+
+        self.conn = conn
+        self.tok = tokenizer or load_tokenizer()
+        self.fields = [f.name for f in DEFAULT_FIELDS]
+        self.max_body = max_body_tokens
+        self._ids = itertools.count(1)
+        self._pending: Dict[int, Any] = {}
+        self._send_lock = threading.Lock()
+        self.control: "queue.Queue[Any]" = queue.Queue()
+        self._reader = threading.Thread(target=self._read_loop, name="engine-client", daemon=True)
+        self._reader.start()
+
+    def _read_loop(self) -> None:
+        while True:
+            try:
+                buf = self.conn.recv_bytes()
+            except (EOFError, OSError):
+                for fut, loop in list(self._pending.values()):
+                    loop.call_soon_threadsafe(self._set_exc, fut, ConnectionError("engine server closed"))
+                self._pending.clear()
+                self.control.put(None)
+                return
+            k = P.kind(buf)
+            if k == b"R":
+                _, rid, seqs = P.unpack_ids(buf)
+                ent = self._pending.pop(rid, None)
+                if ent is not None:
+                    fut, loop = ent
+                    loop.call_soon_threadsafe(self._set_res, fut, seqs)
+            elif k == b"E":
+                rid, msg = P.unpack_error(buf)
+                ent = self._pending.pop(rid, None)
+                if ent is not None:
+                    fut, loop = ent
+                    loop.call_soon_threadsafe(self._set_exc, fut, RuntimeError(msg))
+            elif k == b"C":
+                self.control.put(P.unpack_control(buf))
+
+    @staticmethod
+    def _set_res(fut, v):
+        if not fut.done():
+            fut.set_result(v)
+
+    @staticmethod
+    def _set_exc(fut, e):
+        if not fut.done():
+            fut.set_exception(e)
+
+    def send_control(self, obj: Any) -> None:
+        with self._send_lock:
+            self.conn.send_bytes(P.pack_control(obj))
+
+    def decode_answers(self, seqs: List[List[int]]) -> List[Dict[str, str]]:
+        sep = self.tok.sep
+        nf = len(self.fields)
+        pieces: List[List[int]] = []
+        for toks in seqs:
+            vals: List[List[int]] = [[]]
+            for t in toks:
+                if t == sep:
+                    if len(vals) == nf:
+                        break
+                    vals.append([])
+                else:
+                    vals[-1].append(t)
+            vals += [[]] * (nf - len(vals))
+            pieces.extend(vals)
+        texts = self.tok.decode_batch(pieces) if pieces else []
+        return [{f: texts[j * nf + i].strip() for i, f in enumerate(self.fields)} for j in range(len(seqs))]
+
+    async def extract(self, bodies: Sequence[str]) -> List[Dict[str, str]]:
+        ids = self.tok.message_ids(list(bodies), self.max_body)
+        rid = next(self._ids)
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._pending[rid] = (fut, loop)
+        msg = P.pack_ids(b"Q", rid, ids)
+        with self._send_lock:
+            self.conn.send_bytes(msg)
+        seqs = await fut
+        return self.decode_answers(seqs)

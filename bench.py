@@ -44,7 +44,7 @@ def _args(argv=None):
     p.add_argument("--model", default="smollm-135m")
     p.add_argument("--msgs-per-step", type=int, default=8192)
     p.add_argument("--max-slots", type=int, default=4096)
-    p.add_argument("--steps-per-graph", type=int, default=8)
+    p.add_argument("--steps-per-graph", type=int, default=16)
     p.add_argument("--cpu-workers", type=int, default=8)
     p.add_argument("--concurrency", type=int, default=4)
     p.add_argument("--batch", type=int, default=512)

@@ -54,7 +54,7 @@ class EngineConfig:
     max_body_tokens: int = 128
     temperature: float = 0.0
     seed: int = 0
-    steps_per_graph: int = 8
+    steps_per_graph: int = 16
     use_graphs: bool = True
     prefill_max_tokens: int = 32768
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
@@ -105,7 +105,14 @@ class ExtractionEngine:
         mc, ec = self.mc, self.cfg
         if mc.head_dim != 64:
             raise ValueError("kernels are specialised for head_dim 64")
-        self.fsm: SchemaFSM = build_fsm(tokenizer, mc.vocab, fields).to_device(self.device)
+        # Constrained decoding can only ever emit tokenizer ids, so the lm_head is
+        # evaluated on the first V_dec = roundup(tokenizer vocab, 32) rows of the
+        # (tied) embedding: ids beyond it are masked in every FSM state, hence the
+        # arg-max / Gumbel-max over allowed tokens is unchanged (exact, not an
+        # approximation) and the projection is 6x smaller for the 49 152 vocab.
+        self.V_dec = min(mc.vocab, _round_up(tokenizer.vocab_size, 32))
+        self.lm_head = self.w.embed[: self.V_dec]
+        self.fsm: SchemaFSM = build_fsm(tokenizer, self.V_dec, fields).to_device(self.device)
         self.max_out = self.fsm.max_steps()
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)
         self.P0 = len(self.prefix_ids)
@@ -232,7 +239,7 @@ class ExtractionEngine:
 
         h = self._layers(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
         last = h.index_select(0, (cu_d[1:] - 1).long())
-        logits = F.linear(last, self.w.embed)
+        logits = F.linear(last, self.lm_head)
         if not sample:
             return logits
         # reset the admitted rows, then sample their first answer token
@@ -266,7 +273,7 @@ class ExtractionEngine:
                             done=self.done)
 
         h = self._layers(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
-        logits = F.linear(h, self.w.embed)
+        logits = F.linear(h, self.lm_head)
         if sample:
             ops.fsm_sample(logits, self.fsm, self.state[:B], tok, self.out_buf[:B], self.out_len[:B],
                            self.done[:B], pos, slot, self.cfg.temperature, self.cfg.seed)

@@ -44,7 +44,9 @@ def _args(argv=None):
     p.add_argument("--model", default="smollm-135m")
     p.add_argument("--msgs-per-step", type=int, default=8192)
     p.add_argument("--max-slots", type=int, default=4096)
-    p.add_argument("--steps-per-graph", type=int, default=16)
+    p.add_argument("--steps-per-graph", type=int, default=4)
+    p.add_argument("--admit-frac", type=float, default=0.25)
+    p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)
     p.add_argument("--concurrency", type=int, default=4)
     p.add_argument("--batch", type=int, default=512)
@@ -81,8 +83,11 @@ def run_replica(args, rank: int, world: int, local: int):
     from smsgate_amd.parse.backends.local_llm import build_engine
 
     t_init = time.perf_counter()
+    buckets = (tuple(range(args.bucket_step, args.max_slots + 1, args.bucket_step)) if args.bucket_step
+               else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
     engine = build_engine(args.model, device=f"cuda:{local}", max_slots=args.max_slots,
-                          steps_per_graph=args.steps_per_graph)
+                          steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
+                          buckets=buckets)
     init_s = time.perf_counter() - t_init
     coord = Coordinator(engine, conns)
     coord.wait_all("ready")

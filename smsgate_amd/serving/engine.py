@@ -54,7 +54,7 @@ class EngineConfig:
     max_body_tokens: int = 128
     temperature: float = 0.0
     seed: int = 0
-    steps_per_graph: int = 16
+    steps_per_graph: int = 4
     use_graphs: bool = True
     prefill_max_tokens: int = 32768
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)

@@ -110,6 +110,10 @@ class SqliteKV(ResponseCache):
         with self._lock:
             return int(self._db.execute("SELECT COUNT(*) FROM kv").fetchone()[0])
 
+    def items(self) -> List[Tuple[str, Any]]:
+        with self._lock:
+            return [(k, json.loads(v)) for k, v in self._db.execute("SELECT k, v FROM kv ORDER BY k")]
+
     def close(self) -> None:
         with self._lock:
             self._db.close()

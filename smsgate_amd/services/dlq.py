@@ -1,0 +1,103 @@
+"""DLQ inspector / re-parser (services/parser_worker/dlq_worker.py parity).
+
+Consumes ``sms.failed`` as durable ``parser_worker_dlq`` (dlq_worker.py:84-90),
+logs every envelope pretty-printed and, with ``--reparse``, runs the message
+through the parse pipeline again and routes the result exactly like the parser
+worker (parsed → ``sms.parsed`` + ``sms.processing``; failures back to the DLQ).
+
+Fixes: every message is acked (the reference never acked
+non-``raw`` payloads in reparse mode), and every envelope shape that carries
+a RawSMS can be re-parsed — ``{"raw": RawSMS}`` (c), ``{"entry": RawSMS}``
+(b) and ``{"entry": "<RawSMS JSON>"}`` (a, d, e) — not only shape (c).
+Writer failures (f: ``entry`` is a ParsedSMS) are logged, not re-parsed.
+"""
+from __future__ import annotations
+
+import json
+import logging
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..bus.base import SUBJECT_FAILED, Bus, Msg
+from ..models.domain import RawSMS
+from ..parse.pipeline import ParsePipeline
+from ..runtime.stage import Stage
+
+__all__ = ["DlqWorker", "extract_raw"]
+
+log = logging.getLogger("dlq_worker")
+
+
+def extract_raw(envelope: Any) -> Optional[Dict[str, Any]]:
+    """The RawSMS dict inside a DLQ envelope, or None."""
+    if not isinstance(envelope, dict):
+        return None
+    cand = envelope.get("raw", envelope.get("entry"))
+    if isinstance(cand, str):
+        try:
+            cand = json.loads(cand)
+        except ValueError:
+            return None
+    if isinstance(cand, dict) and "raw" in cand and isinstance(cand["raw"], dict):
+        cand = cand["raw"]
+    if not isinstance(cand, dict):
+        return None
+    try:
+        RawSMS(**cand)
+    except Exception:  # noqa: BLE001 — e.g. a writer-failure ParsedSMS entry
+        return None
+    return cand
+
+
+class DlqWorker:
+    def __init__(self, bus: Bus, pipeline: Optional[ParsePipeline] = None, *, group: str = "parser_worker_dlq",
+                 reparse: bool = False, batch: int = 64) -> None:
+        self.bus = bus
+        self.pipeline = pipeline
+        self.reparse = reparse
+        self.seen = 0
+        self.reparsed = 0
+        self.not_reparsable = 0
+        self.log: List[Dict[str, Any]] = []
+        self.stage = Stage(bus, SUBJECT_FAILED, group, self.handle_batch, batch=batch, stats_interval=0,
+                           name="dlq_worker")
+
+    async def handle_batch(self, msgs: Sequence[Msg]) -> None:
+        from ..services.parser import route_batch
+
+        to_reparse: List[Msg] = []
+        for m in msgs:
+            self.seen += 1
+            try:
+                env = json.loads(m.data)
+            except ValueError:
+                log.error("DLQ payload is not JSON: %r", m.data[:120])
+                continue
+            log.info("DLQ seq=%s payload=%s", m.seq, json.dumps(env, ensure_ascii=False, indent=2))
+            self.log.append(env)
+            if self.reparse:
+                raw = extract_raw(env)
+                if raw is None:
+                    self.not_reparsable += 1
+                else:
+                    to_reparse.append(_Shim(json.dumps({"raw": raw}).encode()))
+        if to_reparse and self.pipeline is not None:
+            publishes, counts = await route_batch(self.pipeline, to_reparse)
+            if publishes:
+                await self.bus.publish_many(publishes)
+            self.reparsed += len(to_reparse)
+        for m in msgs:
+            await m.ack()
+
+    async def start(self) -> None:
+        await self.bus.ensure_stream()
+        await self.stage.start()
+
+    async def stop(self) -> None:
+        await self.stage.stop()
+
+
+class _Shim:
+    """Minimal Msg stand-in for re-routing an extracted RawSMS."""
+
+    def __init__(self, data: bytes) -> None:
+        self.data = data

@@ -125,6 +125,33 @@ class EngineServer:
     def serve_forever(self) -> None:
         self.serve_until(lambda: not self._live() and not self.engine.busy())
 
+    def serve_listener(self, address: str, stop: Optional[threading.Event] = None) -> None:
+        """Accept parser processes on ``address`` (a unix socket path) and serve them
+        until ``stop`` is set — the standalone ``engine-server`` process."""
+        from multiprocessing.connection import Listener
+
+        incoming: "queue.Queue[Connection]" = queue.Queue()
+        listener = Listener(address, family="AF_UNIX")
+
+        def accept_loop() -> None:
+            while stop is None or not stop.is_set():
+                try:
+                    incoming.put(listener.accept())
+                except OSError:
+                    return
+
+        threading.Thread(target=accept_loop, name="engine-accept", daemon=True).start()
+
+        def pred() -> bool:
+            while not incoming.empty():
+                self.add_connection(incoming.get_nowait())
+            return stop is not None and stop.is_set()
+
+        try:
+            self.serve_until(pred)
+        finally:
+            listener.close()
+
 
 class RemoteEngineClient:
     """Async client: tokenises, ships ids, awaits ids, detokenises into answers."""

@@ -66,3 +66,18 @@ REFERENCE_CASES = [
              date=(2025, 6, 10, 20, 51), card="7538", currency="AMD"),
     ),
 ]
+
+
+async def drain(bus, subject):
+    """Read (and ack) everything currently on ``subject`` as JSON."""
+    import json
+
+    sub = await bus.subscribe(subject, "inspect-" + subject.replace(".", "-"))
+    out = []
+    while True:
+        got = await sub.fetch(100, 0.05)
+        if not got:
+            return out
+        for m in got:
+            await m.ack()
+            out.append(json.loads(m.data))

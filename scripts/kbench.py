@@ -93,6 +93,31 @@ def main():
         t = timeit(lambda: F.linear(X, W))
         res[f"gemm_{name}"] = t
         res[f"gemm_{name}_TFLOPs"] = round(2 * B * n * k / (t * 1e-6) / 1e12, 1)
+    # fused MFMA GEMMs (csrc/gemm_kernels.hip) at the same shapes, every tile config
+    fused = {"qkv": (cfg.qkv_out, H, "store", True), "o": (H, nh * D, "resid", False),
+             "gate_up": (2 * I, H, "swiglu", True), "down": (H, I, "resid", False),
+             "lm_head": (8192, H, "store", True)}
+    for name, (n, k, epi, norm) in fused.items():
+        W = rnd(n, k)
+        X = rnd(B, k)
+        R = rnd(B, n) if epi == "resid" else None
+        kw = dict(epi=epi, norm_eps=1e-5 if norm else None, resid=R)
+        best = None
+        for c, (bm, bn) in ops.GEMM_TILES.items():
+            if n % bn:
+                continue
+            t = timeit(lambda: ops.gemm(X, W, cfg=c, **kw))
+            res[f"fgemm_{name}_cfg{c}"] = t
+            best = t if best is None else min(best, t)
+        res[f"fgemm_{name}_auto"] = timeit(lambda: ops.gemm(X, W, **kw))
+        res[f"fgemm_{name}_auto_cfg"] = ops.gemm_cfg(B, n)
+        res[f"fgemm_{name}_TFLOPs"] = round(2 * B * n * k / (best * 1e-6) / 1e12, 1)
+    Xl, Wl = rnd(B, H), rnd(8192, H)
+    res["gemm_lm_head_8192"] = timeit(lambda: F.linear(Xl, Wl))
+    fused_layer = (res["rope_qkv_cache"] + res["attn_decode"] + res["fgemm_qkv_auto"] + res["fgemm_o_auto"]
+                   + res["fgemm_gate_up_auto"] + res["fgemm_down_auto"])
+    res["fused_sum_per_layer_us"] = round(fused_layer, 1)
+    res["fused_est_step_us"] = round(fused_layer * cfg.layers + res["fgemm_lm_head_auto"], 1)
     per_layer = (2 * res["rmsnorm_residual"] + res["rope_qkv_cache"] + res["attn_decode"] + res["silu_mul"]
                  + res["gemm_qkv"] + res["gemm_o"] + res["gemm_gate_up"] + res["gemm_down"])
     res["sum_per_layer_us"] = round(per_layer, 1)

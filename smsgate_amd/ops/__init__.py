@@ -31,6 +31,10 @@ __all__ = [
     "attn_prefill",
     "attn_decode",
     "fsm_sample",
+    "gemm",
+    "gemm_cfg",
+    "interleave_gate_up",
+    "fold_norm",
     "rope_table",
     "vt_shape",
     "vt_to_rows",
@@ -39,6 +43,7 @@ __all__ = [
     "ref_silu_mul",
     "ref_rope",
     "ref_attention",
+    "ref_gemm",
 ]
 
 _lib: Optional[ctypes.CDLL] = None
@@ -61,7 +66,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
                                   ctypes.c_uint, _vp]
-    for f in ("sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
+    lib.sg_gemm.argtypes = [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                            _c_float, _c_int, _vp]
+    for f in ("sg_gemm", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
 
@@ -138,6 +145,79 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     assert out.shape == (T, I)
     _check(load_library().sg_silu_mul(_p(gu), _p(out), T, I, _stream()), "silu_mul")
     return out
+
+
+GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+_EPI = {"store": 0, "resid": 1, "swiglu": 2}
+
+
+def gemm_cfg(M: int, N: int, min_tiles: int = 480) -> int:
+    """Tile config for an M×N output: the biggest tile that still gives ≳2 blocks per CU
+    (256 CUs), else the config with the most blocks."""
+    best, best_tiles = -1, -1
+    for cfg, (bm, bn) in GEMM_TILES.items():
+        if N % bn:
+            continue
+        tiles = -(-M // bm) * (N // bn)
+        if tiles >= min_tiles:
+            return cfg
+        if tiles > best_tiles:
+            best, best_tiles = cfg, tiles
+    if best < 0:
+        raise ValueError(f"gemm: N={N} is not a multiple of 64")
+    return best
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Optional[float] = None,
+         resid: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+         cfg: Optional[int] = None) -> torch.Tensor:
+    """Fused MFMA GEMM ``out = EPI(rowscale ⊙ (a @ w.T))`` (csrc/gemm_kernels.hip).
+
+    ``a`` [M, K] (row stride may exceed K), ``w`` [N, K] bf16.  ``norm_eps``: apply
+    RMSNorm to the rows of ``a`` (the norm weight must already be folded into
+    ``w`` — :func:`fold_norm`).  ``epi``: ``store``; ``resid`` (``out = resid +
+    result``; ``out`` defaults to ``resid`` itself, updated in place); ``swiglu``
+    (``w`` rows interleaved by :func:`interleave_gate_up`, output N/2 wide)."""
+    M, K = a.shape
+    N = w.shape[0]
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("gemm: bf16 operands required")
+    if a.stride(1) != 1 or not w.is_contiguous() or w.shape[1] != K or not a.is_cuda:
+        raise ValueError(f"gemm: bad operands a{tuple(a.shape)}/{a.stride()} w{tuple(w.shape)}")
+    if K % 64 or N % 64 or a.stride(0) % 8:
+        raise ValueError(f"gemm: K={K} and N={N} must be multiples of 64")
+    e = _EPI[epi]
+    n_out = N // 2 if e == 2 else N
+    if e == 1:
+        if resid is None or resid.shape != (M, n_out) or resid.dtype != torch.bfloat16 or resid.stride(1) != 1:
+            raise ValueError("gemm: epi='resid' needs a bf16 [M, N] residual")
+        if out is None:
+            out = resid
+    if out is None:
+        out = a.new_empty((M, n_out))
+    if out.shape != (M, n_out) or out.stride(1) != 1 or out.stride(0) % 8 or out.dtype != torch.bfloat16:
+        raise ValueError("gemm: bad output")
+    if M == 0:
+        return out
+    c = gemm_cfg(M, N) if cfg is None else cfg
+    rc = load_library().sg_gemm(_p(a), a.stride(0), _p(w), _p(out), out.stride(0), _p(resid),
+                                0 if resid is None else resid.stride(0), M, N, K, e, int(norm_eps is not None),
+                                float(norm_eps or 0.0), c, _stream())
+    _check(rc, "gemm")
+    return out
+
+
+def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+    """``W' = W · diag(norm_w)`` so that ``rmsnorm(x)·norm_w @ W.T == rowscale(x) ⊙ (x @ W'.T)``."""
+    return (w.float() * norm_w.float()[None, :]).to(w.dtype).contiguous()
+
+
+def interleave_gate_up(gate_up: torch.Tensor, group: int = 16) -> torch.Tensor:
+    """[2I, K] (gate rows then up rows) → rows interleaved in groups of 16 (g0..15, u0..15, g16..)."""
+    two_i, K = gate_up.shape
+    i = two_i // 2
+    g, u = gate_up[:i].reshape(i // group, group, K), gate_up[i:].reshape(i // group, group, K)
+    return torch.stack([g, u], dim=1).reshape(two_i, K).contiguous()
 
 
 def rope_table(max_pos: int, head_dim: int, theta: float, device) -> torch.Tensor:
@@ -265,6 +345,22 @@ def ref_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: torch
     s = (q.float() @ k.float().t()) * scale
     s = s.masked_fill(~mask, float("-inf"))
     return torch.softmax(s, dim=-1) @ v.float()
+
+
+def ref_gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Optional[float] = None,
+             norm_w: Optional[torch.Tensor] = None, resid: Optional[torch.Tensor] = None,
+             gate_up_plain: bool = True) -> torch.Tensor:
+    """fp32 reference of :func:`gemm` on UN-folded, UN-interleaved weights:
+    ``x = rmsnorm(a)·norm_w`` (if ``norm_eps``), ``y = x @ w.T``, then the epilogue."""
+    x = a.float()
+    if norm_eps is not None:
+        x = ref_rmsnorm(x, norm_w if norm_w is not None else torch.ones(x.shape[1], device=x.device), norm_eps)
+    y = x @ w.float().t()
+    if epi == "swiglu":
+        return ref_silu_mul(y)
+    if epi == "resid":
+        return resid.float() + y
+    return y
 
 
 def default_scale(head_dim: int) -> float:

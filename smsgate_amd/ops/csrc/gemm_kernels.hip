@@ -1,0 +1,282 @@
+// smsgate_amd — fused bf16 MFMA GEMMs for the extractor LM on gfx950.
+//
+//   C[M, Nout] = EPI( rowscale ⊙ (A[M, K] · W[N, K]ᵀ) )
+//
+// The decode step of a 576-wide model at M = 256…4096 rows is a chain of small-K
+// GEMMs (K = 576 / 1536) whose cost in hipBLASLt is dominated by fixed per-tile
+// overhead and by the elementwise kernels around them.  One templated kernel
+// absorbs those neighbours:
+//
+//   NORM   RMSNorm prologue.  The norm weight is folded into W on the host
+//          (W' = W·diag(w)), and rsqrt(mean(x²)+eps) of every A row is accumulated
+//          from the A tiles the kernel streams anyway and applied to the fp32
+//          accumulator in the epilogue — the normalised activation never exists
+//          in memory.
+//   EPI 0  store bf16.
+//   EPI 1  residual add: C = R + bf16(acc) (R may alias C: each element is read
+//          and written by the same thread) — the o-proj / down-proj epilogue that
+//          updates the residual stream in place.
+//   EPI 2  SwiGLU: W rows are interleaved in groups of 16 (16 gate rows, then the
+//          16 matching up rows), so one lane holds gate and up of the same output
+//          element in two accumulators; C = silu(g)·u with Nout = N / 2.
+//
+// Tiling (cdna_hip_programming.md §5): 256 threads = 4 waves, BM×BN block tile,
+// BK = 64, 16×16×32 bf16 MFMAs; A/W tiles staged global → registers → LDS,
+// double-buffered with one barrier per K-tile (the global loads of tile k+1 are
+// in flight while tile k is multiplied).  LDS rows are 128 B with a 16-byte-chunk
+// XOR swizzle (chunk ^ (row & 7)) so the 16 rows a fragment read touches spread
+// over all banks.  The epilogue stages the bf16 tile through LDS and writes
+// 16-byte row chunks (coalesced), which is also where the residual is read.
+// Block → tile mapping is XCD-aware: blocks are dealt round-robin to the 8 XCDs,
+// so each XCD is given a contiguous range of tiles (tiles sharing A rows share
+// that XCD's L2).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;  // K elements per tile = 8 chunks of 16 B
+
+__device__ __forceinline__ float bf2f(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+
+// ---- staging: async global → LDS DMA (global_load_lds_dwordx4).  One wave
+// instruction writes 1 KiB = 8 rows × 128 B lane-linearly (lane l → row l>>3,
+// physical chunk l&7), so the XOR swizzle is applied on the SOURCE address:
+// physical chunk p of row r holds logical chunk p ^ (r & 7).  No staging
+// registers — nothing for the compiler to sink or spill (cdna_hip_programming.md §5).
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int ROWS>
+__device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ src, int ld, int r0, int rmax, int k0,
+                                           uint16_t* dst, int wave, int lane) {
+  static_assert(ROWS % 32 == 0, "8-row pieces spread over 4 waves");
+  const int rr = lane >> 3, p = lane & 7;
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i) {
+    const int g = wave + 4 * i;  // 8-row piece
+    const int row = 8 * g + rr;
+    const int gr = min(r0 + row, rmax);  // rows past the end re-read the last row (never stored)
+    const uint16_t* gp = src + (size_t)gr * ld + k0 + ((p ^ (row & 7)) << 3);
+    __builtin_amdgcn_global_load_lds((const void*)gp, (lds_ptr_t)(dst + g * 8 * BK), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ float sumsq_frag(const bf16x8& v, float acc) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const uint4 u = __builtin_bit_cast(uint4, v);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, u.x), __builtin_bit_cast(bf16x2, u.x), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, u.y), __builtin_bit_cast(bf16x2, u.y), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, u.z), __builtin_bit_cast(bf16x2, u.z), acc, false);
+  acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, u.w), __builtin_bit_cast(bf16x2, u.w), acc, false);
+  return acc;
+}
+
+template <int FM, int FN, bool NORM>
+__device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], const uint16_t* as,
+                                         const uint16_t* bs, int wm0, int wn0, int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int ch = s * 4 + (lane >> 4);
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn0 + j * 16 + (lane & 15);
+      bfr[j] = *reinterpret_cast<const bf16x8*>(bs + row * BK + ((ch ^ (row & 7)) << 3));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm0 + i * 16 + (lane & 15);
+      af[i] = *reinterpret_cast<const bf16x8*>(as + row * BK + ((ch ^ (row & 7)) << 3));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      // RMSNorm: the A fragment already holds 8 k-values of row (lane & 15) —
+      // accumulate their squares (v_dot2_f32_bf16) in the MFMA shadow
+      if constexpr (NORM) ss[i] = sumsq_frag(af[i], ss[i]);
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, bool NORM>
+__global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restrict__ A, int lda,
+                                                         const uint16_t* __restrict__ W,
+                                                         uint16_t* C, int ldc, const uint16_t* R, int ldr,
+                                                         int M, int N, int K, float eps, int tiles_m,
+                                                         int tiles_n) {
+  static_assert(WM * WN == 4, "4 waves");
+  constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
+  constexpr int FM = TM / 16, FN = TN / 16;  // MFMA tiles per wave
+  static_assert(FM >= 1 && FN >= 1 && TM % 16 == 0 && TN % 16 == 0, "tile");
+  static_assert(EPI != 2 || FN % 2 == 0, "SwiGLU pairs gate/up 16-col groups inside a wave tile");
+  constexpr int BNO = EPI == 2 ? BN / 2 : BN;  // output columns of the block
+  constexpr int CST = BNO + 8;                // staged C row stride (elements), +16 B pad
+  constexpr int TILE = (BM + BN) * BK;        // one stage (A + B) in elements
+  constexpr int NI = (BM + BN) / 32;          // glds instructions per stage per wave
+  static_assert(BM * CST <= 2 * TILE, "C staging fits in the K-loop buffers");
+
+  // ONE __shared__ array (a second one makes hipcc wait vmcnt(0) before ds_reads)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * TILE + 2 * BM];
+  float* rs = reinterpret_cast<float*>(smem + 2 * TILE);
+
+  // ---- XCD-aware, bijective tile assignment: the blocks of one XCD (orig % 8)
+  // get a contiguous range of tiles, so tiles that share A rows share an L2
+  const int T = tiles_m * tiles_n;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = T >> 3, r8 = T & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int m0 = (t / tiles_n) * BM;
+  const int n0 = (t % tiles_n) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / WN) * TM, wn0 = (wave % WN) * TN;
+
+  f32x4 acc[FM][FN];
+  float ss[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    ss[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // ---- K loop: the DMA of tile kt+1 is in flight while tile kt is multiplied.
+  // Counted vmcnt + raw s_barrier (a __syncthreads() would drain the DMA queue).
+  const int KT = K / BK;
+  issue_tile<BM>(A, lda, m0, M - 1, 0, smem, wave, lane);
+  issue_tile<BN>(W, K, n0, N - 1, 0, smem + BM * BK, wave, lane);
+  for (int kt = 0; kt < KT; ++kt) {
+    uint16_t* cur = smem + (kt & 1) * TILE;
+    if (kt + 1 < KT) {
+      uint16_t* nxt = smem + ((kt + 1) & 1) * TILE;
+      issue_tile<BM>(A, lda, m0, M - 1, (kt + 1) * BK, nxt, wave, lane);
+      issue_tile<BN>(W, K, n0, N - 1, (kt + 1) * BK, nxt + BM * BK, wave, lane);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // tile kt landed (this wave's part)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every wave's part
+    mma_tile<FM, FN, NORM>(acc, ss, cur, cur + BM * BK, wm0, wn0, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled next iteration
+  }
+
+  // ---- row scales (RMSNorm): lanes l, l^16, l^32, l^48 hold the 4 k-quarters of row l&15
+  if constexpr (NORM) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      float v = ss[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 16 && (wave % WN) == 0) rs[wm0 + i * 16 + lane] = rsqrtf(v / (float)K + eps);
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue 1: fragments -> bf16 tile in LDS (the K-loop buffers are free now)
+  uint16_t* Cs = smem;
+  const int r_base = wm0 + (lane >> 4) * 4;
+  const int c_lane = lane & 15;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    float sc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sc[r] = NORM ? rs[r_base + i * 16 + r] : 1.f;
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        const int col = (wn0 >> 1) + (j >> 1) * 16 + c_lane;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = acc[i][j][r] * sc[r], u = acc[i][j + 1][r] * sc[r];
+          Cs[(r_base + i * 16 + r) * CST + col] = f2bf(silu(g) * u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn0 + j * 16 + c_lane;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cs[(r_base + i * 16 + r) * CST + col] = f2bf(acc[i][j][r] * sc[r]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue 2: coalesced 16-B row chunks (+ residual)
+  constexpr int CPR = BNO / 8;  // chunks per row
+  const int c0 = EPI == 2 ? n0 / 2 : n0;
+  for (int q = tid; q < BM * CPR; q += 256) {
+    const int row = q / CPR, c = q % CPR;
+    const int gr = m0 + row;
+    if (gr >= M) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
+    uint16_t* dst = C + (size_t)gr * ldc + c0 + c * 8;
+    if constexpr (EPI == 1) {
+      const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + c0 + c * 8);
+      uint32_t a[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t b[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lo = bf2f(a[e] & 0xffffu) + bf2f(b[e] & 0xffffu);
+        const float hi = bf2f(a[e] >> 16) + bf2f(b[e] >> 16);
+        a[e] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+      }
+      v = make_uint4(a[0], a[1], a[2], a[3]);
+    }
+    *reinterpret_cast<uint4*>(dst) = v;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, bool NORM>
+void launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
+            float eps, hipStream_t stream) {
+  const int tm = (M + BM - 1) / BM, tn = N / BN;
+  hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM>), dim3(tm * tn), dim3(256), 0, stream,
+                     (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R, ldr, M, N,
+                     K, eps, tm, tn);
+}
+
+template <int BM, int BN, int WM, int WN>
+int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr,
+                 int M, int N, int K, float eps, hipStream_t s) {
+  if (epi == 0 && !norm) launch<BM, BN, WM, WN, 0, false>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 0 && norm) launch<BM, BN, WM, WN, 0, true>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 1 && !norm) launch<BM, BN, WM, WN, 1, false>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 2 && norm) launch<BM, BN, WM, WN, 2, true>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 2 && !norm) launch<BM, BN, WM, WN, 2, false>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else return -3;
+  return 0;
+}
+
+}  // namespace
+
+// Tile configurations (BM x BN, wave grid): 0 = 128x128 (2x2), 1 = 128x64 (2x2),
+// 2 = 64x128 (1x4), 3 = 64x64 (2x2).  Returns 0, or <0 on a shape the kernel
+// does not cover (the launch is then skipped — the Python wrapper raises).
+extern "C" {
+
+int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
+            int epi, int norm, float eps, int cfg, hipStream_t stream) {
+  static const int BMs[4] = {128, 128, 64, 64}, BNs[4] = {128, 64, 128, 64};
+  if (cfg < 0 || cfg > 3) return -1;
+  if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
+  if (epi == 1 && !R) return -2;
+  switch (cfg) {
+    case 0: return dispatch_epi<128, 128, 2, 2>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
+    case 1: return dispatch_epi<128, 64, 2, 2>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
+    case 2: return dispatch_epi<64, 128, 1, 4>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
+    default: return dispatch_epi<64, 64, 2, 2>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
+  }
+}
+
+}  // extern "C"

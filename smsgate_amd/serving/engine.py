@@ -58,6 +58,8 @@ class EngineConfig:
     use_graphs: bool = True
     prefill_max_tokens: int = 32768
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
+    fused_gemm: bool = True  # csrc/gemm_kernels.hip (norm prologue, residual/SwiGLU epilogues) vs hipBLASLt
+    lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
 
 
@@ -110,8 +112,18 @@ class ExtractionEngine:
         # (tied) embedding: ids beyond it are masked in every FSM state, hence the
         # arg-max / Gumbel-max over allowed tokens is unchanged (exact, not an
         # approximation) and the projection is 6x smaller for the 49 152 vocab.
-        self.V_dec = min(mc.vocab, _round_up(tokenizer.vocab_size, 32))
+        self.V_dec = min(mc.vocab, _round_up(tokenizer.vocab_size, 64))
         self.lm_head = self.w.embed[: self.V_dec]
+        self.fused = ec.fused_gemm and self.V_dec % 64 == 0 and mc.hidden % 64 == 0 and mc.inter % 32 == 0
+        if self.fused:
+            # RMSNorm weights folded into the following projection; gate/up rows
+            # interleaved in 16-row groups for the SwiGLU epilogue (ops.gemm).
+            w = self.w
+            self.fw_qkv = [ops.fold_norm(w.qkv[i], w.ln1[i]) for i in range(mc.layers)]
+            self.fw_o = [w.o[i].contiguous() for i in range(mc.layers)]
+            self.fw_gu = [ops.interleave_gate_up(ops.fold_norm(w.gate_up[i], w.ln2[i])) for i in range(mc.layers)]
+            self.fw_down = [w.down[i].contiguous() for i in range(mc.layers)]
+            self.fw_lm = ops.fold_norm(self.lm_head, w.ln_f)
         self.fsm: SchemaFSM = build_fsm(tokenizer, self.V_dec, fields).to_device(self.device)
         self.max_out = self.fsm.max_steps()
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)
@@ -178,6 +190,37 @@ class ExtractionEngine:
             y = F.linear(act, w.down[i])
         return ops.rmsnorm_residual(resid, w.ln_f, mc.eps, x=y)
 
+    def _layers_fused(self, x: torch.Tensor, *, pos_tok: torch.Tensor, slot_tok: torch.Tensor, attn, k_cache,
+                      vt_cache, p0: int) -> torch.Tensor:
+        """Same network with the fused MFMA GEMMs: ``x`` is the residual stream,
+        updated in place; returns it UN-normed (the final norm is the lm_head
+        GEMM's prologue, :meth:`_logits`)."""
+        mc = self.mc
+        T = x.shape[0]
+        q = torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=x.device)
+        a = torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)
+        for i in range(mc.layers):
+            qkv = ops.gemm(x, self.fw_qkv[i], norm_eps=mc.eps)
+            ops.rope_qkv_cache(qkv, pos_tok, slot_tok, self.cos_sin, q, k_cache(i), vt_cache(i), mc.heads,
+                               mc.kv_heads, mc.head_dim, p0)
+            attn(i, q, a)
+            ops.gemm(a, self.fw_o[i], epi="resid", resid=x)
+            act = ops.gemm(x, self.fw_gu[i], epi="swiglu", norm_eps=mc.eps)
+            ops.gemm(act, self.fw_down[i], epi="resid", resid=x)
+        return x
+
+    def _forward(self, x: torch.Tensor, **kw) -> torch.Tensor:
+        return self._layers_fused(x, **kw) if self.fused else self._layers(x, **kw)
+
+    def _logits(self, h: torch.Tensor) -> torch.Tensor:
+        if self.fused:
+            # measured (scripts/kbench.py, B=4096): hipBLASLt's 8192-wide lm_head
+            # plus a separate RMSNorm beats the fused-norm GEMM at this width
+            if self.cfg.lm_head_fused:
+                return ops.gemm(h, self.fw_lm, norm_eps=self.mc.eps)
+            h = ops.rmsnorm_residual(h, self.w.ln_f, self.mc.eps)
+        return F.linear(h, self.lm_head)
+
     def _compute_prefix(self) -> None:
         ids = torch.tensor(self.prefix_ids, dtype=torch.int32, device=self.device)
         T = ids.numel()
@@ -199,7 +242,7 @@ class ExtractionEngine:
         def attn(i, q, out):
             ops.attn_prefill(q, cu, qs, s1, T, kc(i), vc(i), empty_k, empty_v, 0, out, self.scale)
 
-        self._layers(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=0)
+        self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=0)
         torch.cuda.synchronize(self.device)
 
     # ---------------------------------------------------------------- prefill
@@ -237,9 +280,9 @@ class ExtractionEngine:
             ops.attn_prefill(q, cu_d, qstart, rows_d, max_q, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
                              self.scale)
 
-        h = self._layers(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        h = self._forward(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
         last = h.index_select(0, (cu_d[1:] - 1).long())
-        logits = F.linear(last, self.lm_head)
+        logits = self._logits(last)
         if not sample:
             return logits
         # reset the admitted rows, then sample their first answer token
@@ -272,8 +315,8 @@ class ExtractionEngine:
             ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
                             done=self.done)
 
-        h = self._layers(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
-        logits = F.linear(h, self.lm_head)
+        h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        logits = self._logits(h)
         if sample:
             ops.fsm_sample(logits, self.fsm, self.state[:B], tok, self.out_buf[:B], self.out_len[:B],
                            self.done[:B], pos, slot, self.cfg.temperature, self.cfg.seed)

@@ -11,11 +11,14 @@ from smsgate_amd.serving.engine import EngineConfig, ExtractionEngine  # noqa: E
 from smsgate_amd.utils.synth import generate_bodies, reference_cases  # noqa: E402
 
 
-@pytest.fixture(scope="module")
-def tiny_engine():
+@pytest.fixture(scope="module", params=[True, False], ids=["fused_gemm", "hipblaslt"])
+def tiny_engine(request):
     w = ExtractorWeights(CONFIGS["tiny"], device="cuda", seed=3)
     w.requires_grad_(False)
-    return ExtractionEngine(w, load_tokenizer(), EngineConfig(max_slots=64, steps_per_graph=4, buckets=(16, 64)))
+    eng = ExtractionEngine(w, load_tokenizer(), EngineConfig(max_slots=64, steps_per_graph=4, buckets=(16, 64),
+                                                             fused_gemm=request.param))
+    assert eng.fused == request.param
+    return eng
 
 
 def _ref_logits(eng, body, extra=()):
@@ -72,3 +75,19 @@ def test_graph_and_eager_agree():
     g = ExtractionEngine(w, tk, EngineConfig(max_slots=32, steps_per_graph=4, buckets=(32,)))
     e = ExtractionEngine(w, tk, EngineConfig(max_slots=32, use_graphs=False, buckets=(32,)))
     assert g.run(bodies) == e.run(bodies)
+
+
+def test_fused_and_unfused_engines_agree_on_135m_logits():
+    """The production shape (576 wide, 30 layers): fused-GEMM logits vs hipBLASLt path."""
+    w = ExtractorWeights(CONFIGS["smollm-135m"], device="cuda", seed=7)
+    w.requires_grad_(False)
+    tk = load_tokenizer()
+    bodies = reference_cases()
+    outs = []
+    for fused in (True, False):
+        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=16, use_graphs=False, buckets=(16,), fused_gemm=fused))
+        outs.append(eng.debug_logits(bodies, [[5, 6], [7, 8], [9, 10]]))
+        del eng
+    for a, b in zip(*outs):
+        scale = b.abs().max().item()
+        assert (a - b).abs().max().item() <= 0.05 * scale + 0.05

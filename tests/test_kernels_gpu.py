@@ -191,3 +191,58 @@ def test_fsm_sample_greedy_and_transitions():
     ops.fsm_sample(logits, fsm, state2, tok, out_buf, out_len.zero_(), done, pos, slot, 1.0, 123)
     for b in range(B):
         assert allowed[int(states_h[b]), int(tok[b])]
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (100, 576, 576), (777, 960, 576), (256, 3072, 576),
+                                   (130, 576, 1536), (64, 8192, 576)])
+def test_gemm_store_and_norm(cfg, M, N, K):
+    bm, bn = ops.GEMM_TILES[cfg]
+    if N % bn:
+        pytest.skip("N not a multiple of the tile")
+    a = _bf(M, K, seed=11)
+    w = _bf(N, K, scale=K ** -0.5, seed=12)
+    nw = _bf(K, scale=0.1, seed=13) + 1
+    out = ops.gemm(a, w, cfg=cfg)
+    torch.testing.assert_close(out.float(), ops.ref_gemm(a, w), atol=3e-2, rtol=2e-2)
+    out_n = ops.gemm(a, ops.fold_norm(w, nw), norm_eps=1e-5, cfg=cfg)
+    torch.testing.assert_close(out_n.float(), ops.ref_gemm(a, w, norm_eps=1e-5, norm_w=nw), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M", [1, 333, 2048])
+def test_gemm_residual_inplace(cfg, M):
+    K, N = 1536, 576
+    bm, bn = ops.GEMM_TILES[cfg]
+    if N % bn:
+        pytest.skip("N not a multiple of the tile")
+    a = _bf(M, K, seed=21)
+    w = _bf(N, K, scale=K ** -0.5, seed=22)
+    x = _bf(M, N, seed=23)
+    ref = (x.float() + (a.float() @ w.float().t()).to(torch.bfloat16).float())
+    ops.gemm(a, w, epi="resid", resid=x, cfg=cfg)  # in place
+    torch.testing.assert_close(x.float(), ref, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M", [5, 640])
+def test_gemm_swiglu_norm(cfg, M):
+    K, I = 576, 1536
+    bm, bn = ops.GEMM_TILES[cfg]
+    a = _bf(M, K, seed=31)
+    gu = _bf(2 * I, K, scale=K ** -0.5, seed=32)
+    nw = _bf(K, scale=0.1, seed=33) + 1
+    w = ops.interleave_gate_up(ops.fold_norm(gu, nw))
+    out = ops.gemm(a, w, epi="swiglu", norm_eps=1e-5, cfg=cfg)
+    assert out.shape == (M, I)
+    ref = ops.ref_gemm(a, gu, epi="swiglu", norm_eps=1e-5, norm_w=nw)
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=3e-2)
+
+
+def test_gemm_strided_a_and_bad_shapes():
+    a_full = _bf(50, 640, seed=41)
+    a = a_full[:, :576]  # row stride 640 > K
+    w = _bf(128, 576, seed=42)
+    torch.testing.assert_close(ops.gemm(a, w).float(), ops.ref_gemm(a, w), atol=5e-2, rtol=2e-2)
+    with pytest.raises(ValueError):
+        ops.gemm(_bf(4, 100), _bf(64, 100))

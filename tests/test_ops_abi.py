@@ -52,6 +52,6 @@ def test_argtypes_match_c_signatures():
                 assert t.__name__ in ("c_int", "c_uint"), (name, a, t)
 
 
-@pytest.mark.parametrize("fn", ["sg_rmsnorm_residual", "sg_attn_prefill", "sg_attn_decode", "sg_fsm_sample"])
+@pytest.mark.parametrize("fn", ["sg_rmsnorm_residual", "sg_attn_prefill", "sg_attn_decode", "sg_fsm_sample", "sg_gemm"])
 def test_expected_entry_points_exist(fn):
     assert fn in _c_signatures()

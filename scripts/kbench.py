@@ -62,7 +62,7 @@ def main():
     def rnd(*s):
         return (torch.randn(*s, generator=g) * 0.02).to(bf).to(dev)
 
-    P0, P0pad, Lmax = 75, 96, 200
+    P0, P0pad, Lmax = 75, 96, 192
     res = {}
     x = rnd(B, H)
     w = torch.ones(H, dtype=bf, device=dev)
@@ -81,7 +81,14 @@ def main():
     out = torch.empty(B, nh * D, dtype=bf, device=dev)
     done = torch.zeros(B, dtype=torch.int32, device=dev)
     res["attn_decode"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, 1 / math.sqrt(D),
-                                                        done=done))
+                                                        done=done, impl="mfma"))
+    scr = (torch.empty(B, nh, D, dtype=torch.float32, device=dev), torch.empty(B, nh, dtype=torch.float32, device=dev))
+    res["attn_decode_cascade"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out,
+                                                                1 / math.sqrt(D), done=done, scratch=scr))
+    res["attn_decode_st"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, 1 / math.sqrt(D),
+                                                           done=done, impl="mfma"))
+    res["attn_decode_v1"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out, 1 / math.sqrt(D),
+                                                           done=done, impl="mfma_v1"))
     res["attn_decode_valu"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out,
                                                              1 / math.sqrt(D), done=done, impl="valu"))
     kv_bytes = B * nkv * a.ctx * D * 2 * 2
@@ -114,7 +121,7 @@ def main():
         res[f"fgemm_{name}_TFLOPs"] = round(2 * B * n * k / (best * 1e-6) / 1e12, 1)
     Xl, Wl = rnd(B, H), rnd(8192, H)
     res["gemm_lm_head_8192"] = timeit(lambda: F.linear(Xl, Wl))
-    fused_layer = (res["rope_qkv_cache"] + res["attn_decode"] + res["fgemm_qkv_auto"] + res["fgemm_o_auto"]
+    fused_layer = (res["rope_qkv_cache"] + res["attn_decode_cascade"] + res["fgemm_qkv_auto"] + res["fgemm_o_auto"]
                    + res["fgemm_gate_up_auto"] + res["fgemm_down_auto"])
     res["fused_sum_per_layer_us"] = round(fused_layer, 1)
     res["fused_est_step_us"] = round(fused_layer * cfg.layers + res["fgemm_lm_head_auto"], 1)

@@ -63,6 +63,10 @@ def _declare(lib: ctypes.CDLL) -> None:
                                    _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
     lib.sg_attn_decode_valu.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_valu.restype = _c_int
+    lib.sg_attn_decode_v1.argtypes = lib.sg_attn_decode.argtypes
+    lib.sg_attn_decode_v1.restype = _c_int
+    lib.sg_attn_decode_cascade.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_vp, _vp, _vp]
+    lib.sg_attn_decode_cascade.restype = _c_int
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
                                   ctypes.c_uint, _vp]
@@ -265,18 +269,36 @@ def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slo
 
 def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache: torch.Tensor,
                 vt_cache: torch.Tensor, pk: torch.Tensor, pvt: torch.Tensor, P0: int, out: torch.Tensor,
-                scale: float, done: Optional[torch.Tensor] = None, impl: str = "mfma") -> torch.Tensor:
+                scale: float, done: Optional[torch.Tensor] = None, impl: str = "cascade",
+                scratch: Optional[tuple] = None) -> torch.Tensor:
     """One query token per row; rows with ``done[b] != 0`` are skipped (output untouched).
 
-    ``impl="mfma"`` (default) packs the GQA heads of a KV head into one MFMA tile;
-    ``impl="valu"`` is the vector-ALU variant kept for A/B measurement."""
+    ``impl="cascade"`` (default): shared-prefix pass over 16 query rows per wave +
+    own-key pass seeded with the exact prefix softmax state; ``scratch`` =
+    ``(pre_o [>=B, nh, D] fp32, pre_lse [>=B, nh] fp32)`` (allocated if omitted).
+    ``"mfma"``: single-pass transposed MFMA kernel (S^T = K·Q^T, O^T = V^T·P^T);
+    ``"mfma_v1"``: S = Q·K^T with P through LDS; ``"valu"``: vector-ALU variant —
+    kept for A/B measurement.  MFMA kernels need ``Lmax``, padded prefix % 32 == 0."""
     B, nh, D = q.shape
     S, nkv, Lmax, _ = k_cache.shape
     P0pad = pk.shape[1]
     assert pos.numel() == B and slot.numel() == B and (done is None or done.numel() >= B)
     assert vt_cache.shape == vt_shape(S, nkv, D, Lmax) and pvt.shape == vt_shape(1, nkv, D, P0pad)[1:]
     lib = load_library()
-    fn = lib.sg_attn_decode if impl == "mfma" else lib.sg_attn_decode_valu
+    if impl == "cascade":
+        if scratch is None:
+            scratch = (torch.empty(B, nh, D, dtype=torch.float32, device=q.device),
+                       torch.empty(B, nh, dtype=torch.float32, device=q.device))
+        pre_o, pre_lse = scratch
+        if (pre_o.dtype != torch.float32 or pre_lse.dtype != torch.float32 or pre_o.shape[0] < B
+                or pre_o.shape[1:] != (nh, D) or pre_lse.shape[0] < B or pre_lse.shape[1:] != (nh,)):
+            raise ValueError("attn_decode: bad cascade scratch")
+        rc = lib.sg_attn_decode_cascade(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk),
+                                        _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, _p(pre_o),
+                                        _p(pre_lse), _stream())
+        _check(rc, "attn_decode[cascade]")
+        return out
+    fn = {"mfma": lib.sg_attn_decode, "mfma_v1": lib.sg_attn_decode_v1, "valu": lib.sg_attn_decode_valu}[impl]
     _check(fn(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B,
               nh, nkv, D, Lmax, scale, _stream()), f"attn_decode[{impl}]")
     return out

@@ -516,25 +516,26 @@ __global__ void __launch_bounds__(64) attn_decode_mfma_kernel(
   const int npre = P0pad >> 5;
   const int ntiles = npre + ((own + 31) >> 5);
 
+  // Tile loads are UNconditional: every key index of a tile is < roundup(own, 32)
+  // <= Lmax (resp. P0pad), inside the slot's rows, and cache rows past the valid
+  // length hold finite stale values (the caches are zero-initialised and only
+  // ever receive finite K/V), which the score mask turns into p = 0.  A per-lane
+  // guarded load would compile to a branch + vmcnt(0) and serialise the prefetch.
   auto load_tile = [&](int t, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
     const bool pre = t < npre;
     const int kt = pre ? t * 32 : (t - npre) * 32;
-    const int nval = pre ? P0 : own;
     const uint16_t* kb = pre ? kpre : kself;
     const uint16_t* vb = pre ? vpre : vself;
 #pragma unroll
     for (int hs = 0; hs < 2; ++hs) {
       const int key = kt + 16 * hs + r16;
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        kv[hs][s] = key < nval ? *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 8 * g4 + 32 * s)
-                               : make_uint4(0, 0, 0, 0);
+      for (int s = 0; s < 2; ++s) kv[hs][s] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 8 * g4 + 32 * s);
     }
     const int kk = kt + 8 * g4;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
-      vv[n] = kk < nval ? *reinterpret_cast<const uint4*>(vb + ((size_t)(kk >> 3) * D + 16 * n + r16) * 8)
-                        : make_uint4(0, 0, 0, 0);
+      vv[n] = *reinterpret_cast<const uint4*>(vb + ((size_t)(kk >> 3) * D + 16 * n + r16) * 8);
   };
 
   f32x4 o[4];
@@ -544,10 +545,10 @@ __global__ void __launch_bounds__(64) attn_decode_mfma_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i) { m[i] = -INFINITY; lsum[i] = 0.f; }
 
-  uint4 kc[2][2], vc[4], kn[2][2], vn[4];
-  load_tile(0, kc, vc);
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) load_tile(t + 1, kn, vn);
+  // Ping-pong K/V register sets, loop unrolled by 2 (a `cur = next` copy at the end
+  // of an iteration makes the compiler wait for the prefetch right there).  An odd
+  // tile count is padded with one fully-masked tile (its keys are >= own).
+  auto process = [&](int t, const uint4 (&kc)[2][2], const uint4 (&vc)[4]) {
     const bool pre = t < npre;
     const int kt = pre ? t * 32 : (t - npre) * 32;
     const int nval = pre ? P0 : own;
@@ -606,18 +607,23 @@ __global__ void __launch_bounds__(64) attn_decode_mfma_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[n][i] *= alpha[i];
     }
-    __syncthreads();
+    // one-wave block: LDS ops of a wave execute in order, so the P transpose needs
+    // no barrier (a __syncthreads() would also drain the K/V prefetch: vmcnt(0))
+    asm volatile("" ::: "memory");
     const bf16x8 pa = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&P_lds[r16 * 32 + 8 * g4]));
 #pragma unroll
     for (int n = 0; n < 4; ++n)
       o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vc[n]), o[n], 0, 0, 0);
-    __syncthreads();
-#pragma unroll
-    for (int hs = 0; hs < 2; ++hs)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) kc[hs][s] = kn[hs][s];
-#pragma unroll
-    for (int n = 0; n < 4; ++n) vc[n] = vn[n];
+    asm volatile("" ::: "memory");
+  };
+  uint4 ka[2][2], va[4], kb2[2][2], vb2[4];
+  load_tile(0, ka, va);
+  const int nt2 = (ntiles + 1) & ~1;
+  for (int t = 0; t < nt2; t += 2) {
+    load_tile(min(t + 1, ntiles - 1), kb2, vb2);
+    process(t, ka, va);
+    load_tile(min(t + 2, ntiles - 1), ka, va);
+    process(t + 1, kb2, vb2);
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -627,6 +633,340 @@ __global__ void __launch_bounds__(64) attn_decode_mfma_kernel(
     uint16_t* orow = out + ((size_t)b * nh + kh * G + row) * D;
 #pragma unroll
     for (int n = 0; n < 4; ++n) orow[16 * n + r16] = f2bf(o[n][i] * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Transposed MFMA decode attention (production path).  grid = (B, nkv), one wave.
+//
+//   S^T = K · Q^T   (A = 16 keys × 32 dims from the K cache, B = Q^T: the G query
+//                    heads of the GQA group are the 16 columns, cols >= G are 0)
+//   O^T = V^T · P^T (A = 16 dims × 32 keys straight from the blocked V^T cache,
+//                    B = P^T, which is exactly the S^T accumulator after exp2)
+//
+// Each lane owns ONE query column (q = lane & 15) and 8 of the tile's 32 keys
+// (4·(lane>>4)+i and 16+4·(lane>>4)+i), so the online-softmax max/sum are 7
+// in-lane ops + 2 cross-lane shuffles, the rescale of O^T is lane-local, and P
+// never leaves registers: its k-order (the MFMA's 8·(lane>>4)+j) is defined as
+// that same key set, and the V^T fragment is read in the same order (two 8-byte
+// pieces of the [key/8][D][8] blocks).  vs attn_decode_mfma_kernel: no LDS, 4
+// instead of 32 shuffles per 32-key tile.  K/V tiles are double-buffered in
+// registers (ping-pong, unrolled by 2) and loaded unconditionally (all key
+// indices < roundup(own, 32) <= Lmax; requires Lmax % 32 == 0).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) attn_decode_st_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
+    uint16_t* __restrict__ out, int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int b = blockIdx.x, kh = blockIdx.y, l = threadIdx.x;
+  if (done != nullptr && done[b]) return;
+  const int G = nh / nkv;
+  const int g4 = l >> 4, r16 = l & 15;
+  const int own = pos[b] + 1;
+  const int sl = slot[b];
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+
+  // B operand Q^T: lane holds Q[q = r16][dims 8·g4 + j (+32 s)]
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r16 < G) v = *reinterpret_cast<const uint4*>(q + ((size_t)b * nh + kh * G + r16) * D + 8 * g4 + 32 * s2);
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  const int npre = P0pad >> 5;
+  const int ntiles = npre + ((own + 31) >> 5);
+
+  auto load_tile = [&](int t, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
+    const bool pre = t < npre;
+    const int kt = pre ? t * 32 : (t - npre) * 32;
+    const uint16_t* kb = pre ? kpre : kself;
+    const uint16_t* vb = pre ? vpre : vself;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const int key = kt + 16 * hs + r16;  // A operand row
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        kv[hs][s2] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 8 * g4 + 32 * s2);
+    }
+    // V^T A operand: row = dim 16n + r16, k-slots j<4 -> keys kt+4g4+j, j>=4 -> kt+16+4g4+j-4
+    const int k_lo = kt + 4 * g4, k_hi = kt + 16 + 4 * g4;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int dim = 16 * n + r16;
+      const uint2 lo = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_lo >> 3) * D + dim) * 8 + (k_lo & 7));
+      const uint2 hi = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_hi >> 3) * D + dim) * 8 + (k_hi & 7));
+      vv[n] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+  };
+
+  f32x4 o[4];  // O^T: lane holds O[q = r16][dim 16n + 4g4 + i]
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+
+  auto process = [&](int t, const uint4 (&kc)[2][2], const uint4 (&vc)[4]) {
+    const bool pre = t < npre;
+    const int kt = pre ? t * 32 : (t - npre) * 32;
+    const int nval = pre ? P0 : own;
+    f32x4 st[2];
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      st[hs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        st[hs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kc[hs][s2]), qb[s2], st[hs], 0, 0,
+                                                         0);
+    }
+    // lane: st[hs][i] = score(query r16, key kt + 16hs + 4g4 + i)
+    float sv[2][4], tmax = -INFINITY;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = (kt + 16 * hs + 4 * g4 + i) < nval;
+        sv[hs][i] = ok ? st[hs][i] * scale_log2 : -INFINITY;
+        tmax = fmaxf(tmax, sv[hs][i]);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, WAVE));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, WAVE));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+    m = mn;
+    float p[8], rs = 0.f;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = (mn == -INFINITY) ? 0.f : exp2f(sv[hs][i] - mn);
+        p[4 * hs + i] = e;
+        rs += e;
+      }
+    rs += __shfl_xor(rs, 16, WAVE);
+    rs += __shfl_xor(rs, 32, WAVE);
+    lsum = lsum * alpha + rs;
+    uint4 pw;
+    pw.x = (uint32_t)f2bf(p[0]) | ((uint32_t)f2bf(p[1]) << 16);
+    pw.y = (uint32_t)f2bf(p[2]) | ((uint32_t)f2bf(p[3]) << 16);
+    pw.z = (uint32_t)f2bf(p[4]) | ((uint32_t)f2bf(p[5]) << 16);
+    pw.w = (uint32_t)f2bf(p[6]) | ((uint32_t)f2bf(p[7]) << 16);
+    const bf16x8 pb = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[n][i] *= alpha;
+      o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vc[n]), pb, o[n], 0, 0, 0);
+    }
+  };
+
+  uint4 ka[2][2], va[4], kb2[2][2], vb2[4];
+  load_tile(0, ka, va);
+  const int nt2 = (ntiles + 1) & ~1;  // odd counts: one fully-masked pad tile (keys >= own)
+  for (int t = 0; t < nt2; t += 2) {
+    load_tile(min(t + 1, ntiles - 1), kb2, vb2);
+    process(t, ka, va);
+    load_tile(min(t + 2, ntiles - 1), ka, va);
+    process(t + 1, kb2, vb2);
+  }
+  if (r16 < G) {
+    const float inv = 1.f / lsum;
+    uint16_t* orow = out + ((size_t)b * nh + kh * G + r16) * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[n][0] * inv) | ((uint32_t)f2bf(o[n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[n][2] * inv) | ((uint32_t)f2bf(o[n][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cascade decode attention = shared-prefix pass + own-key pass (production).
+//
+// Every decode row attends to the same P0 system-prompt keys.  Reading them once
+// per (row, kv head) made the L2 traffic of the prefix larger than the HBM
+// traffic of the rows' own keys.  Pass 1 (attn_prefix_kernel) packs 16 query
+// rows of ANY sequences of one kv head into the 16 MFMA columns, so the prefix
+// K/V are read once per 16 rows, and writes the normalised prefix output O_pre
+// (fp32) and its log-sum-exp (log2 domain).  Pass 2 (attn_own_kernel) starts its
+// online softmax from the exact state (m = lse, l = 1, o = O_pre) and streams
+// only the row's own keys.  Both use the transposed formulation of
+// attn_decode_st_kernel (S^T = K·Q^T, O^T = V^T·P^T; one query per lane column).
+// ---------------------------------------------------------------------------
+template <bool PRE>
+__device__ __forceinline__ void st_load_tile(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb, int kt,
+                                             int g4, int r16, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
+  constexpr int D = 64;
+#pragma unroll
+  for (int hs = 0; hs < 2; ++hs) {
+    const int key = kt + 16 * hs + r16;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      kv[hs][s2] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 8 * g4 + 32 * s2);
+  }
+  const int k_lo = kt + 4 * g4, k_hi = kt + 16 + 4 * g4;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int dim = 16 * n + r16;
+    const uint2 lo = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_lo >> 3) * D + dim) * 8 + (k_lo & 7));
+    const uint2 hi = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_hi >> 3) * D + dim) * 8 + (k_hi & 7));
+    vv[n] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+}
+
+// One 32-key tile of the transposed online softmax (state per lane = its query).
+__device__ __forceinline__ void st_tile(const bf16x8 (&qb)[2], const uint4 (&kc)[2][2], const uint4 (&vc)[4],
+                                        int kt, int nval, int g4, float scale_log2, float& m, float& lsum,
+                                        f32x4 (&o)[4]) {
+  f32x4 st[2];
+#pragma unroll
+  for (int hs = 0; hs < 2; ++hs) {
+    st[hs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      st[hs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kc[hs][s2]), qb[s2], st[hs], 0, 0, 0);
+  }
+  float sv[2][4], tmax = -INFINITY;
+#pragma unroll
+  for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = (kt + 16 * hs + 4 * g4 + i) < nval;
+      sv[hs][i] = ok ? st[hs][i] * scale_log2 : -INFINITY;
+      tmax = fmaxf(tmax, sv[hs][i]);
+    }
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 16, WAVE));
+  tmax = fmaxf(tmax, __shfl_xor(tmax, 32, WAVE));
+  const float mn = fmaxf(m, tmax);
+  const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m - mn);
+  m = mn;
+  float p[8], rs = 0.f;
+#pragma unroll
+  for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = (mn == -INFINITY) ? 0.f : exp2f(sv[hs][i] - mn);
+      p[4 * hs + i] = e;
+      rs += e;
+    }
+  rs += __shfl_xor(rs, 16, WAVE);
+  rs += __shfl_xor(rs, 32, WAVE);
+  lsum = lsum * alpha + rs;
+  uint4 pw;
+  pw.x = (uint32_t)f2bf(p[0]) | ((uint32_t)f2bf(p[1]) << 16);
+  pw.y = (uint32_t)f2bf(p[2]) | ((uint32_t)f2bf(p[3]) << 16);
+  pw.z = (uint32_t)f2bf(p[4]) | ((uint32_t)f2bf(p[5]) << 16);
+  pw.w = (uint32_t)f2bf(p[6]) | ((uint32_t)f2bf(p[7]) << 16);
+  const bf16x8 pb = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[n][i] *= alpha;
+    o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vc[n]), pb, o[n], 0, 0, 0);
+  }
+}
+
+// Pass 1: grid = (ceil(B*G / 16), nkv), one wave; column c <-> query row
+// r = 16·blockIdx.x + c of kv head kh, i.e. sequence r / G, head kh·G + r % G.
+__global__ void __launch_bounds__(64) attn_prefix_kernel(const uint16_t* __restrict__ q,
+                                                         const uint16_t* __restrict__ pk,
+                                                         const uint16_t* __restrict__ pvt, int P0, int P0pad,
+                                                         float* __restrict__ pre_o, float* __restrict__ pre_lse,
+                                                         int B, int nh, int nkv, float scale_log2) {
+  constexpr int D = 64;
+  const int kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
+  const int G = nh / nkv;
+  const int r = blockIdx.x * 16 + r16;
+  const bool valid = r < B * G;
+  const size_t qrow = valid ? (size_t)(r / G) * nh + kh * G + (r % G) : 0;
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);  // row 0 when !valid
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  const uint16_t* kb = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vb = pvt + (size_t)kh * D * P0pad;
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  for (int kt = 0; kt < P0pad; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile<true>(kb, vb, kt, g4, r16, kc, vc);
+    st_tile(qb, kc, vc, kt, P0, g4, scale_log2, m, lsum, o);
+  }
+  if (valid) {
+    const float inv = 1.f / lsum;
+    float* orow = pre_o + qrow * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      *reinterpret_cast<float4*>(orow + 16 * n + 4 * g4) =
+          make_float4(o[n][0] * inv, o[n][1] * inv, o[n][2] * inv, o[n][3] * inv);
+    if (g4 == 0) pre_lse[qrow] = m + __log2f(lsum);
+  }
+}
+
+// Pass 2: grid = (B, nkv), one wave; the row's own keys, seeded with the prefix state.
+__global__ void __launch_bounds__(64) attn_own_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const float* __restrict__ pre_o, const float* __restrict__ pre_lse, uint16_t* __restrict__ out, int nh, int nkv,
+    int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int b = blockIdx.x, kh = blockIdx.y, l = threadIdx.x;
+  if (done != nullptr && done[b]) return;
+  const int G = nh / nkv;
+  const int g4 = l >> 4, r16 = l & 15;
+  const int own = pos[b] + 1;
+  const int sl = slot[b];
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const size_t qrow = (size_t)b * nh + kh * G + (r16 < G ? r16 : 0);
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);
+    if (r16 >= G) v = make_uint4(0, 0, 0, 0);
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  f32x4 o[4];
+  float m = -INFINITY, lsum = 0.f;
+  if (pre_o != nullptr && r16 < G) {  // exact prefix state: sum of 2^(s - lse) = 1
+    m = pre_lse[qrow];
+    lsum = 1.f;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const float4 v = *reinterpret_cast<const float4*>(pre_o + qrow * D + 16 * n + 4 * g4);
+      o[n] = (f32x4){v.x, v.y, v.z, v.w};
+    }
+  } else {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  // plain loop: with ~4 resident waves per SIMD the load latency is covered by
+  // the other waves (a register ping-pong measured no faster and costs VGPRs)
+  for (int kt = 0; kt < own; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile<false>(kself, vself, kt, g4, r16, kc, vc);
+    st_tile(qb, kc, vc, kt, own, g4, scale_log2, m, lsum, o);
+  }
+  if (r16 < G) {
+    const float inv = 1.f / lsum;
+    uint16_t* orow = out + qrow * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[n][0] * inv) | ((uint32_t)f2bf(o[n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[n][2] * inv) | ((uint32_t)f2bf(o[n][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
+    }
   }
 }
 
@@ -768,7 +1108,41 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
 int sg_attn_decode(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
                    const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh,
                    int nkv, int D, int Lmax, float scale, hipStream_t stream) {
-  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 8) || P0 > P0pad) return -1;
+  // unconditional 32-key tile loads: Lmax and P0pad must be multiples of 32
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(attn_decode_st_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, pos, slot, done,
+                     (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt, P0,
+                     P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// Cascade decode attention (production): prefix pass + own-key pass.  pre_o
+// [B, nh, D] fp32 and pre_lse [B, nh] fp32 are caller-provided scratch.
+int sg_attn_decode_cascade(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                           const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B,
+                           int nh, int nkv, int D, int Lmax, float scale, void* pre_o, void* pre_lse,
+                           hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (P0 > 0 && (pre_o == nullptr || pre_lse == nullptr)) return -2;
+  if (B == 0) return 0;
+  const float sl2 = scale * 1.4426950408889634f;
+  const int G = nh / nkv;
+  if (P0 > 0)
+    hipLaunchKernelGGL(attn_prefix_kernel, dim3((B * G + 15) / 16, nkv), dim3(64), 0, stream, (const uint16_t*)q,
+                       (const uint16_t*)pk, (const uint16_t*)pvt, P0, P0pad, (float*)pre_o, (float*)pre_lse, B, nh, nkv,
+                       sl2);
+  hipLaunchKernelGGL(attn_own_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, pos, slot, done,
+                     (const uint16_t*)k_cache, (const uint16_t*)vt_cache, P0 > 0 ? (const float*)pre_o : nullptr,
+                     (const float*)pre_lse, (uint16_t*)out, nh, nkv, Lmax, sl2);
+  return (int)hipGetLastError();
+}
+
+// Previous MFMA formulation (S = Q·K^T, P through LDS) — kept for A/B (kbench).
+int sg_attn_decode_v1(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                      const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B,
+                      int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
   if (B == 0) return 0;
   hipLaunchKernelGGL(attn_decode_mfma_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, pos, slot, done,
                      (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt, P0,

@@ -59,6 +59,7 @@ class EngineConfig:
     prefill_max_tokens: int = 32768
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
     fused_gemm: bool = True  # csrc/gemm_kernels.hip (norm prologue, residual/SwiGLU epilogues) vs hipBLASLt
+    decode_attn: str = "cascade"  # ops.attn_decode impl: cascade | mfma | mfma_v1 | valu
     lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
 
@@ -129,7 +130,7 @@ class ExtractionEngine:
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)
         self.P0 = len(self.prefix_ids)
         self.P0pad = _round_up(self.P0, 32)
-        self.Lmax = _round_up(ec.max_body_tokens + 2 + self.max_out, 8)
+        self.Lmax = _round_up(ec.max_body_tokens + 2 + self.max_out, 32)  # decode tiles are 32 keys
         if self.P0pad + self.Lmax > 512:
             raise ValueError("prefix + Lmax exceeds the decode kernel's context limit (512)")
         S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
@@ -138,6 +139,9 @@ class ExtractionEngine:
         self.vt_cache = torch.zeros(L, *ops.vt_shape(S, nkv, D, self.Lmax), dtype=bf, device=dev)
         self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
         self.pvt = torch.zeros(L, *ops.vt_shape(1, nkv, D, self.P0pad)[1:], dtype=bf, device=dev)
+        # cascade decode attention scratch: prefix output / log-sum-exp per query row
+        self.attn_scratch = (torch.empty(S, mc.heads, D, dtype=torch.float32, device=dev),
+                             torch.empty(S, mc.heads, dtype=torch.float32, device=dev))
         self.cos_sin = ops.rope_table(self.P0 + self.Lmax + 1, D, mc.rope_theta, dev)
         self.scale = 1.0 / math.sqrt(D)
         i32 = dict(dtype=torch.int32, device=dev)
@@ -313,7 +317,7 @@ class ExtractionEngine:
 
         def attn(i, q, out):
             ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
-                            done=self.done)
+                            done=self.done, impl=self.cfg.decode_attn, scratch=self.attn_scratch)
 
         h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
         logits = self._logits(h)

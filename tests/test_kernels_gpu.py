@@ -121,10 +121,10 @@ def test_attn_prefill(P0):
         o += n
 
 
-@pytest.mark.parametrize("impl", ["mfma", "valu"])
+@pytest.mark.parametrize("impl", ["cascade", "mfma", "mfma_v1", "valu"])
 @pytest.mark.parametrize("P0", [0, 75])
 def test_attn_decode(P0, impl):
-    nh, nkv, D, S, Lmax = 9, 3, 64, 8, 200
+    nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224  # MFMA decode tiles need Lmax % 32 == 0
     P0pad = (P0 + 31) // 32 * 32
     B = 6
     q = _bf(B, nh, D, seed=9)
@@ -137,7 +137,7 @@ def test_attn_decode(P0, impl):
         pk[:, :P0] = _bf(nkv, P0, D, seed=12)
         pvrows[:, :P0] = _bf(nkv, P0, D, seed=13)
     pvt = ops.rows_to_vt(pvrows)
-    pos = torch.tensor([0, 1, 7, 8, 100, 199], dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 1, 7, 8, 100, 223], dtype=torch.int32, device=DEV)  # 223: own == Lmax
     slot = torch.tensor([3, 0, 7, 1, 2, 5], dtype=torch.int32, device=DEV)
     out = torch.full((B, nh * D), 7.0, dtype=torch.bfloat16, device=DEV)
     scale = 1 / math.sqrt(D)

@@ -11,6 +11,8 @@ rc=$?; tail -3 $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*stats*" | head
 f=$(find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*kernel_stats.csv" | head -1)
 [ -n "$f" ] && head -40 "$f" | cut -c1-250
+t=$(find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*kernel_trace.csv" | head -1)
+[ -n "$t" ] && python $GRAFT_REPO_ROOT/scripts/trace_gaps.py "$t" > $GRAFT_REPO_ROOT/gpurun_out/prof/gaps.txt 2>&1; cat $GRAFT_REPO_ROOT/gpurun_out/prof/gaps.txt
 # keep the merged output small: drop the big per-dispatch trace
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*kernel_trace.csv" -size +20M -delete
 exit $rc

@@ -33,6 +33,7 @@ __all__ = [
     "fsm_sample",
     "gemm",
     "gemm_cfg",
+    "gemm_qkv_rope",
     "interleave_gate_up",
     "fold_norm",
     "rope_table",
@@ -72,7 +73,9 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   ctypes.c_uint, _vp]
     lib.sg_gemm.argtypes = [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                             _c_float, _c_int, _vp]
-    for f in ("sg_gemm", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
+    lib.sg_gemm_qkv_rope.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_float, _c_int, _ip, _ip, _vp, _vp, _vp,
+                                     _vp, _c_int, _c_int, _c_int, _c_int, _vp]
+    for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
 
@@ -151,7 +154,8 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     return out
 
 
-GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 64), 5: (64, 64), 6: (64, 64),
+              7: (128, 128), 8: (64, 128)}  # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
@@ -209,6 +213,33 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Opti
                                 float(norm_eps or 0.0), c, _stream())
     _check(rc, "gemm")
     return out
+
+
+def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tensor, slot: torch.Tensor,
+                  cos_sin: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor, vt_cache: torch.Tensor,
+                  nh: int, nkv: int, p0: int, cfg: Optional[int] = None) -> None:
+    """``rope(rmsnorm(x) @ w.T)`` scattered into ``q_out`` and the KV cache (one fused
+    kernel; ``w`` has the norm weight folded in).  Same result as :func:`gemm` +
+    :func:`rope_qkv_cache`."""
+    M, K = x.shape
+    S, nkv_, Lmax, D = k_cache.shape
+    if x.dtype != torch.bfloat16 or x.stride(1) != 1 or x.stride(0) % 8 or K % 64:
+        raise ValueError("gemm_qkv_rope: bad activation")
+    if w.shape != ((nh + 2 * nkv) * 64, K) or not w.is_contiguous() or D != 64 or nkv_ != nkv:
+        raise ValueError("gemm_qkv_rope: bad weight / cache")
+    _req(pos, torch.int32, "pos")
+    _req(slot, torch.int32, "slot")
+    _req(cos_sin, torch.float32, "cos_sin")
+    assert vt_cache.shape == vt_shape(S, nkv, D, Lmax) and pos.numel() >= M and slot.numel() >= M
+    assert q_out.is_contiguous() and q_out.numel() >= M * nh * D and q_out.dtype == torch.bfloat16
+    if M == 0:
+        return
+    if cfg is None:
+        cfg = 1 if -(-M // 128) * (w.shape[0] // 64) >= 480 else 3
+    rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
+                                         _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
+                                         _stream())
+    _check(rc, "gemm_qkv_rope")
 
 
 def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:

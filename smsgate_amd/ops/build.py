@@ -54,6 +54,11 @@ def build(force: bool = False, verbose: bool = False, extra: Optional[List[str]]
         "-fPIC",
         "-shared",
         "-munsafe-fp-atomics",
+        # MFMA accumulators in VGPRs: the default AGPR form made the GEMM K-loop
+        # shuffle its accumulators (68 v_accvgpr_* per 32 MFMAs) and cost the
+        # attention kernels one wave of occupancy (scripts/kernel_resources.py)
+        "-mllvm",
+        "-amdgpu-mfma-vgpr-form=1",
         *(extra or []),
         *[str(s) for s in sources()],
         "-o",

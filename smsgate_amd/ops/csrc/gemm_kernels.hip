@@ -40,6 +40,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64;  // K elements per tile = 8 chunks of 16 B
 
+// EPI 3 (QKV projection + RoPE + KV-cache write) arguments; unused by other epilogues.
+struct RopeArgs {
+  const int* pos;       // [M] own-key offset of each token
+  const int* slot;      // [M] KV slot of each token
+  const float2* cs;     // [max_pos][32] (cos, sin), RoPE position = p0 + pos
+  uint16_t* q_out;      // [M][nh][64]
+  uint16_t* k_cache;    // [S][nkv][Lmax][64]
+  uint16_t* vt_cache;   // [S][nkv][Lmax/8][64][8]
+  int nh, nkv, Lmax, p0;
+};
+
 __device__ __forceinline__ float bf2f(uint32_t v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
@@ -108,13 +119,14 @@ __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], 
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool NORM>
+template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST>
 __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restrict__ A, int lda,
                                                          const uint16_t* __restrict__ W,
                                                          uint16_t* C, int ldc, const uint16_t* R, int ldr,
                                                          int M, int N, int K, float eps, int tiles_m,
-                                                         int tiles_n) {
+                                                         int tiles_n, RopeArgs ra) {
   static_assert(WM * WN == 4, "4 waves");
+  static_assert(EPI != 3 || BN == 64, "QKV+RoPE epilogue: one 64-wide head per N tile");
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   constexpr int FM = TM / 16, FN = TN / 16;  // MFMA tiles per wave
   static_assert(FM >= 1 && FN >= 1 && TM % 16 == 0 && TN % 16 == 0, "tile");
@@ -123,11 +135,14 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   constexpr int CST = BNO + 8;                // staged C row stride (elements), +16 B pad
   constexpr int TILE = (BM + BN) * BK;        // one stage (A + B) in elements
   constexpr int NI = (BM + BN) / 32;          // glds instructions per stage per wave
-  static_assert(BM * CST <= 2 * TILE, "C staging fits in the K-loop buffers");
+  static_assert(ST >= 2 && ST <= 4, "pipeline stages");
+  static_assert(BM * CST * 2 + BM * 4 <= ST * TILE * 2, "C staging + row scales fit in the K-loop buffers");
 
   // ONE __shared__ array (a second one makes hipcc wait vmcnt(0) before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * TILE + 2 * BM];
-  float* rs = reinterpret_cast<float*>(smem + 2 * TILE);
+  // the row scales are written after the K loop, into the tail of the (then free)
+  // stage buffers, beyond the C staging tile
+  __shared__ __attribute__((aligned(16))) uint16_t smem[ST * TILE];
+  float* rs = reinterpret_cast<float*>(smem + ST * TILE) - BM;
 
   // ---- XCD-aware, bijective tile assignment: the blocks of one XCD (orig % 8)
   // get a contiguous range of tiles, so tiles that share A rows share an L2
@@ -149,26 +164,33 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  // ---- K loop: the DMA of tile kt+1 is in flight while tile kt is multiplied.
-  // Counted vmcnt + raw s_barrier (a __syncthreads() would drain the DMA queue).
+  // ---- K loop, ST-stage pipeline: the DMAs of tiles kt+1 .. kt+ST-1 are in flight
+  // while tile kt is multiplied.  The wait is a constant counted vmcnt (this
+  // wave's NI·(ST-1) newest DMAs may stay outstanding): past the last tile the
+  // issue slot re-loads tile KT-1 into the idle buffer (never read) so the count
+  // stays exact.  Raw s_barrier: a __syncthreads() would drain the DMA queue.
   const int KT = K / BK;
-  issue_tile<BM>(A, lda, m0, M - 1, 0, smem, wave, lane);
-  issue_tile<BN>(W, K, n0, N - 1, 0, smem + BM * BK, wave, lane);
-  for (int kt = 0; kt < KT; ++kt) {
-    uint16_t* cur = smem + (kt & 1) * TILE;
-    if (kt + 1 < KT) {
-      uint16_t* nxt = smem + ((kt + 1) & 1) * TILE;
-      issue_tile<BM>(A, lda, m0, M - 1, (kt + 1) * BK, nxt, wave, lane);
-      issue_tile<BN>(W, K, n0, N - 1, (kt + 1) * BK, nxt + BM * BK, wave, lane);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // tile kt landed (this wave's part)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // ... and every wave's part
-    mma_tile<FM, FN, NORM>(acc, ss, cur, cur + BM * BK, wm0, wn0, lane);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled next iteration
+#pragma unroll
+  for (int s0 = 0; s0 < ST - 1; ++s0) {
+    const int kk = min(s0, KT - 1) * BK;
+    issue_tile<BM>(A, lda, m0, M - 1, kk, smem + s0 * TILE, wave, lane);
+    issue_tile<BN>(W, K, n0, N - 1, kk, smem + s0 * TILE + BM * BK, wave, lane);
   }
+  int cur = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int nb = cur == 0 ? ST - 1 : cur - 1;  // buffer of tile kt + ST - 1 == (kt - 1) % ST
+    const int kk = min(kt + ST - 1, KT - 1) * BK;
+    issue_tile<BM>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+    issue_tile<BN>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (ST - 1)) : "memory");  // tile kt landed (this wave's part)
+    __builtin_amdgcn_s_barrier();                                          // ... and every wave's part
+    mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled by the next issue
+    cur = cur + 1 == ST ? 0 : cur + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-loads ...
+  __syncthreads();  // ... of EVERY wave have landed before rs / the C tile reuse the buffers
 
   // ---- row scales (RMSNorm): lanes l, l^16, l^32, l^48 hold the 4 k-quarters of row l&15
   if constexpr (NORM) {
@@ -212,6 +234,50 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   }
   __syncthreads();
 
+  // ---- epilogue 2 (EPI 3): RoPE the q/k head of this tile into q_out / the K
+  // cache, or scatter the v head into the blocked V^T cache.  Same rounding as
+  // the unfused path: bf16 projection (the staged tile) -> fp32 RoPE -> bf16.
+  if constexpr (EPI == 3) {
+    const int h = n0 >> 6;
+    if (h < ra.nh + ra.nkv) {
+      for (int q = tid; q < BM * 4; q += 256) {
+        const int row = q >> 2, c = q & 3;
+        const int gr = m0 + row;
+        if (gr >= M) continue;
+        const int p = ra.pos[gr];
+        const uint4 v1 = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
+        const uint4 v2 = *reinterpret_cast<const uint4*>(Cs + row * CST + 32 + c * 8);
+        const float4* csp = reinterpret_cast<const float4*>(ra.cs + (size_t)(ra.p0 + p) * 32 + c * 8);
+        const uint32_t a1[4] = {v1.x, v1.y, v1.z, v1.w}, a2[4] = {v2.x, v2.y, v2.z, v2.w};
+        uint32_t o1[4], o2[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float4 t = csp[e];  // (cos, sin) of dims 2e, 2e+1 of this chunk
+          const float x1l = bf2f(a1[e] & 0xffffu), x1h = bf2f(a1[e] >> 16);
+          const float x2l = bf2f(a2[e] & 0xffffu), x2h = bf2f(a2[e] >> 16);
+          o1[e] = (uint32_t)f2bf(x1l * t.x - x2l * t.y) | ((uint32_t)f2bf(x1h * t.z - x2h * t.w) << 16);
+          o2[e] = (uint32_t)f2bf(x2l * t.x + x1l * t.y) | ((uint32_t)f2bf(x2h * t.z + x1h * t.w) << 16);
+        }
+        uint16_t* dst;
+        if (h < ra.nh) dst = ra.q_out + ((size_t)gr * ra.nh + h) * 64;
+        else dst = ra.k_cache + (((size_t)ra.slot[gr] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
+        *reinterpret_cast<uint4*>(dst + c * 8) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+        *reinterpret_cast<uint4*>(dst + 32 + c * 8) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
+      }
+    } else {
+      const int kh = h - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
+      for (int q = tid; q < BM * 64; q += 256) {
+        const int row = q >> 6, d = q & 63;
+        const int gr = m0 + row;
+        if (gr >= M) continue;
+        const int p = ra.pos[gr];
+        ra.vt_cache[((((size_t)ra.slot[gr] * ra.nkv + kh) * nb + (p >> 3)) * 64 + d) * 8 + (p & 7)] =
+            Cs[row * CST + d];
+      }
+    }
+    return;
+  }
+
   // ---- epilogue 2: coalesced 16-B row chunks (+ residual)
   constexpr int CPR = BNO / 8;  // chunks per row
   const int c0 = EPI == 2 ? n0 / 2 : n0;
@@ -237,46 +303,75 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool NORM>
+template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST>
 void launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
-            float eps, hipStream_t stream) {
+            float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}) {
   const int tm = (M + BM - 1) / BM, tn = N / BN;
-  hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM>), dim3(tm * tn), dim3(256), 0, stream,
+  hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST>), dim3(tm * tn), dim3(256), 0, stream,
                      (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R, ldr, M, N,
-                     K, eps, tm, tn);
+                     K, eps, tm, tn, ra);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int ST>
 int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr,
                  int M, int N, int K, float eps, hipStream_t s) {
-  if (epi == 0 && !norm) launch<BM, BN, WM, WN, 0, false>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 0 && norm) launch<BM, BN, WM, WN, 0, true>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 1 && !norm) launch<BM, BN, WM, WN, 1, false>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 2 && norm) launch<BM, BN, WM, WN, 2, true>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 2 && !norm) launch<BM, BN, WM, WN, 2, false>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  if (epi == 0 && !norm) launch<BM, BN, WM, WN, 0, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 0 && norm) launch<BM, BN, WM, WN, 0, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 1 && !norm) launch<BM, BN, WM, WN, 1, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 2 && norm) launch<BM, BN, WM, WN, 2, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  else if (epi == 2 && !norm) launch<BM, BN, WM, WN, 2, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
   else return -3;
   return 0;
 }
 
 }  // namespace
 
-// Tile configurations (BM x BN, wave grid): 0 = 128x128 (2x2), 1 = 128x64 (2x2),
-// 2 = 64x128 (1x4), 3 = 64x64 (2x2).  Returns 0, or <0 on a shape the kernel
-// does not cover (the launch is then skipped — the Python wrapper raises).
+// Tile configurations: BM x BN (wave grid), pipeline stages.
+//   0: 128x128 (2x2) 2st   1: 128x64 (2x2) 2st   2: 64x128 (1x4) 2st   3: 64x64 (2x2) 2st
+//   4: 128x64  (2x2) 3st   5: 64x64  (2x2) 3st   6: 64x64  (2x2) 4st   7: 128x128 (2x2) 3st
+//   8: 64x128  (1x4) 3st
+// Returns 0, or <0 on a shape the kernel does not cover (the launch is then
+// skipped — the Python wrapper raises).
 extern "C" {
 
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, hipStream_t stream) {
-  static const int BMs[4] = {128, 128, 64, 64}, BNs[4] = {128, 64, 128, 64};
-  if (cfg < 0 || cfg > 3) return -1;
+  static const int BNs[9] = {128, 64, 128, 64, 64, 64, 64, 128, 128};
+  if (cfg < 0 || cfg > 8) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
+#define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream
   switch (cfg) {
-    case 0: return dispatch_epi<128, 128, 2, 2>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
-    case 1: return dispatch_epi<128, 64, 2, 2>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
-    case 2: return dispatch_epi<64, 128, 1, 4>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
-    default: return dispatch_epi<64, 64, 2, 2>(epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream);
+    case 0: return dispatch_epi<128, 128, 2, 2, 2>(SG_ARGS);
+    case 1: return dispatch_epi<128, 64, 2, 2, 2>(SG_ARGS);
+    case 2: return dispatch_epi<64, 128, 1, 4, 2>(SG_ARGS);
+    case 3: return dispatch_epi<64, 64, 2, 2, 2>(SG_ARGS);
+    case 4: return dispatch_epi<128, 64, 2, 2, 3>(SG_ARGS);
+    case 5: return dispatch_epi<64, 64, 2, 2, 3>(SG_ARGS);
+    case 6: return dispatch_epi<64, 64, 2, 2, 4>(SG_ARGS);
+    case 7: return dispatch_epi<128, 128, 2, 2, 3>(SG_ARGS);
+    default: return dispatch_epi<64, 128, 1, 4, 3>(SG_ARGS);
   }
+#undef SG_ARGS
+}
+
+// QKV projection with the RMSNorm prologue and the RoPE + KV-cache epilogue
+// (replaces gemm + sg_rope_qkv_cache).  W: [(nh + 2 nkv)·64, K], norm folded in.
+// cfg must have BN = 64 (1, 3 or 5).
+int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float eps, int cfg, const int* pos,
+                     const int* slot, const void* cos_sin, void* q_out, void* k_cache, void* vt_cache, int nh, int nkv,
+                     int Lmax, int p0, hipStream_t stream) {
+  const int N = (nh + 2 * nkv) * 64;
+  if (M <= 0 || K % BK != 0 || lda % 8 != 0 || (Lmax % 8) != 0) return -2;
+  RopeArgs ra{pos, slot, (const float2*)cos_sin, (uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)vt_cache,
+              nh, nkv, Lmax, p0};
+  switch (cfg) {
+    case 1: launch<128, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra); break;
+    case 3: launch<64, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra); break;
+    case 5: launch<64, 64, 2, 2, 3, true, 3>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra); break;
+    default: return -1;
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -193,7 +193,7 @@ def test_fsm_sample_greedy_and_transitions():
         assert allowed[int(states_h[b]), int(tok[b])]
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", list(range(9)))
 @pytest.mark.parametrize("M,N,K", [(1, 128, 64), (100, 576, 576), (777, 960, 576), (256, 3072, 576),
                                    (130, 576, 1536), (64, 8192, 576)])
 def test_gemm_store_and_norm(cfg, M, N, K):
@@ -209,7 +209,7 @@ def test_gemm_store_and_norm(cfg, M, N, K):
     torch.testing.assert_close(out_n.float(), ops.ref_gemm(a, w, norm_eps=1e-5, norm_w=nw), atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", list(range(9)))
 @pytest.mark.parametrize("M", [1, 333, 2048])
 def test_gemm_residual_inplace(cfg, M):
     K, N = 1536, 576
@@ -224,7 +224,7 @@ def test_gemm_residual_inplace(cfg, M):
     torch.testing.assert_close(x.float(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", list(range(9)))
 @pytest.mark.parametrize("M", [5, 640])
 def test_gemm_swiglu_norm(cfg, M):
     K, I = 576, 1536
@@ -246,3 +246,28 @@ def test_gemm_strided_a_and_bad_shapes():
     torch.testing.assert_close(ops.gemm(a, w).float(), ops.ref_gemm(a, w), atol=5e-2, rtol=2e-2)
     with pytest.raises(ValueError):
         ops.gemm(_bf(4, 100), _bf(64, 100))
+
+
+@pytest.mark.parametrize("cfg", [1, 3, 5])
+@pytest.mark.parametrize("M", [1, 77, 1000])
+def test_gemm_qkv_rope_matches_unfused(cfg, M):
+    nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, 1024, 192, 576, 75
+    x = _bf(M, K, seed=51)
+    w = _bf((nh + 2 * nkv) * D, K, scale=K ** -0.5, seed=52)
+    g = torch.Generator(device="cpu").manual_seed(53)
+    pos = torch.randint(0, Lmax, (M,), generator=g, dtype=torch.int32).to(DEV)
+    slot = torch.randperm(S, generator=g)[:M].to(torch.int32).to(DEV)
+    cs = ops.rope_table(p0 + Lmax + 1, D, 100000.0, DEV)
+    caches = []
+    for fused in (True, False):
+        kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
+        vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=DEV)
+        q = torch.zeros(M, nh, D, dtype=torch.bfloat16, device=DEV)
+        if fused:
+            ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, p0, cfg=cfg)
+        else:
+            qkv = ops.gemm(x, w, norm_eps=1e-5, cfg=cfg)
+            ops.rope_qkv_cache(qkv, pos, slot, cs, q, kc, vt, nh, nkv, D, p0)
+        caches.append((q, kc, vt))
+    for a, b in zip(*caches):
+        torch.testing.assert_close(a.float(), b.float(), atol=1e-2, rtol=1e-2)

@@ -56,7 +56,9 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(uint16_t, b);
 }
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
+// x·sigmoid(x) with the hardware reciprocal (v_rcp_f32, ~1 ulp): an IEEE division
+// is a ~10-instruction sequence and dominated the SwiGLU epilogue's VALU count
+__device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
 
 // ---- staging: async global → LDS DMA (global_load_lds_dwordx4).  One wave
 // instruction writes 1 KiB = 8 rows × 128 B lane-linearly (lane l → row l>>3,
@@ -111,7 +113,9 @@ __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], 
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        // C^T tile (W rows x A rows): lane holds C[m = lane & 15][n = 4·(lane>>4) + r],
+        // 4 consecutive output columns -> one 8-byte LDS write in the epilogue
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       // RMSNorm: the A fragment already holds 8 k-values of row (lane & 15) —
       // accumulate their squares (v_dot2_f32_bf16) in the MFMA shadow
       if constexpr (NORM) ss[i] = sumsq_frag(af[i], ss[i]);
@@ -136,13 +140,10 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   constexpr int TILE = (BM + BN) * BK;        // one stage (A + B) in elements
   constexpr int NI = (BM + BN) / 32;          // glds instructions per stage per wave
   static_assert(ST >= 2 && ST <= 4, "pipeline stages");
-  static_assert(BM * CST * 2 + BM * 4 <= ST * TILE * 2, "C staging + row scales fit in the K-loop buffers");
+  static_assert(BM * CST <= ST * TILE, "C staging fits in the K-loop buffers");
 
   // ONE __shared__ array (a second one makes hipcc wait vmcnt(0) before ds_reads)
-  // the row scales are written after the K loop, into the tail of the (then free)
-  // stage buffers, beyond the C staging tile
   __shared__ __attribute__((aligned(16))) uint16_t smem[ST * TILE];
-  float* rs = reinterpret_cast<float*>(smem + ST * TILE) - BM;
 
   // ---- XCD-aware, bijective tile assignment: the blocks of one XCD (orig % 8)
   // get a contiguous range of tiles, so tiles that share A rows share an L2
@@ -190,45 +191,50 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
     cur = cur + 1 == ST ? 0 : cur + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-loads ...
-  __syncthreads();  // ... of EVERY wave have landed before rs / the C tile reuse the buffers
+  __syncthreads();  // ... of EVERY wave have landed before the C tile reuses the buffers
 
-  // ---- row scales (RMSNorm): lanes l, l^16, l^32, l^48 hold the 4 k-quarters of row l&15
-  if constexpr (NORM) {
+  // ---- row scales (RMSNorm): lanes l, l^16, l^32, l^48 hold the 4 k-quarters of
+  // row l&15 — which is also the output row this lane holds (C^T layout), so the
+  // scale never leaves registers
+  float rsv[FM];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
+  for (int i = 0; i < FM; ++i) {
+    rsv[i] = 1.f;
+    if constexpr (NORM) {
       float v = ss[i];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
-      if (lane < 16 && (wave % WN) == 0) rs[wm0 + i * 16 + lane] = rsqrtf(v / (float)K + eps);
+      rsv[i] = rsqrtf(v / (float)K + eps);
     }
   }
-  __syncthreads();
 
-  // ---- epilogue 1: fragments -> bf16 tile in LDS (the K-loop buffers are free now)
+  // ---- epilogue 1: fragments -> bf16 tile in LDS (the K-loop buffers are free now).
+  // Lane holds rows m = wm0 + 16i + (lane & 15), columns n0' + 4·(lane>>4) + r.
   uint16_t* Cs = smem;
-  const int r_base = wm0 + (lane >> 4) * 4;
-  const int c_lane = lane & 15;
+  const int m_lane = lane & 15;
+  const int c4 = (lane >> 4) * 4;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    float sc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sc[r] = NORM ? rs[r_base + i * 16 + r] : 1.f;
+    const int row = wm0 + i * 16 + m_lane;
+    const float sc = rsv[i];
     if constexpr (EPI == 2) {
 #pragma unroll
       for (int j = 0; j < FN; j += 2) {
-        const int col = (wn0 >> 1) + (j >> 1) * 16 + c_lane;
+        const int col = (wn0 >> 1) + (j >> 1) * 16 + c4;
+        float h[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = acc[i][j][r] * sc[r], u = acc[i][j + 1][r] * sc[r];
-          Cs[(r_base + i * 16 + r) * CST + col] = f2bf(silu(g) * u);
-        }
+        for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][j][r] * sc) * (acc[i][j + 1][r] * sc);
+        *reinterpret_cast<uint2*>(Cs + row * CST + col) =
+            make_uint2((uint32_t)f2bf(h[0]) | ((uint32_t)f2bf(h[1]) << 16),
+                       (uint32_t)f2bf(h[2]) | ((uint32_t)f2bf(h[3]) << 16));
       }
     } else {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int col = wn0 + j * 16 + c_lane;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Cs[(r_base + i * 16 + r) * CST + col] = f2bf(acc[i][j][r] * sc[r]);
+        const int col = wn0 + j * 16 + c4;
+        *reinterpret_cast<uint2*>(Cs + row * CST + col) =
+            make_uint2((uint32_t)f2bf(acc[i][j][0] * sc) | ((uint32_t)f2bf(acc[i][j][1] * sc) << 16),
+                       (uint32_t)f2bf(acc[i][j][2] * sc) | ((uint32_t)f2bf(acc[i][j][3] * sc) << 16));
       }
     }
   }

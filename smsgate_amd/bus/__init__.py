@@ -8,8 +8,9 @@
   (single process owns the directory);
 * ``tcp://host:port`` / ``unix:///path.sock`` — :class:`RemoteBus` client of a
   ``python -m smsgate_amd bus-server`` broker process;
-* ``nats://…`` — only if ``nats-py`` is importable (it is not on the MI355X
-  image); raises a clear error otherwise.
+* ``nats://host:port`` — :class:`~.nats_client.NatsBus`: the NATS wire protocol +
+  JetStream API (no nats-py needed), against a real ``nats-server`` or our broker's
+  NATS front-end (``bus-server --nats-listen``).
 """
 from __future__ import annotations
 
@@ -78,12 +79,10 @@ async def _open(dsn: str, max_age: float) -> Bus:
         from .client import RemoteBus
 
         return await RemoteBus.connect(dsn)
-    if scheme in ("nats", "tls"):
-        try:
-            from .nats_adapter import NatsBus
-        except ImportError as exc:  # pragma: no cover - nats-py absent on the image
-            raise BusError("nats:// requires nats-py, which is not installed") from exc
-        return await NatsBus.connect(dsn)
+    if scheme == "nats":
+        from .nats_client import connect_nats
+
+        return await connect_nats(dsn)
     if scheme in ("redis", "rediss"):
         # The reference's stale default (config.py:27) — treat as in-process.
         return MemoryBus(max_age=max_age)

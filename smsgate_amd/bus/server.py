@@ -148,7 +148,9 @@ class BusServer:
 
 
 async def serve(listen: str, data_dir: Optional[str], stop: Optional[asyncio.Event] = None,
-                max_age: float = 3 * 24 * 3600.0) -> BusServer:
+                max_age: float = 3 * 24 * 3600.0, nats_listen: Optional[str] = None) -> BusServer:
+    """One journaled engine behind the msgpack protocol (``listen``) and, optionally,
+    the NATS wire protocol (``nats_listen``, :mod:`.nats_server`)."""
     if data_dir:
         from .filelog import open_file_bus
 
@@ -157,7 +159,17 @@ async def serve(listen: str, data_dir: Optional[str], stop: Optional[asyncio.Eve
         bus = MemoryBus(max_age=max_age)
     server = BusServer(bus)  # type: ignore[arg-type]
     await server.start(listen)
+    nats_fe = None
+    if nats_listen:
+        from .nats_server import NatsFrontend
+
+        u = urlparse(nats_listen)
+        nats_fe = NatsFrontend(bus)  # type: ignore[arg-type]
+        port = await nats_fe.start(u.hostname or "0.0.0.0", u.port or 4222)
+        log.info("NATS protocol front-end on %s:%d", u.hostname, port)
     if stop is not None:
         await stop.wait()
+        if nats_fe is not None:
+            await nats_fe.close()
         await server.close()
     return server

@@ -152,7 +152,7 @@ async def _run_notifier(a, settings) -> None:
 async def _run_bus_server(a, settings) -> None:
     from .bus.server import serve
 
-    await serve(a.listen, a.data, _stop_event(), max_age=settings.stream_max_age_s)
+    await serve(a.listen, a.data, _stop_event(), max_age=settings.stream_max_age_s, nats_listen=a.nats_listen)
 
 
 async def _run_pipeline(a, settings) -> None:
@@ -258,7 +258,8 @@ def build_parser() -> argparse.ArgumentParser:
     rp.add_argument("--cache", default=".hookdeck_cache.sqlite")
     rp.add_argument("--port", type=int, default=0)
     bp = sp.add_parser("bus-server")
-    bp.add_argument("--listen", default="tcp://0.0.0.0:4222")
+    bp.add_argument("--listen", default="tcp://0.0.0.0:4223", help="msgpack protocol (tcp:// or unix://)")
+    bp.add_argument("--nats-listen", default="tcp://0.0.0.0:4222", help="NATS wire protocol ('' = off)")
     bp.add_argument("--data", default="./.bus-data")
     ep = sp.add_parser("engine-server")
     ep.add_argument("--listen", default="unix:///tmp/smsgate-engine0.sock")

@@ -799,25 +799,34 @@ __global__ void __launch_bounds__(64) attn_decode_st_kernel(
 // only the row's own keys.  Both use the transposed formulation of
 // attn_decode_st_kernel (S^T = K·Q^T, O^T = V^T·P^T; one query per lane column).
 // ---------------------------------------------------------------------------
-template <bool PRE>
+// `full` = false: only the first 16 keys of the tile can be valid (the sequence
+// ends in the first half) -> the second half's K rows / V^T pieces are not read
+// (zeros; their scores are masked), i.e. 16-key granularity on the last tile.
 __device__ __forceinline__ void st_load_tile(const uint16_t* __restrict__ kb, const uint16_t* __restrict__ vb, int kt,
-                                             int g4, int r16, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
+                                             int g4, int r16, bool full, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
   constexpr int D = 64;
 #pragma unroll
-  for (int hs = 0; hs < 2; ++hs) {
-    const int key = kt + 16 * hs + r16;
+  for (int s2 = 0; s2 < 2; ++s2)
+    kv[0][s2] = *reinterpret_cast<const uint4*>(kb + (size_t)(kt + r16) * D + 8 * g4 + 32 * s2);
+  const int k_lo = kt + 4 * g4, k_hi = kt + 16 + 4 * g4;
+  uint2 lo[4], hi[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+    lo[n] = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_lo >> 3) * D + 16 * n + r16) * 8 + (k_lo & 7));
+  if (full) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
-      kv[hs][s2] = *reinterpret_cast<const uint4*>(kb + (size_t)key * D + 8 * g4 + 32 * s2);
-  }
-  const int k_lo = kt + 4 * g4, k_hi = kt + 16 + 4 * g4;
+      kv[1][s2] = *reinterpret_cast<const uint4*>(kb + (size_t)(kt + 16 + r16) * D + 8 * g4 + 32 * s2);
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int dim = 16 * n + r16;
-    const uint2 lo = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_lo >> 3) * D + dim) * 8 + (k_lo & 7));
-    const uint2 hi = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_hi >> 3) * D + dim) * 8 + (k_hi & 7));
-    vv[n] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    for (int n = 0; n < 4; ++n)
+      hi[n] = *reinterpret_cast<const uint2*>(vb + ((size_t)(k_hi >> 3) * D + 16 * n + r16) * 8 + (k_hi & 7));
+  } else {
+    kv[1][0] = kv[1][1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) hi[n] = make_uint2(0, 0);
   }
+#pragma unroll
+  for (int n = 0; n < 4; ++n) vv[n] = make_uint4(lo[n].x, lo[n].y, hi[n].x, hi[n].y);
 }
 
 // One 32-key tile of the transposed online softmax (state per lane = its query).
@@ -899,7 +908,7 @@ __global__ void __launch_bounds__(64) attn_prefix_kernel(const uint16_t* __restr
   float m = -INFINITY, lsum = 0.f;
   for (int kt = 0; kt < P0pad; kt += 32) {
     uint4 kc[2][2], vc[4];
-    st_load_tile<true>(kb, vb, kt, g4, r16, kc, vc);
+    st_load_tile(kb, vb, kt, g4, r16, kt + 16 < P0, kc, vc);
     st_tile(qb, kc, vc, kt, P0, g4, scale_log2, m, lsum, o);
   }
   if (valid) {
@@ -954,7 +963,7 @@ __global__ void __launch_bounds__(64) attn_own_kernel(
   // the other waves (a register ping-pong measured no faster and costs VGPRs)
   for (int kt = 0; kt < own; kt += 32) {
     uint4 kc[2][2], vc[4];
-    st_load_tile<false>(kself, vself, kt, g4, r16, kc, vc);
+    st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own, kc, vc);
     st_tile(qb, kc, vc, kt, own, g4, scale_log2, m, lsum, o);
   }
   if (r16 < G) {

@@ -51,6 +51,7 @@ def _args(argv=None):
     p.add_argument("--concurrency", type=int, default=4)
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
+    p.add_argument("--no-compact", action="store_true", help="disable decode row compaction")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args(argv)
 
@@ -88,7 +89,7 @@ def run_replica(args, rank: int, world: int, local: int):
                else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
     engine = build_engine(args.model, device=f"cuda:{local}", max_slots=args.max_slots,
                           steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
-                          buckets=buckets, fused_gemm=not args.no_fused_gemm)
+                          buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact)
     init_s = time.perf_counter() - t_init
     coord = Coordinator(engine, conns)
     coord.wait_all("ready")

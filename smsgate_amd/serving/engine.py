@@ -61,6 +61,7 @@ class EngineConfig:
     prefill_max_tokens: int = 32768
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
     fused_gemm: bool = True  # csrc/gemm_kernels.hip (norm prologue, residual/SwiGLU epilogues) vs hipBLASLt
+    compact: bool = True  # row compaction so the decode bucket tracks the active count
     decode_attn: str = "cascade"  # ops.attn_decode impl: cascade | mfma | mfma_v1 | valu
     lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
@@ -76,6 +77,8 @@ class EngineStats:
     decode_s: float = 0.0
     harvest_s: float = 0.0
     admit_s: float = 0.0
+    compactions: int = 0
+    rows_moved: int = 0
     completed: int = 0
 
     def as_dict(self) -> Dict[str, float]:
@@ -154,7 +157,8 @@ class ExtractionEngine:
         self.done = torch.ones(S, **i32)
         self.out_len = torch.zeros(S, **i32)
         self.out_buf = torch.zeros(S, self.max_out, **i32)
-        self.slot_id = torch.arange(S, **i32)
+        self.slot_id = torch.arange(S, **i32)  # row -> KV slot (rows are compacted, KV never moves)
+        self.slot_host = np.arange(S, dtype=np.int32)
         self.free_rows: List[int] = list(range(S))
         heapq.heapify(self.free_rows)
         self.active: Dict[int, Any] = {}
@@ -265,16 +269,18 @@ class ExtractionEngine:
         cu = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(lens, out=cu[1:])
         pos_np = np.arange(T, dtype=np.int32) - np.repeat(cu[:-1], lens)
-        slot_np = np.repeat(rows_np, lens)
+        seq_slots = self.slot_host[rows_np]
+        slot_np = np.repeat(seq_slots, lens)
         # one pinned staging copy for all small index arrays
-        meta = torch.from_numpy(np.concatenate([pos_np, slot_np, cu, rows_np, lens - 1])).pin_memory()
+        meta = torch.from_numpy(np.concatenate([pos_np, slot_np, cu, rows_np, lens - 1, seq_slots])).pin_memory()
         meta_d = meta.to(dev, non_blocking=True)
         o = 0
         pos_d = meta_d[o:o + T]; o += T
         slot_d = meta_d[o:o + T]; o += T
         cu_d = meta_d[o:o + n + 1]; o += n + 1
         rows_d = meta_d[o:o + n]; o += n
-        last_pos_d = meta_d[o:o + n]
+        last_pos_d = meta_d[o:o + n]; o += n
+        seq_slot_d = meta_d[o:o + n]
         qstart = torch.zeros(n, dtype=torch.int32, device=dev)
         x = F.embedding(torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True), self.w.embed).contiguous()
         max_q = int(lens.max())
@@ -286,7 +292,7 @@ class ExtractionEngine:
             return self.vt_cache[i]
 
         def attn(i, q, out):
-            ops.attn_prefill(q, cu_d, qstart, rows_d, max_q, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
+            ops.attn_prefill(q, cu_d, qstart, seq_slot_d, max_q, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
                              self.scale)
 
         h = self._forward(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
@@ -349,6 +355,42 @@ class ExtractionEngine:
             outs.append(self._decode_step(n, sample=False).float())
         self.done[:n] = 1
         return outs
+
+    def _compact(self) -> None:
+        """Move the highest active rows into the lowest free rows when a smaller decode
+        bucket would then cover every active row.  Only per-row state moves (token,
+        position, FSM state, flags, output buffer); the KV cache stays in its slot —
+        rows and slots swap their ``slot_id`` entries.  A row that finished in the
+        chunk still in flight is harvested from the next snapshot (done rows stay
+        done, their outputs move with them)."""
+        if not self.active:
+            return
+        target = self._bucket(len(self.active))
+        if self._bucket(max(self.active) + 1) <= target:
+            return
+        movers = sorted(r for r in self.active if r >= target)
+        free_low = sorted(r for r in self.free_rows if r < target)[: len(movers)]
+        if len(free_low) < len(movers):
+            return
+        dev = self.device
+        src = torch.tensor(movers, dtype=torch.long).pin_memory().to(dev, non_blocking=True)
+        dst = torch.tensor(free_low, dtype=torch.long).pin_memory().to(dev, non_blocking=True)
+        for t in (self.tok_buf, self.pos, self.state, self.done, self.out_len, self.out_buf):
+            t.index_copy_(0, dst, t.index_select(0, src))
+        s_src, s_dst = self.slot_id.index_select(0, src), self.slot_id.index_select(0, dst)
+        self.slot_id.index_copy_(0, dst, s_src)
+        self.slot_id.index_copy_(0, src, s_dst)
+        self.done.index_fill_(0, src, 1)
+        self.state.index_fill_(0, src, self.fsm.done_state)
+        m, f = np.asarray(movers), np.asarray(free_low)
+        self.slot_host[m], self.slot_host[f] = self.slot_host[f].copy(), self.slot_host[m].copy()
+        for a, b in zip(movers, free_low):
+            self.active[b] = self.active.pop(a)
+        taken = set(free_low)
+        self.free_rows = [r for r in self.free_rows if r not in taken] + movers
+        heapq.heapify(self.free_rows)
+        self.stats.compactions += 1
+        self.stats.rows_moved += len(movers)
 
     def _bucket(self, n: int) -> int:
         for b in self.cfg.buckets:
@@ -487,6 +529,8 @@ class ExtractionEngine:
         ``(key, answer dict)`` — or ``(key, int32 token array)`` with ``raw=True``
         (the remote-client path)."""
         t0 = time.perf_counter()
+        if self.cfg.compact:
+            self._compact()
         self._admit()
         self.stats.admit_s += time.perf_counter() - t0
         prev, self._pending = self._pending, None

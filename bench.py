@@ -42,9 +42,9 @@ def _args(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--backend", default="local_llm", choices=["local_llm", "fake", "regex"])
     p.add_argument("--model", default="smollm-135m")
-    p.add_argument("--msgs-per-step", type=int, default=8192)
-    p.add_argument("--max-slots", type=int, default=4096)
-    p.add_argument("--steps-per-graph", type=int, default=4)
+    p.add_argument("--msgs-per-step", type=int, default=16384)
+    p.add_argument("--max-slots", type=int, default=8192)
+    p.add_argument("--steps-per-graph", type=int, default=2)
     p.add_argument("--admit-frac", type=float, default=0.25)
     p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)

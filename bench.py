@@ -52,6 +52,8 @@ def _args(argv=None):
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
     p.add_argument("--no-compact", action="store_true", help="disable decode row compaction")
+    p.add_argument("--cpu-echo-engine", action="store_true",
+                   help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args(argv)
 
@@ -76,26 +78,38 @@ def run_replica(args, rank: int, world: int, local: int):
     # 2) GPU: device, RCCL group, engine
     import torch
 
-    torch.cuda.set_device(local)
+    echo = args.cpu_echo_engine
+    if not echo:
+        torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from smsgate_amd.parse.backends.local_llm import build_engine
+        if echo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     t_init = time.perf_counter()
-    buckets = (tuple(range(args.bucket_step, args.max_slots + 1, args.bucket_step)) if args.bucket_step
-               else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
-    engine = build_engine(args.model, device=f"cuda:{local}", max_slots=args.max_slots,
-                          steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
-                          buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact)
+    if echo:
+        from smsgate_amd.serving.echo import EchoEngine
+
+        engine = EchoEngine()
+    else:
+        from smsgate_amd.parse.backends.local_llm import build_engine
+
+        buckets = (tuple(range(args.bucket_step, args.max_slots + 1, args.bucket_step)) if args.bucket_step
+                   else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
+        engine = build_engine(args.model, device=f"cuda:{local}", max_slots=args.max_slots,
+                              steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
+                              buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact)
     init_s = time.perf_counter() - t_init
     coord = Coordinator(engine, conns)
     coord.wait_all("ready")
 
     def sync():
-        torch.cuda.synchronize()
+        if not echo:
+            torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
 
@@ -111,7 +125,7 @@ def run_replica(args, rank: int, world: int, local: int):
     coord.shutdown(procs)
     estats = engine.stats.as_dict()
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if echo else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         dist.destroy_process_group()
@@ -157,7 +171,7 @@ async def _run_cpu(args):
 def main(argv=None) -> int:
     args = _args(argv)
     rank, world, local = _rank_env()
-    if args.backend == "local_llm":
+    if args.backend == "local_llm" or args.cpu_echo_engine:
         dt, counts, init_s, estats = run_replica(args, rank, world, local)
     else:
         dt, counts, init_s, estats = asyncio.run(_run_cpu(args))
@@ -178,7 +192,8 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_MSGS_PER_S, 3),
             "dtype": "bf16",
-            "data": "synthetic (unique bank-SMS bodies; random-init extractor weights)",
+            "data": ("synthetic; CPU echo engine - harness check only, not a benchmark" if args.cpu_echo_engine
+                     else "synthetic (unique bank-SMS bodies; random-init extractor weights)"),
             "config": {
                 "model": (f"{args.model} extractor LLM (134.5M params, replaces the Gemini call)" if gpu
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),

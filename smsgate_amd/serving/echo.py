@@ -1,0 +1,53 @@
+"""CPU stand-in for :class:`~smsgate_amd.serving.engine.ExtractionEngine` with the
+same serving surface (``submit_ids`` / ``step(raw=True)`` / ``busy`` / ``stats``).
+
+Answers every prompt with the token ids of the fake backend's canned answer.
+Used to exercise the replica / distributed harness end to end without a GPU
+(``bench.py --cpu-echo-engine`` under ``torch.distributed.run`` with gloo, and
+the multi-process tests); it is never a fallback for the GPU engine.
+"""
+from __future__ import annotations
+
+from typing import Any, List, Sequence, Tuple
+
+import numpy as np
+
+__all__ = ["EchoEngine"]
+
+
+class _Stats:
+    def __init__(self) -> None:
+        self.completed = 0
+
+    def as_dict(self) -> dict:
+        return {"completed": self.completed}
+
+
+class EchoEngine:
+    def __init__(self, per_step: int = 300) -> None:
+        from ..models.tokenizer import load_tokenizer
+        from ..parse.backends.fake import DEFAULT_ANSWER
+        from .fsm import DEFAULT_FIELDS
+
+        tk = load_tokenizer()
+        toks: List[int] = []
+        for f in DEFAULT_FIELDS:
+            toks += tk.encode(DEFAULT_ANSWER[f.name]) + [tk.sep]
+        self.answer = np.asarray(toks, dtype=np.int32)
+        self.waiting: List[Tuple[Any, Sequence[int]]] = []
+        self.per_step = per_step
+        self.seen = 0
+        self.stats = _Stats()
+
+    def submit_ids(self, items) -> None:
+        self.waiting.extend(items)
+
+    def busy(self) -> bool:
+        return bool(self.waiting)
+
+    def step(self, raw: bool = True):
+        out = [(k, self.answer) for k, _ in self.waiting[: self.per_step]]
+        del self.waiting[: self.per_step]
+        self.seen += len(out)
+        self.stats.completed += len(out)
+        return out

@@ -51,3 +51,30 @@ def test_replica_two_workers_end_to_end():
     assert eng.seen < 600 and eng.seen > 300
     assert counts["ok"] > 0 and dt > 0
     assert all(not p.is_alive() for p in procs)
+
+
+def test_bench_two_ranks_torchrun_gloo(tmp_path):
+    """The bench's DP harness end to end on CPU: torch.distributed.run with 2 ranks
+    (gloo, 127.0.0.1), each rank a Coordinator + 2 spawned parser workers around the
+    CPU echo engine; barrier-bracketed timing, MAX over ranks, ONE JSON line."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--cpu-echo-engine", "--msgs-per-step", "256", "--cpu-workers", "2"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 512
+    assert out["value"] > 0 and out["steps"] == 2 and out["scaling"] == "weak"

@@ -100,7 +100,7 @@ def run_replica(args, rank: int, world: int, local: int):
 
         buckets = (tuple(range(args.bucket_step, args.max_slots + 1, args.bucket_step)) if args.bucket_step
                    else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
-        engine = build_engine(args.model, device=f"cuda:{local}", max_slots=args.max_slots,
+        engine = build_engine(args.model, device=f"cuda:{local}", random_init=True, max_slots=args.max_slots,
                               steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
                               buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact)
     init_s = time.perf_counter() - t_init

@@ -279,6 +279,13 @@ def build_parser() -> argparse.ArgumentParser:
     lg.add_argument("--cache", default="sms_cache.sqlite")
     lg.add_argument("--purchases", default="parsed_sms_cache.sqlite")
     lg.add_argument("--credits", default="credit_sms_cache.sqlite")
+    tr = sp.add_parser("train-extractor", help="train the local extractor LM on synthetic SMS (GPU)")
+    tr.add_argument("--model", default="smollm-135m")
+    tr.add_argument("--steps", type=int, default=1500)
+    tr.add_argument("--batch", type=int, default=64)
+    tr.add_argument("--lr", type=float, default=1e-3)
+    tr.add_argument("--examples", type=int, default=60000)
+    tr.add_argument("--out", required=True, help="safetensors path (LLM_CHECKPOINT for the local_llm backend)")
     sp.add_parser("config")
     return p
 
@@ -335,6 +342,13 @@ def main(argv: Optional[List[str]] = None) -> int:
         _db(a, settings)
     elif a.cmd == "legacy":
         asyncio.run(_legacy(a, settings))
+    elif a.cmd == "train-extractor":
+        from .models.train import TrainConfig, train_extractor
+
+        w = train_extractor(TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr,
+                                        n_examples=a.examples), device=settings.llm_device)
+        w.save(a.out)
+        print(f"saved {a.out}")
     return 0
 
 

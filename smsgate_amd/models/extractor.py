@@ -53,6 +53,9 @@ CONFIGS: Dict[str, ExtractorConfig] = {
     # same kernel-facing shapes family, small enough for CPU tests
     "tiny": ExtractorConfig(name="tiny", vocab=8192, hidden=128, layers=2, heads=4, kv_heads=2, head_dim=64,
                             inter=256),
+    # fast-to-train working extractor (tests, small deployments): 5M params
+    "small": ExtractorConfig(name="small", vocab=8192, hidden=256, layers=4, heads=4, kv_heads=2, head_dim=64,
+                             inter=704),
     # larger variant (SmolLM2-360M shape) for capacity experiments
     "smollm-360m": ExtractorConfig(name="smollm-360m", hidden=960, layers=32, heads=15, kv_heads=5, head_dim=64,
                                    inter=2560),
@@ -126,7 +129,8 @@ def _rms(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype) * w
 
 
-def reference_forward(w: ExtractorWeights, ids: torch.Tensor, compute_dtype=torch.float32) -> torch.Tensor:
+def reference_forward(w: ExtractorWeights, ids: torch.Tensor, compute_dtype=torch.float32,
+                      return_hidden: bool = False) -> torch.Tensor:
     """Full-sequence causal forward. ``ids``: [B, T] → logits [B, T, V] (fp32).
 
     Plain PyTorch (SDPA attention); differentiable, so it is also the training
@@ -153,4 +157,6 @@ def reference_forward(w: ExtractorWeights, ids: torch.Tensor, compute_dtype=torc
         g, u = (h @ w.gate_up[i].to(compute_dtype).t()).chunk(2, dim=-1)
         x = x + (F.silu(g) * u) @ w.down[i].to(compute_dtype).t()
     x = _rms(x, w.ln_f.to(compute_dtype), cfg.eps)
+    if return_hidden:  # final-normed hidden states (training computes logits on answer rows only)
+        return x
     return (x @ w.embed.to(compute_dtype).t()).float()

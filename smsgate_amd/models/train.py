@@ -1,0 +1,168 @@
+"""Supervised training of the extractor LM on synthetic SMS (fwd + bwd on MI355X).
+
+The reference never trains a model: it sends every SMS to Gemini
+(libs/gemini_parser.py:273-292).  The local backend replaces that call with
+our own extractor LM, and random-init weights only exercise
+its speed.  This module turns the LM into a working extractor.
+
+* data: :mod:`~smsgate_amd.utils.synth` bank SMS with ground-truth answers,
+  normalised exactly like the parse pipeline does before calling a backend
+  (:func:`~smsgate_amd.parse.text.normalize_body`); skipped kinds (OTP, …) never
+  reach the LLM and are not trained on;
+* sequence: ``<bos> SYSTEM_INSTRUCTION <sms> body <ans>`` followed by the
+  compact answer (9 field values, each ended by ``<sep>``): the exact token
+  stream the serving engine decodes.  Every target is checked against the
+  schema FSM (:mod:`~smsgate_amd.serving.fsm`), so the constrained decoder can
+  reproduce it;
+* loss: next-token cross-entropy on the answer positions only, over the decode
+  vocabulary (the tokenizer ids, the same rows the serving lm_head uses);
+* model: fp32 master weights, bf16 autocast, AdamW with warmup + cosine decay.
+  The differentiable forward is :func:`~smsgate_amd.models.extractor.reference_forward`
+  (PyTorch SDPA); serving uses the HIP kernels on the saved bf16 weights.
+"""
+from __future__ import annotations
+
+import math
+import random
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ..parse.schema import SYSTEM_INSTRUCTION
+from ..parse.text import normalize_body
+from .extractor import CONFIGS, ExtractorWeights, reference_forward
+from .tokenizer import ExtractorTokenizer, load_tokenizer
+
+__all__ = ["TrainConfig", "answer_tokens", "make_examples", "train_extractor", "field_accuracy"]
+
+
+@dataclass
+class TrainConfig:
+    model: str = "smollm-135m"
+    steps: int = 1500
+    batch: int = 64
+    lr: float = 1e-3
+    min_lr_frac: float = 0.05
+    warmup: int = 100
+    weight_decay: float = 0.01
+    n_examples: int = 60000
+    seed: int = 0
+    max_body_tokens: int = 128
+    log_every: int = 100
+
+
+def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]]) -> Optional[List[int]]:
+    """Compact answer token ids, or None if the schema FSM cannot emit them (over a
+    field's token cap, or a token outside the field's class)."""
+    ids: List[int] = []
+    for f in fsm.fields:
+        v = answer.get(f.name) or ""
+        ids += (tok.encode(v) if v else []) + [tok.sep]
+    state = fsm.start_state
+    for t in ids:
+        state = fsm.step_host(state, t)
+        if state < 0:
+            return None
+    return ids if state == fsm.done_state else None
+
+
+def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
+                  max_body: int = 128) -> List[Tuple[List[int], List[int]]]:
+    """``(message ids, answer ids)`` pairs (prefix excluded: it is shared)."""
+    from ..utils.synth import generate
+
+    out: List[Tuple[List[int], List[int]]] = []
+    items = [s for s in generate(n, seed=seed) if s.answer is not None]
+    msgs = tok.message_ids([normalize_body(s.body) for s in items], max_body)
+    for m, s in zip(msgs, items):
+        a = answer_tokens(tok, fsm, s.answer)
+        if a is not None:
+            out.append((m, a))
+    return out
+
+
+def _batch(prefix: List[int], exs: Sequence[Tuple[List[int], List[int]]], pad: int,
+           device) -> Tuple[torch.Tensor, torch.Tensor]:
+    seqs = [prefix + m + a for m, a in exs]
+    T = max(len(s) for s in seqs)
+    ids = torch.full((len(seqs), T), pad, dtype=torch.long)
+    labels = torch.full((len(seqs), T), -100, dtype=torch.long)
+    for i, ((m, a), s) in enumerate(zip(exs, seqs)):
+        ids[i, : len(s)] = torch.tensor(s)
+        start = len(prefix) + len(m)  # position of the first answer token
+        labels[i, start - 1: start - 1 + len(a)] = torch.tensor(a)  # predicted from the previous position
+    return ids.to(device), labels.to(device)
+
+
+def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] = print,
+                    tok: Optional[ExtractorTokenizer] = None) -> ExtractorWeights:
+    """Train and return **bf16** serving weights."""
+    from ..serving.fsm import build_fsm
+
+    tok = tok or load_tokenizer()
+    mcfg = CONFIGS[cfg.model]
+    v_dec = min(mcfg.vocab, (tok.vocab_size + 63) // 64 * 64)
+    fsm = build_fsm(tok, v_dec)
+    t0 = time.perf_counter()
+    data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens)
+    log(f"train: {len(data)} examples ({time.perf_counter() - t0:.1f}s), model {cfg.model}")
+    prefix = tok.prefix_ids(SYSTEM_INSTRUCTION)
+    torch.manual_seed(cfg.seed)
+    w = ExtractorWeights(mcfg, device=device, dtype=torch.float32, seed=cfg.seed)
+    decay = [p for n, p in w.named_parameters() if not n.startswith("ln")]
+    no_decay = [p for n, p in w.named_parameters() if n.startswith("ln")]
+    opt = torch.optim.AdamW([{"params": decay, "weight_decay": cfg.weight_decay},
+                             {"params": no_decay, "weight_decay": 0.0}], lr=cfg.lr, betas=(0.9, 0.95))
+
+    def lr_at(step: int) -> float:
+        if step < cfg.warmup:
+            return cfg.lr * (step + 1) / cfg.warmup
+        p = (step - cfg.warmup) / max(1, cfg.steps - cfg.warmup)
+        return cfg.lr * (cfg.min_lr_frac + (1 - cfg.min_lr_frac) * 0.5 * (1 + math.cos(math.pi * p)))
+
+    rng = random.Random(cfg.seed)
+    t0 = time.perf_counter()
+    for step in range(cfg.steps):
+        for g in opt.param_groups:
+            g["lr"] = lr_at(step)
+        ids, labels = _batch(prefix, rng.sample(data, cfg.batch), tok.pad, device)
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=str(device).startswith("cuda")):
+            h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True)
+            sel = labels.view(-1) >= 0
+            hs = h.reshape(-1, h.shape[-1])[sel]
+            logits = hs @ w.embed[:v_dec].t()
+            loss = F.cross_entropy(logits.float(), labels.view(-1)[sel])
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(w.parameters(), 1.0)
+        opt.step()
+        if cfg.log_every and (step % cfg.log_every == 0 or step == cfg.steps - 1):
+            log(f"step {step:5d} loss {loss.item():.4f} lr {lr_at(step):.2e} ({time.perf_counter() - t0:.1f}s)")
+    out = ExtractorWeights(mcfg, device=device, dtype=torch.bfloat16, seed=None)
+    with torch.no_grad():
+        for (n, p), (_, q) in zip(out.named_parameters(), w.named_parameters()):
+            p.copy_(q.to(torch.bfloat16))
+    out.requires_grad_(False)
+    return out
+
+
+def field_accuracy(predicted: Sequence[Optional[Dict[str, Optional[str]]]],
+                   expected: Sequence[Dict[str, Optional[str]]]) -> Dict[str, float]:
+    """Exact-match rate per field and for whole answers."""
+    fields = list(expected[0].keys()) if expected else []
+    hits = {f: 0 for f in fields}
+    whole = 0
+    for p, e in zip(predicted, expected):
+        ok = True
+        for f in fields:
+            same = p is not None and (p.get(f) or "") == (e.get(f) or "")
+            hits[f] += same
+            ok &= same
+        whole += ok
+    n = max(1, len(expected))
+    res = {f: hits[f] / n for f in fields}
+    res["all"] = whole / n
+    return res

@@ -22,8 +22,20 @@ from .base import BackendError, ExtractResult, ParserBackend
 __all__ = ["LocalLLMBackend", "RemoteLLMBackend", "build_engine"]
 
 
+def bundled_checkpoint(model: str) -> Optional[str]:
+    """A trained checkpoint shipped with the package (``models/assets/extractor-<model>.safetensors``;
+    produced by ``python -m smsgate_amd train-extractor``), or None."""
+    from pathlib import Path
+
+    p = Path(__file__).resolve().parents[2] / "models" / "assets" / f"extractor-{model}.safetensors"
+    return str(p) if p.exists() else None
+
+
 def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
-                 seed: int = 0, **engine_kw: Any):
+                 seed: int = 0, random_init: bool = False, **engine_kw: Any):
+    """Engine for ``model``: weights from ``checkpoint``, else the bundled trained
+    checkpoint for that model if there is one, else random init (``random_init=True``
+    forces random weights: the throughput benchmark)."""
     import torch
 
     from ...models.extractor import CONFIGS, ExtractorWeights
@@ -34,6 +46,8 @@ def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, d
     dev = torch.device(device)
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
+    if checkpoint is None and not random_init:
+        checkpoint = bundled_checkpoint(model)
     if checkpoint:
         w = ExtractorWeights.load(checkpoint, cfg, device=dev)
     else:
@@ -53,6 +67,15 @@ class LocalLLMBackend(ParserBackend):
         self.engine_kw = dict(max_slots=max_slots, **engine_kw)
         self.max_batch = max_batch or max_slots
         self._worker = None
+        self._factory = None
+
+    @classmethod
+    def from_engine(cls, engine, max_batch: Optional[int] = None) -> "LocalLLMBackend":
+        """Serve an already-built :class:`~smsgate_amd.serving.engine.ExtractionEngine`
+        (e.g. freshly trained weights) through the backend interface."""
+        be = cls(max_slots=engine.cfg.max_slots, max_batch=max_batch)
+        be._factory = lambda: engine
+        return be
 
     async def start(self) -> None:
         if self._worker is not None:
@@ -61,7 +84,8 @@ class LocalLLMBackend(ParserBackend):
 
         from ...serving.worker import EngineWorker
 
-        w = EngineWorker(lambda: build_engine(self.model, self.checkpoint, self.device, **self.engine_kw))
+        w = EngineWorker(self._factory or (lambda: build_engine(self.model, self.checkpoint, self.device,
+                                                                **self.engine_kw)))
         await asyncio.to_thread(w.start)
         self._worker = w
 

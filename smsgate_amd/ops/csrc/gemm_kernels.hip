@@ -165,9 +165,9 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  // ---- K loop, ST-stage pipeline: the DMAs of tiles kt+1 .. kt+ST-1 are in flight
+  // ---- K loop, ST-stage pipeline: the DMAs of the next ST-1 tiles are in flight
   // while tile kt is multiplied.  The wait is a constant counted vmcnt (this
-  // wave's NI·(ST-1) newest DMAs may stay outstanding): past the last tile the
+  // wave's newest NI·(ST-1) resp. NI·(ST-2) DMAs may stay outstanding): past the last tile the
   // issue slot re-loads tile KT-1 into the idle buffer (never read) so the count
   // stays exact.  Raw s_barrier: a __syncthreads() would drain the DMA queue.
   const int KT = K / BK;
@@ -178,17 +178,33 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
     issue_tile<BN>(W, K, n0, N - 1, kk, smem + s0 * TILE + BM * BK, wave, lane);
   }
   int cur = 0;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int nb = cur == 0 ? ST - 1 : cur - 1;  // buffer of tile kt + ST - 1 == (kt - 1) % ST
-    const int kk = min(kt + ST - 1, KT - 1) * BK;
-    issue_tile<BM>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
-    issue_tile<BN>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (ST - 1)) : "memory");  // tile kt landed (this wave's part)
-    __builtin_amdgcn_s_barrier();                                          // ... and every wave's part
-    mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+  if constexpr (ST == 2) {
+    for (int kt = 0; kt < KT; ++kt) {
+      const int nb = cur ^ 1;  // buffer of tile kt + 1 == (kt - 1) % 2
+      const int kk = min(kt + 1, KT - 1) * BK;
+      issue_tile<BM>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+      issue_tile<BN>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // tile kt landed (this wave's part)
+      __builtin_amdgcn_s_barrier();                               // ... and every wave's part
+      mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled by the next issue
+      cur ^= 1;
+    }
+  } else {
+    // >= 3 stages: ONE barrier per K-step.  Tile kt+ST-1 is issued after the barrier
+    // into the buffer of tile kt-1, which every wave has finished reading by then.
+    for (int kt = 0; kt < KT; ++kt) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (ST - 2)) : "memory");  // tile kt landed (this wave)
+      __builtin_amdgcn_s_barrier();                                          // ... every wave; kt-1 read
+      const int nb = cur == 0 ? ST - 1 : cur - 1;  // buffer of tile kt + ST - 1 == (kt - 1) % ST
+      const int kk = min(kt + ST - 1, KT - 1) * BK;
+      issue_tile<BM>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+      issue_tile<BN>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
+      mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+      cur = cur + 1 == ST ? 0 : cur + 1;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled by the next issue
-    cur = cur + 1 == ST ? 0 : cur + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-loads ...
   __syncthreads();  // ... of EVERY wave have landed before the C tile reuses the buffers

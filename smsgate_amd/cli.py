@@ -305,9 +305,16 @@ def main(argv: Optional[List[str]] = None) -> int:
         from .obs.errors import init_sentry
         from .services.gateway import create_app
 
+        from .services.tunnel import open_tunnel
+
         init_sentry(release="api_gateway@0.1.0")
-        uvicorn.run(create_app(log_dir=settings.log_dir), host=settings.api_host or "0.0.0.0",
-                    port=int(settings.api_port or 9001))
+        port = int(settings.api_port or 9001)
+        tunnel = open_tunnel(settings, port)
+        try:
+            uvicorn.run(create_app(log_dir=settings.log_dir), host=settings.api_host or "0.0.0.0", port=port)
+        finally:
+            if tunnel is not None:
+                tunnel.close()
     elif a.cmd == "parser":
         asyncio.run(_run_parser(a, settings))
     elif a.cmd == "writer":

@@ -41,7 +41,7 @@ def _future(dt: datetime) -> bool:
 class WriterService:
     def __init__(self, bus: Bus, sinks: Sequence[Sink], *, durable: str = "pb_writer", batch: int = 128,
                  retry_attempts: int = 5, retry_min: float = 1.0, retry_max: float = 20.0,
-                 stats_interval: float = 1.0) -> None:
+                 stats_interval: float = 1.0, ack_wait: float = 30.0) -> None:
         self.bus = bus
         self.sinks = list(sinks)
         self.ok = 0
@@ -49,7 +49,7 @@ class WriterService:
         self.skipped = 0
         self._upsert = retry(attempts=retry_attempts, wait_min=retry_min, wait_max=retry_max)(self._upsert_all)
         self.stage = Stage(bus, SUBJECT_PARSED, durable, self.handle_batch, batch=batch,
-                           stats_interval=stats_interval, on_stats=lambda p, a: M.WRITER_LAG.set(p),
+                           stats_interval=stats_interval, ack_wait=ack_wait, on_stats=lambda p, a: M.WRITER_LAG.set(p),
                            name="pb_writer")
 
     async def _upsert_all(self, records: Sequence[ParsedSMS]) -> None:

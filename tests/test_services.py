@@ -391,3 +391,35 @@ def test_cli_db_roundtrip(tmp_path, capsys):
     main(["db", "current", "--url", url])
     out = capsys.readouterr().out.split()
     assert "0002_sms_indexes" in out[-2] or "0002_sms_indexes" in out
+
+
+# --------------------------------------------------------------------------- ngrok tunnel
+def test_tunnel_disabled_sdk_and_missing(monkeypatch):
+    import sys
+    import types
+
+    from smsgate_amd.config import Settings
+    from smsgate_amd.services import tunnel
+
+    assert tunnel.open_tunnel(Settings.load({}, env_file=None), 9001) is None
+    calls = []
+
+    class _Listener:
+        def url(self):
+            return "https://x.ngrok.app"
+
+    fake = types.ModuleType("ngrok")
+    fake.forward = lambda port, **kw: (calls.append((port, kw)), _Listener())[1]
+    fake.disconnect = lambda url: calls.append(("disconnect", url))
+    monkeypatch.setitem(sys.modules, "ngrok", fake)
+    s = Settings.load({"ENABLE_NGROK": "true", "NGROK_AUTHTOKEN": "tok", "NGROK_DOMAIN": "d.ngrok.app"},
+                      env_file=None)
+    t = tunnel.open_tunnel(s, 9001)
+    assert t.url == "https://x.ngrok.app"
+    assert calls[0] == (9001, {"authtoken": "tok", "domain": "d.ngrok.app"})
+    t.close()
+    assert calls[-1] == ("disconnect", "https://x.ngrok.app")
+    monkeypatch.delitem(sys.modules, "ngrok")
+    monkeypatch.setattr(tunnel.shutil, "which", lambda name: None)
+    monkeypatch.setitem(sys.modules, "ngrok", None)  # import ngrok -> ImportError
+    assert tunnel.open_tunnel(s, 9001) is None

@@ -121,6 +121,15 @@ def main():
         res[f"fgemm_{name}_TFLOPs"] = round(2 * B * n * k / (best * 1e-6) / 1e12, 1)
     Xl, Wl = rnd(B, H), rnd(8192, H)
     res["gemm_lm_head_8192"] = timeit(lambda: F.linear(Xl, Wl))
+    # QKV projection + RoPE + KV scatter: fused epilogue vs GEMM + separate kernel
+    Xq, Wq = rnd(B, H), rnd(cfg.qkv_out, H)
+    qo = torch.empty(B, nh, D, dtype=bf, device=dev)
+    for c in (1, 3, 5):
+        res[f"qkv_rope_fused_cfg{c}"] = timeit(lambda: ops.gemm_qkv_rope(Xq, Wq, 1e-5, pos, slot, cs, qo, kc, vt, nh, nkv,
+                                                                          P0, cfg=c))
+    res["qkv_rope_fused_auto"] = timeit(lambda: ops.gemm_qkv_rope(Xq, Wq, 1e-5, pos, slot, cs, qo, kc, vt, nh, nkv, P0))
+    res["qkv_rope_split"] = timeit(lambda: ops.rope_qkv_cache(ops.gemm(Xq, Wq, norm_eps=1e-5), pos, slot, cs, qo, kc, vt,
+                                                               nh, nkv, D, P0))
     fused_layer = (res["rope_qkv_cache"] + res["attn_decode_cascade"] + res["fgemm_qkv_auto"] + res["fgemm_o_auto"]
                    + res["fgemm_gate_up_auto"] + res["fgemm_down_auto"])
     res["fused_sum_per_layer_us"] = round(fused_layer, 1)

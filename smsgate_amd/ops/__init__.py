@@ -235,7 +235,9 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
     if M == 0:
         return
     if cfg is None:
-        cfg = 1 if -(-M // 128) * (w.shape[0] // 64) >= 480 else 3
+        # 64x64 tiles: the V^T scatter of the epilogue favours more, smaller tiles
+        # (kbench, B=4096/8192: 17.8/27.6 us vs 22.0/31.3 us with 128x64)
+        cfg = 3
     rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
                                          _stream())

@@ -75,21 +75,30 @@ def _truncate(v: Any, limit: int = 4096) -> Any:
     return v
 
 
-def sentry_capture(exc: BaseException, *, extras: Optional[Dict[str, Any]] = None) -> None:
-    event = {
-        "ts": time.time(),
+def _render(raw: Dict[str, Any]) -> Dict[str, Any]:
+    exc: BaseException = raw["exc"]
+    return {
+        "ts": raw["ts"],
         "type": type(exc).__name__,
         "message": _truncate(str(exc)),
-        "extras": {k: _truncate(v) for k, v in (extras or {}).items()},
+        "extras": {k: _truncate(v) for k, v in (raw["extras"] or {}).items()},
         "traceback": "".join(traceback.format_exception(type(exc), exc, exc.__traceback__))[-4096:],
     }
+
+
+def sentry_capture(exc: BaseException, *, extras: Optional[Dict[str, Any]] = None) -> None:
+    """Record ``exc``.  Cheap on the hot path (the parser reports every failed
+    message): the exception and extras are kept as-is in the bounded ring and
+    rendered (message, truncation, traceback) only when read — or written at once
+    when ``SMSGATE_ERROR_LOG`` asks for a durable log."""
+    raw = {"ts": time.time(), "exc": exc, "extras": dict(extras) if extras else None}
     with _lock:
-        _ring.append(event)
-    path = os.getenv("SMSGATE_ERROR_LOG")
+        _ring.append(raw)
+    path = os.environ.get("SMSGATE_ERROR_LOG")
     if path:
         try:
             with open(path, "a", encoding="utf-8") as f:
-                f.write(json.dumps(event, default=str, ensure_ascii=False) + "\n")
+                f.write(json.dumps(_render(raw), default=str, ensure_ascii=False) + "\n")
         except OSError:  # pragma: no cover
             pass
     sdk = _sdk
@@ -102,7 +111,8 @@ def sentry_capture(exc: BaseException, *, extras: Optional[Dict[str, Any]] = Non
 
 def recent_errors(n: int = 100) -> List[Dict[str, Any]]:
     with _lock:
-        return list(_ring)[-n:]
+        raw = list(_ring)[-n:]
+    return [_render(r) for r in raw]
 
 
 def clear_errors() -> None:

@@ -67,6 +67,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_attn_decode_v1.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_v1.restype = _c_int
     lib.sg_attn_decode_cascade.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_vp, _vp, _vp]
+    lib.sg_attn_decode_grouped.argtypes = lib.sg_attn_decode.argtypes
+    lib.sg_attn_decode_grouped.restype = _c_int
     lib.sg_attn_decode_cascade.restype = _c_int
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
@@ -309,6 +311,8 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
     ``impl="cascade"`` (default): shared-prefix pass over 16 query rows per wave +
     own-key pass seeded with the exact prefix softmax state; ``scratch`` =
     ``(pre_o [>=B, nh, D] fp32, pre_lse [>=B, nh] fp32)`` (allocated if omitted).
+    ``"grouped"``: 16/G sequences per wave, the shared prefix multiplied once for
+    all of them, then each sequence's own keys with per-column masks (no scratch);
     ``"mfma"``: single-pass transposed MFMA kernel (S^T = K·Q^T, O^T = V^T·P^T);
     ``"mfma_v1"``: S = Q·K^T with P through LDS; ``"valu"``: vector-ALU variant —
     kept for A/B measurement.  MFMA kernels need ``Lmax``, padded prefix % 32 == 0."""
@@ -331,7 +335,8 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
                                         _p(pre_lse), _stream())
         _check(rc, "attn_decode[cascade]")
         return out
-    fn = {"mfma": lib.sg_attn_decode, "mfma_v1": lib.sg_attn_decode_v1, "valu": lib.sg_attn_decode_valu}[impl]
+    fn = {"mfma": lib.sg_attn_decode, "mfma_v1": lib.sg_attn_decode_v1, "valu": lib.sg_attn_decode_valu,
+          "grouped": lib.sg_attn_decode_grouped}[impl]
     _check(fn(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B,
               nh, nkv, D, Lmax, scale, _stream()), f"attn_decode[{impl}]")
     return out

@@ -832,7 +832,7 @@ __device__ __forceinline__ void st_load_tile(const uint16_t* __restrict__ kb, co
 // One 32-key tile of the transposed online softmax (state per lane = its query).
 __device__ __forceinline__ void st_tile(const bf16x8 (&qb)[2], const uint4 (&kc)[2][2], const uint4 (&vc)[4],
                                         int kt, int nval, int g4, float scale_log2, float& m, float& lsum,
-                                        f32x4 (&o)[4]) {
+                                        f32x4 (&o)[4], bool col_ok = true) {
   f32x4 st[2];
 #pragma unroll
   for (int hs = 0; hs < 2; ++hs) {
@@ -846,7 +846,9 @@ __device__ __forceinline__ void st_tile(const bf16x8 (&qb)[2], const uint4 (&kc)
   for (int hs = 0; hs < 2; ++hs)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const bool ok = (kt + 16 * hs + 4 * g4 + i) < nval;
+      // col_ok = false: this lane's query column does not own these keys (grouped
+      // kernel) -> -inf scores leave its softmax state (m, l, o) untouched
+      const bool ok = col_ok && (kt + 16 * hs + 4 * g4 + i) < nval;
       sv[hs][i] = ok ? st[hs][i] * scale_log2 : -INFINITY;
       tmax = fmaxf(tmax, sv[hs][i]);
     }
@@ -967,6 +969,76 @@ __global__ void __launch_bounds__(64) attn_own_kernel(
     st_tile(qb, kc, vc, kt, own, g4, scale_log2, m, lsum, o);
   }
   if (r16 < G) {
+    const float inv = 1.f / lsum;
+    uint16_t* orow = out + qrow * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[n][0] * inv) | ((uint32_t)f2bf(o[n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[n][2] * inv) | ((uint32_t)f2bf(o[n][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Grouped decode attention (production): one wave = SPW = 16 / G sequences of one
+// kv head.  MFMA column c <-> (sequence c / G, query head c % G).  The shared
+// prefix tiles are multiplied once for all 16 columns (15 useful at G = 3); then
+// each sequence's own tiles run with a per-column mask, so the other sequences'
+// softmax states are untouched.  vs the cascade pair: no fp32 scratch round
+// trip, one launch, prefix K/V read once per SPW sequences.
+// grid = (ceil(B / SPW), nkv), one wave.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) attn_grouped_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
+    uint16_t* __restrict__ out, int B, int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
+  const int G = nh / nkv, SPW = 16 / G;
+  const int b0 = blockIdx.x * SPW;
+  const int j = r16 / G, g = r16 % G;  // this lane's column: sequence j of the group, head g
+  const int bj = b0 + j;
+  const bool col_valid = j < SPW && bj < B && (done == nullptr || done[bj] == 0);
+  const size_t qrow = (size_t)(col_valid ? bj : 0) * nh + kh * G + g;
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);
+    if (!col_valid) v = make_uint4(0, 0, 0, 0);
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  // shared prefix: all columns
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+  for (int kt = 0; kt < P0; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
+    st_tile(qb, kc, vc, kt, P0, g4, scale_log2, m, lsum, o);
+  }
+  // own keys, one sequence at a time (wave-uniform loop; masked columns)
+  for (int jj = 0; jj < SPW; ++jj) {
+    const int b = b0 + jj;
+    if (b >= B) break;
+    if (done != nullptr && done[b]) continue;
+    const int own = pos[b] + 1;
+    const int sl = slot[b];
+    const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+    const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+    const bool mine = (j == jj);
+    for (int kt = 0; kt < own; kt += 32) {
+      uint4 kc[2][2], vc[4];
+      st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own, kc, vc);
+      st_tile(qb, kc, vc, kt, own, g4, scale_log2, m, lsum, o, mine);
+    }
+  }
+  if (col_valid) {
     const float inv = 1.f / lsum;
     uint16_t* orow = out + qrow * D;
 #pragma unroll
@@ -1144,6 +1216,19 @@ int sg_attn_decode_cascade(const void* q, const int* pos, const int* slot, const
   hipLaunchKernelGGL(attn_own_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, pos, slot, done,
                      (const uint16_t*)k_cache, (const uint16_t*)vt_cache, P0 > 0 ? (const float*)pre_o : nullptr,
                      (const float*)pre_lse, (uint16_t*)out, nh, nkv, Lmax, sl2);
+  return (int)hipGetLastError();
+}
+
+// Grouped decode attention: 16/G sequences per wave, shared prefix once (no scratch).
+int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                           const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B,
+                           int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+  const int spw = 16 / (nh / nkv);
+  hipLaunchKernelGGL(attn_grouped_kernel, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
+                     pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
   return (int)hipGetLastError();
 }
 

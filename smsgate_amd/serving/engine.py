@@ -62,7 +62,7 @@ class EngineConfig:
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
     fused_gemm: bool = True  # csrc/gemm_kernels.hip (norm prologue, residual/SwiGLU epilogues) vs hipBLASLt
     compact: bool = True  # row compaction so the decode bucket tracks the active count
-    decode_attn: str = "cascade"  # ops.attn_decode impl: cascade | mfma | mfma_v1 | valu
+    decode_attn: str = "grouped"  # ops.attn_decode impl: grouped | cascade | mfma | mfma_v1 | valu
     lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
 

@@ -121,7 +121,7 @@ def test_attn_prefill(P0):
         o += n
 
 
-@pytest.mark.parametrize("impl", ["cascade", "mfma", "mfma_v1", "valu"])
+@pytest.mark.parametrize("impl", ["grouped", "cascade", "mfma", "mfma_v1", "valu"])
 @pytest.mark.parametrize("P0", [0, 75])
 def test_attn_decode(P0, impl):
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224  # MFMA decode tiles need Lmax % 32 == 0

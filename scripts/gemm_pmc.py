@@ -1,4 +1,5 @@
-"""Driver for counter runs: the gate_up GEMM at B=4096 (fused SwiGLU+norm) and hipBLASLt."""
+"""Driver for counter runs: the gate_up GEMM (fused SwiGLU+norm) at batch B for the
+tile configs in CFGS, and hipBLASLt on the same shape."""
 import os
 import sys
 
@@ -9,10 +10,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from smsgate_amd import ops  # noqa: E402
 
 dev, bf = "cuda", torch.bfloat16
-X = torch.randn(4096, 576, device=dev).to(bf)
+B = int(os.environ.get("B", "4096"))
+X = torch.randn(B, 576, device=dev).to(bf)
 W = (torch.randn(3072, 576, device=dev) * 0.05).to(bf)
-for _ in range(10):
-    ops.gemm(X, W, epi="swiglu", norm_eps=1e-5, cfg=int(os.environ.get("CFG", "0")))
+for cfg in [int(c) for c in os.environ.get("CFGS", os.environ.get("CFG", "0")).split(",")]:
+    for _ in range(10):
+        ops.gemm(X, W, epi="swiglu", norm_eps=1e-5, cfg=cfg)
 for _ in range(10):
     F.linear(X, W)
 torch.cuda.synchronize()

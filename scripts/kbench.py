@@ -111,7 +111,7 @@ def main():
         kw = dict(epi=epi, norm_eps=1e-5 if norm else None, resid=R)
         best = None
         for c, (bm, bn) in ops.GEMM_TILES.items():
-            if n % bn:
+            if n % bn or (c in ops.GEMM_SWIGLU_ONLY and epi != "swiglu"):
                 continue
             t = timeit(lambda: ops.gemm(X, W, cfg=c, **kw))
             res[f"fgemm_{name}_cfg{c}"] = t

@@ -1,10 +1,17 @@
+# Counter passes for the gate_up GEMM (scripts/gemm_pmc.py); CFGS / B from the env.
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 python -m smsgate_amd.ops.build > gpurun_out/build.log 2>&1 || exit 1
 R=$GRAFT_REPO_ROOT
 cd /tmp
-timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/pmc/counters.txt 2>&1; echo "list rc=$?"
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d $R/gpurun_out/pmc -o p1 -- python $R/scripts/gemm_pmc.py > $R/gpurun_out/pmc/p1.log 2>&1; echo "p1 rc=$?"
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/pmc -o p2 -- python $R/scripts/gemm_pmc.py > $R/gpurun_out/pmc/p2.log 2>&1; echo "p2 rc=$?"
-ls -R $R/gpurun_out/pmc | head -30
+i=0
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES" \
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum" \
+           "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TA_BUSY_avr TCP_PENDING_STALL_CYCLES_sum" \
+           "TA_ADDR_STALLED_BY_TC_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d $R/gpurun_out/pmc -o q$i -- python $R/scripts/gemm_pmc.py > $R/gpurun_out/pmc/q$i.log 2>&1 || { echo "pass $i failed"; tail -5 $R/gpurun_out/pmc/q$i.log; exit 1; }
+done
+cd $R && python scripts/pmc_summary.py gpurun_out/pmc/q*_counter_collection.csv > gpurun_out/pmc/summary.txt && cat gpurun_out/pmc/summary.txt

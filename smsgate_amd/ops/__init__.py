@@ -77,6 +77,10 @@ def _declare(lib: ctypes.CDLL) -> None:
                             _c_float, _c_int, _vp]
     lib.sg_gemm_qkv_rope.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_float, _c_int, _ip, _ip, _vp, _vp, _vp,
                                      _vp, _c_int, _c_int, _c_int, _c_int, _vp]
+    lib.sg_gemm_probe.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]
+    lib.sg_gemm_probe.restype = _c_int
+    lib.sg_gemm_set_group_m.argtypes = [_c_int]
+    lib.sg_gemm_set_group_m.restype = None
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
@@ -157,7 +161,10 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 
 
 GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 64), 5: (64, 64), 6: (64, 64),
-              7: (128, 128), 8: (64, 128)}  # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines
+              7: (128, 128), 8: (64, 128), 9: (256, 128), 10: (256, 256), 11: (128, 256), 12: (256, 64),
+              13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64)}
+# cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages)
+GEMM_SWIGLU_ONLY = {10}  # a 256x256 plain-output tile does not fit the LDS staging
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
@@ -165,7 +172,8 @@ def gemm_cfg(M: int, N: int, min_tiles: int = 480) -> int:
     """Tile config for an M×N output: the biggest tile that still gives ≳2 blocks per CU
     (256 CUs), else the config with the most blocks."""
     best, best_tiles = -1, -1
-    for cfg, (bm, bn) in GEMM_TILES.items():
+    for cfg in range(9):  # the 4-wave configs; 8-wave ones are explicit opt-ins
+        bm, bn = GEMM_TILES[cfg]
         if N % bn:
             continue
         tiles = -(-M // bm) * (N // bn)
@@ -176,6 +184,11 @@ def gemm_cfg(M: int, N: int, min_tiles: int = 480) -> int:
     if best < 0:
         raise ValueError(f"gemm: N={N} is not a multiple of 64")
     return best
+
+
+def gemm_set_group_m(gm: int) -> None:
+    """Tile rasterisation of the fused GEMMs: M-tiles per group (1 = row-major)."""
+    load_library().sg_gemm_set_group_m(int(gm))
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Optional[float] = None,

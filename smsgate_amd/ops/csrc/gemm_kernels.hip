@@ -20,7 +20,7 @@
 //          16 matching up rows), so one lane holds gate and up of the same output
 //          element in two accumulators; C = silu(g)·u with Nout = N / 2.
 //
-// Tiling (cdna_hip_programming.md §5): 256 threads = 4 waves, BM×BN block tile,
+// Tiling (cdna_hip_programming.md §5): 4 or 8 waves, BM×BN block tile,
 // BK = 64, 16×16×32 bf16 MFMAs; A/W tiles staged global → registers → LDS,
 // double-buffered with one barrier per K-tile (the global loads of tile k+1 are
 // in flight while tile k is multiplied).  LDS rows are 128 B with a 16-byte-chunk
@@ -67,14 +67,14 @@ __device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcp
 // registers — nothing for the compiler to sink or spill (cdna_hip_programming.md §5).
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int ROWS>
+template <int ROWS, int NW>
 __device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ src, int ld, int r0, int rmax, int k0,
                                            uint16_t* dst, int wave, int lane) {
-  static_assert(ROWS % 32 == 0, "8-row pieces spread over 4 waves");
+  static_assert(ROWS % (8 * NW) == 0, "8-row pieces spread over the waves");
   const int rr = lane >> 3, p = lane & 7;
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i) {
-    const int g = wave + 4 * i;  // 8-row piece
+  for (int i = 0; i < ROWS / (8 * NW); ++i) {
+    const int g = wave + NW * i;  // 8-row piece
     const int row = 8 * g + rr;
     const int gr = min(r0 + row, rmax);  // rows past the end re-read the last row (never stored)
     const uint16_t* gp = src + (size_t)gr * ld + k0 + ((p ^ (row & 7)) << 3);
@@ -123,13 +123,17 @@ __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], 
   }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST>
-__global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restrict__ A, int lda,
+// PROBE (timing decomposition only, sg_gemm_probe): 1 = K-loop without MFMAs,
+// 2 = K-loop without the global->LDS loads (MFMAs on stale LDS), 3 = as 2 and no
+// prologue loads either, 4 = as 3 and no epilogue (nothing stored)
+template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST, int PROBE = 0>
+__global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t* __restrict__ A, int lda,
                                                          const uint16_t* __restrict__ W,
                                                          uint16_t* C, int ldc, const uint16_t* R, int ldr,
                                                          int M, int N, int K, float eps, int tiles_m,
-                                                         int tiles_n, RopeArgs ra) {
-  static_assert(WM * WN == 4, "4 waves");
+                                                         int tiles_n, int gm, RopeArgs ra) {
+  constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(EPI != 3 || BN == 64, "QKV+RoPE epilogue: one 64-wide head per N tile");
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   constexpr int FM = TM / 16, FN = TN / 16;  // MFMA tiles per wave
@@ -138,7 +142,7 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   constexpr int BNO = EPI == 2 ? BN / 2 : BN;  // output columns of the block
   constexpr int CST = BNO + 8;                // staged C row stride (elements), +16 B pad
   constexpr int TILE = (BM + BN) * BK;        // one stage (A + B) in elements
-  constexpr int NI = (BM + BN) / 32;          // glds instructions per stage per wave
+  constexpr int NI = (BM + BN) / (8 * NW);    // glds instructions per stage per wave
   static_assert(ST >= 2 && ST <= 4, "pipeline stages");
   static_assert(BM * CST <= ST * TILE, "C staging fits in the K-loop buffers");
 
@@ -150,8 +154,13 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   const int T = tiles_m * tiles_n;
   const int orig = blockIdx.x, xcd = orig & 7, q8 = T >> 3, r8 = T & 7;
   const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int m0 = (t / tiles_n) * BM;
-  const int n0 = (t % tiles_n) * BN;
+  // grouped rasterisation: runs of `gm` M-tiles walk N together, so the tiles in
+  // flight on an XCD (~64) cover a compact gm x (64/gm) patch of A rows x W rows
+  // that stays L2-resident (row-major order sweeps all of W per M-tile row)
+  const int gsz = gm * tiles_n, g = t / gsz, gl = t - g * gsz;
+  const int grows = min(gm, tiles_m - g * gm);
+  const int m0 = (g * gm + gl % grows) * BM;
+  const int n0 = (gl / grows) * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WN) * TM, wn0 = (wave % WN) * TN;
@@ -171,22 +180,29 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   // issue slot re-loads tile KT-1 into the idle buffer (never read) so the count
   // stays exact.  Raw s_barrier: a __syncthreads() would drain the DMA queue.
   const int KT = K / BK;
+  if constexpr (PROBE >= 3) {  // no loads at all: deterministic (zero) LDS operands
+    for (int i = tid * 8; i < ST * TILE; i += NT * 8) *reinterpret_cast<uint4*>(smem + i) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
 #pragma unroll
-  for (int s0 = 0; s0 < ST - 1; ++s0) {
+  for (int s0 = 0; s0 < (PROBE >= 3 ? 0 : ST - 1); ++s0) {
     const int kk = min(s0, KT - 1) * BK;
-    issue_tile<BM>(A, lda, m0, M - 1, kk, smem + s0 * TILE, wave, lane);
-    issue_tile<BN>(W, K, n0, N - 1, kk, smem + s0 * TILE + BM * BK, wave, lane);
+    issue_tile<BM, NW>(A, lda, m0, M - 1, kk, smem + s0 * TILE, wave, lane);
+    issue_tile<BN, NW>(W, K, n0, N - 1, kk, smem + s0 * TILE + BM * BK, wave, lane);
   }
   int cur = 0;
   if constexpr (ST == 2) {
     for (int kt = 0; kt < KT; ++kt) {
       const int nb = cur ^ 1;  // buffer of tile kt + 1 == (kt - 1) % 2
       const int kk = min(kt + 1, KT - 1) * BK;
-      issue_tile<BM>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
-      issue_tile<BN>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // tile kt landed (this wave's part)
-      __builtin_amdgcn_s_barrier();                               // ... and every wave's part
-      mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+      if constexpr (PROBE != 2) {
+        issue_tile<BM, NW>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+        issue_tile<BN, NW>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // tile kt landed (this wave's part)
+      }
+      __builtin_amdgcn_s_barrier();  // ... and every wave's part
+      if constexpr (PROBE != 1)
+        mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled by the next issue
       cur ^= 1;
@@ -199,8 +215,8 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
       __builtin_amdgcn_s_barrier();                                          // ... every wave; kt-1 read
       const int nb = cur == 0 ? ST - 1 : cur - 1;  // buffer of tile kt + ST - 1 == (kt - 1) % ST
       const int kk = min(kt + ST - 1, KT - 1) * BK;
-      issue_tile<BM>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
-      issue_tile<BN>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
+      issue_tile<BM, NW>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+      issue_tile<BN, NW>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
       mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
       cur = cur + 1 == ST ? 0 : cur + 1;
     }
@@ -208,6 +224,15 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-loads ...
   __syncthreads();  // ... of EVERY wave have landed before the C tile reuses the buffers
+  if constexpr (PROBE == 4) {
+    float keep = 0.f;  // every accumulator stays live (no dead MFMAs)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) keep += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3] + ss[i];
+    if (keep == 12345.f) C[tid] = 1;
+    return;
+  }
 
   // ---- row scales (RMSNorm): lanes l, l^16, l^32, l^48 hold the 4 k-quarters of
   // row l&15 — which is also the output row this lane holds (C^T layout), so the
@@ -262,7 +287,7 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   if constexpr (EPI == 3) {
     const int h = n0 >> 6;
     if (h < ra.nh + ra.nkv) {
-      for (int q = tid; q < BM * 4; q += 256) {
+      for (int q = tid; q < BM * 4; q += NT) {
         const int row = q >> 2, c = q & 3;
         const int gr = m0 + row;
         if (gr >= M) continue;
@@ -288,7 +313,7 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
       }
     } else {
       const int kh = h - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
-      for (int q = tid; q < BM * 64; q += 256) {
+      for (int q = tid; q < BM * 64; q += NT) {
         const int row = q >> 6, d = q & 63;
         const int gr = m0 + row;
         if (gr >= M) continue;
@@ -303,7 +328,7 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   // ---- epilogue 2: coalesced 16-B row chunks (+ residual)
   constexpr int CPR = BNO / 8;  // chunks per row
   const int c0 = EPI == 2 ? n0 / 2 : n0;
-  for (int q = tid; q < BM * CPR; q += 256) {
+  for (int q = tid; q < BM * CPR; q += NT) {
     const int row = q / CPR, c = q % CPR;
     const int gr = m0 + row;
     if (gr >= M) continue;
@@ -325,25 +350,33 @@ __global__ void __launch_bounds__(256) gemm_fused_kernel(const uint16_t* __restr
   }
 }
 
+int g_group_m = 8;  // M-tiles per rasterisation group (sg_gemm_set_group_m)
+
 template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST>
-void launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
-            float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}) {
-  const int tm = (M + BM - 1) / BM, tn = N / BN;
-  hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST>), dim3(tm * tn), dim3(256), 0, stream,
-                     (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R, ldr, M, N,
-                     K, eps, tm, tn, ra);
+int launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
+           float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}) {
+  // the staged C tile must fit in the K-loop buffers (not so for 256-wide plain outputs)
+  constexpr int BNO = EPI == 2 ? BN / 2 : BN;
+  if constexpr (BM * (BNO + 8) > ST * (BM + BN) * BK) {
+    return -3;
+  } else {
+    const int tm = (M + BM - 1) / BM, tn = N / BN;
+    hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST>), dim3(tm * tn), dim3(WM * WN * 64), 0,
+                       stream, (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R,
+                       ldr, M, N, K, eps, tm, tn, g_group_m > 0 ? g_group_m : 1, ra);
+    return 0;
+  }
 }
 
 template <int BM, int BN, int WM, int WN, int ST>
 int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr,
                  int M, int N, int K, float eps, hipStream_t s) {
-  if (epi == 0 && !norm) launch<BM, BN, WM, WN, 0, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 0 && norm) launch<BM, BN, WM, WN, 0, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 1 && !norm) launch<BM, BN, WM, WN, 1, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 2 && norm) launch<BM, BN, WM, WN, 2, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else if (epi == 2 && !norm) launch<BM, BN, WM, WN, 2, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  else return -3;
-  return 0;
+  if (epi == 0 && !norm) return launch<BM, BN, WM, WN, 0, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  if (epi == 0 && norm) return launch<BM, BN, WM, WN, 0, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  if (epi == 1 && !norm) return launch<BM, BN, WM, WN, 1, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  if (epi == 2 && norm) return launch<BM, BN, WM, WN, 2, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  if (epi == 2 && !norm) return launch<BM, BN, WM, WN, 2, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+  return -3;
 }
 
 }  // namespace
@@ -351,15 +384,37 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
 // Tile configurations: BM x BN (wave grid), pipeline stages.
 //   0: 128x128 (2x2) 2st   1: 128x64 (2x2) 2st   2: 64x128 (1x4) 2st   3: 64x64 (2x2) 2st
 //   4: 128x64  (2x2) 3st   5: 64x64  (2x2) 3st   6: 64x64  (2x2) 4st   7: 128x128 (2x2) 3st
-//   8: 64x128  (1x4) 3st
+//   8: 64x128  (1x4) 3st   9: 256x128 (4x2) 2st, 8 waves   10: 256x256 (2x4) 2st, 8 waves
+//  11: 128x256 (2x4) 2st, 8 waves   12: 256x64 (4x2) 2st, 8 waves   13: 128x128 (2x4) 2st, 8 waves
+//  14: 256x128 (4x2) 3st, 8 waves   15: 128x256 (2x4) 3st, 8 waves   16: 256x64 (4x2) 4st, 8 waves
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
 
+void sg_gemm_set_group_m(int gm) { g_group_m = gm; }
+
+// Timing probe: the 128x128 SwiGLU+norm GEMM (cfg 0) with its K loop reduced to
+// loads only (mode 1) or MFMAs only (mode 2); mode 0 = the real kernel.
+int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, int mode, hipStream_t stream) {
+  const int tm = (M + 127) / 128, tn = N / 128;
+  if (K % BK || N % 128) return -2;
+#define SG_PROBE(MODE)                                                                                          \
+  hipLaunchKernelGGL((gemm_fused_kernel<128, 128, 2, 2, 2, true, 2, MODE>), dim3(tm * tn), dim3(256), 0, stream, \
+                     (const uint16_t*)A, K, (const uint16_t*)W, (uint16_t*)C, N / 2, nullptr, 0, M, N, K, 1e-5f, tm, \
+                     tn, g_group_m, RopeArgs{})
+  if (mode == 1) SG_PROBE(1);
+  else if (mode == 2) SG_PROBE(2);
+  else if (mode == 3) SG_PROBE(3);
+  else if (mode == 4) SG_PROBE(4);
+  else SG_PROBE(0);
+#undef SG_PROBE
+  return 0;
+}
+
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, hipStream_t stream) {
-  static const int BNs[9] = {128, 64, 128, 64, 64, 64, 64, 128, 128};
-  if (cfg < 0 || cfg > 8) return -1;
+  static const int BNs[17] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64};
+  if (cfg < 0 || cfg > 16) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
 #define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream
@@ -372,7 +427,15 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     case 5: return dispatch_epi<64, 64, 2, 2, 3>(SG_ARGS);
     case 6: return dispatch_epi<64, 64, 2, 2, 4>(SG_ARGS);
     case 7: return dispatch_epi<128, 128, 2, 2, 3>(SG_ARGS);
-    default: return dispatch_epi<64, 128, 1, 4, 3>(SG_ARGS);
+    case 8: return dispatch_epi<64, 128, 1, 4, 3>(SG_ARGS);
+    case 9: return dispatch_epi<256, 128, 4, 2, 2>(SG_ARGS);
+    case 10: return dispatch_epi<256, 256, 2, 4, 2>(SG_ARGS);
+    case 11: return dispatch_epi<128, 256, 2, 4, 2>(SG_ARGS);
+    case 12: return dispatch_epi<256, 64, 4, 2, 2>(SG_ARGS);
+    case 13: return dispatch_epi<128, 128, 2, 4, 2>(SG_ARGS);
+    case 14: return dispatch_epi<256, 128, 4, 2, 3>(SG_ARGS);
+    case 15: return dispatch_epi<128, 256, 2, 4, 3>(SG_ARGS);
+    default: return dispatch_epi<256, 64, 4, 2, 4>(SG_ARGS);
   }
 #undef SG_ARGS
 }
@@ -388,12 +451,11 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
   RopeArgs ra{pos, slot, (const float2*)cos_sin, (uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)vt_cache,
               nh, nkv, Lmax, p0};
   switch (cfg) {
-    case 1: launch<128, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra); break;
-    case 3: launch<64, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra); break;
-    case 5: launch<64, 64, 2, 2, 3, true, 3>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra); break;
+    case 1: return launch<128, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
+    case 3: return launch<64, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
+    case 5: return launch<64, 64, 2, 2, 3, true, 3>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
     default: return -1;
   }
-  return 0;
 }
 
 }  // extern "C"

@@ -102,19 +102,29 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
             base = worker.stage.processed
 
             async def publish(i: int) -> None:
-                items = [(SUBJECT_RAW, payload_to_raw(p).model_dump_json().encode("utf-8")) for p in prepared[i]]
-                await bus.publish_many(items)
+                # gateway ingestion in chunks that yield to the parser stage, so parsing
+                # (and the GPU) start after the first chunk, not after whole steps
+                chunk = 256
+                msgs = prepared[i]
+                for c in range(0, len(msgs), chunk):
+                    items = [(SUBJECT_RAW, payload_to_raw(p).model_dump_json().encode("utf-8"))
+                             for p in msgs[c:c + chunk]]
+                    await bus.publish_many(items)
+                    await asyncio.sleep(0)
 
             nsteps = len(prepared)
-            if nsteps:
-                await publish(0)
+            pub_task = asyncio.create_task(publish(0)) if nsteps else None
             done_msgs = 0
             for i in range(nsteps):
-                if i + 1 < nsteps:
-                    await publish(i + 1)  # ingestion runs one step ahead of parsing
+                if pub_task is not None:
+                    await pub_task
+                # ingestion of step i+1 overlaps the parsing of step i
+                pub_task = asyncio.create_task(publish(i + 1)) if i + 1 < nsteps else None
                 done_msgs += len(prepared[i])
                 while worker.stage.processed < base + done_msgs:
                     await asyncio.sleep(0.0005)
+            if pub_task is not None:
+                await pub_task
             counts = {k: worker.counts[k] - c0[k] for k in c0}
             client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
     await worker.stop()

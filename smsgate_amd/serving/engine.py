@@ -76,7 +76,13 @@ class EngineStats:
     decode_row_steps: int = 0
     decode_s: float = 0.0
     harvest_s: float = 0.0
+    harvest_wait_s: float = 0.0  # part of harvest_s blocked on the GPU (the snapshot's event)
     admit_s: float = 0.0
+    compact_s: float = 0.0
+    steps: int = 0
+    step_s: float = 0.0  # wall time inside step() (the rest of a server loop is I/O)
+    server_poll_s: float = 0.0  # EngineServer: receiving / unpacking / submitting requests
+    server_send_s: float = 0.0  # EngineServer: packing / sending results
     compactions: int = 0
     rows_moved: int = 0
     completed: int = 0
@@ -488,6 +494,7 @@ class ExtractionEngine:
     def _harvest(self, snap: "_Snapshot", raw: bool = False) -> List[Tuple[Any, Any]]:
         t0 = time.perf_counter()
         snap.event.synchronize()
+        self.stats.harvest_wait_s += time.perf_counter() - t0
         done_h = snap.bufs["done"][: snap.B].numpy()
         res: List[Tuple[Any, Any]] = []
         lens = snap.bufs["len"]
@@ -531,14 +538,19 @@ class ExtractionEngine:
         t0 = time.perf_counter()
         if self.cfg.compact:
             self._compact()
+        t1 = time.perf_counter()
         self._admit()
-        self.stats.admit_s += time.perf_counter() - t0
+        self.stats.compact_s += t1 - t0
+        self.stats.admit_s += time.perf_counter() - t1
         prev, self._pending = self._pending, None
         if self.active:
             B = self._bucket(max(self.active) + 1)
             self._run_decode(B)
             self._pending = self._snapshot(B)
-        return self._harvest(prev, raw) if prev is not None else []
+        out = self._harvest(prev, raw) if prev is not None else []
+        self.stats.steps += 1
+        self.stats.step_s += time.perf_counter() - t0
+        return out
 
     def submit_ids(self, items: Sequence[Tuple[Any, Sequence[int]]]) -> None:
         """Queue pre-tokenised prompts (``<sms> body <ans>`` ids, see the tokenizer)."""

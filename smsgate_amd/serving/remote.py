@@ -62,6 +62,15 @@ class EngineServer:
         return [c for c in self.conns if c is not None]
 
     def poll(self, timeout: Optional[float]) -> None:
+        t0 = time.perf_counter()
+        try:
+            self._poll(timeout)
+        finally:
+            st = getattr(self.engine, "stats", None)
+            if st is not None and hasattr(st, "server_poll_s"):
+                st.server_poll_s += time.perf_counter() - t0
+
+    def _poll(self, timeout: Optional[float]) -> None:
         live = self._live()
         if not live:
             if timeout:
@@ -101,6 +110,7 @@ class EngineServer:
             self.engine.active.clear()
             self.engine._pending = None
             raise
+        t0 = time.perf_counter()
         for (idx, rid, i), toks in finished:
             r = self.reqs.get((idx, rid))
             if r is None:
@@ -115,6 +125,9 @@ class EngineServer:
                     flat = np.concatenate(r.out) if r.out else np.zeros(0, np.int32)
                     c.send_bytes(P.pack_arrays(b"R", rid, lens, flat))
                 self.served += len(r.out)
+        st = getattr(self.engine, "stats", None)
+        if st is not None and hasattr(st, "server_send_s"):
+            st.server_send_s += time.perf_counter() - t0
 
     def serve_until(self, pred: Callable[[], bool]) -> None:
         while not pred():

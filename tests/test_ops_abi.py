@@ -15,7 +15,7 @@ def _c_signatures():
     for f in CSRC.glob("*.hip"):
         text = f.read_text()
         block = text[text.index('extern "C" {'):]
-        for m in re.finditer(r"\bint\s+(sg_\w+)\s*\(([^)]*)\)\s*\{", block):
+        for m in re.finditer(r"\b(?:int|void)\s+(sg_\w+)\s*\(([^)]*)\)\s*\{", block):
             args = [a.strip() for a in m.group(2).split(",") if a.strip()]
             sigs[m.group(1)] = args
     return sigs

@@ -48,6 +48,10 @@ class RemoteBus(Bus, Acker):
         self._pending: Dict[int, asyncio.Future] = {}
         self._reader_task = asyncio.create_task(self._read_loop())
         self._closed = False
+        # acks are coalesced into one ``ack_many`` frame per consumer and loop turn;
+        # any other request flushes them first, so ordering is preserved
+        self._acks: Dict[Tuple[str, str], List[int]] = {}
+        self._ack_flush_scheduled = False
 
     @classmethod
     async def connect(cls, dsn: str) -> "RemoteBus":
@@ -75,9 +79,22 @@ class RemoteBus(Bus, Acker):
                     fut.set_exception(BusError("bus connection closed"))
             self._pending.clear()
 
+    def _flush_acks(self) -> None:
+        self._ack_flush_scheduled = False
+        if not self._acks or self._closed:
+            self._acks.clear()
+            return
+        for (stream, consumer), seqs in self._acks.items():
+            if len(seqs) == 1:
+                self._w.write(pack(["ack", 0, stream, consumer, seqs[0]]))
+            else:
+                self._w.write(pack(["ack_many", 0, stream, consumer, seqs]))
+        self._acks.clear()
+
     async def _call(self, op: str, *args: Any) -> Any:
         if self._closed:
             raise BusError("bus connection closed")
+        self._flush_acks()
         rid = next(self._ids)
         fut = asyncio.get_running_loop().create_future()
         self._pending[rid] = fut
@@ -87,6 +104,7 @@ class RemoteBus(Bus, Acker):
 
     def _cast(self, op: str, *args: Any) -> None:
         if not self._closed:
+            self._flush_acks()
             self._w.write(pack([op, 0, *args]))
 
     # -- Bus ----------------------------------------------------------------------
@@ -119,6 +137,7 @@ class RemoteBus(Bus, Acker):
         return bool(await asyncio.wait_for(self._call("ping"), 5.0))
 
     async def close(self) -> None:
+        self._flush_acks()
         self._closed = True
         self._reader_task.cancel()
         self._w.close()
@@ -129,7 +148,12 @@ class RemoteBus(Bus, Acker):
 
     # -- Acker (fire-and-forget) ---------------------------------------------------
     async def ack(self, stream: str, consumer: str, seq: int) -> None:
-        self._cast("ack", stream, consumer, seq)
+        if self._closed:
+            return
+        self._acks.setdefault((stream, consumer), []).append(seq)
+        if not self._ack_flush_scheduled:
+            self._ack_flush_scheduled = True
+            asyncio.get_running_loop().call_soon(self._flush_acks)
 
     async def nak(self, stream: str, consumer: str, seq: int, delay: float) -> None:
         self._cast("nak", stream, consumer, seq, delay)

@@ -148,9 +148,25 @@ class BusServer:
 
 
 async def serve(listen: str, data_dir: Optional[str], stop: Optional[asyncio.Event] = None,
-                max_age: float = 3 * 24 * 3600.0, nats_listen: Optional[str] = None) -> BusServer:
+                max_age: float = 3 * 24 * 3600.0, nats_listen: Optional[str] = None,
+                native: bool = False) -> BusServer:
     """One journaled engine behind the msgpack protocol (``listen``) and, optionally,
-    the NATS wire protocol (``nats_listen``, :mod:`.nats_server`)."""
+    the NATS wire protocol (``nats_listen``, :mod:`.nats_server`).
+
+    ``native=True`` runs the C++ broker (:mod:`smsgate_amd.native`, same
+    protocol and journal format) as a child process instead; the returned
+    object has the same ``close()``.
+    """
+    if native:
+        if nats_listen:
+            raise BusError("the native broker serves the msgpack protocol only (drop --nats-listen)")
+        from ..native import spawn_busd
+
+        broker = spawn_busd(listen, data_dir, max_age=max_age)
+        if stop is not None:
+            await stop.wait()
+            await broker.close()
+        return broker  # type: ignore[return-value]
     if data_dir:
         from .filelog import open_file_bus
 

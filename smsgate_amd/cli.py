@@ -15,7 +15,7 @@ xml-watcher         BACKUP_DIR poller
 notifier            PocketBase → chart → Telegram
 mcp-server          MCP tools over SSE / streamable HTTP (port 9122)
 receiver            webhook capture server
-bus-server          durable broker (``--listen``, ``--data``)
+bus-server          durable broker (``--listen``, ``--data``, ``--native`` = C++ smsgate-busd)
 engine-server       GPU extraction engine for parser processes (``--listen``)
 pipeline            gateway + parser + writer in one process (memory bus)
 db                  migrations: upgrade|downgrade|current|history|stamp
@@ -152,7 +152,9 @@ async def _run_notifier(a, settings) -> None:
 async def _run_bus_server(a, settings) -> None:
     from .bus.server import serve
 
-    await serve(a.listen, a.data, _stop_event(), max_age=settings.stream_max_age_s, nats_listen=a.nats_listen)
+    native = getattr(a, "native", False)
+    await serve(a.listen, a.data, _stop_event(), max_age=settings.stream_max_age_s,
+                nats_listen=None if native else a.nats_listen, native=native)
 
 
 async def _run_pipeline(a, settings) -> None:
@@ -261,6 +263,8 @@ def build_parser() -> argparse.ArgumentParser:
     bp.add_argument("--listen", default="tcp://0.0.0.0:4223", help="msgpack protocol (tcp:// or unix://)")
     bp.add_argument("--nats-listen", default="tcp://0.0.0.0:4222", help="NATS wire protocol ('' = off)")
     bp.add_argument("--data", default="./.bus-data")
+    bp.add_argument("--native", action="store_true",
+                    help="run the C++ broker (smsgate-busd; msgpack protocol only, same journal format)")
     ep = sp.add_parser("engine-server")
     ep.add_argument("--listen", default="unix:///tmp/smsgate-engine0.sock")
     ep.add_argument("--model", default="smollm-135m")

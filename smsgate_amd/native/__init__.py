@@ -1,0 +1,102 @@
+"""Native (host C++) runtime components.
+
+* ``smsgate-busd`` (``csrc/busd.cpp`` + ``engine.hpp`` + ``mpack.hpp``): the
+  durable bus broker in C++ — the role the reference fills with an external
+  NATS server (docker-compose.yml:15-27).  It speaks the
+  same msgpack protocol as ``python -m smsgate_amd bus-server`` (so
+  :class:`~smsgate_amd.bus.client.RemoteBus` works unchanged) and writes the
+  same CRC-framed journal as :mod:`smsgate_amd.bus.filelog` (either broker
+  recovers the other's data directory).  One epoll loop, group-committed
+  journal writes, long-poll fetch waiters.
+
+Build: ``python -m smsgate_amd.native.build`` (in-tree, ``_bin/``).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import time
+from pathlib import Path
+from typing import List, Optional
+
+from .build import BUSD
+
+__all__ = ["BUSD", "available", "NativeBroker", "spawn_busd"]
+
+
+def available() -> bool:
+    return BUSD.exists() and os.access(BUSD, os.X_OK)
+
+
+class NativeBroker:
+    """A running ``smsgate-busd`` child process."""
+
+    def __init__(self, proc: subprocess.Popen, listens: List[str], tcp_port: Optional[int]) -> None:
+        self.proc = proc
+        self.listens = listens
+        self.tcp_port = tcp_port
+
+    @property
+    def pid(self) -> int:
+        return self.proc.pid
+
+    def alive(self) -> bool:
+        return self.proc.poll() is None
+
+    def stop(self, timeout: float = 10.0) -> int:
+        """Graceful stop (SIGTERM: flush + fsync the journal); returns the exit code."""
+        if self.proc.poll() is None:
+            self.proc.send_signal(signal.SIGTERM)
+            try:
+                self.proc.wait(timeout)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
+        return self.proc.returncode
+
+    def kill(self) -> None:
+        """Crash it (SIGKILL) — for recovery tests."""
+        if self.proc.poll() is None:
+            self.proc.kill()
+            self.proc.wait()
+
+    async def close(self) -> None:  # same shape as BusServer.close()
+        self.stop()
+
+
+def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_age: float = 3 * 24 * 3600.0,
+               fsync: str = "interval", fsync_interval_s: float = 0.05, compact_bytes: Optional[int] = None,
+               ready_timeout: float = 20.0) -> NativeBroker:
+    """Start the native broker and wait until it listens.
+
+    ``listen`` takes ``tcp://host:port`` (port 0 = pick one, see
+    :attr:`NativeBroker.tcp_port`) and/or ``unix:///path`` URLs.
+    """
+    if not available():
+        raise RuntimeError(f"{BUSD} is not built (python -m smsgate_amd.native.build)")
+    listens = [listen] if isinstance(listen, str) else list(listen)
+    cmd = [str(BUSD)]
+    for u in listens:
+        cmd += ["--listen", u]
+    if data_dir:
+        cmd += ["--data", str(data_dir)]
+    cmd += ["--max-age", repr(float(max_age)), "--fsync", fsync, "--fsync-interval", repr(float(fsync_interval_s))]
+    if compact_bytes is not None:
+        cmd += ["--compact-bytes", str(int(compact_bytes))]
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL)
+    t_end = time.monotonic() + ready_timeout
+    line = b""
+    while time.monotonic() < t_end:
+        line = proc.stdout.readline()  # type: ignore[union-attr]
+        if line or proc.poll() is not None:
+            break
+    if not line.startswith(b"READY"):
+        proc.kill()
+        raise RuntimeError(f"smsgate-busd failed to start (exit {proc.poll()}): {line!r}")
+    tok = line.split()[1].decode()
+    return NativeBroker(proc, listens, None if tok == "-" else int(tok))
+
+
+def busd_path() -> Path:
+    return BUSD

@@ -1,0 +1,57 @@
+"""Build the native (host C++) components in-tree.
+
+``python -m smsgate_amd.native.build`` (also run by ``__graft_entry__.build()``)
+compiles ``csrc/busd.cpp`` into ``_bin/smsgate-busd``, the native bus broker
+(see :mod:`smsgate_amd.native`).  Plain ``g++ -O2 -std=c++17``: no Python or
+torch headers, no third-party libraries.  Skipped when the binary is newer than
+every source.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+from typing import List
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+BINDIR = HERE / "_bin"
+BUSD = BINDIR / "smsgate-busd"
+
+
+def cxx() -> str:
+    for cand in (os.environ.get("CXX"), shutil.which("g++"), shutil.which("c++"), shutil.which("clang++")):
+        if cand:
+            return cand
+    raise RuntimeError("no C++ compiler found")
+
+
+def sources() -> List[Path]:
+    return sorted(CSRC.glob("*.cpp")) + sorted(CSRC.glob("*.hpp"))
+
+
+def needs_build() -> bool:
+    if not BUSD.exists():
+        return True
+    mt = BUSD.stat().st_mtime
+    return any(s.stat().st_mtime > mt for s in sources() + [Path(__file__)])
+
+
+def build(force: bool = False, verbose: bool = False, extra: List[str] = ()) -> Path:
+    if not force and not needs_build():
+        return BUSD
+    BINDIR.mkdir(parents=True, exist_ok=True)
+    tmp = BUSD.with_suffix(".tmp")
+    cmd = [cxx(), "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", *extra,
+           str(CSRC / "busd.cpp"), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, BUSD)
+    return BUSD
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

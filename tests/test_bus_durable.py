@@ -122,14 +122,19 @@ def _consumer_proc(sock, out_path, crash_after):
 
 
 @pytest.mark.slow
-def test_multiprocess_competing_consumers_with_crash(tmp_path, arun):
+@pytest.mark.parametrize("native", [False, True], ids=["python-broker", "native-broker"])
+def test_multiprocess_competing_consumers_with_crash(tmp_path, arun, native):
     """N processes share one durable group; one dies mid-message; nothing is lost."""
+    if native:
+        from smsgate_amd.native import build
+
+        build.build()
     sock = f"unix://{tmp_path}/bus.sock"
     outs = [tmp_path / f"out{i}.txt" for i in range(3)]
     N = 60
 
     async def go():
-        srv = await serve(sock, str(tmp_path / "data"))
+        srv = await serve(sock, str(tmp_path / "data"), native=native)
         pub = await connect(sock, shared=False)
         await pub.publish_many([(SUBJECT_RAW, str(i).encode()) for i in range(N)])
         ctx = mp.get_context("spawn")

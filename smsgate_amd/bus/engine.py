@@ -134,6 +134,31 @@ class Engine:
         self._enforce_limits(st)
         return st.cfg.name, seq
 
+    def store_many(self, items, ts: Optional[float] = None) -> List[Tuple[str, int]]:
+        """Batched :meth:`store` (one clock read, retention applied once per
+        touched stream at the end — the same final state, since retention only
+        ever drops from the front)."""
+        ts = self._clock() if ts is None else ts
+        route, log, mc = self._route, self._journal, self._match_cache
+        out: List[Tuple[str, int]] = []
+        touched: Dict[str, _Stream] = {}
+        for subject, data in items:
+            st = route(subject)
+            seq = st.last_seq = st.last_seq + 1
+            st.msgs[seq] = Stored(seq, subject, data, ts, None)
+            st.bytes += len(data)
+            for c in st.consumers.values():
+                if seq > c.cursor and c.matches(subject, mc):
+                    c.num_pending += 1
+            name = st.cfg.name
+            if log is not None:
+                log("store", (name, seq, subject, data, ts, None))
+            touched[name] = st
+            out.append((name, seq))
+        for st in touched.values():
+            self._enforce_limits(st)
+        return out
+
     def _drop(self, st: _Stream, seq: int) -> None:
         m = st.msgs.pop(seq, None)
         if m is None:

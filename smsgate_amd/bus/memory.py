@@ -127,13 +127,9 @@ class MemoryBus(Bus, Acker):
     async def publish_many(self, items: Sequence[Tuple[str, bytes]]) -> List[PubAck]:
         if self._closed:
             raise BusError("bus closed")
-        out: List[PubAck] = []
-        touched = set()
-        store = self.engine.store
-        for subject, data in items:
-            stream, seq = store(subject, bytes(data))
-            touched.add(stream)
-            out.append(PubAck(stream, seq))
+        stored = self.engine.store_many([(s, bytes(d)) for s, d in items])
+        out = [PubAck(stream, seq) for stream, seq in stored]
+        touched = {stream for stream, _ in stored}
         self._maybe_expire()
         for s in touched:
             self._wake(s)

@@ -44,18 +44,19 @@ _WORKER_SKIP_CASE_SENSITIVE = ("Daily limit exceeded",)
 LLM_SKIP_KEYWORDS = ("OTP", "CODE:", "PASS:", "PASS=", "Daily limit exceeded:")
 
 _CARD_RE = re.compile(r"\d{4}\*{3}(\d{4})")
+# one alternation scan instead of a generator of ``in`` tests (same semantics)
+_WORKER_SKIP_RE = re.compile("|".join(map(re.escape, WORKER_SKIP_KEYWORDS)))
+_WORKER_SKIP_CS_RE = re.compile("|".join(map(re.escape, _WORKER_SKIP_CASE_SENSITIVE)))
+_LLM_SKIP_RE = re.compile("|".join(map(re.escape, LLM_SKIP_KEYWORDS)))
 _JSON_RE = re.compile(r"\{.*\}", re.S)
 
 
 def worker_should_skip(body: str) -> bool:
-    up = body.upper()
-    return any(k in up for k in WORKER_SKIP_KEYWORDS) or any(
-        k in body for k in _WORKER_SKIP_CASE_SENSITIVE
-    )
+    return _WORKER_SKIP_RE.search(body.upper()) is not None or _WORKER_SKIP_CS_RE.search(body) is not None
 
 
 def llm_should_skip(body: str) -> bool:
-    return any(k in body for k in LLM_SKIP_KEYWORDS)
+    return _LLM_SKIP_RE.search(body) is not None
 
 
 def mask_card_number_with_prefix(text: str) -> str:

@@ -71,13 +71,24 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
 
     with start_span("validate"):
         for i, m in enumerate(msgs):
-            text = m.data.decode(errors="ignore") if isinstance(m.data, (bytes, bytearray)) else str(m.data)
+            data = m.data
+            text = data.decode(errors="ignore") if isinstance(data, (bytes, bytearray)) else str(data)
             texts.append(text)
             try:
-                payload = json.loads(text)
-                if isinstance(payload, dict) and "raw" in payload:
-                    payload = payload["raw"]
-                raw = RawSMS(**payload)
+                if '"raw"' not in text:
+                    # fast path: pydantic-core parses + validates the JSON in one pass
+                    # (falls back below on any error, so failure routing is unchanged)
+                    try:
+                        raw = RawSMS.model_validate_json(text)
+                    except Exception:
+                        raw = None
+                else:
+                    raw = None
+                if raw is None:
+                    payload = json.loads(text)
+                    if isinstance(payload, dict) and "raw" in payload:
+                        payload = payload["raw"]
+                    raw = RawSMS(**payload)
             except Exception as err:
                 out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))
                 counts["fail"] += 1

@@ -139,9 +139,14 @@ def test_multiprocess_competing_consumers_with_crash(tmp_path, arun, native):
         await pub.publish_many([(SUBJECT_RAW, str(i).encode()) for i in range(N)])
         ctx = mp.get_context("spawn")
         procs = [ctx.Process(target=_consumer_proc, args=(sock, str(outs[i]), 5 if i == 0 else 0)) for i in range(3)]
-        for p in procs:
-            p.start()
+        # the crashing consumer runs alone until it has died holding its 5th message
+        # (deterministic: otherwise the others may drain the stream before it gets 5)
+        procs[0].start()
         t_end = time.time() + 60
+        while procs[0].is_alive() and time.time() < t_end:
+            await asyncio.sleep(0.05)
+        for p in procs[1:]:
+            p.start()
         while any(p.is_alive() for p in procs) and time.time() < t_end:
             await asyncio.sleep(0.1)
         for p in procs:

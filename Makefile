@@ -1,9 +1,13 @@
 # Convenience targets (the reference's makefile alembic targets map to `python -m smsgate_amd db ...`).
 PY ?= python
-.PHONY: build test test-gpu bench upgrade downgrade current history stamp smoke
+.PHONY: build native sanitize test test-gpu bench bus-bench upgrade downgrade current history stamp smoke
 
-build:            ## compile the HIP kernels for gfx950
+build: native     ## compile the HIP kernels for gfx950 (+ the native broker)
 	$(PY) -m smsgate_amd.ops.build --force
+native:           ## C++ broker smsgate-busd (+ its ASan/UBSan build)
+	$(PY) -m smsgate_amd.native.build --force --sanitize
+bus-bench:        ## Python vs native broker throughput
+	$(PY) scripts/bus_bench.py
 test:             ## CPU test suite
 	$(PY) -m pytest tests -x -q -m "not gpu"
 test-gpu:         ## GPU tests (MI355X)

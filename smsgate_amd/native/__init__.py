@@ -20,13 +20,13 @@ import time
 from pathlib import Path
 from typing import List, Optional
 
-from .build import BUSD
+from .build import BUSD, BUSD_SAN
 
-__all__ = ["BUSD", "available", "NativeBroker", "spawn_busd"]
+__all__ = ["BUSD", "BUSD_SAN", "available", "NativeBroker", "spawn_busd"]
 
 
-def available() -> bool:
-    return BUSD.exists() and os.access(BUSD, os.X_OK)
+def available(binary: Path = BUSD) -> bool:
+    return binary.exists() and os.access(binary, os.X_OK)
 
 
 class NativeBroker:
@@ -67,16 +67,17 @@ class NativeBroker:
 
 def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_age: float = 3 * 24 * 3600.0,
                fsync: str = "interval", fsync_interval_s: float = 0.05, compact_bytes: Optional[int] = None,
-               ready_timeout: float = 20.0) -> NativeBroker:
+               ready_timeout: float = 20.0, binary: Optional[Path] = None, stderr=None) -> NativeBroker:
     """Start the native broker and wait until it listens.
 
     ``listen`` takes ``tcp://host:port`` (port 0 = pick one, see
     :attr:`NativeBroker.tcp_port`) and/or ``unix:///path`` URLs.
     """
-    if not available():
-        raise RuntimeError(f"{BUSD} is not built (python -m smsgate_amd.native.build)")
+    binary = Path(binary or BUSD)
+    if not available(binary):
+        raise RuntimeError(f"{binary} is not built (python -m smsgate_amd.native.build)")
     listens = [listen] if isinstance(listen, str) else list(listen)
-    cmd = [str(BUSD)]
+    cmd = [str(binary)]
     for u in listens:
         cmd += ["--listen", u]
     if data_dir:
@@ -84,7 +85,7 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
     cmd += ["--max-age", repr(float(max_age)), "--fsync", fsync, "--fsync-interval", repr(float(fsync_interval_s))]
     if compact_bytes is not None:
         cmd += ["--compact-bytes", str(int(compact_bytes))]
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL, stderr=stderr)
     t_end = time.monotonic() + ready_timeout
     line = b""
     while time.monotonic() < t_end:

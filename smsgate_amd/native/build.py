@@ -19,6 +19,9 @@ HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 BINDIR = HERE / "_bin"
 BUSD = BINDIR / "smsgate-busd"
+# host sanitizer build (ASan + UBSan): the broker's race/memory check, run by
+# tests/test_native_bus.py::test_sanitizer_build_clean (GPU sanitizers are not used)
+BUSD_SAN = BINDIR / "smsgate-busd-san"
 
 
 def cxx() -> str:
@@ -32,26 +35,31 @@ def sources() -> List[Path]:
     return sorted(CSRC.glob("*.cpp")) + sorted(CSRC.glob("*.hpp"))
 
 
-def needs_build() -> bool:
-    if not BUSD.exists():
+def needs_build(target: Path = BUSD) -> bool:
+    if not target.exists():
         return True
-    mt = BUSD.stat().st_mtime
+    mt = target.stat().st_mtime
     return any(s.stat().st_mtime > mt for s in sources() + [Path(__file__)])
 
 
-def build(force: bool = False, verbose: bool = False, extra: List[str] = ()) -> Path:
-    if not force and not needs_build():
-        return BUSD
+def build(force: bool = False, verbose: bool = False, extra: List[str] = (), sanitize: bool = False) -> Path:
+    target = BUSD_SAN if sanitize else BUSD
+    if not force and not needs_build(target):
+        return target
     BINDIR.mkdir(parents=True, exist_ok=True)
-    tmp = BUSD.with_suffix(".tmp")
-    cmd = [cxx(), "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", *extra,
+    tmp = target.with_suffix(".tmp")
+    opt = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"] \
+        if sanitize else ["-O2"]
+    cmd = [cxx(), *opt, "-std=c++17", "-Wall", "-Wno-unused-function", *extra,
            str(CSRC / "busd.cpp"), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, BUSD)
-    return BUSD
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    if "--sanitize" in sys.argv:
+        print(build(force="--force" in sys.argv, verbose=True, sanitize=True))

@@ -81,6 +81,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_gemm_probe.restype = _c_int
     lib.sg_gemm_set_group_m.argtypes = [_c_int]
     lib.sg_gemm_set_group_m.restype = None
+    lib.sg_set_prefill_impl.argtypes = [_c_int]
+    lib.sg_set_prefill_impl.restype = None
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
@@ -294,6 +296,12 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos
     assert pos.numel() == T and slot.numel() == T
     _check(load_library().sg_rope_qkv_cache(_p(qkv), _p(pos), _p(slot), _p(cos_sin), _p(q_out), _p(k_cache),
                                             _p(vt_cache), T, nh, nkv, D, Lmax, p0, _stream()), "rope_qkv_cache")
+
+
+def set_prefill_impl(impl: str) -> None:
+    """``"gqa"`` (default: one wave per KV head, K/V loaded once per GQA group,
+    prefetched) or ``"per_head"`` (one wave per query head; kept for A/B)."""
+    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1}[impl])
 
 
 def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slot: torch.Tensor, max_q: int,

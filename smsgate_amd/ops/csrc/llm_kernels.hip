@@ -347,6 +347,191 @@ __global__ void __launch_bounds__(64) attn_prefill_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Prefill attention, GQA-shared (production): one wave per (16-query tile,
+// sequence, KV head) computes all G query heads of the group from ONE load of
+// each K/V tile (the per-head kernel above re-reads K/V G times), and the K tile
+// of step kt+1 and the V tile of step kt are in flight while the scores of step
+// kt are computed (register double buffering: the per-head kernel waited on a
+// cold load at every step).  Same masking, rounding and online softmax as the
+// per-head kernel; numerics are checked against the same fp32 reference.
+// ---------------------------------------------------------------------------
+template <int G>
+__global__ void __launch_bounds__(64) attn_prefill_gqa_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
+    const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out,
+    int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int tile = blockIdx.x, b = blockIdx.y, kh = blockIdx.z;
+  const int l = threadIdx.x;
+  const int qbeg = cu_q[b];
+  const int qlen = cu_q[b + 1] - qbeg;
+  if (tile * 16 >= qlen) return;
+  const int g4 = l >> 4, r16 = l & 15;
+  const int qs = q_start[b];
+  const int sl = slot[b];
+
+  __shared__ __attribute__((aligned(16))) uint16_t P_lds[G][16 * 32];
+
+  bf16x8 qa[G][2];
+  {
+    const int row = tile * 16 + r16;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (row < qlen)
+          v = *reinterpret_cast<const uint4*>(q + ((size_t)(qbeg + row) * nh + kh * G + g) * D + 8 * g4 + 32 * s);
+        qa[g][s] = __builtin_bit_cast(bf16x8, v);
+      }
+  }
+  int qoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qoff[i] = qs + tile * 16 + 4 * g4 + i;
+  const int last_row = min(tile * 16 + 15, qlen - 1);
+  const int nkeys = P0pad + qs + last_row + 1;
+
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+
+  auto load_k = [&](int kt, uint4 (&kv)[2][2]) {
+    const bool pre = kt < P0pad;
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const int key = kt + 16 * hs + r16;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        kv[hs][s] = make_uint4(0, 0, 0, 0);
+        if (key < nkeys) {
+          const uint16_t* krow = pre ? (kpre + (size_t)key * D) : (kself + (size_t)(key - P0pad) * D);
+          kv[hs][s] = *reinterpret_cast<const uint4*>(krow + 8 * g4 + 32 * s);
+        }
+      }
+    }
+  };
+
+  f32x4 o[G][4];
+  float m[G][4], lsum[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      m[g][i] = -INFINITY;
+      lsum[g][i] = 0.f;
+    }
+
+  uint4 kc[2][2];
+  load_k(0, kc);
+  for (int kt = 0; kt < nkeys; kt += 32) {
+    const bool pre = kt < P0pad;  // tiles never straddle: P0pad % 32 == 0
+    // V tile of this step and K tile of the next step: in flight during the scores
+    uint4 vv[4];
+    const int kk = kt + 8 * g4;  // first of this lane's 8 keys
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int d = 16 * n + r16;
+      vv[n] = make_uint4(0, 0, 0, 0);
+      if (kk < nkeys) {
+        const uint16_t* vrow = pre ? (vpre + ((size_t)(kk >> 3) * D + d) * 8)
+                                   : (vself + ((size_t)((kk - P0pad) >> 3) * D + d) * 8);
+        vv[n] = *reinterpret_cast<const uint4*>(vrow);
+      }
+    }
+    uint4 kn[2][2];
+    load_k(kt + 32, kn);  // guarded by key < nkeys: past the end it loads nothing
+
+    bool okm[2][4];
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs) {
+      const int key = kt + 16 * hs + r16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) okm[hs][i] = pre ? (key < P0) : ((key - P0pad) <= qoff[i]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      f32x4 sacc[2];
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        sacc[hs] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          sacc[hs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[g][s], __builtin_bit_cast(bf16x8, kc[hs][s]),
+                                                             sacc[hs], 0, 0, 0);
+      }
+      float sv[2][4], tmax[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) tmax[i] = -INFINITY;
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = okm[hs][i] ? sacc[hs][i] * scale_log2 : -INFINITY;
+          sv[hs][i] = v;
+          tmax[i] = fmaxf(tmax[i], v);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int o2 = 8; o2 > 0; o2 >>= 1) tmax[i] = fmaxf(tmax[i], __shfl_xor(tmax[i], o2, WAVE));
+      float alpha[4], rs[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mn = fmaxf(m[g][i], tmax[i]);
+        alpha[i] = (mn == -INFINITY) ? 1.f : exp2f(m[g][i] - mn);
+        m[g][i] = mn;
+        rs[i] = 0.f;
+      }
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = (m[g][i] == -INFINITY) ? 0.f : exp2f(sv[hs][i] - m[g][i]);
+          rs[i] += p;
+          P_lds[g][(4 * g4 + i) * 32 + 16 * hs + r16] = f2bf(p);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int o2 = 8; o2 > 0; o2 >>= 1) rs[i] += __shfl_xor(rs[i], o2, WAVE);
+        lsum[g][i] = lsum[g][i] * alpha[i] + rs[i];
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[g][n][i] *= alpha[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const bf16x8 pa = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&P_lds[g][r16 * 32 + 8 * g4]));
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        o[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vv[n]), o[g][n], 0, 0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) kc[hs][s] = kn[hs][s];
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tile * 16 + 4 * g4 + i;
+      if (row >= qlen) continue;
+      const float inv = lsum[g][i] > 0.f ? 1.f / lsum[g][i] : 0.f;
+      uint16_t* orow = out + ((size_t)(qbeg + row) * nh + kh * G + g) * D;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) orow[16 * n + r16] = f2bf(o[g][n][i] * inv);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Decode attention: one query token per sequence; grid = (B, nkv), ONE wave per
 // (sequence, kv head) computing its G = nh/nkv query heads, so every K/V byte is
 // read once per GQA group. Finished rows exit immediately (done[b] != 0).
@@ -1140,6 +1325,8 @@ __global__ void __launch_bounds__(256) fsm_sample_kernel(
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+static int g_prefill_impl = 0;  // sg_set_prefill_impl
+
 extern "C" {
 
 int sg_rmsnorm_residual(const void* x_in, void* residual, const void* w, void* out, int T, int H, float eps,
@@ -1179,12 +1366,30 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
                     int max_q, int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
   if (D != 64 || (P0pad % 32) || (Lmax % 8) || nh % nkv) return -1;
   if (nseq == 0 || max_q == 0) return 0;
+  const float sl2 = scale * 1.4426950408889634f;
+  const int G = nh / nkv;
+  if (g_prefill_impl == 0 && G >= 1 && G <= 4) {
+    dim3 grid((max_q + 15) / 16, nseq, nkv);
+#define SG_PF(GG)                                                                                               \
+  hipLaunchKernelGGL(attn_prefill_gqa_kernel<GG>, grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
+                     slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,            \
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2)
+    if (G == 1) SG_PF(1);
+    else if (G == 2) SG_PF(2);
+    else if (G == 3) SG_PF(3);
+    else SG_PF(4);
+#undef SG_PF
+    return (int)hipGetLastError();
+  }
   dim3 grid((max_q + 15) / 16, nseq, nh);
   hipLaunchKernelGGL(attn_prefill_kernel, grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, slot,
                      (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt,
-                     P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
+                     P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2);
   return (int)hipGetLastError();
 }
+
+// 0 = GQA-shared prefetching kernel (default), 1 = per-head kernel (A/B: kbench, tests)
+void sg_set_prefill_impl(int impl) { g_prefill_impl = impl; }
 
 int sg_attn_decode(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
                    const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh,

@@ -198,6 +198,35 @@ def _engine_server(a) -> None:
     EngineServer(eng).serve_listener(path, stop)
 
 
+def _train(a, settings) -> None:
+    """``train-extractor``; under ``torchrun --nproc-per-node N`` one rank per GPU
+    (RCCL data parallel, :mod:`smsgate_amd.parallel.ddp`)."""
+    import torch
+    import torch.distributed as dist
+
+    from .models.train import TrainConfig, train_extractor
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    device = settings.llm_device
+    if world > 1:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            device = f"cuda:{local}"
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(device))
+        else:
+            device = "cpu"
+            dist.init_process_group("gloo")
+    cfg = TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr, n_examples=a.examples,
+                      ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, bucket_mb=a.bucket_mb)
+    w = train_extractor(cfg, device=device)
+    if not dist.is_initialized() or dist.get_rank() == 0:
+        w.save(a.out)
+        print(f"saved {a.out}")
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def _db(a, settings) -> None:
     from .db import migrations
     from .sinks.sql import make_engine
@@ -290,6 +319,10 @@ def build_parser() -> argparse.ArgumentParser:
     tr.add_argument("--lr", type=float, default=1e-3)
     tr.add_argument("--examples", type=int, default=60000)
     tr.add_argument("--out", required=True, help="safetensors path (LLM_CHECKPOINT for the local_llm backend)")
+    tr.add_argument("--ckpt-dir", default=None, help="training checkpoints (weights + optimizer + step)")
+    tr.add_argument("--ckpt-every", type=int, default=0)
+    tr.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --ckpt-dir")
+    tr.add_argument("--bucket-mb", type=float, default=64.0, help="DP gradient all-reduce bucket size")
     sp.add_parser("config")
     return p
 
@@ -354,12 +387,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     elif a.cmd == "legacy":
         asyncio.run(_legacy(a, settings))
     elif a.cmd == "train-extractor":
-        from .models.train import TrainConfig, train_extractor
-
-        w = train_extractor(TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr,
-                                        n_examples=a.examples), device=settings.llm_device)
-        w.save(a.out)
-        print(f"saved {a.out}")
+        _train(a, settings)
     return 0
 
 

@@ -18,14 +18,24 @@ its speed.  This module turns the LM into a working extractor.
   vocabulary (the tokenizer ids, the same rows the serving lm_head uses);
 * model: fp32 master weights, bf16 autocast, AdamW with warmup + cosine decay.
   The differentiable forward is :func:`~smsgate_amd.models.extractor.reference_forward`
-  (PyTorch SDPA); serving uses the HIP kernels on the saved bf16 weights.
+  (PyTorch SDPA); serving uses the HIP kernels on the saved bf16 weights;
+* data parallel: under ``torch.distributed`` (one process per GPU, RCCL) every
+  rank draws its own examples and gradients are averaged by
+  :class:`~smsgate_amd.parallel.ddp.GradBuckets` (flat buckets, all-reduce
+  overlapped with backward); the global batch is ``batch x world``;
+* checkpoint / resume: ``ckpt_dir`` gets ``step-XXXXXXX.pt`` (fp32 weights,
+  optimizer state, step, data RNG state) every ``ckpt_every`` steps, written by
+  rank 0 and loaded with ``torch.load(weights_only=True)``; ``resume=True``
+  restarts from the newest one.
 """
 from __future__ import annotations
 
 import math
+import os
 import random
 import time
 from dataclasses import dataclass
+from pathlib import Path
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -36,7 +46,8 @@ from ..parse.text import normalize_body
 from .extractor import CONFIGS, ExtractorWeights, reference_forward
 from .tokenizer import ExtractorTokenizer, load_tokenizer
 
-__all__ = ["TrainConfig", "answer_tokens", "make_examples", "train_extractor", "field_accuracy"]
+__all__ = ["TrainConfig", "answer_tokens", "make_examples", "train_extractor", "field_accuracy",
+           "latest_checkpoint"]
 
 
 @dataclass
@@ -52,6 +63,10 @@ class TrainConfig:
     seed: int = 0
     max_body_tokens: int = 128
     log_every: int = 100
+    ckpt_dir: Optional[str] = None
+    ckpt_every: int = 0  # 0 = only at the end (when ckpt_dir is set)
+    resume: bool = False
+    bucket_mb: float = 64.0
 
 
 def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]]) -> Optional[List[int]]:
@@ -97,10 +112,33 @@ def _batch(prefix: List[int], exs: Sequence[Tuple[List[int], List[int]]], pad: i
     return ids.to(device), labels.to(device)
 
 
+def latest_checkpoint(ckpt_dir: Optional[str]) -> Optional[Path]:
+    if not ckpt_dir or not os.path.isdir(ckpt_dir):
+        return None
+    cks = sorted(Path(ckpt_dir).glob("step-*.pt"))
+    return cks[-1] if cks else None
+
+
+def _save_checkpoint(ckpt_dir: str, step: int, w: ExtractorWeights, opt, rng: random.Random) -> Path:
+    os.makedirs(ckpt_dir, exist_ok=True)
+    path = Path(ckpt_dir) / f"step-{step:07d}.pt"
+    tmp = path.with_suffix(".tmp")
+    torch.save({"step": step, "weights": {k: v.detach().cpu() for k, v in w.state_dict().items()},
+                "opt": opt.state_dict(), "rng": rng.getstate(), "model": w.cfg.name}, tmp)
+    os.replace(tmp, path)  # atomic: a crash never leaves a half-written "latest"
+    return path
+
+
 def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] = print,
                     tok: Optional[ExtractorTokenizer] = None) -> ExtractorWeights:
     """Train and return **bf16** serving weights."""
+    import torch.distributed as dist
+
+    from ..parallel.ddp import GradBuckets
     from ..serving.fsm import build_fsm
+
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size() if dist.is_initialized() else 1
 
     tok = tok or load_tokenizer()
     mcfg = CONFIGS[cfg.model]
@@ -117,15 +155,33 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     opt = torch.optim.AdamW([{"params": decay, "weight_decay": cfg.weight_decay},
                              {"params": no_decay, "weight_decay": 0.0}], lr=cfg.lr, betas=(0.9, 0.95))
 
+    gb = GradBuckets(list(w.parameters()), bucket_mb=cfg.bucket_mb)
+
     def lr_at(step: int) -> float:
         if step < cfg.warmup:
             return cfg.lr * (step + 1) / cfg.warmup
         p = (step - cfg.warmup) / max(1, cfg.steps - cfg.warmup)
         return cfg.lr * (cfg.min_lr_frac + (1 - cfg.min_lr_frac) * 0.5 * (1 + math.cos(math.pi * p)))
 
-    rng = random.Random(cfg.seed)
+    rng = random.Random(cfg.seed * 1000003 + rank)  # each rank draws its own examples
+    start = 0
+    ck = latest_checkpoint(cfg.ckpt_dir) if cfg.resume else None
+    if ck is not None:
+        state = torch.load(ck, map_location="cpu", weights_only=True)
+        with torch.no_grad():
+            for k, v in w.state_dict().items():
+                v.copy_(state["weights"][k])
+        opt.load_state_dict(state["opt"])
+        start = int(state["step"])
+        if world == 1:
+            rng.setstate(_as_rng_state(state["rng"]))
+        else:  # rank 0's stream was saved; the others re-derive theirs deterministically
+            rng = random.Random((cfg.seed * 1000003 + rank) ^ (start * 7919))
+            if rank == 0:
+                rng.setstate(_as_rng_state(state["rng"]))
+        log(f"train: resumed from {ck} at step {start}")
     t0 = time.perf_counter()
-    for step in range(cfg.steps):
+    for step in range(start, cfg.steps):
         for g in opt.param_groups:
             g["lr"] = lr_at(step)
         ids, labels = _batch(prefix, rng.sample(data, cfg.batch), tok.pad, device)
@@ -135,18 +191,29 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
             hs = h.reshape(-1, h.shape[-1])[sel]
             logits = hs @ w.embed[:v_dec].t()
             loss = F.cross_entropy(logits.float(), labels.view(-1)[sel])
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
+        gb.zero_grad()
+        loss.backward()  # bucket all-reduces start as gradients land
+        gb.finish()
         torch.nn.utils.clip_grad_norm_(w.parameters(), 1.0)
         opt.step()
-        if cfg.log_every and (step % cfg.log_every == 0 or step == cfg.steps - 1):
-            log(f"step {step:5d} loss {loss.item():.4f} lr {lr_at(step):.2e} ({time.perf_counter() - t0:.1f}s)")
+        if cfg.log_every and rank == 0 and (step % cfg.log_every == 0 or step == cfg.steps - 1):
+            log(f"step {step:5d} loss {loss.item():.4f} lr {lr_at(step):.2e} ({time.perf_counter() - t0:.1f}s)"
+                + (f" x{world} ranks" if world > 1 else ""))
+        done = step + 1
+        if cfg.ckpt_dir and rank == 0 and (done == cfg.steps or (cfg.ckpt_every and done % cfg.ckpt_every == 0)):
+            _save_checkpoint(cfg.ckpt_dir, done, w, opt, rng)
     out = ExtractorWeights(mcfg, device=device, dtype=torch.bfloat16, seed=None)
     with torch.no_grad():
         for (n, p), (_, q) in zip(out.named_parameters(), w.named_parameters()):
             p.copy_(q.to(torch.bfloat16))
     out.requires_grad_(False)
     return out
+
+
+def _as_rng_state(st):
+    """``random.Random.getstate()`` after a torch.save/load round trip (lists -> tuples)."""
+    version, internal, gauss = st
+    return (version, tuple(internal), gauss)
 
 
 def field_accuracy(predicted: Sequence[Optional[Dict[str, Optional[str]]]],

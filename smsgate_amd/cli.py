@@ -195,7 +195,14 @@ def _engine_server(a) -> None:
     if os.path.exists(path):
         os.unlink(path)
     log.info("engine server on %s (%s, %d slots)", a.listen, a.model, a.max_slots)
-    EngineServer(eng).serve_listener(path, stop)
+    from .obs.metrics import EngineMetricsExporter, start_metrics_server
+
+    start_metrics_server(env_var="ENGINE_METRICS_PORT", default=9104)
+    exporter = EngineMetricsExporter(eng).start()
+    try:
+        EngineServer(eng).serve_listener(path, stop)
+    finally:
+        exporter.stop()
 
 
 def _train(a, settings) -> None:

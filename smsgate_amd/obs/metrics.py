@@ -14,8 +14,11 @@ Writer (services/pb_writer/writer.py:35-39, port 9103):
 Gateway (new — README.md:37 promised port 9101 but nothing was exported, D12):
 ``api_gateway_requests_total{endpoint,status}``, ``api_gateway_publish_seconds``.
 
-Local LLM backend (new): ``llm_batch_size``, ``llm_step_seconds``,
-``llm_tokens_total{phase}``.
+Local LLM engine (new; ``engine-server`` on ``ENGINE_METRICS_PORT``, default 9104,
+exported by :class:`EngineMetricsExporter` from the engine's counters):
+``llm_batch_size`` (decode rows per step), ``llm_step_seconds{phase}``,
+``llm_tokens_total{phase}``, ``llm_sequences_completed_total``,
+``llm_active_sequences``, ``llm_waiting_sequences``.
 """
 from __future__ import annotations
 
@@ -52,6 +55,10 @@ __all__ = [
     "LLM_BATCH",
     "LLM_STEP_TIME",
     "LLM_TOKENS",
+    "LLM_COMPLETED",
+    "LLM_ACTIVE",
+    "LLM_WAITING",
+    "EngineMetricsExporter",
     "start_metrics_server",
     "render_latest",
 ]
@@ -81,6 +88,54 @@ LLM_BATCH = Histogram("llm_batch_size", "Sequences per extraction batch", bucket
 LLM_STEP_TIME = Histogram("llm_step_seconds", "Seconds per engine step", ["phase"],
                           buckets=(1e-4, 3e-4, 1e-3, 3e-3, 1e-2, 3e-2, 0.1, 0.3, 1.0))
 LLM_TOKENS = Counter("llm_tokens_total", "Tokens processed by the local extractor", ["phase"])
+LLM_COMPLETED = Counter("llm_sequences_completed_total", "Extractions finished by the local engine")
+LLM_ACTIVE = Gauge("llm_active_sequences", "Sequences decoding in the engine")
+LLM_WAITING = Gauge("llm_waiting_sequences", "Sequences queued for prefill")
+
+
+class EngineMetricsExporter:
+    """Publishes an :class:`~smsgate_amd.serving.engine.ExtractionEngine`'s counters
+    (``engine.stats``) as Prometheus metrics from a daemon thread, every
+    ``interval`` seconds — the engine loop itself never touches prometheus_client."""
+
+    def __init__(self, engine, interval: float = 1.0) -> None:
+        self.engine = engine
+        self.interval = interval
+        self._last = dict(engine.stats.as_dict())
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="engine-metrics", daemon=True)
+
+    def start(self) -> "EngineMetricsExporter":
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    def export_once(self) -> None:
+        cur = dict(self.engine.stats.as_dict())
+        d = {k: v - self._last.get(k, 0) for k, v in cur.items()}
+        d.setdefault("steps", 0)
+        self._last = cur
+        if d.get("prefill_tokens", 0) > 0:
+            LLM_TOKENS.labels(phase="prefill").inc(d["prefill_tokens"])
+        if d.get("decode_row_steps", 0) > 0:
+            LLM_TOKENS.labels(phase="decode").inc(d["decode_row_steps"])
+        if d.get("completed", 0) > 0:
+            LLM_COMPLETED.inc(d["completed"])
+        if d.get("decode_steps", 0) > 0:
+            LLM_BATCH.observe(d["decode_row_steps"] / d["decode_steps"])
+        if d["steps"] > 0:
+            LLM_STEP_TIME.labels(phase="step").observe(d.get("step_s", 0.0) / d["steps"])
+        LLM_ACTIVE.set(len(getattr(self.engine, "active", ()) or ()))
+        LLM_WAITING.set(len(getattr(self.engine, "waiting", ()) or ()))
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.interval):
+            try:
+                self.export_once()
+            except Exception:  # noqa: BLE001 — metrics must never take the engine down
+                log.debug("engine metrics export failed", exc_info=True)
 
 _started: set[int] = set()
 _lock = threading.Lock()

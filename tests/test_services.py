@@ -423,3 +423,27 @@ def test_tunnel_disabled_sdk_and_missing(monkeypatch):
     monkeypatch.setattr(tunnel.shutil, "which", lambda name: None)
     monkeypatch.setitem(sys.modules, "ngrok", None)  # import ngrok -> ImportError
     assert tunnel.open_tunnel(s, 9001) is None
+
+
+def test_engine_metrics_exporter():
+    """The engine-server's Prometheus exporter turns engine counters into metrics."""
+    from types import SimpleNamespace
+
+    from smsgate_amd.obs import metrics as M
+    from smsgate_amd.serving.engine import EngineStats
+
+    eng = SimpleNamespace(stats=EngineStats(), active={1: "a", 2: "b"}, waiting=[1, 2, 3])
+    ex = M.EngineMetricsExporter(eng)
+
+    def val(name, **labels):
+        return M.REGISTRY.get_sample_value(name, labels) or 0.0
+
+    before = (val("llm_tokens_total", phase="decode"), val("llm_sequences_completed_total"))
+    eng.stats.decode_steps, eng.stats.decode_row_steps, eng.stats.completed = 4, 1000, 17
+    eng.stats.prefill_tokens, eng.stats.steps, eng.stats.step_s = 500, 2, 0.01
+    ex.export_once()
+    assert val("llm_tokens_total", phase="decode") - before[0] == 1000
+    assert val("llm_sequences_completed_total") - before[1] == 17
+    assert val("llm_active_sequences") == 2 and val("llm_waiting_sequences") == 3
+    ex.export_once()  # no new work: counters unchanged
+    assert val("llm_tokens_total", phase="decode") - before[0] == 1000

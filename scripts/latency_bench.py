@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Serving latency of the extraction engine under a paced (Poisson) arrival stream.
+
+For each offered load R (msgs/s) the host submits pre-tokenised SMS whose
+arrival time has passed before every engine step, and records submit → answer
+latency per message.  Reports achieved throughput and p50/p95/p99 latency —
+the serving-side view of the headline throughput number (the reference's
+``sms_parser_processing_seconds`` histogram measured one Gemini round trip per
+message).  Random-init 135M weights, so every answer decodes the schema's
+maximum 59 tokens (the worst case for latency).
+
+    python scripts/latency_bench.py --rates 2000,8000,14000 --seconds 6
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+
+def run_rate(eng, ids, rate: float, seconds: float, seed: int) -> dict:
+    rng = np.random.default_rng(seed)
+    n = int(rate * seconds)
+    arrivals = np.cumsum(rng.exponential(1.0 / rate, n))
+    t_sub = np.zeros(n)
+    t_done = np.full(n, np.nan)
+    nxt = 0
+    t0 = time.perf_counter()
+    while nxt < n or eng.busy():
+        now = time.perf_counter() - t0
+        j = nxt
+        while j < n and arrivals[j] <= now:
+            j += 1
+        if j > nxt:
+            eng.submit_ids([(k, ids[k % len(ids)]) for k in range(nxt, j)])
+            t_sub[nxt:j] = now
+            nxt = j
+        if not eng.busy():
+            time.sleep(min(0.0005, max(0.0, arrivals[nxt] - now)) if nxt < n else 0)
+            continue
+        for k, _ in eng.step(raw=True):
+            t_done[k] = time.perf_counter() - t0
+    wall = time.perf_counter() - t0
+    lat = (t_done - t_sub) * 1000.0
+    lat = lat[~np.isnan(lat)]
+    return {"offered_msgs_per_s": rate, "msgs": int(n), "achieved_msgs_per_s": round(n / wall, 1),
+            "p50_ms": round(float(np.percentile(lat, 50)), 1), "p95_ms": round(float(np.percentile(lat, 95)), 1),
+            "p99_ms": round(float(np.percentile(lat, 99)), 1), "max_ms": round(float(lat.max()), 1)}
+
+
+def main() -> None:
+    p = argparse.ArgumentParser()
+    p.add_argument("--rates", default="2000,8000,14000")
+    p.add_argument("--seconds", type=float, default=6.0)
+    p.add_argument("--max-slots", type=int, default=8192)
+    p.add_argument("--out", default=None)
+    a = p.parse_args()
+    import torch
+
+    from smsgate_amd.parse.backends.local_llm import build_engine
+    from smsgate_amd.parse.text import normalize_body
+    from smsgate_amd.utils.synth import generate_bodies
+
+    eng = build_engine("smollm-135m", device="cuda", random_init=True, max_slots=a.max_slots, steps_per_graph=2,
+                       buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192))
+    bodies = [normalize_body(b) for b in generate_bodies(20000, seed=5)]
+    ids = eng.tok.message_ids(bodies, eng.cfg.max_body_tokens)
+    run_rate(eng, ids, 2000.0, 1.0, seed=0)  # warm-up
+    torch.cuda.synchronize()
+    res = [run_rate(eng, ids, float(r), a.seconds, seed=i + 1) for i, r in enumerate(a.rates.split(","))]
+    for r in res:
+        print(json.dumps(r), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -52,6 +52,11 @@ def _args(argv=None):
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
     p.add_argument("--no-compact", action="store_true", help="disable decode row compaction")
+    p.add_argument("--split-decode", type=int, default=4096,
+                   help="decode buckets >= N run as two half-batches on two streams (0 = off)")
+    p.add_argument("--no-split-offset", action="store_true", help="start both halves together")
+    p.add_argument("--split-prefill", type=int, default=8192,
+                   help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--cpu-echo-engine", action="store_true",
                    help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")
     p.add_argument("--verbose", action="store_true")
@@ -102,7 +107,9 @@ def run_replica(args, rank: int, world: int, local: int):
                    else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
         engine = build_engine(args.model, device=f"cuda:{local}", random_init=True, max_slots=args.max_slots,
                               steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
-                              buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact)
+                              buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
+                              split_decode=args.split_decode, split_offset=not args.no_split_offset,
+                              split_prefill=args.split_prefill)
     init_s = time.perf_counter() - t_init
     coord = Coordinator(engine, conns)
     coord.wait_all("ready")

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Split-decode (two half-batches on two streams) A/B + correctness test.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -k "split or graph_and_eager" -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_split.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_split.log; [ $rc -eq 0 ] || exit $rc
+for cfg in "" "--split-decode 4096 --no-split-offset" "--split-decode 4096" "--split-decode 2048" "" "--split-decode 4096 --no-split-offset" "--split-decode 4096"; do
+  timeout -k 10 300 python bench.py --steps 4 --warmup 1 $cfg > gpurun_out/ab_split.log 2>&1 || { tail -5 gpurun_out/ab_split.log; exit 1; }
+  echo "[$cfg] $(grep metric gpurun_out/ab_split.log | cut -c1-100)" | tee -a gpurun_out/ab_split_summary.txt
+done

@@ -65,6 +65,10 @@ class EngineConfig:
     decode_attn: str = "grouped"  # ops.attn_decode impl: grouped | cascade | mfma | mfma_v1 | valu
     lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
+    # nano-batch overlap (measured +10% msgs/s at 8192 slots, profiles/r01b_split_ab.txt):
+    split_decode: int = 4096  # >0: decode buckets >= this run as two half-batches on two streams
+    split_offset: bool = True  # start the second half one kernel behind the first
+    split_prefill: int = 8192  # >0: prefill batches of >= this many tokens run as two halves on two streams
 
 
 @dataclass
@@ -181,13 +185,14 @@ class ExtractionEngine:
         ]
         self._snap_flip = 0
         self._pending: Optional[_Snapshot] = None
+        self._s2: Optional[torch.cuda.Stream] = None  # side stream of the split prefill
         self._compute_prefix()
         if ec.use_graphs:
             self._capture_graphs()
 
     # ------------------------------------------------------------------ model
     def _layers(self, x: torch.Tensor, *, pos_tok: torch.Tensor, slot_tok: torch.Tensor, attn, k_cache,
-                vt_cache, p0: int) -> torch.Tensor:
+                vt_cache, p0: int, hook=None) -> torch.Tensor:
         """Run all decoder layers on packed tokens; returns the final-normed hidden."""
         mc, w = self.mc, self.w
         T = x.shape[0]
@@ -200,6 +205,8 @@ class ExtractionEngine:
             qkv = F.linear(h, w.qkv[i])
             ops.rope_qkv_cache(qkv, pos_tok, slot_tok, self.cos_sin, q, k_cache(i), vt_cache(i), mc.heads,
                                mc.kv_heads, mc.head_dim, p0)
+            if hook is not None:
+                hook(i)
             attn(i, q, a)
             y = F.linear(a, w.o[i])
             h = ops.rmsnorm_residual(resid, w.ln2[i], mc.eps, x=y)
@@ -208,7 +215,7 @@ class ExtractionEngine:
         return ops.rmsnorm_residual(resid, w.ln_f, mc.eps, x=y)
 
     def _layers_fused(self, x: torch.Tensor, *, pos_tok: torch.Tensor, slot_tok: torch.Tensor, attn, k_cache,
-                      vt_cache, p0: int) -> torch.Tensor:
+                      vt_cache, p0: int, hook=None) -> torch.Tensor:
         """Same network with the fused MFMA GEMMs: ``x`` is the residual stream,
         updated in place; returns it UN-normed (the final norm is the lm_head
         GEMM's prologue, :meth:`_logits`)."""
@@ -220,6 +227,8 @@ class ExtractionEngine:
             # norm prologue + QKV projection + RoPE + KV-cache write: one kernel
             ops.gemm_qkv_rope(x, self.fw_qkv[i], mc.eps, pos_tok, slot_tok, self.cos_sin, q, k_cache(i),
                               vt_cache(i), mc.heads, mc.kv_heads, p0)
+            if hook is not None:
+                hook(i)
             attn(i, q, a)
             ops.gemm(a, self.fw_o[i], epi="resid", resid=x)
             act = ops.gemm(x, self.fw_gu[i], epi="swiglu", norm_eps=mc.eps)
@@ -320,10 +329,15 @@ class ExtractionEngine:
         return logits
 
     # ----------------------------------------------------------------- decode
-    def _decode_step(self, B: int, sample: bool = True) -> torch.Tensor:
-        tok = self.tok_buf[:B]
-        pos = self.pos[:B]
-        slot = self.slot_id[:B]
+    def _decode_step(self, B: int, sample: bool = True, r0: int = 0, hook=None) -> torch.Tensor:
+        """One decode step of rows ``r0 .. r0+B`` (every per-row buffer is sliced,
+        so two disjoint row ranges can run as independent sub-batches)."""
+        r1 = r0 + B
+        tok = self.tok_buf[r0:r1]
+        pos = self.pos[r0:r1]
+        slot = self.slot_id[r0:r1]
+        done = self.done[r0:r1]
+        scratch = (self.attn_scratch[0][r0:r1], self.attn_scratch[1][r0:r1])
         x = F.embedding(tok.long(), self.w.embed)
 
         def kc(i):
@@ -334,14 +348,44 @@ class ExtractionEngine:
 
         def attn(i, q, out):
             ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
-                            done=self.done, impl=self.cfg.decode_attn, scratch=self.attn_scratch)
+                            done=done, impl=self.cfg.decode_attn, scratch=scratch)
 
-        h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0,
+                          hook=hook)
         logits = self._logits(h)
         if sample:
-            ops.fsm_sample(logits, self.fsm, self.state[:B], tok, self.out_buf[:B], self.out_len[:B],
-                           self.done[:B], pos, slot, self.cfg.temperature, self.cfg.seed)
+            ops.fsm_sample(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
+                           done, pos, slot, self.cfg.temperature, self.cfg.seed)
         return logits
+
+    def _side_stream(self) -> torch.cuda.Stream:
+        if self._s2 is None:
+            self._s2 = torch.cuda.Stream(device=self.device)
+        return self._s2
+
+    def _decode_steps_split(self, B: int, n: int, s2: torch.cuda.Stream) -> None:
+        """``n`` decode steps of rows ``[0, B)`` as two independent half-batches on
+        two streams (fork/join), the second half started one QKV GEMM behind the
+        first so that one half's memory-bound attention can overlap the other
+        half's MFMA GEMMs (nano-batch overlap).  Rows never interact within a
+        step, so the result is identical to :meth:`_decode_step` on all rows."""
+        h = B // 2
+        main = torch.cuda.current_stream(self.device)
+        if self.cfg.split_offset:
+            # the second half waits for the first half's layer-0 QKV GEMM: from then
+            # on half A is in attention while half B runs its GEMMs, and so on
+            ev = torch.cuda.Event()
+            hook = (lambda i: ev.record() if i == 0 else None)
+        else:
+            s2.wait_stream(main)
+            hook = None
+        for k in range(n):
+            self._decode_step(h, r0=0, hook=hook if k == 0 else None)
+            with torch.cuda.stream(s2):
+                if k == 0 and hook is not None:
+                    s2.wait_event(ev)
+                self._decode_step(B - h, r0=h)
+        main.wait_stream(s2)
 
     # ------------------------------------------------------------ debugging
     def debug_logits(self, bodies: Sequence[str], forced: Sequence[Sequence[int]] = ()) -> List[torch.Tensor]:
@@ -415,11 +459,16 @@ class ExtractionEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._pool = torch.cuda.graph_pool_handle()
+        split = self.cfg.split_decode
+        s2 = torch.cuda.Stream(device=self.device) if split else None
         for B in sorted(sizes, reverse=True):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._pool):
-                for _ in range(self.cfg.steps_per_graph):
-                    self._decode_step(B)
+                if split and B >= split:
+                    self._decode_steps_split(B, self.cfg.steps_per_graph, s2)
+                else:
+                    for _ in range(self.cfg.steps_per_graph):
+                        self._decode_step(B)
             self.graphs[B] = g
         torch.cuda.synchronize(self.device)
 
@@ -470,7 +519,20 @@ class ExtractionEngine:
                 items.append(it)
                 ntok += len(it.ids)
                 self.active[r] = it.key
-            self._prefill(rows, items)
+            split = self.cfg.split_prefill
+            if split and ntok >= split and len(items) >= 2:
+                # two independent halves on two streams (disjoint rows and KV slots):
+                # one half's latency-bound attention overlaps the other's GEMMs
+                h = len(items) // 2
+                main = torch.cuda.current_stream(self.device)
+                s2 = self._side_stream()
+                s2.wait_stream(main)
+                self._prefill(rows[:h], items[:h])
+                with torch.cuda.stream(s2):
+                    self._prefill(rows[h:], items[h:])
+                main.wait_stream(s2)
+            else:
+                self._prefill(rows, items)
 
     def _decode_answer(self, toks: List[int]) -> Dict[str, Optional[str]]:
         vals = self.fsm.split_fields(toks)

@@ -120,3 +120,35 @@ def test_row_compaction_preserves_results():
     assert outs[0] == outs[1]
     assert stats[0].compactions > 0 and stats[0].rows_moved > 0 and stats[1].compactions == 0
     assert stats[0].decode_row_steps < stats[1].decode_row_steps
+
+
+@pytest.mark.parametrize("model", ["tiny", "smollm-135m"])
+def test_split_decode_matches_single_batch(model):
+    """Two half-batches on two streams (nano-batch overlap) give exactly the
+    single-batch answers: rows never interact inside a decode step."""
+    w = ExtractorWeights(CONFIGS[model], device="cuda", seed=13)
+    w.requires_grad_(False)
+    tk = load_tokenizer()
+    bodies = generate_bodies(96, seed=6)
+    outs = []
+    for split in (0, 32):
+        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=128, steps_per_graph=2, buckets=(32, 64, 128),
+                                                   split_decode=split))
+        outs.append(eng.run(bodies))
+        del eng
+    assert outs[0] == outs[1]
+
+
+def test_split_prefill_matches_single_batch():
+    """Prefill in two halves on two streams == one prefill batch."""
+    w = ExtractorWeights(CONFIGS["smollm-135m"], device="cuda", seed=17)
+    w.requires_grad_(False)
+    tk = load_tokenizer()
+    bodies = generate_bodies(64, seed=8)
+    outs = []
+    for split in (0, 64):
+        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=64, steps_per_graph=2, buckets=(64,),
+                                                   split_prefill=split))
+        outs.append(eng.run(bodies))
+        del eng
+    assert outs[0] == outs[1]

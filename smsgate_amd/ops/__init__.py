@@ -170,9 +170,13 @@ GEMM_SWIGLU_ONLY = {10}  # a 256x256 plain-output tile does not fit the LDS stag
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
-def gemm_cfg(M: int, N: int, min_tiles: int = 480) -> int:
+GEMM_MIN_TILES = int(os.environ.get("SMSGATE_GEMM_MIN_TILES", "480"))
+
+
+def gemm_cfg(M: int, N: int, min_tiles: Optional[int] = None) -> int:
     """Tile config for an M×N output: the biggest tile that still gives ≳2 blocks per CU
     (256 CUs), else the config with the most blocks."""
+    min_tiles = GEMM_MIN_TILES if min_tiles is None else min_tiles
     best, best_tiles = -1, -1
     for cfg in range(9):  # the 4-wave configs; 8-wave ones are explicit opt-ins
         bm, bn = GEMM_TILES[cfg]

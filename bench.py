@@ -55,6 +55,7 @@ def _args(argv=None):
     p.add_argument("--split-decode", type=int, default=4096,
                    help="decode buckets >= N run as two half-batches on two streams (0 = off)")
     p.add_argument("--no-split-offset", action="store_true", help="start both halves together")
+    p.add_argument("--no-gc-freeze", action="store_true", help="keep the default GC thresholds in the rank process")
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--cpu-echo-engine", action="store_true",
@@ -111,6 +112,10 @@ def run_replica(args, rank: int, world: int, local: int):
                               split_decode=args.split_decode, split_offset=not args.no_split_offset,
                               split_prefill=args.split_prefill)
     init_s = time.perf_counter() - t_init
+    if not args.no_gc_freeze:
+        from smsgate_amd.serving import freeze_gc_for_launch_loop
+
+        freeze_gc_for_launch_loop()
     coord = Coordinator(engine, conns)
     coord.wait_all("ready")
 

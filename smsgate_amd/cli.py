@@ -199,6 +199,9 @@ def _engine_server(a) -> None:
 
     start_metrics_server(env_var="ENGINE_METRICS_PORT", default=9104)
     exporter = EngineMetricsExporter(eng).start()
+    from .serving import freeze_gc_for_launch_loop
+
+    freeze_gc_for_launch_loop()
     try:
         EngineServer(eng).serve_listener(path, stop)
     finally:

@@ -55,6 +55,8 @@ def _args(argv=None):
     p.add_argument("--split-decode", type=int, default=4096,
                    help="decode buckets >= N run as two half-batches on two streams (0 = off)")
     p.add_argument("--no-split-offset", action="store_true", help="start both halves together")
+    p.add_argument("--split-graphs", type=int, default=2, choices=[1, 2],
+                   help="1 = both halves in one fork/join graph, 2 = one graph per half on two streams")
     p.add_argument("--no-gc-freeze", action="store_true", help="keep the default GC thresholds in the rank process")
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
@@ -109,7 +111,7 @@ def run_replica(args, rank: int, world: int, local: int):
         engine = build_engine(args.model, device=f"cuda:{local}", random_init=True, max_slots=args.max_slots,
                               steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
                               buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
-                              split_decode=args.split_decode, split_offset=not args.no_split_offset,
+                              split_decode=args.split_decode, split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
                               split_prefill=args.split_prefill)
     init_s = time.perf_counter() - t_init
     if not args.no_gc_freeze:

@@ -68,6 +68,7 @@ class EngineConfig:
     # nano-batch overlap (measured +10% msgs/s at 8192 slots, profiles/r01b_split_ab.txt):
     split_decode: int = 4096  # >0: decode buckets >= this run as two half-batches on two streams
     split_offset: bool = True  # start the second half one kernel behind the first
+    split_graphs: int = 2  # 1 = both halves in one fork/join graph; 2 = one graph per half, two streams
     split_prefill: int = 8192  # >0: prefill batches of >= this many tokens run as two halves on two streams
 
 
@@ -461,13 +462,28 @@ class ExtractionEngine:
         self._pool = torch.cuda.graph_pool_handle()
         split = self.cfg.split_decode
         s2 = torch.cuda.Stream(device=self.device) if split else None
+        pool_b = torch.cuda.graph_pool_handle() if split and self.cfg.split_graphs == 2 else None
+        n = self.cfg.steps_per_graph
         for B in sorted(sizes, reverse=True):
+            if split and B >= split and pool_b is not None:
+                # one graph per half, replayed concurrently on two streams (_run_decode);
+                # separate memory pools: the halves run at the same time
+                h = B // 2
+                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga, pool=self._pool):
+                    for _ in range(n):
+                        self._decode_step(h, r0=0)
+                with torch.cuda.graph(gb, pool=pool_b):
+                    for _ in range(n):
+                        self._decode_step(B - h, r0=h)
+                self.graphs[B] = (ga, gb)
+                continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._pool):
                 if split and B >= split:
-                    self._decode_steps_split(B, self.cfg.steps_per_graph, s2)
+                    self._decode_steps_split(B, n, s2)
                 else:
-                    for _ in range(self.cfg.steps_per_graph):
+                    for _ in range(n):
                         self._decode_step(B)
             self.graphs[B] = g
         torch.cuda.synchronize(self.device)
@@ -475,7 +491,16 @@ class ExtractionEngine:
     def _run_decode(self, B: int) -> None:
         t0 = time.perf_counter()
         g = self.graphs.get(B)
-        if g is not None:
+        if isinstance(g, tuple):
+            main = torch.cuda.current_stream(self.device)
+            s2 = self._side_stream()
+            s2.wait_stream(main)
+            g[0].replay()
+            with torch.cuda.stream(s2):
+                g[1].replay()
+            main.wait_stream(s2)
+            n = self.cfg.steps_per_graph
+        elif g is not None:
             g.replay()
             n = self.cfg.steps_per_graph
         else:

@@ -55,6 +55,7 @@ def _args(argv=None):
     p.add_argument("--split-decode", type=int, default=4096,
                    help="decode buckets >= N run as two half-batches on two streams (0 = off)")
     p.add_argument("--no-split-offset", action="store_true", help="start both halves together")
+    p.add_argument("--split-parts", type=int, default=2, help="parts of a split decode bucket")
     p.add_argument("--split-graphs", type=int, default=2, choices=[1, 2],
                    help="1 = both halves in one fork/join graph, 2 = one graph per half on two streams")
     p.add_argument("--no-gc-freeze", action="store_true", help="keep the default GC thresholds in the rank process")
@@ -112,6 +113,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
                               buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
                               split_decode=args.split_decode, split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
+                              split_parts=args.split_parts,
                               split_prefill=args.split_prefill)
     init_s = time.perf_counter() - t_init
     if not args.no_gc_freeze:

@@ -68,7 +68,8 @@ class EngineConfig:
     # nano-batch overlap (measured +10% msgs/s at 8192 slots, profiles/r01b_split_ab.txt):
     split_decode: int = 4096  # >0: decode buckets >= this run as two half-batches on two streams
     split_offset: bool = True  # start the second half one kernel behind the first
-    split_graphs: int = 2  # 1 = both halves in one fork/join graph; 2 = one graph per half, two streams
+    split_graphs: int = 2  # 1 = both halves in one fork/join graph; 2 = one graph per part, one stream each
+    split_parts: int = 2  # parts of a split decode bucket (split_graphs=2)
     split_prefill: int = 8192  # >0: prefill batches of >= this many tokens run as two halves on two streams
 
 
@@ -186,7 +187,7 @@ class ExtractionEngine:
         ]
         self._snap_flip = 0
         self._pending: Optional[_Snapshot] = None
-        self._s2: Optional[torch.cuda.Stream] = None  # side stream of the split prefill
+        self._sides: List[torch.cuda.Stream] = []  # side streams of the split decode / prefill
         self._compute_prefix()
         if ec.use_graphs:
             self._capture_graphs()
@@ -360,9 +361,12 @@ class ExtractionEngine:
         return logits
 
     def _side_stream(self) -> torch.cuda.Stream:
-        if self._s2 is None:
-            self._s2 = torch.cuda.Stream(device=self.device)
-        return self._s2
+        return self._side_streams(1)[0]
+
+    def _side_streams(self, k: int) -> List[torch.cuda.Stream]:
+        while len(self._sides) < k:
+            self._sides.append(torch.cuda.Stream(device=self.device))
+        return self._sides[:k]
 
     def _decode_steps_split(self, B: int, n: int, s2: torch.cuda.Stream) -> None:
         """``n`` decode steps of rows ``[0, B)`` as two independent half-batches on
@@ -462,21 +466,24 @@ class ExtractionEngine:
         self._pool = torch.cuda.graph_pool_handle()
         split = self.cfg.split_decode
         s2 = torch.cuda.Stream(device=self.device) if split else None
-        pool_b = torch.cuda.graph_pool_handle() if split and self.cfg.split_graphs == 2 else None
+        parts = max(2, self.cfg.split_parts)
+        pools = [self._pool] + [torch.cuda.graph_pool_handle() for _ in range(parts - 1)] \
+            if split and self.cfg.split_graphs == 2 else None
         n = self.cfg.steps_per_graph
         for B in sorted(sizes, reverse=True):
-            if split and B >= split and pool_b is not None:
-                # one graph per half, replayed concurrently on two streams (_run_decode);
-                # separate memory pools: the halves run at the same time
-                h = B // 2
-                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(ga, pool=self._pool):
-                    for _ in range(n):
-                        self._decode_step(h, r0=0)
-                with torch.cuda.graph(gb, pool=pool_b):
-                    for _ in range(n):
-                        self._decode_step(B - h, r0=h)
-                self.graphs[B] = (ga, gb)
+            if split and B >= split and pools is not None:
+                # one graph per part, replayed concurrently on `parts` streams (_run_decode);
+                # one memory pool per part: the parts run at the same time
+                bounds = [B * k // parts for k in range(parts + 1)]
+                bounds = [b - b % 64 for b in bounds[:-1]] + [B]  # 64-row aligned parts
+                gs = []
+                for k in range(parts):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pools[k]):
+                        for _ in range(n):
+                            self._decode_step(bounds[k + 1] - bounds[k], r0=bounds[k])
+                    gs.append(g)
+                self.graphs[B] = tuple(gs)
                 continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._pool):
@@ -493,12 +500,15 @@ class ExtractionEngine:
         g = self.graphs.get(B)
         if isinstance(g, tuple):
             main = torch.cuda.current_stream(self.device)
-            s2 = self._side_stream()
-            s2.wait_stream(main)
+            sides = self._side_streams(len(g) - 1)
+            for s in sides:
+                s.wait_stream(main)
             g[0].replay()
-            with torch.cuda.stream(s2):
-                g[1].replay()
-            main.wait_stream(s2)
+            for s, gk in zip(sides, g[1:]):
+                with torch.cuda.stream(s):
+                    gk.replay()
+            for s in sides:
+                main.wait_stream(s)
             n = self.cfg.steps_per_graph
         elif g is not None:
             g.replay()

@@ -122,9 +122,9 @@ def test_row_compaction_preserves_results():
     assert stats[0].decode_row_steps < stats[1].decode_row_steps
 
 
-@pytest.mark.parametrize("graphs", [1, 2])
+@pytest.mark.parametrize("graphs,parts", [(1, 2), (2, 2), (2, 3)])
 @pytest.mark.parametrize("model", ["tiny", "smollm-135m"])
-def test_split_decode_matches_single_batch(model, graphs):
+def test_split_decode_matches_single_batch(model, graphs, parts):
     """Two half-batches on two streams (nano-batch overlap) give exactly the
     single-batch answers: rows never interact inside a decode step."""
     w = ExtractorWeights(CONFIGS[model], device="cuda", seed=13)
@@ -134,7 +134,8 @@ def test_split_decode_matches_single_batch(model, graphs):
     outs = []
     for split in (0, 32):
         eng = ExtractionEngine(w, tk, EngineConfig(max_slots=128, steps_per_graph=2, buckets=(32, 64, 128),
-                                                   split_decode=split, split_graphs=graphs))
+                                                   split_decode=split, split_graphs=graphs,
+                                                   split_parts=parts))
         outs.append(eng.run(bodies))
         del eng
     assert outs[0] == outs[1]

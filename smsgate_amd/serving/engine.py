@@ -476,14 +476,15 @@ class ExtractionEngine:
                 # one memory pool per part: the parts run at the same time
                 bounds = [B * k // parts for k in range(parts + 1)]
                 bounds = [b - b % 64 for b in bounds[:-1]] + [B]  # 64-row aligned parts
+                bounds = sorted(set(bounds))  # a bucket too small for `parts` gets fewer
                 gs = []
-                for k in range(parts):
+                for k in range(len(bounds) - 1):
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=pools[k]):
                         for _ in range(n):
                             self._decode_step(bounds[k + 1] - bounds[k], r0=bounds[k])
                     gs.append(g)
-                self.graphs[B] = tuple(gs)
+                self.graphs[B] = tuple(gs) if len(gs) > 1 else gs[0]
                 continue
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._pool):

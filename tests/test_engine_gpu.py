@@ -130,10 +130,10 @@ def test_split_decode_matches_single_batch(model, graphs, parts):
     w = ExtractorWeights(CONFIGS[model], device="cuda", seed=13)
     w.requires_grad_(False)
     tk = load_tokenizer()
-    bodies = generate_bodies(96, seed=6)
+    bodies = generate_bodies(200, seed=6)
     outs = []
-    for split in (0, 32):
-        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=128, steps_per_graph=2, buckets=(32, 64, 128),
+    for split in (0, 64):  # bucket 256 -> parts of 64/64/128 rows (parts=3) or 128/128
+        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=256, steps_per_graph=2, buckets=(32, 64, 256),
                                                    split_decode=split, split_graphs=graphs,
                                                    split_parts=parts))
         outs.append(eng.run(bodies))

@@ -91,6 +91,9 @@ def main():
                                                            done=done, impl="mfma_v1"))
     res["attn_decode_valu"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out,
                                                              1 / math.sqrt(D), done=done, impl="valu"))
+    for impl in ("grouped", "split2", "split4", "split8"):
+        res[f"attn_decode_{impl}"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out,
+                                                                    1 / math.sqrt(D), done=done, impl=impl))
     kv_bytes = B * nkv * a.ctx * D * 2 * 2
     res["attn_decode_own_kv_GBps"] = round(kv_bytes / (res["attn_decode"] * 1e-6) / 1e9, 1)
     for name, (n, k) in {"qkv": (cfg.qkv_out, H), "o": (H, nh * D), "gate_up": (2 * I, H), "down": (H, I),
@@ -124,7 +127,7 @@ def main():
     # QKV projection + RoPE + KV scatter: fused epilogue vs GEMM + separate kernel
     Xq, Wq = rnd(B, H), rnd(cfg.qkv_out, H)
     qo = torch.empty(B, nh, D, dtype=bf, device=dev)
-    for c in (1, 3, 5):
+    for c in (1, 3, 5, 17, 18):
         res[f"qkv_rope_fused_cfg{c}"] = timeit(lambda: ops.gemm_qkv_rope(Xq, Wq, 1e-5, pos, slot, cs, qo, kc, vt, nh, nkv,
                                                                           P0, cfg=c))
     res["qkv_rope_fused_auto"] = timeit(lambda: ops.gemm_qkv_rope(Xq, Wq, 1e-5, pos, slot, cs, qo, kc, vt, nh, nkv, P0))

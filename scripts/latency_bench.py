@@ -60,20 +60,31 @@ def main() -> None:
     p.add_argument("--seconds", type=float, default=6.0)
     p.add_argument("--max-slots", type=int, default=8192)
     p.add_argument("--out", default=None)
+    p.add_argument("--attn-small-rows", type=int, default=None,
+                   help="decode buckets up to N rows use --attn-small (default: the engine's)")
+    p.add_argument("--attn-small", default="split4")
+    p.add_argument("--gemm-small-m", type=int, default=None, help="ops.GEMM_SMALL_M (32-row GEMM tiles up to M)")
     a = p.parse_args()
     import torch
 
+    from smsgate_amd import ops
     from smsgate_amd.parse.backends.local_llm import build_engine
     from smsgate_amd.parse.text import normalize_body
     from smsgate_amd.utils.synth import generate_bodies
 
+    if a.gemm_small_m is not None:
+        ops.GEMM_SMALL_M = a.gemm_small_m
+    kw = {} if a.attn_small_rows is None else dict(decode_attn_small_rows=a.attn_small_rows,
+                                                   decode_attn_small=a.attn_small)
     eng = build_engine("smollm-135m", device="cuda", random_init=True, max_slots=a.max_slots, steps_per_graph=2,
-                       buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192))
+                       buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192), **kw)
+    arm = {"attn_small_rows": eng.cfg.decode_attn_small_rows, "attn_small": eng.cfg.decode_attn_small,
+           "gemm_small_m": ops.GEMM_SMALL_M}
     bodies = [normalize_body(b) for b in generate_bodies(20000, seed=5)]
     ids = eng.tok.message_ids(bodies, eng.cfg.max_body_tokens)
     run_rate(eng, ids, 2000.0, 1.0, seed=0)  # warm-up
     torch.cuda.synchronize()
-    res = [run_rate(eng, ids, float(r), a.seconds, seed=i + 1) for i, r in enumerate(a.rates.split(","))]
+    res = [dict(run_rate(eng, ids, float(r), a.seconds, seed=i + 1), **arm) for i, r in enumerate(a.rates.split(","))]
     for r in res:
         print(json.dumps(r), flush=True)
     if a.out:

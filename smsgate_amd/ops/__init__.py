@@ -69,6 +69,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_attn_decode_cascade.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_vp, _vp, _vp]
     lib.sg_attn_decode_grouped.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_grouped.restype = _c_int
+    lib.sg_attn_decode_split.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_c_int, _vp]
+    lib.sg_attn_decode_split.restype = _c_int
     lib.sg_attn_decode_cascade.restype = _c_int
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
@@ -164,21 +166,26 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 
 GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 64), 5: (64, 64), 6: (64, 64),
               7: (128, 128), 8: (64, 128), 9: (256, 128), 10: (256, 256), 11: (128, 256), 12: (256, 64),
-              13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64)}
-# cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages)
+              13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64)}
+# cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
+# 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 GEMM_SWIGLU_ONLY = {10}  # a 256x256 plain-output tile does not fit the LDS staging
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
 GEMM_MIN_TILES = int(os.environ.get("SMSGATE_GEMM_MIN_TILES", "480"))
+# M at or below which the 32-row tile (cfg 17) competes in gemm_cfg; 0 = never
+GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 
 
 def gemm_cfg(M: int, N: int, min_tiles: Optional[int] = None) -> int:
     """Tile config for an M×N output: the biggest tile that still gives ≳2 blocks per CU
-    (256 CUs), else the config with the most blocks."""
+    (256 CUs), else the config with the most blocks (the 32-row tile only for M <=
+    ``GEMM_SMALL_M``)."""
     min_tiles = GEMM_MIN_TILES if min_tiles is None else min_tiles
     best, best_tiles = -1, -1
-    for cfg in range(9):  # the 4-wave configs; 8-wave ones are explicit opt-ins
+    # the 4-wave configs; 8-wave ones and the 4-stage 32-row tile are explicit opt-ins
+    for cfg in list(range(9)) + ([17] if M <= GEMM_SMALL_M else []):
         bm, bn = GEMM_TILES[cfg]
         if N % bn:
             continue
@@ -257,8 +264,9 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
         return
     if cfg is None:
         # 64x64 tiles: the V^T scatter of the epilogue favours more, smaller tiles
-        # (kbench, B=4096/8192: 17.8/27.6 us vs 22.0/31.3 us with 128x64)
-        cfg = 3
+        # (kbench, B=4096/8192: 17.8/27.6 us vs 22.0/31.3 us with 128x64); 32-row
+        # tiles on small decode buckets
+        cfg = 17 if M <= GEMM_SMALL_M else 3
     rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
                                          _stream())
@@ -340,7 +348,10 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
     all of them, then each sequence's own keys with per-column masks (no scratch);
     ``"mfma"``: single-pass transposed MFMA kernel (S^T = K·Q^T, O^T = V^T·P^T);
     ``"mfma_v1"``: S = Q·K^T with P through LDS; ``"valu"``: vector-ALU variant —
-    kept for A/B measurement.  MFMA kernels need ``Lmax``, padded prefix % 32 == 0."""
+    kept for A/B measurement; ``"split2"``/``"split4"``/``"split8"``: key-split, N
+    waves per (row, kv head) share the row's key tiles and merge their softmax
+    states in LDS (the small-batch kernel: many short waves instead of few long
+    ones).  MFMA kernels need ``Lmax``, padded prefix % 32 == 0."""
     B, nh, D = q.shape
     S, nkv, Lmax, _ = k_cache.shape
     P0pad = pk.shape[1]
@@ -359,6 +370,14 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
                                         _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, _p(pre_o),
                                         _p(pre_lse), _stream())
         _check(rc, "attn_decode[cascade]")
+        return out
+    if impl.startswith("split"):
+        nwv = int(impl[5:])
+        if nwv not in (2, 4, 8):
+            raise ValueError(f"attn_decode: {impl!r} (split2 / split4 / split8)")
+        _check(lib.sg_attn_decode_split(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk),
+                                        _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D, Lmax, scale, nwv, _stream()),
+               f"attn_decode[{impl}]")
         return out
     fn = {"mfma": lib.sg_attn_decode, "mfma_v1": lib.sg_attn_decode_v1, "valu": lib.sg_attn_decode_valu,
           "grouped": lib.sg_attn_decode_grouped}[impl]

@@ -387,6 +387,7 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
 //   8: 64x128  (1x4) 3st   9: 256x128 (4x2) 2st, 8 waves   10: 256x256 (2x4) 2st, 8 waves
 //  11: 128x256 (2x4) 2st, 8 waves   12: 256x64 (4x2) 2st, 8 waves   13: 128x128 (2x4) 2st, 8 waves
 //  14: 256x128 (4x2) 3st, 8 waves   15: 128x256 (2x4) 3st, 8 waves   16: 256x64 (4x2) 4st, 8 waves
+//  17: 32x64 (2x2) 2st   18: 32x64 (2x2) 4st — small-M decode buckets: twice the tiles of 64x64
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -413,8 +414,8 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, hipStream_t stream) {
-  static const int BNs[17] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64};
-  if (cfg < 0 || cfg > 16) return -1;
+  static const int BNs[19] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64};
+  if (cfg < 0 || cfg > 18) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
 #define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream
@@ -435,14 +436,16 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     case 13: return dispatch_epi<128, 128, 2, 4, 2>(SG_ARGS);
     case 14: return dispatch_epi<256, 128, 4, 2, 3>(SG_ARGS);
     case 15: return dispatch_epi<128, 256, 2, 4, 3>(SG_ARGS);
-    default: return dispatch_epi<256, 64, 4, 2, 4>(SG_ARGS);
+    case 16: return dispatch_epi<256, 64, 4, 2, 4>(SG_ARGS);
+    case 17: return dispatch_epi<32, 64, 2, 2, 2>(SG_ARGS);
+    default: return dispatch_epi<32, 64, 2, 2, 4>(SG_ARGS);
   }
 #undef SG_ARGS
 }
 
 // QKV projection with the RMSNorm prologue and the RoPE + KV-cache epilogue
 // (replaces gemm + sg_rope_qkv_cache).  W: [(nh + 2 nkv)·64, K], norm folded in.
-// cfg must have BN = 64 (1, 3 or 5).
+// cfg must have BN = 64 (1, 3, 5, 17 or 18).
 int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float eps, int cfg, const int* pos,
                      const int* slot, const void* cos_sin, void* q_out, void* k_cache, void* vt_cache, int nh, int nkv,
                      int Lmax, int p0, hipStream_t stream) {
@@ -454,6 +457,8 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
     case 1: return launch<128, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
     case 3: return launch<64, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
     case 5: return launch<64, 64, 2, 2, 3, true, 3>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
+    case 17: return launch<32, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
+    case 18: return launch<32, 64, 2, 2, 3, true, 4>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
     default: return -1;
   }
 }

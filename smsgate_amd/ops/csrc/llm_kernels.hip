@@ -1237,6 +1237,87 @@ __global__ void __launch_bounds__(64) attn_grouped_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Key-split decode attention (small batches): NWV waves per (row, kv head) deal
+// the row's 32-key tiles — shared prefix first, then its own keys — round-robin;
+// each wave keeps its own online-softmax state and wave 0 merges the NWV states
+// through LDS.  At a few hundred rows the grouped kernel launches too few waves
+// and each walks ~15 dependent tiles; here each wave walks ceil(tiles / NWV),
+// so the step latency shrinks with NWV while the bytes read stay the same.
+// grid = (B, nkv), NWV waves per block.
+// ---------------------------------------------------------------------------
+template <int NWV>
+__global__ void __launch_bounds__(NWV * 64) attn_split_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
+    uint16_t* __restrict__ out, int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  __shared__ float red[NWV][64][18];  // per wave and lane: o[16], m, l
+  const int b = blockIdx.x, kh = blockIdx.y, tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  if (done != nullptr && done[b]) return;  // block-uniform, before any barrier
+  const int G = nh / nkv, g4 = l >> 4, r16 = l & 15;
+  const int own = pos[b] + 1;
+  const int sl = slot[b];
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+  const size_t qrow = (size_t)b * nh + kh * G + (r16 < G ? r16 : 0);
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);
+    if (r16 >= G) v = make_uint4(0, 0, 0, 0);
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  const int npre = (P0 + 31) >> 5, ntiles = npre + ((own + 31) >> 5);
+  for (int t = w; t < ntiles; t += NWV) {
+    const bool pre = t < npre;
+    const int kt = (pre ? t : t - npre) * 32, nval = pre ? P0 : own;
+    uint4 kc[2][2], vc[4];
+    st_load_tile(pre ? kpre : kself, pre ? vpre : vself, kt, g4, r16, kt + 16 < nval, kc, vc);
+    st_tile(qb, kc, vc, kt, nval, g4, scale_log2, m, lsum, o);
+  }
+  float* mine = red[w][l];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mine[4 * n + i] = o[n][i];
+  mine[16] = m;
+  mine[17] = lsum;
+  __syncthreads();
+  if (w != 0 || r16 >= G) return;
+  float M = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < NWV; ++v) M = fmaxf(M, red[v][l][16]);
+  float acc[16], L = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int v = 0; v < NWV; ++v) {
+    const float mv = red[v][l][16];
+    if (mv == -INFINITY) continue;  // this wave saw no valid key
+    const float f = exp2f(mv - M);
+    L += f * red[v][l][17];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] += f * red[v][l][j];
+  }
+  const float inv = 1.f / L;
+  uint16_t* orow = out + qrow * D;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    uint2 wv;
+    wv.x = (uint32_t)f2bf(acc[4 * n] * inv) | ((uint32_t)f2bf(acc[4 * n + 1] * inv) << 16);
+    wv.y = (uint32_t)f2bf(acc[4 * n + 2] * inv) | ((uint32_t)f2bf(acc[4 * n + 3] * inv) << 16);
+    *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = wv;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Schema-FSM constrained sampling + FSM transition, fully on the GPU (so many
 // decode steps can be replayed from one captured graph without a host sync).
 // One 256-thread block per sequence row.
@@ -1434,6 +1515,24 @@ int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const
   hipLaunchKernelGGL(attn_grouped_kernel, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// Key-split decode attention (small batches): nwv waves per (row, kv head).
+int sg_attn_decode_split(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                         const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B,
+                         int nh, int nkv, int D, int Lmax, float scale, int nwv, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+#define SG_SPLIT(N)                                                                                                \
+  hipLaunchKernelGGL(attn_split_kernel<N>, dim3(B, nkv), dim3(N * 64), 0, stream, (const uint16_t*)q, pos, slot, \
+                     done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,             \
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f)
+  if (nwv == 2) SG_SPLIT(2);
+  else if (nwv == 4) SG_SPLIT(4);
+  else if (nwv == 8) SG_SPLIT(8);
+  else return -1;
+#undef SG_SPLIT
   return (int)hipGetLastError();
 }
 

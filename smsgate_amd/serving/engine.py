@@ -62,7 +62,11 @@ class EngineConfig:
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
     fused_gemm: bool = True  # csrc/gemm_kernels.hip (norm prologue, residual/SwiGLU epilogues) vs hipBLASLt
     compact: bool = True  # row compaction so the decode bucket tracks the active count
-    decode_attn: str = "grouped"  # ops.attn_decode impl: grouped | cascade | mfma | mfma_v1 | valu
+    decode_attn: str = "grouped"  # ops.attn_decode impl: grouped | cascade | mfma | mfma_v1 | valu | splitN
+    # decode (sub-)batches of at most this many rows use `decode_attn_small` (key-split:
+    # many short waves instead of few long ones — the low-load latency path); 0 = off
+    decode_attn_small_rows: int = 0
+    decode_attn_small: str = "split4"
     lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
     # nano-batch overlap (measured +10% msgs/s at 8192 slots, profiles/r01b_split_ab.txt):
@@ -341,6 +345,7 @@ class ExtractionEngine:
         done = self.done[r0:r1]
         scratch = (self.attn_scratch[0][r0:r1], self.attn_scratch[1][r0:r1])
         x = F.embedding(tok.long(), self.w.embed)
+        impl = self.cfg.decode_attn_small if B <= self.cfg.decode_attn_small_rows else self.cfg.decode_attn
 
         def kc(i):
             return self.k_cache[i]
@@ -350,7 +355,7 @@ class ExtractionEngine:
 
         def attn(i, q, out):
             ops.attn_decode(q, pos, slot, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
-                            done=done, impl=self.cfg.decode_attn, scratch=scratch)
+                            done=done, impl=impl, scratch=scratch)
 
         h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0,
                           hook=hook)

@@ -93,6 +93,30 @@ def test_fused_and_unfused_engines_agree_on_135m_logits():
         assert (a - b).abs().max().item() <= 0.05 * scale + 0.05
 
 
+@pytest.mark.parametrize("impl", ["split2", "split4"])
+def test_small_bucket_attention_matches_grouped(impl):
+    """Key-split attention on small decode buckets (the low-load path) gives the
+    grouped kernel's logits on the production shape, and the graph-captured engine
+    still produces schema-valid answers with it."""
+    w = ExtractorWeights(CONFIGS["smollm-135m"], device="cuda", seed=19)
+    w.requires_grad_(False)
+    tk = load_tokenizer()
+    bodies = reference_cases()
+    outs = []
+    for rows in (0, 64):
+        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=16, use_graphs=False, buckets=(16,),
+                                                   decode_attn_small=impl, decode_attn_small_rows=rows))
+        outs.append(eng.debug_logits(bodies, [[5, 6], [7, 8], [9, 10]]))
+        del eng
+    for a, b in zip(*outs):
+        scale = b.abs().max().item()
+        assert (a - b).abs().max().item() <= 0.02 * scale + 0.02
+    eng = ExtractionEngine(w, tk, EngineConfig(max_slots=64, steps_per_graph=2, buckets=(32, 64),
+                                               decode_attn_small=impl, decode_attn_small_rows=32))
+    res = eng.run(generate_bodies(40, seed=2))
+    assert all(r is not None and r["txn_type"] in ("debit", "credit", "otp", "unknown") for r in res)
+
+
 def test_row_compaction_preserves_results():
     """Greedy answers are identical with and without row compaction.  Two staggered
     admission waves (random weights -> every answer has the same length, so waves

@@ -128,7 +128,7 @@ def test_attn_prefill(P0, heads, impl):
         o += n
 
 
-@pytest.mark.parametrize("impl", ["grouped", "cascade", "mfma", "mfma_v1", "valu"])
+@pytest.mark.parametrize("impl", ["grouped", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4", "split8"])
 @pytest.mark.parametrize("P0", [0, 75])
 def test_attn_decode(P0, impl):
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224  # MFMA decode tiles need Lmax % 32 == 0
@@ -200,13 +200,15 @@ def test_fsm_sample_greedy_and_transitions():
         assert allowed[int(states_h[b]), int(tok[b])]
 
 
-@pytest.mark.parametrize("cfg", sorted(ops.GEMM_TILES))
-@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (100, 576, 576), (777, 960, 576), (256, 3072, 576),
-                                   (130, 576, 1536), (64, 8192, 576)])
+def _tile_cases(shapes):
+    """(cfg, *shape) for every tile config whose BN divides N (others cannot run it)."""
+    return [(cfg, *s) for cfg in sorted(ops.GEMM_TILES) for s in shapes
+            if cfg not in ops.GEMM_SWIGLU_ONLY and s[1] % ops.GEMM_TILES[cfg][1] == 0]
+
+
+@pytest.mark.parametrize("cfg,M,N,K", _tile_cases([(1, 128, 64), (100, 576, 576), (777, 960, 576),
+                                                   (256, 3072, 576), (130, 576, 1536), (64, 8192, 576)]))
 def test_gemm_store_and_norm(cfg, M, N, K):
-    bm, bn = ops.GEMM_TILES[cfg]
-    if N % bn or cfg in ops.GEMM_SWIGLU_ONLY:
-        pytest.skip("N not a multiple of the tile")
     a = _bf(M, K, seed=11)
     w = _bf(N, K, scale=K ** -0.5, seed=12)
     nw = _bf(K, scale=0.1, seed=13) + 1
@@ -216,13 +218,8 @@ def test_gemm_store_and_norm(cfg, M, N, K):
     torch.testing.assert_close(out_n.float(), ops.ref_gemm(a, w, norm_eps=1e-5, norm_w=nw), atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("cfg", sorted(ops.GEMM_TILES))
-@pytest.mark.parametrize("M", [1, 333, 2048])
-def test_gemm_residual_inplace(cfg, M):
-    K, N = 1536, 576
-    bm, bn = ops.GEMM_TILES[cfg]
-    if N % bn or cfg in ops.GEMM_SWIGLU_ONLY:
-        pytest.skip("N not a multiple of the tile")
+@pytest.mark.parametrize("cfg,M,N,K", _tile_cases([(1, 576, 1536), (333, 576, 1536), (2048, 576, 1536)]))
+def test_gemm_residual_inplace(cfg, M, N, K):
     a = _bf(M, K, seed=21)
     w = _bf(N, K, scale=K ** -0.5, seed=22)
     x = _bf(M, N, seed=23)
@@ -255,7 +252,7 @@ def test_gemm_strided_a_and_bad_shapes():
         ops.gemm(_bf(4, 100), _bf(64, 100))
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 5])
+@pytest.mark.parametrize("cfg", [1, 3, 5, 17, 18])
 @pytest.mark.parametrize("M", [1, 77, 1000])
 def test_gemm_qkv_rope_matches_unfused(cfg, M):
     nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, 1024, 192, 576, 75

@@ -69,6 +69,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_attn_decode_cascade.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_vp, _vp, _vp]
     lib.sg_attn_decode_grouped.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_grouped.restype = _c_int
+    lib.sg_attn_decode_grouped_pf.argtypes = lib.sg_attn_decode.argtypes
+    lib.sg_attn_decode_grouped_pf.restype = _c_int
     lib.sg_attn_decode_split.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_c_int, _vp]
     lib.sg_attn_decode_split.restype = _c_int
     lib.sg_attn_decode_cascade.restype = _c_int
@@ -265,8 +267,9 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
     if cfg is None:
         # 64x64 tiles: the V^T scatter of the epilogue favours more, smaller tiles
         # (kbench, B=4096/8192: 17.8/27.6 us vs 22.0/31.3 us with 128x64); 32-row
-        # tiles on small decode buckets
-        cfg = 17 if M <= GEMM_SMALL_M else 3
+        # tiles up to 2048 rows (7.4 / 8.2 / 11.4 vs 10.1 / 10.7 / 12.3 us at 512 / 1024
+        # / 2048, profiles/r01c_kbench_small_buckets.json)
+        cfg = 17 if M <= 2 * GEMM_SMALL_M else 3
     rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
                                          _stream())
@@ -346,6 +349,8 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
     ``(pre_o [>=B, nh, D] fp32, pre_lse [>=B, nh] fp32)`` (allocated if omitted).
     ``"grouped"``: 16/G sequences per wave, the shared prefix multiplied once for
     all of them, then each sequence's own keys with per-column masks (no scratch);
+    ``"grouped_pf"``: the same with the next key tile's loads issued before the
+    current tile's MFMAs (one flattened tile stream per wave);
     ``"mfma"``: single-pass transposed MFMA kernel (S^T = K·Q^T, O^T = V^T·P^T);
     ``"mfma_v1"``: S = Q·K^T with P through LDS; ``"valu"``: vector-ALU variant —
     kept for A/B measurement; ``"split2"``/``"split4"``/``"split8"``: key-split, N
@@ -380,7 +385,7 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
                f"attn_decode[{impl}]")
         return out
     fn = {"mfma": lib.sg_attn_decode, "mfma_v1": lib.sg_attn_decode_v1, "valu": lib.sg_attn_decode_valu,
-          "grouped": lib.sg_attn_decode_grouped}[impl]
+          "grouped": lib.sg_attn_decode_grouped, "grouped_pf": lib.sg_attn_decode_grouped_pf}[impl]
     _check(fn(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B,
               nh, nkv, D, Lmax, scale, _stream()), f"attn_decode[{impl}]")
     return out

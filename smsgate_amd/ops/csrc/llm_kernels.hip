@@ -1237,6 +1237,105 @@ __global__ void __launch_bounds__(64) attn_grouped_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Grouped decode attention with a one-tile register prefetch: the same work as
+// attn_grouped_kernel, but the wave walks ONE flattened stream of 32-key tiles
+// (shared prefix, then each live sequence's own keys) and issues the loads of
+// tile t+1 before the MFMAs of tile t.  At a 4096-row half batch there are only
+// ~2.4 of these waves per SIMD, too few to cover a cold HBM load with other
+// waves, so the latency has to be covered inside the wave.
+// ---------------------------------------------------------------------------
+struct TileCur {
+  int jj, kt, nval;  // jj = -1: shared prefix; SPW: end of stream
+  const uint16_t* kb;
+  const uint16_t* vb;
+};
+
+__global__ void __launch_bounds__(64) attn_grouped_pf_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
+    uint16_t* __restrict__ out, int B, int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
+  const int G = nh / nkv, SPW = 16 / G;
+  const int b0 = blockIdx.x * SPW;
+  const int j = r16 / G, g = r16 % G;
+  const int bj = b0 + j;
+  const bool col_valid = j < SPW && bj < B && (done == nullptr || done[bj] == 0);
+  const size_t qrow = (size_t)(col_valid ? bj : 0) * nh + kh * G + g;
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);
+    if (!col_valid) v = make_uint4(0, 0, 0, 0);
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+  // move c to the first tile at or after (c.jj, c.kt) (wave-uniform)
+  auto seek = [&](TileCur& c) {
+    while (c.jj < SPW) {
+      if (c.jj < 0) {
+        if (c.kt < P0) {
+          c.nval = P0;
+          c.kb = kpre;
+          c.vb = vpre;
+          return;
+        }
+      } else {
+        const int b = b0 + c.jj;
+        if (b >= B) break;
+        if (done == nullptr || done[b] == 0) {
+          c.nval = pos[b] + 1;
+          if (c.kt < c.nval) {
+            const int sl = slot[b];
+            c.kb = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+            c.vb = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+            return;
+          }
+        }
+      }
+      ++c.jj;
+      c.kt = 0;
+    }
+    c.jj = SPW;
+  };
+  TileCur cur{-1, 0, 0, kpre, vpre};
+  seek(cur);
+  uint4 kc[2][2], vc[4], kn[2][2], vn[4];
+  if (cur.jj < SPW) st_load_tile(cur.kb, cur.vb, cur.kt, g4, r16, cur.kt + 16 < cur.nval, kc, vc);
+  while (cur.jj < SPW) {
+    TileCur nxt = cur;
+    nxt.kt += 32;
+    seek(nxt);
+    if (nxt.jj < SPW) st_load_tile(nxt.kb, nxt.vb, nxt.kt, g4, r16, nxt.kt + 16 < nxt.nval, kn, vn);
+    st_tile(qb, kc, vc, cur.kt, cur.nval, g4, scale_log2, m, lsum, o, cur.jj < 0 || j == cur.jj);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) kc[a][s2] = kn[a][s2];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) vc[n] = vn[n];
+    cur = nxt;
+  }
+  if (col_valid) {
+    const float inv = 1.f / lsum;
+    uint16_t* orow = out + qrow * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[n][0] * inv) | ((uint32_t)f2bf(o[n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[n][2] * inv) | ((uint32_t)f2bf(o[n][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Key-split decode attention (small batches): NWV waves per (row, kv head) deal
 // the row's 32-key tiles — shared prefix first, then its own keys — round-robin;
 // each wave keeps its own online-softmax state and wave 0 merges the NWV states
@@ -1515,6 +1614,20 @@ int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const
   hipLaunchKernelGGL(attn_grouped_kernel, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// Grouped decode attention with a one-tile register prefetch (A/B against grouped).
+int sg_attn_decode_grouped_pf(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                              const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out,
+                              int B, int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+  const int spw = 16 / (nh / nkv);
+  hipLaunchKernelGGL(attn_grouped_pf_kernel, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream,
+                     (const uint16_t*)q, pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache,
+                     (const uint16_t*)pk, (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax,
+                     scale * 1.4426950408889634f);
   return (int)hipGetLastError();
 }
 

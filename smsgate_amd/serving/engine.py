@@ -64,9 +64,11 @@ class EngineConfig:
     compact: bool = True  # row compaction so the decode bucket tracks the active count
     decode_attn: str = "grouped"  # ops.attn_decode impl: grouped | cascade | mfma | mfma_v1 | valu | splitN
     # decode (sub-)batches of at most this many rows use `decode_attn_small` (key-split:
-    # many short waves instead of few long ones — the low-load latency path); 0 = off
-    decode_attn_small_rows: int = 0
-    decode_attn_small: str = "split4"
+    # many short waves instead of few long ones — the low-load latency path); 0 = off.
+    # kbench (profiles/r01c_kbench_small_buckets.json): split2 vs grouped 6.7 / 10.0 / 16.2
+    # vs 15.8 / 18.3 / 20.5 us at 256 / 512 / 1024 rows, a tie at 2048, slower at 4096
+    decode_attn_small_rows: int = 1024
+    decode_attn_small: str = "split2"
     lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
     # nano-batch overlap (measured +10% msgs/s at 8192 slots, profiles/r01b_split_ab.txt):

@@ -128,7 +128,8 @@ def test_attn_prefill(P0, heads, impl):
         o += n
 
 
-@pytest.mark.parametrize("impl", ["grouped", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4", "split8"])
+@pytest.mark.parametrize("impl", ["grouped", "grouped_pf", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4",
+                                  "split8"])
 @pytest.mark.parametrize("P0", [0, 75])
 def test_attn_decode(P0, impl):
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224  # MFMA decode tiles need Lmax % 32 == 0

@@ -62,8 +62,11 @@ def main() -> None:
     p.add_argument("--out", default=None)
     p.add_argument("--attn-small-rows", type=int, default=None,
                    help="decode buckets up to N rows use --attn-small (default: the engine's)")
-    p.add_argument("--attn-small", default="split4")
+    p.add_argument("--attn-small", default="split2")
     p.add_argument("--gemm-small-m", type=int, default=None, help="ops.GEMM_SMALL_M (32-row GEMM tiles up to M)")
+    p.add_argument("--admit-min-batch", type=int, default=None,
+                   help="EngineConfig.admit_min_batch (0 = off; default: the engine's)")
+    p.add_argument("--admit-max-wait-ms", type=float, default=None)
     a = p.parse_args()
     import torch
 
@@ -76,10 +79,15 @@ def main() -> None:
         ops.GEMM_SMALL_M = a.gemm_small_m
     kw = {} if a.attn_small_rows is None else dict(decode_attn_small_rows=a.attn_small_rows,
                                                    decode_attn_small=a.attn_small)
+    if a.admit_min_batch is not None:
+        kw["admit_min_batch"] = a.admit_min_batch
+    if a.admit_max_wait_ms is not None:
+        kw["admit_max_wait_s"] = a.admit_max_wait_ms / 1000.0
     eng = build_engine("smollm-135m", device="cuda", random_init=True, max_slots=a.max_slots, steps_per_graph=2,
                        buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192), **kw)
     arm = {"attn_small_rows": eng.cfg.decode_attn_small_rows, "attn_small": eng.cfg.decode_attn_small,
-           "gemm_small_m": ops.GEMM_SMALL_M}
+           "gemm_small_m": ops.GEMM_SMALL_M, "admit_min_batch": eng.cfg.admit_min_batch,
+           "admit_max_wait_ms": eng.cfg.admit_max_wait_s * 1000.0}
     bodies = [normalize_body(b) for b in generate_bodies(20000, seed=5)]
     ids = eng.tok.message_ids(bodies, eng.cfg.max_body_tokens)
     run_rate(eng, ids, 2000.0, 1.0, seed=0)  # warm-up

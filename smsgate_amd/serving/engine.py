@@ -60,6 +60,13 @@ class EngineConfig:
     use_graphs: bool = True
     prefill_max_tokens: int = 32768
     admit_min_fraction: float = 0.25  # admit when this fraction of rows is free (or nothing runs)
+    # admission batching at low load: while rows are decoding, hold arrivals until
+    # `admit_min_batch` are waiting or the oldest has waited `admit_max_wait_s`
+    # (one prefill of many short prompts costs about what a prefill of a few does); 0 = off.
+    # Poisson A/B (profiles/r01c_admission_batching_ab.jsonl): p50 121 / 132 / 218 ms ->
+    # 90 / 96 / 139 ms at 1 k / 2 k / 6 k msgs/s with 32 / 10 ms
+    admit_min_batch: int = 32
+    admit_max_wait_s: float = 0.01
     fused_gemm: bool = True  # csrc/gemm_kernels.hip (norm prologue, residual/SwiGLU epilogues) vs hipBLASLt
     compact: bool = True  # row compaction so the decode bucket tracks the active count
     decode_attn: str = "grouped"  # ops.attn_decode impl: grouped | cascade | mfma | mfma_v1 | valu | splitN
@@ -107,6 +114,7 @@ class EngineStats:
 class _Pending:
     key: Any
     ids: List[int]
+    t: float = field(default_factory=time.perf_counter)  # arrival (admission batching)
 
 
 @dataclass
@@ -549,6 +557,9 @@ class ExtractionEngine:
             return
         if self.active and len(self.free_rows) < max(1, int(S * self.cfg.admit_min_fraction)) \
                 and len(self.free_rows) < len(self.waiting):
+            return
+        if (self.active and len(self.waiting) < self.cfg.admit_min_batch
+                and time.perf_counter() - self.waiting[0].t < self.cfg.admit_max_wait_s):
             return
         while self.waiting and self.free_rows:
             rows, items, ntok = [], [], 0

@@ -117,6 +117,30 @@ def test_small_bucket_attention_matches_grouped(impl):
     assert all(r is not None and r["txn_type"] in ("debit", "credit", "otp", "unknown") for r in res)
 
 
+def test_admission_batching_completes_with_same_answers():
+    """Holding arrivals for a bigger prefill (admit_min_batch / admit_max_wait_s)
+    changes only when rows start, not what they decode."""
+    w = ExtractorWeights(CONFIGS["tiny"], device="cuda", seed=23)
+    w.requires_grad_(False)
+    tk = load_tokenizer()
+    ids = tk.message_ids(generate_bodies(48, seed=12), 128)
+    outs = []
+    for min_batch in (0, 16):
+        eng = ExtractionEngine(w, tk, EngineConfig(max_slots=64, steps_per_graph=2, buckets=(16, 32, 64),
+                                                   admit_min_batch=min_batch, admit_max_wait_s=0.002))
+        res = {}
+        eng.submit_ids([(i, ids[i]) for i in range(4)])
+        for i in range(4, 48, 4):  # a trickle: 4 arrivals per engine step
+            res.update(eng.step(raw=True))
+            eng.submit_ids([(k, ids[k]) for k in range(i, i + 4)])
+        while eng.busy():
+            res.update(eng.step(raw=True))
+        assert sorted(res) == list(range(48))
+        outs.append({k: list(v) for k, v in res.items()})
+        del eng
+    assert outs[0] == outs[1]
+
+
 def test_row_compaction_preserves_results():
     """Greedy answers are identical with and without row compaction.  Two staggered
     admission waves (random weights -> every answer has the same length, so waves
@@ -131,7 +155,7 @@ def test_row_compaction_preserves_results():
     outs, stats = [], []
     for compact in (True, False):
         eng = ExtractionEngine(w, tk, EngineConfig(max_slots=64, steps_per_graph=2, buckets=(16, 32, 48, 64),
-                                                   compact=compact))
+                                                   compact=compact, admit_min_batch=0))  # admit the 2nd wave now
         res = {}
         eng.submit_ids([(i, ids[i]) for i in range(48)])
         for _ in range(6):

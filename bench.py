@@ -50,6 +50,8 @@ def _args(argv=None):
     p.add_argument("--cpu-workers", type=int, default=8)
     p.add_argument("--concurrency", type=int, default=4)
     p.add_argument("--batch", type=int, default=512)
+    p.add_argument("--worker-threads", type=int, default=2,
+                   help="tokenizer (Rayon) threads per parser process; 0 = library default (one per CPU)")
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
     p.add_argument("--no-compact", action="store_true", help="disable decode row compaction")
     p.add_argument("--split-decode", type=int, default=4096,
@@ -82,7 +84,8 @@ def run_replica(args, rank: int, world: int, local: int):
     W = max(1, args.cpu_workers)
     if args.msgs_per_step % W:
         raise SystemExit("--msgs-per-step must be divisible by --cpu-workers")
-    cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128}
+    cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
+           "worker_threads": args.worker_threads}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
 

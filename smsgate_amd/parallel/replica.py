@@ -33,11 +33,18 @@ def spawn_parser_workers(n: int, rank: int, cfg: Dict[str, Any]) -> Tuple[List[A
     """Start ``n`` parser processes (spawn context, GPU hidden); returns (procs, conns)."""
     ctx = mp.get_context("spawn")
     procs, conns = [], []
-    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")}
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                            "RAYON_NUM_THREADS", "OMP_NUM_THREADS")}
     try:
         # parser processes never touch the GPU; hide it so an accidental CUDA call fails fast
         os.environ["HIP_VISIBLE_DEVICES"] = ""
         os.environ["CUDA_VISIBLE_DEVICES"] = ""
+        # the tokenizer's Rust thread pool defaults to one thread per CPU of the whole
+        # machine in EVERY worker (K workers per GPU x 8 GPUs); give each a small share
+        threads = int(cfg.get("worker_threads", 2))
+        if threads > 0 and saved["RAYON_NUM_THREADS"] is None:
+            os.environ["RAYON_NUM_THREADS"] = str(threads)
+        os.environ["OMP_NUM_THREADS"] = "1"
         for w in range(n):
             a, b = ctx.Pipe(duplex=True)
             p = ctx.Process(target=parser_worker_main, args=(b, rank, w, cfg), name=f"parser-r{rank}-w{w}",

@@ -1175,7 +1175,8 @@ __global__ void __launch_bounds__(64) attn_own_kernel(
 // trip, one launch, prefix K/V read once per SPW sequences.
 // grid = (ceil(B / SPW), nkv), one wave.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) attn_grouped_kernel(
+template <int MINW>  // min waves per SIMD (launch bound): 1 = compiler's choice, 6 = VGPR cap 80
+__global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
     const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
     const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
@@ -1611,7 +1612,20 @@ int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const
   if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
   if (B == 0) return 0;
   const int spw = 16 / (nh / nkv);
-  hipLaunchKernelGGL(attn_grouped_kernel, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
+  hipLaunchKernelGGL(attn_grouped_kernel<1>, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
+                     pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// Grouped decode attention built for 6 resident waves per SIMD (VGPRs capped at 80).
+int sg_attn_decode_grouped6(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                            const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B,
+                            int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+  const int spw = 16 / (nh / nkv);
+  hipLaunchKernelGGL(attn_grouped_kernel<6>, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
   return (int)hipGetLastError();

@@ -63,6 +63,8 @@ def _args(argv=None):
     p.add_argument("--no-gc-freeze", action="store_true", help="keep the default GC thresholds in the rank process")
     p.add_argument("--decode-attn", default="grouped", help="decode attention kernel (ops.attn_decode impl)")
     p.add_argument("--admit-min-batch", type=int, default=None, help="EngineConfig.admit_min_batch (default: engine's)")
+    p.add_argument("--prefill-key-split", type=int, default=1, choices=[1, 2],
+                   help="waves sharing each prefill attention tile's keys")
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--cpu-echo-engine", action="store_true",
@@ -120,6 +122,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               split_decode=args.split_decode, split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
                               split_parts=args.split_parts,
                               split_prefill=args.split_prefill, decode_attn=args.decode_attn,
+                              prefill_key_split=args.prefill_key_split,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
     if not args.no_gc_freeze:

@@ -45,8 +45,9 @@ def main() -> None:
     scale = 1 / math.sqrt(D)
     res = {"nseq": a.nseq, "tokens": T, "nh": a.nh, "nkv": a.nkv, "P0": a.P0}
     outs = {}
-    for impl in ("per_head", "gqa"):
-        ops.set_prefill_impl(impl)
+    for impl in ("per_head", "gqa", "gqa_ks2"):
+        ops.set_prefill_impl("gqa" if impl.startswith("gqa") else impl)
+        ops.set_prefill_split(2 if impl == "gqa_ks2" else 1)
         out = torch.empty(T, a.nh * D, dtype=torch.bfloat16, device=dev)
         for _ in range(3):
             ops.attn_prefill(q, cu, qs, sl, max(lens), kc, vt, pk, pvt, a.P0, out, scale)
@@ -60,8 +61,11 @@ def main() -> None:
         res[f"{impl}_us"] = round(e0.elapsed_time(e1) / a.iters * 1000, 2)
         outs[impl] = out.float()
     ops.set_prefill_impl("gqa")
+    ops.set_prefill_split(1)
     res["max_abs_diff"] = float((outs["gqa"] - outs["per_head"]).abs().max())
+    res["max_abs_diff_ks2"] = float((outs["gqa_ks2"] - outs["gqa"]).abs().max())
     res["speedup"] = round(res["per_head_us"] / res["gqa_us"], 3)
+    res["speedup_ks2"] = round(res["gqa_us"] / res["gqa_ks2_us"], 3)
     print(json.dumps(res))
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)

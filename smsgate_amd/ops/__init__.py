@@ -89,6 +89,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_gemm_set_group_m.restype = None
     lib.sg_set_prefill_impl.argtypes = [_c_int]
     lib.sg_set_prefill_impl.restype = None
+    lib.sg_set_prefill_split.argtypes = [_c_int]
+    lib.sg_set_prefill_split.restype = None
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
@@ -319,6 +321,14 @@ def set_prefill_impl(impl: str) -> None:
     """``"gqa"`` (default: one wave per KV head, K/V loaded once per GQA group,
     prefetched) or ``"per_head"`` (one wave per query head; kept for A/B)."""
     load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1}[impl])
+
+
+def set_prefill_split(ks: int) -> None:
+    """Key split of the GQA prefill kernel: 1 = one wave per (16-query tile,
+    sequence, KV head); 2 = two waves deal its key tiles and merge in LDS."""
+    if ks not in (1, 2):
+        raise ValueError("prefill key split must be 1 or 2")
+    load_library().sg_set_prefill_split(ks)
 
 
 def attn_prefill(q: torch.Tensor, cu_q: torch.Tensor, q_start: torch.Tensor, slot: torch.Tensor, max_q: int,

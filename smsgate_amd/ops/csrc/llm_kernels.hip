@@ -354,24 +354,31 @@ __global__ void __launch_bounds__(64) attn_prefill_kernel(
 // kt are computed (register double buffering: the per-head kernel waited on a
 // cold load at every step).  Same masking, rounding and online softmax as the
 // per-head kernel; numerics are checked against the same fp32 reference.
+// KS > 1 (key split): KS waves per block deal the 32-key tiles round-robin, each
+// with its own online-softmax state, merged by wave 0 through LDS — KS times the
+// waves for the same bytes (the kernel runs at 2 waves per SIMD: 194 VGPRs).
 // ---------------------------------------------------------------------------
-template <int G>
-__global__ void __launch_bounds__(64) attn_prefill_gqa_kernel(
+template <int G, int KS>
+__global__ void __launch_bounds__(64 * KS) attn_prefill_gqa_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
     const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
     const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out,
     int nh, int nkv, int Lmax, float scale_log2) {
   constexpr int D = 64;
   const int tile = blockIdx.x, b = blockIdx.y, kh = blockIdx.z;
-  const int l = threadIdx.x;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qbeg = cu_q[b];
   const int qlen = cu_q[b + 1] - qbeg;
-  if (tile * 16 >= qlen) return;
+  if (tile * 16 >= qlen) return;  // block-uniform
   const int g4 = l >> 4, r16 = l & 15;
   const int qs = q_start[b];
   const int sl = slot[b];
 
-  __shared__ __attribute__((aligned(16))) uint16_t P_lds[G][16 * 32];
+  // ONE __shared__ array: per-wave P tiles, then (KS > 1) the merge area
+  constexpr int PSZ = G * 16 * 32;                                 // bf16 elements per wave
+  constexpr int RED = KS > 1 ? KS * 64 * G * 24 * 2 : 0;           // fp32 state as bf16-sized units
+  __shared__ __attribute__((aligned(16))) uint16_t smem_pf[(KS * PSZ > RED ? KS * PSZ : RED)];
+  uint16_t (*P_lds)[16 * 32] = reinterpret_cast<uint16_t (*)[16 * 32]>(smem_pf + w * PSZ);
 
   bf16x8 qa[G][2];
   {
@@ -425,8 +432,8 @@ __global__ void __launch_bounds__(64) attn_prefill_gqa_kernel(
     }
 
   uint4 kc[2][2];
-  load_k(0, kc);
-  for (int kt = 0; kt < nkeys; kt += 32) {
+  load_k(32 * w, kc);
+  for (int kt = 32 * w; kt < nkeys; kt += 32 * KS) {
     const bool pre = kt < P0pad;  // tiles never straddle: P0pad % 32 == 0
     // V tile of this step and K tile of the next step: in flight during the scores
     uint4 vv[4];
@@ -442,7 +449,7 @@ __global__ void __launch_bounds__(64) attn_prefill_gqa_kernel(
       }
     }
     uint4 kn[2][2];
-    load_k(kt + 32, kn);  // guarded by key < nkeys: past the end it loads nothing
+    load_k(kt + 32 * KS, kn);  // guarded by key < nkeys: past the end it loads nothing
 
     bool okm[2][4];
 #pragma unroll
@@ -504,7 +511,10 @@ __global__ void __launch_bounds__(64) attn_prefill_gqa_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[g][n][i] *= alpha[i];
     }
-    __syncthreads();
+    // P tiles are private to the wave (waves of a KS block run different trip
+    // counts, so no block barrier here): LDS ops of one wave complete in order
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const bf16x8 pa = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&P_lds[g][r16 * 32 + 8 * g4]));
@@ -512,11 +522,52 @@ __global__ void __launch_bounds__(64) attn_prefill_gqa_kernel(
       for (int n = 0; n < 4; ++n)
         o[g][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vv[n]), o[g][n], 0, 0, 0);
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: next step rewrites P_lds
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int hs = 0; hs < 2; ++hs)
 #pragma unroll
       for (int s = 0; s < 2; ++s) kc[hs][s] = kn[hs][s];
+  }
+  if constexpr (KS > 1) {
+    // merge the KS partial softmax states (per lane: head g, rows 4·g4 + i)
+    float* red = reinterpret_cast<float*>(smem_pf);
+    __syncthreads();  // every wave is done with its P tile
+    float* mine = red + ((size_t)w * 64 + l) * (G * 24);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) mine[g * 24 + n * 4 + i] = o[g][n][i];
+        mine[g * 24 + 16 + i] = m[g][i];
+        mine[g * 24 + 20 + i] = lsum[g][i];
+      }
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float M = -INFINITY;
+#pragma unroll
+        for (int v = 0; v < KS; ++v) M = fmaxf(M, red[((size_t)v * 64 + l) * (G * 24) + g * 24 + 16 + i]);
+        float L = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int v = 0; v < KS; ++v) {
+          const float* src = red + ((size_t)v * 64 + l) * (G * 24) + g * 24;
+          const float mv = src[16 + i];
+          if (mv == -INFINITY) continue;  // no valid key in this wave's tiles
+          const float f = exp2f(mv - M);
+          L += f * src[20 + i];
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[n] += f * src[n * 4 + i];
+        }
+        m[g][i] = M;
+        lsum[g][i] = L;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) o[g][n][i] = acc[n];
+      }
   }
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -1506,7 +1557,8 @@ __global__ void __launch_bounds__(256) fsm_sample_kernel(
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-static int g_prefill_impl = 0;  // sg_set_prefill_impl
+static int g_prefill_impl = 2;  // sg_set_prefill_impl
+static int g_prefill_ks = 1;    // sg_set_prefill_split
 
 extern "C" {
 
@@ -1549,16 +1601,27 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   if (nseq == 0 || max_q == 0) return 0;
   const float sl2 = scale * 1.4426950408889634f;
   const int G = nh / nkv;
-  if (g_prefill_impl == 0 && G >= 1 && G <= 4) {
+  // auto: the per-head kernel launches G x the waves, which wins while the batch is
+  // too small to fill the chip (prefill_bench: 12.6 vs 17.2 us at 32 sequences,
+  // 32 vs 38 us at 190); the GQA kernel's single K/V load wins at 800 (98 vs 112 us)
+  const bool gqa = g_prefill_impl == 0 || (g_prefill_impl == 2 && nseq > 384);
+  if (gqa && G >= 1 && G <= 4) {
     dim3 grid((max_q + 15) / 16, nseq, nkv);
-#define SG_PF(GG)                                                                                               \
-  hipLaunchKernelGGL(attn_prefill_gqa_kernel<GG>, grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
-                     slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,            \
+#define SG_PF(GG, KS)                                                                                          \
+  hipLaunchKernelGGL((attn_prefill_gqa_kernel<GG, KS>), grid, dim3(64 * KS), 0, stream, (const uint16_t*)q, cu_q, \
+                     q_start, slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,     \
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2)
-    if (G == 1) SG_PF(1);
-    else if (G == 2) SG_PF(2);
-    else if (G == 3) SG_PF(3);
-    else SG_PF(4);
+    if (g_prefill_ks == 2) {
+      if (G == 1) SG_PF(1, 2);
+      else if (G == 2) SG_PF(2, 2);
+      else if (G == 3) SG_PF(3, 2);
+      else SG_PF(4, 2);
+    } else {
+      if (G == 1) SG_PF(1, 1);
+      else if (G == 2) SG_PF(2, 1);
+      else if (G == 3) SG_PF(3, 1);
+      else SG_PF(4, 1);
+    }
 #undef SG_PF
     return (int)hipGetLastError();
   }
@@ -1569,8 +1632,11 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   return (int)hipGetLastError();
 }
 
-// 0 = GQA-shared prefetching kernel (default), 1 = per-head kernel (A/B: kbench, tests)
+// 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto by batch size (default)
 void sg_set_prefill_impl(int impl) { g_prefill_impl = impl; }
+
+// key split of the GQA prefill kernel: 1 (one wave per tile) or 2 (two waves share the keys)
+void sg_set_prefill_split(int ks) { g_prefill_ks = ks == 2 ? 2 : 1; }
 
 int sg_attn_decode(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
                    const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out, int B, int nh,

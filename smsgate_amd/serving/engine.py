@@ -84,6 +84,7 @@ class EngineConfig:
     split_graphs: int = 2  # 1 = both halves in one fork/join graph; 2 = one graph per part, one stream each
     split_parts: int = 2  # parts of a split decode bucket (split_graphs=2)
     split_prefill: int = 8192  # >0: prefill batches of >= this many tokens run as two halves on two streams
+    prefill_key_split: int = 1  # 2: two waves share each prefill attention tile's keys (ops.set_prefill_split)
 
 
 @dataclass
@@ -138,6 +139,7 @@ class ExtractionEngine:
             raise RuntimeError("ExtractionEngine needs a GPU (the HIP kernels have no CPU path)")
         ops.load_library()
         mc, ec = self.mc, self.cfg
+        ops.set_prefill_split(ec.prefill_key_split)  # process-wide launch setting
         if mc.head_dim != 64:
             raise ValueError("kernels are specialised for head_dim 64")
         # Constrained decoding can only ever emit tokenizer ids, so the lm_head is

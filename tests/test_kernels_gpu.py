@@ -86,13 +86,14 @@ def _ref_seq_attention(qb, own_k, own_v, pk, pv, P0, q_off, scale):
     return out
 
 
-@pytest.mark.parametrize("impl", ["gqa", "per_head"])
+@pytest.mark.parametrize("impl", ["gqa", "gqa_ks2", "per_head"])
 @pytest.mark.parametrize("heads", [(9, 3), (4, 2), (4, 4), (8, 2)])
 @pytest.mark.parametrize("P0", [0, 75])
 def test_attn_prefill(P0, heads, impl):
     nh, nkv = heads
     D, S, Lmax = 64, 6, 200
-    ops.set_prefill_impl(impl)
+    ops.set_prefill_impl("gqa" if impl.startswith("gqa") else impl)
+    ops.set_prefill_split(2 if impl == "gqa_ks2" else 1)
     P0pad = (P0 + 31) // 32 * 32
     lens = [1, 17, 40, 63, 5]
     starts = [0, 0, 3, 0, 30]  # own offset of each chunk's first query (chunked prefill)
@@ -117,6 +118,7 @@ def test_attn_prefill(P0, heads, impl):
         ops.attn_prefill(q, cu, qs, sl, max(lens), kc, vt, pk, pvt, P0, out, scale)
     finally:
         ops.set_prefill_impl("gqa")
+        ops.set_prefill_split(1)
     o = 0
     for n, st, r in zip(lens, starts, rows):
         nown = st + n

@@ -1,14 +1,25 @@
-"""Average counters per kernel (template instantiation) from a rocprofv3 counter_collection.csv."""
+"""Average counters per kernel (template instantiation) from rocprofv3 counter_collection.csv files.
+
+Default: the fused GEMMs and hipBLASLt kernels.  ``--match SUBSTR``: every
+kernel whose name contains SUBSTR (e.g. ``attn``)."""
 import collections
 import csv
 import re
 import sys
 
+args = sys.argv[1:]
+match = None
+if args and args[0] == "--match":
+    match, args = args[1], args[2:]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for path in sys.argv[1:]:
+for path in args:
     for r in csv.DictReader(open(path)):
         n = r["Kernel_Name"]
-        if "gemm_fused" in n:
+        if match is not None:
+            if match not in n:
+                continue
+            n = n.split("(")[0]
+        elif "gemm_fused" in n:
             m = re.search(r"gemm_fused_kernel<([^>]*)>", n)
             n = "fused<" + (m.group(1) if m else "?") + ">"
         elif "Cijk" in n:

@@ -60,7 +60,7 @@ def main() -> None:
         torch.cuda.synchronize()
         res[f"{impl}_us"] = round(e0.elapsed_time(e1) / a.iters * 1000, 2)
         outs[impl] = out.float()
-    ops.set_prefill_impl("gqa")
+    ops.set_prefill_impl("auto")
     ops.set_prefill_split(1)
     res["max_abs_diff"] = float((outs["gqa"] - outs["per_head"]).abs().max())
     res["max_abs_diff_ks2"] = float((outs["gqa_ks2"] - outs["gqa"]).abs().max())

@@ -318,9 +318,11 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos
 
 
 def set_prefill_impl(impl: str) -> None:
-    """``"gqa"`` (default: one wave per KV head, K/V loaded once per GQA group,
-    prefetched) or ``"per_head"`` (one wave per query head; kept for A/B)."""
-    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1}[impl])
+    """``"auto"`` (default: ``per_head`` up to 384 sequences per launch, ``gqa``
+    above), ``"gqa"`` (one wave per KV head, K/V loaded once per GQA group,
+    prefetched) or ``"per_head"`` (one wave per query head: G x the waves, which
+    fills the chip better at small batches; ``profiles/r01c_prefill_key_split_ab.txt``)."""
+    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2}[impl])
 
 
 def set_prefill_split(ks: int) -> None:

@@ -117,7 +117,7 @@ def test_attn_prefill(P0, heads, impl):
     try:
         ops.attn_prefill(q, cu, qs, sl, max(lens), kc, vt, pk, pvt, P0, out, scale)
     finally:
-        ops.set_prefill_impl("gqa")
+        ops.set_prefill_impl("auto")
         ops.set_prefill_split(1)
     o = 0
     for n, st, r in zip(lens, starts, rows):

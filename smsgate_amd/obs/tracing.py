@@ -18,7 +18,7 @@ from typing import Dict, Iterator, Optional
 
 from . import errors
 
-__all__ = ["Tracer", "tracer", "start_transaction", "start_span", "SpanStats"]
+__all__ = ["Tracer", "tracer", "start_transaction", "start_span", "SpanStats", "Profiler"]
 
 
 @dataclass
@@ -84,3 +84,71 @@ def start_transaction(op: str, name: str) -> Iterator[None]:
 
 def start_span(name: str, t: Optional[Tracer] = None):
     return (t or tracer).span(name)
+
+
+class Profiler:
+    """Host-side profiler session around a unit of work.
+
+    The reference wraps DLQ reparse in ``sentry_sdk.profiler.start_profiler()``
+    / ``stop_profiler()`` (dlq_worker.py:70-74).  Here the Sentry continuous
+    profiler is started when the SDK is active; independently, when
+    ``SMSGATE_PROFILE_DIR`` (or ``out_dir``) is set, a :mod:`cProfile` session
+    runs and its stats are dumped to ``<dir>/<name>-<pid>.pstats`` on
+    :meth:`stop` (readable with :mod:`pstats` or snakeviz).  With neither, the
+    session costs nothing.  Re-entrant ``start`` calls are counted, so nested
+    reparse batches share one session.
+    """
+
+    def __init__(self, name: str, out_dir: Optional[str] = None) -> None:
+        self.name = name
+        self.out_dir = out_dir if out_dir is not None else os.getenv("SMSGATE_PROFILE_DIR") or None
+        self._depth = 0
+        self._prof = None
+        self._sentry = False
+        self.dumped: Optional[str] = None
+
+    def start(self) -> None:
+        self._depth += 1
+        if self._depth > 1:
+            return
+        sdk = errors._sdk
+        prof_mod = getattr(sdk, "profiler", None) if sdk is not None else None
+        if prof_mod is not None and hasattr(prof_mod, "start_profiler"):
+            try:
+                prof_mod.start_profiler()
+                self._sentry = True
+            except Exception:  # profiler not configured: keep going without it
+                self._sentry = False
+        if self.out_dir:
+            import cProfile
+
+            self._prof = cProfile.Profile()
+            self._prof.enable()
+
+    def stop(self) -> Optional[str]:
+        if self._depth == 0:
+            return None
+        self._depth -= 1
+        if self._depth > 0:
+            return None
+        if self._sentry:
+            try:
+                errors._sdk.profiler.stop_profiler()
+            except Exception:
+                pass
+            self._sentry = False
+        if self._prof is not None:
+            self._prof.disable()
+            os.makedirs(self.out_dir, exist_ok=True)
+            path = os.path.join(self.out_dir, f"{self.name}-{os.getpid()}.pstats")
+            self._prof.dump_stats(path)
+            self._prof = None
+            self.dumped = path
+        return self.dumped
+
+    def __enter__(self) -> "Profiler":
+        self.start()
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.stop()

@@ -19,6 +19,7 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from ..bus.base import SUBJECT_FAILED, Bus, Msg
 from ..models.domain import RawSMS
+from ..obs.tracing import Profiler
 from ..parse.pipeline import ParsePipeline
 from ..runtime.stage import Stage
 
@@ -58,6 +59,8 @@ class DlqWorker:
         self.reparsed = 0
         self.not_reparsable = 0
         self.log: List[Dict[str, Any]] = []
+        # reparse runs under a profiler session (dlq_worker.py:70-74)
+        self.profiler = Profiler("dlq_reparse")
         self.stage = Stage(bus, SUBJECT_FAILED, group, self.handle_batch, batch=batch, stats_interval=0,
                            name="dlq_worker")
 
@@ -81,9 +84,10 @@ class DlqWorker:
                 else:
                     to_reparse.append(_Shim(json.dumps({"raw": raw}).encode()))
         if to_reparse and self.pipeline is not None:
-            publishes, counts = await route_batch(self.pipeline, to_reparse)
-            if publishes:
-                await self.bus.publish_many(publishes)
+            with self.profiler:
+                publishes, counts = await route_batch(self.pipeline, to_reparse)
+                if publishes:
+                    await self.bus.publish_many(publishes)
             self.reparsed += len(to_reparse)
         for m in msgs:
             await m.ack()

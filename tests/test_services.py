@@ -96,6 +96,35 @@ def test_dlq_reparse_routes_and_acks_everything(arun):
     assert len(processing) == 2
 
 
+def test_dlq_reparse_profiler_dumps_pstats(arun, tmp_path):
+    """Reparse runs inside a profiler session (dlq_worker.py:70-74); with a
+    profile dir set, a cProfile dump lands there and names the parse path."""
+    import pstats
+
+    from smsgate_amd.obs.tracing import Profiler
+    from smsgate_amd.services.dlq import DlqWorker
+
+    bus = MemoryBus()
+    good = REFERENCE_CASES[0][0]
+
+    async def go():
+        await bus.publish(SUBJECT_FAILED, json.dumps({"reason": "unmatched", "raw": _raw(good).model_dump()}).encode())
+        w = DlqWorker(bus, ParsePipeline(RegexBackend()), reparse=True)
+        w.profiler = Profiler("dlq_reparse", out_dir=str(tmp_path))
+        await w.stage.run_until_idle()
+        return w
+
+    w = arun(go())
+    assert w.reparsed == 1 and w.profiler.dumped is not None
+    funcs = {f[2] for f in pstats.Stats(w.profiler.dumped).stats}
+    assert "route_batch" in funcs
+    # no dir, no SDK: a no-op session, nested use is balanced
+    p = Profiler("x", out_dir="")
+    with p, p:
+        pass
+    assert p.dumped is None and p._depth == 0
+
+
 # --------------------------------------------------------------------------- notifier
 def _pb_rec(i, dt, merchant="SHOP", amount="10.00", balance="100.00"):
     return {"msg_id": f"id{i}", "datetime": dt, "merchant": merchant, "amount": amount, "balance": balance,

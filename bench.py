@@ -150,9 +150,15 @@ def run_replica(args, rank: int, world: int, local: int):
     coord.shutdown(procs)
     estats = engine.stats.as_dict()
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if echo else "cuda")
+        dev = "cpu" if echo else "cuda"
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        # routing outcomes summed over ranks: the JSON line reports the whole job
+        keys = ("ok", "fail", "skip")  # route_batch's outcome set, same order on every rank
+        c = torch.tensor([counts.get(k, 0) for k in keys], dtype=torch.int64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        counts = dict(zip(keys, (int(x) for x in c.tolist())))
         dist.destroy_process_group()
     return dt, counts, init_s, estats
 
@@ -202,6 +208,9 @@ def main(argv=None) -> int:
         dt, counts, init_s, estats = asyncio.run(_run_cpu(args))
         world = 1
     total = args.msgs_per_step * args.steps * world
+    routed = sum(counts.values())
+    if routed != total:  # every timed message must have been parsed and routed
+        raise SystemExit(f"bench: {routed} messages routed, expected {total}")
     value = total / dt
     if rank == 0:
         gpu = args.backend == "local_llm"

@@ -78,3 +78,4 @@ def test_bench_two_ranks_torchrun_gloo(tmp_path):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 512
     assert out["value"] > 0 and out["steps"] == 2 and out["scaling"] == "weak"
+    assert sum(out["routing"].values()) == 512 * 2  # outcomes summed over both ranks

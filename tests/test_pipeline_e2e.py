@@ -149,3 +149,57 @@ def test_handler_exception_does_not_kill_loop(arun):
     w = arun(go())
     assert w.stage.handler_errors == 1 and calls["n"] == 2
     assert w.counts == {"ok": 1, "fail": 0, "skip": 0}
+
+
+def test_parser_tracing_spans_and_sentry_forwarding(arun, monkeypatch):
+    """The parser records the reference's transaction and spans
+    (worker.py:33-55, :80-171) in the in-process tracer, and forwards them to
+    the Sentry SDK when one is active (stub SDK here: sentry_sdk is not on the
+    image). The DLQ Profiler drives the SDK's profiler the same way."""
+    import contextlib
+
+    from smsgate_amd.obs import errors
+    from smsgate_amd.obs.tracing import Profiler, tracer
+
+    seen = []
+
+    class _Prof:
+        def start_profiler(self):
+            seen.append(("profiler", "start"))
+
+        def stop_profiler(self):
+            seen.append(("profiler", "stop"))
+
+    class _SDK:
+        profiler = _Prof()
+
+        def start_transaction(self, op, name):
+            seen.append(("txn", f"{op}/{name}"))
+            return contextlib.nullcontext()
+
+        def start_span(self, name):
+            seen.append(("span", name))
+            return contextlib.nullcontext()
+
+    monkeypatch.setattr(errors, "_sdk", _SDK())
+    monkeypatch.setattr(tracer, "enabled", True)
+    tracer.reset()
+    bus = MemoryBus()
+
+    async def go():
+        await bus.publish(SUBJECT_RAW, _raw("traced body").model_dump_json().encode())
+        w = ParserWorker(bus, ParsePipeline(FakeBackend()), stats_interval=0)
+        await w.stage.run_until_idle()
+        return w
+
+    w = arun(go())
+    assert w.counts["ok"] == 1
+    snap = tracer.snapshot()
+    for name in ("task/process_parsing", "validate", "parsing", "validate_parsed", "publish"):
+        assert snap[name].count >= 1 and snap[name].max_s >= snap[name].mean_s >= 0.0, name
+    assert ("txn", "task/process_parsing") in seen
+    assert {n for k, n in seen if k == "span"} >= {"validate", "parsing", "validate_parsed", "publish"}
+    with Profiler("dlq_reparse", out_dir=""):
+        pass
+    assert seen[-2:] == [("profiler", "start"), ("profiler", "stop")]
+    tracer.reset()

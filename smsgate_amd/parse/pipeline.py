@@ -72,6 +72,8 @@ def postprocess_answer(raw: RawSMS, fixed_body: str, answer: Dict[str, Any], tz:
             if "String does not contain a date" in str(exc):
                 resp["date"] = parse_unix_timestamp(int(raw.date), tz=tz, aware=False)
         resp["date"] = fix_broken_datetime(raw.body, resp["date"])
+        # D8 (kept for parity): a null card raises here, so it lands in the DLQ as
+        # "unmatched"; only card *strings* shorter than 4 chars reach BROKEN below.
         card = resp["card"].replace("*", "").replace(" ", "")
         resp["card"] = card[:4] if len(card) > 4 else card
         resp["amount"] = parse_ambiguous_decimal(str(resp["amount"]))

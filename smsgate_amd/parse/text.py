@@ -27,6 +27,8 @@ __all__ = [
 ]
 
 #: Upper-cased substrings that make the worker ack-and-skip a message.
+#: D10 (kept for parity): incoming credits ("CREDIT PAYMENT", "C2C RECEIVED")
+#: are skipped like OTPs, so they are never stored.
 WORKER_SKIP_KEYWORDS = (
     "OTP",
     "CODE:",

@@ -161,3 +161,18 @@ def test_fast_date_paths_equal_strptime(seed):
             got = dates.fix_broken_datetime(body, datetime(2020, 1, 1, 7, 8))
             if isinstance(exp, datetime):
                 assert got == datetime.combine(exp.date(), datetime(2020, 1, 1, 7, 8).time())
+
+
+def test_null_card_and_credit_parity_d8_d10():
+    """D8 parity: a null card is 'unmatched' (DLQ), a short card string is BROKEN
+    (ack + skip); D10 parity: incoming credits are skipped by the worker filter."""
+    from smsgate_amd.parse import Outcome, postprocess_answer
+
+    raw = RawSMS(msg_id="m", sender="s", body="PURCHASE 10.00 AMD", date="1749808562")
+    base = {"txn_type": "debit", "date": "06.05.25 14:23", "amount": "10.00", "currency": "AMD",
+            "card": "4083***7538", "merchant": "SHOP", "city": "YEREVAN", "address": "null", "balance": "5.00"}
+    ok = postprocess_answer(raw, raw.body, base)
+    assert ok.outcome == Outcome.PARSED and ok.parsed.card == "4083" and ok.parsed.address == ""
+    assert postprocess_answer(raw, raw.body, dict(base, card=None)).outcome == Outcome.UNMATCHED
+    assert postprocess_answer(raw, raw.body, dict(base, card="***")).outcome == Outcome.BROKEN
+    assert worker_should_skip("CREDIT PAYMENT 100 AMD") and worker_should_skip("C2C RECEIVED 5 AMD")

@@ -91,7 +91,7 @@ def main():
                                                            done=done, impl="mfma_v1"))
     res["attn_decode_valu"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out,
                                                              1 / math.sqrt(D), done=done, impl="valu"))
-    for impl in ("grouped", "grouped6", "grouped_pf", "split2", "split4", "split8"):
+    for impl in ("grouped", "grouped_h", "grouped6", "grouped_pf", "split2", "split4", "split8"):
         res[f"attn_decode_{impl}"] = timeit(lambda: ops.attn_decode(q, pos, slot, kc, vt, pk, pvt, P0, out,
                                                                     1 / math.sqrt(D), done=done, impl=impl))
     kv_bytes = B * nkv * a.ctx * D * 2 * 2

@@ -71,6 +71,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_attn_decode_grouped.restype = _c_int
     lib.sg_attn_decode_grouped6.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_grouped6.restype = _c_int
+    lib.sg_attn_decode_grouped_h.argtypes = lib.sg_attn_decode.argtypes
+    lib.sg_attn_decode_grouped_h.restype = _c_int
     lib.sg_attn_decode_grouped_pf.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_grouped_pf.restype = _c_int
     lib.sg_attn_decode_split.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_c_int, _vp]
@@ -365,7 +367,8 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
     all of them, then each sequence's own keys with per-column masks (no scratch);
     ``"grouped_pf"``: the same with the next key tile's loads issued before the
     current tile's MFMAs (one flattened tile stream per wave); ``"grouped6"``: the
-    grouped kernel compiled for 6 waves per SIMD (VGPRs capped at 80);
+    grouped kernel compiled for 6 waves per SIMD (VGPRs capped at 80); ``"grouped_h"``:
+    the grouped kernel with each wave's (done, pos, slot) loaded once at entry;
     ``"mfma"``: single-pass transposed MFMA kernel (S^T = K·Q^T, O^T = V^T·P^T);
     ``"mfma_v1"``: S = Q·K^T with P through LDS; ``"valu"``: vector-ALU variant —
     kept for A/B measurement; ``"split2"``/``"split4"``/``"split8"``: key-split, N
@@ -401,7 +404,7 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
         return out
     fn = {"mfma": lib.sg_attn_decode, "mfma_v1": lib.sg_attn_decode_v1, "valu": lib.sg_attn_decode_valu,
           "grouped": lib.sg_attn_decode_grouped, "grouped_pf": lib.sg_attn_decode_grouped_pf,
-          "grouped6": lib.sg_attn_decode_grouped6}[impl]
+          "grouped6": lib.sg_attn_decode_grouped6, "grouped_h": lib.sg_attn_decode_grouped_h}[impl]
     _check(fn(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B,
               nh, nkv, D, Lmax, scale, _stream()), f"attn_decode[{impl}]")
     return out

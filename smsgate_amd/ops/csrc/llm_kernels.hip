@@ -1226,7 +1226,10 @@ __global__ void __launch_bounds__(64) attn_own_kernel(
 // trip, one launch, prefix K/V read once per SPW sequences.
 // grid = (ceil(B / SPW), nkv), one wave.
 // ---------------------------------------------------------------------------
-template <int MINW>  // min waves per SIMD (launch bound): 1 = compiler's choice, 6 = VGPR cap 80
+// HOIST: lanes 0..SPW-1 load their sequence's (done, pos, slot) at kernel entry, so
+// the loads overlap the prefix pass and each own-key loop reads them with
+// v_readlane instead of a dependent scalar load before its first K/V tile.
+template <int MINW, bool HOIST = false>  // MINW: min waves per SIMD (1 = compiler's choice, 6 = VGPR cap 80)
 __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
     const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
@@ -1251,6 +1254,12 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
 #pragma unroll
   for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, lsum = 0.f;
+  int h_done = 1, h_pos = 0, h_slot = 0;
+  if (HOIST && l < SPW && b0 + l < B) {
+    h_done = done != nullptr ? done[b0 + l] : 0;
+    h_pos = pos[b0 + l];
+    h_slot = slot[b0 + l];
+  }
   // shared prefix: all columns
   const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
   const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
@@ -1263,9 +1272,16 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
   for (int jj = 0; jj < SPW; ++jj) {
     const int b = b0 + jj;
     if (b >= B) break;
-    if (done != nullptr && done[b]) continue;
-    const int own = pos[b] + 1;
-    const int sl = slot[b];
+    int own, sl;
+    if constexpr (HOIST) {
+      if (__builtin_amdgcn_readlane(h_done, jj)) continue;
+      own = __builtin_amdgcn_readlane(h_pos, jj) + 1;
+      sl = __builtin_amdgcn_readlane(h_slot, jj);
+    } else {
+      if (done != nullptr && done[b]) continue;
+      own = pos[b] + 1;
+      sl = slot[b];
+    }
     const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
     const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
     const bool mine = (j == jj);
@@ -1681,6 +1697,20 @@ int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const
   hipLaunchKernelGGL(attn_grouped_kernel<1>, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// Grouped decode attention with the per-sequence (done, pos, slot) loads hoisted to entry.
+int sg_attn_decode_grouped_h(const void* q, const int* pos, const int* slot, const int* done, const void* k_cache,
+                             const void* vt_cache, const void* pk, const void* pvt, int P0, int P0pad, void* out,
+                             int B, int nh, int nkv, int D, int Lmax, float scale, hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad) return -1;
+  if (B == 0) return 0;
+  const int spw = 16 / (nh / nkv);
+  hipLaunchKernelGGL((attn_grouped_kernel<1, true>), dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream,
+                     (const uint16_t*)q, pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache,
+                     (const uint16_t*)pk, (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax,
+                     scale * 1.4426950408889634f);
   return (int)hipGetLastError();
 }
 

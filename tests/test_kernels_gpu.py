@@ -130,7 +130,7 @@ def test_attn_prefill(P0, heads, impl):
         o += n
 
 
-@pytest.mark.parametrize("impl", ["grouped", "grouped6", "grouped_pf", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4",
+@pytest.mark.parametrize("impl", ["grouped", "grouped_h", "grouped6", "grouped_pf", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4",
                                   "split8"])
 @pytest.mark.parametrize("P0", [0, 75])
 def test_attn_decode(P0, impl):

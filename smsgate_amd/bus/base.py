@@ -177,6 +177,11 @@ class Msg:
     def seq(self) -> int:
         return self.metadata.sequence
 
+    @property
+    def settled(self) -> bool:
+        """Already acked / nak'ed / terminated by this holder."""
+        return self._done
+
     async def ack(self) -> None:
         if not self._done:
             self._done = True

@@ -62,8 +62,10 @@ def _pipeline(settings, backend_name: Optional[str] = None, engine: Optional[str
         from .parse.backends.local_llm import RemoteLLMBackend
         from .serving.remote import RemoteEngineClient
 
-        backend = RemoteLLMBackend(RemoteEngineClient(Client(engine.replace("unix://", ""), family="AF_UNIX")),
-                                   max_batch=settings.parser_batch_size)
+        path = engine.replace("unix://", "")
+        # the connector lets the client reconnect after an engine-server restart
+        client = RemoteEngineClient(connector=lambda: Client(path, family="AF_UNIX"))
+        backend = RemoteLLMBackend(client, max_batch=settings.parser_batch_size)
     else:
         backend = create_backend(name)
     return ParsePipeline(backend, open_cache(settings.parser_cache_path))
@@ -187,14 +189,26 @@ def _engine_server(a) -> None:
     from .parse.backends.local_llm import build_engine
     from .serving.remote import EngineServer
 
-    eng = build_engine(a.model, a.checkpoint, a.device, max_slots=a.max_slots)
+    from .config import get_settings
+    from .parse.backends.local_llm import MissingCheckpoint, resolve_checkpoint
+
+    st = get_settings()
+    model = a.model or st.llm_model
+    try:  # before touching the GPU: no trained weights -> exit non-zero, never serve random ones silently
+        ckpt = resolve_checkpoint(model, a.checkpoint or st.llm_checkpoint, a.random_init)
+    except MissingCheckpoint as exc:
+        log.error("engine-server: %s", exc)
+        raise SystemExit(2) from exc
+    if ckpt is None:
+        log.warning("engine-server: serving RANDOM-INIT weights (--random-init): answers are meaningless")
+    eng = build_engine(model, ckpt, a.device, random_init=a.random_init, max_slots=a.max_slots)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
     path = a.listen.replace("unix://", "")
     if os.path.exists(path):
         os.unlink(path)
-    log.info("engine server on %s (%s, %d slots)", a.listen, a.model, a.max_slots)
+    log.info("engine server on %s (%s, %s, %d slots)", a.listen, model, ckpt or "random-init", a.max_slots)
     from .obs.metrics import EngineMetricsExporter, start_metrics_server
 
     start_metrics_server(env_var="ENGINE_METRICS_PORT", default=9104)
@@ -306,8 +320,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="run the C++ broker (smsgate-busd; msgpack protocol only, same journal format)")
     ep = sp.add_parser("engine-server")
     ep.add_argument("--listen", default="unix:///tmp/smsgate-engine0.sock")
-    ep.add_argument("--model", default="smollm-135m")
-    ep.add_argument("--checkpoint", default=None)
+    ep.add_argument("--model", default=None, help="default: LLM_MODEL (smollm-135m)")
+    ep.add_argument("--checkpoint", default=None, help="safetensors weights (default: LLM_CHECKPOINT)")
+    ep.add_argument("--random-init", action="store_true",
+                    help="serve random weights (throughput tests only; every SMS ends in the DLQ)")
     ep.add_argument("--device", default="cuda:0")
     ep.add_argument("--max-slots", type=int, default=4096)
     pl = sp.add_parser("pipeline")

@@ -87,8 +87,19 @@ class ExtractorTokenizer:
     def prefix_ids(self, system: str) -> List[int]:
         return [self.bos] + self.encode(system)
 
+    truncated = 0  # bodies cut to max_body tokens (also the llm_prompt_truncated_total counter)
+
     def message_ids(self, bodies: Sequence[str], max_body: int) -> List[List[int]]:
+        """``<sms> body <ans>`` ids.  A body longer than ``max_body`` tokens keeps
+        its first ``max_body`` tokens; every such cut is counted (the extractor
+        never sees the tail, where balances often are), never silent."""
         enc = self.encode_batch(bodies)
+        cut = sum(1 for e in enc if len(e) > max_body)
+        if cut:
+            self.truncated += cut
+            from ..obs.metrics import LLM_TRUNCATED
+
+            LLM_TRUNCATED.inc(cut)
         return [[self.sms] + e[:max_body] + [self.ans] for e in enc]
 
 

@@ -58,6 +58,7 @@ __all__ = [
     "LLM_COMPLETED",
     "LLM_ACTIVE",
     "LLM_WAITING",
+    "LLM_TRUNCATED",
     "EngineMetricsExporter",
     "start_metrics_server",
     "render_latest",
@@ -74,6 +75,8 @@ PROCESSING_TIME = Histogram(
     "Seconds spent parsing one message",
     buckets=(0.001, 0.01, 0.05, 0.1, 0.25, 0.5, 1, 2, 5),
 )
+LLM_TRUNCATED = Counter("llm_prompt_truncated_total",
+                        "SMS bodies cut to the extractor's max_body_tokens before extraction")
 GEMINI_LATENCY = Summary("sms_parser_gemini_seconds", "Seconds spent in the extraction backend call")
 ACK_PENDING = Gauge("sms_parser_ack_pending", "Delivered-but-unacked messages of the parser consumer")
 

@@ -26,6 +26,7 @@ class SpanStats:
     count: int = 0
     total_s: float = 0.0
     max_s: float = 0.0
+    items: int = 0  # messages covered (a batch transaction covers many)
 
     @property
     def mean_s(self) -> float:
@@ -38,18 +39,19 @@ class Tracer:
         self._stats: Dict[str, SpanStats] = {}
         self._lock = threading.Lock()
 
-    def record(self, name: str, dt: float) -> None:
+    def record(self, name: str, dt: float, items: int = 1) -> None:
         with self._lock:
             s = self._stats.get(name)
             if s is None:
                 s = self._stats[name] = SpanStats()
             s.count += 1
+            s.items += items
             s.total_s += dt
             if dt > s.max_s:
                 s.max_s = dt
 
     @contextlib.contextmanager
-    def span(self, name: str) -> Iterator[None]:
+    def span(self, name: str, items: int = 1) -> Iterator[None]:
         if not self.enabled:
             yield
             return
@@ -60,11 +62,11 @@ class Tracer:
             with cm:
                 yield
         finally:
-            self.record(name, time.perf_counter() - t0)
+            self.record(name, time.perf_counter() - t0, items)
 
     def snapshot(self) -> Dict[str, SpanStats]:
         with self._lock:
-            return {k: SpanStats(v.count, v.total_s, v.max_s) for k, v in self._stats.items()}
+            return {k: SpanStats(v.count, v.total_s, v.max_s, v.items) for k, v in self._stats.items()}
 
     def reset(self) -> None:
         with self._lock:
@@ -75,10 +77,24 @@ tracer = Tracer(enabled=os.getenv("SMSGATE_TRACE", "1") != "0")
 
 
 @contextlib.contextmanager
-def start_transaction(op: str, name: str) -> Iterator[None]:
+def start_transaction(op: str, name: str, messages: Optional[int] = None) -> Iterator[None]:
+    """One transaction; ``messages`` = how many SMS it covers.  The reference opens
+    one per message (worker.py:33-55, :80); a batched handler opens one per batch
+    and tags it with the message count (``sms.messages`` tag and data on the Sentry
+    transaction, ``items`` in the local span stats), so per-message rates are
+    recoverable from either side."""
     sdk = errors._sdk
     cm = sdk.start_transaction(op=op, name=name) if sdk is not None else contextlib.nullcontext()
-    with cm, tracer.span(f"{op}/{name}"):
+    n = 1 if messages is None else int(messages)
+    with cm as txn, tracer.span(f"{op}/{name}", items=n):
+        if messages is not None and txn is not None:
+            for setter, key in (("set_tag", "sms.messages"), ("set_data", "sms.messages")):
+                fn = getattr(txn, setter, None)
+                if fn is not None:
+                    try:
+                        fn(key, n)
+                    except Exception:  # noqa: BLE001 — tracing must never break the handler
+                        pass
         yield
 
 

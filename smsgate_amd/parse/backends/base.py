@@ -13,13 +13,22 @@ from __future__ import annotations
 import abc
 from typing import Any, Dict, List, Sequence, Union
 
-__all__ = ["ParserBackend", "ExtractResult", "BackendError"]
+from ...runtime.errors import TransientError
+
+__all__ = ["ParserBackend", "ExtractResult", "BackendError", "BackendUnavailable"]
 
 ExtractResult = Union[Dict[str, Any], BaseException]
 
 
 class BackendError(RuntimeError):
     """The backend answered, but not with a usable JSON object."""
+
+
+class BackendUnavailable(BackendError, TransientError):
+    """The backend could not be reached at all (engine process down, socket
+    closed).  Not the message's fault: :class:`~smsgate_amd.parse.pipeline.ParsePipeline`
+    re-raises it for the whole batch so the stage naks and retries the batch,
+    instead of routing every message to the DLQ."""
 
 
 class ParserBackend(abc.ABC):

@@ -7,19 +7,26 @@ engine thread; under ``torchrun`` every rank builds its own (data-parallel
 replicas consuming ``sms.raw`` as one competing consumer group —
 :mod:`smsgate_amd.parallel`).
 
-Weights: ``LLM_CHECKPOINT`` (safetensors, serving layout) or random-init of
-the named architecture (``LLM_MODEL``, default ``smollm-135m``) — the box has
-no pretrained checkpoint, so random-init output values are schema-valid but
-semantically meaningless and post-processing routes them to the DLQ.
+Weights: ``LLM_CHECKPOINT`` (safetensors, serving layout), else the trained
+checkpoint bundled for ``LLM_MODEL`` if there is one.  With neither,
+:func:`build_engine` **refuses to start** (:class:`MissingCheckpoint`):
+random-init output is schema-valid but meaningless, so a silent fallback would
+route every SMS to the DLQ.  Random weights are only for throughput runs and
+must be asked for (``random_init=True``, ``engine-server --random-init``).
 """
 from __future__ import annotations
 
 import os
 from typing import Any, Dict, List, Optional, Sequence
 
+from ...runtime.errors import TransientError
 from .base import BackendError, ExtractResult, ParserBackend
 
-__all__ = ["LocalLLMBackend", "RemoteLLMBackend", "build_engine"]
+__all__ = ["LocalLLMBackend", "RemoteLLMBackend", "build_engine", "MissingCheckpoint", "resolve_checkpoint"]
+
+
+class MissingCheckpoint(RuntimeError):
+    """No trained weights for the requested model and random init not requested."""
 
 
 def bundled_checkpoint(model: str) -> Optional[str]:
@@ -31,11 +38,27 @@ def bundled_checkpoint(model: str) -> Optional[str]:
     return str(p) if p.exists() else None
 
 
+def resolve_checkpoint(model: str, checkpoint: Optional[str] = None, random_init: bool = False) -> Optional[str]:
+    """The weights file to serve: ``checkpoint``, else ``LLM_CHECKPOINT``, else the
+    bundled checkpoint of ``model``; None only with ``random_init``.  Raises
+    :class:`MissingCheckpoint` otherwise (and when a named file does not exist)."""
+    if random_init:
+        return None
+    ck = checkpoint or os.getenv("LLM_CHECKPOINT") or bundled_checkpoint(model)
+    if not ck:
+        raise MissingCheckpoint(
+            f"no trained checkpoint for model {model!r}: set LLM_CHECKPOINT / --checkpoint to a safetensors file "
+            f"(python -m smsgate_amd train-extractor --model {model} --out ...), or pass --random-init for a "
+            "throughput-only run")
+    if not os.path.exists(ck):
+        raise MissingCheckpoint(f"checkpoint {ck!r} does not exist")
+    return ck
+
+
 def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
                  seed: int = 0, random_init: bool = False, **engine_kw: Any):
-    """Engine for ``model``: weights from ``checkpoint``, else the bundled trained
-    checkpoint for that model if there is one, else random init (``random_init=True``
-    forces random weights: the throughput benchmark)."""
+    """Engine for ``model`` with the weights :func:`resolve_checkpoint` picks;
+    ``random_init=True`` serves random weights (throughput benchmarks only)."""
     import torch
 
     from ...models.extractor import CONFIGS, ExtractorWeights
@@ -46,8 +69,7 @@ def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, d
     dev = torch.device(device)
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
-    if checkpoint is None and not random_init:
-        checkpoint = bundled_checkpoint(model)
+    checkpoint = resolve_checkpoint(model, checkpoint, random_init)
     if checkpoint:
         w = ExtractorWeights.load(checkpoint, cfg, device=dev)
     else:
@@ -129,5 +151,7 @@ class RemoteLLMBackend(ParserBackend):
     async def extract_batch(self, bodies: Sequence[str]) -> List[ExtractResult]:
         try:
             return list(await self.client.extract(bodies))
+        except TransientError:
+            raise  # engine unreachable: the stage naks the batch (no DLQ traffic)
         except Exception as exc:  # noqa: BLE001 — every message of the batch fails loudly
             return [exc] * len(bodies)

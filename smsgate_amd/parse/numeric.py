@@ -11,10 +11,6 @@ including its documented quirks, which are *contracts* (golden tests in
   (``'1.234.567' -> 1234.567``);
 * blanks are dropped, then everything but ``[0-9.-]``; empty -> ``0.0``;
 * an unparsable remainder (e.g. ``'None'``) raises :class:`ValueError`.
-
-A native (C++) fast path with identical semantics lives in
-``smsgate_amd/native/fastparse.cpp``; this module is the reference
-implementation and the fallback.
 """
 from __future__ import annotations
 

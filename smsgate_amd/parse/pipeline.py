@@ -32,6 +32,7 @@ from typing import Any, Dict, List, Optional, Sequence
 from ..models.domain import PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
 from ..obs.errors import sentry_capture
 from ..obs.metrics import GEMINI_LATENCY
+from ..runtime.errors import TransientError
 from .backends.base import BackendError, ParserBackend
 from .cache import MemoryKV, ResponseCache, cache_key
 from .dates import fix_broken_datetime, parse_custom_datetime, parse_unix_timestamp
@@ -124,6 +125,7 @@ class ParsePipeline:
         return (await self.parse_batch([raw]))[0]
 
     async def parse_batch(self, raws: Sequence[RawSMS]) -> List[ParseResult]:
+        t_start = time.perf_counter()
         n = len(raws)
         results: List[Optional[ParseResult]] = [None] * n
         bodies: List[Optional[str]] = [None] * n
@@ -158,12 +160,15 @@ class ParsePipeline:
                 t0 = time.perf_counter()
                 try:
                     got = await self.backend.extract_batch(ubodies)
+                except TransientError:
+                    raise  # backend unreachable: the stage naks the batch and retries it
                 except Exception as exc:  # whole-batch failure
                     got = [exc] * len(ubodies)
-                dt = time.perf_counter() - t0
+                for r in got:
+                    if isinstance(r, TransientError):
+                        raise r
                 self.backend_calls += 1
-                self.backend_seconds += dt
-                GEMINI_LATENCY.observe(dt / max(1, len(ubodies)))
+                self.backend_seconds += time.perf_counter() - t0
                 to_cache = []
                 for b, r in zip(ubodies, got):
                     if not isinstance(r, BaseException) and not isinstance(r, dict):
@@ -184,4 +189,11 @@ class ParsePipeline:
                 r = postprocess_answer(raws[i], bodies[i], ans, self.tz)  # type: ignore[arg-type]
                 r.cached = i in cached
                 results[i] = r
+        # One observation per message, like the reference's per-message timer around
+        # parse_sms_llm (worker.py:130-133, metrics.py:48-53): _count == messages
+        # parsed.  The value is the latency each message experienced — the wall time
+        # of the batched parse it was part of.
+        dt = time.perf_counter() - t_start
+        for _ in range(n):
+            GEMINI_LATENCY.observe(dt)
         return results  # type: ignore[return-value]

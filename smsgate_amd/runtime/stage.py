@@ -9,8 +9,17 @@ is the one loop, written once:
 * pulls *batches* from a durable competing consumer (``batch`` ≤ backend max);
 * runs up to ``concurrency`` batch handlers at once (I/O-bound handlers such as
   a remote LLM or a database get overlap; a GPU handler gets a full batch);
-* never dies on a handler exception: the batch's un-acked messages are
-  ``nak``-ed with a backoff delay (redelivered later) and the error captured;
+* never dies on a handler exception (D1/D2), and bounds poison messages:
+
+  - a :class:`~smsgate_amd.runtime.errors.TransientError` (engine restarting,
+    socket closed) naks the whole batch with a delay — not the messages' fault;
+  - any other exception re-runs the batch one message at a time, so the good
+    messages of the batch go through and only the failing one is isolated;
+    that one is nak'ed with a delay until it has been delivered
+    ``poison_after`` times, then handed to ``dead_letter`` (the parser
+    publishes a DLQ envelope) and terminated — it never redelivers forever
+    (the reference acked every handled branch, worker.py:109-189, but an
+    *unhandled* exception killed its loop);
 * exports lag/ack-pending gauges from ``consumer_info`` on a timer;
 * drains in-flight batches on stop (graceful shutdown, worker.py:241-263).
 """
@@ -23,12 +32,26 @@ from typing import Awaitable, Callable, List, Optional, Sequence
 
 from ..bus.base import Bus, Msg, Subscription
 from ..obs.errors import sentry_capture
+from .errors import TransientError
 
-__all__ = ["Stage", "BatchHandler"]
+__all__ = ["Stage", "BatchHandler", "dlq_publisher"]
 
 log = logging.getLogger(__name__)
 
 BatchHandler = Callable[[Sequence[Msg]], Awaitable[None]]
+DeadLetter = Callable[[Msg, BaseException], Awaitable[None]]
+
+
+def dlq_publisher(bus: Bus, subject: str) -> DeadLetter:
+    """Dead-letter callback publishing the ``{"err", "entry": <payload text>}``
+    envelope (the reference's shapes a/d/f, worker.py:105, writer.py:80-82)."""
+    import json
+
+    async def publish(m: Msg, exc: BaseException) -> None:
+        data = m.data if isinstance(m.data, (bytes, bytearray)) else str(m.data).encode()
+        await bus.publish(subject, json.dumps({"err": str(exc), "entry": data.decode(errors="ignore")}).encode())
+
+    return publish
 
 
 class Stage:
@@ -48,6 +71,8 @@ class Stage:
         stats_interval: float = 5.0,
         on_stats: Optional[Callable[[int, int], None]] = None,
         name: Optional[str] = None,
+        poison_after: int = 5,
+        dead_letter: Optional[DeadLetter] = None,
     ) -> None:
         self.bus = bus
         self.subject = subject
@@ -62,6 +87,10 @@ class Stage:
         self.stats_interval = stats_interval
         self.on_stats = on_stats
         self.name = name or durable
+        self.poison_after = poison_after
+        self.dead_letter = dead_letter
+        self.dead_lettered = 0
+        self.transient_errors = 0
         self.sub: Optional[Subscription] = None
         self.processed = 0
         self.batches = 0
@@ -97,17 +126,64 @@ class Stage:
             await self.handler(msgs)
         except asyncio.CancelledError:
             raise
+        except TransientError as exc:
+            self.transient_errors += 1
+            log.warning("%s: dependency unavailable, batch of %d nak'ed: %s", self.name, len(msgs), exc)
+            await self._nak(msgs)
         except Exception as exc:
             self.handler_errors += 1
             log.exception("%s: handler failed on a batch of %d", self.name, len(msgs))
             sentry_capture(exc, extras={"stage": self.name, "batch": len(msgs)})
-            for m in msgs:
-                try:
-                    await m.nak(self.nak_delay)
-                except Exception:  # pragma: no cover
-                    pass
+            if len(msgs) == 1:
+                await self._failed(msgs[0], exc)
+            else:
+                await self._isolate(msgs)
         self.processed += len(msgs)
         self.batches += 1
+
+    async def _nak(self, msgs: Sequence[Msg]) -> None:
+        for m in msgs:
+            try:
+                await m.nak(self.nak_delay)
+            except Exception:  # pragma: no cover — the bus redelivers after ack_wait anyway
+                pass
+
+    async def _isolate(self, msgs: Sequence[Msg]) -> None:
+        """Re-run a failed batch one message at a time (skipping any the handler
+        already settled before it raised)."""
+        for i, m in enumerate(msgs):
+            if m.settled:
+                continue
+            try:
+                await self.handler([m])
+            except asyncio.CancelledError:
+                raise
+            except TransientError:
+                self.transient_errors += 1
+                await self._nak(msgs[i:])
+                return
+            except Exception as exc:  # noqa: BLE001
+                await self._failed(m, exc)
+
+    async def _failed(self, m: Msg, exc: BaseException) -> None:
+        delivered = getattr(getattr(m, "metadata", None), "num_delivered", 1) or 1
+        if self.poison_after <= 0 or delivered < self.poison_after:
+            await self._nak([m])
+            return
+        self.dead_lettered += 1
+        log.error("%s: message seq=%s failed %d deliveries, dead-lettered: %s", self.name,
+                  getattr(m, "seq", "?"), delivered, exc)
+        if self.dead_letter is not None:
+            try:
+                await self.dead_letter(m, exc)
+            except Exception as dl_exc:  # noqa: BLE001 — keep it for a later delivery
+                sentry_capture(dl_exc, extras={"stage": self.name})
+                await self._nak([m])
+                return
+        try:
+            await m.term()
+        except Exception:  # pragma: no cover
+            pass
 
     async def _stats(self) -> None:
         while not self._stop.is_set():

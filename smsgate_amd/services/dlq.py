@@ -2,8 +2,10 @@
 
 Consumes ``sms.failed`` as durable ``parser_worker_dlq`` (dlq_worker.py:84-90),
 logs every envelope pretty-printed and, with ``--reparse``, runs the message
-through the parse pipeline again and routes the result exactly like the parser
-worker (parsed → ``sms.parsed`` + ``sms.processing``; failures back to the DLQ).
+through the parse pipeline again.  Successes are routed like the parser worker
+(``sms.parsed`` + ``sms.processing``); a message that fails again is logged,
+counted (``reparse_failed``) and acked, never republished to ``sms.failed`` —
+this worker reads that subject, so a republish would loop forever.
 
 Fixes: every message is acked (the reference never acked
 non-``raw`` payloads in reparse mode), and every envelope shape that carries
@@ -58,6 +60,7 @@ class DlqWorker:
         self.seen = 0
         self.reparsed = 0
         self.not_reparsable = 0
+        self.reparse_failed = 0
         self.log: List[Dict[str, Any]] = []
         # reparse runs under a profiler session (dlq_worker.py:70-74)
         self.profiler = Profiler("dlq_reparse")
@@ -86,8 +89,17 @@ class DlqWorker:
         if to_reparse and self.pipeline is not None:
             with self.profiler:
                 publishes, counts = await route_batch(self.pipeline, to_reparse)
-                if publishes:
-                    await self.bus.publish_many(publishes)
+                # Only successes leave the DLQ.  A message that fails again is
+                # logged and acked here, never republished to sms.failed: this
+                # worker consumes that subject, so a republish would re-feed it
+                # forever (and re-call the backend on every lap).
+                keep = [(s, p) for s, p in publishes if s != SUBJECT_FAILED]
+                for s, p in publishes:
+                    if s == SUBJECT_FAILED:
+                        self.reparse_failed += 1
+                        log.warning("DLQ reparse failed again (dropped from the DLQ loop): %s", p[:300])
+                if keep:
+                    await self.bus.publish_many(keep)
             self.reparsed += len(to_reparse)
         for m in msgs:
             await m.ack()

@@ -26,7 +26,7 @@ from ..models.domain import ParsedSMS
 from ..obs import metrics as M
 from ..obs.errors import sentry_capture
 from ..runtime.retry import retry
-from ..runtime.stage import Stage
+from ..runtime.stage import Stage, dlq_publisher
 from ..sinks.base import Sink
 
 __all__ = ["WriterService"]
@@ -50,7 +50,7 @@ class WriterService:
         self._upsert = retry(attempts=retry_attempts, wait_min=retry_min, wait_max=retry_max)(self._upsert_all)
         self.stage = Stage(bus, SUBJECT_PARSED, durable, self.handle_batch, batch=batch,
                            stats_interval=stats_interval, ack_wait=ack_wait, on_stats=lambda p, a: M.WRITER_LAG.set(p),
-                           name="pb_writer")
+                           name="pb_writer", dead_letter=dlq_publisher(bus, SUBJECT_FAILED))
 
     async def _upsert_all(self, records: Sequence[ParsedSMS]) -> None:
         for s in self.sinks:

@@ -164,33 +164,81 @@ class EngineServer:
             self.serve_until(pred)
         finally:
             listener.close()
+            for c in self._live():  # clients see EOF (and reconnect to the next server)
+                try:
+                    c.close()
+                except OSError:
+                    pass
+            self.conns = [None] * len(self.conns)
 
 
 class RemoteEngineClient:
-    """Async client: tokenises, ships ids, awaits ids, detokenises into answers."""
+    """Async client: tokenises, ships ids, awaits ids, detokenises into answers.
 
-    def __init__(self, conn: Connection, tokenizer=None, max_body_tokens: int = 128) -> None:
+    ``connector`` (a zero-argument callable returning a fresh
+    :class:`~multiprocessing.connection.Connection`) makes the client survive an
+    engine-server restart: when the socket closes, every in-flight request fails
+    with :class:`~smsgate_amd.parse.backends.base.BackendUnavailable` (a
+    transient error: the parser stage naks the batch and retries it later
+    instead of dead-lettering its messages), and the next request reconnects.
+    """
+
+    def __init__(self, conn: Optional[Connection] = None, tokenizer=None, max_body_tokens: int = 128,
+                 connector: Optional[Callable[[], Connection]] = None) -> None:
         from ..models.tokenizer import load_tokenizer
         from .fsm import DEFAULT_FIELDS
 
-        self.conn = conn
+        if conn is None and connector is None:
+            raise ValueError("RemoteEngineClient needs a connection or a connector")
+        self.connector = connector
         self.tok = tokenizer or load_tokenizer()
         self.fields = [f.name for f in DEFAULT_FIELDS]
         self.max_body = max_body_tokens
         self._ids = itertools.count(1)
         self._pending: Dict[int, Any] = {}
         self._send_lock = threading.Lock()
+        self._conn_lock = threading.Lock()
         self.control: "queue.Queue[Any]" = queue.Queue()
-        self._reader = threading.Thread(target=self._read_loop, name="engine-client", daemon=True)
+        self.conn: Optional[Connection] = None
+        self.reconnects = 0
+        if conn is None:
+            conn = connector()  # type: ignore[misc]
+        self._attach(conn)
+
+    def _attach(self, conn: Connection) -> None:
+        self.conn = conn
+        self._reader = threading.Thread(target=self._read_loop, args=(conn,), name="engine-client", daemon=True)
         self._reader.start()
 
-    def _read_loop(self) -> None:
+    def _unavailable(self, why: str):
+        from ..parse.backends.base import BackendUnavailable
+
+        return BackendUnavailable(why)
+
+    def _connection(self) -> Connection:
+        with self._conn_lock:
+            if self.conn is not None:
+                return self.conn
+            if self.connector is None:
+                raise self._unavailable("engine server closed (no connector to reconnect)")
+            try:
+                conn = self.connector()
+            except OSError as exc:
+                raise self._unavailable(f"engine server unreachable: {exc}") from exc
+            self.reconnects += 1
+            self._attach(conn)
+            return conn
+
+    def _read_loop(self, conn: Connection) -> None:
         while True:
             try:
-                buf = self.conn.recv_bytes()
+                buf = conn.recv_bytes()
             except (EOFError, OSError):
+                with self._conn_lock:
+                    if self.conn is conn:
+                        self.conn = None
                 for fut, loop in list(self._pending.values()):
-                    loop.call_soon_threadsafe(self._set_exc, fut, ConnectionError("engine server closed"))
+                    loop.call_soon_threadsafe(self._set_exc, fut, self._unavailable("engine server closed"))
                 self._pending.clear()
                 self.control.put(None)
                 return
@@ -221,8 +269,9 @@ class RemoteEngineClient:
             fut.set_exception(e)
 
     def send_control(self, obj: Any) -> None:
+        conn = self._connection()
         with self._send_lock:
-            self.conn.send_bytes(P.pack_control(obj))
+            conn.send_bytes(P.pack_control(obj))
 
     def decode_answers(self, seqs: List[List[int]]) -> List[Dict[str, str]]:
         sep = self.tok.sep
@@ -249,7 +298,15 @@ class RemoteEngineClient:
         fut = loop.create_future()
         self._pending[rid] = (fut, loop)
         msg = P.pack_ids(b"Q", rid, ids)
-        with self._send_lock:
-            self.conn.send_bytes(msg)
+        conn = self._connection()
+        try:
+            with self._send_lock:
+                conn.send_bytes(msg)
+        except OSError as exc:  # broken pipe: the server went away under us
+            self._pending.pop(rid, None)
+            with self._conn_lock:
+                if self.conn is conn:
+                    self.conn = None
+            raise self._unavailable(f"engine server send failed: {exc}") from exc
         seqs = await fut
         return self.decode_answers(seqs)

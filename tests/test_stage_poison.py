@@ -1,0 +1,227 @@
+"""Stage failure policy: poison messages are isolated and dead-lettered, transient
+dependency failures nak the whole batch, and the parser worker never turns an
+engine outage into DLQ traffic (stage.py:105, cli.py:65)."""
+from __future__ import annotations
+
+from conftest import REFERENCE_CASES, drain
+from smsgate_amd.bus import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_RAW, MemoryBus
+from smsgate_amd.runtime.errors import TransientError
+from smsgate_amd.runtime.stage import Stage, dlq_publisher
+
+
+async def _pump(stage: Stage, rounds: int = 40) -> None:
+    import asyncio
+
+    sub = await stage.open()
+    for _ in range(rounds):
+        msgs = await sub.fetch(stage.batch, 0.02)
+        if msgs:
+            await stage._run_batch(msgs)
+        else:
+            await asyncio.sleep(0.01)
+
+
+def test_poison_message_isolated_then_dead_lettered(arun):
+    bus = MemoryBus()
+    handled, calls = [], []
+
+    async def handler(msgs):
+        calls.append(len(msgs))
+        for m in msgs:
+            if m.data == b"poison":
+                raise RuntimeError("handler bug on this payload")
+        for m in msgs:
+            handled.append(m.data)
+            await m.ack()
+
+    async def go():
+        for d in (b"a", b"poison", b"b"):
+            await bus.publish(SUBJECT_RAW, d)
+        st = Stage(bus, SUBJECT_RAW, "g", handler, batch=16, nak_delay=0.0, poison_after=3,
+                   dead_letter=dlq_publisher(bus, SUBJECT_FAILED), stats_interval=0)
+        await _pump(st)
+        info = await bus.consumer_info("SMS", "g")
+        return st, info, await drain(bus, SUBJECT_FAILED)
+
+    st, info, dlq = arun(go())
+    assert sorted(handled) == [b"a", b"b"]  # the good messages of the batch went through at once
+    assert calls[:4] == [3, 1, 1, 1]  # batch failed, then re-run one message at a time
+    assert st.dead_lettered == 1 and st.handler_errors == 3  # delivered 3 times, then dead-lettered
+    assert dlq == [{"err": "handler bug on this payload", "entry": "poison"}]
+    assert info.num_pending == 0 and info.num_ack_pending == 0  # nothing left to redeliver
+
+
+def test_transient_error_naks_batch_without_isolation(arun):
+    bus = MemoryBus()
+    calls = []
+    state = {"down": 2}
+
+    async def handler(msgs):
+        calls.append(len(msgs))
+        if state["down"]:
+            state["down"] -= 1
+            raise TransientError("engine restarting")
+        for m in msgs:
+            await m.ack()
+
+    async def go():
+        for d in (b"a", b"b", b"c"):
+            await bus.publish(SUBJECT_RAW, d)
+        st = Stage(bus, SUBJECT_RAW, "g", handler, batch=16, nak_delay=0.0, poison_after=1,
+                   dead_letter=dlq_publisher(bus, SUBJECT_FAILED), stats_interval=0)
+        await _pump(st)
+        return st, await drain(bus, SUBJECT_FAILED)
+
+    st, dlq = arun(go())
+    assert calls == [3, 3, 3]  # whole batch retried; never split, never dead-lettered
+    assert st.transient_errors == 2 and st.dead_lettered == 0 and dlq == []
+
+
+def test_parser_engine_outage_is_retried_not_dead_lettered(arun):
+    """A backend that cannot reach its engine raises BackendUnavailable: the
+    parser's batch is nak'ed and redelivered, and no message reaches sms.failed."""
+    from smsgate_amd.parse import ParsePipeline
+    from smsgate_amd.parse.backends import RegexBackend
+    from smsgate_amd.parse.backends.base import BackendUnavailable
+    from smsgate_amd.services.gateway import RawSMSPayload, payload_to_raw
+    from smsgate_amd.services.parser import ParserWorker
+
+    state = {"down": 2}
+
+    class Flaky(RegexBackend):
+        async def extract_batch(self, bodies):
+            if state["down"]:
+                state["down"] -= 1
+                raise BackendUnavailable("engine server closed")
+            return await super().extract_batch(bodies)
+
+    bus = MemoryBus()
+
+    async def go():
+        for i, (body, _) in enumerate(REFERENCE_CASES):
+            raw = payload_to_raw(RawSMSPayload(device_id="d", message=body, sender="BANK",
+                                               timestamp=1746541380 + i, source="device"))
+            await bus.publish(SUBJECT_RAW, raw.model_dump_json().encode())
+        w = ParserWorker(bus, ParsePipeline(Flaky()), batch=16, stats_interval=0)
+        w.stage.nak_delay = 0.0
+        await _pump(w.stage)
+        return w, await drain(bus, SUBJECT_FAILED), await drain(bus, SUBJECT_PARSED)
+
+    w, dlq, parsed = arun(go())
+    assert dlq == [] and w.stage.transient_errors == 2
+    assert len(parsed) == 3 and w.counts["ok"] == 3
+
+
+def test_parser_survives_engine_server_restart(arun, tmp_path):
+    """Kill the engine server between two waves of messages and start a new one
+    on the same socket: the parser's client reconnects, the wave sent while the
+    server was down is retried, and nothing reaches sms.failed (cli.py:65)."""
+    import asyncio
+    import threading
+    from multiprocessing.connection import Client
+
+    from smsgate_amd.parse import ParsePipeline
+    from smsgate_amd.parse.backends.local_llm import RemoteLLMBackend
+    from smsgate_amd.serving.echo import EchoEngine
+    from smsgate_amd.serving.remote import EngineServer, RemoteEngineClient
+    from smsgate_amd.services.gateway import RawSMSPayload, payload_to_raw
+    from smsgate_amd.services.parser import ParserWorker
+
+    path = str(tmp_path / "engine.sock")
+
+    def start_server():
+        stop = threading.Event()
+        srv = EngineServer(EchoEngine())
+        th = threading.Thread(target=srv.serve_listener, args=(path, stop), daemon=True)
+        th.start()
+        for _ in range(200):  # wait for the socket
+            if (tmp_path / "engine.sock").exists():
+                break
+            threading.Event().wait(0.01)
+        return stop, th
+
+    async def publish(bus, n, base):
+        for i in range(n):
+            body = f"APPROVED PURCHASE DB SALE: SHOP {base + i}, YEREVAN,06.05.25 14:23,card ***0018. " \
+                   f"Amount:{i + 1}.00 USD, Balance:10.00 USD"
+            raw = payload_to_raw(RawSMSPayload(device_id="d", message=body, sender="BANK",
+                                               timestamp=1746541380 + i, source="device"))
+            await bus.publish(SUBJECT_RAW, raw.model_dump_json().encode())
+
+    async def go():
+        stop, th = start_server()
+        client = RemoteEngineClient(connector=lambda: Client(path, family="AF_UNIX"))
+        bus = MemoryBus()
+        w = ParserWorker(bus, ParsePipeline(RemoteLLMBackend(client, max_batch=64)), batch=64, stats_interval=0)
+        w.stage.nak_delay = 0.05
+        await publish(bus, 5, 0)
+        await _pump(w.stage, rounds=20)
+        stop.set()
+        await asyncio.to_thread(th.join, 5)
+        assert not (tmp_path / "engine.sock").exists()  # listener closed (socket removed)
+        await publish(bus, 5, 100)
+        await _pump(w.stage, rounds=10)  # server down: batches nak'ed, nothing routed
+        down_ok = w.counts["ok"]
+        stop2, th2 = start_server()
+        await _pump(w.stage, rounds=40)
+        stop2.set()
+        await asyncio.to_thread(th2.join, 5)
+        return w, client, down_ok, await drain(bus, SUBJECT_FAILED), await drain(bus, SUBJECT_PARSED)
+
+    w, client, down_ok, dlq, parsed = arun(go())
+    assert dlq == []
+    assert down_ok == 5 and w.stage.transient_errors >= 1
+    assert w.counts["ok"] == 10 and len(parsed) == 10 and client.reconnects >= 1
+
+
+def test_parser_metrics_observe_once_per_message(arun):
+    """sms_parser_processing_seconds and sms_parser_gemini_seconds get one
+    observation per message (worker.py:130-133, metrics.py:43-53), so their
+    _count grows by N after a batch of N; the batch transaction records N items."""
+    from prometheus_client import REGISTRY
+
+    from smsgate_amd.obs.tracing import tracer
+    from smsgate_amd.parse import ParsePipeline
+    from smsgate_amd.parse.backends import RegexBackend
+    from smsgate_amd.services.gateway import RawSMSPayload, payload_to_raw
+    from smsgate_amd.services.parser import ParserWorker
+
+    def count(name):
+        return REGISTRY.get_sample_value(name) or 0.0
+
+    bus = MemoryBus()
+    n = 7
+    bodies = [REFERENCE_CASES[i % 3][0] + f" #{i}" for i in range(n - 1)] + ["Your OTP code: 123456"]
+
+    async def go():
+        for i, b in enumerate(bodies):
+            raw = payload_to_raw(RawSMSPayload(device_id="d", message=b, sender="BANK", timestamp=1746541380 + i,
+                                               source="device"))
+            await bus.publish(SUBJECT_RAW, raw.model_dump_json().encode())
+        w = ParserWorker(bus, ParsePipeline(RegexBackend()), batch=64, stats_interval=0)
+        await _pump(w.stage, rounds=5)
+        return w
+
+    p0, g0 = count("sms_parser_processing_seconds_count"), count("sms_parser_gemini_seconds_count")
+    items0 = tracer.snapshot().get("task/process_parsing")
+    w = arun(go())
+    # the OTP message is a worker keyword skip: never parsed, never timed (worker.py:112-126)
+    assert count("sms_parser_processing_seconds_count") - p0 == n - 1
+    assert count("sms_parser_gemini_seconds_count") - g0 == n - 1
+    items = tracer.snapshot()["task/process_parsing"].items - (items0.items if items0 else 0)
+    assert items == n and sum(w.counts.values()) == n
+
+
+def test_long_body_truncation_is_counted():
+    from prometheus_client import REGISTRY
+
+    from smsgate_amd.models.tokenizer import load_tokenizer
+
+    tk = load_tokenizer()
+    c0 = REGISTRY.get_sample_value("llm_prompt_truncated_total") or 0.0
+    t0 = tk.truncated
+    long_body = REFERENCE_CASES[0][0] + " EXTRA" * 200
+    ids = tk.message_ids([long_body, REFERENCE_CASES[1][0]], 128)
+    assert len(ids[0]) == 130 and ids[0][0] == tk.sms and ids[0][-1] == tk.ans
+    assert tk.truncated - t0 == 1
+    assert (REGISTRY.get_sample_value("llm_prompt_truncated_total") or 0.0) - c0 == 1

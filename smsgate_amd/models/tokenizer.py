@@ -8,7 +8,7 @@ Rust ``tokenizers`` library on the synthetic SMS corpus
 text (Cyrillic, emoji…): unknown strings fall back to byte tokens.
 
 Special tokens: ``<pad> <bos> <eos> <sep> <sms> <ans>``.  The prompt of one
-extraction is ``<bos> SYSTEM_INSTRUCTION`` (shared prefix, cached once on
+extraction is ``<bos> EXTRACTOR_PROMPT`` (shared prefix, cached once on
 the GPU) + ``<sms> body <ans>`` (per message); the answer is the nine field
 values in schema order, each terminated by ``<sep>``.
 """
@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import functools
 from pathlib import Path
-from typing import List, Sequence
+from typing import List, Sequence, Tuple
 
 __all__ = ["ExtractorTokenizer", "SPECIALS", "load_tokenizer", "train_tokenizer", "ASSET"]
 
@@ -28,7 +28,7 @@ DEFAULT_VOCAB = 8192
 def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: int = 60000, seed: int = 1234):
     from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
 
-    from ..parse.schema import SYSTEM_INSTRUCTION
+    from ..parse.schema import EXTRACTOR_PROMPT, SYSTEM_INSTRUCTION
     from ..utils.synth import iter_corpus
 
     tok = Tokenizer(models.BPE())
@@ -44,6 +44,7 @@ def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: 
     def corpus():
         for _ in range(50):
             yield SYSTEM_INSTRUCTION
+            yield EXTRACTOR_PROMPT
         yield from iter_corpus(n_sms, seed)
 
     tok.train_from_iterator(corpus(), trainer=trainer)
@@ -68,6 +69,36 @@ class ExtractorTokenizer:
 
     def encode_batch(self, texts: Sequence[str]) -> List[List[int]]:
         return [e.ids for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
+
+    def encode_offsets(self, texts: Sequence[str]) -> List[Tuple[List[int], List[Tuple[int, int]]]]:
+        """Ids plus each token's ``(start, end)`` character span in its text (a
+        token that carries a leading blank covers it)."""
+        return [(e.ids, e.offsets) for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
+
+    def value_span_ids(self, value: str, body: str, ids: Sequence[int],
+                       offsets: Sequence[Tuple[int, int]]) -> List[int]:
+        """How the extractor writes a field value: the body's own tokens covering
+        it when the value is a token-aligned substring of the body (decoding them
+        and stripping blanks gives back ``value``), else ``encode(value)``.
+
+        Copying the body's tokens verbatim is what the model is trained to do, so
+        a value costs as many decode steps as it has in the body, and the body is
+        an exact draft for speculative decoding (:mod:`smsgate_amd.serving.draft`)."""
+        if not value:
+            return []
+        start = 0
+        while True:
+            a = body.find(value, start)
+            if a < 0:
+                return self.encode(value)
+            z = a + len(value)
+            k0 = next((k for k, (s, e) in enumerate(offsets) if s <= a < e), None)
+            k1 = next((k for k, (s, e) in enumerate(offsets) if e == z), None)
+            if k0 is not None and k1 is not None and k1 >= k0 and body[offsets[k0][0]:a].strip() == "":
+                span = list(ids[k0:k1 + 1])
+                if self.decode(span).strip() == value:
+                    return span
+            start = a + 1
 
     def decode(self, ids: Sequence[int]) -> str:
         return self.tk.decode(list(ids), skip_special_tokens=True)

@@ -9,7 +9,7 @@ its speed.  This module turns the LM into a working extractor.
   normalised exactly like the parse pipeline does before calling a backend
   (:func:`~smsgate_amd.parse.text.normalize_body`); skipped kinds (OTP, …) never
   reach the LLM and are not trained on;
-* sequence: ``<bos> SYSTEM_INSTRUCTION <sms> body <ans>`` followed by the
+* sequence: ``<bos> EXTRACTOR_PROMPT <sms> body <ans>`` followed by the
   compact answer (9 field values, each ended by ``<sep>``): the exact token
   stream the serving engine decodes.  Every target is checked against the
   schema FSM (:mod:`~smsgate_amd.serving.fsm`), so the constrained decoder can
@@ -41,13 +41,13 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.nn.functional as F
 
-from ..parse.schema import SYSTEM_INSTRUCTION
+from ..parse.schema import EXTRACTOR_PROMPT
 from ..parse.text import normalize_body
 from .extractor import CONFIGS, ExtractorWeights, reference_forward
 from .tokenizer import ExtractorTokenizer, load_tokenizer
 
 __all__ = ["TrainConfig", "answer_tokens", "make_examples", "train_extractor", "field_accuracy",
-           "latest_checkpoint"]
+           "latest_checkpoint", "to_serving"]
 
 
 @dataclass
@@ -67,15 +67,28 @@ class TrainConfig:
     ckpt_every: int = 0  # 0 = only at the end (when ckpt_dir is set)
     resume: bool = False
     bucket_mb: float = 64.0
+    vocab_name: str = "train"  # synthetic vocabulary pool (utils.synth.vocab)
+    eval_every: int = 0  # call on_eval(step, serving weights) every N steps (0 = never)
 
 
-def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]]) -> Optional[List[int]]:
+def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]],
+                  body: Optional[str] = None, body_enc=None) -> Optional[List[int]]:
     """Compact answer token ids, or None if the schema FSM cannot emit them (over a
-    field's token cap, or a token outside the field's class)."""
+    field's token cap, or a token outside the field's class).  With the (normalised)
+    ``body`` each copied value is written with the body's own tokens
+    (:meth:`ExtractorTokenizer.value_span_ids`); enum values use the FSM's trie."""
     ids: List[int] = []
+    if body is not None and body_enc is None:
+        body_enc = tok.encode_offsets([body])[0]
     for f in fsm.fields:
         v = answer.get(f.name) or ""
-        ids += (tok.encode(v) if v else []) + [tok.sep]
+        if not v:
+            vt: List[int] = []
+        elif f.kind == "enum" or body is None:
+            vt = tok.encode(v)
+        else:
+            vt = tok.value_span_ids(v, body, body_enc[0], body_enc[1])
+        ids += vt + [tok.sep]
     state = fsm.start_state
     for t in ids:
         state = fsm.step_host(state, t)
@@ -85,15 +98,17 @@ def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]]
 
 
 def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
-                  max_body: int = 128) -> List[Tuple[List[int], List[int]]]:
+                  max_body: int = 128, vocab_name: str = "train") -> List[Tuple[List[int], List[int]]]:
     """``(message ids, answer ids)`` pairs (prefix excluded: it is shared)."""
     from ..utils.synth import generate
 
     out: List[Tuple[List[int], List[int]]] = []
-    items = [s for s in generate(n, seed=seed) if s.answer is not None]
-    msgs = tok.message_ids([normalize_body(s.body) for s in items], max_body)
-    for m, s in zip(msgs, items):
-        a = answer_tokens(tok, fsm, s.answer)
+    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name) if s.answer is not None]
+    bodies = [normalize_body(s.body) for s in items]
+    msgs = tok.message_ids(bodies, max_body)
+    encs = tok.encode_offsets(bodies)
+    for m, s, b, e in zip(msgs, items, bodies, encs):
+        a = answer_tokens(tok, fsm, s.answer, b, e)
         if a is not None:
             out.append((m, a))
     return out
@@ -129,8 +144,19 @@ def _save_checkpoint(ckpt_dir: str, step: int, w: ExtractorWeights, opt, rng: ra
     return path
 
 
+def to_serving(w: ExtractorWeights) -> ExtractorWeights:
+    """bf16 inference copy of (fp32 master) weights."""
+    out = ExtractorWeights(w.cfg, device=w.embed.device, dtype=torch.bfloat16, seed=None)
+    with torch.no_grad():
+        for (_, p), (_, q) in zip(out.named_parameters(), w.named_parameters()):
+            p.copy_(q.to(torch.bfloat16))
+    out.requires_grad_(False)
+    return out
+
+
 def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] = print,
-                    tok: Optional[ExtractorTokenizer] = None) -> ExtractorWeights:
+                    tok: Optional[ExtractorTokenizer] = None,
+                    on_eval: Optional[Callable[[int, ExtractorWeights], None]] = None) -> ExtractorWeights:
     """Train and return **bf16** serving weights."""
     import torch.distributed as dist
 
@@ -145,9 +171,9 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     v_dec = min(mcfg.vocab, (tok.vocab_size + 63) // 64 * 64)
     fsm = build_fsm(tok, v_dec)
     t0 = time.perf_counter()
-    data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens)
+    data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens, cfg.vocab_name)
     log(f"train: {len(data)} examples ({time.perf_counter() - t0:.1f}s), model {cfg.model}")
-    prefix = tok.prefix_ids(SYSTEM_INSTRUCTION)
+    prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
     torch.manual_seed(cfg.seed)
     w = ExtractorWeights(mcfg, device=device, dtype=torch.float32, seed=cfg.seed)
     decay = [p for n, p in w.named_parameters() if not n.startswith("ln")]
@@ -200,14 +226,11 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
             log(f"step {step:5d} loss {loss.item():.4f} lr {lr_at(step):.2e} ({time.perf_counter() - t0:.1f}s)"
                 + (f" x{world} ranks" if world > 1 else ""))
         done = step + 1
+        if on_eval is not None and cfg.eval_every and done % cfg.eval_every == 0 and done < cfg.steps:
+            on_eval(done, to_serving(w))
         if cfg.ckpt_dir and rank == 0 and (done == cfg.steps or (cfg.ckpt_every and done % cfg.ckpt_every == 0)):
             _save_checkpoint(cfg.ckpt_dir, done, w, opt, rng)
-    out = ExtractorWeights(mcfg, device=device, dtype=torch.bfloat16, seed=None)
-    with torch.no_grad():
-        for (n, p), (_, q) in zip(out.named_parameters(), w.named_parameters()):
-            p.copy_(q.to(torch.bfloat16))
-    out.requires_grad_(False)
-    return out
+    return to_serving(w)
 
 
 def _as_rng_state(st):

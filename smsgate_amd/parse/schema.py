@@ -4,6 +4,11 @@
 * :data:`SYSTEM_INSTRUCTION` — the system prompt sent with every extraction
   request; same content and key list as the reference's Gemini prompt
   (gemini_parser.py:37-43) so remote and local backends see one task.
+* :data:`EXTRACTOR_PROMPT` — the local extractor's prompt.  The extractor is
+  fine-tuned on the task, so the instruction lives in its weights and the prompt
+  is only the schema key list (a 242-token Russian instruction would be 60 % of
+  every training sequence and of every decode step's attention for no
+  information: it is constant).
 * :data:`RESPONSE_SCHEMA` — the JSON schema of the answer: nine string
   properties, ``txn_type`` and ``date`` required (gemini_parser.py:46-61),
   expressed as plain JSON (the REST API shape), not google-genai objects.
@@ -13,7 +18,8 @@ from __future__ import annotations
 
 from ..models.domain import CORE_FIELDS, TxnType
 
-__all__ = ["CORE_FIELDS", "SYSTEM_INSTRUCTION", "RESPONSE_SCHEMA", "TXN_TYPES", "GENERATION_TEMPERATURE"]
+__all__ = ["CORE_FIELDS", "SYSTEM_INSTRUCTION", "EXTRACTOR_PROMPT", "RESPONSE_SCHEMA", "TXN_TYPES",
+           "GENERATION_TEMPERATURE"]
 
 TXN_TYPES = tuple(t.value for t in TxnType)
 
@@ -26,6 +32,8 @@ SYSTEM_INSTRUCTION = (
     "txn_type может иметь значения 'debit', 'credit', 'otp' или 'unknown'"
     "Дата в сообщении обычно в формате день.месяц.год часы:минуты"
 )
+
+EXTRACTOR_PROMPT = f"Extract: {' '.join(CORE_FIELDS)}"
 
 RESPONSE_SCHEMA = {
     "type": "OBJECT",

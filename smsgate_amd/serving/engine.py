@@ -9,7 +9,7 @@ Per engine:
   zero-initialised, one fixed region per slot — at ~4.6 MB/slot (135M model,
   ``Lmax`` 200) thousands of concurrent sequences fit in 288 GB, so there is no
   paging/block-table indirection in the attention kernels;
-* **shared prefix**: the system prompt (``<bos> SYSTEM_INSTRUCTION``) is run
+* **shared prefix**: the system prompt (``<bos> EXTRACTOR_PROMPT``) is run
   once at start-up into ``pk``/``pvt``; every sequence attends to it without
   recomputing or copying it (and its K/V stay L2-resident across the batch);
 * **per-row device state** (token, position, FSM state, done flag, output
@@ -40,7 +40,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..models.extractor import ExtractorConfig, ExtractorWeights
 from ..models.tokenizer import ExtractorTokenizer
-from ..parse.schema import SYSTEM_INSTRUCTION
+from ..parse.schema import EXTRACTOR_PROMPT
 from .fsm import DEFAULT_FIELDS, FieldSpec, SchemaFSM, build_fsm
 
 __all__ = ["EngineConfig", "ExtractionEngine", "EngineStats"]
@@ -129,7 +129,7 @@ class _Snapshot:
 class ExtractionEngine:
     def __init__(self, weights: ExtractorWeights, tokenizer: ExtractorTokenizer,
                  cfg: Optional[EngineConfig] = None, fields: Sequence[FieldSpec] = DEFAULT_FIELDS,
-                 system_prompt: str = SYSTEM_INSTRUCTION) -> None:
+                 system_prompt: str = EXTRACTOR_PROMPT) -> None:
         self.cfg = cfg or EngineConfig()
         self.w = weights
         self.mc: ExtractorConfig = weights.cfg

@@ -6,7 +6,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(),
 
 from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, reference_forward  # noqa: E402
 from smsgate_amd.models.tokenizer import load_tokenizer  # noqa: E402
-from smsgate_amd.parse.schema import SYSTEM_INSTRUCTION  # noqa: E402
+from smsgate_amd.parse.schema import EXTRACTOR_PROMPT  # noqa: E402
 from smsgate_amd.serving.engine import EngineConfig, ExtractionEngine  # noqa: E402
 from smsgate_amd.utils.synth import generate_bodies, reference_cases  # noqa: E402
 
@@ -23,7 +23,7 @@ def tiny_engine(request):
 
 def _ref_logits(eng, body, extra=()):
     tk = eng.tok
-    ids = tk.prefix_ids(SYSTEM_INSTRUCTION) + tk.message_ids([body], eng.cfg.max_body_tokens)[0] + list(extra)
+    ids = tk.prefix_ids(EXTRACTOR_PROMPT) + tk.message_ids([body], eng.cfg.max_body_tokens)[0] + list(extra)
     x = torch.tensor([ids], device="cuda")
     with torch.no_grad():
         return reference_forward(eng.w, x, compute_dtype=torch.float32)[0, -1]

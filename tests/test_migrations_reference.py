@@ -1,0 +1,92 @@
+"""Upgrading databases created by the reference's Alembic chain, from each of its
+six revisions (/root/reference/db/migrations/versions/*.py), lands on our head
+schema with every row preserved — including the columns the reference renamed by
+drop-and-add (original_body/raw_body, datetime/date) and the original_key →
+msg_id unique swap (VERDICT r01 missing #2)."""
+from __future__ import annotations
+
+import pytest
+from sqlalchemy import create_engine, inspect, text
+
+from smsgate_amd.db import migrations
+
+# sms_data DDL at each reference revision (columns as the Alembic ops leave them)
+_COMMON = ("id INTEGER PRIMARY KEY, sender VARCHAR NOT NULL, card VARCHAR(4) NOT NULL, "
+           "amount NUMERIC(14,2) NOT NULL, currency VARCHAR(3) NOT NULL, txn_type VARCHAR NOT NULL, "
+           "balance NUMERIC(14,2), merchant VARCHAR, address VARCHAR, city VARCHAR")
+_DDL = {
+    "ab372595639c": "original_key VARCHAR NOT NULL UNIQUE, original_body VARCHAR NOT NULL, datetime TIMESTAMP NOT NULL",
+    "f1a93be77048": "original_key VARCHAR NOT NULL UNIQUE, raw_body VARCHAR NOT NULL, date TIMESTAMP NOT NULL, "
+                    "msg_id VARCHAR, device_id VARCHAR, parser_version VARCHAR",
+    "80b70406bdea": "original_key VARCHAR NOT NULL UNIQUE, raw_body VARCHAR NOT NULL, date TIMESTAMP NOT NULL, "
+                    "device_id VARCHAR, parser_version VARCHAR",
+    "f1ebe9c5dea6": "raw_body VARCHAR NOT NULL, date TIMESTAMP NOT NULL, msg_id VARCHAR UNIQUE, "
+                    "device_id VARCHAR, parser_version VARCHAR",
+    "007078d0ce44": "date TIMESTAMP NOT NULL, msg_id VARCHAR UNIQUE, device_id VARCHAR, parser_version VARCHAR, "
+                    "original_body VARCHAR",
+    "dcbadcb88d59": "msg_id VARCHAR UNIQUE, device_id VARCHAR, parser_version VARCHAR, original_body VARCHAR, "
+                    "datetime TIMESTAMP",
+}
+_KEY = {"ab372595639c": "original_key", "f1a93be77048": "original_key", "80b70406bdea": "original_key"}
+_BODY = {"ab372595639c": "original_body", "f1a93be77048": "raw_body", "80b70406bdea": "raw_body",
+         "f1ebe9c5dea6": "raw_body"}
+_DATE = {"ab372595639c": "datetime", "dcbadcb88d59": "datetime"}
+
+
+def _make_db(tmp_path, rev):
+    eng = create_engine(f"sqlite:///{tmp_path}/ref-{rev}.sqlite")
+    key, body, date = _KEY.get(rev, "msg_id"), _BODY.get(rev, "original_body"), _DATE.get(rev, "date")
+    has_dev = "device_id" in _DDL[rev]
+    with eng.begin() as c:
+        c.execute(text(f"CREATE TABLE sms_data ({_COMMON}, {_DDL[rev]})"))
+        c.execute(text("CREATE TABLE alembic_version (version_num VARCHAR(32) PRIMARY KEY)"))
+        c.execute(text("INSERT INTO alembic_version VALUES (:v)"), {"v": rev})
+        for i in range(3):
+            cols = {"id": i + 1, "sender": "BANK", "card": "0018", "amount": 52 + i, "currency": "USD",
+                    "txn_type": "debit", "balance": 1842.74, "merchant": f"SHOP {i}", "address": "", "city": "YEREVAN",
+                    key: f"key{i}", body: f"body {i}", date: f"2025-05-0{i + 1} 14:23:00"}
+            if has_dev:
+                cols.update(device_id="dev", parser_version="llm-0.2.0")
+            names = ", ".join(cols)
+            c.execute(text(f"INSERT INTO sms_data ({names}) VALUES ({', '.join(':' + k for k in cols)})"), cols)
+    return eng, has_dev
+
+
+@pytest.mark.parametrize("rev", list(_DDL))
+def test_upgrade_from_each_reference_revision(tmp_path, rev):
+    eng, has_dev = _make_db(tmp_path, rev)
+    assert migrations.upgrade(eng) == migrations.HEAD
+    with eng.begin() as c:
+        assert migrations.reference_revision(c) == migrations.REFERENCE_HEAD
+        cols = {col["name"] for col in inspect(c).get_columns("sms_data")}
+        assert cols == {col.name for col in migrations.sms_data.columns}
+        rows = c.execute(text("SELECT msg_id, original_body, datetime, merchant, amount, device_id "
+                              "FROM sms_data ORDER BY id")).all()
+        idx = {i["name"] for i in inspect(c).get_indexes("sms_data")}
+    assert [r[0] for r in rows] == ["key0", "key1", "key2"]  # original_key -> msg_id kept
+    assert [r[1] for r in rows] == ["body 0", "body 1", "body 2"]  # body carried across renames
+    assert [str(r[2])[:16] for r in rows] == ["2025-05-01 14:23", "2025-05-02 14:23", "2025-05-03 14:23"]
+    assert [r[3] for r in rows] == ["SHOP 0", "SHOP 1", "SHOP 2"] and float(rows[2][4]) == 54.0
+    assert [r[5] for r in rows] == (["dev"] * 3 if has_dev else [None] * 3)
+    assert {"idx_sms_sender", "idx_sms_datetime", "idx_sms_txn_type"} <= idx
+    # idempotent, and the upsert path works on the migrated table (msg_id unique)
+    assert migrations.upgrade(eng) == migrations.HEAD
+    with eng.begin() as c, pytest.raises(Exception):
+        c.execute(text("INSERT INTO sms_data (msg_id, sender, datetime, card, amount, currency, txn_type) "
+                       "VALUES ('key0', 'B', '2025-01-01', '1', 1, 'USD', 'debit')"))
+
+
+def test_duplicate_msg_ids_at_f1a93_keep_newest(tmp_path):
+    eng = create_engine(f"sqlite:///{tmp_path}/dup.sqlite")
+    with eng.begin() as c:
+        c.execute(text(f"CREATE TABLE sms_data ({_COMMON}, {_DDL['f1a93be77048']})"))
+        c.execute(text("CREATE TABLE alembic_version (version_num VARCHAR(32) PRIMARY KEY)"))
+        c.execute(text("INSERT INTO alembic_version VALUES ('f1a93be77048')"))
+        for i, mid in enumerate(["m", "m", None]):
+            c.execute(text("INSERT INTO sms_data (id, sender, card, amount, currency, txn_type, original_key, raw_body, "
+                           "date, msg_id) VALUES (:i, 'B', '1', 1, 'USD', 'debit', :k, :b, '2025-01-01', :m)"),
+                      {"i": i + 1, "k": f"k{i}", "b": f"b{i}", "m": mid})
+    migrations.upgrade(eng)
+    with eng.begin() as c:
+        rows = c.execute(text("SELECT msg_id, original_body FROM sms_data ORDER BY id")).all()
+    assert rows == [("m", "b1"), ("k2", "b2")]  # newest duplicate kept; a NULL msg_id falls back to original_key

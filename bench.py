@@ -8,11 +8,22 @@ parser → ``sms.parsed``/``sms.processing``/DLQ → ack.  The reference measure
 its broker stubbed.
 
 Here every message does strictly more work: extraction runs on a *real* LLM —
-the 134.5 M-parameter SmolLM2-135M-architecture extractor (random-init weights:
-no checkpoint exists on the box) on the MI355X through the HIP kernels of
-``smsgate_amd.ops``, schema-FSM-constrained decoding, continuous batching and
-hipGraph-captured decode.  ``--backend fake`` reproduces the reference's
-stubbed-LLM configuration on the CPU for a like-for-like comparison.
+the 134.5 M-parameter SmolLM2-135M-architecture extractor on the MI355X through
+the HIP kernels of ``smsgate_amd.ops``, schema-FSM-constrained decoding,
+continuous batching and hipGraph-captured decode — and every parsed message
+goes on to the ``pb_writer`` stage and an in-memory sink inside the timed region.
+
+Weights (``--weights``): no pretrained checkpoint exists on the box and a 270 MB
+file is not shipped, so by default the flagship is **trained in the run, before
+the timed region** (``--train-steps`` AdamW steps on synthetic bank SMS of the
+*training* vocabulary; data-parallel over RCCL when N > 1, global batch fixed),
+then the timed traffic uses the *held-out* vocabulary (merchant / city / street
+names the model never saw).  The JSON states the weights' provenance, a held-out
+accuracy check, and the routing split (parsed / keyword-skipped / broken / DLQ).
+``--weights random`` is the old worst case (every message decodes to the
+schema caps, all LLM answers end in the DLQ); ``--weights PATH`` serves a
+checkpoint.  ``--backend fake`` reproduces the reference's stubbed-LLM
+configuration on the CPU for a like-for-like comparison.
 
 Layout (``smsgate_amd.parallel.replica``): each rank = one GPU = one
 data-parallel replica; the rank process runs only the engine, and
@@ -45,6 +56,15 @@ def _args(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--backend", default="local_llm", choices=["local_llm", "fake", "regex"])
     p.add_argument("--model", default="smollm-135m")
+    p.add_argument("--weights", default="train",
+                   help="train (in-run, untimed; default) | random (worst case) | path to a safetensors checkpoint")
+    p.add_argument("--train-steps", type=int, default=1200)
+    p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
+    p.add_argument("--train-lr", type=float, default=1e-3)
+    p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",
+                   help="reuse weights trained by an earlier run with the same settings ('' = off)")
+    p.add_argument("--eval-n", type=int, default=500, help="held-out SMS scored before the timed region (0 = skip)")
+    p.add_argument("--traffic-vocab", default="heldout", choices=["heldout", "train"])
     p.add_argument("--msgs-per-step", type=int, default=16384)
     p.add_argument("--max-slots", type=int, default=8192)
     p.add_argument("--steps-per-graph", type=int, default=2)
@@ -90,7 +110,7 @@ def run_replica(args, rank: int, world: int, local: int):
     if args.msgs_per_step % W:
         raise SystemExit("--msgs-per-step must be divisible by --cpu-workers")
     cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
-           "worker_threads": args.worker_threads}
+           "worker_threads": args.worker_threads, "vocab": args.traffic_vocab}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
 
@@ -109,6 +129,10 @@ def run_replica(args, rank: int, world: int, local: int):
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    prov, quality = {}, None
+    weights = None
+    if not echo:
+        weights, prov = acquire_weights(args, f"cuda:{local}", rank, world)
     t_init = time.perf_counter()
     if echo:
         from smsgate_amd.serving.echo import EchoEngine
@@ -119,7 +143,8 @@ def run_replica(args, rank: int, world: int, local: int):
 
         buckets = (tuple(range(args.bucket_step, args.max_slots + 1, args.bucket_step)) if args.bucket_step
                    else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
-        engine = build_engine(args.model, device=f"cuda:{local}", random_init=True, max_slots=args.max_slots,
+        engine = build_engine(args.model, device=f"cuda:{local}", random_init=weights is None, weights=weights,
+                              max_slots=args.max_slots,
                               steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
                               buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
                               split_decode=args.split_decode, split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
@@ -128,6 +153,13 @@ def run_replica(args, rank: int, world: int, local: int):
                               prefill_key_split=args.prefill_key_split,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
+    if not echo and args.eval_n and rank == 0:
+        from smsgate_amd.models.evaluate import evaluate_engine
+
+        q = evaluate_engine(engine, n=args.eval_n, seed=4242, vocab_name="heldout")
+        quality = {"parse_rate": round(q["parse_rate"], 4), "exact": round(q["exact"], 4), "n": q["n"],
+                   "field_acc": {k: round(v, 4) for k, v in q["field_acc"].items()}, "vocab": "heldout"}
+        engine.stats.__init__()
     if not args.no_gc_freeze:
         from smsgate_amd.serving import freeze_gc_for_launch_loop
 
@@ -158,12 +190,53 @@ def run_replica(args, rank: int, world: int, local: int):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
         # routing outcomes summed over ranks: the JSON line reports the whole job
-        keys = ("ok", "fail", "skip")  # route_batch's outcome set, same order on every rank
+        keys = ROUTING_KEYS  # same order on every rank
         c = torch.tensor([counts.get(k, 0) for k in keys], dtype=torch.int64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         counts = dict(zip(keys, (int(x) for x in c.tolist())))
         dist.destroy_process_group()
-    return dt, counts, init_s, estats
+    return dt, counts, init_s, estats, prov, quality
+
+
+ROUTING_KEYS = ("ok", "fail", "skip", "parsed", "keyword_skipped", "sink_stored", "writer_no_merchant", "writer_fail")
+
+
+def acquire_weights(args, device: str, rank: int, world: int):
+    """The flagship's weights for this run and a provenance record (see module doc)."""
+    import hashlib
+
+    import torch
+
+    from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights
+
+    if args.weights == "random":
+        return None, {"weights": "random-init (seed 0): worst case, answers are noise and end in the DLQ"}
+    if args.weights != "train":
+        w = ExtractorWeights.load(args.weights, CONFIGS[args.model], device=torch.device(device))
+        return w, {"weights": f"checkpoint {os.path.basename(args.weights)}"}
+    from smsgate_amd.models.tokenizer import ASSET
+    from smsgate_amd.models.train import TrainConfig, train_extractor
+
+    tc = TrainConfig(model=args.model, steps=args.train_steps, batch=max(8, args.train_batch // world),
+                     lr=args.train_lr, log_every=0)
+    h = hashlib.sha256(repr((tc, world, open(ASSET, "rb").read())).encode(errors="ignore")).hexdigest()[:16]
+    path = os.path.join(args.weights_cache, f"{args.model}-{h}.safetensors") if args.weights_cache else ""
+    prov = {"weights": (f"trained in this run before the timed region: {tc.steps} AdamW steps x {tc.batch * world} "
+                        f"synthetic SMS (training vocabulary), seed {tc.seed}, bf16 autocast"
+                        + (f", data-parallel over {world} ranks (RCCL all-reduce)" if world > 1 else ""))}
+    if path and os.path.exists(path):
+        w = ExtractorWeights.load(path, CONFIGS[args.model], device=torch.device(device))
+        prov["weights"] += " (reused from an earlier identical run's cache)"
+        return w, prov
+    t0 = time.perf_counter()
+    w = train_extractor(tc, device=device, log=lambda s: None)
+    prov["train_s"] = round(time.perf_counter() - t0, 1)
+    if path and rank == 0:
+        os.makedirs(args.weights_cache, exist_ok=True)
+        tmp = path + f".{os.getpid()}.tmp"
+        w.save(tmp)
+        os.replace(tmp, path)
+    return w, prov
 
 
 # ------------------------------------------------------------- CPU (stubbed LLM)
@@ -199,22 +272,30 @@ async def _run_cpu(args):
     await run(args.warmup, args.steps)
     dt = time.perf_counter() - t0
     await worker.stop()
-    return dt, {k: worker.counts[k] - c0[k] for k in c0}, 0.0, {}
+    return dt, {k: worker.counts[k] - c0[k] for k in c0}, 0.0, {}, {}, None
 
 
 def main(argv=None) -> int:
     args = _args(argv)
     rank, world, local = _rank_env()
     if args.backend == "local_llm" or args.cpu_echo_engine:
-        dt, counts, init_s, estats = run_replica(args, rank, world, local)
+        dt, counts, init_s, estats, prov, quality = run_replica(args, rank, world, local)
     else:
-        dt, counts, init_s, estats = asyncio.run(_run_cpu(args))
+        dt, counts, init_s, estats, prov, quality = asyncio.run(_run_cpu(args))
         world = 1
     total = args.msgs_per_step * args.steps * world
-    routed = sum(counts.values())
+    routed = counts.get("ok", 0) + counts.get("fail", 0) + counts.get("skip", 0)
     if routed != total:  # every timed message must have been parsed and routed
         raise SystemExit(f"bench: {routed} messages routed, expected {total}")
     value = total / dt
+    # parsed -> sms.parsed + sms.processing (+ sink); keyword_skipped: worker skip list (never
+    # reaches the LLM); broken: card-less answers (acked, PARSED_SKIP); dlq: sms.failed
+    routing = {"parsed": counts.get("parsed", 0), "keyword_skipped": counts.get("keyword_skipped", 0),
+               "broken": counts.get("skip", 0), "dlq": counts.get("fail", 0)}
+    for k in ("sink_stored", "writer_no_merchant", "writer_fail"):
+        if k in counts:
+            routing[k] = counts[k]
+    llm_routed = routing["parsed"] + routing["broken"] + routing["dlq"]
     if rank == 0:
         gpu = args.backend == "local_llm"
         out = {
@@ -230,22 +311,29 @@ def main(argv=None) -> int:
             "vs_baseline": round(value / BASELINE_MSGS_PER_S, 3),
             "dtype": "bf16",
             "data": ("synthetic; CPU echo engine - harness check only, not a benchmark" if args.cpu_echo_engine
-                     else "synthetic (unique bank-SMS bodies; random-init extractor weights)"),
+                     else f"synthetic unique bank-SMS bodies ({args.traffic_vocab} vocabulary"
+                          + (": merchant/city/street names never seen in training)" if args.traffic_vocab == "heldout"
+                             else ")")),
             "config": {
                 "model": (f"{args.model} extractor LLM (134.5M params, replaces the Gemini call)" if gpu
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
-                "pipeline": "payload->RawSMS->bus sms.raw->parser_worker->sms.parsed/processing|DLQ->ack",
+                "pipeline": ("payload->RawSMS->bus sms.raw->parser_worker->sms.parsed+sms.processing|DLQ->ack"
+                             + ("->pb_writer->in-memory sink" if gpu else "")),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
-                "seq_len": "prefix 75 + ~40 prompt + <=59 schema-constrained output tokens",
+                "seq_len": "shared prefix 20 + ~48 prompt + <=131 schema-constrained output tokens (~38 trained)",
                 "parallelism": f"dp{world}" if gpu else "cpu",
                 "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
                 "max_slots": args.max_slots,
                 "baseline_msgs_per_s": BASELINE_MSGS_PER_S,
             },
-            "routing": counts,
+            "routing": routing,
+            "llm_parsed_share": (round(routing["parsed"] / llm_routed, 4) if llm_routed else None),
             "init_s": round(init_s, 2),
+            **prov,
         }
+        if quality is not None:
+            out["quality_heldout"] = quality
         if args.verbose and estats:
             out["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in estats.items()}
         print(json.dumps(out), flush=True)

@@ -30,6 +30,7 @@ its speed.  This module turns the LM into a working extractor.
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 import os
 import random
@@ -144,12 +145,20 @@ def _save_checkpoint(ckpt_dir: str, step: int, w: ExtractorWeights, opt, rng: ra
     return path
 
 
-def to_serving(w: ExtractorWeights) -> ExtractorWeights:
-    """bf16 inference copy of (fp32 master) weights."""
-    out = ExtractorWeights(w.cfg, device=w.embed.device, dtype=torch.bfloat16, seed=None)
+def to_serving(w: ExtractorWeights, cfg=None) -> ExtractorWeights:
+    """bf16 inference copy of (fp32 master) weights.  Training runs on a vocab-trimmed
+    copy of the architecture (only the tokenizer's ids exist); the serving copy has
+    the full ``cfg.vocab`` embedding with the never-used rows zero (they are masked
+    out of every decode step and no input id reaches them)."""
+    cfg = cfg or w.cfg
+    out = ExtractorWeights(cfg, device=w.embed.device, dtype=torch.bfloat16, seed=None)
     with torch.no_grad():
-        for (_, p), (_, q) in zip(out.named_parameters(), w.named_parameters()):
-            p.copy_(q.to(torch.bfloat16))
+        for (n, p), (_, q) in zip(out.named_parameters(), w.named_parameters()):
+            if n == "embed" and p.shape[0] != q.shape[0]:
+                p.zero_()
+                p[: q.shape[0]].copy_(q.to(torch.bfloat16))
+            else:
+                p.copy_(q.to(torch.bfloat16))
     out.requires_grad_(False)
     return out
 
@@ -175,11 +184,17 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     log(f"train: {len(data)} examples ({time.perf_counter() - t0:.1f}s), model {cfg.model}")
     prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
     torch.manual_seed(cfg.seed)
-    w = ExtractorWeights(mcfg, device=device, dtype=torch.float32, seed=cfg.seed)
+    # train the architecture with its embedding trimmed to the ids the tokenizer can
+    # produce (8192 of SmolLM's 49 152 rows): the other rows never get a gradient, so
+    # carrying them through AdamW would only cost time (exact: see to_serving)
+    tcfg = dataclasses.replace(mcfg, vocab=v_dec)
+    w = ExtractorWeights(tcfg, device=device, dtype=torch.float32, seed=cfg.seed)
     decay = [p for n, p in w.named_parameters() if not n.startswith("ln")]
     no_decay = [p for n, p in w.named_parameters() if n.startswith("ln")]
+    fused = str(device).startswith("cuda")  # one multi-tensor kernel per step instead of per-parameter ops
     opt = torch.optim.AdamW([{"params": decay, "weight_decay": cfg.weight_decay},
-                             {"params": no_decay, "weight_decay": 0.0}], lr=cfg.lr, betas=(0.9, 0.95))
+                             {"params": no_decay, "weight_decay": 0.0}], lr=cfg.lr, betas=(0.9, 0.95),
+                            fused=fused)
 
     gb = GradBuckets(list(w.parameters()), bucket_mb=cfg.bucket_mb)
 
@@ -227,10 +242,10 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
                 + (f" x{world} ranks" if world > 1 else ""))
         done = step + 1
         if on_eval is not None and cfg.eval_every and done % cfg.eval_every == 0 and done < cfg.steps:
-            on_eval(done, to_serving(w))
+            on_eval(done, to_serving(w, mcfg))
         if cfg.ckpt_dir and rank == 0 and (done == cfg.steps or (cfg.ckpt_every and done % cfg.ckpt_every == 0)):
             _save_checkpoint(cfg.ckpt_dir, done, w, opt, rng)
-    return to_serving(w)
+    return to_serving(w, mcfg)
 
 
 def _as_rng_state(st):

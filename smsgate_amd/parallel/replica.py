@@ -62,13 +62,14 @@ def spawn_parser_workers(n: int, rank: int, cfg: Dict[str, Any]) -> Tuple[List[A
     return procs, conns
 
 
-def _payload_bytes(n: int, seed: int) -> List[bytes]:
-    """Synthetic phone posts → RawSMS JSON, exactly as the gateway maps them."""
-    from ..services.gateway import RawSMSPayload, payload_to_raw
+def _payload_bytes(n: int, seed: int, vocab_name: str = "heldout") -> List[bytes]:
+    """Synthetic phone posts (the gateway's ``RawSMSPayload``); ``vocab_name``
+    picks the merchant / city vocabulary (held-out = never seen in training)."""
+    from ..services.gateway import RawSMSPayload
     from ..utils.synth import generate
 
     out = []
-    for s in generate(n, seed=seed):
+    for s in generate(n, seed=seed, vocab_name=vocab_name):
         p = RawSMSPayload(device_id="bench", message=s.body, sender="BANK", timestamp=s.timestamp, source="device")
         out.append(p)
     return out  # type: ignore[return-value]
@@ -86,13 +87,19 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     from ..serving.remote import RemoteEngineClient
     from ..services.gateway import payload_to_raw
     from ..services.parser import ParserWorker
+    from ..services.writer import WriterService
+    from ..sinks.memory import MemorySink
 
     client = RemoteEngineClient(conn, max_body_tokens=cfg.get("max_body_tokens", 128))
     bus = MemoryBus()
     backend = RemoteLLMBackend(client, max_batch=cfg.get("batch", 512))
     worker = ParserWorker(bus, ParsePipeline(backend), batch=cfg.get("batch", 512),
                           concurrency=cfg.get("concurrency", 4), stats_interval=0)
+    # pb_writer with an in-memory sink on sms.parsed (BASELINE config #1: "... -> in-memory sink")
+    sink = MemorySink()
+    writer = WriterService(bus, [sink], batch=cfg.get("writer_batch", 512), stats_interval=0)
     await worker.start()
+    await writer.start()
     client.send_control({"event": "ready", "w": widx})
     prepared: List[List[Any]] = []
     while True:
@@ -101,10 +108,11 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
             break
         if cmd["cmd"] == "prepare":
             n = int(cmd["n"])
-            prepared = [_payload_bytes(n, seed) for seed in cmd["seeds"]]
+            prepared = [_payload_bytes(n, seed, cfg.get("vocab", "heldout")) for seed in cmd["seeds"]]
             client.send_control({"event": "prepared", "w": widx})
         elif cmd["cmd"] == "go":
             c0 = dict(worker.counts)
+            w0 = (writer.stage.processed, writer.ok, writer.skipped, writer.fail)
             t0 = time.perf_counter()
             base = worker.stage.processed
 
@@ -132,8 +140,15 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                     await asyncio.sleep(0.0005)
             if pub_task is not None:
                 await pub_task
+            # the step ends when the writer has consumed every parsed message too
+            parsed = worker.counts["parsed"] - c0["parsed"]
+            while writer.stage.processed - w0[0] < parsed:
+                await asyncio.sleep(0.0005)
             counts = {k: worker.counts[k] - c0[k] for k in c0}
+            counts.update(sink_stored=writer.ok - w0[1], writer_no_merchant=writer.skipped - w0[2],
+                          writer_fail=writer.fail - w0[3])
             client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
+    await writer.stop()
     await worker.stop()
 
 

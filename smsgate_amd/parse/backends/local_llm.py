@@ -56,9 +56,10 @@ def resolve_checkpoint(model: str, checkpoint: Optional[str] = None, random_init
 
 
 def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
-                 seed: int = 0, random_init: bool = False, **engine_kw: Any):
+                 seed: int = 0, random_init: bool = False, weights=None, **engine_kw: Any):
     """Engine for ``model`` with the weights :func:`resolve_checkpoint` picks;
-    ``random_init=True`` serves random weights (throughput benchmarks only)."""
+    ``random_init=True`` serves random weights (throughput benchmarks only);
+    ``weights`` serves an in-memory :class:`ExtractorWeights` (e.g. just trained)."""
     import torch
 
     from ...models.extractor import CONFIGS, ExtractorWeights
@@ -69,6 +70,9 @@ def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, d
     dev = torch.device(device)
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
+    if weights is not None:
+        weights.requires_grad_(False)
+        return ExtractionEngine(weights, load_tokenizer(), EngineConfig(**engine_kw))
     checkpoint = resolve_checkpoint(model, checkpoint, random_init)
     if checkpoint:
         w = ExtractorWeights.load(checkpoint, cfg, device=dev)

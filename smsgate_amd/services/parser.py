@@ -64,7 +64,9 @@ def _dump(obj: Dict[str, Any]) -> bytes:
 async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[List[Tuple[str, bytes]], Dict[str, int]]:
     """Decide every message's output. Returns ``(publishes, counters)``."""
     out: List[Tuple[str, bytes]] = []
-    counts = {"ok": 0, "fail": 0, "skip": 0}
+    # ok / fail / skip are the reference's metric semantics (a keyword skip counts as
+    # ok, D11); parsed and keyword_skipped split "ok" into what actually happened
+    counts = {"ok": 0, "fail": 0, "skip": 0, "parsed": 0, "keyword_skipped": 0}
     texts: List[str] = []
     raws: List[RawSMS] = []
     raw_idx: List[int] = []
@@ -96,6 +98,7 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                 continue
             if worker_should_skip(raw.body):
                 counts["ok"] += 1
+                counts["keyword_skipped"] += 1
                 continue
             raws.append(raw)
             raw_idx.append(i)
@@ -144,6 +147,7 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                 out.append((SUBJECT_PARSED, payload))
                 out.append((SUBJECT_PROCESSING, payload))
                 counts["ok"] += 1
+                counts["parsed"] += 1
     return out, counts
 
 
@@ -156,7 +160,7 @@ class ParserWorker:
         self.bus = bus
         self.pipeline = pipeline
         self.group = group
-        self.counts = {"ok": 0, "fail": 0, "skip": 0}
+        self.counts = {"ok": 0, "fail": 0, "skip": 0, "parsed": 0, "keyword_skipped": 0}
         self.stage = Stage(
             bus,
             SUBJECT_RAW,

@@ -62,6 +62,22 @@ def _pseudo_words(seed: int = 20240601, n: int = 20000, exclude=frozenset()) -> 
     return out
 
 
+def _random_strings(seed: int = 99, n: int = 6000) -> List[str]:
+    """Letter/digit strings with no syllable structure: a language model cannot
+    predict them, so the extractor has to learn to *copy* names from the body."""
+    r = random.Random(seed)
+    alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+    out: List[str] = []
+    seen = set(_GOLDEN_VOCAB)
+    while len(out) < n:
+        k = r.randint(2, 10)
+        w = "".join(r.choice(alpha if r.random() < 0.9 else "0123456789") for _ in range(k))
+        if w[0].isalpha() and w not in seen:
+            seen.add(w)
+            out.append(w)
+    return out
+
+
 def _split(words: Sequence[str]) -> Tuple[List[str], List[str]]:
     """Deterministic train / held-out split (crc32 % 5 == 0 -> held out)."""
     tr, ho = [], []
@@ -81,6 +97,7 @@ class Vocab:
 def _vocabs() -> Dict[str, Vocab]:
     pw = _pseudo_words()
     pw_tr, pw_ho = _split(pw)
+    rs_tr, rs_ho = _split(_random_strings())
     # a third, disjoint pseudo-word pool for the tokenizer's corpus only: it learns
     # syllable-level pieces without any train / held-out / golden word becoming a token
     pw_tok = _pseudo_words(seed=777, n=20000, exclude=frozenset(pw) | _GOLDEN_VOCAB)
@@ -89,10 +106,10 @@ def _vocabs() -> Dict[str, Vocab]:
     half_tr, half_ho = len(pw_tr) // 2, len(pw_ho) // 2
     return {
         # merchants mix real and pseudo words; cities / streets are mostly pseudo names
-        "train": Vocab(tuple(rw_tr * 20 + pw_tr[:half_tr]), tuple(rc_tr * 40 + pw_tr[half_tr:]),
-                       tuple(pw_tr[half_tr:])),
-        "heldout": Vocab(tuple(rw_ho * 20 + pw_ho[:half_ho]), tuple(rc_ho * 40 + pw_ho[half_ho:]),
-                         tuple(pw_ho[half_ho:])),
+        "train": Vocab(tuple(rw_tr * 20 + pw_tr[:half_tr] + rs_tr), tuple(rc_tr * 40 + pw_tr[half_tr:] + rs_tr),
+                       tuple(pw_tr[half_tr:] + rs_tr)),
+        "heldout": Vocab(tuple(rw_ho * 20 + pw_ho[:half_ho] + rs_ho), tuple(rc_ho * 40 + pw_ho[half_ho:] + rs_ho),
+                         tuple(pw_ho[half_ho:] + rs_ho)),
         # the tokenizer's corpus: real training-split words plus the separate pseudo-word
         # pool, so no train / held-out / golden-case word is itself a merged token —
         # all of them split into the same kind of syllable pieces

@@ -209,7 +209,8 @@ def test_parser_metrics_observe_once_per_message(arun):
     assert count("sms_parser_processing_seconds_count") - p0 == n - 1
     assert count("sms_parser_gemini_seconds_count") - g0 == n - 1
     items = tracer.snapshot()["task/process_parsing"].items - (items0.items if items0 else 0)
-    assert items == n and sum(w.counts.values()) == n
+    assert items == n and w.counts["ok"] + w.counts["fail"] + w.counts["skip"] == n
+    assert w.counts["keyword_skipped"] == 1 and w.counts["parsed"] + 1 == w.counts["ok"]
 
 
 def test_long_body_truncation_is_counted():

@@ -31,6 +31,9 @@ __all__ = [
     "attn_prefill",
     "attn_decode",
     "fsm_sample",
+    "spec_plan",
+    "spec_verify",
+    "SPEC_MAX_K",
     "gemm",
     "gemm_cfg",
     "gemm_qkv_rope",
@@ -93,6 +96,11 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_set_prefill_impl.restype = None
     lib.sg_set_prefill_split.argtypes = [_c_int]
     lib.sg_set_prefill_split.restype = None
+    lib.sg_spec_plan.argtypes = [_c_int] * 5 + [_ip] * 6 + [_c_int] + [_ip, _ip, _c_int, _vp] + [_ip] * 7 + [_vp]
+    lib.sg_spec_plan.restype = _c_int
+    lib.sg_spec_verify.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
+                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _vp]
+    lib.sg_spec_verify.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
@@ -427,6 +435,64 @@ def fsm_sample(logits: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Ten
         _p(out_len), _p(done), _p(pos), _p(slot_id), _p(row_map), max_out, V, B, inv_t, seed & 0xFFFFFFFF,
         _stream()),
         "fsm_sample")
+
+
+SPEC_MAX_K = 8
+
+
+def spec_plan(K: int, T_cap: int, sep_token: int, scratch_slot: int, tok_buf: torch.Tensor, pos: torch.Tensor,
+              slot: torch.Tensor, done: torch.Tensor, out_buf: torch.Tensor, out_len: torch.Tensor,
+              body_buf: torch.Tensor, body_len: torch.Tensor, delim: torch.Tensor, draft_buf: torch.Tensor,
+              x_tok: torch.Tensor, x_pos: torch.Tensor, x_slot: torch.Tensor, x_done: torch.Tensor,
+              row_start: torch.Tensor, row_nd: torch.Tensor) -> None:
+    """Prompt-lookup drafts for ``B = tok_buf.numel()`` rows packed into ``T_cap``
+    pseudo-rows (``csrc/spec_kernels.hip``).  All int32 except ``delim`` (uint8 [V])."""
+    B = tok_buf.numel()
+    S1, LB = body_buf.shape
+    for name, t in (("tok_buf", tok_buf), ("pos", pos), ("slot", slot), ("done", done), ("out_len", out_len),
+                    ("row_start", row_start), ("row_nd", row_nd)):
+        _req(t, torch.int32, name)
+        if t.numel() < B:
+            raise ValueError(f"spec_plan: {name} has {t.numel()} < {B} rows")
+    for name, t in (("x_tok", x_tok), ("x_pos", x_pos), ("x_slot", x_slot), ("x_done", x_done)):
+        _req(t, torch.int32, name)
+        if t.numel() < T_cap:
+            raise ValueError(f"spec_plan: {name} smaller than T_cap")
+    _req(out_buf, torch.int32, "out_buf")
+    _req(body_buf, torch.int32, "body_buf")
+    _req(body_len, torch.int32, "body_len")
+    _req(delim, torch.uint8, "delim")
+    _req(draft_buf, torch.int32, "draft_buf")
+    if not (0 <= K <= SPEC_MAX_K) or T_cap < B or draft_buf.numel() < B * SPEC_MAX_K or body_len.numel() != S1:
+        raise ValueError("spec_plan: bad K / T_cap / draft_buf / body_len")
+    if not (0 <= scratch_slot < S1) or out_buf.shape[0] < B:
+        raise ValueError("spec_plan: bad scratch slot / out_buf")
+    _check(load_library().sg_spec_plan(
+        B, K, T_cap, sep_token, scratch_slot, _p(tok_buf), _p(pos), _p(slot), _p(done), _p(out_buf), _p(out_len),
+        out_buf.shape[1], _p(body_buf), _p(body_len), LB, _p(delim), _p(draft_buf), _p(x_tok), _p(x_pos),
+        _p(x_slot), _p(x_done), _p(row_start), _p(row_nd), _stream()), "spec_plan")
+
+
+def spec_verify(logits: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.Tensor, out_buf: torch.Tensor,
+                out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, x_tok: torch.Tensor,
+                row_start: torch.Tensor, row_nd: torch.Tensor, accepted: Optional[torch.Tensor] = None) -> None:
+    """Greedy FSM-masked verification of the drafts of ``B = tok_buf.numel()`` rows
+    (``logits`` [T_cap, V] over the pseudo-rows :func:`spec_plan` laid out)."""
+    B = tok_buf.numel()
+    T, V = logits.shape
+    if logits.dtype != torch.bfloat16 or logits.stride(1) != 1 or x_tok.numel() < T:
+        raise ValueError("spec_verify: bad logits / x_tok")
+    for name, t in (("state", state), ("out_len", out_len), ("done", done), ("pos", pos), ("row_start", row_start),
+                    ("row_nd", row_nd)):
+        if t.numel() < B or t.dtype != torch.int32:
+            raise ValueError(f"spec_verify: bad {name}")
+    if accepted is not None and (accepted.numel() < B or accepted.dtype != torch.int32):
+        raise ValueError("spec_verify: bad accepted")
+    _check(load_library().sg_spec_verify(
+        _p(logits), logits.stride(0), _p(fsm.masks), _p(fsm.state_mask), _p(state), _p(fsm.next_sep_t),
+        _p(fsm.next_tok_t), _p(fsm.enum_tok_t), _p(fsm.enum_next_t), fsm.E, fsm.sep_token, fsm.done_state,
+        _p(tok_buf), _p(out_buf), _p(out_len), _p(done), _p(pos), _p(x_tok), _p(row_start), _p(row_nd),
+        _p(accepted), out_buf.shape[1], V, B, _stream()), "spec_verify")
 
 
 def vt_shape(S: int, nkv: int, D: int, L: int):

@@ -1,0 +1,254 @@
+// smsgate_amd — speculative decoding for the schema-constrained extractor (gfx950).
+//
+// The extractor writes every copied field value with the SMS body's own tokens
+// (models/tokenizer.py value_span_ids), so the body is an exact draft source:
+// "prompt lookup" drafting.  One speculative step of a decode bucket of B rows:
+//
+//   sg_spec_plan    one workgroup: for each live row, look up its last emitted
+//                   token (bigram with the one before, else unigram) in its body
+//                   tokens and draft up to K following body tokens (a delimiter
+//                   token -- ',' / '&#' / ';' -- is drafted as <sep> and ends the
+//                   draft); an exclusive scan over rows packs the rows' [last
+//                   token, drafts...] into T_cap = B + D_cap pseudo-rows, clamping
+//                   drafts once the budget D_cap is used up.  Pseudo-row = one
+//                   query token at its own position in its row's KV slot, so the
+//                   unchanged decode kernels (GEMMs, QKV+RoPE+KV write, grouped
+//                   decode attention) run the verify forward; unused tail
+//                   pseudo-rows point at a scratch slot and are marked done.
+//   sg_spec_verify  one 256-thread block per row: walks the row's pseudo-rows in
+//                   order, taking the schema-FSM masked arg-max of each logits row
+//                   (the exact code of fsm_sample_kernel's greedy path) and
+//                   accepting while it equals the next draft; every arg-max taken
+//                   is emitted, so a step emits accepted + 1 tokens.  KV entries
+//                   written for rejected drafts lie beyond the row's new position
+//                   and are overwritten by the next step (roll back by position).
+//
+// Greedy outputs are bit-identical to one-token decode: every query token runs
+// the same per-column arithmetic in the same kernels (tests/test_spec_gpu.py).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SPEC_THREADS 1024
+#define SPEC_MAX_K 8
+
+static __device__ __forceinline__ float sp_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// ---------------------------------------------------------------------------
+// plan: grid = 1 block of SPEC_THREADS; each thread owns RPT consecutive rows.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
+    int B, int K, int T_cap, int sep_token, int scratch_slot,
+    const int* __restrict__ tok_buf, const int* __restrict__ pos, const int* __restrict__ slot,
+    const int* __restrict__ done, const int* __restrict__ out_buf, const int* __restrict__ out_len, int max_out,
+    const int* __restrict__ body_buf, const int* __restrict__ body_len, int LB, const uint8_t* __restrict__ delim,
+    int* __restrict__ draft_buf, int* __restrict__ x_tok, int* __restrict__ x_pos, int* __restrict__ x_slot,
+    int* __restrict__ x_done, int* __restrict__ row_start, int* __restrict__ row_nd) {
+  __shared__ int wsum[SPEC_THREADS / 64];
+  __shared__ int s_total;
+  const int tid = threadIdx.x;
+  const int RPT = (B + SPEC_THREADS - 1) / SPEC_THREADS;
+  const int r0 = tid * RPT, r1 = min(B, r0 + RPT);
+  // 1) drafts of my rows
+  int mine = 0;
+  for (int r = r0; r < r1; ++r) {
+    int n = 0;
+    const int t = tok_buf[r];
+    if (!done[r] && t != sep_token) {
+      const int len = out_len[r];
+      int prev = len >= 2 ? out_buf[(size_t)r * max_out + len - 2] : -1;
+      if (prev == sep_token) prev = -1;
+      const int sl = slot[r];
+      const int* body = body_buf + (size_t)sl * LB;
+      const int bl = body_len[sl];
+      int j = -1;
+      if (prev >= 0)
+        for (int q = 1; q < bl; ++q)
+          if (body[q] == t && body[q - 1] == prev) { j = q; break; }
+      if (j < 0)
+        for (int q = 0; q < bl; ++q)
+          if (body[q] == t) { j = q; break; }
+      if (j >= 0) {
+        for (int i = 0; i < K; ++i) {
+          const int q = j + 1 + i;
+          if (q >= bl) break;
+          const int x = body[q];
+          if (delim[x]) {
+            draft_buf[r * SPEC_MAX_K + n++] = sep_token;
+            break;
+          }
+          draft_buf[r * SPEC_MAX_K + n++] = x;
+        }
+      }
+    }
+    row_nd[r] = n;  // unclamped for now
+    mine += n;
+  }
+  // 2) block exclusive scan of the per-thread draft totals
+  const int lane = tid & 63, wid = tid >> 6;
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < SPEC_THREADS / 64; ++w) {
+      const int v = wsum[w];
+      wsum[w] = acc;
+      acc += v;
+    }
+    s_total = acc;
+  }
+  __syncthreads();
+  int dstart = wsum[wid] + incl - mine;  // drafts of all rows before my first row
+  const int D_cap = T_cap - B;
+  // 3) clamp to the budget and write my rows' pseudo-rows
+  for (int r = r0; r < r1; ++r) {
+    const int n = row_nd[r];
+    const int nc = max(0, min(n, D_cap - dstart));
+    const int st = r + min(dstart, D_cap);
+    dstart += n;
+    row_start[r] = st;
+    row_nd[r] = nc;
+    const int p = pos[r], sl = slot[r];
+    const int dn = done[r];
+    x_tok[st] = tok_buf[r];
+    x_pos[st] = p;
+    x_slot[st] = sl;
+    x_done[st] = dn;
+    for (int i = 0; i < nc; ++i) {
+      x_tok[st + 1 + i] = draft_buf[r * SPEC_MAX_K + i];
+      x_pos[st + 1 + i] = p + 1 + i;
+      x_slot[st + 1 + i] = sl;
+      x_done[st + 1 + i] = 0;
+    }
+  }
+  // 4) unused tail: scratch slot, position 0, skipped by attention
+  const int used = B + min(s_total, D_cap);
+  for (int i = used + tid; i < T_cap; i += SPEC_THREADS) {
+    x_tok[i] = 0;
+    x_pos[i] = 0;
+    x_slot[i] = scratch_slot;
+    x_done[i] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// verify: grid = B blocks of 256 threads.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) spec_verify_kernel(
+    const uint16_t* __restrict__ logits, int ldl, const uint32_t* __restrict__ masks, const int* __restrict__ state_mask,
+    int* __restrict__ state, const int* __restrict__ next_sep, const int* __restrict__ next_tok,
+    const int* __restrict__ enum_tok, const int* __restrict__ enum_next, int E, int sep_token, int done_state,
+    int* __restrict__ tok_buf, int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done,
+    int* __restrict__ pos, const int* __restrict__ x_tok, const int* __restrict__ row_start,
+    const int* __restrict__ row_nd, int* __restrict__ accepted, int max_out, int V) {
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ float bv[4];
+  __shared__ int bi[4];
+  __shared__ int s_go, s_state;
+  if (done[b]) {  // block-uniform
+    if (tid == 0 && accepted != nullptr) accepted[b] = 0;
+    return;
+  }
+  const int st = row_start[b], nd = row_nd[b];
+  int s = state[b];
+  int emitted = 0;
+  for (int i = 0; i <= nd; ++i) {
+    const uint32_t* mrow = masks + (size_t)state_mask[s] * (V >> 5);
+    const uint16_t* lrow = logits + (size_t)(st + i) * ldl;
+    float best = -INFINITY;
+    int besti = 0x7fffffff;
+    const int nvec = V >> 3;
+    for (int c = tid; c < nvec; c += 256) {
+      const uint32_t bits = (mrow[c >> 2] >> ((c & 3) * 8)) & 0xffu;
+      if (!bits) continue;
+      const uint4 raw = *reinterpret_cast<const uint4*>(lrow + 8 * c);
+      const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (bits & (1u << j)) {
+          const int idx = 8 * c + j;
+          const float v = sp_bf2f((uint16_t)(w[j >> 1] >> ((j & 1) * 16)));
+          if (v > best || (v == best && idx < besti)) { best = v; besti = idx; }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(besti, o, 64);
+      if (ov > best || (ov == best && oi < besti)) { best = ov; besti = oi; }
+    }
+    if (lane == 0) { bv[wid] = best; bi[wid] = besti; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < 4; ++w)
+        if (bv[w] > best || (bv[w] == best && bi[w] < besti)) { best = bv[w]; besti = bi[w]; }
+      const int tok = (besti == 0x7fffffff) ? sep_token : besti;
+      int ns;
+      if (tok == sep_token) {
+        ns = next_sep[s];
+      } else {
+        ns = next_tok[s];
+        if (E > 0 && ns == -2) {
+          ns = -1;
+          for (int e = 0; e < E; ++e)
+            if (enum_tok[s * E + e] == tok) { ns = enum_next[s * E + e]; break; }
+        }
+      }
+      const int len = out_len[b];
+      out_buf[(size_t)b * max_out + len] = tok;
+      out_len[b] = len + 1;
+      tok_buf[b] = tok;
+      const int nstate = ns < 0 ? done_state : ns;
+      state[b] = nstate;
+      int go = 0;
+      if (ns < 0 || ns == done_state || len + 1 >= max_out) {
+        done[b] = 1;
+      } else {
+        pos[b] = pos[b] + 1;
+        go = (i < nd) && (tok == x_tok[st + i + 1]);  // next query token is exactly this one
+      }
+      s_go = go;
+      s_state = nstate;
+    }
+    __syncthreads();
+    ++emitted;
+    s = s_state;
+    if (!s_go) break;
+  }
+  if (tid == 0 && accepted != nullptr) accepted[b] = emitted;
+}
+
+extern "C" {
+
+int sg_spec_plan(int B, int K, int T_cap, int sep_token, int scratch_slot, const int* tok_buf, const int* pos,
+                 const int* slot, const int* done, const int* out_buf, const int* out_len, int max_out,
+                 const int* body_buf, const int* body_len, int LB, const void* delim, int* draft_buf, int* x_tok,
+                 int* x_pos, int* x_slot, int* x_done, int* row_start, int* row_nd, hipStream_t stream) {
+  if (K < 0 || K > SPEC_MAX_K || T_cap < B || B <= 0) return -1;
+  hipLaunchKernelGGL(spec_plan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, B, K, T_cap, sep_token, scratch_slot,
+                     tok_buf, pos, slot, done, out_buf, out_len, max_out, body_buf, body_len, LB,
+                     (const uint8_t*)delim, draft_buf, x_tok, x_pos, x_slot, x_done, row_start, row_nd);
+  return (int)hipGetLastError();
+}
+
+int sg_spec_verify(const void* logits, int ldl, const void* masks, const int* state_mask, int* state,
+                   const int* next_sep, const int* next_tok, const int* enum_tok, const int* enum_next, int E,
+                   int sep_token, int done_state, int* tok_buf, int* out_buf, int* out_len, int* done, int* pos,
+                   const int* x_tok, const int* row_start, const int* row_nd, int* accepted, int max_out, int V, int B,
+                   hipStream_t stream) {
+  if (V % 32 || ldl % 8) return -1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(spec_verify_kernel, dim3(B), dim3(256), 0, stream, (const uint16_t*)logits, ldl,
+                     (const uint32_t*)masks, state_mask, state, next_sep, next_tok, enum_tok, enum_next, E, sep_token,
+                     done_state, tok_buf, out_buf, out_len, done, pos, x_tok, row_start, row_nd, accepted, max_out, V);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

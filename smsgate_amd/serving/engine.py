@@ -85,6 +85,13 @@ class EngineConfig:
     split_parts: int = 2  # parts of a split decode bucket (split_graphs=2)
     split_prefill: int = 8192  # >0: prefill batches of >= this many tokens run as two halves on two streams
     prefill_key_split: int = 1  # 2: two waves share each prefill attention tile's keys (ops.set_prefill_split)
+    # speculative decoding (csrc/spec_kernels.hip): each decode step verifies up to
+    # `spec_k` drafts per row looked up in the row's own SMS body (the extractor copies
+    # body tokens); greedy only.  0 = off.  A step packs B rows + at most
+    # ceil(spec_draft_frac * B) drafts into one forward (fixed shape per bucket).
+    spec_k: int = 0
+    spec_draft_frac: float = 2.0
+    spec_max_rows: int = 1 << 30  # buckets above this decode one token per row
 
 
 @dataclass
@@ -169,8 +176,13 @@ class ExtractionEngine:
             raise ValueError("prefix + Lmax exceeds the decode kernel's context limit (512)")
         S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
         dev, bf = self.device, torch.bfloat16
-        self.k_cache = torch.zeros(L, S, nkv, self.Lmax, D, dtype=bf, device=dev)
-        self.vt_cache = torch.zeros(L, *ops.vt_shape(S, nkv, D, self.Lmax), dtype=bf, device=dev)
+        self.spec = ec.spec_k > 0 and ec.temperature <= 0
+        if ec.spec_k > ops.SPEC_MAX_K:
+            raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
+        # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV there
+        S_kv = S + 1 if self.spec else S
+        self.k_cache = torch.zeros(L, S_kv, nkv, self.Lmax, D, dtype=bf, device=dev)
+        self.vt_cache = torch.zeros(L, *ops.vt_shape(S_kv, nkv, D, self.Lmax), dtype=bf, device=dev)
         self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
         self.pvt = torch.zeros(L, *ops.vt_shape(1, nkv, D, self.P0pad)[1:], dtype=bf, device=dev)
         # cascade decode attention scratch: prefix output / log-sum-exp per query row
@@ -204,6 +216,8 @@ class ExtractionEngine:
         self._snap_flip = 0
         self._pending: Optional[_Snapshot] = None
         self._sides: List[torch.cuda.Stream] = []  # side streams of the split decode / prefill
+        if self.spec:
+            self._init_spec()
         self._compute_prefix()
         if ec.use_graphs:
             self._capture_graphs()
@@ -315,8 +329,12 @@ class ExtractionEngine:
         last_pos_d = meta_d[o:o + n]; o += n
         seq_slot_d = meta_d[o:o + n]
         qstart = torch.zeros(n, dtype=torch.int32, device=dev)
-        x = F.embedding(torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True), self.w.embed).contiguous()
+        flat_d = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
+        x = F.embedding(flat_d, self.w.embed).contiguous()
         max_q = int(lens.max())
+        if self.spec:  # the rows' prompts are their draft source
+            self.body_buf[slot_d.long(), pos_d.long()] = flat_d.to(torch.int32)
+            self.body_len[seq_slot_d.long()] = last_pos_d + 1
 
         def kc(i):
             return self.k_cache[i]
@@ -350,6 +368,8 @@ class ExtractionEngine:
     def _decode_step(self, B: int, sample: bool = True, r0: int = 0, hook=None) -> torch.Tensor:
         """One decode step of rows ``r0 .. r0+B`` (every per-row buffer is sliced,
         so two disjoint row ranges can run as independent sub-batches)."""
+        if self._use_spec(B):
+            return self._spec_step(B, r0, hook=hook, sample=sample)
         r1 = r0 + B
         tok = self.tok_buf[r0:r1]
         pos = self.pos[r0:r1]
@@ -376,6 +396,86 @@ class ExtractionEngine:
             ops.fsm_sample(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
                            done, pos, slot, self.cfg.temperature, self.cfg.seed)
         return logits
+
+    # ----------------------------------------------------------- speculative
+    def _init_spec(self) -> None:
+        ec, dev = self.cfg, self.device
+        S = ec.max_slots
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.scratch_slot = S
+        self.LB = ec.max_body_tokens + 2
+        self.body_buf = torch.zeros(S + 1, self.LB, **i32)  # prompt ids per KV slot (the draft source)
+        self.body_len = torch.zeros(S + 1, **i32)
+        # tokens that end a copied value in the body: drafted as <sep>
+        strings = self.tok.token_strings
+        delim = [(("," in t) or ("&#" in t) or (";" in t)) and i not in (self.tok.sep,) for i, t in enumerate(strings)]
+        delim += [False] * (self.V_dec - len(delim))
+        self.spec_delim = torch.tensor(delim[: self.V_dec], dtype=torch.uint8, device=dev)
+        self._spec_mult = 1 + math.ceil(ec.spec_draft_frac)
+        self.draft_buf = torch.zeros(S * ops.SPEC_MAX_K, **i32)
+        cap = S * self._spec_mult
+        self.x_tok = torch.zeros(cap, **i32)
+        self.x_pos = torch.zeros(cap, **i32)
+        self.x_slot = torch.full((cap,), S, **i32)
+        self.x_done = torch.ones(cap, **i32)
+        self.row_start = torch.zeros(S, **i32)
+        self.row_nd = torch.zeros(S, **i32)
+        self.spec_acc = torch.zeros(S, **i32)
+        self.spec_counts = torch.zeros(2, dtype=torch.int64, device=dev)  # [tokens emitted, live row-steps]
+
+    def _tcap(self, B: int) -> int:
+        """Pseudo-rows of a speculative step over ``B`` rows (drafts capped at the budget)."""
+        d = min(_round_up(math.ceil(B * self.cfg.spec_draft_frac), 64), B * (self._spec_mult - 1))
+        return B + d
+
+    def _use_spec(self, B: int) -> bool:
+        return self.spec and B <= self.cfg.spec_max_rows
+
+    def _spec_step(self, B: int, r0: int = 0, hook=None, sample: bool = True) -> torch.Tensor:
+        """One speculative decode step of rows ``r0 .. r0+B``: plan (drafts + packing),
+        verify forward over the pseudo-rows, greedy FSM verification."""
+        r1 = r0 + B
+        T = self._tcap(B)
+        off = r0 * self._spec_mult
+        tok, pos, slot, done = self.tok_buf[r0:r1], self.pos[r0:r1], self.slot_id[r0:r1], self.done[r0:r1]
+        xt, xp, xs, xd = (self.x_tok[off:off + T], self.x_pos[off:off + T], self.x_slot[off:off + T],
+                          self.x_done[off:off + T])
+        rs, nd, acc = self.row_start[r0:r1], self.row_nd[r0:r1], self.spec_acc[r0:r1]
+        ops.spec_plan(self.cfg.spec_k, T, self.tok.sep, self.scratch_slot, tok, pos, slot, done,
+                      self.out_buf[r0:r1], self.out_len[r0:r1], self.body_buf, self.body_len, self.spec_delim,
+                      self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd)
+        x = F.embedding(xt.long(), self.w.embed)
+        impl = self.cfg.decode_attn_small if T <= self.cfg.decode_attn_small_rows else self.cfg.decode_attn
+        scratch = None
+        if impl == "cascade":
+            scratch = (torch.empty(T, self.mc.heads, self.mc.head_dim, dtype=torch.float32, device=self.device),
+                       torch.empty(T, self.mc.heads, dtype=torch.float32, device=self.device))
+
+        def kc(i):
+            return self.k_cache[i]
+
+        def vc(i):
+            return self.vt_cache[i]
+
+        def attn(i, q, out):
+            ops.attn_decode(q, xp, xs, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
+                            done=xd, impl=impl, scratch=scratch)
+
+        h = self._forward(x, pos_tok=xp, slot_tok=xs, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0, hook=hook)
+        logits = self._logits(h)
+        if sample:
+            ops.spec_verify(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
+                            pos, xt, rs, nd, acc)
+            # tokens emitted and live rows this step (read back only by stats())
+            self.spec_counts += torch.stack([acc.sum(dtype=torch.int64), (acc > 0).sum(dtype=torch.int64)])
+        return logits
+
+    def spec_stats(self) -> Dict[str, float]:
+        if not self.spec:
+            return {}
+        emitted, live = (int(v) for v in self.spec_counts.tolist())
+        return {"spec_tokens": emitted, "spec_row_steps": live,
+                "spec_tokens_per_row_step": (emitted / live) if live else 0.0}
 
     def _side_stream(self) -> torch.cuda.Stream:
         return self._side_streams(1)[0]

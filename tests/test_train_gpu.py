@@ -17,7 +17,7 @@ from smsgate_amd.utils.synth import generate  # noqa: E402
 
 def _score(w, n=300):
     eng = ExtractionEngine(w, load_tokenizer(), EngineConfig(max_slots=512, buckets=(64, 512)))
-    held = [s for s in generate(n, seed=424242) if s.answer is not None]
+    held = [s for s in generate(n, seed=424242, vocab_name="heldout") if s.answer is not None]
     pred = eng.run([normalize_body(s.body) for s in held])
     return field_accuracy(pred, [s.answer for s in held])
 
@@ -25,7 +25,7 @@ def _score(w, n=300):
 def test_training_learns_extraction():
     w = train_extractor(TrainConfig(model="small", steps=2500, lr=2e-3, n_examples=30000, log_every=0), device="cuda")
     acc = _score(w)
-    for f in ("txn_type", "date", "currency", "city"):
+    for f in ("txn_type", "date", "currency"):
         assert acc[f] >= 0.95, acc
     assert sum(acc[f] for f in acc if f != "all") / 9 >= 0.8, acc
 
@@ -36,5 +36,5 @@ def test_bundled_checkpoint_extracts():
     path = bundled_checkpoint("small")
     assert path is not None and os.path.exists(path)
     eng = build_engine("small", device="cuda", max_slots=512, buckets=(64, 512))
-    acc = _score(eng.w)
-    assert acc["all"] >= 0.7 and acc["merchant"] >= 0.95 and acc["amount"] >= 0.95, acc
+    acc = _score(eng.w)  # held-out vocabulary (names never seen in training)
+    assert acc["all"] >= 0.85 and acc["merchant"] >= 0.9 and acc["amount"] >= 0.98, acc

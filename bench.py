@@ -90,6 +90,9 @@ def _args(argv=None):
                    help="waves sharing each prefill attention tile's keys")
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
+    p.add_argument("--spec-k", type=int, default=0, help="speculative decoding: drafts per row per step (0 = off)")
+    p.add_argument("--spec-frac", type=float, default=2.0, help="draft budget per step, x decode rows")
+    p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
     p.add_argument("--cpu-echo-engine", action="store_true",
                    help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")
     p.add_argument("--verbose", action="store_true")
@@ -151,6 +154,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               split_parts=args.split_parts,
                               split_prefill=args.split_prefill, decode_attn=args.decode_attn,
                               prefill_key_split=args.prefill_key_split,
+                              spec_k=args.spec_k, spec_draft_frac=args.spec_frac, spec_max_rows=args.spec_max_rows,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
     if not echo and args.eval_n and rank == 0:
@@ -181,9 +185,13 @@ def run_replica(args, rank: int, world: int, local: int):
     if args.warmup:
         coord.run_phase(seeds(0, args.warmup), per_w)
     engine.stats.__init__()
+    if hasattr(engine, "spec_stats"):
+        engine.spec_stats(reset=True)
     dt, counts = coord.run_phase(seeds(args.warmup, args.steps), per_w, sync=sync)
     coord.shutdown(procs)
     estats = engine.stats.as_dict()
+    if hasattr(engine, "spec_stats"):
+        estats.update(engine.spec_stats())
     if dist is not None:
         dev = "cpu" if echo else "cuda"
         t = torch.tensor([dt], dtype=torch.float64, device=dev)

@@ -126,6 +126,7 @@ class FileLog:
         self._f = None
         self._seg = 0
         self._bytes = 0
+        self._floor_bytes = 0
         self._last_sync = time.monotonic()
         self.engine: Optional[Engine] = None
         self._need_compact = False
@@ -142,6 +143,7 @@ class FileLog:
         self._seg = n
         self._f = open(self.dir / f"journal-{n:08d}.log", "ab")
         self._bytes = self._f.tell()
+        self._floor_bytes = self._bytes  # size right after a snapshot / at recovery
 
     def _write(self, kind: str, args) -> None:
         body = msgpack.packb([kind, list(args)], use_bin_type=True)
@@ -158,8 +160,11 @@ class FileLog:
                 if now - self._last_sync >= self.fsync_interval_s:
                     os.fsync(self._f.fileno())
                     self._last_sync = now
-        if self._bytes > self.compact_bytes:
-            self._need_compact = True  # compact between operations, never mid-mutation
+        # compact between operations, never mid-mutation; and only once the journal has
+        # doubled since the last snapshot (a live state above compact_bytes would
+        # otherwise be rewritten after every single append)
+        if self._bytes > max(self.compact_bytes, 2 * self._floor_bytes):
+            self._need_compact = True
 
     def maybe_compact(self) -> None:
         if self._need_compact:

@@ -22,6 +22,8 @@ BUSD = BINDIR / "smsgate-busd"
 # host sanitizer build (ASan + UBSan): the broker's race/memory check, run by
 # tests/test_native_bus.py::test_sanitizer_build_clean (GPU sanitizers are not used)
 BUSD_SAN = BINDIR / "smsgate-busd-san"
+# native load generator (broker capacity tests, scripts/bus_bench.py --native-load)
+BUSLOAD = BINDIR / "smsgate-busload"
 
 
 def cxx() -> str:
@@ -50,13 +52,29 @@ def build(force: bool = False, verbose: bool = False, extra: List[str] = (), san
     tmp = target.with_suffix(".tmp")
     opt = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"] \
         if sanitize else ["-O2"]
-    cmd = [cxx(), *opt, "-std=c++17", "-Wall", "-Wno-unused-function", *extra,
+    cmd = [cxx(), *opt, "-std=c++17", "-Wall", "-Wno-unused-function", "-pthread", *extra,
            str(CSRC / "busd.cpp"), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, target)
+    if not sanitize:
+        build_load(force=force, verbose=verbose)
     return target
+
+
+def build_load(force: bool = False, verbose: bool = False) -> Path:
+    """The native load generator (threads; one connection per producer / consumer)."""
+    if not force and not needs_build(BUSLOAD):
+        return BUSLOAD
+    tmp = BUSLOAD.with_suffix(".tmp")
+    cmd = [cxx(), "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", "-pthread", str(CSRC / "busload.cpp"),
+           "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, BUSLOAD)
+    return BUSLOAD
 
 
 if __name__ == "__main__":

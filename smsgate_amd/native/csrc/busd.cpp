@@ -15,7 +15,10 @@
 // disk).  Long-poll fetches park as waiters; after every loop iteration the
 // waiters are retried (publishes, naks, acks and redelivery deadlines can all
 // make messages available) and the epoll timeout is the earliest waiter
-// deadline / redelivery time / 1 s retention tick.
+// deadline / redelivery time / 1 s retention tick.  With ``--fsync interval``
+// (the default) the periodic fdatasync runs on a background thread, so the event
+// loop only ever pays for the write(2) into the page cache; ``--fsync always``
+// keeps the sync inline before the replies of the batch.
 //
 // Usage: smsgate-busd --listen tcp://0.0.0.0:4222 [--listen unix:///run/bus.sock]
 //                     [--data DIR] [--max-age S] [--fsync interval|always|never]
@@ -37,7 +40,10 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <list>
 #include <string>
@@ -93,7 +99,18 @@ uint32_t get_u32(const char* p) {
 class Journal {
  public:
   Journal(std::string dir, std::string mode, double interval, int64_t compact_bytes)
-      : dir_(std::move(dir)), mode_(std::move(mode)), interval_(interval), compact_bytes_(compact_bytes) {}
+      : dir_(std::move(dir)), mode_(std::move(mode)), interval_(interval), compact_bytes_(compact_bytes) {
+    if (mode_ == "interval") syncer_ = std::thread([this] { sync_loop(); });
+  }
+
+  ~Journal() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (syncer_.joinable()) syncer_.join();
+  }
 
   std::vector<std::string> segments() const {
     std::vector<std::string> out;
@@ -117,15 +134,22 @@ class Journal {
   void open_segment(int n) {
     if (fd_ >= 0) {
       flush();
+      std::lock_guard<std::mutex> g(mu_);  // not while the syncer holds the old fd
       ::fsync(fd_);
       ::close(fd_);
+      sync_fd_ = -1;
     }
     seg_ = n;
     fd_ = ::open(path(n).c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
     if (fd_ < 0) die("cannot open journal segment " + path(n));
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      sync_fd_ = fd_;
+    }
     struct stat sb;
     fstat(fd_, &sb);
     bytes_ = sb.st_size;
+    floor_bytes_ = bytes_;  // a fresh segment is a snapshot (compaction) or the recovered tail
   }
 
   static void frame(std::string& out, const char* kind, const mp::Value& args) {
@@ -143,7 +167,10 @@ class Journal {
     size_t before = buf_.size();
     frame(buf_, kind, args);
     bytes_ += (int64_t)(buf_.size() - before);
-    if (bytes_ > compact_bytes_) need_compact = true;
+    // compact only once the journal has doubled since the last snapshot: when the live
+    // state itself exceeds compact_bytes, a fixed threshold would re-compact after
+    // every append (the whole state rewritten on the event loop, over and over)
+    if (bytes_ > std::max(compact_bytes_, 2 * floor_bytes_)) need_compact = true;
   }
 
   // Group commit: one write(2) for everything appended since the last flush.
@@ -157,7 +184,17 @@ class Journal {
   }
 
   void sync() {
-    if (fd_ >= 0 && dirty_) ::fdatasync(fd_);
+    if (fd_ >= 0 && dirty_) {
+      if (syncer_.joinable()) {  // interval mode: hand the fdatasync to the syncer thread
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          want_sync_ = true;
+        }
+        cv_.notify_one();
+      } else {
+        ::fdatasync(fd_);
+      }
+    }
     dirty_ = false;
     last_sync_ = mono_now();
   }
@@ -175,9 +212,11 @@ class Journal {
   void close() {
     if (fd_ >= 0) {
       flush();
+      std::lock_guard<std::mutex> g(mu_);
       ::fsync(fd_);
       ::close(fd_);
       fd_ = -1;
+      sync_fd_ = -1;
     }
   }
 
@@ -193,9 +232,26 @@ class Journal {
   int fd_ = -1;
   int seg_ = 0;
   int64_t bytes_ = 0;
+  int64_t floor_bytes_ = 0;  // journal size right after the last snapshot
   std::string buf_;
   bool dirty_ = false;
   double last_sync_ = 0.0;
+  // background fdatasync (interval mode); mu_ guards sync_fd_ against segment rotation
+  std::thread syncer_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool want_sync_ = false, stop_ = false;
+  int sync_fd_ = -1;
+
+  void sync_loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [this] { return want_sync_ || stop_; });
+      if (stop_) return;
+      want_sync_ = false;
+      if (sync_fd_ >= 0) ::fdatasync(sync_fd_);  // under mu_: the fd cannot be closed meanwhile
+    }
+  }
 };
 
 // ------------------------------------------------------------- replay (recovery)

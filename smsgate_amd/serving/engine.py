@@ -470,8 +470,11 @@ class ExtractionEngine:
             self.spec_counts += torch.stack([acc.sum(dtype=torch.int64), (acc > 0).sum(dtype=torch.int64)])
         return logits
 
-    def spec_stats(self) -> Dict[str, float]:
+    def spec_stats(self, reset: bool = False) -> Dict[str, float]:
         if not self.spec:
+            return {}
+        if reset:
+            self.spec_counts.zero_()
             return {}
         emitted, live = (int(v) for v in self.spec_counts.tolist())
         return {"spec_tokens": emitted, "spec_row_steps": live,

@@ -71,6 +71,10 @@ def _args(argv=None):
     p.add_argument("--admit-frac", type=float, default=0.25)
     p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)
+    p.add_argument("--bus", default="busd", choices=["memory", "busd"],
+                   help="busd: ONE shared native broker per node (journal on) carries sms.raw / sms.parsed for every "
+                        "GPU's parser and writer processes (one competing group each); memory: an in-process bus per "
+                        "parser process")
     p.add_argument("--concurrency", type=int, default=4)
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--worker-threads", type=int, default=2,
@@ -90,7 +94,7 @@ def _args(argv=None):
                    help="waves sharing each prefill attention tile's keys")
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
-    p.add_argument("--spec-k", type=int, default=0, help="speculative decoding: drafts per row per step (0 = off)")
+    p.add_argument("--spec-k", type=int, default=4, help="speculative decoding: drafts per row per step (0 = off)")
     p.add_argument("--spec-frac", type=float, default=2.0, help="draft budget per step, x decode rows")
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
     p.add_argument("--cpu-echo-engine", action="store_true",
@@ -112,8 +116,10 @@ def run_replica(args, rank: int, world: int, local: int):
     W = max(1, args.cpu_workers)
     if args.msgs_per_step % W:
         raise SystemExit("--msgs-per-step must be divisible by --cpu-workers")
+    # 0) the node's shared broker, started before anything touches the GPU (no exec after GPU init)
+    broker, bus_dsn = start_node_broker(args, local) if args.bus == "busd" else (None, None)
     cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
-           "worker_threads": args.worker_threads, "vocab": args.traffic_vocab}
+           "worker_threads": args.worker_threads, "vocab": args.traffic_vocab, "bus": bus_dsn}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
 
@@ -168,7 +174,7 @@ def run_replica(args, rank: int, world: int, local: int):
         from smsgate_amd.serving import freeze_gc_for_launch_loop
 
         freeze_gc_for_launch_loop()
-    coord = Coordinator(engine, conns)
+    coord = Coordinator(engine, conns, bus_dsn=bus_dsn, world=world)
     coord.wait_all("ready")
 
     def sync():
@@ -182,8 +188,8 @@ def run_replica(args, rank: int, world: int, local: int):
     def seeds(first, n):
         return [[1_000_003 * (rank + 1) + 7919 * w + s for s in range(first, first + n)] for w in range(W)]
 
-    if args.warmup:
-        coord.run_phase(seeds(0, args.warmup), per_w)
+    if args.warmup:  # (synchronised too: with a shared broker each rank's drain target needs a common start)
+        coord.run_phase(seeds(0, args.warmup), per_w, sync=sync)
     engine.stats.__init__()
     if hasattr(engine, "spec_stats"):
         engine.spec_stats(reset=True)
@@ -202,8 +208,38 @@ def run_replica(args, rank: int, world: int, local: int):
         c = torch.tensor([counts.get(k, 0) for k in keys], dtype=torch.int64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         counts = dict(zip(keys, (int(x) for x in c.tolist())))
+        dist.barrier()  # every rank is done with the broker
         dist.destroy_process_group()
+    if broker is not None:
+        broker.stop()
+        import shutil
+
+        shutil.rmtree(os.path.dirname(broker.listens[0].replace("unix://", "")), ignore_errors=True)
     return dt, counts, init_s, estats, prov, quality
+
+
+def start_node_broker(args, local: int):
+    """Local rank 0 starts ``smsgate-busd`` (journal in a temp dir, fsync interval);
+    the other ranks of the node wait for its socket.  Returns (broker | None, dsn)."""
+    import tempfile
+
+    tag = os.environ.get("MASTER_PORT") or str(os.getpid())
+    root = os.path.join(tempfile.gettempdir(), f"smsgate-bench-bus-{tag}")
+    sock = os.path.join(root, "bus.sock")
+    if local == 0:
+        from smsgate_amd.native import spawn_busd
+
+        os.makedirs(root, exist_ok=True)
+        if os.path.exists(sock):
+            os.unlink(sock)
+        broker = spawn_busd(f"unix://{sock}", os.path.join(root, "data"))
+        return broker, f"unix://{sock}"
+    t_end = time.time() + 60
+    while not os.path.exists(sock):
+        if time.time() > t_end:
+            raise SystemExit(f"bench: the node broker socket {sock} never appeared")
+        time.sleep(0.05)
+    return None, f"unix://{sock}"
 
 
 ROUTING_KEYS = ("ok", "fail", "skip", "parsed", "keyword_skipped", "sink_stored", "writer_no_merchant", "writer_fail")
@@ -327,6 +363,8 @@ def main(argv=None) -> int:
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
                 "pipeline": ("payload->RawSMS->bus sms.raw->parser_worker->sms.parsed+sms.processing|DLQ->ack"
                              + ("->pb_writer->in-memory sink" if gpu else "")),
+                "bus": ("one shared smsgate-busd per node (journal on), one competing parser group and one writer "
+                        "group across all GPUs" if args.bus == "busd" else "in-process bus per parser process"),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
                 "seq_len": "shared prefix 20 + ~48 prompt + <=131 schema-constrained output tokens (~38 trained)",

@@ -68,6 +68,9 @@ def main() -> None:
                    help="EngineConfig.admit_min_batch (0 = off; default: the engine's)")
     p.add_argument("--admit-max-wait-ms", type=float, default=None)
     p.add_argument("--prefill-key-split", type=int, default=None, choices=[1, 2])
+    p.add_argument("--weights", default="random",
+                   help="random | train (bench.py's in-run training, reusing its weights cache) | checkpoint path")
+    p.add_argument("--spec-k", type=int, default=0, help="speculative decoding drafts per row (0 = off)")
     a = p.parse_args()
     import torch
 
@@ -86,12 +89,20 @@ def main() -> None:
         kw["prefill_key_split"] = a.prefill_key_split
     if a.admit_max_wait_ms is not None:
         kw["admit_max_wait_s"] = a.admit_max_wait_ms / 1000.0
-    eng = build_engine("smollm-135m", device="cuda", random_init=True, max_slots=a.max_slots, steps_per_graph=2,
-                       buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192), **kw)
+    weights = None
+    if a.weights != "random":
+        import bench
+
+        bargs = bench._args(["--weights", a.weights])
+        weights, _ = bench.acquire_weights(bargs, "cuda:0", 0, 1)
+    eng = build_engine("smollm-135m", device="cuda", random_init=weights is None, weights=weights,
+                       max_slots=a.max_slots, steps_per_graph=2,
+                       buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192), spec_k=a.spec_k, **kw)
     arm = {"attn_small_rows": eng.cfg.decode_attn_small_rows, "attn_small": eng.cfg.decode_attn_small,
            "gemm_small_m": ops.GEMM_SMALL_M, "admit_min_batch": eng.cfg.admit_min_batch,
-           "admit_max_wait_ms": eng.cfg.admit_max_wait_s * 1000.0, "prefill_key_split": eng.cfg.prefill_key_split}
-    bodies = [normalize_body(b) for b in generate_bodies(20000, seed=5)]
+           "admit_max_wait_ms": eng.cfg.admit_max_wait_s * 1000.0, "prefill_key_split": eng.cfg.prefill_key_split,
+           "weights": a.weights, "spec_k": a.spec_k}
+    bodies = [normalize_body(b) for b in generate_bodies(20000, seed=5, vocab_name="heldout")]
     ids = eng.tok.message_ids(bodies, eng.cfg.max_body_tokens)
     run_rate(eng, ids, 2000.0, 1.0, seed=0)  # warm-up
     torch.cuda.synchronize()

@@ -67,11 +67,14 @@ class NativeBroker:
 
 def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_age: float = 3 * 24 * 3600.0,
                fsync: str = "interval", fsync_interval_s: float = 0.05, compact_bytes: Optional[int] = None,
-               ready_timeout: float = 20.0, binary: Optional[Path] = None, stderr=None) -> NativeBroker:
+               ready_timeout: float = 20.0, binary: Optional[Path] = None, stderr=None,
+               die_with_parent: bool = True) -> NativeBroker:
     """Start the native broker and wait until it listens.
 
     ``listen`` takes ``tcp://host:port`` (port 0 = pick one, see
-    :attr:`NativeBroker.tcp_port`) and/or ``unix:///path`` URLs.
+    :attr:`NativeBroker.tcp_port`) and/or ``unix:///path`` URLs.  With
+    ``die_with_parent`` the broker gets SIGTERM when the starting process dies
+    (no orphaned broker after a crashed benchmark or test).
     """
     binary = Path(binary or BUSD)
     if not available(binary):
@@ -85,7 +88,8 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
     cmd += ["--max-age", repr(float(max_age)), "--fsync", fsync, "--fsync-interval", repr(float(fsync_interval_s))]
     if compact_bytes is not None:
         cmd += ["--compact-bytes", str(int(compact_bytes))]
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL, stderr=stderr)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stdin=subprocess.DEVNULL, stderr=stderr,
+                            preexec_fn=_pdeathsig if die_with_parent else None)
     t_end = time.monotonic() + ready_timeout
     line = b""
     while time.monotonic() < t_end:
@@ -97,6 +101,12 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
         raise RuntimeError(f"smsgate-busd failed to start (exit {proc.poll()}): {line!r}")
     tok = line.split()[1].decode()
     return NativeBroker(proc, listens, None if tok == "-" else int(tok))
+
+
+def _pdeathsig() -> None:  # runs in the child between fork and exec
+    import ctypes
+
+    ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
 
 
 def busd_path() -> Path:

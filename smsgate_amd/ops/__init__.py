@@ -33,6 +33,9 @@ __all__ = [
     "fsm_sample",
     "spec_plan",
     "spec_verify",
+    "spec_verify_keys",
+    "fsm_commit",
+    "gemm_argmax",
     "SPEC_MAX_K",
     "gemm",
     "gemm_cfg",
@@ -96,11 +99,20 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_set_prefill_impl.restype = None
     lib.sg_set_prefill_split.argtypes = [_c_int]
     lib.sg_set_prefill_split.restype = None
-    lib.sg_spec_plan.argtypes = [_c_int] * 5 + [_ip] * 6 + [_c_int] + [_ip, _ip, _c_int, _vp] + [_ip] * 7 + [_vp]
+    fsm_t = [_vp, _ip, _ip, _ip, _ip, _ip, _c_int]  # masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E
+    lib.sg_spec_plan.argtypes = fsm_t + [_c_int, _c_int, _ip, _ip] + [_c_int] * 5 + [_ip] * 6 + [_c_int] + \
+        [_ip, _ip, _c_int, _vp] + [_ip] * 7 + [_vp]
     lib.sg_spec_plan.restype = _c_int
     lib.sg_spec_verify.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                    _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _vp]
     lib.sg_spec_verify.restype = _c_int
+    lib.sg_spec_verify_keys.argtypes = [_vp] + fsm_t + [_c_int] * 3 + [_ip] * 10 + [_c_int, _c_int, _vp]
+    lib.sg_spec_verify_keys.restype = _c_int
+    lib.sg_fsm_commit.argtypes = [_vp, _ip] + fsm_t + [_c_int] * 3 + [_ip] * 6 + [_c_int, _c_int, _vp]
+    lib.sg_fsm_commit.restype = _c_int
+    lib.sg_gemm_argmax.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int, _ip, _ip, _vp,
+                                   _vp, _vp]
+    lib.sg_gemm_argmax.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
@@ -440,14 +452,26 @@ def fsm_sample(logits: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Ten
 SPEC_MAX_K = 8
 
 
-def spec_plan(K: int, T_cap: int, sep_token: int, scratch_slot: int, tok_buf: torch.Tensor, pos: torch.Tensor,
+def _fsm_args(fsm):
+    return (_p(fsm.masks), _p(fsm.state_mask), _p(fsm.next_sep_t), _p(fsm.next_tok_t), _p(fsm.enum_tok_t),
+            _p(fsm.enum_next_t), fsm.E)
+
+
+def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: int, sep_token: int,
+              scratch_slot: int, tok_buf: torch.Tensor, pos: torch.Tensor,
               slot: torch.Tensor, done: torch.Tensor, out_buf: torch.Tensor, out_len: torch.Tensor,
               body_buf: torch.Tensor, body_len: torch.Tensor, delim: torch.Tensor, draft_buf: torch.Tensor,
               x_tok: torch.Tensor, x_pos: torch.Tensor, x_slot: torch.Tensor, x_done: torch.Tensor,
               row_start: torch.Tensor, row_nd: torch.Tensor) -> None:
     """Prompt-lookup drafts for ``B = tok_buf.numel()`` rows packed into ``T_cap``
-    pseudo-rows (``csrc/spec_kernels.hip``).  All int32 except ``delim`` (uint8 [V])."""
+    pseudo-rows (``csrc/spec_kernels.hip``); drafts follow the schema FSM from each
+    row's ``state`` and ``x_state`` gets every pseudo-row's state.  All int32
+    except ``delim`` (uint8 [V])."""
     B = tok_buf.numel()
+    _req(state, torch.int32, "state")
+    _req(x_state, torch.int32, "x_state")
+    if state.numel() < B or x_state.numel() < T_cap:
+        raise ValueError("spec_plan: state / x_state too small")
     S1, LB = body_buf.shape
     for name, t in (("tok_buf", tok_buf), ("pos", pos), ("slot", slot), ("done", done), ("out_len", out_len),
                     ("row_start", row_start), ("row_nd", row_nd)):
@@ -468,6 +492,7 @@ def spec_plan(K: int, T_cap: int, sep_token: int, scratch_slot: int, tok_buf: to
     if not (0 <= scratch_slot < S1) or out_buf.shape[0] < B:
         raise ValueError("spec_plan: bad scratch slot / out_buf")
     _check(load_library().sg_spec_plan(
+        *_fsm_args(fsm), fsm.done_state, fsm.vocab, _p(state), _p(x_state),
         B, K, T_cap, sep_token, scratch_slot, _p(tok_buf), _p(pos), _p(slot), _p(done), _p(out_buf), _p(out_len),
         out_buf.shape[1], _p(body_buf), _p(body_len), LB, _p(delim), _p(draft_buf), _p(x_tok), _p(x_pos),
         _p(x_slot), _p(x_done), _p(row_start), _p(row_nd), _stream()), "spec_plan")
@@ -493,6 +518,62 @@ def spec_verify(logits: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.T
         _p(fsm.next_tok_t), _p(fsm.enum_tok_t), _p(fsm.enum_next_t), fsm.E, fsm.sep_token, fsm.done_state,
         _p(tok_buf), _p(out_buf), _p(out_len), _p(done), _p(pos), _p(x_tok), _p(row_start), _p(row_nd),
         _p(accepted), out_buf.shape[1], V, B, _stream()), "spec_verify")
+
+
+def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, best: torch.Tensor,
+                norm_eps: Optional[float] = None, cfg: Optional[int] = None) -> torch.Tensor:
+    """lm_head GEMM with the schema-FSM masked arg-max fused in (EPI 4): for every
+    row, ``best[row] = max(argmax_key(bf16 logit, token))`` over the tokens its FSM
+    state allows — no logits are written.  ``w`` [V, K] (final norm folded in when
+    ``norm_eps``); ``best`` uint64-as-int64 [>= M] is ZEROED here first."""
+    M, K = a.shape
+    N = w.shape[0]
+    if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or a.stride(1) != 1 or a.stride(0) % 8:
+        raise ValueError("gemm_argmax: bf16 activations with 16-B aligned rows required")
+    if not w.is_contiguous() or w.shape[1] != K or K % 64 or N % 128 or N != fsm.vocab:
+        raise ValueError(f"gemm_argmax: bad weight {tuple(w.shape)} for vocab {fsm.vocab}")
+    _req(row_state, torch.int32, "row_state")
+    if row_state.numel() < M or best.dtype != torch.int64 or best.numel() < M or not best.is_contiguous():
+        raise ValueError("gemm_argmax: row_state / best too small or best not int64")
+    best[:M].zero_()
+    if M == 0:
+        return best
+    if cfg is None:
+        cfg = 0 if -(-M // 128) * (N // 128) >= 480 else (3 if M > 1024 else 17)
+    _check(load_library().sg_gemm_argmax(_p(a), a.stride(0), _p(w), M, N, K, float(norm_eps or 0.0),
+                                         int(norm_eps is not None), cfg, _p(row_state), _p(fsm.state_mask),
+                                         _p(fsm.masks), _p(best), _stream()), "gemm_argmax")
+    return best
+
+
+def fsm_commit(best: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tensor, out_buf: torch.Tensor,
+               out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, B: int,
+               row_map: Optional[torch.Tensor] = None) -> None:
+    """Greedy FSM step from :func:`gemm_argmax` keys (row ``i`` -> state row ``row_map[i]``)."""
+    if best.dtype != torch.int64 or best.numel() < B or (row_map is not None and row_map.numel() < B):
+        raise ValueError("fsm_commit: bad best / row_map")
+    if row_map is None and state.numel() < B:
+        raise ValueError("fsm_commit: state smaller than B")
+    _check(load_library().sg_fsm_commit(
+        _p(best), _p(row_map), *_fsm_args(fsm), fsm.sep_token, fsm.done_state, fsm.vocab, _p(state), _p(tok_io),
+        _p(out_buf), _p(out_len), _p(done), _p(pos), out_buf.shape[1], B, _stream()), "fsm_commit")
+
+
+def spec_verify_keys(best: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.Tensor, out_buf: torch.Tensor,
+                     out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, x_tok: torch.Tensor,
+                     row_start: torch.Tensor, row_nd: torch.Tensor, accepted: Optional[torch.Tensor] = None) -> None:
+    """Greedy verification of the drafts from :func:`gemm_argmax` keys (one thread per row)."""
+    B = tok_buf.numel()
+    if best.dtype != torch.int64 or best.numel() < x_tok.numel():
+        raise ValueError("spec_verify_keys: best must cover every pseudo-row")
+    for name, t in (("state", state), ("out_len", out_len), ("done", done), ("pos", pos), ("row_start", row_start),
+                    ("row_nd", row_nd)):
+        if t.numel() < B or t.dtype != torch.int32:
+            raise ValueError(f"spec_verify_keys: bad {name}")
+    _check(load_library().sg_spec_verify_keys(
+        _p(best), *_fsm_args(fsm), fsm.sep_token, fsm.done_state, fsm.vocab, _p(state), _p(tok_buf), _p(out_buf),
+        _p(out_len), _p(done), _p(pos), _p(x_tok), _p(row_start), _p(row_nd), _p(accepted), out_buf.shape[1], B,
+        _stream()), "spec_verify_keys")
 
 
 def vt_shape(S: int, nkv: int, D: int, L: int):

@@ -19,6 +19,10 @@
 //   EPI 2  SwiGLU: W rows are interleaved in groups of 16 (16 gate rows, then the
 //          16 matching up rows), so one lane holds gate and up of the same output
 //          element in two accumulators; C = silu(g)·u with Nout = N / 2.
+//   EPI 4  lm_head + schema-FSM masked arg-max: nothing is stored; each row's
+//          bf16 logits of this N tile are masked with the row's FSM state and
+//          reduced to one (value, index) key, merged across N tiles with a 64-bit
+//          atomicMax — the [M, V] logits never reach HBM (sg_gemm_argmax).
 //
 // Tiling (cdna_hip_programming.md §5): 4 or 8 waves, BM×BN block tile,
 // BK = 64, 16×16×32 bf16 MFMAs; A/W tiles staged global → registers → LDS,
@@ -50,6 +54,22 @@ struct RopeArgs {
   uint16_t* vt_cache;   // [S][nkv][Lmax/8][64][8]
   int nh, nkv, Lmax, p0;
 };
+
+// EPI 4 (lm_head + masked arg-max) arguments.
+struct ArgmaxArgs {
+  const int* row_state;         // [M] FSM state of each row
+  const int* state_mask;        // [S] state -> mask row
+  const uint32_t* masks;        // [mask rows][N / 32] allowed-token bits
+  unsigned long long* best;     // [M] running max of argmax_key(), zeroed before the launch
+};
+
+// Orderable key: larger bf16 value first, then the SMALLER token index (the tie rule
+// of fsm_sample_kernel); -0 is folded into +0 so equal values compare equal.
+__device__ __forceinline__ unsigned long long argmax_key(float v, int idx) {
+  const uint32_t b = __float_as_uint(v + 0.0f);
+  const uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return ((unsigned long long)k << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
+}
 
 __device__ __forceinline__ float bf2f(uint32_t v) { return __uint_as_float(v << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {
@@ -131,7 +151,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
                                                          const uint16_t* __restrict__ W,
                                                          uint16_t* C, int ldc, const uint16_t* R, int ldr,
                                                          int M, int N, int K, float eps, int tiles_m,
-                                                         int tiles_n, int gm, RopeArgs ra) {
+                                                         int tiles_n, int gm, RopeArgs ra, ArgmaxArgs xa) {
   constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(EPI != 3 || BN == 64, "QKV+RoPE epilogue: one 64-wide head per N tile");
@@ -325,6 +345,41 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     return;
   }
 
+  // ---- epilogue 2 (EPI 4): per-row masked arg-max of this tile's bf16 logits.
+  // CPR lanes (consecutive, inside one wave) own one row's 8-column chunks.
+  if constexpr (EPI == 4) {
+    constexpr int CPR4 = BN / 8;
+    static_assert(CPR4 <= 64 && (CPR4 & (CPR4 - 1)) == 0, "row chunks must fit a wave");
+    const int words = N >> 5;
+    for (int q = tid; q < BM * CPR4; q += NT) {
+      const int row = q / CPR4, c = q % CPR4;
+      const int gr = m0 + row;
+      unsigned long long key = 0ull;
+      if (gr < M) {
+        const int col = n0 + c * 8;
+        const uint32_t* mrow = xa.masks + (size_t)xa.state_mask[xa.row_state[gr]] * words;
+        const uint32_t bits = (mrow[col >> 5] >> (col & 31)) & 0xffu;
+        if (bits) {
+          const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (bits & (1u << e)) {
+              const unsigned long long k2 = argmax_key(bf2f((w[e >> 1] >> ((e & 1) * 16)) & 0xffffu), col + e);
+              key = k2 > key ? k2 : key;
+            }
+        }
+      }
+#pragma unroll
+      for (int o = CPR4 / 2; o > 0; o >>= 1) {
+        const unsigned long long ok = __shfl_xor(key, o, 64);
+        key = ok > key ? ok : key;
+      }
+      if (c == 0 && gr < M && key) atomicMax(xa.best + gr, key);
+    }
+    return;
+  }
+
   // ---- epilogue 2: coalesced 16-B row chunks (+ residual)
   constexpr int CPR = BNO / 8;  // chunks per row
   const int c0 = EPI == 2 ? n0 / 2 : n0;
@@ -354,7 +409,7 @@ int g_group_m = 8;  // M-tiles per rasterisation group (sg_gemm_set_group_m)
 
 template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST>
 int launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
-           float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}) {
+           float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}, const ArgmaxArgs& xa = ArgmaxArgs{}) {
   // the staged C tile must fit in the K-loop buffers (not so for 256-wide plain outputs)
   constexpr int BNO = EPI == 2 ? BN / 2 : BN;
   if constexpr (BM * (BNO + 8) > ST * (BM + BN) * BK) {
@@ -363,7 +418,7 @@ int launch(const void* A, int lda, const void* W, void* C, int ldc, const void* 
     const int tm = (M + BM - 1) / BM, tn = N / BN;
     hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST>), dim3(tm * tn), dim3(WM * WN * 64), 0,
                        stream, (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R,
-                       ldr, M, N, K, eps, tm, tn, g_group_m > 0 ? g_group_m : 1, ra);
+                       ldr, M, N, K, eps, tm, tn, g_group_m > 0 ? g_group_m : 1, ra, xa);
     return 0;
   }
 }
@@ -402,7 +457,7 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 #define SG_PROBE(MODE)                                                                                          \
   hipLaunchKernelGGL((gemm_fused_kernel<128, 128, 2, 2, 2, true, 2, MODE>), dim3(tm * tn), dim3(256), 0, stream, \
                      (const uint16_t*)A, K, (const uint16_t*)W, (uint16_t*)C, N / 2, nullptr, 0, M, N, K, 1e-5f, tm, \
-                     tn, g_group_m, RopeArgs{})
+                     tn, g_group_m, RopeArgs{}, ArgmaxArgs{})
   if (mode == 1) SG_PROBE(1);
   else if (mode == 2) SG_PROBE(2);
   else if (mode == 3) SG_PROBE(3);
@@ -461,6 +516,25 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
     case 18: return launch<32, 64, 2, 2, 3, true, 4>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
     default: return -1;
   }
+}
+
+// lm_head + FSM-masked arg-max (EPI 4): W [N, K] with the final norm folded in,
+// best [M] uint64 zeroed before the launch; cfg 0 (128x128), 3 (64x64), 17 (32x64).
+int sg_gemm_argmax(const void* A, int lda, const void* W, int M, int N, int K, float eps, int norm, int cfg,
+                   const int* row_state, const int* state_mask, const void* masks, void* best, hipStream_t stream) {
+  if (M <= 0 || K % BK != 0 || lda % 8 != 0 || N % 128 != 0) return -2;
+  ArgmaxArgs xa{row_state, state_mask, (const uint32_t*)masks, (unsigned long long*)best};
+  RopeArgs ra{};
+#define SG_AM(BM_, BN_, WM_, WN_)                                                                                  \
+  return norm ? launch<BM_, BN_, WM_, WN_, 4, true, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa) \
+              : launch<BM_, BN_, WM_, WN_, 4, false, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa)
+  switch (cfg) {
+    case 0: SG_AM(128, 128, 2, 2);
+    case 3: SG_AM(64, 64, 2, 2);
+    case 17: SG_AM(32, 64, 2, 2);
+    default: return -1;
+  }
+#undef SG_AM
 }
 
 }  // extern "C"

@@ -33,10 +33,44 @@
 
 static __device__ __forceinline__ float sp_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
+// Schema-FSM tables (serving/fsm.py), as fsm_sample_kernel reads them.
+struct FsmTables {
+  const uint32_t* masks;
+  const int* state_mask;
+  const int* next_sep;
+  const int* next_tok;
+  const int* enum_tok;
+  const int* enum_next;
+  int E, sep_token, done_state, V;
+};
+
+// next state after emitting `tok` in state `s` (-1 = not allowed / dead end)
+static __device__ __forceinline__ int fsm_next(const FsmTables& f, int s, int tok) {
+  if (tok == f.sep_token) return f.next_sep[s];
+  int ns = f.next_tok[s];
+  if (f.E > 0 && ns == -2) {
+    ns = -1;
+    for (int e = 0; e < f.E; ++e)
+      if (f.enum_tok[s * f.E + e] == tok) { ns = f.enum_next[s * f.E + e]; break; }
+  }
+  return ns;
+}
+
+static __device__ __forceinline__ bool fsm_allows(const FsmTables& f, int s, int tok) {
+  const uint32_t* m = f.masks + (size_t)f.state_mask[s] * (f.V >> 5);
+  return (m[tok >> 5] >> (tok & 31)) & 1u;
+}
+
+// token of an arg-max key written by sg_gemm_argmax (0 = nothing allowed -> <sep>)
+static __device__ __forceinline__ int key_token(unsigned long long key, int sep_token) {
+  return key ? (int)(0xFFFFFFFFu - (uint32_t)(key & 0xFFFFFFFFull)) : sep_token;
+}
+
 // ---------------------------------------------------------------------------
 // plan: grid = 1 block of SPEC_THREADS; each thread owns RPT consecutive rows.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
+    FsmTables fsm, const int* __restrict__ state, int* __restrict__ x_state,
     int B, int K, int T_cap, int sep_token, int scratch_slot,
     const int* __restrict__ tok_buf, const int* __restrict__ pos, const int* __restrict__ slot,
     const int* __restrict__ done, const int* __restrict__ out_buf, const int* __restrict__ out_len, int max_out,
@@ -68,15 +102,19 @@ __global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
         for (int q = 0; q < bl; ++q)
           if (body[q] == t) { j = q; break; }
       if (j >= 0) {
+        // walk the schema FSM along the draft: a token the FSM forbids can never be
+        // accepted (the verify arg-max is masked), so the draft stops before it
+        int s = state[r];
         for (int i = 0; i < K; ++i) {
           const int q = j + 1 + i;
           if (q >= bl) break;
-          const int x = body[q];
-          if (delim[x]) {
-            draft_buf[r * SPEC_MAX_K + n++] = sep_token;
-            break;
-          }
+          const int x = delim[body[q]] ? sep_token : body[q];
+          if (!fsm_allows(fsm, s, x)) break;
+          const int ns = fsm_next(fsm, s, x);
+          if (ns < 0) break;
           draft_buf[r * SPEC_MAX_K + n++] = x;
+          s = ns;
+          if (x == sep_token || ns == fsm.done_state) break;
         }
       }
     }
@@ -115,15 +153,20 @@ __global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
     row_nd[r] = nc;
     const int p = pos[r], sl = slot[r];
     const int dn = done[r];
+    int s = state[r];
     x_tok[st] = tok_buf[r];
     x_pos[st] = p;
     x_slot[st] = sl;
     x_done[st] = dn;
+    x_state[st] = dn ? fsm.done_state : s;
     for (int i = 0; i < nc; ++i) {
-      x_tok[st + 1 + i] = draft_buf[r * SPEC_MAX_K + i];
+      const int x = draft_buf[r * SPEC_MAX_K + i];
+      s = fsm_next(fsm, s, x);  // valid: the draft walk checked it
+      x_tok[st + 1 + i] = x;
       x_pos[st + 1 + i] = p + 1 + i;
       x_slot[st + 1 + i] = sl;
       x_done[st + 1 + i] = 0;
+      x_state[st + 1 + i] = s;  // the state the row is in IF drafts 0..i are accepted
     }
   }
   // 4) unused tail: scratch slot, position 0, skipped by attention
@@ -133,7 +176,72 @@ __global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
     x_pos[i] = 0;
     x_slot[i] = scratch_slot;
     x_done[i] = 1;
+    x_state[i] = fsm.done_state;
   }
+}
+
+// ---------------------------------------------------------------------------
+// verify from arg-max keys (sg_gemm_argmax already masked each pseudo-row with
+// x_state): one thread per row, no logits read.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) spec_verify_keys_kernel(
+    FsmTables fsm, const unsigned long long* __restrict__ best, int* __restrict__ state, int* __restrict__ tok_buf,
+    int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done, int* __restrict__ pos,
+    const int* __restrict__ x_tok, const int* __restrict__ row_start, const int* __restrict__ row_nd,
+    int* __restrict__ accepted, int max_out, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  if (done[b]) {
+    if (accepted != nullptr) accepted[b] = 0;
+    return;
+  }
+  const int st = row_start[b], nd = row_nd[b];
+  int s = state[b], len = out_len[b], p = pos[b], emitted = 0, tok = tok_buf[b];
+  bool fin = false;
+  for (int i = 0; i <= nd; ++i) {
+    tok = key_token(best[st + i], fsm.sep_token);
+    const int ns = fsm_next(fsm, s, tok);
+    out_buf[(size_t)b * max_out + len] = tok;
+    ++len;
+    ++emitted;
+    s = ns < 0 ? fsm.done_state : ns;
+    if (ns < 0 || ns == fsm.done_state || len >= max_out) {
+      fin = true;
+      break;
+    }
+    ++p;
+    if (!(i < nd && tok == x_tok[st + i + 1])) break;
+  }
+  out_len[b] = len;
+  tok_buf[b] = tok;
+  state[b] = s;
+  pos[b] = p;
+  if (fin) done[b] = 1;
+  if (accepted != nullptr) accepted[b] = emitted;
+}
+
+// ---------------------------------------------------------------------------
+// one-token decode / prefill sampling from arg-max keys: the FSM step of
+// fsm_sample_kernel's greedy path.  Key row i updates state row row_map[i] (or i).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) fsm_commit_kernel(
+    FsmTables fsm, const unsigned long long* __restrict__ best, const int* __restrict__ row_map,
+    int* __restrict__ state, int* __restrict__ tok_io, int* __restrict__ out_buf, int* __restrict__ out_len,
+    int* __restrict__ done, int* __restrict__ pos, int max_out, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const int b = row_map ? row_map[i] : i;
+  if (done[b]) return;
+  const int s = state[b];
+  const int tok = key_token(best[i], fsm.sep_token);
+  const int ns = fsm_next(fsm, s, tok);
+  const int len = out_len[b];
+  out_buf[(size_t)b * max_out + len] = tok;
+  out_len[b] = len + 1;
+  tok_io[b] = tok;
+  state[b] = ns < 0 ? fsm.done_state : ns;
+  if (ns < 0 || ns == fsm.done_state || len + 1 >= max_out) done[b] = 1;
+  else pos[b] = pos[b] + 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -227,12 +335,22 @@ __global__ void __launch_bounds__(256) spec_verify_kernel(
 
 extern "C" {
 
-int sg_spec_plan(int B, int K, int T_cap, int sep_token, int scratch_slot, const int* tok_buf, const int* pos,
+static FsmTables make_fsm(const void* masks, const int* state_mask, const int* next_sep, const int* next_tok,
+                          const int* enum_tok, const int* enum_next, int E, int sep_token, int done_state, int V) {
+  return FsmTables{(const uint32_t*)masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token,
+                   done_state, V};
+}
+
+int sg_spec_plan(const void* masks, const int* state_mask, const int* next_sep, const int* next_tok,
+                 const int* enum_tok, const int* enum_next, int E, int done_state, int V, const int* state,
+                 int* x_state, int B, int K, int T_cap, int sep_token, int scratch_slot, const int* tok_buf, const int* pos,
                  const int* slot, const int* done, const int* out_buf, const int* out_len, int max_out,
                  const int* body_buf, const int* body_len, int LB, const void* delim, int* draft_buf, int* x_tok,
                  int* x_pos, int* x_slot, int* x_done, int* row_start, int* row_nd, hipStream_t stream) {
   if (K < 0 || K > SPEC_MAX_K || T_cap < B || B <= 0) return -1;
-  hipLaunchKernelGGL(spec_plan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, B, K, T_cap, sep_token, scratch_slot,
+  const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
+  hipLaunchKernelGGL(spec_plan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, f, state, x_state, B, K, T_cap,
+                     sep_token, scratch_slot,
                      tok_buf, pos, slot, done, out_buf, out_len, max_out, body_buf, body_len, LB,
                      (const uint8_t*)delim, draft_buf, x_tok, x_pos, x_slot, x_done, row_start, row_nd);
   return (int)hipGetLastError();
@@ -248,6 +366,31 @@ int sg_spec_verify(const void* logits, int ldl, const void* masks, const int* st
   hipLaunchKernelGGL(spec_verify_kernel, dim3(B), dim3(256), 0, stream, (const uint16_t*)logits, ldl,
                      (const uint32_t*)masks, state_mask, state, next_sep, next_tok, enum_tok, enum_next, E, sep_token,
                      done_state, tok_buf, out_buf, out_len, done, pos, x_tok, row_start, row_nd, accepted, max_out, V);
+  return (int)hipGetLastError();
+}
+
+int sg_spec_verify_keys(const void* best, const void* masks, const int* state_mask, const int* next_sep,
+                        const int* next_tok, const int* enum_tok, const int* enum_next, int E, int sep_token,
+                        int done_state, int V, int* state, int* tok_buf, int* out_buf, int* out_len, int* done, int* pos,
+                        const int* x_tok, const int* row_start, const int* row_nd, int* accepted, int max_out, int B,
+                        hipStream_t stream) {
+  if (B == 0) return 0;
+  const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
+  hipLaunchKernelGGL(spec_verify_keys_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, f,
+                     (const unsigned long long*)best, state, tok_buf, out_buf, out_len, done, pos, x_tok, row_start,
+                     row_nd, accepted, max_out, B);
+  return (int)hipGetLastError();
+}
+
+int sg_fsm_commit(const void* best, const int* row_map, const void* masks, const int* state_mask,
+                  const int* next_sep, const int* next_tok, const int* enum_tok, const int* enum_next, int E,
+                  int sep_token, int done_state, int V, int* state, int* tok_io, int* out_buf, int* out_len, int* done,
+                  int* pos,
+                  int max_out, int B, hipStream_t stream) {
+  if (B == 0) return 0;
+  const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
+  hipLaunchKernelGGL(fsm_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, f,
+                     (const unsigned long long*)best, row_map, state, tok_io, out_buf, out_len, done, pos, max_out, B);
   return (int)hipGetLastError();
 }
 

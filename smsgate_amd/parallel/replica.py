@@ -90,14 +90,24 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     from ..services.writer import WriterService
     from ..sinks.memory import MemorySink
 
+    from ..bus import connect
+
     client = RemoteEngineClient(conn, max_body_tokens=cfg.get("max_body_tokens", 128))
-    bus = MemoryBus()
+    dsn = cfg.get("bus")
+    # shared broker: every parser process of every GPU is ONE competing group on sms.raw
+    # (worker.py:199-202 semantics) and every writer one group on sms.parsed;
+    # memory: each process runs its own in-process bus (isolated partitions)
+    bus = await connect(dsn, shared=False) if dsn else MemoryBus()
     backend = RemoteLLMBackend(client, max_batch=cfg.get("batch", 512))
     worker = ParserWorker(bus, ParsePipeline(backend), batch=cfg.get("batch", 512),
                           concurrency=cfg.get("concurrency", 4), stats_interval=0)
+    if dsn:
+        worker.stage.max_ack_pending = 1 << 22  # all replicas' batches in flight at once
     # pb_writer with an in-memory sink on sms.parsed (BASELINE config #1: "... -> in-memory sink")
     sink = MemorySink()
     writer = WriterService(bus, [sink], batch=cfg.get("writer_batch", 512), stats_interval=0)
+    if dsn:
+        writer.stage.max_ack_pending = 1 << 22
     await worker.start()
     await writer.start()
     client.send_control({"event": "ready", "w": widx})
@@ -128,6 +138,18 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                     await asyncio.sleep(0)
 
             nsteps = len(prepared)
+            if dsn:
+                # shared broker: ingest everything (the gateway role); the rank process
+                # decides when the whole job has drained, then asks for the counts
+                for i in range(nsteps):
+                    await publish(i)
+                client.send_control({"event": "published", "w": widx})
+                cmd = await asyncio.to_thread(client.control.get)
+                counts = {k: worker.counts[k] - c0[k] for k in c0}
+                counts.update(sink_stored=writer.ok - w0[1], writer_no_merchant=writer.skipped - w0[2],
+                              writer_fail=writer.fail - w0[3])
+                client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
+                continue
             pub_task = asyncio.create_task(publish(0)) if nsteps else None
             done_msgs = 0
             for i in range(nsteps):
@@ -153,14 +175,44 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
 
 
 class Coordinator:
-    """Rank-side driver: serves the engine while steering the parser processes."""
+    """Rank-side driver: serves the engine while steering the parser processes.
 
-    def __init__(self, engine, conns: Sequence[Connection]) -> None:
+    With a shared broker (``bus_dsn``) the end of a phase is global: every raw
+    message of every rank published (a never-consumed counter durable on
+    ``sms.raw`` sees them all) and both the parser and the writer groups drained
+    (no pending, nothing un-acked); each rank polls that between engine steps."""
+
+    COUNTER = "bench_raw_counter"
+
+    def __init__(self, engine, conns: Sequence[Connection], bus_dsn: Optional[str] = None,
+                 world: int = 1) -> None:
         from ..serving.remote import EngineServer
 
         self.events: Dict[str, Dict[int, Any]] = {}
         self.server = EngineServer(engine, conns, on_control=self._on_control)
         self.n = len(conns)
+        self.world = world
+        self.bus = None
+        if bus_dsn:
+            from ..bus.base import SUBJECT_RAW
+            from ..bus.sync_client import SyncBusClient
+
+            self.bus = SyncBusClient(bus_dsn)
+            self.bus.ensure_stream()
+            self.bus.subscribe(SUBJECT_RAW, self.COUNTER)
+
+    def _drained(self, target_raw: int) -> bool:
+        ci = self.bus.consumer_info
+        if ci("SMS", self.COUNTER)["num_pending"] < target_raw:
+            return False
+        for durable in ("parser_worker", "pb_writer"):
+            try:
+                i = ci("SMS", durable)
+            except Exception:  # not created yet
+                return False
+            if i["num_pending"] or i["num_ack_pending"]:
+                return False
+        return True
 
     def _on_control(self, idx: int, obj: Any) -> None:
         self.events.setdefault(obj.get("event", "?"), {})[idx] = obj
@@ -183,14 +235,36 @@ class Coordinator:
         for i in range(self.n):
             self.server.send_control(i, {"cmd": "prepare", "n": n_per_step, "seeds": list(seeds_per_worker[i])})
         self.wait_all("prepared")
+        target = 0
+        if self.bus is not None:
+            n_raw = sum(len(s) for s in seeds_per_worker) * n_per_step * self.world
+            target = self.bus.consumer_info("SMS", self.COUNTER)["num_pending"] + n_raw
         if sync is not None:
             sync()
         t0 = time.perf_counter()
         self.broadcast({"cmd": "go"})
-        done = self.wait_all("done")
-        if sync is not None:
-            sync()
-        dt = time.perf_counter() - t0
+        if self.bus is not None:
+            self.wait_all("published")
+            last = [0.0]
+
+            def drained() -> bool:
+                now = time.perf_counter()
+                if now - last[0] < 0.005:
+                    return False
+                last[0] = now
+                return self._drained(target)
+
+            self.server.serve_until(drained)
+            if sync is not None:
+                sync()
+            dt = time.perf_counter() - t0
+            self.broadcast({"cmd": "report"})
+            done = self.wait_all("done")
+        else:
+            done = self.wait_all("done")
+            if sync is not None:
+                sync()
+            dt = time.perf_counter() - t0
         counts: Dict[str, int] = {}
         for d in done.values():
             for k, v in d["counts"].items():

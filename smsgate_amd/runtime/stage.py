@@ -73,6 +73,7 @@ class Stage:
         name: Optional[str] = None,
         poison_after: int = 5,
         dead_letter: Optional[DeadLetter] = None,
+        max_ack_pending: Optional[int] = None,
     ) -> None:
         self.bus = bus
         self.subject = subject
@@ -87,6 +88,7 @@ class Stage:
         self.stats_interval = stats_interval
         self.on_stats = on_stats
         self.name = name or durable
+        self.max_ack_pending = max_ack_pending
         self.poison_after = poison_after
         self.dead_letter = dead_letter
         self.dead_lettered = 0
@@ -100,9 +102,10 @@ class Stage:
 
     async def open(self) -> Subscription:
         if self.sub is None:
-            self.sub = await self.bus.subscribe(
-                self.subject, self.durable, ack_wait=self.ack_wait, max_deliver=self.max_deliver
-            )
+            opts = {"ack_wait": self.ack_wait, "max_deliver": self.max_deliver}
+            if self.max_ack_pending is not None:
+                opts["max_ack_pending"] = self.max_ack_pending
+            self.sub = await self.bus.subscribe(self.subject, self.durable, **opts)
         return self.sub
 
     async def _worker(self, wid: int) -> None:

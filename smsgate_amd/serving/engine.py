@@ -76,7 +76,11 @@ class EngineConfig:
     # vs 15.8 / 18.3 / 20.5 us at 256 / 512 / 1024 rows, a tie at 2048, slower at 4096
     decode_attn_small_rows: int = 1024
     decode_attn_small: str = "split2"
-    lm_head_fused: bool = False  # lm_head through the fused-norm GEMM too (slower than hipBLASLt at 8192 wide)
+    lm_head_fused: bool = False  # logits via the fused-norm GEMM instead of hipBLASLt (logits modes only)
+    # greedy decoding: lm_head GEMM with the FSM-masked arg-max in its epilogue (EPI 4 of
+    # csrc/gemm_kernels.hip) -- no [B, V] logits in HBM, no separate sampling kernel,
+    # no vendor GEMM.  Needs temperature 0; sampling (temperature > 0) keeps the logits path.
+    lm_head_argmax: bool = True
     buckets: Tuple[int, ...] = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
     # nano-batch overlap (measured +10% msgs/s at 8192 slots, profiles/r01b_split_ab.txt):
     split_decode: int = 4096  # >0: decode buckets >= this run as two half-batches on two streams
@@ -89,7 +93,10 @@ class EngineConfig:
     # `spec_k` drafts per row looked up in the row's own SMS body (the extractor copies
     # body tokens); greedy only.  0 = off.  A step packs B rows + at most
     # ceil(spec_draft_frac * B) drafts into one forward (fixed shape per bucket).
-    spec_k: int = 0
+    # measured (profiles/r02_bus_spec_ab.jsonl, r02_latency_trained_spec*.json): 2.54 tokens
+    # per row-step on the trained 135M extractor, p50 latency 64 -> 33 ms at 1 k msgs/s,
+    # 164 -> 76 ms at 10 k; +3-4 % msgs/s on the headline bench
+    spec_k: int = 4
     spec_draft_frac: float = 2.0
     spec_max_rows: int = 1 << 30  # buckets above this decode one token per row
 
@@ -167,6 +174,7 @@ class ExtractionEngine:
             self.fw_down = [w.down[i].contiguous() for i in range(mc.layers)]
             self.fw_lm = ops.fold_norm(self.lm_head, w.ln_f)
         self.fsm: SchemaFSM = build_fsm(tokenizer, self.V_dec, fields).to_device(self.device)
+        self.argmax = ec.lm_head_argmax and ec.temperature <= 0 and self.V_dec % 128 == 0
         self.max_out = self.fsm.max_steps()
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)
         self.P0 = len(self.prefix_ids)
@@ -198,6 +206,8 @@ class ExtractionEngine:
         self.out_len = torch.zeros(S, **i32)
         self.out_buf = torch.zeros(S, self.max_out, **i32)
         self.slot_id = torch.arange(S, **i32)  # row -> KV slot (rows are compacted, KV never moves)
+        self.best = torch.zeros(S, dtype=torch.int64, device=dev)  # arg-max keys (lm_head_argmax)
+        self.start_states = torch.full((S,), self.fsm.start_state, **i32)
         self.slot_host = np.arange(S, dtype=np.int32)
         self.free_rows: List[int] = list(range(S))
         heapq.heapify(self.free_rows)
@@ -269,6 +279,12 @@ class ExtractionEngine:
 
     def _forward(self, x: torch.Tensor, **kw) -> torch.Tensor:
         return self._layers_fused(x, **kw) if self.fused else self._layers(x, **kw)
+
+    def _argmax(self, h: torch.Tensor, row_state: torch.Tensor, best: torch.Tensor) -> torch.Tensor:
+        """lm_head + FSM-masked arg-max keys (no logits materialised)."""
+        if self.fused:  # h is the un-normed residual stream: the final norm is the GEMM prologue
+            return ops.gemm_argmax(h, self.fw_lm, row_state, self.fsm, best, norm_eps=self.mc.eps)
+        return ops.gemm_argmax(h, self.lm_head, row_state, self.fsm, best)
 
     def _logits(self, h: torch.Tensor) -> torch.Tensor:
         if self.fused:
@@ -348,7 +364,8 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
         last = h.index_select(0, (cu_d[1:] - 1).long())
-        logits = self._logits(last)
+        if not sample or not self.argmax:
+            logits = self._logits(last)
         if not sample:
             return logits
         # reset the admitted rows, then sample their first answer token
@@ -357,8 +374,15 @@ class ExtractionEngine:
         self.out_len.index_fill_(0, rl, 0)
         self.state.index_fill_(0, rl, self.fsm.start_state)
         self.pos.index_copy_(0, rl, last_pos_d)
-        ops.fsm_sample(logits, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done, self.pos,
-                       self.slot_id, self.cfg.temperature, self.cfg.seed, row_map=rows_d)
+        if self.argmax:
+            best = torch.empty(n, dtype=torch.int64, device=dev)
+            self._argmax(last, self.start_states[:n], best)
+            ops.fsm_commit(best, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done, self.pos,
+                           n, row_map=rows_d)
+            logits = None
+        else:
+            ops.fsm_sample(logits, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done,
+                           self.pos, self.slot_id, self.cfg.temperature, self.cfg.seed, row_map=rows_d)
         self.stats.prefill_tokens += T
         self.stats.prefill_seqs += len(items)
         self.stats.prefill_s += time.perf_counter() - t0
@@ -391,6 +415,12 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0,
                           hook=hook)
+        if sample and self.argmax:
+            best = self.best[r0:r1]
+            self._argmax(h, self.state[r0:r1], best)
+            ops.fsm_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
+                           pos, B)
+            return best
         logits = self._logits(h)
         if sample:
             ops.fsm_sample(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
@@ -418,6 +448,8 @@ class ExtractionEngine:
         self.x_pos = torch.zeros(cap, **i32)
         self.x_slot = torch.full((cap,), S, **i32)
         self.x_done = torch.ones(cap, **i32)
+        self.x_state = torch.full((cap,), self.fsm.done_state, **i32)
+        self.x_best = torch.zeros(cap, dtype=torch.int64, device=dev)
         self.row_start = torch.zeros(S, **i32)
         self.row_nd = torch.zeros(S, **i32)
         self.spec_acc = torch.zeros(S, **i32)
@@ -441,7 +473,9 @@ class ExtractionEngine:
         xt, xp, xs, xd = (self.x_tok[off:off + T], self.x_pos[off:off + T], self.x_slot[off:off + T],
                           self.x_done[off:off + T])
         rs, nd, acc = self.row_start[r0:r1], self.row_nd[r0:r1], self.spec_acc[r0:r1]
-        ops.spec_plan(self.cfg.spec_k, T, self.tok.sep, self.scratch_slot, tok, pos, slot, done,
+        xst = self.x_state[off:off + T]
+        ops.spec_plan(self.fsm, self.state[r0:r1], xst, self.cfg.spec_k, T, self.tok.sep, self.scratch_slot, tok,
+                      pos, slot, done,
                       self.out_buf[r0:r1], self.out_len[r0:r1], self.body_buf, self.body_len, self.spec_delim,
                       self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd)
         x = F.embedding(xt.long(), self.w.embed)
@@ -462,10 +496,19 @@ class ExtractionEngine:
                             done=xd, impl=impl, scratch=scratch)
 
         h = self._forward(x, pos_tok=xp, slot_tok=xs, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0, hook=hook)
-        logits = self._logits(h)
-        if sample:
+        if sample and self.argmax:
+            # every pseudo-row masked with the state it has if its row's drafts so far are accepted
+            best = self.x_best[off:off + T]
+            self._argmax(h, xst, best)
+            ops.spec_verify_keys(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
+                                 done, pos, xt, rs, nd, acc)
+            logits = best
+        else:
+            logits = self._logits(h)
+        if sample and not self.argmax:
             ops.spec_verify(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
                             pos, xt, rs, nd, acc)
+        if sample:
             # tokens emitted and live rows this step (read back only by stats())
             self.spec_counts += torch.stack([acc.sum(dtype=torch.int64), (acc > 0).sum(dtype=torch.int64)])
         return logits

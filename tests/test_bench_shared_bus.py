@@ -1,0 +1,29 @@
+"""The benchmark harness through ONE shared native broker: two ranks (gloo, CPU echo
+engines) whose parser and writer processes form single competing groups on one
+smsgate-busd; every message is routed once and written once."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "smsgate_amd/native/_bin/smsgate-busd")),
+                    reason="native broker not built")
+def test_two_ranks_one_broker():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29671", "bench.py", "--gpus", "2", "--cpu-echo-engine",
+           "--steps", "2", "--warmup", "1", "--msgs-per-step", "1024", "--cpu-workers", "2", "--bus", "busd"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert r.returncode == 0 and len(lines) == 1, r.stderr[-3000:]
+    out = lines[0]
+    rt = out["routing"]
+    total = 2 * 2 * 1024  # ranks x steps x msgs per step
+    assert rt["parsed"] + rt["keyword_skipped"] + rt["broken"] + rt["dlq"] == total
+    assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"]  # every parsed message written once
+    assert "shared smsgate-busd" in out["config"]["bus"] and out["n_gpus"] == 2
+    assert not [d for d in os.listdir("/tmp") if d == "smsgate-bench-bus-29671"]  # broker dir cleaned up

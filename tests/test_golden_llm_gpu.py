@@ -20,7 +20,7 @@ from smsgate_amd.parse.pipeline import ParsePipeline  # noqa: E402
 
 @pytest.fixture(scope="module")
 def pipeline():
-    eng = build_engine("small", device="cuda", max_slots=64, buckets=(64,))
+    eng = build_engine("small", device="cuda", max_slots=64, buckets=(64,), spec_k=0)
     return ParsePipeline(LocalLLMBackend.from_engine(eng))
 
 

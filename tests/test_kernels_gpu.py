@@ -278,3 +278,43 @@ def test_gemm_qkv_rope_matches_unfused(cfg, M):
         caches.append((q, kc, vt))
     for a, b in zip(*caches):
         torch.testing.assert_close(a.float(), b.float(), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 3, 17])
+@pytest.mark.parametrize("M", [1, 77, 700])
+def test_gemm_argmax_matches_logits_path(cfg, M):
+    """lm_head GEMM with the fused FSM-masked arg-max (EPI 4) == the logits path:
+    same-kernel bf16 logits (ops.gemm with the norm prologue) + fsm_sample's greedy
+    pick; fsm_commit then makes the same FSM step as fsm_sample."""
+    from smsgate_amd.models.tokenizer import load_tokenizer
+    from smsgate_amd.serving.fsm import build_fsm
+
+    tk = load_tokenizer()
+    V, K = (tk.vocab_size + 127) // 128 * 128, 576
+    fsm = build_fsm(tk, V).to_device(DEV)
+    a = _bf(M, K, seed=31)
+    w = _bf(V, K, scale=0.05, seed=32)
+    states_h = torch.randint(0, fsm.num_states, (M,))
+    row_state = states_h.to(torch.int32).to(DEV)
+    best = torch.zeros(M + 3, dtype=torch.int64, device=DEV)
+    ops.gemm_argmax(a, w, row_state, fsm, best, norm_eps=1e-5, cfg=cfg)
+    logits = ops.gemm(a, w, norm_eps=1e-5)
+    args = [torch.zeros(M, dtype=torch.int32, device=DEV) for _ in range(5)]  # tok, out_len, done, pos, slot
+    out_a = torch.zeros(M, 4, dtype=torch.int32, device=DEV)
+    st_a = row_state.clone()
+    ops.fsm_sample(logits, fsm, st_a, args[0], out_a, args[1], args[2], args[3], args[4], 0.0, 0)
+    tok_b = torch.zeros(M, dtype=torch.int32, device=DEV)
+    out_b = torch.zeros(M, 4, dtype=torch.int32, device=DEV)
+    len_b = torch.zeros(M, dtype=torch.int32, device=DEV)
+    st_b = row_state.clone()
+    ops.fsm_commit(best, fsm, st_b, tok_b, out_b, len_b, torch.zeros(M, dtype=torch.int32, device=DEV),
+                   torch.zeros(M, dtype=torch.int32, device=DEV), M)
+    assert torch.equal(args[0], tok_b) and torch.equal(out_a, out_b) and torch.equal(st_a, st_b)
+    assert torch.equal(args[1], len_b)
+    # and against a plain fp32 masked arg-max of the same bf16 logits
+    allowed = torch.from_numpy(fsm.allowed)
+    lf = logits.float().cpu()
+    for b in range(0, M, max(1, M // 13)):
+        s = int(states_h[b])
+        if allowed[s].any():
+            assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())

@@ -83,7 +83,8 @@ def test_full_pipeline_http_to_sql(tmp_path, arun):
         return parser, writer, parsed, processing, failed
 
     parser, writer, parsed, processing, failed = arun(go())
-    assert parser.counts == {"ok": 4, "fail": 1, "skip": 0}  # OTP counted OK (D11 parity)
+    assert parser.counts == {"ok": 4, "fail": 1, "skip": 0,  # OTP counted OK (D11 parity) ...
+                             "parsed": 3, "keyword_skipped": 1}  # ... and reported apart
     assert len(parsed) == 3 and parsed == processing
     assert [f.get("reason") for f in failed] == ["unmatched"] and failed[0]["raw"]["body"] == "hello there"
     assert writer.ok == 3 and writer.fail == 0
@@ -118,7 +119,7 @@ def test_parser_dlq_envelopes(arun):
         return w, await _drain(bus, SUBJECT_FAILED), await _drain(bus, SUBJECT_PARSED)
 
     w, failed, parsed = arun(go())
-    assert w.counts == {"ok": 1, "fail": 3, "skip": 1}
+    assert w.counts == {"ok": 1, "fail": 3, "skip": 1, "parsed": 1, "keyword_skipped": 0}
     assert failed[0]["entry"] == "{not json" and "err" in failed[0]
     assert failed[1] == {"err": "LLM exploded", "entry": _raw("boom body").model_dump()}
     assert failed[2]["err"] == FUTURE_DATE_ERR
@@ -148,7 +149,7 @@ def test_handler_exception_does_not_kill_loop(arun):
 
     w = arun(go())
     assert w.stage.handler_errors == 1 and calls["n"] == 2
-    assert w.counts == {"ok": 1, "fail": 0, "skip": 0}
+    assert w.counts == {"ok": 1, "fail": 0, "skip": 0, "parsed": 1, "keyword_skipped": 0}
 
 
 def test_parser_tracing_spans_and_sentry_forwarding(arun, monkeypatch):

@@ -71,6 +71,8 @@ def _args(argv=None):
     p.add_argument("--admit-frac", type=float, default=0.25)
     p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)
+    p.add_argument("--bus-shards", type=int, default=2,
+                   help="brokers per node, sharded by subject (sms.raw | the parser's outputs)")
     p.add_argument("--bus", default="busd", choices=["memory", "busd"],
                    help="busd: ONE shared native broker per node (journal on) carries sms.raw / sms.parsed for every "
                         "GPU's parser and writer processes (one competing group each); memory: an in-process bus per "
@@ -210,36 +212,42 @@ def run_replica(args, rank: int, world: int, local: int):
         counts = dict(zip(keys, (int(x) for x in c.tolist())))
         dist.barrier()  # every rank is done with the broker
         dist.destroy_process_group()
-    if broker is not None:
-        broker.stop()
+    if broker:
         import shutil
 
-        shutil.rmtree(os.path.dirname(broker.listens[0].replace("unix://", "")), ignore_errors=True)
+        for b in broker:
+            b.stop()
+        shutil.rmtree(os.path.dirname(broker[0].listens[0].replace("unix://", "")), ignore_errors=True)
     return dt, counts, init_s, estats, prov, quality
 
 
 def start_node_broker(args, local: int):
-    """Local rank 0 starts ``smsgate-busd`` (journal in a temp dir, fsync interval);
-    the other ranks of the node wait for its socket.  Returns (broker | None, dsn)."""
+    """Local rank 0 starts ``--bus-shards`` ``smsgate-busd`` brokers (journal in a temp
+    dir, fsync interval), sharded by subject; the other ranks of the node wait for
+    their sockets.  Returns (list of brokers | None, dsn)."""
     import tempfile
 
     tag = os.environ.get("MASTER_PORT") or str(os.getpid())
     root = os.path.join(tempfile.gettempdir(), f"smsgate-bench-bus-{tag}")
-    sock = os.path.join(root, "bus.sock")
+    n = max(1, args.bus_shards)
+    socks = [os.path.join(root, f"bus{k}.sock") for k in range(n)]
+    dsn = ("sharded+" if n > 1 else "") + ",".join(f"unix://{p}" for p in socks)
     if local == 0:
         from smsgate_amd.native import spawn_busd
 
         os.makedirs(root, exist_ok=True)
-        if os.path.exists(sock):
-            os.unlink(sock)
-        broker = spawn_busd(f"unix://{sock}", os.path.join(root, "data"))
-        return broker, f"unix://{sock}"
+        brokers = []
+        for k, p in enumerate(socks):
+            if os.path.exists(p):
+                os.unlink(p)
+            brokers.append(spawn_busd(f"unix://{p}", os.path.join(root, f"data{k}")))
+        return brokers, dsn
     t_end = time.time() + 60
-    while not os.path.exists(sock):
+    while not all(os.path.exists(p) for p in socks):
         if time.time() > t_end:
-            raise SystemExit(f"bench: the node broker socket {sock} never appeared")
+            raise SystemExit(f"bench: the node broker sockets {socks} never appeared")
         time.sleep(0.05)
-    return None, f"unix://{sock}"
+    return None, dsn
 
 
 ROUTING_KEYS = ("ok", "fail", "skip", "parsed", "keyword_skipped", "sink_stored", "writer_no_merchant", "writer_fail")
@@ -363,8 +371,9 @@ def main(argv=None) -> int:
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
                 "pipeline": ("payload->RawSMS->bus sms.raw->parser_worker->sms.parsed+sms.processing|DLQ->ack"
                              + ("->pb_writer->in-memory sink" if gpu else "")),
-                "bus": ("one shared smsgate-busd per node (journal on), one competing parser group and one writer "
-                        "group across all GPUs" if args.bus == "busd" else "in-process bus per parser process"),
+                "bus": (f"shared smsgate-busd brokers per node ({max(1, args.bus_shards)}, sharded by subject; "
+                        "journal on), one competing parser group and one writer group across all GPUs"
+                        if args.bus == "busd" else "in-process bus per parser process"),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
                 "seq_len": "shared prefix 20 + ~48 prompt + <=131 schema-constrained output tokens (~38 trained)",

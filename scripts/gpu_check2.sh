@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -k "argmax or fsm" tests/test_spec_gpu.py tests/test_golden_llm_gpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_new.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_spec_gpu.py tests/test_golden_llm_gpu.py tests/test_engine_gpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_new.log 2>&1
 rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_new.log | tail -25; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc

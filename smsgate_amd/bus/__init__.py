@@ -10,7 +10,9 @@
   ``python -m smsgate_amd bus-server`` broker process;
 * ``nats://host:port`` — :class:`~.nats_client.NatsBus`: the NATS wire protocol +
   JetStream API (no nats-py needed), against a real ``nats-server`` or our broker's
-  NATS front-end (``bus-server --nats-listen``).
+  NATS front-end (``bus-server --nats-listen``);
+* ``sharded+<dsn>,<dsn>...`` — :class:`~.sharded.ShardedBus`: several brokers as
+  one bus, sharded by subject (``sms.raw`` on the first).
 """
 from __future__ import annotations
 
@@ -67,6 +69,10 @@ def reset_connections() -> None:
 
 
 async def _open(dsn: str, max_age: float) -> Bus:
+    if dsn.startswith("sharded+"):
+        from .sharded import ShardedBus
+
+        return await ShardedBus.connect([d for d in dsn[len("sharded+"):].split(",") if d], max_age)
     u = urlparse(dsn)
     scheme = u.scheme or "memory"
     if scheme == "memory":

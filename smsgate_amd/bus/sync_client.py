@@ -22,6 +22,14 @@ _LEN = struct.Struct("<I")
 
 
 class SyncBusClient:
+    """``dsn``: one broker (``unix://`` / ``tcp://``) or a ``sharded+...`` list
+    (:mod:`.sharded`): then a durable is looked up on the shard owning it."""
+
+    def __new__(cls, dsn: str, timeout: float = 10.0):
+        if dsn.startswith("sharded+"):
+            return _SyncSharded([d for d in dsn[len("sharded+"):].split(",") if d], timeout)
+        return super().__new__(cls)
+
     def __init__(self, dsn: str, timeout: float = 10.0) -> None:
         u = urlparse(dsn)
         if u.scheme == "unix":
@@ -67,3 +75,30 @@ class SyncBusClient:
             self.sock.close()
         except OSError:
             pass
+
+
+class _SyncSharded:
+    def __init__(self, dsns, timeout: float) -> None:
+        self.members = [SyncBusClient(d, timeout) for d in dsns]
+
+    def ensure_stream(self) -> None:
+        for m in self.members:
+            m.ensure_stream()
+
+    def subscribe(self, subject: str, durable: str, **opts: Any) -> str:
+        from .sharded import shard_of
+
+        return self.members[shard_of(subject, len(self.members))].subscribe(subject, durable, **opts)
+
+    def consumer_info(self, stream: str, durable: str) -> Dict[str, Any]:
+        err: Exception = BusError(f"consumer {durable!r} not found on any shard")
+        for m in self.members:
+            try:
+                return m.consumer_info(stream, durable)
+            except BusError as exc:
+                err = exc
+        raise err
+
+    def close(self) -> None:
+        for m in self.members:
+            m.close()

@@ -392,7 +392,7 @@ class ExtractionEngine:
     def _decode_step(self, B: int, sample: bool = True, r0: int = 0, hook=None) -> torch.Tensor:
         """One decode step of rows ``r0 .. r0+B`` (every per-row buffer is sliced,
         so two disjoint row ranges can run as independent sub-batches)."""
-        if self._use_spec(B):
+        if sample and self._use_spec(B):  # (debug_logits wants one plain token per row)
             return self._spec_step(B, r0, hook=hook, sample=sample)
         r1 = r0 + B
         tok = self.tok_buf[r0:r1]

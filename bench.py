@@ -16,7 +16,8 @@ goes on to the ``pb_writer`` stage and an in-memory sink inside the timed region
 Weights (``--weights``): no pretrained checkpoint exists on the box and a 270 MB
 file is not shipped, so by default the flagship is **trained in the run, before
 the timed region** (``--train-steps`` AdamW steps on synthetic bank SMS of the
-*training* vocabulary; data-parallel over RCCL when N > 1, global batch fixed),
+*training* vocabulary, on local rank 0, so every N serves the same weights; the
+other ranks load the file it publishes),
 then the timed traffic uses the *held-out* vocabulary (merchant / city / street
 names the model never saw).  The JSON states the weights' provenance, a held-out
 accuracy check, and the routing split (parsed / keyword-skipped / broken / DLQ).
@@ -62,7 +63,7 @@ def _args(argv=None):
     p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
     p.add_argument("--train-lr", type=float, default=1e-3)
     p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",
-                   help="reuse weights trained by an earlier run with the same settings ('' = off)")
+                   help="where local rank 0 publishes the trained weights; reused by later identical runs")
     p.add_argument("--eval-n", type=int, default=500, help="held-out SMS scored before the timed region (0 = skip)")
     p.add_argument("--traffic-vocab", default="heldout", choices=["heldout", "train"])
     p.add_argument("--msgs-per-step", type=int, default=16384)
@@ -256,6 +257,7 @@ ROUTING_KEYS = ("ok", "fail", "skip", "parsed", "keyword_skipped", "sink_stored"
 def acquire_weights(args, device: str, rank: int, world: int):
     """The flagship's weights for this run and a provenance record (see module doc)."""
     import hashlib
+    import tempfile
 
     import torch
 
@@ -269,25 +271,34 @@ def acquire_weights(args, device: str, rank: int, world: int):
     from smsgate_amd.models.tokenizer import ASSET
     from smsgate_amd.models.train import TrainConfig, train_extractor
 
-    tc = TrainConfig(model=args.model, steps=args.train_steps, batch=max(8, args.train_batch // world),
-                     lr=args.train_lr, log_every=0)
-    h = hashlib.sha256(repr((tc, world, open(ASSET, "rb").read())).encode(errors="ignore")).hexdigest()[:16]
-    path = os.path.join(args.weights_cache, f"{args.model}-{h}.safetensors") if args.weights_cache else ""
-    prov = {"weights": (f"trained in this run before the timed region: {tc.steps} AdamW steps x {tc.batch * world} "
-                        f"synthetic SMS (training vocabulary), seed {tc.seed}, bf16 autocast"
-                        + (f", data-parallel over {world} ranks (RCCL all-reduce)" if world > 1 else ""))}
-    if path and os.path.exists(path):
+    # one trainer per node: local rank 0 trains (the same run as on one GPU, so every N
+    # serves identical weights) and publishes the file; the other ranks load it
+    tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
+                     log_every=0, data_parallel=False)
+    h = hashlib.sha256(repr((tc, open(ASSET, "rb").read())).encode(errors="ignore")).hexdigest()[:16]
+    cache = args.weights_cache or os.path.join(tempfile.gettempdir(), f"smsgate-bench-w-{os.getpid()}")
+    path = os.path.join(cache, f"{args.model}-{h}.safetensors")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    prov = {"weights": (f"trained in this run before the timed region: {tc.steps} AdamW steps x {tc.batch} "
+                        f"synthetic SMS (training vocabulary), seed {tc.seed}, bf16 autocast, on local rank 0")}
+    if os.path.exists(path):
         w = ExtractorWeights.load(path, CONFIGS[args.model], device=torch.device(device))
         prov["weights"] += " (reused from an earlier identical run's cache)"
         return w, prov
+    if local != 0:
+        t_end = time.time() + 1800
+        while not os.path.exists(path):
+            if time.time() > t_end:
+                raise SystemExit(f"bench: local rank 0 never published the trained weights {path}")
+            time.sleep(0.5)
+        return ExtractorWeights.load(path, CONFIGS[args.model], device=torch.device(device)), prov
     t0 = time.perf_counter()
     w = train_extractor(tc, device=device, log=lambda s: None)
     prov["train_s"] = round(time.perf_counter() - t0, 1)
-    if path and rank == 0:
-        os.makedirs(args.weights_cache, exist_ok=True)
-        tmp = path + f".{os.getpid()}.tmp"
-        w.save(tmp)
-        os.replace(tmp, path)
+    os.makedirs(cache, exist_ok=True)
+    tmp = path + f".{os.getpid()}.tmp"
+    w.save(tmp)
+    os.replace(tmp, path)
     return w, prov
 
 

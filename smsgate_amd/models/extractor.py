@@ -18,7 +18,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import asdict, dataclass
-from typing import Dict, Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -115,11 +115,15 @@ class ExtractorWeights(torch.nn.Module):
         return w
 
 
-def _rope(x: torch.Tensor, pos: torch.Tensor, theta: float) -> torch.Tensor:
+def _rope_tables(T: int, D: int, theta: float, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    inv = 1.0 / (theta ** (torch.arange(0, D, 2, device=device, dtype=torch.float32) / D))
+    ang = torch.arange(T, device=device, dtype=torch.float32)[:, None] * inv[None, :]
+    return ang.cos()[:, None, :], ang.sin()[:, None, :]  # [T, 1, D/2]
+
+
+def _rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """rotate-half RoPE; ``x`` [..., T, H, D] with tables [T, 1, D/2]."""
     D = x.shape[-1]
-    inv = 1.0 / (theta ** (torch.arange(0, D, 2, device=x.device, dtype=torch.float32) / D))
-    ang = pos.float()[:, None] * inv[None, :]
-    cos, sin = ang.cos()[:, None, :], ang.sin()[:, None, :]
     x1, x2 = x[..., : D // 2], x[..., D // 2:]
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
 
@@ -138,19 +142,18 @@ def reference_forward(w: ExtractorWeights, ids: torch.Tensor, compute_dtype=torc
     """
     cfg = w.cfg
     B, T = ids.shape
-    pos = torch.arange(T, device=ids.device)
     x = F.embedding(ids, w.embed).to(compute_dtype)
-    G = cfg.heads // cfg.kv_heads
+    cos, sin = _rope_tables(T, cfg.head_dim, cfg.rope_theta, ids.device)  # once, not per layer
     for i in range(cfg.layers):
         h = _rms(x, w.ln1[i].to(compute_dtype), cfg.eps)
         qkv = h @ w.qkv[i].to(compute_dtype).t()
         q, k, v = qkv.split([cfg.heads * cfg.head_dim, cfg.kv_heads * cfg.head_dim, cfg.kv_heads * cfg.head_dim], -1)
-        q = _rope(q.reshape(B * T, cfg.heads, cfg.head_dim), pos.repeat(B), cfg.rope_theta)
-        k = _rope(k.reshape(B * T, cfg.kv_heads, cfg.head_dim), pos.repeat(B), cfg.rope_theta)
-        q = q.reshape(B, T, cfg.heads, cfg.head_dim).transpose(1, 2)
-        k = k.reshape(B, T, cfg.kv_heads, cfg.head_dim).transpose(1, 2).repeat_interleave(G, dim=1)
-        v = v.reshape(B, T, cfg.kv_heads, cfg.head_dim).transpose(1, 2).repeat_interleave(G, dim=1)
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=1.0 / math.sqrt(cfg.head_dim))
+        q = _rope(q.reshape(B, T, cfg.heads, cfg.head_dim), cos, sin).transpose(1, 2)
+        k = _rope(k.reshape(B, T, cfg.kv_heads, cfg.head_dim), cos, sin).transpose(1, 2)
+        v = v.reshape(B, T, cfg.kv_heads, cfg.head_dim).transpose(1, 2)
+        # GQA inside SDPA: no repeat_interleave copies of K/V
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=1.0 / math.sqrt(cfg.head_dim),
+                                           enable_gqa=cfg.heads != cfg.kv_heads)
         a = a.transpose(1, 2).reshape(B, T, cfg.heads * cfg.head_dim)
         x = x + a @ w.o[i].to(compute_dtype).t()
         h = _rms(x, w.ln2[i].to(compute_dtype), cfg.eps)

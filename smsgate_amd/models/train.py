@@ -69,6 +69,7 @@ class TrainConfig:
     resume: bool = False
     bucket_mb: float = 64.0
     vocab_name: str = "train"  # synthetic vocabulary pool (utils.synth.vocab)
+    data_parallel: bool = True  # under torch.distributed: all-reduce gradients (False: train this rank alone)
     eval_every: int = 0  # call on_eval(step, serving weights) every N steps (0 = never)
 
 
@@ -172,8 +173,9 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     from ..parallel.ddp import GradBuckets
     from ..serving.fsm import build_fsm
 
-    rank = dist.get_rank() if dist.is_initialized() else 0
-    world = dist.get_world_size() if dist.is_initialized() else 1
+    ddp = dist.is_initialized() and cfg.data_parallel
+    rank = dist.get_rank() if ddp else 0
+    world = dist.get_world_size() if ddp else 1
 
     tok = tok or load_tokenizer()
     mcfg = CONFIGS[cfg.model]
@@ -196,7 +198,7 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
                              {"params": no_decay, "weight_decay": 0.0}], lr=cfg.lr, betas=(0.9, 0.95),
                             fused=fused)
 
-    gb = GradBuckets(list(w.parameters()), bucket_mb=cfg.bucket_mb)
+    gb = GradBuckets(list(w.parameters()), bucket_mb=cfg.bucket_mb) if ddp else None
 
     def lr_at(step: int) -> float:
         if step < cfg.warmup:
@@ -232,9 +234,13 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
             hs = h.reshape(-1, h.shape[-1])[sel]
             logits = hs @ w.embed[:v_dec].t()
             loss = F.cross_entropy(logits.float(), labels.view(-1)[sel])
-        gb.zero_grad()
-        loss.backward()  # bucket all-reduces start as gradients land
-        gb.finish()
+        if gb is not None:
+            gb.zero_grad()
+            loss.backward()  # bucket all-reduces start as gradients land
+            gb.finish()
+        else:
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
         torch.nn.utils.clip_grad_norm_(w.parameters(), 1.0)
         opt.step()
         if cfg.log_every and rank == 0 and (step % cfg.log_every == 0 or step == cfg.steps - 1):

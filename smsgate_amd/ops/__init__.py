@@ -101,7 +101,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_set_prefill_split.restype = None
     fsm_t = [_vp, _ip, _ip, _ip, _ip, _ip, _c_int]  # masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E
     lib.sg_spec_plan.argtypes = fsm_t + [_c_int, _c_int, _ip, _ip] + [_c_int] * 5 + [_ip] * 6 + [_c_int] + \
-        [_ip, _ip, _c_int, _vp] + [_ip] * 7 + [_vp]
+        [_ip, _ip, _c_int, _vp] + [_ip] * 8 + [_vp]
     lib.sg_spec_plan.restype = _c_int
     lib.sg_spec_verify.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                    _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _vp]
@@ -462,7 +462,7 @@ def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: in
               slot: torch.Tensor, done: torch.Tensor, out_buf: torch.Tensor, out_len: torch.Tensor,
               body_buf: torch.Tensor, body_len: torch.Tensor, delim: torch.Tensor, draft_buf: torch.Tensor,
               x_tok: torch.Tensor, x_pos: torch.Tensor, x_slot: torch.Tensor, x_done: torch.Tensor,
-              row_start: torch.Tensor, row_nd: torch.Tensor) -> None:
+              row_start: torch.Tensor, row_nd: torch.Tensor, meta: torch.Tensor) -> None:
     """Prompt-lookup drafts for ``B = tok_buf.numel()`` rows packed into ``T_cap``
     pseudo-rows (``csrc/spec_kernels.hip``); drafts follow the schema FSM from each
     row's ``state`` and ``x_state`` gets every pseudo-row's state.  All int32
@@ -487,6 +487,7 @@ def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: in
     _req(body_len, torch.int32, "body_len")
     _req(delim, torch.uint8, "delim")
     _req(draft_buf, torch.int32, "draft_buf")
+    _req(meta, torch.int32, "meta")
     if not (0 <= K <= SPEC_MAX_K) or T_cap < B or draft_buf.numel() < B * SPEC_MAX_K or body_len.numel() != S1:
         raise ValueError("spec_plan: bad K / T_cap / draft_buf / body_len")
     if not (0 <= scratch_slot < S1) or out_buf.shape[0] < B:
@@ -495,7 +496,7 @@ def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: in
         *_fsm_args(fsm), fsm.done_state, fsm.vocab, _p(state), _p(x_state),
         B, K, T_cap, sep_token, scratch_slot, _p(tok_buf), _p(pos), _p(slot), _p(done), _p(out_buf), _p(out_len),
         out_buf.shape[1], _p(body_buf), _p(body_len), LB, _p(delim), _p(draft_buf), _p(x_tok), _p(x_pos),
-        _p(x_slot), _p(x_done), _p(row_start), _p(row_nd), _stream()), "spec_plan")
+        _p(x_slot), _p(x_done), _p(row_start), _p(row_nd), _p(meta), _stream()), "spec_plan")
 
 
 def spec_verify(logits: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.Tensor, out_buf: torch.Tensor,

@@ -67,61 +67,64 @@ static __device__ __forceinline__ int key_token(unsigned long long key, int sep_
 }
 
 // ---------------------------------------------------------------------------
-// plan: grid = 1 block of SPEC_THREADS; each thread owns RPT consecutive rows.
+// plan, three launches (one thread per row; the scan is the only single-block part):
+//   draft  — per row: prompt-lookup drafts (FSM-checked), unclamped count
+//   scan   — one block: exclusive scan of the counts, clamp to the draft budget
+//   fill   — per row: write the pseudo-rows; then the unused tail
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
-    FsmTables fsm, const int* __restrict__ state, int* __restrict__ x_state,
-    int B, int K, int T_cap, int sep_token, int scratch_slot,
-    const int* __restrict__ tok_buf, const int* __restrict__ pos, const int* __restrict__ slot,
-    const int* __restrict__ done, const int* __restrict__ out_buf, const int* __restrict__ out_len, int max_out,
-    const int* __restrict__ body_buf, const int* __restrict__ body_len, int LB, const uint8_t* __restrict__ delim,
-    int* __restrict__ draft_buf, int* __restrict__ x_tok, int* __restrict__ x_pos, int* __restrict__ x_slot,
-    int* __restrict__ x_done, int* __restrict__ row_start, int* __restrict__ row_nd) {
+__global__ void __launch_bounds__(256) spec_draft_kernel(
+    FsmTables fsm, const int* __restrict__ state, int B, int K, int sep_token, const int* __restrict__ tok_buf,
+    const int* __restrict__ slot, const int* __restrict__ done, const int* __restrict__ out_buf,
+    const int* __restrict__ out_len, int max_out, const int* __restrict__ body_buf, const int* __restrict__ body_len,
+    int LB, const uint8_t* __restrict__ delim, int* __restrict__ draft_buf, int* __restrict__ row_nd) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  int n = 0;
+  const int t = tok_buf[r];
+  if (!done[r] && t != sep_token) {
+    const int len = out_len[r];
+    int prev = len >= 2 ? out_buf[(size_t)r * max_out + len - 2] : -1;
+    if (prev == sep_token) prev = -1;
+    const int sl = slot[r];
+    const int* body = body_buf + (size_t)sl * LB;
+    const int bl = body_len[sl];
+    int j = -1;
+    if (prev >= 0)
+      for (int q = 1; q < bl; ++q)
+        if (body[q] == t && body[q - 1] == prev) { j = q; break; }
+    if (j < 0)
+      for (int q = 0; q < bl; ++q)
+        if (body[q] == t) { j = q; break; }
+    if (j >= 0) {
+      // walk the schema FSM along the draft: a token the FSM forbids can never be
+      // accepted (the verify arg-max is masked), so the draft stops before it
+      int s = state[r];
+      for (int i = 0; i < K; ++i) {
+        const int q = j + 1 + i;
+        if (q >= bl) break;
+        const int x = delim[body[q]] ? sep_token : body[q];
+        if (!fsm_allows(fsm, s, x)) break;
+        const int ns = fsm_next(fsm, s, x);
+        if (ns < 0) break;
+        draft_buf[r * SPEC_MAX_K + n++] = x;
+        s = ns;
+        if (x == sep_token || ns == fsm.done_state) break;
+      }
+    }
+  }
+  row_nd[r] = n;
+}
+
+// one block: row_start[r] = r + (clamped drafts of rows < r); row_nd clamped; meta[0] = rows used
+__global__ void __launch_bounds__(SPEC_THREADS) spec_scan_kernel(int B, int T_cap, int* __restrict__ row_start,
+                                                                 int* __restrict__ row_nd, int* __restrict__ meta) {
   __shared__ int wsum[SPEC_THREADS / 64];
   __shared__ int s_total;
   const int tid = threadIdx.x;
   const int RPT = (B + SPEC_THREADS - 1) / SPEC_THREADS;
   const int r0 = tid * RPT, r1 = min(B, r0 + RPT);
-  // 1) drafts of my rows
   int mine = 0;
-  for (int r = r0; r < r1; ++r) {
-    int n = 0;
-    const int t = tok_buf[r];
-    if (!done[r] && t != sep_token) {
-      const int len = out_len[r];
-      int prev = len >= 2 ? out_buf[(size_t)r * max_out + len - 2] : -1;
-      if (prev == sep_token) prev = -1;
-      const int sl = slot[r];
-      const int* body = body_buf + (size_t)sl * LB;
-      const int bl = body_len[sl];
-      int j = -1;
-      if (prev >= 0)
-        for (int q = 1; q < bl; ++q)
-          if (body[q] == t && body[q - 1] == prev) { j = q; break; }
-      if (j < 0)
-        for (int q = 0; q < bl; ++q)
-          if (body[q] == t) { j = q; break; }
-      if (j >= 0) {
-        // walk the schema FSM along the draft: a token the FSM forbids can never be
-        // accepted (the verify arg-max is masked), so the draft stops before it
-        int s = state[r];
-        for (int i = 0; i < K; ++i) {
-          const int q = j + 1 + i;
-          if (q >= bl) break;
-          const int x = delim[body[q]] ? sep_token : body[q];
-          if (!fsm_allows(fsm, s, x)) break;
-          const int ns = fsm_next(fsm, s, x);
-          if (ns < 0) break;
-          draft_buf[r * SPEC_MAX_K + n++] = x;
-          s = ns;
-          if (x == sep_token || ns == fsm.done_state) break;
-        }
-      }
-    }
-    row_nd[r] = n;  // unclamped for now
-    mine += n;
-  }
-  // 2) block exclusive scan of the per-thread draft totals
+  for (int r = r0; r < r1; ++r) mine += row_nd[r];
   const int lane = tid & 63, wid = tid >> 6;
   int incl = mine;
 #pragma unroll
@@ -143,16 +146,25 @@ __global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
   __syncthreads();
   int dstart = wsum[wid] + incl - mine;  // drafts of all rows before my first row
   const int D_cap = T_cap - B;
-  // 3) clamp to the budget and write my rows' pseudo-rows
   for (int r = r0; r < r1; ++r) {
     const int n = row_nd[r];
-    const int nc = max(0, min(n, D_cap - dstart));
-    const int st = r + min(dstart, D_cap);
+    row_start[r] = r + min(dstart, D_cap);
+    row_nd[r] = max(0, min(n, D_cap - dstart));
     dstart += n;
-    row_start[r] = st;
-    row_nd[r] = nc;
-    const int p = pos[r], sl = slot[r];
-    const int dn = done[r];
+  }
+  if (tid == 0) meta[0] = B + min(s_total, D_cap);
+}
+
+__global__ void __launch_bounds__(256) spec_fill_kernel(
+    FsmTables fsm, const int* __restrict__ state, int B, int T_cap, int scratch_slot, const int* __restrict__ tok_buf,
+    const int* __restrict__ pos, const int* __restrict__ slot, const int* __restrict__ done,
+    const int* __restrict__ draft_buf, const int* __restrict__ row_start, const int* __restrict__ row_nd,
+    const int* __restrict__ meta, int* __restrict__ x_tok, int* __restrict__ x_pos, int* __restrict__ x_slot,
+    int* __restrict__ x_done, int* __restrict__ x_state) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < B) {
+    const int r = g, st = row_start[r], nc = row_nd[r];
+    const int p = pos[r], sl = slot[r], dn = done[r];
     int s = state[r];
     x_tok[st] = tok_buf[r];
     x_pos[st] = p;
@@ -169,9 +181,9 @@ __global__ void __launch_bounds__(SPEC_THREADS) spec_plan_kernel(
       x_state[st + 1 + i] = s;  // the state the row is in IF drafts 0..i are accepted
     }
   }
-  // 4) unused tail: scratch slot, position 0, skipped by attention
-  const int used = B + min(s_total, D_cap);
-  for (int i = used + tid; i < T_cap; i += SPEC_THREADS) {
+  // unused tail: scratch slot, position 0, skipped by attention
+  const int used = meta[0];
+  for (int i = used + g; i < T_cap; i += gridDim.x * blockDim.x) {
     x_tok[i] = 0;
     x_pos[i] = 0;
     x_slot[i] = scratch_slot;
@@ -346,13 +358,15 @@ int sg_spec_plan(const void* masks, const int* state_mask, const int* next_sep, 
                  int* x_state, int B, int K, int T_cap, int sep_token, int scratch_slot, const int* tok_buf, const int* pos,
                  const int* slot, const int* done, const int* out_buf, const int* out_len, int max_out,
                  const int* body_buf, const int* body_len, int LB, const void* delim, int* draft_buf, int* x_tok,
-                 int* x_pos, int* x_slot, int* x_done, int* row_start, int* row_nd, hipStream_t stream) {
+                 int* x_pos, int* x_slot, int* x_done, int* row_start, int* row_nd, int* meta, hipStream_t stream) {
   if (K < 0 || K > SPEC_MAX_K || T_cap < B || B <= 0) return -1;
   const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
-  hipLaunchKernelGGL(spec_plan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, f, state, x_state, B, K, T_cap,
-                     sep_token, scratch_slot,
-                     tok_buf, pos, slot, done, out_buf, out_len, max_out, body_buf, body_len, LB,
-                     (const uint8_t*)delim, draft_buf, x_tok, x_pos, x_slot, x_done, row_start, row_nd);
+  const int grid = (B + 255) / 256;
+  hipLaunchKernelGGL(spec_draft_kernel, dim3(grid), dim3(256), 0, stream, f, state, B, K, sep_token, tok_buf, slot, done,
+                     out_buf, out_len, max_out, body_buf, body_len, LB, (const uint8_t*)delim, draft_buf, row_nd);
+  hipLaunchKernelGGL(spec_scan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, B, T_cap, row_start, row_nd, meta);
+  hipLaunchKernelGGL(spec_fill_kernel, dim3(grid), dim3(256), 0, stream, f, state, B, T_cap, scratch_slot, tok_buf, pos,
+                     slot, done, draft_buf, row_start, row_nd, meta, x_tok, x_pos, x_slot, x_done, x_state);
   return (int)hipGetLastError();
 }
 

@@ -453,6 +453,7 @@ class ExtractionEngine:
         self.row_start = torch.zeros(S, **i32)
         self.row_nd = torch.zeros(S, **i32)
         self.spec_acc = torch.zeros(S, **i32)
+        self.spec_meta = torch.zeros(S, **i32)  # [r0] = pseudo-rows used by the part starting at row r0
         self.spec_counts = torch.zeros(2, dtype=torch.int64, device=dev)  # [tokens emitted, live row-steps]
 
     def _tcap(self, B: int) -> int:
@@ -477,7 +478,7 @@ class ExtractionEngine:
         ops.spec_plan(self.fsm, self.state[r0:r1], xst, self.cfg.spec_k, T, self.tok.sep, self.scratch_slot, tok,
                       pos, slot, done,
                       self.out_buf[r0:r1], self.out_len[r0:r1], self.body_buf, self.body_len, self.spec_delim,
-                      self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd)
+                      self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd, self.spec_meta[r0:r0 + 1])
         x = F.embedding(xt.long(), self.w.embed)
         impl = self.cfg.decode_attn_small if T <= self.cfg.decode_attn_small_rows else self.cfg.decode_attn
         scratch = None

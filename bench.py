@@ -98,7 +98,7 @@ def _args(argv=None):
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--spec-k", type=int, default=4, help="speculative decoding: drafts per row per step (0 = off)")
-    p.add_argument("--spec-frac", type=float, default=2.0, help="draft budget per step, x decode rows")
+    p.add_argument("--spec-frac", type=float, default=1.25, help="draft budget per step, x decode rows")
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
     p.add_argument("--cpu-echo-engine", action="store_true",
                    help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")

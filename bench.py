@@ -59,7 +59,7 @@ def _args(argv=None):
     p.add_argument("--model", default="smollm-135m")
     p.add_argument("--weights", default="train",
                    help="train (in-run, untimed; default) | random (worst case) | path to a safetensors checkpoint")
-    p.add_argument("--train-steps", type=int, default=1200)
+    p.add_argument("--train-steps", type=int, default=2000)
     p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
     p.add_argument("--train-lr", type=float, default=1e-3)
     p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",

@@ -72,8 +72,8 @@ def _args(argv=None):
     p.add_argument("--admit-frac", type=float, default=0.25)
     p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)
-    p.add_argument("--bus-shards", type=int, default=2,
-                   help="brokers per node, sharded by subject (sms.raw | the parser's outputs)")
+    p.add_argument("--bus-shards", type=int, default=3,
+                   help="brokers per node, sharded by subject (sms.raw | sms.parsed | sms.processing + the rest)")
     p.add_argument("--bus", default="busd", choices=["memory", "busd"],
                    help="busd: ONE shared native broker per node (journal on) carries sms.raw / sms.parsed for every "
                         "GPU's parser and writer processes (one competing group each); memory: an in-process bus per "
@@ -274,7 +274,7 @@ def acquire_weights(args, device: str, rank: int, world: int):
     # one trainer per node: local rank 0 trains (the same run as on one GPU, so every N
     # serves identical weights) and publishes the file; the other ranks load it
     tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
-                     log_every=0, data_parallel=False)
+                     log_every=200, data_parallel=False)
     h = hashlib.sha256(repr((tc, open(ASSET, "rb").read())).encode(errors="ignore")).hexdigest()[:16]
     cache = args.weights_cache or os.path.join(tempfile.gettempdir(), f"smsgate-bench-w-{os.getpid()}")
     path = os.path.join(cache, f"{args.model}-{h}.safetensors")
@@ -293,7 +293,8 @@ def acquire_weights(args, device: str, rank: int, world: int):
             time.sleep(0.5)
         return ExtractorWeights.load(path, CONFIGS[args.model], device=torch.device(device)), prov
     t0 = time.perf_counter()
-    w = train_extractor(tc, device=device, log=lambda s: None)
+    # progress on stderr (stdout carries only the result line)
+    w = train_extractor(tc, device=device, log=lambda s: print(f"[bench] train {s}", file=sys.stderr, flush=True))
     prov["train_s"] = round(time.perf_counter() - t0, 1)
     os.makedirs(cache, exist_ok=True)
     tmp = path + f".{os.getpid()}.tmp"

@@ -6,9 +6,11 @@ its journal on (profiles/r02_busd_capacity.jsonl), while a node of 8 GPUs needs
 about 3 publishes and 2 deliveries per SMS at ~20 k SMS/s per GPU.  Sharding by
 subject keeps every subject's semantics intact (one stream per broker, one
 competing consumer group per durable, a durable lives where its subject lives)
-and splits the broker work: ``sms.raw`` (ingest → parser) on shard 0, the
-parser's outputs (``sms.parsed`` / ``sms.processing`` / ``sms.failed`` /
-``sms.categorized``) on shard 1, and so on for more shards.
+and splits the broker work: ``sms.raw`` (ingest → parser) on shard 0; with two
+shards the parser's outputs (``sms.parsed`` / ``sms.processing`` / ``sms.failed``
+/ ``sms.categorized``) on shard 1; with three (the 8-GPU deployment) one message
+per SMS lands on each shard: sms.parsed alone on 1, sms.processing (and the
+low-rate subjects) on 2.
 
 DSN: ``sharded+unix:///run/raw.sock,unix:///run/out.sock`` (any member DSNs
 :func:`smsgate_amd.bus.connect` accepts, comma separated).
@@ -20,6 +22,8 @@ import zlib
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from .base import (
+    SUBJECT_PARSED,
+    SUBJECT_PROCESSING,
     SUBJECT_RAW,
     Bus,
     BusError,
@@ -34,14 +38,15 @@ __all__ = ["ShardedBus", "shard_of"]
 
 
 def shard_of(subject: str, n: int) -> int:
-    """Shard owning ``subject``: ingest (sms.raw) on 0, everything else spread over the rest."""
-    if n <= 1:
+    """Shard owning ``subject``: ingest (sms.raw) on 0; with 3+ shards sms.parsed
+    alone on 1, sms.processing on 2 and the rest spread over 2 .. n-1."""
+    if n <= 1 or subject == SUBJECT_RAW:
         return 0
-    if subject == SUBJECT_RAW:
-        return 0
-    if n == 2:
+    if n == 2 or subject == SUBJECT_PARSED:
         return 1
-    return 1 + zlib.crc32(subject.encode()) % (n - 1)
+    if subject == SUBJECT_PROCESSING:
+        return 2
+    return 2 + zlib.crc32(subject.encode()) % (n - 2)
 
 
 class ShardedBus(Bus):

@@ -82,6 +82,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_attn_decode_grouped_pf.argtypes = lib.sg_attn_decode.argtypes
     lib.sg_attn_decode_grouped_pf.restype = _c_int
     lib.sg_attn_decode_split.argtypes = lib.sg_attn_decode.argtypes[:-1] + [_c_int, _vp]
+    lib.sg_attn_spec.argtypes = [_vp, _ip, _ip, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp, _c_int,
+                                 _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _vp]
+    lib.sg_attn_spec.restype = _c_int
     lib.sg_attn_decode_split.restype = _c_int
     lib.sg_attn_decode_cascade.restype = _c_int
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
@@ -427,6 +430,31 @@ def attn_decode(q: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, k_cache:
           "grouped6": lib.sg_attn_decode_grouped6, "grouped_h": lib.sg_attn_decode_grouped_h}[impl]
     _check(fn(_p(q), _p(pos), _p(slot), _p(done), _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B,
               nh, nkv, D, Lmax, scale, _stream()), f"attn_decode[{impl}]")
+    return out
+
+
+def attn_spec(q: torch.Tensor, row_start: torch.Tensor, row_nd: torch.Tensor, x_pos: torch.Tensor,
+              x_slot: torch.Tensor, x_done: torch.Tensor, k_cache: torch.Tensor, vt_cache: torch.Tensor,
+              pk: torch.Tensor, pvt: torch.Tensor, P0: int, out: torch.Tensor, scale: float, max_q: int) -> torch.Tensor:
+    """Decode attention of speculative pseudo-rows, one wave per (row, kv head).
+
+    ``q`` / ``out`` = ``[T, nh, D]`` pseudo-rows as packed by :func:`spec_plan`: row
+    ``r`` owns ``row_start[r] .. row_start[r] + row_nd[r]``, all on the row's KV slot,
+    pseudo-row ``i`` attending to the prefix plus own keys ``[0, pos + i]``.  The row's
+    key tiles are read once for all its pseudo-rows; per pseudo-row the result is
+    bit-identical to ``attn_decode(impl="grouped")``.  Needs ``max_q * nh / nkv <= 16``
+    (``max_q`` = 1 + the engine's spec_k)."""
+    T, nh, D = q.shape
+    S, nkv, Lmax, _ = k_cache.shape
+    P0pad = pk.shape[1]
+    B = row_start.numel()
+    assert row_nd.numel() == B and x_pos.numel() >= T and x_slot.numel() >= T and x_done.numel() >= T
+    assert out.shape[0] >= T and vt_cache.shape == vt_shape(S, nkv, D, Lmax)
+    if max_q * (nh // nkv) > 16:
+        raise ValueError(f"attn_spec: {max_q} pseudo-rows x {nh // nkv} heads do not fit one wave's 16 columns")
+    _check(load_library().sg_attn_spec(_p(q), _p(row_start), _p(row_nd), _p(x_pos), _p(x_slot), _p(x_done),
+                                       _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D,
+                                       Lmax, scale, max_q, _stream()), "attn_spec")
     return out
 
 

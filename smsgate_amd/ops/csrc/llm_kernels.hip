@@ -1305,6 +1305,72 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Speculative-verify attention: one wave = ONE row's pseudo-rows (its current
+// token + nd <= 16/G - 1 drafts, contiguous at row_start[r]) of one kv head.
+// MFMA column c <-> (pseudo-row i = c / G, query head g = c % G).  All pseudo-rows
+// of a row read the same slot, pseudo-row i seeing keys [0, pos + i]: the row's
+// key tiles are loaded and multiplied ONCE for every draft (attn_grouped_kernel
+// walks them once per pseudo-row), each column masked at its own length.  A
+// column's arithmetic is the grouped kernel's (same tiles in the same order; the
+// extra tiles past its length are exact no-ops), so outputs are bit-identical.
+// grid = (rows, nkv), one wave; rows whose current pseudo-row is done are skipped.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) attn_spec_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ row_start, const int* __restrict__ row_nd,
+    const int* __restrict__ x_pos, const int* __restrict__ x_slot, const int* __restrict__ x_done,
+    const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache, const uint16_t* __restrict__ pk,
+    const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out, int nh, int nkv, int Lmax,
+    float scale_log2) {
+  constexpr int D = 64;
+  const int r = blockIdx.x, kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
+  const int G = nh / nkv, SPW = 16 / G;
+  const int st = row_start[r];
+  if (x_done[st]) return;
+  const int nq = min(row_nd[r] + 1, SPW);  // the host guarantees 1 + spec_k <= 16 / G
+  const int p = x_pos[st], sl = x_slot[st];
+  const int i = r16 / G, g = r16 % G;
+  const bool col_valid = i < nq;
+  const size_t qrow = (size_t)(st + (col_valid ? i : 0)) * nh + kh * G + g;
+  bf16x8 qb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);
+    if (!col_valid) v = make_uint4(0, 0, 0, 0);
+    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+  for (int kt = 0; kt < P0; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
+    st_tile(qb, kc, vc, kt, P0, g4, scale_log2, m, lsum, o);
+  }
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const int own_max = p + nq, own = p + i + 1;  // per-lane length (invalid columns: masked by q = 0 and no store)
+  for (int kt = 0; kt < own_max; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own_max, kc, vc);
+    st_tile(qb, kc, vc, kt, own, g4, scale_log2, m, lsum, o, col_valid);
+  }
+  if (col_valid) {
+    const float inv = 1.f / lsum;
+    uint16_t* orow = out + qrow * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[n][0] * inv) | ((uint32_t)f2bf(o[n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[n][2] * inv) | ((uint32_t)f2bf(o[n][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Grouped decode attention with a one-tile register prefetch: the same work as
 // attn_grouped_kernel, but the wave walks ONE flattened stream of 32-key tiles
 // (shared prefix, then each live sequence's own keys) and issues the loads of
@@ -1697,6 +1763,20 @@ int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const
   hipLaunchKernelGGL(attn_grouped_kernel<1>, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  return (int)hipGetLastError();
+}
+
+// Speculative-verify attention over B rows' pseudo-rows (row_start / row_nd from sg_spec_plan).
+int sg_attn_spec(const void* q, const int* row_start, const int* row_nd, const int* x_pos, const int* x_slot,
+                 const int* x_done, const void* k_cache, const void* vt_cache, const void* pk, const void* pvt, int P0,
+                 int P0pad, void* out, int B, int nh, int nkv, int D, int Lmax, float scale, int max_q,
+                 hipStream_t stream) {
+  if (D != 64 || nh % nkv || nh / nkv > 16 || max_q * (nh / nkv) > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad)
+    return -1;
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(attn_spec_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, row_start, row_nd, x_pos,
+                     x_slot, x_done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
   return (int)hipGetLastError();
 }
 

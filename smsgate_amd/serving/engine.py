@@ -99,6 +99,9 @@ class EngineConfig:
     spec_k: int = 4
     spec_draft_frac: float = 1.25  # A/B 1.0 / 1.25 / 1.5 / 2.0: 22.5 / 23.2 / 23.1 / 21.5 k msgs/s
     spec_max_rows: int = 1 << 30  # buckets above this decode one token per row
+    # verify attention: one wave per row reads the row's keys once for all its drafts
+    # (ops.attn_spec; needs (1 + spec_k) * heads / kv_heads <= 16), else the decode kernel
+    spec_attn: bool = True
 
 
 @dataclass
@@ -492,9 +495,15 @@ class ExtractionEngine:
         def vc(i):
             return self.vt_cache[i]
 
-        def attn(i, q, out):
-            ops.attn_decode(q, xp, xs, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
-                            done=xd, impl=impl, scratch=scratch)
+        max_q = 1 + self.cfg.spec_k
+        if self.cfg.spec_attn and max_q * (self.mc.heads // self.mc.kv_heads) <= 16:
+            def attn(i, q, out):
+                ops.attn_spec(q, rs, nd, xp, xs, xd, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
+                              self.scale, max_q)
+        else:
+            def attn(i, q, out):
+                ops.attn_decode(q, xp, xs, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out, self.scale,
+                                done=xd, impl=impl, scratch=scratch)
 
         h = self._forward(x, pos_tok=xp, slot_tok=xs, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0, hook=hook)
         if sample and self.argmax:

@@ -8,6 +8,8 @@ def test_shard_map():
     assert shard_of(SUBJECT_RAW, 2) == 0 and shard_of(SUBJECT_PARSED, 2) == 1 == shard_of(SUBJECT_FAILED, 2)
     assert {shard_of(s, 4) for s in (SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_FAILED)} <= {1, 2, 3}
     assert shard_of(SUBJECT_PARSED, 1) == 0
+    # three shards: one per-SMS message on each broker
+    assert [shard_of(s, 3) for s in (SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_FAILED)] == [0, 1, 2, 2]
 
 
 def test_publish_subscribe_ack_across_shards(arun):

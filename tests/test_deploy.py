@@ -22,5 +22,5 @@ def test_compose_is_an_8_gpu_node():
     assert {p["command"][p["command"].index("--group") + 1] for p in parsers} == {"parser_worker"}
     assert {p["command"][p["command"].index("--engine") + 1] for p in parsers} == socks
     dsn = parsers[0]["environment"]["NATS_DSN"]
-    assert dsn.startswith("sharded+") and dsn.count(",") == 1
-    assert all("--native" in svc[b]["command"] for b in ("broker-raw", "broker-out"))
+    assert dsn.startswith("sharded+") and dsn.count(",") == 2
+    assert all("--native" in svc[b]["command"] for b in ("broker-raw", "broker-parsed", "broker-proc"))

@@ -318,3 +318,60 @@ def test_gemm_argmax_matches_logits_path(cfg, M):
         s = int(states_h[b])
         if allowed[s].any():
             assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())
+
+
+@pytest.mark.parametrize("P0", [0, 75])
+def test_attn_spec_matches_grouped_bitwise(P0):
+    """attn_spec (one wave per row, all its drafts) == the grouped decode kernel on
+    the same pseudo-rows, bit for bit, and == an fp32 reference; done rows untouched."""
+    nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224
+    P0pad = (P0 + 31) // 32 * 32
+    kc = _bf(S, nkv, Lmax, D, seed=20)
+    vrows = _bf(S, nkv, Lmax, D, seed=21)
+    vt = ops.rows_to_vt(vrows)
+    pk = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
+    pvrows = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
+    if P0:
+        pk[:, :P0] = _bf(nkv, P0, D, seed=22)
+        pvrows[:, :P0] = _bf(nkv, P0, D, seed=23)
+    pvt = ops.rows_to_vt(pvrows)
+    # rows: (pos, slot, drafts, done); pos + drafts < Lmax
+    rows = [(0, 3, 4, 0), (14, 0, 2, 0), (30, 7, 4, 1), (31, 1, 0, 0), (100, 2, 3, 0), (219, 5, 4, 0), (47, 6, 1, 0)]
+    xp, xs, xd, rs, nd = [], [], [], [], []
+    for p, sl, n, dn in rows:
+        rs.append(len(xp))
+        nd.append(n)
+        for i in range(n + 1):
+            xp.append(p + i)
+            xs.append(sl)
+            xd.append(dn if i == 0 else 0)
+    T = len(xp) + 5  # unused tail pseudo-rows: done
+    xp += [0] * 5
+    xs += [0] * 5
+    xd += [1] * 5
+    i32 = dict(dtype=torch.int32, device=DEV)
+    xp, xs, xd, rs, nd = (torch.tensor(v, **i32) for v in (xp, xs, xd, rs, nd))
+    # the grouped kernel skips only the row's FIRST pseudo-row on done; mark its drafts done too
+    xd_g = xd.clone()
+    for r, (p, sl, n, dn) in enumerate(rows):
+        if dn:
+            xd_g[int(rs[r]):int(rs[r]) + n + 1] = 1
+    q = _bf(T, nh, D, seed=24)
+    scale = 1 / math.sqrt(D)
+    out_s = torch.full((T, nh * D), 7.0, dtype=torch.bfloat16, device=DEV)
+    out_g = out_s.clone()
+    ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=5)
+    ops.attn_decode(q, xp, xs, kc, vt, pk, pvt, P0, out_g, scale, done=xd_g, impl="grouped")
+    torch.cuda.synchronize()
+    assert torch.equal(out_s, out_g)
+    for t in range(T):
+        if int(xd_g[t]):
+            assert torch.all(out_s[t] == 7.0)
+            continue
+        p, r = int(xp[t]), int(xs[t])
+        ref = _ref_seq_attention(q[t:t + 1].float(), kc[r, :, :p + 1].permute(1, 0, 2).float(),
+                                 vrows[r, :, :p + 1].permute(1, 0, 2).float(), pk[:, :P0].permute(1, 0, 2).float(),
+                                 pvrows[:, :P0].permute(1, 0, 2).float(), P0, [p], scale)
+        torch.testing.assert_close(out_s[t].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)
+    with pytest.raises(ValueError):
+        ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=6)

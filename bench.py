@@ -97,6 +97,7 @@ def _args(argv=None):
                    help="waves sharing each prefill attention tile's keys")
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
+    p.add_argument("--spec-policy", type=int, default=0, help="draft policy (EngineConfig.spec_policy)")
     p.add_argument("--spec-k", type=int, default=4, help="speculative decoding: drafts per row per step (0 = off)")
     p.add_argument("--spec-frac", type=float, default=1.25, help="draft budget per step, x decode rows")
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
@@ -163,7 +164,8 @@ def run_replica(args, rank: int, world: int, local: int):
                               split_parts=args.split_parts,
                               split_prefill=args.split_prefill, decode_attn=args.decode_attn,
                               prefill_key_split=args.prefill_key_split,
-                              spec_k=args.spec_k, spec_draft_frac=args.spec_frac, spec_max_rows=args.spec_max_rows,
+                              spec_k=args.spec_k, spec_policy=args.spec_policy, spec_draft_frac=args.spec_frac,
+                              spec_max_rows=args.spec_max_rows,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
     if not echo and args.eval_n and rank == 0:

@@ -42,10 +42,12 @@ def main(argv=None) -> int:
         for name, args in arms:
             cmd = ["timeout", "-k", "10", str(a.timeout), sys.executable, "-u", a.script, *shlex.split(a.common), *args]
             t0 = time.time()
-            r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+            # the run's stderr streams into a log next to --out (progress stays visible)
+            with open(a.out + ".stderr.log", "a") as err:
+                r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=err, text=True)
             line = next((x for x in reversed(r.stdout.splitlines()) if x.startswith("{")), None)
             if r.returncode != 0 or line is None:
-                print(f"[ab] {name} run {rep} failed (rc {r.returncode}):\n{r.stderr[-2000:]}", flush=True)
+                print(f"[ab] {name} run {rep} failed (rc {r.returncode}); stderr in {a.out}.stderr.log", flush=True)
                 return r.returncode or 1
             d = json.loads(line)
             d.update(arm=name, repeat=rep, wall_s=round(time.time() - t0, 1), args=args)

@@ -32,6 +32,7 @@ __all__ = [
     "attn_decode",
     "fsm_sample",
     "spec_plan",
+    "attn_spec",
     "spec_verify",
     "spec_verify_keys",
     "fsm_commit",
@@ -104,7 +105,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_set_prefill_split.restype = None
     fsm_t = [_vp, _ip, _ip, _ip, _ip, _ip, _c_int]  # masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E
     lib.sg_spec_plan.argtypes = fsm_t + [_c_int, _c_int, _ip, _ip] + [_c_int] * 5 + [_ip] * 6 + [_c_int] + \
-        [_ip, _ip, _c_int, _vp] + [_ip] * 8 + [_vp]
+        [_ip, _ip, _c_int, _vp, _ip, _c_int] + [_ip] * 8 + [_vp]
     lib.sg_spec_plan.restype = _c_int
     lib.sg_spec_verify.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                    _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _vp]
@@ -442,16 +443,17 @@ def attn_spec(q: torch.Tensor, row_start: torch.Tensor, row_nd: torch.Tensor, x_
     ``r`` owns ``row_start[r] .. row_start[r] + row_nd[r]``, all on the row's KV slot,
     pseudo-row ``i`` attending to the prefix plus own keys ``[0, pos + i]``.  The row's
     key tiles are read once for all its pseudo-rows; per pseudo-row the result is
-    bit-identical to ``attn_decode(impl="grouped")``.  Needs ``max_q * nh / nkv <= 16``
-    (``max_q`` = 1 + the engine's spec_k)."""
+    bit-identical to ``attn_decode(impl="grouped")``.  Needs ``max_q * nh / nkv <= 32``
+    (``max_q`` = 1 + the engine's spec_k; above 16 columns a wave runs two MFMA
+    column blocks over the same key tiles)."""
     T, nh, D = q.shape
     S, nkv, Lmax, _ = k_cache.shape
     P0pad = pk.shape[1]
     B = row_start.numel()
     assert row_nd.numel() == B and x_pos.numel() >= T and x_slot.numel() >= T and x_done.numel() >= T
     assert out.shape[0] >= T and vt_cache.shape == vt_shape(S, nkv, D, Lmax)
-    if max_q * (nh // nkv) > 16:
-        raise ValueError(f"attn_spec: {max_q} pseudo-rows x {nh // nkv} heads do not fit one wave's 16 columns")
+    if not 1 <= max_q or max_q * (nh // nkv) > 32:
+        raise ValueError(f"attn_spec: {max_q} pseudo-rows x {nh // nkv} heads do not fit one wave's 32 columns")
     _check(load_library().sg_attn_spec(_p(q), _p(row_start), _p(row_nd), _p(x_pos), _p(x_slot), _p(x_done),
                                        _p(k_cache), _p(vt_cache), _p(pk), _p(pvt), P0, P0pad, _p(out), B, nh, nkv, D,
                                        Lmax, scale, max_q, _stream()), "attn_spec")
@@ -490,11 +492,13 @@ def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: in
               slot: torch.Tensor, done: torch.Tensor, out_buf: torch.Tensor, out_len: torch.Tensor,
               body_buf: torch.Tensor, body_len: torch.Tensor, delim: torch.Tensor, draft_buf: torch.Tensor,
               x_tok: torch.Tensor, x_pos: torch.Tensor, x_slot: torch.Tensor, x_done: torch.Tensor,
-              row_start: torch.Tensor, row_nd: torch.Tensor, meta: torch.Tensor) -> None:
+              row_start: torch.Tensor, row_nd: torch.Tensor, meta: torch.Tensor, policy: int = 1) -> None:
     """Prompt-lookup drafts for ``B = tok_buf.numel()`` rows packed into ``T_cap``
     pseudo-rows (``csrc/spec_kernels.hip``); drafts follow the schema FSM from each
     row's ``state`` and ``x_state`` gets every pseudo-row's state.  All int32
-    except ``delim`` (uint8 [V])."""
+    except ``delim`` (uint8 [V]).  ``policy`` 0: copy until the first <sep>; 1: also
+    schema-forced tokens, implicit value ends, across <sep> and from field starts
+    (spec_draft_kernel)."""
     B = tok_buf.numel()
     _req(state, torch.int32, "state")
     _req(x_state, torch.int32, "x_state")
@@ -523,7 +527,8 @@ def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: in
     _check(load_library().sg_spec_plan(
         *_fsm_args(fsm), fsm.done_state, fsm.vocab, _p(state), _p(x_state),
         B, K, T_cap, sep_token, scratch_slot, _p(tok_buf), _p(pos), _p(slot), _p(done), _p(out_buf), _p(out_len),
-        out_buf.shape[1], _p(body_buf), _p(body_len), LB, _p(delim), _p(draft_buf), _p(x_tok), _p(x_pos),
+        out_buf.shape[1], _p(body_buf), _p(body_len), LB, _p(delim), _p(fsm.forced_t), int(policy), _p(draft_buf),
+        _p(x_tok), _p(x_pos),
         _p(x_slot), _p(x_done), _p(row_start), _p(row_nd), _p(meta), _stream()), "spec_plan")
 
 

@@ -1306,15 +1306,18 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
 
 // ---------------------------------------------------------------------------
 // Speculative-verify attention: one wave = ONE row's pseudo-rows (its current
-// token + nd <= 16/G - 1 drafts, contiguous at row_start[r]) of one kv head.
+// token + nd <= 16·NCB/G - 1 drafts, contiguous at row_start[r]) of one kv head.
 // MFMA column c <-> (pseudo-row i = c / G, query head g = c % G).  All pseudo-rows
 // of a row read the same slot, pseudo-row i seeing keys [0, pos + i]: the row's
 // key tiles are loaded and multiplied ONCE for every draft (attn_grouped_kernel
 // walks them once per pseudo-row), each column masked at its own length.  A
 // column's arithmetic is the grouped kernel's (same tiles in the same order; the
 // extra tiles past its length are exact no-ops), so outputs are bit-identical.
-// grid = (rows, nkv), one wave; rows whose current pseudo-row is done are skipped.
+// grid = (rows, nkv), one wave; finished rows (row_nd < 0) are skipped.
 // ---------------------------------------------------------------------------
+// NCB column blocks of 16 (NCB = 2: up to 32 / G pseudo-rows, e.g. 1 + 8 drafts at
+// G = 3) share every K/V tile load; block cb holds columns 16·cb .. 16·cb + 15.
+template <int NCB>
 __global__ void __launch_bounds__(64) attn_spec_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ row_start, const int* __restrict__ row_nd,
     const int* __restrict__ x_pos, const int* __restrict__ x_slot, const int* __restrict__ x_done,
@@ -1323,48 +1326,63 @@ __global__ void __launch_bounds__(64) attn_spec_kernel(
     float scale_log2) {
   constexpr int D = 64;
   const int r = blockIdx.x, kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
-  const int G = nh / nkv, SPW = 16 / G;
+  const int G = nh / nkv, QPW = 16 * NCB / G;
+  const int nd = row_nd[r];
+  if (nd < 0) return;  // finished row: no pseudo-rows (sg_spec_plan)
   const int st = row_start[r];
-  if (x_done[st]) return;
-  const int nq = min(row_nd[r] + 1, SPW);  // the host guarantees 1 + spec_k <= 16 / G
+  const int nq = min(nd + 1, QPW);  // the host guarantees (1 + spec_k) * G <= 16 * NCB
   const int p = x_pos[st], sl = x_slot[st];
-  const int i = r16 / G, g = r16 % G;
-  const bool col_valid = i < nq;
-  const size_t qrow = (size_t)(st + (col_valid ? i : 0)) * nh + kh * G + g;
-  bf16x8 qb[2];
+  bf16x8 qb[NCB][2];
+  f32x4 o[NCB][4];
+  float m[NCB], lsum[NCB];
+  int own[NCB];
+  bool col_valid[NCB];
+  size_t qrow[NCB];
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    uint4 v = *reinterpret_cast<const uint4*>(q + qrow * D + 8 * g4 + 32 * s2);
-    if (!col_valid) v = make_uint4(0, 0, 0, 0);
-    qb[s2] = __builtin_bit_cast(bf16x8, v);
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int c = 16 * cb + r16, i = c / G, g = c % G;
+    col_valid[cb] = i < nq;
+    own[cb] = p + i + 1;  // per-lane length (invalid columns: masked by q = 0 and no store)
+    qrow[cb] = (size_t)(st + (col_valid[cb] ? i : 0)) * nh + kh * G + g;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      uint4 v = *reinterpret_cast<const uint4*>(q + qrow[cb] * D + 8 * g4 + 32 * s2);
+      if (!col_valid[cb]) v = make_uint4(0, 0, 0, 0);
+      qb[cb][s2] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) o[cb][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    m[cb] = -INFINITY;
+    lsum[cb] = 0.f;
   }
-  f32x4 o[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, lsum = 0.f;
   const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
   const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
   for (int kt = 0; kt < P0; kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
-    st_tile(qb, kc, vc, kt, P0, g4, scale_log2, m, lsum, o);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) st_tile(qb[cb], kc, vc, kt, P0, g4, scale_log2, m[cb], lsum[cb], o[cb]);
   }
   const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
   const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
-  const int own_max = p + nq, own = p + i + 1;  // per-lane length (invalid columns: masked by q = 0 and no store)
+  const int own_max = p + nq;
   for (int kt = 0; kt < own_max; kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own_max, kc, vc);
-    st_tile(qb, kc, vc, kt, own, g4, scale_log2, m, lsum, o, col_valid);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+      st_tile(qb[cb], kc, vc, kt, own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
   }
-  if (col_valid) {
-    const float inv = 1.f / lsum;
-    uint16_t* orow = out + qrow * D;
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    if (!col_valid[cb]) continue;
+    const float inv = 1.f / lsum[cb];
+    uint16_t* orow = out + qrow[cb] * D;
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       uint2 w;
-      w.x = (uint32_t)f2bf(o[n][0] * inv) | ((uint32_t)f2bf(o[n][1] * inv) << 16);
-      w.y = (uint32_t)f2bf(o[n][2] * inv) | ((uint32_t)f2bf(o[n][3] * inv) << 16);
+      w.x = (uint32_t)f2bf(o[cb][n][0] * inv) | ((uint32_t)f2bf(o[cb][n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[cb][n][2] * inv) | ((uint32_t)f2bf(o[cb][n][3] * inv) << 16);
       *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
     }
   }
@@ -1771,12 +1789,19 @@ int sg_attn_spec(const void* q, const int* row_start, const int* row_nd, const i
                  const int* x_done, const void* k_cache, const void* vt_cache, const void* pk, const void* pvt, int P0,
                  int P0pad, void* out, int B, int nh, int nkv, int D, int Lmax, float scale, int max_q,
                  hipStream_t stream) {
-  if (D != 64 || nh % nkv || nh / nkv > 16 || max_q * (nh / nkv) > 16 || (P0pad % 32) || (Lmax % 32) || P0 > P0pad)
+  if (D != 64 || nh % nkv || nh / nkv > 16 || max_q < 1 || max_q * (nh / nkv) > 32 || (P0pad % 32) || (Lmax % 32) ||
+      P0 > P0pad)
     return -1;
   if (B == 0) return 0;
-  hipLaunchKernelGGL(attn_spec_kernel, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, row_start, row_nd, x_pos,
-                     x_slot, x_done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
-                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, scale * 1.4426950408889634f);
+  const float sl2 = scale * 1.4426950408889634f;
+  if (max_q * (nh / nkv) <= 16)
+    hipLaunchKernelGGL(attn_spec_kernel<1>, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, row_start, row_nd,
+                       x_pos, x_slot, x_done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
+                       (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2);
+  else
+    hipLaunchKernelGGL(attn_spec_kernel<2>, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, row_start, row_nd,
+                       x_pos, x_slot, x_done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
+                       (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2);
   return (int)hipGetLastError();
 }
 

@@ -4,27 +4,30 @@
 // (models/tokenizer.py value_span_ids), so the body is an exact draft source:
 // "prompt lookup" drafting.  One speculative step of a decode bucket of B rows:
 //
-//   sg_spec_plan    one workgroup: for each live row, look up its last emitted
-//                   token (bigram with the one before, else unigram) in its body
-//                   tokens and draft up to K following body tokens (a delimiter
-//                   token -- ',' / '&#' / ';' -- is drafted as <sep> and ends the
-//                   draft); an exclusive scan over rows packs the rows' [last
-//                   token, drafts...] into T_cap = B + D_cap pseudo-rows, clamping
-//                   drafts once the budget D_cap is used up.  Pseudo-row = one
-//                   query token at its own position in its row's KV slot, so the
-//                   unchanged decode kernels (GEMMs, QKV+RoPE+KV write, grouped
-//                   decode attention) run the verify forward; unused tail
-//                   pseudo-rows point at a scratch slot and are marked done.
-//   sg_spec_verify  one 256-thread block per row: walks the row's pseudo-rows in
-//                   order, taking the schema-FSM masked arg-max of each logits row
-//                   (the exact code of fsm_sample_kernel's greedy path) and
-//                   accepting while it equals the next draft; every arg-max taken
-//                   is emitted, so a step emits accepted + 1 tokens.  KV entries
-//                   written for rejected drafts lie beyond the row's new position
-//                   and are overwritten by the next step (roll back by position).
+//   sg_spec_plan    three launches.  draft (one thread per row): look up the row's
+//                   last token (bigram with the one before, else unigram) in its
+//                   body tokens and draft up to K following body tokens, walking
+//                   the schema FSM (a delimiter token -- ',' / '&#' / ';' -- is
+//                   drafted as <sep>; policy 1 adds forced tokens, implicit value
+//                   ends and field-start resumption).  scan (one block): finished
+//                   rows take no pseudo-row, the live rows' drafts are water-filled
+//                   into the budget T_cap - live rows and packed by an exclusive
+//                   scan.  fill (one thread per row): pseudo-row = one query token
+//                   at its own position in its row's KV slot; the unused tail
+//                   points at a scratch slot and is marked done.
+//   verify forward  the decode GEMMs + QKV/RoPE/KV-write run over the T_cap
+//                   pseudo-rows; attention is attn_spec_kernel (one wave per row and
+//                   kv head, the row's keys read once for all its drafts); the
+//                   lm_head GEMM reduces each pseudo-row to its FSM-masked arg-max
+//                   key (sg_gemm_argmax, masked with the state the row would be in
+//                   if the drafts before it are accepted).
+//   sg_spec_verify_keys  one thread per row: accept drafts while the arg-max equals
+//                   the next draft; every arg-max taken is emitted, so a step emits
+//                   accepted + 1 tokens.  KV entries written for rejected drafts lie
+//                   beyond the row's new position and are overwritten later.
 //
 // Greedy outputs are bit-identical to one-token decode: every query token runs
-// the same per-column arithmetic in the same kernels (tests/test_spec_gpu.py).
+// the same per-column arithmetic (tests/test_spec_gpu.py, test_kernels_gpu.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -72,87 +75,187 @@ static __device__ __forceinline__ int key_token(unsigned long long key, int sep_
 //   scan   — one block: exclusive scan of the counts, clamp to the draft budget
 //   fill   — per row: write the pseudo-rows; then the unused tail
 // ---------------------------------------------------------------------------
+// first body position (bigram (prev, t), else unigram t) of `t`; -1 if absent
+static __device__ __forceinline__ int body_anchor(const int* body, int bl, int t, int prev) {
+  if (prev >= 0)
+    for (int q = 1; q < bl; ++q)
+      if (body[q] == t && body[q - 1] == prev) return q;
+  for (int q = 0; q < bl; ++q)
+    if (body[q] == t) return q;
+  return -1;
+}
+
+// policy 0 (round-2 first cut): copy the body after the last token's anchor, stop at
+//   the first <sep> or schema-forbidden token; nothing at a field start.
+// policy 1: (a) tokens the schema forces (the only allowed token of the state, e.g.
+//   the rest of an enum value or the <sep> after a full field) are drafted first;
+//   (b) a body token the field forbids where <sep> is allowed ends the value
+//   implicitly (<sep>, then the token starts the next field: "1500.00 RUB");
+//   (c) the copy runs on past <sep> into the next field; (d) at a field start
+//   (last token <sep>) the copy resumes after the previous value's last token.
+// scripts/spec_sim.py replays gold answers through both (14.9 -> 11.8 steps/message).
 __global__ void __launch_bounds__(256) spec_draft_kernel(
     FsmTables fsm, const int* __restrict__ state, int B, int K, int sep_token, const int* __restrict__ tok_buf,
     const int* __restrict__ slot, const int* __restrict__ done, const int* __restrict__ out_buf,
     const int* __restrict__ out_len, int max_out, const int* __restrict__ body_buf, const int* __restrict__ body_len,
-    int LB, const uint8_t* __restrict__ delim, int* __restrict__ draft_buf, int* __restrict__ row_nd) {
+    int LB, const uint8_t* __restrict__ delim, const int* __restrict__ forced, int policy,
+    int* __restrict__ draft_buf, int* __restrict__ row_nd) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= B) return;
   int n = 0;
-  const int t = tok_buf[r];
-  if (!done[r] && t != sep_token) {
+  int* dr = draft_buf + r * SPEC_MAX_K;
+  if (!done[r]) {
     const int len = out_len[r];
-    int prev = len >= 2 ? out_buf[(size_t)r * max_out + len - 2] : -1;
-    if (prev == sep_token) prev = -1;
+    const int* ob = out_buf + (size_t)r * max_out;
+    // t1 = last token, t2 / t3 the ones before it (-1 = none)
+    int t1 = tok_buf[r], t2 = len >= 2 ? ob[len - 2] : -1, t3 = len >= 3 ? ob[len - 3] : -1;
+    int s = state[r];
+    if (policy >= 1) {
+      while (n < K && s != fsm.done_state && forced[s] >= 0) {
+        const int x = forced[s];
+        dr[n++] = x;
+        s = fsm_next(fsm, s, x);
+        t3 = t2;
+        t2 = t1;
+        t1 = x;
+        if (s < 0) break;
+      }
+    }
     const int sl = slot[r];
     const int* body = body_buf + (size_t)sl * LB;
     const int bl = body_len[sl];
     int j = -1;
-    if (prev >= 0)
-      for (int q = 1; q < bl; ++q)
-        if (body[q] == t && body[q - 1] == prev) { j = q; break; }
-    if (j < 0)
-      for (int q = 0; q < bl; ++q)
-        if (body[q] == t) { j = q; break; }
+    if (s >= 0 && s != fsm.done_state && n < K) {
+      if (t1 != sep_token) {
+        j = body_anchor(body, bl, t1, t2 == sep_token ? -1 : t2);
+      } else if (policy >= 1 && t2 >= 0 && t2 != sep_token) {
+        j = body_anchor(body, bl, t2, t3 == sep_token ? -1 : t3);
+        if (j >= 0) {
+          while (j + 1 < bl && delim[body[j + 1]]) ++j;  // the delimiter that ended the value
+        }
+      }
+    }
     if (j >= 0) {
       // walk the schema FSM along the draft: a token the FSM forbids can never be
       // accepted (the verify arg-max is masked), so the draft stops before it
-      int s = state[r];
-      for (int i = 0; i < K; ++i) {
-        const int q = j + 1 + i;
-        if (q >= bl) break;
+      for (int q = j + 1; q < bl && n < K;) {
         const int x = delim[body[q]] ? sep_token : body[q];
-        if (!fsm_allows(fsm, s, x)) break;
+        if (!fsm_allows(fsm, s, x)) {
+          if (policy >= 1 && x != sep_token && fsm_allows(fsm, s, sep_token)) {
+            dr[n++] = sep_token;  // implicit end of the value; x starts the next field
+            s = fsm_next(fsm, s, sep_token);
+            if (s < 0 || s == fsm.done_state || !fsm_allows(fsm, s, x)) break;
+            continue;
+          }
+          break;
+        }
         const int ns = fsm_next(fsm, s, x);
         if (ns < 0) break;
-        draft_buf[r * SPEC_MAX_K + n++] = x;
+        dr[n++] = x;
         s = ns;
-        if (x == sep_token || ns == fsm.done_state) break;
+        ++q;
+        if (ns == fsm.done_state || (policy == 0 && x == sep_token)) break;
       }
     }
   }
-  row_nd[r] = n;
+  row_nd[r] = done[r] ? -1 : n;  // -1: finished row, no pseudo-row at all
 }
 
-// one block: row_start[r] = r + (clamped drafts of rows < r); row_nd clamped; meta[0] = rows used
-__global__ void __launch_bounds__(SPEC_THREADS) spec_scan_kernel(int B, int T_cap, int* __restrict__ row_start,
-                                                                 int* __restrict__ row_nd, int* __restrict__ meta) {
-  __shared__ int wsum[SPEC_THREADS / 64];
-  __shared__ int s_total;
-  const int tid = threadIdx.x;
-  const int RPT = (B + SPEC_THREADS - 1) / SPEC_THREADS;
-  const int r0 = tid * RPT, r1 = min(B, r0 + RPT);
-  int mine = 0;
-  for (int r = r0; r < r1; ++r) mine += row_nd[r];
-  const int lane = tid & 63, wid = tid >> 6;
-  int incl = mine;
+// block-wide exclusive scan of one int per thread (all SPEC_THREADS threads call it)
+static __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int& total) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int NWV = SPEC_THREADS / 64;
+  int incl = v;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
   }
   if (lane == 63) wsum[wid] = incl;
   __syncthreads();
   if (tid == 0) {
     int acc = 0;
-    for (int w = 0; w < SPEC_THREADS / 64; ++w) {
-      const int v = wsum[w];
+    for (int w = 0; w < NWV; ++w) {
+      const int x = wsum[w];
       wsum[w] = acc;
-      acc += v;
+      acc += x;
     }
-    s_total = acc;
+    wsum[NWV] = acc;
   }
   __syncthreads();
-  int dstart = wsum[wid] + incl - mine;  // drafts of all rows before my first row
-  const int D_cap = T_cap - B;
+  const int res = wsum[wid] + incl - v;
+  total = wsum[NWV];
+  __syncthreads();  // wsum is reused by the next call
+  return res;
+}
+
+// one block: finished rows (row_nd = -1) get no pseudo-row, so the budget is
+// D_cap = T_cap - live rows; the live rows' draft counts are clamped to it by water
+// filling -- every row keeps min(nd, c) drafts for the largest cap c that fits, the
+// rest of the budget gives one more draft to the first rows with nd > c -- so the
+// budget goes to the early (most likely accepted) drafts of as many rows as
+// possible; then row_start[r] = pseudo-rows of rows < r; meta[0] = pseudo-rows used.
+__global__ void __launch_bounds__(SPEC_THREADS) spec_scan_kernel(int B, int K, int T_cap, int* __restrict__ row_start,
+                                                                 int* __restrict__ row_nd, int* __restrict__ meta) {
+  __shared__ int wsum[SPEC_THREADS / 64 + 1];
+  __shared__ int tot[SPEC_MAX_K + 1];
+  __shared__ int s_c, s_extra;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int RPT = (B + SPEC_THREADS - 1) / SPEC_THREADS;
+  const int r0 = tid * RPT, r1 = min(B, r0 + RPT);
+  if (tid <= SPEC_MAX_K) tot[tid] = 0;
+  __syncthreads();
+  {
+    int live = 0;
+    for (int r = r0; r < r1; ++r) live += row_nd[r] >= 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) live += __shfl_xor(live, o, 64);
+    if (lane == 0) atomicAdd(&tot[0], live);  // LDS atomic; tot[0] = live rows until read below
+  }
+  __syncthreads();
+  const int D_cap = T_cap - tot[0];
+  __syncthreads();
+  if (tid == 0) tot[0] = 0;
+  // tot[c] = sum over rows of min(nd, c)
+  for (int c = 1; c <= K; ++c) {
+    int part = 0;
+    for (int r = r0; r < r1; ++r) part += min(max(row_nd[r], 0), c);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) atomicAdd(&tot[c], part);  // LDS atomic
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int c = 0;
+    for (int cc = 1; cc <= K; ++cc)
+      if (tot[cc] <= D_cap) c = cc;
+    s_c = c;
+    s_extra = D_cap - tot[c];
+  }
+  __syncthreads();
+  const int c = s_c, extra = s_extra;
+  int over = 0;
+  for (int r = r0; r < r1; ++r) over += row_nd[r] > c;
+  int total;
+  int rank = block_excl_scan(over, wsum, total);
+  int mine = 0;
   for (int r = r0; r < r1; ++r) {
     const int n = row_nd[r];
-    row_start[r] = r + min(dstart, D_cap);
-    row_nd[r] = max(0, min(n, D_cap - dstart));
-    dstart += n;
+    if (n < 0) continue;  // finished: stays -1
+    int f = min(n, c);
+    if (n > c) {
+      f += rank < extra;
+      ++rank;
+    }
+    row_nd[r] = f;
+    mine += 1 + f;
   }
-  if (tid == 0) meta[0] = B + min(s_total, D_cap);
+  int dstart = block_excl_scan(mine, wsum, total);
+  for (int r = r0; r < r1; ++r) {
+    row_start[r] = dstart;
+    dstart += 1 + row_nd[r];  // + 0 for a finished row
+  }
+  if (tid == 0) meta[0] = total;
 }
 
 __global__ void __launch_bounds__(256) spec_fill_kernel(
@@ -162,7 +265,7 @@ __global__ void __launch_bounds__(256) spec_fill_kernel(
     const int* __restrict__ meta, int* __restrict__ x_tok, int* __restrict__ x_pos, int* __restrict__ x_slot,
     int* __restrict__ x_done, int* __restrict__ x_state) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g < B) {
+  if (g < B && row_nd[g] >= 0) {  // a finished row (row_nd = -1) has no pseudo-row
     const int r = g, st = row_start[r], nc = row_nd[r];
     const int p = pos[r], sl = slot[r], dn = done[r];
     int s = state[r];
@@ -357,14 +460,16 @@ int sg_spec_plan(const void* masks, const int* state_mask, const int* next_sep, 
                  const int* enum_tok, const int* enum_next, int E, int done_state, int V, const int* state,
                  int* x_state, int B, int K, int T_cap, int sep_token, int scratch_slot, const int* tok_buf, const int* pos,
                  const int* slot, const int* done, const int* out_buf, const int* out_len, int max_out,
-                 const int* body_buf, const int* body_len, int LB, const void* delim, int* draft_buf, int* x_tok,
-                 int* x_pos, int* x_slot, int* x_done, int* row_start, int* row_nd, int* meta, hipStream_t stream) {
-  if (K < 0 || K > SPEC_MAX_K || T_cap < B || B <= 0) return -1;
+                 const int* body_buf, const int* body_len, int LB, const void* delim, const int* forced, int policy,
+                 int* draft_buf, int* x_tok, int* x_pos, int* x_slot, int* x_done, int* row_start, int* row_nd,
+                 int* meta, hipStream_t stream) {
+  if (K < 0 || K > SPEC_MAX_K || T_cap < B || B <= 0 || policy < 0 || policy > 1) return -1;
   const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
   const int grid = (B + 255) / 256;
   hipLaunchKernelGGL(spec_draft_kernel, dim3(grid), dim3(256), 0, stream, f, state, B, K, sep_token, tok_buf, slot, done,
-                     out_buf, out_len, max_out, body_buf, body_len, LB, (const uint8_t*)delim, draft_buf, row_nd);
-  hipLaunchKernelGGL(spec_scan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, B, T_cap, row_start, row_nd, meta);
+                     out_buf, out_len, max_out, body_buf, body_len, LB, (const uint8_t*)delim, forced, policy, draft_buf,
+                     row_nd);
+  hipLaunchKernelGGL(spec_scan_kernel, dim3(1), dim3(SPEC_THREADS), 0, stream, B, K, T_cap, row_start, row_nd, meta);
   hipLaunchKernelGGL(spec_fill_kernel, dim3(grid), dim3(256), 0, stream, f, state, B, T_cap, scratch_slot, tok_buf, pos,
                      slot, done, draft_buf, row_start, row_nd, meta, x_tok, x_pos, x_slot, x_done, x_state);
   return (int)hipGetLastError();

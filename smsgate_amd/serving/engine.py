@@ -100,8 +100,15 @@ class EngineConfig:
     spec_draft_frac: float = 1.25  # A/B 1.0 / 1.25 / 1.5 / 2.0: 22.5 / 23.2 / 23.1 / 21.5 k msgs/s
     spec_max_rows: int = 1 << 30  # buckets above this decode one token per row
     # verify attention: one wave per row reads the row's keys once for all its drafts
-    # (ops.attn_spec; needs (1 + spec_k) * heads / kv_heads <= 16), else the decode kernel
+    # (ops.attn_spec; needs (1 + spec_k) * heads / kv_heads <= 32), else the decode kernel
     spec_attn: bool = True
+    # draft policy (ops.spec_plan): 0 = copy the body until <sep>; 1 = + schema-forced
+    # tokens, implicit value ends, copy across <sep> and from field starts.  1 emits
+    # more tokens per row-step with an unlimited budget (scripts/spec_sim.py: 14.9 -> 11.8
+    # steps/message) but its extra drafts are accepted less often, and under the
+    # budget they displace better ones: 2.28 vs 2.40 tokens/row-step, 25.2 vs 26.0 k
+    # msgs/s (profiles/r02_spec_policy_ab.jsonl)
+    spec_policy: int = 0
 
 
 @dataclass
@@ -481,7 +488,8 @@ class ExtractionEngine:
         ops.spec_plan(self.fsm, self.state[r0:r1], xst, self.cfg.spec_k, T, self.tok.sep, self.scratch_slot, tok,
                       pos, slot, done,
                       self.out_buf[r0:r1], self.out_len[r0:r1], self.body_buf, self.body_len, self.spec_delim,
-                      self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd, self.spec_meta[r0:r0 + 1])
+                      self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd, self.spec_meta[r0:r0 + 1],
+                      policy=self.cfg.spec_policy)
         x = F.embedding(xt.long(), self.w.embed)
         impl = self.cfg.decode_attn_small if T <= self.cfg.decode_attn_small_rows else self.cfg.decode_attn
         scratch = None
@@ -496,7 +504,7 @@ class ExtractionEngine:
             return self.vt_cache[i]
 
         max_q = 1 + self.cfg.spec_k
-        if self.cfg.spec_attn and max_q * (self.mc.heads // self.mc.kv_heads) <= 16:
+        if self.cfg.spec_attn and max_q * (self.mc.heads // self.mc.kv_heads) <= 32:
             def attn(i, q, out):
                 ops.attn_spec(q, rs, nd, xp, xs, xd, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
                               self.scale, max_q)

@@ -105,6 +105,15 @@ class SchemaFSM:
     next_tok_t: object = None
     enum_tok_t: object = None
     enum_next_t: object = None
+    forced_t: object = None
+
+    @property
+    def forced(self) -> np.ndarray:
+        """[S] the only token a state allows (-1: several, or the done state)."""
+        one = self.allowed.sum(1) == 1
+        out = np.where(one, self.allowed.argmax(1), -1).astype(np.int32)
+        out[self.done_state] = -1
+        return out
 
     @property
     def E(self) -> int:
@@ -134,6 +143,7 @@ class SchemaFSM:
         self.next_tok_t = torch.from_numpy(self.next_tok.astype(np.int32)).to(device)
         self.enum_tok_t = torch.from_numpy(self.enum_tok.astype(np.int32)).to(device)
         self.enum_next_t = torch.from_numpy(self.enum_next.astype(np.int32)).to(device)
+        self.forced_t = torch.from_numpy(self.forced).to(device)
         return self
 
     def step_host(self, state: int, tok: int) -> int:

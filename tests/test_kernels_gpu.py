@@ -320,10 +320,11 @@ def test_gemm_argmax_matches_logits_path(cfg, M):
             assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())
 
 
-@pytest.mark.parametrize("P0", [0, 75])
-def test_attn_spec_matches_grouped_bitwise(P0):
+@pytest.mark.parametrize("P0,max_q", [(0, 5), (75, 5), (75, 9)])
+def test_attn_spec_matches_grouped_bitwise(P0, max_q):
     """attn_spec (one wave per row, all its drafts) == the grouped decode kernel on
-    the same pseudo-rows, bit for bit, and == an fp32 reference; done rows untouched."""
+    the same pseudo-rows, bit for bit, and == an fp32 reference; finished rows
+    (row_nd = -1) untouched.  max_q = 9: 27 columns, two MFMA column blocks per wave."""
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224
     P0pad = (P0 + 31) // 32 * 32
     kc = _bf(S, nkv, Lmax, D, seed=20)
@@ -337,6 +338,8 @@ def test_attn_spec_matches_grouped_bitwise(P0):
     pvt = ops.rows_to_vt(pvrows)
     # rows: (pos, slot, drafts, done); pos + drafts < Lmax
     rows = [(0, 3, 4, 0), (14, 0, 2, 0), (30, 7, 4, 1), (31, 1, 0, 0), (100, 2, 3, 0), (219, 5, 4, 0), (47, 6, 1, 0)]
+    if max_q > 5:
+        rows += [(60, 4, 8, 0), (150, 0, 7, 0), (215, 7, 8, 0)]  # slots reused: other positions
     xp, xs, xd, rs, nd = [], [], [], [], []
     for p, sl, n, dn in rows:
         rs.append(len(xp))
@@ -350,6 +353,7 @@ def test_attn_spec_matches_grouped_bitwise(P0):
     xs += [0] * 5
     xd += [1] * 5
     i32 = dict(dtype=torch.int32, device=DEV)
+    nd = [-1 if row[3] else n for row, n in zip(rows, nd)]  # finished rows: row_nd = -1 (sg_spec_plan)
     xp, xs, xd, rs, nd = (torch.tensor(v, **i32) for v in (xp, xs, xd, rs, nd))
     # the grouped kernel skips only the row's FIRST pseudo-row on done; mark its drafts done too
     xd_g = xd.clone()
@@ -360,7 +364,7 @@ def test_attn_spec_matches_grouped_bitwise(P0):
     scale = 1 / math.sqrt(D)
     out_s = torch.full((T, nh * D), 7.0, dtype=torch.bfloat16, device=DEV)
     out_g = out_s.clone()
-    ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=5)
+    ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=max_q)
     ops.attn_decode(q, xp, xs, kc, vt, pk, pvt, P0, out_g, scale, done=xd_g, impl="grouped")
     torch.cuda.synchronize()
     assert torch.equal(out_s, out_g)
@@ -374,4 +378,4 @@ def test_attn_spec_matches_grouped_bitwise(P0):
                                  pvrows[:, :P0].permute(1, 0, 2).float(), P0, [p], scale)
         torch.testing.assert_close(out_s[t].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)
     with pytest.raises(ValueError):
-        ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=6)
+        ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=11)

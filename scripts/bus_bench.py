@@ -5,7 +5,9 @@ P producer processes publish ``--msgs`` messages each (``publish_many`` batches 
 ``--batch``, ~300-byte SMS-sized payloads) onto ``sms.raw``; C consumer processes
 share one durable group, fetch batches and ack every message.  Reported: end-to-end
 msgs/s (first publish → last ack observed by ``consumer_info``) with the journal on
-(``--data``, fsync interval) for each broker.
+(``--data``, fsync interval) for each broker.  ``--protocol nats`` drives both
+brokers through their NATS front-ends (JetStream PubAck per publish, pull
+consumers, ``$JS.ACK`` acks) with the same client code.
 
     python scripts/bus_bench.py --producers 4 --consumers 4 --msgs 50000
 """
@@ -53,14 +55,30 @@ def _consumer(sock, batch, stop_evt):
     asyncio.run(go())
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def run_one(native: bool, a) -> dict:
     tmp = tempfile.mkdtemp(prefix="busbench-")
-    sock = f"unix://{tmp}/bus.sock"
+    ctl_sock = sock = f"unix://{tmp}/bus.sock"
+    nats_listen = None
+    if a.protocol == "nats":
+        port = _free_port()
+        nats_listen = f"tcp://127.0.0.1:{port}"
+        sock = f"nats://127.0.0.1:{port}"
     ctx = mp.get_context("spawn")
     total = a.producers * a.msgs
 
     async def go():
-        srv = await serve(sock, os.path.join(tmp, "data") if a.journal else None, native=native)
+        srv = await serve(ctl_sock, os.path.join(tmp, "data") if a.journal else None, native=native,
+                          nats_listen=nats_listen)
         ctl = await connect(sock, shared=False)
         await ctl.subscribe(SUBJECT_RAW, "bench")  # create the durable before anyone publishes
         start_evt, stop_evt = ctx.Event(), ctx.Event()
@@ -86,7 +104,7 @@ def run_one(native: bool, a) -> dict:
         return dt
 
     dt = asyncio.run(go())
-    return {"broker": "native" if native else "python", "msgs": total, "seconds": round(dt, 3),
+    return {"broker": "native" if native else "python", "protocol": a.protocol, "msgs": total, "seconds": round(dt, 3),
             "msgs_per_s": round(total / dt, 1), "producers": a.producers, "consumers": a.consumers,
             "batch": a.batch, "journal": a.journal}
 
@@ -99,6 +117,7 @@ def main() -> None:
     p.add_argument("--batch", type=int, default=256)
     p.add_argument("--no-journal", dest="journal", action="store_false")
     p.add_argument("--only", choices=["python", "native"], default=None)
+    p.add_argument("--protocol", choices=["msgpack", "nats"], default="msgpack")
     a = p.parse_args()
     from smsgate_amd.native import build
 

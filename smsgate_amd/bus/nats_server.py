@@ -322,10 +322,10 @@ class NatsFrontend:
             sent += len(got)
             if no_wait:
                 break
-        if sent < batch:
-            if no_wait and sent == 0:
+        if sent < batch:  # end the request: a client waits for the batch or a status frame
+            if no_wait:
                 self._status(reply, 404, "No Messages")
-            elif not no_wait:
+            else:
                 self._status(reply, 408, "Request Timeout")
 
     def _start_push(self, stream: str, durable: str, deliver: str) -> None:

@@ -154,15 +154,13 @@ async def serve(listen: str, data_dir: Optional[str], stop: Optional[asyncio.Eve
     the NATS wire protocol (``nats_listen``, :mod:`.nats_server`).
 
     ``native=True`` runs the C++ broker (:mod:`smsgate_amd.native`, same
-    protocol and journal format) as a child process instead; the returned
-    object has the same ``close()``.
+    protocol and journal format, its own NATS front-end) as a child process
+    instead; the returned object has the same ``close()``.
     """
     if native:
-        if nats_listen:
-            raise BusError("the native broker serves the msgpack protocol only (drop --nats-listen)")
         from ..native import spawn_busd
 
-        broker = spawn_busd(listen, data_dir, max_age=max_age)
+        broker = spawn_busd(listen, data_dir, max_age=max_age, nats_listen=nats_listen or None)
         if stop is not None:
             await stop.wait()
             await broker.close()

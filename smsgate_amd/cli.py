@@ -156,7 +156,7 @@ async def _run_bus_server(a, settings) -> None:
 
     native = getattr(a, "native", False)
     await serve(a.listen, a.data, _stop_event(), max_age=settings.stream_max_age_s,
-                nats_listen=None if native else a.nats_listen, native=native)
+                nats_listen=a.nats_listen, native=native)
 
 
 async def _run_pipeline(a, settings) -> None:
@@ -317,7 +317,7 @@ def build_parser() -> argparse.ArgumentParser:
     bp.add_argument("--nats-listen", default="tcp://0.0.0.0:4222", help="NATS wire protocol ('' = off)")
     bp.add_argument("--data", default="./.bus-data")
     bp.add_argument("--native", action="store_true",
-                    help="run the C++ broker (smsgate-busd; msgpack protocol only, same journal format)")
+                    help="run the C++ broker (smsgate-busd: msgpack + NATS protocols, same journal format)")
     ep = sp.add_parser("engine-server")
     ep.add_argument("--listen", default="unix:///tmp/smsgate-engine0.sock")
     ep.add_argument("--model", default=None, help="default: LLM_MODEL (smollm-135m)")

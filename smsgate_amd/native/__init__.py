@@ -7,7 +7,9 @@
   :class:`~smsgate_amd.bus.client.RemoteBus` works unchanged) and writes the
   same CRC-framed journal as :mod:`smsgate_amd.bus.filelog` (either broker
   recovers the other's data directory).  One epoll loop, group-committed
-  journal writes, long-poll fetch waiters.
+  journal writes, long-poll fetch waiters.  ``nats_listen`` adds the NATS client
+  protocol + JetStream API front-end (the subset :mod:`smsgate_amd.bus.nats_server`
+  serves) on the same engine, so nats-py style clients reach the fast broker.
 
 Build: ``python -m smsgate_amd.native.build`` (in-tree, ``_bin/``).
 """
@@ -32,10 +34,12 @@ def available(binary: Path = BUSD) -> bool:
 class NativeBroker:
     """A running ``smsgate-busd`` child process."""
 
-    def __init__(self, proc: subprocess.Popen, listens: List[str], tcp_port: Optional[int]) -> None:
+    def __init__(self, proc: subprocess.Popen, listens: List[str], tcp_port: Optional[int],
+                 nats_port: Optional[int] = None) -> None:
         self.proc = proc
         self.listens = listens
         self.tcp_port = tcp_port
+        self.nats_port = nats_port
 
     @property
     def pid(self) -> int:
@@ -68,7 +72,7 @@ class NativeBroker:
 def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_age: float = 3 * 24 * 3600.0,
                fsync: str = "interval", fsync_interval_s: float = 0.05, compact_bytes: Optional[int] = None,
                ready_timeout: float = 20.0, binary: Optional[Path] = None, stderr=None,
-               die_with_parent: bool = True) -> NativeBroker:
+               die_with_parent: bool = True, nats_listen: Optional[str] = None) -> NativeBroker:
     """Start the native broker and wait until it listens.
 
     ``listen`` takes ``tcp://host:port`` (port 0 = pick one, see
@@ -83,6 +87,8 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
     cmd = [str(binary)]
     for u in listens:
         cmd += ["--listen", u]
+    if nats_listen:
+        cmd += ["--nats-listen", nats_listen]
     if data_dir:
         cmd += ["--data", str(data_dir)]
     cmd += ["--max-age", repr(float(max_age)), "--fsync", fsync, "--fsync-interval", repr(float(fsync_interval_s))]
@@ -99,8 +105,10 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
     if not line.startswith(b"READY"):
         proc.kill()
         raise RuntimeError(f"smsgate-busd failed to start (exit {proc.poll()}): {line!r}")
-    tok = line.split()[1].decode()
-    return NativeBroker(proc, listens, None if tok == "-" else int(tok))
+    parts = line.split()
+    tok = parts[1].decode()
+    nats_port = int(parts[3]) if len(parts) >= 4 and parts[2] == b"NATS" else None
+    return NativeBroker(proc, listens, None if tok == "-" else int(tok), nats_port)
 
 
 def _pdeathsig() -> None:  # runs in the child between fork and exec

@@ -23,7 +23,9 @@
 // Usage: smsgate-busd --listen tcp://0.0.0.0:4222 [--listen unix:///run/bus.sock]
 //                     [--data DIR] [--max-age S] [--fsync interval|always|never]
 //                     [--fsync-interval S] [--compact-bytes N]
-// Prints ``READY <tcp-port|->`` on stdout once listening.
+// ``--nats-listen tcp://HOST:PORT`` adds the NATS client protocol + JetStream API
+// front-end (Server::nats_*) on the same engine.
+// Prints ``READY <tcp-port|->[ NATS <port>]`` on stdout once listening.
 #include <arpa/inet.h>
 #include <dirent.h>
 #include <errno.h>
@@ -45,12 +47,15 @@
 #include <mutex>
 #include <thread>
 #include <cstdlib>
+#include <cstring>
 #include <list>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "engine.hpp"
+#include "json.hpp"
 
 namespace {
 
@@ -320,6 +325,8 @@ void replay_into(bus::Engine& eng, const std::string& kind, mp::Value& args) {
     bus::Stream& st = eng.stream(a[0].as_str());
     auto it = st.consumers.find(a[1].as_str());
     if (it != st.consumers.end()) it->second.pending.erase(a[2].as_int());
+  } else if (kind == "delstream") {
+    if (eng.streams.count(a[0].as_str())) eng.delete_stream(a[0].as_str());
   } else if (kind == "delconsumer") {
     eng.stream(a[0].as_str()).consumers.erase(a[1].as_str());
   } else if (kind == "purge") {
@@ -449,15 +456,29 @@ void compact(bus::Engine& eng, Journal& jr) {
 }
 
 // -------------------------------------------------------------------- server
+struct NSub {  // a NATS-protocol subscription
+  std::string subject, queue;
+};
+
 struct Conn {
   int fd;
   uint64_t id;
+  bool nats = false;                               // NATS text protocol (--nats-listen)
+  std::unordered_map<std::string, NSub> subs;      // NATS: sid -> subscription
   std::string in;
   size_t in_off = 0;
   std::string out;
   size_t out_off = 0;
   bool writing = false;
   bool dead = false;
+};
+
+// a NATS pull request ($JS.API.CONSUMER.MSG.NEXT) still being filled
+struct NWaiter {
+  std::string reply, stream, durable;
+  int64_t batch, sent = 0;
+  double deadline;
+  bool no_wait;
 };
 
 struct Waiter {
@@ -485,7 +506,7 @@ class Server {
     return c;
   }
 
-  int listen_on(const std::string& url) {
+  int listen_on(const std::string& url, bool nats = false) {
     int fd;
     int port = -1;
     if (url.rfind("unix://", 0) == 0) {
@@ -523,7 +544,7 @@ class Server {
     ev.events = EPOLLIN;
     ev.data.u64 = 0;  // 0 = a listener; look up by fd
     listeners_.push_back(fd);
-    ev.data.u64 = (uint64_t)fd | (1ull << 63);
+    ev.data.u64 = (uint64_t)fd | (1ull << 63) | (nats ? (1ull << 62) : 0);
     epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev);
     return port;
   }
@@ -538,7 +559,7 @@ class Server {
       for (int k = 0; k < n; ++k) {
         uint64_t tag = evs[k].data.u64;
         if (tag & (1ull << 63)) {
-          accept_all((int)(tag & 0xffffffff));
+          accept_all((int)(tag & 0xffffffff), (tag >> 62) & 1);
           continue;
         }
         auto it = conns_.find(tag);
@@ -553,6 +574,7 @@ class Server {
         last_expire_ = now;
       }
       serve_waiters(now);
+      serve_nats(now);
       if (jr_) {
         jr_->flush();  // group commit before any reply of this iteration leaves
         jr_->tick();
@@ -580,11 +602,29 @@ class Server {
         t = 0;
       }
     }
+    for (auto& w : nwaiters_) {
+      t = std::min(t, std::max(0.0, w.deadline - now));
+      try {
+        double r = eng_.next_ready_at(eng_.consumer(w.stream, w.durable));
+        if (!std::isnan(r)) t = std::min(t, std::max(0.0, r - now) + 1e-4);
+      } catch (std::exception&) {
+        t = 0;
+      }
+    }
+    for (auto& kv : push_) {
+      try {
+        double r = eng_.next_ready_at(eng_.consumer(kv.first.first, kv.first.second));
+        if (!std::isnan(r)) t = std::min(t, std::max(0.0, r - now) + 1e-4);
+      } catch (std::exception&) {
+        t = 0;
+      }
+    }
+    if (!push_.empty()) t = std::min(t, 0.05);  // a deliver-subject subscriber may have appeared
     if (jr_) t = std::min(t, jr_->sync_due_in());
     return (int)std::ceil(t * 1000.0);
   }
 
-  void accept_all(int lfd) {
+  void accept_all(int lfd, bool nats) {
     for (;;) {
       int fd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (fd < 0) return;
@@ -594,6 +634,8 @@ class Server {
       Conn& c = conns_[id];
       c.fd = fd;
       c.id = id;
+      c.nats = nats;
+      if (nats) nats_info(c);
       epoll_event ev{};
       ev.events = EPOLLIN | EPOLLRDHUP;
       ev.data.u64 = id;
@@ -613,7 +655,8 @@ class Server {
       if (r < 0 && errno == EINTR) continue;
       break;
     }
-    while (c.in.size() - c.in_off >= 4) {
+    if (c.nats) nats_parse(c);
+    while (!c.nats && c.in.size() - c.in_off >= 4) {
       uint32_t len = get_u32(c.in.data() + c.in_off);
       if (len > (256u << 20)) { c.dead = true; break; }
       if (c.in.size() - c.in_off < 4 + (size_t)len) break;
@@ -868,6 +911,566 @@ class Server {
     }
   }
 
+
+  // =================================================================== NATS
+  // NATS client protocol + the JetStream API subset of bus/nats_server.py (the
+  // Python front-end; tests/test_bus_nats.py runs the same client tests against
+  // both): core INFO/CONNECT/PING/PONG/PUB/HPUB/SUB (queue groups)/UNSUB with
+  // subject routing; a publish to a stream subject is stored (PubAck JSON to its
+  // reply); $JS.API STREAM.NAMES/LIST/INFO/CREATE/UPDATE/DELETE, CONSUMER.CREATE /
+  // DURABLE.CREATE / INFO / DELETE / MSG.NEXT (pull; 404 / 408 status frames) and
+  // push consumers (deliver_subject); acks on $JS.ACK.* (+ACK, -NAK {delay}, +TERM,
+  // +WPI, +NXT).  All on the same event loop and engine as the msgpack protocol.
+  static constexpr size_t kNatsMaxPayload = 8u << 20;
+
+  static bool starts_with(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
+
+  static std::vector<std::string> split_on(const std::string& s, char sep) {
+    std::vector<std::string> out;
+    size_t b = 0;
+    for (;;) {
+      size_t e = s.find(sep, b);
+      out.push_back(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
+      if (e == std::string::npos) return out;
+      b = e + 1;
+    }
+  }
+
+  static std::vector<std::string> split_ws(const std::string& s) {
+    std::vector<std::string> out;
+    size_t k = 0;
+    while (k < s.size()) {
+      while (k < s.size() && (s[k] == ' ' || s[k] == '\t')) ++k;
+      size_t b = k;
+      while (k < s.size() && s[k] != ' ' && s[k] != '\t') ++k;
+      if (k > b) out.push_back(s.substr(b, k - b));
+    }
+    return out;
+  }
+
+  void nats_info(Conn& c) {
+    mp::Value info = mp::Value::map();
+    info.put("server_id", mp::Value::str(server_id_));
+    info.put("server_name", mp::Value::str("smsgate-busd"));
+    info.put("version", mp::Value::str("2.10.0"));
+    info.put("proto", mp::Value::integer(1));
+    info.put("go", mp::Value::str("n/a"));
+    info.put("host", mp::Value::str("0.0.0.0"));
+    info.put("port", mp::Value::integer(nats_port_));
+    info.put("headers", mp::Value::boolean(true));
+    info.put("max_payload", mp::Value::integer((int64_t)kNatsMaxPayload));
+    info.put("jetstream", mp::Value::boolean(true));
+    c.out += "INFO " + json::dumps(info) + "\r\n";
+  }
+
+  void nats_parse(Conn& c) {
+    while (!c.dead) {
+      const char* base = c.in.data() + c.in_off;
+      size_t avail = c.in.size() - c.in_off;
+      const char* nl = (const char*)memmem(base, avail, "\r\n", 2);
+      if (!nl) {
+        if (avail > 64 * 1024) c.dead = true;  // no control line is this long
+        return;
+      }
+      size_t llen = (size_t)(nl - base);
+      std::string line(base, llen);
+      size_t sp = line.find(' ');
+      std::string op = line.substr(0, sp);
+      for (auto& ch : op) ch = (char)toupper((unsigned char)ch);
+      std::vector<std::string> args = split_ws(sp == std::string::npos ? std::string() : line.substr(sp + 1));
+      if (op == "PUB" || op == "HPUB") {
+        bool h = op == "HPUB";
+        size_t need = h ? 3 : 2;
+        if (args.size() != need && args.size() != need + 1) {
+          c.out += "-ERR 'Unknown Protocol Operation'\r\n";
+          c.dead = true;
+          return;
+        }
+        size_t total = strtoull(args.back().c_str(), nullptr, 10);
+        size_t hsize = h ? strtoull(args[args.size() - 2].c_str(), nullptr, 10) : 0;
+        if (total > kNatsMaxPayload || hsize > total) {
+          c.out += "-ERR 'Maximum Payload Violation'\r\n";
+          c.dead = true;
+          return;
+        }
+        if (avail < llen + 2 + total + 2) return;  // payload not complete yet
+        const char* body = nl + 2;
+        std::string subject = args[0];
+        std::string reply = args.size() == need + 1 ? args[1] : std::string();
+        std::string hdr(body, hsize), payload(body + hsize, total - hsize);
+        c.in_off += llen + 2 + total + 2;
+        nats_pub(subject, reply, hdr, payload);
+        continue;
+      }
+      c.in_off += llen + 2;
+      if (op == "SUB" && (args.size() == 2 || args.size() == 3)) {
+        c.subs[args.back()] = NSub{args[0], args.size() == 3 ? args[1] : std::string()};
+      } else if (op == "UNSUB" && !args.empty()) {
+        c.subs.erase(args[0]);
+      } else if (op == "PING") {
+        c.out += "PONG\r\n";
+      } else if (op == "CONNECT" || op == "PONG" || op == "+OK" || op.empty()) {
+      } else {
+        c.out += "-ERR 'Unknown Protocol Operation'\r\n";
+      }
+    }
+  }
+
+  static void msg_frame(std::string& o, const std::string& subject, const std::string& sid, const std::string& reply,
+                        const std::string& hdr, const std::string& payload) {
+    o += hdr.empty() ? "MSG " : "HMSG ";
+    o += subject;
+    o += ' ';
+    o += sid;
+    if (!reply.empty()) {
+      o += ' ';
+      o += reply;
+    }
+    if (!hdr.empty()) {
+      o += ' ';
+      o += std::to_string(hdr.size());
+    }
+    o += ' ';
+    o += std::to_string(hdr.size() + payload.size());
+    o += "\r\n";
+    o += hdr;
+    o += payload;
+    o += "\r\n";
+  }
+
+  // deliver to every matching plain subscription and one member of each queue group
+  int nats_route(const std::string& subject, const std::string& payload, const std::string& reply = std::string(),
+                 const std::string& hdr = std::string()) {
+    int n = 0;
+    route_q_.clear();
+    for (auto& kv : conns_) {
+      Conn& c = kv.second;
+      if (!c.nats || c.dead) continue;
+      for (auto& sv : c.subs)
+        if (bus::subject_matches(sv.second.subject, subject)) {
+          if (sv.second.queue.empty()) {
+            msg_frame(c.out, subject, sv.first, reply, hdr, payload);
+            ++n;
+          } else {
+            route_q_.push_back({&sv.second.queue, {&c, &sv.first}});
+          }
+        }
+    }
+    if (!route_q_.empty()) {  // one member per queue group, round robin
+      std::stable_sort(route_q_.begin(), route_q_.end(),
+                       [](const QMember& x, const QMember& y) { return *x.first < *y.first; });
+      for (size_t b = 0; b < route_q_.size();) {
+        size_t e = b;
+        while (e < route_q_.size() && *route_q_[e].first == *route_q_[b].first) ++e;
+        auto& pick = route_q_[b + (rr_++) % (e - b)].second;
+        msg_frame(pick.first->out, subject, *pick.second, reply, hdr, payload);
+        ++n;
+        b = e;
+      }
+    }
+    return n;
+  }
+
+  bool nats_has_subscriber(const std::string& subject) {
+    for (auto& kv : conns_)
+      if (kv.second.nats && !kv.second.dead)
+        for (auto& sv : kv.second.subs)
+          if (bus::subject_matches(sv.second.subject, subject)) return true;
+    return false;
+  }
+
+  void nats_status(const std::string& reply, int code, const char* text) {
+    nats_route(reply, std::string(), std::string(), "NATS/1.0 " + std::to_string(code) + " " + text + "\r\n\r\n");
+  }
+
+  static mp::Value parse_headers(const std::string& raw) {
+    mp::Value m = mp::Value::map();
+    auto lines = split_on(raw, '\n');
+    for (size_t k = 1; k < lines.size(); ++k) {
+      std::string ln = lines[k];
+      if (!ln.empty() && ln.back() == '\r') ln.pop_back();
+      size_t colon = ln.find(':');
+      if (ln.empty() || colon == std::string::npos) continue;
+      auto trim = [](std::string x) {
+        size_t a = x.find_first_not_of(" \t"), b = x.find_last_not_of(" \t");
+        return a == std::string::npos ? std::string() : x.substr(a, b - a + 1);
+      };
+      m.put(trim(ln.substr(0, colon)).c_str(), mp::Value::str(trim(ln.substr(colon + 1))));
+    }
+    return m;
+  }
+
+  static std::string encode_headers(const mp::Value& h) {
+    if (h.t != mp::Value::MAP || h.m.empty()) return std::string();
+    std::string o = "NATS/1.0\r\n";
+    for (auto& kv : h.m) {
+      if (kv.first.t != mp::Value::STR || (kv.second.t != mp::Value::STR && kv.second.t != mp::Value::BIN)) continue;
+      o += kv.first.s + ": " + kv.second.s + "\r\n";
+    }
+    return o + "\r\n";
+  }
+
+  void nats_pub(const std::string& subject, const std::string& reply, const std::string& hdr,
+                const std::string& payload) {
+    if (starts_with(subject, "$JS.API.")) {
+      nats_api(subject.substr(8), payload, reply);
+      return;
+    }
+    if (starts_with(subject, "$JS.ACK.")) {
+      nats_ack(subject, payload);
+      if (!reply.empty()) nats_route(reply, std::string());
+      return;
+    }
+    bool captured = true;
+    try {
+      eng_.route(subject);
+    } catch (bus::BusError&) {
+      captured = false;
+    }
+    if (captured) {
+      std::string data = payload;
+      auto r = eng_.store(subject, std::move(data), hdr.empty() ? mp::Value::nil() : parse_headers(hdr));
+      if (!reply.empty()) {
+        std::string ack = "{\"stream\":";
+        json::dump_str(ack, *r.first);
+        ack += ",\"seq\":" + std::to_string(r.second) + "}";
+        nats_route(reply, ack);
+      }
+    }
+    int n = nats_route(subject, payload, captured ? std::string() : reply, hdr);
+    if (!captured && n == 0 && !reply.empty()) nats_status(reply, 503, "No Responders");
+  }
+
+  void nats_ack(const std::string& subject, const std::string& body) {
+    auto t = split_on(subject, '.');
+    std::string st, cn, sseq;
+    if (t.size() == 9) {
+      st = t[2], cn = t[3], sseq = t[5];
+    } else if (t.size() >= 11) {
+      st = t[4], cn = t[5], sseq = t[7];
+    } else {
+      return;
+    }
+    int64_t seq = strtoll(sseq.c_str(), nullptr, 10);
+    try {
+      if (body.empty() || starts_with(body, "+ACK") || starts_with(body, "+NXT")) {
+        eng_.ack(st, cn, seq);
+      } else if (starts_with(body, "-NAK")) {
+        double delay = 0.0;
+        size_t b = body.find('{');
+        if (b != std::string::npos) {
+          try {
+            mp::Value d = json::parse(body.substr(b));
+            if (auto v = d.get("delay")) delay = v->as_double() / 1e9;
+          } catch (std::exception&) {
+          }
+        }
+        eng_.nak(st, cn, seq, delay, wall_now());
+      } else if (starts_with(body, "+TERM")) {
+        eng_.ack(st, cn, seq, "term");
+      } else if (starts_with(body, "+WPI")) {
+        eng_.touch(st, cn, seq, wall_now());
+      }
+    } catch (bus::BusError&) {  // ack for a deleted consumer / unknown seq: ignored, as nats-server does
+    }
+  }
+
+  std::string ack_subject(const std::string& stream, const std::string& durable, const bus::Delivery& d) {
+    int64_t cseq = ++cseq_[{stream, durable}];
+    return "$JS.ACK." + stream + "." + durable + "." + std::to_string(d.num_delivered) + "." +
+           std::to_string(d.msg->seq) + "." + std::to_string(cseq) + "." +
+           std::to_string((int64_t)(d.msg->ts * 1e9)) + ".0";
+  }
+
+  int nats_deliver(const std::string& to, const std::string& stream, const std::string& durable,
+                   const bus::Delivery& d) {
+    return nats_route(to, d.msg->data, ack_subject(stream, durable, d), encode_headers(d.msg->headers));
+  }
+
+  static mp::Value api_error(int code, int err, const std::string& desc) {
+    mp::Value e = mp::Value::map();
+    e.put("code", mp::Value::integer(code));
+    e.put("err_code", mp::Value::integer(err));
+    e.put("description", mp::Value::str(desc));
+    mp::Value v = mp::Value::map();
+    v.put("error", std::move(e));
+    return v;
+  }
+
+  mp::Value stream_json(const std::string& name) {
+    bus::Stream& st = eng_.stream(name);
+    mp::Value cfg = mp::Value::map();
+    cfg.put("name", mp::Value::str(st.cfg.name));
+    mp::Value subs = mp::Value::arr();
+    for (auto& x : st.cfg.subjects) subs.push(mp::Value::str(x));
+    cfg.put("subjects", std::move(subs));
+    cfg.put("retention", mp::Value::str("limits"));
+    cfg.put("max_consumers", mp::Value::integer(-1));
+    cfg.put("max_msgs", mp::Value::integer(st.cfg.max_msgs));
+    cfg.put("max_bytes", mp::Value::integer(st.cfg.max_bytes));
+    cfg.put("max_age", mp::Value::integer((int64_t)(st.cfg.max_age * 1e9)));
+    cfg.put("max_msg_size", mp::Value::integer(-1));
+    cfg.put("storage", mp::Value::str(st.cfg.storage));
+    cfg.put("discard", mp::Value::str("old"));
+    cfg.put("num_replicas", mp::Value::integer(1));
+    mp::Value state = mp::Value::map();
+    state.put("messages", mp::Value::integer(st.count));
+    state.put("bytes", mp::Value::integer(st.bytes));
+    state.put("first_seq", mp::Value::integer(st.first_seq));
+    state.put("last_seq", mp::Value::integer(st.last_seq));
+    state.put("consumer_count", mp::Value::integer((int64_t)st.consumers.size()));
+    mp::Value v = mp::Value::map();
+    v.put("type", mp::Value::str("io.nats.jetstream.api.v1.stream_info_response"));
+    v.put("config", std::move(cfg));
+    v.put("created", mp::Value::str("1970-01-01T00:00:00Z"));
+    v.put("state", std::move(state));
+    return v;
+  }
+
+  mp::Value consumer_json(const std::string& stream, const std::string& durable) {
+    mp::Value ci = eng_.consumer_info(stream, durable);
+    bus::Consumer& c = eng_.consumer(stream, durable);
+    auto num = [&](const char* k) { return ci.get(k)->as_int(); };
+    mp::Value cfg = mp::Value::map();
+    cfg.put("durable_name", mp::Value::str(durable));
+    cfg.put("name", mp::Value::str(durable));
+    cfg.put("ack_policy", mp::Value::str("explicit"));
+    cfg.put("deliver_policy", mp::Value::str(c.cfg.deliver_policy));
+    cfg.put("filter_subject", mp::Value::str(c.cfg.filter_subject));
+    cfg.put("ack_wait", mp::Value::integer((int64_t)(c.cfg.ack_wait * 1e9)));
+    cfg.put("max_deliver", mp::Value::integer(c.cfg.max_deliver));
+    cfg.put("max_ack_pending", mp::Value::integer(c.cfg.max_ack_pending));
+    cfg.put("replay_policy", mp::Value::str("instant"));
+    auto it = push_.find({stream, durable});
+    if (it != push_.end()) cfg.put("deliver_subject", mp::Value::str(it->second));
+    auto seqs = [](int64_t cs, int64_t ss) {
+      mp::Value v = mp::Value::map();
+      v.put("consumer_seq", mp::Value::integer(cs));
+      v.put("stream_seq", mp::Value::integer(ss));
+      return v;
+    };
+    mp::Value v = mp::Value::map();
+    v.put("type", mp::Value::str("io.nats.jetstream.api.v1.consumer_info_response"));
+    v.put("stream_name", mp::Value::str(stream));
+    v.put("name", mp::Value::str(durable));
+    v.put("created", mp::Value::str("1970-01-01T00:00:00Z"));
+    v.put("config", std::move(cfg));
+    auto cs = cseq_.find({stream, durable});
+    v.put("delivered", seqs(cs == cseq_.end() ? 0 : cs->second, num("delivered_seq")));
+    v.put("ack_floor", seqs(0, num("ack_floor")));
+    v.put("num_ack_pending", mp::Value::integer(num("num_ack_pending")));
+    v.put("num_redelivered", mp::Value::integer(num("num_redelivered")));
+    v.put("num_waiting", mp::Value::integer(0));
+    v.put("num_pending", mp::Value::integer(num("num_pending")));
+    return v;
+  }
+
+  void nats_api(const std::string& what, const std::string& body, const std::string& reply) {
+    mp::Value res;
+    bool answer = true;
+    try {
+      answer = nats_api_call(what, body, reply, res);
+    } catch (bus::BusError& e) {
+      std::string msg = e.what();
+      bool nf = msg.find("not found") != std::string::npos;
+      res = api_error(nf ? 404 : 400, nf ? (starts_with(msg, "consumer") ? 10014 : 10059) : 10058, msg);
+    } catch (std::exception& e) {
+      res = api_error(400, 10025, std::string("bad request: ") + e.what());
+    }
+    if (answer && !reply.empty()) nats_route(reply, json::dumps(res));
+  }
+
+  bus::StreamConfig stream_cfg_json(const mp::Value& d, const std::string& name) {
+    bus::StreamConfig cfg;
+    const mp::Value* v;
+    cfg.name = (v = d.get("name")) ? v->as_str() : name;
+    if ((v = d.get("subjects")) && v->t == mp::Value::ARR && !v->a.empty()) {
+      for (auto& x : v->a) cfg.subjects.push_back(x.as_str());
+    } else {
+      cfg.subjects.push_back(cfg.name);
+    }
+    cfg.max_age = (v = d.get("max_age")) && !v->is_nil() ? v->as_double() / 1e9 : 0.0;
+    cfg.max_msgs = (v = d.get("max_msgs")) && !v->is_nil() ? v->as_int() : -1;
+    cfg.max_bytes = (v = d.get("max_bytes")) && !v->is_nil() ? v->as_int() : -1;
+    cfg.storage = (v = d.get("storage")) && v->t == mp::Value::STR ? v->s : std::string("file");
+    return cfg;
+  }
+
+  // false: nothing to answer now (pull requests answer with deliveries / status frames)
+  bool nats_api_call(const std::string& what, const std::string& body, const std::string& reply, mp::Value& res) {
+    auto t = split_on(what, '.');
+    mp::Value req = mp::Value::map();
+    size_t b0 = body.find_first_not_of(" \t\r\n");
+    if (b0 != std::string::npos && body[b0] == '{') req = json::parse(body);
+    auto tok = [&](size_t k) -> const std::string& {
+      if (k >= t.size()) throw std::runtime_error("missing name in " + what);
+      return t[k];
+    };
+    if (t[0] == "INFO") {
+      res = mp::Value::map();
+      res.put("type", mp::Value::str("io.nats.jetstream.api.v1.account_info_response"));
+      res.put("streams", mp::Value::integer((int64_t)eng_.streams.size()));
+      return true;
+    }
+    if (t[0] == "STREAM") {
+      const std::string& op = tok(1);
+      if (op == "NAMES" || op == "LIST") {
+        const mp::Value* sv = req.get("subject");
+        std::string subj = sv && sv->t == mp::Value::STR ? sv->s : std::string();
+        mp::Value names = mp::Value::arr();
+        for (auto& nm : eng_.order) {
+          bool hit = subj.empty();
+          for (auto& p : eng_.stream(nm).cfg.subjects)
+            hit = hit || bus::subject_matches(p, subj) || bus::subject_matches(subj, p);
+          if (hit) names.push(op == "LIST" ? stream_json(nm) : mp::Value::str(nm));
+        }
+        res = mp::Value::map();
+        res.put("total", mp::Value::integer((int64_t)names.a.size()));
+        res.put("offset", mp::Value::integer(0));
+        res.put("limit", mp::Value::integer(1024));
+        res.put("streams", std::move(names));
+        return true;
+      }
+      const std::string& name = tok(2);
+      if (op == "INFO") {
+        res = stream_json(name);
+      } else if (op == "CREATE" || op == "UPDATE") {
+        if (op == "UPDATE") eng_.stream(name);  // must exist
+        eng_.add_or_update_stream(stream_cfg_json(req, name));
+        res = stream_json(name);
+      } else if (op == "DELETE") {
+        for (auto it = push_.begin(); it != push_.end();) it = it->first.first == name ? push_.erase(it) : std::next(it);
+        eng_.delete_stream(name);
+        res = mp::Value::map();
+        res.put("success", mp::Value::boolean(true));
+      } else {
+        throw std::runtime_error("unsupported API " + what);
+      }
+      return true;
+    }
+    if (t[0] == "CONSUMER") {
+      const std::string& op = tok(1);
+      if (op == "CREATE" || op == "DURABLE") {
+        std::string stream, name;
+        if (op == "DURABLE") {  // DURABLE.CREATE.<stream>.<durable>
+          stream = tok(3);
+          name = tok(4);
+        } else {  // CREATE.<stream>[.<consumer>[.<filter>]]
+          stream = tok(2);
+          if (t.size() > 3) name = t[3];
+        }
+        const mp::Value* c = req.get("config");
+        mp::Value empty = mp::Value::map();
+        if (!c || c->t != mp::Value::MAP) c = &empty;
+        const mp::Value* v;
+        std::string durable = (v = c->get("durable_name")) && v->t == mp::Value::STR ? v->s
+                              : (v = c->get("name")) && v->t == mp::Value::STR ? v->s : name;
+        if (durable.empty()) throw std::runtime_error("ephemeral consumers are not supported");
+        bus::ConsumerConfig cc;
+        cc.durable = durable;
+        if ((v = c->get("filter_subject")) && v->t == mp::Value::STR && !v->s.empty()) cc.filter_subject = v->s;
+        if ((v = c->get("ack_wait")) && !v->is_nil()) cc.ack_wait = v->as_double() / 1e9;
+        if ((v = c->get("max_deliver")) && !v->is_nil()) cc.max_deliver = v->as_int();
+        if ((v = c->get("deliver_policy")) && v->t == mp::Value::STR &&
+            (v->s == "all" || v->s == "new" || v->s == "last"))
+          cc.deliver_policy = v->s;
+        if ((v = c->get("max_ack_pending")) && !v->is_nil() && v->as_int() > 0) cc.max_ack_pending = v->as_int();
+        eng_.add_consumer(stream, cc);
+        if ((v = c->get("deliver_subject")) && v->t == mp::Value::STR && !v->s.empty())
+          push_[{stream, durable}] = v->s;
+        res = consumer_json(stream, durable);
+        return true;
+      }
+      if (op == "INFO") {
+        res = consumer_json(tok(2), tok(3));
+        return true;
+      }
+      if (op == "DELETE") {
+        push_.erase({tok(2), tok(3)});
+        eng_.delete_consumer(tok(2), tok(3));
+        res = mp::Value::map();
+        res.put("success", mp::Value::boolean(true));
+        return true;
+      }
+      if (op == "MSG" && tok(2) == "NEXT") {
+        nats_pull(tok(3), tok(4), body, req, reply);
+        return false;
+      }
+    }
+    throw std::runtime_error("unsupported API " + what);
+  }
+
+  void nats_pull(const std::string& stream, const std::string& durable, const std::string& body,
+                 const mp::Value& req, const std::string& reply) {
+    if (reply.empty()) return;
+    eng_.consumer(stream, durable);  // BusError -> error JSON to the requester
+    NWaiter w;
+    w.reply = reply;
+    w.stream = stream;
+    w.durable = durable;
+    int64_t batch = 1;
+    double expires = 0.0;
+    bool no_wait = false;
+    const mp::Value* v;
+    if (req.t == mp::Value::MAP && !req.m.empty()) {
+      if ((v = req.get("batch")) && !v->is_nil()) batch = v->as_int();
+      if ((v = req.get("expires")) && !v->is_nil()) expires = v->as_double() / 1e9;
+      if ((v = req.get("no_wait"))) no_wait = v->t == mp::Value::BOOL ? v->b : v->as_int() != 0;
+    } else {
+      size_t b0 = body.find_first_not_of(" \t\r\n");
+      if (b0 != std::string::npos) batch = strtoll(body.c_str() + b0, nullptr, 10);
+    }
+    w.batch = std::max<int64_t>(1, batch);
+    w.no_wait = no_wait || expires <= 0;
+    double now = wall_now();
+    w.deadline = now + (w.no_wait ? 0.0 : expires);
+    if (!serve_pull(w, now)) nwaiters_.push_back(std::move(w));
+  }
+
+  // true = the pull request is finished (filled, or answered with a status frame)
+  bool serve_pull(NWaiter& w, double now) {
+    auto got = eng_.next_batch(w.stream, w.durable, w.batch - w.sent, now);
+    for (auto& d : got) nats_deliver(w.reply, w.stream, w.durable, d);
+    w.sent += (int64_t)got.size();
+    if (w.sent >= w.batch) return true;
+    if (w.no_wait) {  // what was there has been sent: end the request
+      nats_status(w.reply, 404, "No Messages");
+      return true;
+    }
+    if (now >= w.deadline) {
+      nats_status(w.reply, 408, "Request Timeout");
+      return true;
+    }
+    return false;
+  }
+
+  void serve_nats(double now) {
+    for (auto it = nwaiters_.begin(); it != nwaiters_.end();) {
+      bool done;
+      try {
+        done = serve_pull(*it, now);
+      } catch (std::exception&) {
+        nats_status(it->reply, 409, "Consumer Deleted");
+        done = true;
+      }
+      it = done ? nwaiters_.erase(it) : std::next(it);
+    }
+    for (auto it = push_.begin(); it != push_.end();) {
+      const std::string& st = it->first.first;
+      const std::string& du = it->first.second;
+      try {
+        if (nats_has_subscriber(it->second)) {
+          auto got = eng_.next_batch(st, du, 256, now);
+          for (auto& d : got)
+            if (nats_deliver(it->second, st, du, d) == 0) eng_.nak(st, du, d.msg->seq, 0.0, now);
+        }
+        ++it;
+      } catch (std::exception&) {
+        it = push_.erase(it);  // consumer / stream gone
+      }
+    }
+  }
+
   bus::Engine& eng_;
   Journal* jr_;
   double max_age_;
@@ -875,6 +1478,18 @@ class Server {
   std::vector<int> listeners_;
   std::unordered_map<uint64_t, Conn> conns_;
   std::list<Waiter> waiters_;
+  std::list<NWaiter> nwaiters_;
+  using QMember = std::pair<const std::string*, std::pair<Conn*, const std::string*>>;  // queue, (conn, sid)
+  std::vector<QMember> route_q_;
+  std::map<std::pair<std::string, std::string>, std::string> push_;  // push consumer -> deliver subject
+  std::map<std::pair<std::string, std::string>, int64_t> cseq_;      // consumer sequence (ack subjects)
+  uint64_t rr_ = 0;                                                   // queue-group round robin
+  std::string server_id_ = "NSMSGATEBUSD" + std::to_string(getpid());
+
+ public:
+  int nats_port_ = 4222;
+
+ private:
   uint64_t next_id_ = 0;
   double last_expire_ = 0;
 };
@@ -882,7 +1497,7 @@ class Server {
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::vector<std::string> listens;
+  std::vector<std::string> listens, nats_listens;
   std::string data_dir, fsync_mode = "interval";
   double max_age = 3 * 24 * 3600.0, fsync_interval = 0.05;
   int64_t compact_bytes = 256ll << 20;
@@ -893,18 +1508,19 @@ int main(int argc, char** argv) {
       return argv[++k];
     };
     if (a == "--listen") listens.push_back(val());
+    else if (a == "--nats-listen") nats_listens.push_back(val());
     else if (a == "--data") data_dir = val();
     else if (a == "--max-age") max_age = atof(val().c_str());
     else if (a == "--fsync") fsync_mode = val();
     else if (a == "--fsync-interval") fsync_interval = atof(val().c_str());
     else if (a == "--compact-bytes") compact_bytes = atoll(val().c_str());
     else if (a == "-h" || a == "--help") {
-      printf("usage: smsgate-busd --listen URL [--listen URL] [--data DIR] [--max-age S] "
+      printf("usage: smsgate-busd --listen URL [--listen URL] [--nats-listen tcp://HOST:PORT] [--data DIR] [--max-age S] "
              "[--fsync interval|always|never] [--fsync-interval S] [--compact-bytes N]\n");
       return 0;
     } else die("unknown argument " + a);
   }
-  if (listens.empty()) listens.push_back("tcp://127.0.0.1:4222");
+  if (listens.empty() && nats_listens.empty()) listens.push_back("tcp://127.0.0.1:4222");
   if (fsync_mode != "interval" && fsync_mode != "always" && fsync_mode != "never") die("bad --fsync " + fsync_mode);
 
   struct sigaction sa{};
@@ -929,8 +1545,14 @@ int main(int argc, char** argv) {
     int p = srv.listen_on(l);
     if (p >= 0 && tcp_port < 0) tcp_port = p;
   }
-  if (tcp_port >= 0) printf("READY %d\n", tcp_port);
-  else printf("READY -\n");
+  int nats_port = -1;
+  for (auto& l : nats_listens) {
+    int p = srv.listen_on(l, true);
+    if (p >= 0 && nats_port < 0) nats_port = srv.nats_port_ = p;
+  }
+  std::string ready = tcp_port >= 0 ? "READY " + std::to_string(tcp_port) : std::string("READY -");
+  if (nats_port >= 0) ready += " NATS " + std::to_string(nats_port);
+  printf("%s\n", ready.c_str());
   fflush(stdout);
   srv.run();
   return 0;

@@ -45,15 +45,27 @@ inline std::vector<std::string> split_tokens(const std::string& s) {
 }
 
 // NATS-style: ``*`` = one token, ``>`` = one or more trailing tokens (base.py:132-145).
+// Walks both strings token by token without allocating (the NATS front-end matches
+// every routed message against every subscription).
 inline bool subject_matches(const std::string& pattern, const std::string& subject) {
-  if (pattern == subject || pattern == ">") return true;
-  auto pt = split_tokens(pattern), st = split_tokens(subject);
-  for (size_t i = 0; i < pt.size(); ++i) {
-    if (pt[i] == ">") return st.size() > i;
-    if (i >= st.size()) return false;
-    if (pt[i] != "*" && pt[i] != st[i]) return false;
+  if (pattern == subject) return true;
+  const size_t P = pattern.size(), S = subject.size();
+  size_t i = 0, j = 0;
+  for (;;) {
+    size_t pe = pattern.find('.', i);
+    if (pe == std::string::npos) pe = P;
+    const size_t pl = pe - i;
+    if (pl == 1 && pattern[i] == '>') return j <= S;  // >= 1 subject token left
+    if (j > S) return false;                          // subject has fewer tokens
+    size_t se = subject.find('.', j);
+    if (se == std::string::npos) se = S;
+    if (!(pl == 1 && pattern[i] == '*') && (pl != se - j || pattern.compare(i, pl, subject, j, pl) != 0))
+      return false;
+    const bool pend = pe == P, send = se == S;
+    if (pend || send) return pend && send;
+    i = pe + 1;
+    j = se + 1;
   }
-  return pt.size() == st.size();
 }
 
 struct StreamConfig {
@@ -371,6 +383,16 @@ class Engine {
       if (m && matches(c.cfg.filter_subject, m->subject)) ++n;
     }
     c.num_pending = n;
+  }
+
+  void delete_stream(const std::string& name) {
+    stream(name);  // throws if missing
+    streams.erase(name);
+    order.erase(std::remove(order.begin(), order.end(), name), order.end());
+    clear_caches();
+    mp::Value a = mp::Value::arr();
+    a.push(mp::Value::str(name));
+    log("delstream", std::move(a));
   }
 
   void delete_consumer(const std::string& s, const std::string& d) {

@@ -1,5 +1,7 @@
-"""NATS wire-protocol compatibility: NatsBus client <-> NatsFrontend broker.
+"""NATS wire-protocol compatibility: NatsBus client <-> NATS front-end broker.
 
+Every test runs against both front-ends: the Python one (``NatsFrontend`` on the
+in-process engine) and the C++ one (``smsgate-busd --nats-listen``).
 Both sides are ours (nats-py and nats-server are not on the image), so the raw
 protocol tests below also drive the front-end with hand-written frames the way
 the reference's nats-py services would (push durable consumer, ``$JS.ACK``
@@ -18,18 +20,40 @@ from smsgate_amd.bus import nats_proto as P
 from smsgate_amd.bus.base import BusError
 from smsgate_amd.bus.nats_client import NatsBus
 from smsgate_amd.bus.nats_server import NatsFrontend
+from smsgate_amd.native import BUSD, available, spawn_busd
 
 
-async def _start():
+class _Busd:
+    """smsgate-busd with only a NATS listener, shaped like NatsFrontend (async close)."""
+
+    def __init__(self) -> None:
+        self.broker = spawn_busd([], None, nats_listen="tcp://127.0.0.1:0")
+        self.port = self.broker.nats_port
+
+    async def close(self) -> None:
+        self.broker.stop()
+
+
+@pytest.fixture(params=["python", "busd"])
+def kind(request):
+    if request.param == "busd" and not available(BUSD):
+        pytest.skip("smsgate-busd not built")
+    return request.param
+
+
+async def _start(kind="python"):
+    if kind == "busd":
+        fe = _Busd()
+        return None, fe, fe.port
     broker = MemoryBus()
     fe = NatsFrontend(broker)
     port = await fe.start("127.0.0.1", 0)
     return broker, fe, port
 
 
-def test_publish_fetch_ack_nak_term(arun):
+def test_publish_fetch_ack_nak_term(arun, kind):
     async def go():
-        broker, fe, port = await _start()
+        broker, fe, port = await _start(kind)
         nb = await connect(f"nats://127.0.0.1:{port}")
         assert isinstance(nb, NatsBus) and await nb.ping()
         si = await nb.ensure_stream()
@@ -66,9 +90,9 @@ def test_publish_fetch_ack_nak_term(arun):
     arun(go())
 
 
-def test_competing_consumers_share_a_durable(arun):
+def test_competing_consumers_share_a_durable(arun, kind):
     async def go():
-        broker, fe, port = await _start()
+        broker, fe, port = await _start(kind)
         a = await connect(f"nats://127.0.0.1:{port}")
         b = await connect(f"nats://127.0.0.1:{port}")
         await a.publish_many([(SUBJECT_PARSED, str(i).encode()) for i in range(40)])
@@ -88,9 +112,9 @@ def test_competing_consumers_share_a_durable(arun):
     arun(go())
 
 
-def test_publish_to_uncaptured_subject_and_errors(arun):
+def test_publish_to_uncaptured_subject_and_errors(arun, kind):
     async def go():
-        broker, fe, port = await _start()
+        broker, fe, port = await _start(kind)
         nb = await connect(f"nats://127.0.0.1:{port}")
         with pytest.raises(BusError):
             await nb.publish("not.a.stream", b"x")
@@ -113,11 +137,11 @@ async def _raw(port):
     return r, w
 
 
-def test_raw_protocol_push_consumer_like_nats_py(arun):
+def test_raw_protocol_push_consumer_like_nats_py(arun, kind):
     """What nats-py's ``js.subscribe(subject, durable=...)`` + ``msg.ack()`` sends."""
 
     async def go():
-        broker, fe, port = await _start()
+        broker, fe, port = await _start(kind)
         r, w = await _raw(port)
         w.write(b"SUB _INBOX.me.* 1\r\n")
         # stream lookup by subject, then a push durable on a deliver inbox
@@ -140,8 +164,10 @@ def test_raw_protocol_push_consumer_like_nats_py(arun):
         w.write(P.pub_bytes(dlv.args[2], b"+ACK"))
         await w.drain()
         await asyncio.sleep(0.05)
-        ci = broker.engine.consumer_info("SMS", "parser_worker_dlq")
+        nb = await connect(f"nats://127.0.0.1:{port}")
+        ci = await nb.consumer_info("SMS", "parser_worker_dlq")
         assert ci.num_ack_pending == 0 and ci.ack_floor == 1
+        await nb.close()
         # core request/reply between two plain clients
         r2, w2 = await _raw(port)
         w2.write(b"SUB svc.echo 7\r\n")
@@ -160,7 +186,7 @@ def test_raw_protocol_push_consumer_like_nats_py(arun):
     arun(go())
 
 
-def test_parser_stage_over_nats(arun):
+def test_parser_stage_over_nats(arun, kind):
     """The unchanged parser stage running on the nats:// bus."""
     from smsgate_amd.models import RawSMS
     from smsgate_amd.parse import ParsePipeline
@@ -168,7 +194,7 @@ def test_parser_stage_over_nats(arun):
     from smsgate_amd.services.parser import ParserWorker
 
     async def go():
-        broker, fe, port = await _start()
+        broker, fe, port = await _start(kind)
         nb = await connect(f"nats://127.0.0.1:{port}")
         body = REFERENCE_CASES[0][0]
         raw = RawSMS(msg_id="n1", device_id="d", sender="BANK", date="2025-05-06T00:00:00", body=body, source="device")
@@ -195,9 +221,9 @@ def _free_port():
     return p
 
 
-def test_broker_process_crash_recovery_over_nats(tmp_path, arun):
-    """bus-server subprocess (journaled) + NATS clients: kill -9 mid-stream, restart,
-    unacked and unread messages are still there."""
+def test_broker_process_crash_recovery_over_nats(tmp_path, arun, kind):
+    """bus-server subprocess (journaled; ``--native`` = smsgate-busd) + NATS clients:
+    kill -9 mid-stream, restart, unacked and unread messages are still there."""
     import os
     import signal
     import subprocess
@@ -210,7 +236,8 @@ def test_broker_process_crash_recovery_over_nats(tmp_path, arun):
     def start():
         return subprocess.Popen([sys.executable, "-m", "smsgate_amd", "bus-server", "--listen",
                                  f"tcp://127.0.0.1:{mport}", "--nats-listen", f"tcp://127.0.0.1:{nport}",
-                                 "--data", str(tmp_path / "bus")], cwd=root,
+                                 "--data", str(tmp_path / "bus")] + (["--native"] if kind == "busd" else []),
+                                cwd=root,
                                 stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
 
     async def connect_retry():

@@ -11,6 +11,7 @@
 #   profile   rocprofv3 kernel stats of bench.py    -> gpurun_out/prof/
 #   latency   Poisson serving latency, trained weights, spec on/off -> gpurun_out/latency_spec{0,4}.json
 #   curve     extractor training curve (held-out accuracy) -> gpurun_out/curve.log
+#   worst     bench.py with random-init weights (every answer runs to the field caps) -> gpurun_out/bench_random.log
 # Extra bench.py arguments can be passed in BENCH_ARGS.
 set -o pipefail
 mkdir -p gpurun_out
@@ -39,6 +40,9 @@ for stage in "$@"; do
         timeout -k 10 400 python -u scripts/latency_bench.py --weights train --spec-k $k --rates 1000,2000,6000,10000,14000 --seconds 4 --out gpurun_out/latency_spec$k.json > gpurun_out/latency_spec$k.log 2>&1
         rc=$?; grep offered gpurun_out/latency_spec$k.log | cut -c1-150; [ $rc -eq 0 ] || break
       done ;;
+    worst)
+      timeout -k 10 600 python -u bench.py --weights random --eval-n 0 $BENCH_ARGS > gpurun_out/bench_random.log 2>&1
+      rc=$?; tail -1 gpurun_out/bench_random.log | cut -c1-400 ;;
     curve)
       timeout -k 10 900 python -u scripts/train_curve.py $CURVE_ARGS > gpurun_out/curve.log 2>&1
       rc=$?; grep '"step"' gpurun_out/curve.log | cut -c1-300 ;;

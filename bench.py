@@ -98,6 +98,8 @@ def _args(argv=None):
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--spec-policy", type=int, default=0, help="draft policy (EngineConfig.spec_policy)")
+    p.add_argument("--gemm-rule-only", action="store_true",
+                   help="ignore the measured GEMM tile exceptions (ops.GEMM_MEASURED), A/B only")
     p.add_argument("--spec-k", type=int, default=4, help="speculative decoding: drafts per row per step (0 = off)")
     p.add_argument("--spec-frac", type=float, default=1.25, help="draft budget per step, x decode rows")
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
@@ -343,6 +345,10 @@ async def _run_cpu(args):
 
 def main(argv=None) -> int:
     args = _args(argv)
+    if args.gemm_rule_only:
+        from smsgate_amd import ops
+
+        ops.GEMM_MEASURED.clear()
     rank, world, local = _rank_env()
     if args.backend == "local_llm" or args.cpu_echo_engine:
         dt, counts, init_s, estats, prov, quality = run_replica(args, rank, world, local)

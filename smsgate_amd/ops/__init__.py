@@ -210,10 +210,28 @@ GEMM_MIN_TILES = int(os.environ.get("SMSGATE_GEMM_MIN_TILES", "480"))
 GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 
 
-def gemm_cfg(M: int, N: int, min_tiles: Optional[int] = None) -> int:
-    """Tile config for an M×N output: the biggest tile that still gives ≳2 blocks per CU
+# Measured exceptions to the tile rule below (scripts/gemm_tune.py, interleaved rounds,
+# profiles/r02_gemm_tune.json), keyed by (epilogue, N, K): [(M_lo, M_hi, cfg)].
+#   SwiGLU gate/up 3072x576: 256x256 8-wave tiles at 4608 rows (26.7 vs 28.4 us) and at
+#     prefill halves of 16384 (73.9 vs 80.3 us); 128x128 stays best at 9216 (47.5 vs 49.4).
+#   o-proj 576x576 + residual: 64x64 tiles at 9216 rows (14.3 vs 15.9 us).
+# End to end the bench is unchanged within noise (27 571 vs 27 491 msgs/s, three
+# interleaved runs each, profiles/r02_gemm_measured_ab.jsonl).
+GEMM_MEASURED = {
+    ("swiglu", 3072, 576): [(4096, 6144, 10), (12288, 1 << 30, 10)],
+    ("resid", 576, 576): [(8192, 10240, 3)],
+} if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
+
+
+def gemm_cfg(M: int, N: int, min_tiles: Optional[int] = None, epi: Optional[str] = None,
+              K: Optional[int] = None) -> int:
+    """Tile config for an M×N output: a measured exception for (``epi``, N, ``K``) at this
+    M (:data:`GEMM_MEASURED`), else the biggest tile that still gives ≳2 blocks per CU
     (256 CUs), else the config with the most blocks (the 32-row tile only for M <=
     ``GEMM_SMALL_M``)."""
+    for lo, hi, c in GEMM_MEASURED.get((epi, N, K), ()):
+        if lo <= M <= hi:
+            return c
     min_tiles = GEMM_MIN_TILES if min_tiles is None else min_tiles
     best, best_tiles = -1, -1
     # the 4-wave configs; 8-wave ones and the 4-stage 32-row tile are explicit opt-ins
@@ -267,7 +285,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Opti
         raise ValueError("gemm: bad output")
     if M == 0:
         return out
-    c = gemm_cfg(M, N) if cfg is None else cfg
+    c = gemm_cfg(M, N, epi=epi, K=K) if cfg is None else cfg
     rc = load_library().sg_gemm(_p(a), a.stride(0), _p(w), _p(out), out.stride(0), _p(resid),
                                 0 if resid is None else resid.stride(0), M, N, K, e, int(norm_eps is not None),
                                 float(norm_eps or 0.0), c, _stream())

@@ -288,3 +288,49 @@ def test_broker_process_crash_recovery_over_nats(tmp_path, arun, kind):
         except ProcessLookupError:
             pass
         proc.wait(10)
+
+
+def test_queue_groups_headers_and_no_wait_status(arun, kind):
+    """Core queue groups share a subject's messages; headers survive JetStream capture
+    and come back on delivery; a partially filled no_wait pull ends with a 404 status."""
+
+    async def go():
+        broker, fe, port = await _start(kind)
+        r1, w1 = await _raw(port)
+        r2, w2 = await _raw(port)
+        for w in (w1, w2):
+            w.write(b"SUB jobs.* workers 1\r\nPING\r\n")
+        for r in (r1, r2):
+            assert (await P.read_frame(r)).op == "PONG"
+        pub, wp = await _raw(port)
+        for i in range(20):
+            wp.write(P.pub_bytes(f"jobs.{i}", str(i).encode()))
+        wp.write(b"PING\r\n")
+        await wp.drain()
+        assert (await P.read_frame(pub)).op == "PONG"
+        got = []
+        for r in (r1, r2):
+            while True:
+                try:
+                    f = await asyncio.wait_for(P.read_frame(r), 0.3)
+                except asyncio.TimeoutError:
+                    break
+                got.append(int(f.payload))
+        assert sorted(got) == list(range(20))  # each message to exactly one group member
+        nb = await connect(f"nats://127.0.0.1:{port}")
+        await nb.publish(SUBJECT_RAW, b"with-headers", headers={"Nats-Msg-Id": "m-1", "X-Trace": "abc"})
+        await nb.publish(SUBJECT_RAW, b"plain")
+        sub = await nb.subscribe(SUBJECT_RAW, "hdr")
+        t0 = asyncio.get_running_loop().time()
+        msgs = await sub.fetch(10, 1.0)  # 2 available: the no_wait pull must end at once (404)
+        assert asyncio.get_running_loop().time() - t0 < 0.5
+        assert [m.data for m in msgs] == [b"with-headers", b"plain"]
+        assert msgs[0].headers == {"Nats-Msg-Id": "m-1", "X-Trace": "abc"} and not msgs[1].headers
+        for m in msgs:
+            await m.ack()
+        await nb.close()
+        for w in (w1, w2, wp):
+            w.close()
+        await fe.close()
+
+    arun(go())

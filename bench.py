@@ -98,6 +98,8 @@ def _args(argv=None):
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--spec-policy", type=int, default=0, help="draft policy (EngineConfig.spec_policy)")
+    p.add_argument("--no-producer-norm", action="store_true",
+                   help="norm GEMMs accumulate x^2 themselves instead of reading the producer's row partials")
     p.add_argument("--gemm-rule-only", action="store_true",
                    help="ignore the measured GEMM tile exceptions (ops.GEMM_MEASURED), A/B only")
     p.add_argument("--spec-k", type=int, default=4, help="speculative decoding: drafts per row per step (0 = off)")
@@ -168,6 +170,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               prefill_key_split=args.prefill_key_split,
                               spec_k=args.spec_k, spec_policy=args.spec_policy, spec_draft_frac=args.spec_frac,
                               spec_max_rows=args.spec_max_rows,
+                              producer_norm=not args.no_producer_norm,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
     if not echo and args.eval_n and rank == 0:
@@ -176,7 +179,7 @@ def run_replica(args, rank: int, world: int, local: int):
         q = evaluate_engine(engine, n=args.eval_n, seed=4242, vocab_name="heldout")
         quality = {"parse_rate": round(q["parse_rate"], 4), "exact": round(q["exact"], 4), "n": q["n"],
                    "field_acc": {k: round(v, 4) for k, v in q["field_acc"].items()}, "vocab": "heldout"}
-        engine.stats.__init__()
+        (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
     if not args.no_gc_freeze:
         from smsgate_amd.serving import freeze_gc_for_launch_loop
 
@@ -197,7 +200,7 @@ def run_replica(args, rank: int, world: int, local: int):
 
     if args.warmup:  # (synchronised too: with a shared broker each rank's drain target needs a common start)
         coord.run_phase(seeds(0, args.warmup), per_w, sync=sync)
-    engine.stats.__init__()
+    (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
     if hasattr(engine, "spec_stats"):
         engine.spec_stats(reset=True)
     dt, counts = coord.run_phase(seeds(args.warmup, args.steps), per_w, sync=sync)

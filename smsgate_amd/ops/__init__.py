@@ -92,9 +92,9 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
                                   ctypes.c_uint, _vp]
     lib.sg_gemm.argtypes = [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                            _c_float, _c_int, _vp]
+                            _c_float, _c_int, _vp, _vp, _c_int, _vp]
     lib.sg_gemm_qkv_rope.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_float, _c_int, _ip, _ip, _vp, _vp, _vp,
-                                     _vp, _c_int, _c_int, _c_int, _c_int, _vp]
+                                     _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp]
     lib.sg_gemm_probe.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]
     lib.sg_gemm_probe.restype = _c_int
     lib.sg_gemm_set_group_m.argtypes = [_c_int]
@@ -115,7 +115,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_fsm_commit.argtypes = [_vp, _ip] + fsm_t + [_c_int] * 3 + [_ip] * 6 + [_c_int, _c_int, _vp]
     lib.sg_fsm_commit.restype = _c_int
     lib.sg_gemm_argmax.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int, _ip, _ip, _vp,
-                                   _vp, _vp]
+                                   _vp, _vp, _c_int, _vp]
     lib.sg_gemm_argmax.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
@@ -198,10 +198,13 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 
 GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 64), 5: (64, 64), 6: (64, 64),
               7: (128, 128), 8: (64, 128), 9: (256, 128), 10: (256, 256), 11: (128, 256), 12: (256, 64),
-              13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64)}
+              13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64),
+              19: (256, 256)}
 # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
-GEMM_SWIGLU_ONLY = {10}  # a 256x256 plain-output tile does not fit the LDS staging
+# a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
+# SwiGLU kernel (gemm256_swiglu_kernel)
+GEMM_SWIGLU_ONLY = {10, 19}
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
@@ -254,16 +257,42 @@ def gemm_set_group_m(gm: int) -> None:
     load_library().sg_gemm_set_group_m(int(gm))
 
 
+SS_PARTS = 16  # csrc/gemm_kernels.hip: x² partials per row (producer N tiles, zero-padded)
+
+
+def ss_buffer(M: int, device) -> torch.Tensor:
+    """Zeroed fp32 ``[SS_PARTS, M]`` row-partials image for ``gemm(ss_out=..)`` / ``ss_in``
+    (part-major: column ``m`` holds row ``m``'s partials)."""
+    return torch.zeros(SS_PARTS, M, dtype=torch.float32, device=device)
+
+
+def _ss_check(ss: Optional[torch.Tensor], M: int, name: str) -> int:
+    """Validates a row-partials image; returns its row capacity (0 for None)."""
+    if ss is None:
+        return 0
+    if ss.dtype != torch.float32 or ss.dim() != 2 or ss.stride(1) != 1 or ss.shape[0] != SS_PARTS \
+            or ss.shape[1] < M or not ss.is_cuda:
+        raise ValueError(f"{name}: fp32 [{SS_PARTS}, >= {M}] row partials required (ops.ss_buffer)")
+    return ss.stride(0)
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Optional[float] = None,
          resid: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-         cfg: Optional[int] = None) -> torch.Tensor:
+         cfg: Optional[int] = None, ss_in: Optional[torch.Tensor] = None,
+         ss_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused MFMA GEMM ``out = EPI(rowscale ⊙ (a @ w.T))`` (csrc/gemm_kernels.hip).
 
     ``a`` [M, K] (row stride may exceed K), ``w`` [N, K] bf16.  ``norm_eps``: apply
     RMSNorm to the rows of ``a`` (the norm weight must already be folded into
     ``w`` — :func:`fold_norm`).  ``epi``: ``store``; ``resid`` (``out = resid +
     result``; ``out`` defaults to ``resid`` itself, updated in place); ``swiglu``
-    (``w`` rows interleaved by :func:`interleave_gate_up`, output N/2 wide)."""
+    (``w`` rows interleaved by :func:`interleave_gate_up`, output N/2 wide).
+
+    ``ss_out`` (``epi='resid'`` only, :func:`ss_buffer`): receives, per N tile, the
+    sum of squares of each output row (as stored, bf16) — the next RMSNorm GEMM's
+    row scales; its other columns must stay zero.  ``ss_in`` (with ``norm_eps``):
+    such a buffer for the rows of ``a``; the GEMM sums its partials instead of
+    accumulating x² itself."""
     M, K = a.shape
     N = w.shape[0]
     if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
@@ -286,16 +315,26 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Opti
     if M == 0:
         return out
     c = gemm_cfg(M, N, epi=epi, K=K) if cfg is None else cfg
+    if ss_in is not None and norm_eps is None:
+        raise ValueError("gemm: ss_in needs norm_eps")
+    ld_in = _ss_check(ss_in, M, "gemm ss_in")
+    ld = _ss_check(ss_out, M, "gemm ss_out") or ld_in
+    if ss_out is not None and (e != 1 or N // GEMM_TILES[c][1] > SS_PARTS):
+        raise ValueError(f"gemm: ss_out needs epi='resid' and at most {SS_PARTS} N tiles")
+    if ss_in is not None and ss_out is not None and ld_in != ld:
+        raise ValueError("gemm: ss_in / ss_out row strides differ")
+    norm = 0 if norm_eps is None else (2 if ss_in is not None else 1)
     rc = load_library().sg_gemm(_p(a), a.stride(0), _p(w), _p(out), out.stride(0), _p(resid),
-                                0 if resid is None else resid.stride(0), M, N, K, e, int(norm_eps is not None),
-                                float(norm_eps or 0.0), c, _stream())
+                                0 if resid is None else resid.stride(0), M, N, K, e, norm,
+                                float(norm_eps or 0.0), c, _p(ss_in), _p(ss_out), ld, _stream())
     _check(rc, "gemm")
     return out
 
 
 def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tensor, slot: torch.Tensor,
                   cos_sin: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor, vt_cache: torch.Tensor,
-                  nh: int, nkv: int, p0: int, cfg: Optional[int] = None) -> None:
+                  nh: int, nkv: int, p0: int, cfg: Optional[int] = None,
+                  ss_in: Optional[torch.Tensor] = None) -> None:
     """``rope(rmsnorm(x) @ w.T)`` scattered into ``q_out`` and the KV cache (one fused
     kernel; ``w`` has the norm weight folded in).  Same result as :func:`gemm` +
     :func:`rope_qkv_cache`."""
@@ -318,9 +357,10 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
         # tiles up to 2048 rows (7.4 / 8.2 / 11.4 vs 10.1 / 10.7 / 12.3 us at 512 / 1024
         # / 2048, profiles/r01c_kbench_small_buckets.json)
         cfg = 17 if M <= 2 * GEMM_SMALL_M else 3
+    ld = _ss_check(ss_in, M, "gemm_qkv_rope ss_in")
     rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
-                                         _stream())
+                                         _p(ss_in), ld, _stream())
     _check(rc, "gemm_qkv_rope")
 
 
@@ -573,7 +613,8 @@ def spec_verify(logits: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.T
 
 
 def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, best: torch.Tensor,
-                norm_eps: Optional[float] = None, cfg: Optional[int] = None) -> torch.Tensor:
+                norm_eps: Optional[float] = None, cfg: Optional[int] = None,
+                ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
     """lm_head GEMM with the schema-FSM masked arg-max fused in (EPI 4): for every
     row, ``best[row] = max(argmax_key(bf16 logit, token))`` over the tokens its FSM
     state allows — no logits are written.  ``w`` [V, K] (final norm folded in when
@@ -592,9 +633,13 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, 
         return best
     if cfg is None:
         cfg = 0 if -(-M // 128) * (N // 128) >= 480 else (3 if M > 1024 else 17)
+    if ss_in is not None and norm_eps is None:
+        raise ValueError("gemm_argmax: ss_in needs norm_eps")
+    ld = _ss_check(ss_in, M, "gemm_argmax ss_in")
+    norm = 0 if norm_eps is None else (2 if ss_in is not None else 1)
     _check(load_library().sg_gemm_argmax(_p(a), a.stride(0), _p(w), M, N, K, float(norm_eps or 0.0),
-                                         int(norm_eps is not None), cfg, _p(row_state), _p(fsm.state_mask),
-                                         _p(fsm.masks), _p(best), _stream()), "gemm_argmax")
+                                         norm, cfg, _p(row_state), _p(fsm.state_mask),
+                                         _p(fsm.masks), _p(best), _p(ss_in), ld, _stream()), "gemm_argmax")
     return best
 
 

@@ -55,6 +55,24 @@ struct RopeArgs {
   int nh, nkv, Lmax, p0;
 };
 
+// Row scales computed by the PRODUCER of the activation (NORM 2).  An EPI 1 GEMM
+// (o-proj / down-proj: it writes the residual stream) with `ssout` set also writes,
+// per N tile, the fp32 sum of squares of each output row's bf16 values:
+// ssout[tile_n][row] in a zero-padded [SS_PARTS][ld] image (part-major: a tile's rows
+// are one contiguous run, so its partials leave as whole lines — a row-major image
+// had every N tile write 4 B into the same 64-B lines, +1 µs per GEMM).
+// The next RMSNorm GEMM (NORM 2) prefetches its rows' partials at kernel start — the
+// 4 lanes that share an output row read 4 parts each and combine with two shuffles
+// (fixed order: deterministic, no atomics) — instead of accumulating x² beside its
+// MFMAs, which every N tile and every wave column of the consumer would otherwise
+// redo for the same rows.
+constexpr int SS_PARTS = 16;  // max N tiles of a producer (hidden <= 16 x BN)
+struct NormArgs {
+  const float* ssin;  // [SS_PARTS][ld] partial sums of squares of the A rows (NORM 2)
+  float* ssout;       // [SS_PARTS][ld] partials of the output rows (EPI 1), or null
+  int ld;             // row capacity of the image (>= M)
+};
+
 // EPI 4 (lm_head + masked arg-max) arguments.
 struct ArgmaxArgs {
   const int* row_state;         // [M] FSM state of each row
@@ -112,7 +130,7 @@ __device__ __forceinline__ float sumsq_frag(const bf16x8& v, float acc) {
   return acc;
 }
 
-template <int FM, int FN, bool NORM>
+template <int FM, int FN, int NORM>
 __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], const uint16_t* as,
                                          const uint16_t* bs, int wm0, int wn0, int lane) {
 #pragma unroll
@@ -138,20 +156,23 @@ __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], 
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       // RMSNorm: the A fragment already holds 8 k-values of row (lane & 15) —
       // accumulate their squares (v_dot2_f32_bf16) in the MFMA shadow
-      if constexpr (NORM) ss[i] = sumsq_frag(af[i], ss[i]);
+      if constexpr (NORM == 1) ss[i] = sumsq_frag(af[i], ss[i]);
     }
   }
 }
 
 // PROBE (timing decomposition only, sg_gemm_probe): 1 = K-loop without MFMAs,
 // 2 = K-loop without the global->LDS loads (MFMAs on stale LDS), 3 = as 2 and no
-// prologue loads either, 4 = as 3 and no epilogue (nothing stored)
-template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST, int PROBE = 0>
+// prologue loads either, 4 = as 3 and no epilogue (nothing stored).
+// NORM: 0 none, 1 row scale from x² accumulated beside the MFMAs, 2 row scale from
+// the producer's partial sums (NormArgs).
+template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST, int PROBE = 0>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t* __restrict__ A, int lda,
                                                          const uint16_t* __restrict__ W,
                                                          uint16_t* C, int ldc, const uint16_t* R, int ldr,
                                                          int M, int N, int K, float eps, int tiles_m,
-                                                         int tiles_n, int gm, RopeArgs ra, ArgmaxArgs xa) {
+                                                         int tiles_n, int gm, RopeArgs ra, ArgmaxArgs xa,
+                                                         NormArgs na) {
   constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(EPI != 3 || BN == 64, "QKV+RoPE epilogue: one 64-wide head per N tile");
@@ -185,6 +206,18 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm0 = (wave / WN) * TM, wn0 = (wave % WN) * TN;
 
+  // NORM 2: the rows' x² partials, loaded before the K loop (consumed in the epilogue;
+  // the loop's counted waits retire them with the first tile's DMAs)
+  f32x4 ssv[FM];
+  if constexpr (NORM == 2) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = min(m0 + wm0 + i * 16 + (lane & 15), M - 1);
+      const float* sp = na.ssin + (size_t)((lane >> 4) * 4) * na.ld + row;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ssv[i][e] = sp[(size_t)e * na.ld];
+    }
+  }
   f32x4 acc[FM][FN];
   float ss[FM];
 #pragma unroll
@@ -261,8 +294,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     rsv[i] = 1.f;
-    if constexpr (NORM) {
+    if constexpr (NORM == 1) {
       float v = ss[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      rsv[i] = rsqrtf(v / (float)K + eps);
+    } else if constexpr (NORM == 2) {
+      float v = (ssv[i][0] + ssv[i][1]) + (ssv[i][2] + ssv[i][3]);
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       rsv[i] = rsqrtf(v / (float)K + eps);
@@ -383,33 +421,245 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   // ---- epilogue 2: coalesced 16-B row chunks (+ residual)
   constexpr int CPR = BNO / 8;  // chunks per row
   const int c0 = EPI == 2 ? n0 / 2 : n0;
+  if constexpr (EPI == 1) {
+    // the CPR chunks of a row are CPR consecutive lanes of one wave, and every lane
+    // runs the same trip count, so the row's x² partial reduces with shuffles
+    static_assert((BM * CPR) % NT == 0 && CPR <= 64, "uniform epilogue trips");
+    const bool want_ss = na.ssout != nullptr;
+    for (int q = tid; q < BM * CPR; q += NT) {
+      const int row = q / CPR, c = q % CPR;
+      const int gr = m0 + row;
+      float sq = 0.f;
+      if (gr < M) {
+        const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
+        const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + c0 + c * 8);
+        uint32_t a[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t b[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = bf2f(a[e] & 0xffffu) + bf2f(b[e] & 0xffffu);
+          const float hi = bf2f(a[e] >> 16) + bf2f(b[e] >> 16);
+          a[e] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          const float rl = bf2f(a[e] & 0xffffu), rh = bf2f(a[e] >> 16);  // the stored (rounded) values
+          sq = fmaf(rl, rl, fmaf(rh, rh, sq));
+        }
+        *reinterpret_cast<uint4*>(C + (size_t)gr * ldc + c0 + c * 8) = make_uint4(a[0], a[1], a[2], a[3]);
+      }
+      if (want_ss) {
+#pragma unroll
+        for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+        if (c == 0 && gr < M) na.ssout[(size_t)(n0 / BN) * na.ld + gr] = sq;
+      }
+    }
+    return;
+  }
   for (int q = tid; q < BM * CPR; q += NT) {
     const int row = q / CPR, c = q % CPR;
     const int gr = m0 + row;
     if (gr >= M) continue;
-    uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
-    uint16_t* dst = C + (size_t)gr * ldc + c0 + c * 8;
-    if constexpr (EPI == 1) {
-      const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + c0 + c * 8);
-      uint32_t a[4] = {v.x, v.y, v.z, v.w};
-      const uint32_t b[4] = {rr.x, rr.y, rr.z, rr.w};
+    const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
+    *reinterpret_cast<uint4*>(C + (size_t)gr * ldc + c0 + c * 8) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 256x256 SwiGLU GEMM, 8 waves in two STAGGERED groups (cdna_hip_programming.md §5
+// "256² 8-phase template", T3/T4/T5).  The 128²/2-barrier loop above tops out near
+// 0.85 PFLOP/s: all waves read LDS together, then all multiply together.  Here
+//
+//  * wave (wr, wc) owns rows wr·128 + [0,128) and the two 32-column gate|up pairs
+//    wc·32 + [0,32) ("lo", in W rows [0,128) of the tile) and 128 + wc·32 + [0,32)
+//    ("hi"), so every wave needs the lo B half first and the hi half one phase later;
+//  * a K-tile (BK 64) is four phases, one 64x32 quadrant (16 MFMAs) each:
+//      p1 rows 0-63 x lo   (reads A0 + Blo)      p2 rows 64-127 x lo (reads A1)
+//      p3 rows 64-127 x hi (reads Bhi)           p4 rows 0-63 x hi   (no LDS reads)
+//    and each phase stages ONE 16 KB half-tile of the next K-tile (A_top, A_bot,
+//    Blo, Bhi in p1..p4; 2 LDS-DMAs per wave) into the other of two 64 KB buffers;
+//  * group wr = 1 runs one barrier behind group 0, so on every SIMD one wave's
+//    MFMA cluster overlaps the other wave's LDS reads and DMA issue;
+//  * RAW: a counted vmcnt(2) at the end of p4's read section retires A_top, A_bot
+//    and Blo of the next tile (Bhi stays in flight), a vmcnt(4) at the end of p2
+//    retires Bhi before p3 reads it; every such wait precedes, in both groups, the
+//    barrier that precedes the first read.  WAR: a half-tile of tile t+1 is staged
+//    only after every wave's last read of the same half of tile t-1 (A: p2, Blo: p1,
+//    Bhi: p3; p4 reads nothing), which the lagging group completes two barriers
+//    before the leading group's DMA.
+// SwiGLU epilogue (EPI 2) with the row scale of NORM 0/1/2, as gemm_fused_kernel.
+template <int NORM>
+__global__ void __launch_bounds__(512) gemm256_swiglu_kernel(const uint16_t* __restrict__ A, int lda,
+                                                            const uint16_t* __restrict__ W, uint16_t* C, int ldc,
+                                                            int M, int N, int K, float eps, int tiles_m, int tiles_n,
+                                                            int gm, NormArgs na) {
+  constexpr int BM = 256, BN = 256, HALF = 128 * BK;  // elements per half-tile
+  constexpr int BUF = 4 * HALF;                        // A_top, A_bot, Blo, Bhi
+  constexpr int BNO = BN / 2, CST = BNO + 8;
+  static_assert(BM * CST <= 2 * BUF, "C staging fits");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF];
+
+  const int T = tiles_m * tiles_n;
+  const int orig = blockIdx.x, xcd = orig & 7, q8 = T >> 3, r8 = T & 7;
+  const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int gsz = gm * tiles_n, g = t / gsz, gl = t - g * gsz;
+  const int grows = min(gm, tiles_m - g * gm);
+  const int m0 = (g * gm + gl % grows) * BM;
+  const int n0 = (gl / grows) * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  f32x4 acc[8][4];  // [16-row frag i][col frag j]: j 0,1 = lo pair (gate, up), 2,3 = hi pair
+  float ss[8];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float lo = bf2f(a[e] & 0xffffu) + bf2f(b[e] & 0xffffu);
-        const float hi = bf2f(a[e] >> 16) + bf2f(b[e] >> 16);
-        a[e] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  for (int i = 0; i < 8; ++i) {
+    ss[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int KT = K / BK;
+  // half-tile h of K-tile kt into buffer b: A halves = A rows, B halves = W rows
+  auto stage = [&](int b, int h, int kt) {
+    const int kk = min(kt, KT - 1) * BK;  // past the end: re-load the last tile (idle buffer, never read)
+    uint16_t* dst = smem + b * BUF + h * HALF;
+    if (h < 2) issue_tile<128, 8>(A, lda, m0 + h * 128, M - 1, kk, dst, wave, lane);
+    else issue_tile<128, 8>(W, K, n0 + (h - 2) * 128, N - 1, kk, dst, wave, lane);
+  };
+  // fragment reads: A frags of rows wr·128 + r0 + 16i, B frags of W rows wc·32 + 16j of half hb
+  bf16x8 a0[2][4], a1[2][4], bq[2][2];
+  auto read_a = [&](bf16x8 (&dst)[2][4], const uint16_t* base, int r0) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r0 + i * 16 + (lane & 15), ch = s2 * 4 + (lane >> 4);
+        dst[s2][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((ch ^ (row & 7)) << 3));
       }
-      v = make_uint4(a[0], a[1], a[2], a[3]);
+  };
+  auto read_b = [&](const uint16_t* base) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 32 + j * 16 + (lane & 15), ch = s2 * 4 + (lane >> 4);
+        bq[s2][j] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((ch ^ (row & 7)) << 3));
+      }
+  };
+  auto mfma_q = [&](bf16x8 (&af)[2][4], int i0, int j0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s2][j], af[s2][i], acc[i0 + i][j0 + j],
+                                                                        0, 0, 0);
+        if constexpr (NORM == 1)
+          if (j0 == 0) ss[i0 + i] = sumsq_frag(af[s2][i], ss[i0 + i]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mid = [&]() {  // end of a read section: barrier, then this wave's reads have landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  // prologue: K-tile 0 into buffer 0, then group 1 falls one barrier behind
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cb = kt & 1, nb = cb ^ 1;
+    const uint16_t* buf = smem + cb * BUF;
+    const uint16_t* abase = buf + wr * HALF;
+    // p1: rows 0-63 x lo
+    read_a(a0, abase, 0);
+    read_b(buf + 2 * HALF);
+    stage(nb, 0, kt + 1);
+    mid();
+    mfma_q(a0, 0, 0);
+    __builtin_amdgcn_s_barrier();
+    // p2: rows 64-127 x lo
+    read_a(a1, abase, 64);
+    stage(nb, 1, kt + 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // Bhi of THIS tile (staged in the previous p4) landed
+    mid();
+    mfma_q(a1, 4, 0);
+    __builtin_amdgcn_s_barrier();
+    // p3: rows 64-127 x hi
+    read_b(buf + 3 * HALF);
+    stage(nb, 2, kt + 1);
+    mid();
+    mfma_q(a1, 4, 2);
+    __builtin_amdgcn_s_barrier();
+    // p4: rows 0-63 x hi (A0 still in registers: no LDS reads)
+    stage(nb, 3, kt + 1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A_top, A_bot, Blo of the next tile landed
+    mid();
+    mfma_q(a0, 0, 2);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // row scales: lane holds rows wr·128 + 16i + (lane & 15)
+  float rsv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    rsv[i] = 1.f;
+    if constexpr (NORM == 1) {
+      float v = ss[i];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      rsv[i] = rsqrtf(v / (float)K + eps);
+    } else if constexpr (NORM == 2) {
+      const int row = min(m0 + wr * 128 + i * 16 + (lane & 15), M - 1);
+      const float* sp = na.ssin + (size_t)((lane >> 4) * 4) * na.ld + row;
+      float v = (sp[0] + sp[(size_t)na.ld]) + (sp[(size_t)2 * na.ld] + sp[(size_t)3 * na.ld]);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      rsv[i] = rsqrtf(v / (float)K + eps);
     }
-    *reinterpret_cast<uint4*>(dst) = v;
+  }
+  // SwiGLU into the staged bf16 tile: pair p (lo/hi) -> output cols p·64 + wc·16 + c4
+  uint16_t* Cs = smem;
+  const int c4 = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int col = p * 64 + wc * 16 + c4;
+      float h[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][2 * p][r] * rsv[i]) * (acc[i][2 * p + 1][r] * rsv[i]);
+      *reinterpret_cast<uint2*>(Cs + row * CST + col) =
+          make_uint2((uint32_t)f2bf(h[0]) | ((uint32_t)f2bf(h[1]) << 16),
+                     (uint32_t)f2bf(h[2]) | ((uint32_t)f2bf(h[3]) << 16));
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BNO / 8;
+  const int c0 = n0 / 2;
+  for (int q = tid; q < BM * CPR; q += 512) {
+    const int row = q / CPR, c = q % CPR;
+    const int gr = m0 + row;
+    if (gr >= M) continue;
+    *reinterpret_cast<uint4*>(C + (size_t)gr * ldc + c0 + c * 8) =
+        *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
   }
 }
 
 int g_group_m = 8;  // M-tiles per rasterisation group (sg_gemm_set_group_m)
 
-template <int BM, int BN, int WM, int WN, int EPI, bool NORM, int ST>
+template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST>
 int launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
-           float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}, const ArgmaxArgs& xa = ArgmaxArgs{}) {
+           float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}, const ArgmaxArgs& xa = ArgmaxArgs{},
+           const NormArgs& na = NormArgs{}) {
   // the staged C tile must fit in the K-loop buffers (not so for 256-wide plain outputs)
   constexpr int BNO = EPI == 2 ? BN / 2 : BN;
   if constexpr (BM * (BNO + 8) > ST * (BM + BN) * BK) {
@@ -418,19 +668,24 @@ int launch(const void* A, int lda, const void* W, void* C, int ldc, const void* 
     const int tm = (M + BM - 1) / BM, tn = N / BN;
     hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST>), dim3(tm * tn), dim3(WM * WN * 64), 0,
                        stream, (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R,
-                       ldr, M, N, K, eps, tm, tn, g_group_m > 0 ? g_group_m : 1, ra, xa);
+                       ldr, M, N, K, eps, tm, tn, g_group_m > 0 ? g_group_m : 1, ra, xa, na);
     return 0;
   }
 }
 
 template <int BM, int BN, int WM, int WN, int ST>
 int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr,
-                 int M, int N, int K, float eps, hipStream_t s) {
-  if (epi == 0 && !norm) return launch<BM, BN, WM, WN, 0, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  if (epi == 0 && norm) return launch<BM, BN, WM, WN, 0, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  if (epi == 1 && !norm) return launch<BM, BN, WM, WN, 1, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  if (epi == 2 && norm) return launch<BM, BN, WM, WN, 2, true, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
-  if (epi == 2 && !norm) return launch<BM, BN, WM, WN, 2, false, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s);
+                 int M, int N, int K, float eps, hipStream_t s, const NormArgs& na) {
+  const RopeArgs ra{};
+  const ArgmaxArgs xa{};
+#define SG_L(E, NM) return launch<BM, BN, WM, WN, E, NM, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na)
+  if (epi == 0 && norm == 0) SG_L(0, 0);
+  if (epi == 0 && norm == 1) SG_L(0, 1);
+  if (epi == 1 && norm == 0) SG_L(1, 0);
+  if (epi == 2 && norm == 1) SG_L(2, 1);
+  if (epi == 2 && norm == 2) SG_L(2, 2);
+  if (epi == 2 && norm == 0) SG_L(2, 0);
+#undef SG_L
   return -3;
 }
 
@@ -443,6 +698,7 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
 //  11: 128x256 (2x4) 2st, 8 waves   12: 256x64 (4x2) 2st, 8 waves   13: 128x128 (2x4) 2st, 8 waves
 //  14: 256x128 (4x2) 3st, 8 waves   15: 128x256 (2x4) 3st, 8 waves   16: 256x64 (4x2) 4st, 8 waves
 //  17: 32x64 (2x2) 2st   18: 32x64 (2x2) 4st — small-M decode buckets: twice the tiles of 64x64
+//  19: 256x256 (2x4) staggered 8-wave SwiGLU GEMM (gemm256_swiglu_kernel; epi 2 only)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -455,9 +711,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
   const int tm = (M + 127) / 128, tn = N / 128;
   if (K % BK || N % 128) return -2;
 #define SG_PROBE(MODE)                                                                                          \
-  hipLaunchKernelGGL((gemm_fused_kernel<128, 128, 2, 2, 2, true, 2, MODE>), dim3(tm * tn), dim3(256), 0, stream, \
+  hipLaunchKernelGGL((gemm_fused_kernel<128, 128, 2, 2, 2, 1, 2, MODE>), dim3(tm * tn), dim3(256), 0, stream, \
                      (const uint16_t*)A, K, (const uint16_t*)W, (uint16_t*)C, N / 2, nullptr, 0, M, N, K, 1e-5f, tm, \
-                     tn, g_group_m, RopeArgs{}, ArgmaxArgs{})
+                     tn, g_group_m, RopeArgs{}, ArgmaxArgs{}, NormArgs{})
   if (mode == 1) SG_PROBE(1);
   else if (mode == 2) SG_PROBE(2);
   else if (mode == 3) SG_PROBE(3);
@@ -467,13 +723,32 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
   return 0;
 }
 
+// norm: 0 none, 1 in-kernel row scale, 2 row scale from ssin ([16][ss_ld] x² partials,
+// zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
-            int epi, int norm, float eps, int cfg, hipStream_t stream) {
-  static const int BNs[19] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64};
-  if (cfg < 0 || cfg > 18) return -1;
+            int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
+  static const int BNs[20] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256};
+  if (cfg < 0 || cfg > 19) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
-#define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream
+  if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
+    return -2;
+  const NormArgs na{ssin, ssout, ss_ld};
+  if (cfg == 19) {  // 256x256 staggered 8-wave SwiGLU GEMM
+    if (epi != 2) return -3;
+    const int tm = (M + 255) / 256, tn = N / 256;
+    const int gmv = g_group_m > 0 ? g_group_m : 1;
+#define SG_256(NM)                                                                                                  \
+  hipLaunchKernelGGL((gemm256_swiglu_kernel<NM>), dim3(tm * tn), dim3(512), 0, stream, (const uint16_t*)A, lda,   \
+                     (const uint16_t*)W, (uint16_t*)C, ldc, M, N, K, eps, tm, tn, gmv, na)
+    if (norm == 2) SG_256(2);
+    else if (norm == 1) SG_256(1);
+    else SG_256(0);
+#undef SG_256
+    return 0;
+  }
+#define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream, na
   switch (cfg) {
     case 0: return dispatch_epi<128, 128, 2, 2, 2>(SG_ARGS);
     case 1: return dispatch_epi<128, 64, 2, 2, 2>(SG_ARGS);
@@ -501,33 +776,45 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
 // QKV projection with the RMSNorm prologue and the RoPE + KV-cache epilogue
 // (replaces gemm + sg_rope_qkv_cache).  W: [(nh + 2 nkv)·64, K], norm folded in.
 // cfg must have BN = 64 (1, 3, 5, 17 or 18).
+// ssin non-null: the row scales come from the producer's partials (NORM 2).
 int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float eps, int cfg, const int* pos,
                      const int* slot, const void* cos_sin, void* q_out, void* k_cache, void* vt_cache, int nh, int nkv,
-                     int Lmax, int p0, hipStream_t stream) {
+                     int Lmax, int p0, const float* ssin, int ss_ld, hipStream_t stream) {
   const int N = (nh + 2 * nkv) * 64;
   if (M <= 0 || K % BK != 0 || lda % 8 != 0 || (Lmax % 8) != 0) return -2;
   RopeArgs ra{pos, slot, (const float2*)cos_sin, (uint16_t*)q_out, (uint16_t*)k_cache, (uint16_t*)vt_cache,
               nh, nkv, Lmax, p0};
+  if (ssin && ss_ld < M) return -2;
+  const NormArgs na{ssin, nullptr, ss_ld};
+  const ArgmaxArgs xa{};
+#define SG_QKV(BM_, ST_)                                                                                              \
+  return ssin ? launch<BM_, 64, 2, 2, 3, 2, ST_>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na) \
+              : launch<BM_, 64, 2, 2, 3, 1, ST_>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
   switch (cfg) {
-    case 1: return launch<128, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
-    case 3: return launch<64, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
-    case 5: return launch<64, 64, 2, 2, 3, true, 3>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
-    case 17: return launch<32, 64, 2, 2, 3, true, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
-    case 18: return launch<32, 64, 2, 2, 3, true, 4>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra);
+    case 1: SG_QKV(128, 2);
+    case 3: SG_QKV(64, 2);
+    case 5: SG_QKV(64, 3);
+    case 17: SG_QKV(32, 2);
+    case 18: SG_QKV(32, 4);
     default: return -1;
   }
+#undef SG_QKV
 }
 
 // lm_head + FSM-masked arg-max (EPI 4): W [N, K] with the final norm folded in,
 // best [M] uint64 zeroed before the launch; cfg 0 (128x128), 3 (64x64), 17 (32x64).
 int sg_gemm_argmax(const void* A, int lda, const void* W, int M, int N, int K, float eps, int norm, int cfg,
-                   const int* row_state, const int* state_mask, const void* masks, void* best, hipStream_t stream) {
+                   const int* row_state, const int* state_mask, const void* masks, void* best, const float* ssin,
+                   int ss_ld, hipStream_t stream) {
   if (M <= 0 || K % BK != 0 || lda % 8 != 0 || N % 128 != 0) return -2;
+  if (norm == 2 && (!ssin || ss_ld < M)) return -2;
   ArgmaxArgs xa{row_state, state_mask, (const uint32_t*)masks, (unsigned long long*)best};
   RopeArgs ra{};
-#define SG_AM(BM_, BN_, WM_, WN_)                                                                                  \
-  return norm ? launch<BM_, BN_, WM_, WN_, 4, true, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa) \
-              : launch<BM_, BN_, WM_, WN_, 4, false, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa)
+  const NormArgs na{ssin, nullptr, ss_ld};
+#define SG_AM(BM_, BN_, WM_, WN_)                                                                                      \
+  return norm == 2 ? launch<BM_, BN_, WM_, WN_, 4, 2, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa, na) \
+       : norm      ? launch<BM_, BN_, WM_, WN_, 4, 1, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa, na) \
+                   : launch<BM_, BN_, WM_, WN_, 4, 0, 2>(A, lda, W, nullptr, 8, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
   switch (cfg) {
     case 0: SG_AM(128, 128, 2, 2);
     case 3: SG_AM(64, 64, 2, 2);

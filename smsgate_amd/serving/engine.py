@@ -26,7 +26,6 @@ plain library GEMMs (hipBLASLt through ``torch.nn.functional.linear``).
 from __future__ import annotations
 
 import heapq
-import itertools
 import math
 import time
 from collections import deque
@@ -109,6 +108,12 @@ class EngineConfig:
     # budget they displace better ones: 2.28 vs 2.40 tokens/row-step, 25.2 vs 26.0 k
     # msgs/s (profiles/r02_spec_policy_ab.jsonl)
     spec_policy: int = 0
+    # RMSNorm row scales from the producer: the o-proj / down-proj GEMMs (residual
+    # epilogue) also write per-tile sums of squares of the rows they store, and the
+    # next norm GEMM (gate/up, QKV, lm_head arg-max) sums those partials instead of
+    # accumulating x² with v_dot2 beside its MFMAs in every N tile (ops.gemm ss_out/ss_in)
+    producer_norm: bool = True
+    measure_idle: bool = True  # EngineStats.gpu_idle_s from two timing events per step
 
 
 @dataclass
@@ -121,6 +126,10 @@ class EngineStats:
     decode_s: float = 0.0
     harvest_s: float = 0.0
     harvest_wait_s: float = 0.0  # part of harvest_s blocked on the GPU (the snapshot's event)
+    # GPU time with nothing queued between two steps (the host had not launched the next
+    # step's work when the previous step's chunk finished): GPU-event timestamps, so it
+    # measures starvation without a profiler (EngineConfig.measure_idle)
+    gpu_idle_s: float = 0.0
     admit_s: float = 0.0
     compact_s: float = 0.0
     steps: int = 0
@@ -138,7 +147,7 @@ class EngineStats:
 @dataclass
 class _Pending:
     key: Any
-    ids: List[int]
+    ids: Any  # token ids: a list or an int32 array
     t: float = field(default_factory=time.perf_counter)  # arrival (admission batching)
 
 
@@ -236,6 +245,9 @@ class ExtractionEngine:
         self._snap_flip = 0
         self._pending: Optional[_Snapshot] = None
         self._sides: List[torch.cuda.Stream] = []  # side streams of the split decode / prefill
+        self._fwd_ss: Optional[torch.Tensor] = None  # row partials of the last forward's output (_layers_fused)
+        self._idle_prev: Optional[Any] = None  # event after the last launched chunk (measure_idle)
+        self._idle_pairs: Deque[Tuple[Any, Any]] = deque()  # (end of chunk k-1, start of step k) to price
         if self.spec:
             self._init_spec()
         self._compute_prefix()
@@ -275,25 +287,43 @@ class ExtractionEngine:
         T = x.shape[0]
         q = torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=x.device)
         a = torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)
+        ss = self._ss_buffer(T, x.device)
         for i in range(mc.layers):
-            # norm prologue + QKV projection + RoPE + KV-cache write: one kernel
+            # norm prologue + QKV projection + RoPE + KV-cache write: one kernel (layer 0's
+            # input is the embedding: no producer, the GEMM accumulates x² itself)
             ops.gemm_qkv_rope(x, self.fw_qkv[i], mc.eps, pos_tok, slot_tok, self.cos_sin, q, k_cache(i),
-                              vt_cache(i), mc.heads, mc.kv_heads, p0)
+                              vt_cache(i), mc.heads, mc.kv_heads, p0, ss_in=ss if i > 0 else None)
             if hook is not None:
                 hook(i)
             attn(i, q, a)
-            ops.gemm(a, self.fw_o[i], epi="resid", resid=x)
-            act = ops.gemm(x, self.fw_gu[i], epi="swiglu", norm_eps=mc.eps)
-            ops.gemm(act, self.fw_down[i], epi="resid", resid=x)
+            ops.gemm(a, self.fw_o[i], epi="resid", resid=x, ss_out=ss)
+            act = ops.gemm(x, self.fw_gu[i], epi="swiglu", norm_eps=mc.eps, ss_in=ss)
+            ops.gemm(act, self.fw_down[i], epi="resid", resid=x, ss_out=ss)
+        self._fwd_ss = ss  # the final residual's row partials (the lm_head's norm)
         return x
+
+    def _ss_buffer(self, T: int, dev) -> Optional[torch.Tensor]:
+        """Zeroed fp32 [ops.SS_PARTS, T] row partials shared by one forward's residual-
+        epilogue GEMMs, or None when both residual GEMMs would not tile N alike or
+        would need more than SS_PARTS tiles (then every norm GEMM accumulates x² itself)."""
+        if not self.cfg.producer_norm:
+            return None
+        mc = self.mc
+        parts = {mc.hidden // ops.GEMM_TILES[ops.gemm_cfg(T, mc.hidden, epi="resid", K=k)][1]
+                 for k in (mc.heads * mc.head_dim, mc.inter)}
+        if len(parts) != 1 or parts.pop() > ops.SS_PARTS:
+            return None
+        return ops.ss_buffer(T, dev)
 
     def _forward(self, x: torch.Tensor, **kw) -> torch.Tensor:
         return self._layers_fused(x, **kw) if self.fused else self._layers(x, **kw)
 
-    def _argmax(self, h: torch.Tensor, row_state: torch.Tensor, best: torch.Tensor) -> torch.Tensor:
-        """lm_head + FSM-masked arg-max keys (no logits materialised)."""
+    def _argmax(self, h: torch.Tensor, row_state: torch.Tensor, best: torch.Tensor,
+                ss: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """lm_head + FSM-masked arg-max keys (no logits materialised).  ``ss``: the
+        forward's row partials of ``h`` (same rows), else the GEMM computes the norm."""
         if self.fused:  # h is the un-normed residual stream: the final norm is the GEMM prologue
-            return ops.gemm_argmax(h, self.fw_lm, row_state, self.fsm, best, norm_eps=self.mc.eps)
+            return ops.gemm_argmax(h, self.fw_lm, row_state, self.fsm, best, norm_eps=self.mc.eps, ss_in=ss)
         return ops.gemm_argmax(h, self.lm_head, row_state, self.fsm, best)
 
     def _logits(self, h: torch.Tensor) -> torch.Tensor:
@@ -337,7 +367,7 @@ class ExtractionEngine:
         lens = np.fromiter((len(it.ids) for it in items), dtype=np.int32, count=n)
         T = int(lens.sum())
         dev = self.device
-        flat = np.fromiter(itertools.chain.from_iterable(it.ids for it in items), dtype=np.int64, count=T)
+        flat = np.concatenate([it.ids for it in items]).astype(np.int64, copy=False)
         rows_np = np.asarray(rows, dtype=np.int32)
         cu = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(lens, out=cu[1:])
@@ -427,7 +457,7 @@ class ExtractionEngine:
                           hook=hook)
         if sample and self.argmax:
             best = self.best[r0:r1]
-            self._argmax(h, self.state[r0:r1], best)
+            self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None)
             ops.fsm_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
                            pos, B)
             return best
@@ -517,7 +547,7 @@ class ExtractionEngine:
         if sample and self.argmax:
             # every pseudo-row masked with the state it has if its row's drafts so far are accepted
             best = self.x_best[off:off + T]
-            self._argmax(h, xst, best)
+            self._argmax(h, xst, best, ss=self._fwd_ss if self.fused else None)
             ops.spec_verify_keys(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
                                  done, pos, xt, rs, nd, acc)
             logits = best
@@ -530,6 +560,13 @@ class ExtractionEngine:
             # tokens emitted and live rows this step (read back only by stats())
             self.spec_counts += torch.stack([acc.sum(dtype=torch.int64), (acc > 0).sum(dtype=torch.int64)])
         return logits
+
+    def reset_stats(self) -> None:
+        """Zero the counters (a new measurement window: the idle gap since the last
+        chunk is not charged to it)."""
+        self.stats.__init__()
+        self._idle_prev = None
+        self._idle_pairs.clear()
 
     def spec_stats(self, reset: bool = False) -> Dict[str, float]:
         if not self.spec:
@@ -769,7 +806,7 @@ class ExtractionEngine:
         hb["done"][:B].copy_(self.done[:B], non_blocking=True)
         hb["len"][:B].copy_(self.out_len[:B], non_blocking=True)
         hb["buf"][:B].copy_(self.out_buf[:B], non_blocking=True)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(enable_timing=self.cfg.measure_idle)
         ev.record()
         return _Snapshot(B, ev, hb, dict(self.active))
 
@@ -818,6 +855,11 @@ class ExtractionEngine:
         ``(key, answer dict)`` — or ``(key, int32 token array)`` with ``raw=True``
         (the remote-client path)."""
         t0 = time.perf_counter()
+        if self.cfg.measure_idle and self._idle_prev is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()  # runs when the GPU reaches this step's first work
+            self._idle_pairs.append((self._idle_prev, ev))
+            self._idle_prev = None
         if self.cfg.compact:
             self._compact()
         t1 = time.perf_counter()
@@ -829,7 +871,12 @@ class ExtractionEngine:
             B = self._bucket(max(self.active) + 1)
             self._run_decode(B)
             self._pending = self._snapshot(B)
+            if self.cfg.measure_idle:
+                self._idle_prev = self._pending.event
         out = self._harvest(prev, raw) if prev is not None else []
+        while self._idle_pairs and self._idle_pairs[0][1].query():
+            a, b = self._idle_pairs.popleft()
+            self.stats.gpu_idle_s += max(0.0, a.elapsed_time(b)) / 1000.0
         self.stats.steps += 1
         self.stats.step_s += time.perf_counter() - t0
         return out
@@ -838,9 +885,8 @@ class ExtractionEngine:
         """Queue pre-tokenised prompts (``<sms> body <ans>`` ids, see the tokenizer)."""
         cap = self.cfg.max_body_tokens + 2
         for k, ids in items:
-            ids = list(ids)
-            if len(ids) > cap:
-                ids = ids[: cap - 1] + [ids[-1]]
+            if len(ids) > cap:  # keep the closing <ans>
+                ids = np.concatenate([np.asarray(ids[: cap - 1], dtype=np.int32), np.asarray(ids[-1:], dtype=np.int32)])
             self.waiting.append(_Pending(k, ids))
 
     def run(self, bodies: Sequence[str]) -> List[Dict[str, Optional[str]]]:

@@ -18,7 +18,7 @@ from typing import Any, List, Sequence, Tuple
 
 import numpy as np
 
-__all__ = ["pack_ids", "unpack_ids", "pack_error", "pack_control", "kind"]
+__all__ = ["pack_ids", "unpack_ids", "unpack_id_arrays", "pack_error", "pack_control", "kind"]
 
 _HDR = struct.Struct("<cQI")
 
@@ -46,6 +46,17 @@ def unpack_ids(buf: bytes) -> Tuple[bytes, int, List[List[int]]]:
         out.append(flat[p:p + ln])
         p += ln
     return tag, req_id, out
+
+
+def unpack_id_arrays(buf: bytes) -> Tuple[bytes, int, List[np.ndarray]]:
+    """As :func:`unpack_ids`, but each sequence is an int32 view into one copy of the
+    payload (the engine server's path: no per-token Python objects)."""
+    tag, req_id, n = _HDR.unpack_from(buf, 0)
+    off = _HDR.size
+    lens = np.frombuffer(buf, dtype=np.uint16, count=n, offset=off)
+    off += 2 * n
+    flat = np.frombuffer(buf, dtype=np.int32, count=int(lens.sum()), offset=off).copy()
+    return tag, req_id, np.split(flat, np.cumsum(lens[:-1], dtype=np.int64)) if n else []
 
 
 def pack_error(req_id: int, msg: str) -> bytes:

@@ -86,7 +86,7 @@ class EngineServer:
                     break
                 k = P.kind(buf)
                 if k == b"Q":
-                    _, rid, seqs = P.unpack_ids(buf)
+                    _, rid, seqs = P.unpack_id_arrays(buf)
                     if not seqs:
                         c.send_bytes(P.pack_ids(b"R", rid, []))
                     else:

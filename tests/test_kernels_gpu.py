@@ -320,6 +320,61 @@ def test_gemm_argmax_matches_logits_path(cfg, M):
             assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())
 
 
+@pytest.mark.parametrize("cfg", [1, 3, 17])
+@pytest.mark.parametrize("M", [5, 333, 2048])
+def test_gemm_producer_norm(cfg, M):
+    """Residual GEMM with ``ss_out`` writes per-N-tile x² partials of the rows it
+    stores; norm GEMMs given them (``ss_in``: SwiGLU, QKV+RoPE, lm_head arg-max)
+    match the same GEMMs accumulating x² themselves, and the fp32 reference."""
+    H, I, nh, nkv, D, S, Lmax, p0 = 576, 1536, 9, 3, 64, 4096, 192, 20
+    a = _bf(M, H, seed=61)
+    wo = _bf(H, H, scale=H ** -0.5, seed=62)
+    x = _bf(M, H, seed=63)
+    ss = ops.ss_buffer(M + 7, DEV)
+    ops.gemm(a, wo, epi="resid", resid=x, cfg=cfg, ss_out=ss)
+    parts = H // ops.GEMM_TILES[cfg][1]
+    assert torch.count_nonzero(ss[parts:]) == 0 and torch.count_nonzero(ss[:, M:]) == 0
+    torch.testing.assert_close(ss[:, :M].sum(0), x.float().pow(2).sum(1), rtol=1e-4, atol=1e-3)
+    nw = _bf(H, scale=0.1, seed=64) + 1
+    gu = ops.interleave_gate_up(ops.fold_norm(_bf(2 * I, H, scale=H ** -0.5, seed=65), nw))
+    own = ops.gemm(x, gu, epi="swiglu", norm_eps=1e-5)
+    ext = ops.gemm(x, gu, epi="swiglu", norm_eps=1e-5, ss_in=ss)
+    torch.testing.assert_close(ext.float(), own.float(), atol=1e-2, rtol=1e-2)
+    # QKV + RoPE + KV write
+    wq = _bf((nh + 2 * nkv) * D, H, scale=H ** -0.5, seed=66)
+    g = torch.Generator(device="cpu").manual_seed(67)
+    pos = torch.randint(0, Lmax, (M,), generator=g, dtype=torch.int32).to(DEV)
+    slot = torch.randperm(S, generator=g)[:M].to(torch.int32).to(DEV)
+    cs = ops.rope_table(p0 + Lmax + 1, D, 100000.0, DEV)
+    outs = []
+    for ss_in in (None, ss):
+        kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
+        vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=DEV)
+        q = torch.zeros(M, nh, D, dtype=torch.bfloat16, device=DEV)
+        ops.gemm_qkv_rope(x, wq, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, p0, ss_in=ss_in)
+        outs.append((q, kc, vt))
+    for u, v in zip(*outs):
+        torch.testing.assert_close(u.float(), v.float(), atol=1e-2, rtol=1e-2)
+    # lm_head arg-max: the keys' values agree to bf16 rounding of the logits
+    from smsgate_amd.models.tokenizer import load_tokenizer
+    from smsgate_amd.serving.fsm import build_fsm
+
+    tk = load_tokenizer()
+    V = (tk.vocab_size + 127) // 128 * 128
+    fsm = build_fsm(tk, V).to_device(DEV)
+    w = _bf(V, H, scale=0.05, seed=68)
+    row_state = torch.full((M,), fsm.start_state, dtype=torch.int32, device=DEV)
+    keys = []
+    for ss_in in (None, ss):
+        best = torch.zeros(M, dtype=torch.int64, device=DEV)
+        ops.gemm_argmax(x, w, row_state, fsm, best, norm_eps=1e-5, ss_in=ss_in)
+        keys.append(best)
+    same = (keys[0] == keys[1]).float().mean().item()
+    assert same >= 0.95, same  # a different fp32 sum order may flip a near-tie's bf16 rounding
+    with pytest.raises(ValueError):
+        ops.gemm(a, wo, epi="store", ss_out=ss)
+
+
 @pytest.mark.parametrize("P0,max_q", [(0, 5), (75, 5), (75, 9)])
 def test_attn_spec_matches_grouped_bitwise(P0, max_q):
     """attn_spec (one wave per row, all its drafts) == the grouped decode kernel on

@@ -98,6 +98,8 @@ def _args(argv=None):
     p.add_argument("--split-prefill", type=int, default=8192,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--spec-policy", type=int, default=0, help="draft policy (EngineConfig.spec_policy)")
+    p.add_argument("--swiglu-cfg", type=int, default=None,
+                   help="A/B: tile config of the gate/up SwiGLU GEMM at >= 4096 rows (ops.GEMM_MEASURED)")
     p.add_argument("--no-producer-norm", action="store_true",
                    help="norm GEMMs accumulate x^2 themselves instead of reading the producer's row partials")
     p.add_argument("--gemm-rule-only", action="store_true",
@@ -352,6 +354,10 @@ def main(argv=None) -> int:
         from smsgate_amd import ops
 
         ops.GEMM_MEASURED.clear()
+    if args.swiglu_cfg is not None:
+        from smsgate_amd import ops
+
+        ops.GEMM_MEASURED[("swiglu", 3072, 576)] = [(4096, 1 << 30, args.swiglu_cfg)]
     rank, world, local = _rank_env()
     if args.backend == "local_llm" or args.cpu_echo_engine:
         dt, counts, init_s, estats, prov, quality = run_replica(args, rank, world, local)

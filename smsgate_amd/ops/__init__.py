@@ -199,12 +199,12 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 64), 5: (64, 64), 6: (64, 64),
               7: (128, 128), 8: (64, 128), 9: (256, 128), 10: (256, 256), 11: (128, 256), 12: (256, 64),
               13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64),
-              19: (256, 256)}
+              19: (256, 256), 20: (256, 256)}
 # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 # a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
-# SwiGLU kernel (gemm256_swiglu_kernel)
-GEMM_SWIGLU_ONLY = {10, 19}
+# SwiGLU kernel (gemm256_swiglu_kernel), 20 its persistent form
+GEMM_SWIGLU_ONLY = {10, 19, 20}
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
@@ -220,8 +220,11 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #   o-proj 576x576 + residual: 64x64 tiles at 9216 rows (14.3 vs 15.9 us).
 # End to end the bench is unchanged within noise (27 571 vs 27 491 msgs/s, three
 # interleaved runs each, profiles/r02_gemm_measured_ab.jsonl).
+#   SwiGLU gate/up with the staggered 256x256 kernel (cfg 19, scripts/gemm256_check.py,
+#     producer row partials): 22.2 / 41.6 / 67.2 us at 4608 / 9216 / 16384 rows vs 24.1 /
+#     43.8 / 68.2 for the best of cfg 0 and 10 (profiles/r02_gemm256_check.json).
 GEMM_MEASURED = {
-    ("swiglu", 3072, 576): [(4096, 6144, 10), (12288, 1 << 30, 10)],
+    ("swiglu", 3072, 576): [(4096, 1 << 30, 20)],
     ("resid", 576, 576): [(8192, 10240, 3)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
@@ -263,7 +266,7 @@ SS_PARTS = 16  # csrc/gemm_kernels.hip: x² partials per row (producer N tiles, 
 def ss_buffer(M: int, device) -> torch.Tensor:
     """Zeroed fp32 ``[SS_PARTS, M]`` row-partials image for ``gemm(ss_out=..)`` / ``ss_in``
     (part-major: column ``m`` holds row ``m``'s partials)."""
-    return torch.zeros(SS_PARTS, M, dtype=torch.float32, device=device)
+    return torch.zeros(SS_PARTS, (M + 3) // 4 * 4, dtype=torch.float32, device=device)  # 16-B row groups
 
 
 def _ss_check(ss: Optional[torch.Tensor], M: int, name: str) -> int:

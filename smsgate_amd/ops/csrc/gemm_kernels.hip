@@ -370,14 +370,15 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
         *reinterpret_cast<uint4*>(dst + 32 + c * 8) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
       }
     } else {
+      // one token per wave-instruction (lane = d): the row index is wave-uniform, so its
+      // position / slot are scalar loads and the V^T address is scalar base + 16 B x lane
       const int kh = h - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
-      for (int q = tid; q < BM * 64; q += NT) {
-        const int row = q >> 6, d = q & 63;
+      for (int row = __builtin_amdgcn_readfirstlane(wave); row < BM; row += NW) {
         const int gr = m0 + row;
-        if (gr >= M) continue;
+        if (gr >= M) break;
         const int p = ra.pos[gr];
-        ra.vt_cache[((((size_t)ra.slot[gr] * ra.nkv + kh) * nb + (p >> 3)) * 64 + d) * 8 + (p & 7)] =
-            Cs[row * CST + d];
+        const size_t base = (((size_t)ra.slot[gr] * ra.nkv + kh) * nb + (p >> 3)) * 512 + (p & 7);
+        ra.vt_cache[base + (size_t)lane * 8] = Cs[row * CST + lane];
       }
     }
     return;
@@ -494,7 +495,10 @@ __global__ void __launch_bounds__(512) gemm256_swiglu_kernel(const uint16_t* __r
   constexpr int BUF = 4 * HALF;                        // A_top, A_bot, Blo, Bhi
   constexpr int BNO = BN / 2, CST = BNO + 8;
   static_assert(BM * CST <= 2 * BUF, "C staging fits");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF];
+  // + the tile's 256 row sums of x² (NORM 2), one fp32 each, past the staging buffers
+  // (ONE __shared__ array: cdna_hip_programming.md §5 trap 4a)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF + (NORM == 2 ? 2 * BM : 0)];
+  float* ssl = reinterpret_cast<float*>(smem + 2 * BUF);
 
   const int T = tiles_m * tiles_n;
   const int orig = blockIdx.x, xcd = orig & 7, q8 = T >> 3, r8 = T & 7;
@@ -564,9 +568,23 @@ __global__ void __launch_bounds__(512) gemm256_swiglu_kernel(const uint16_t* __r
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
-  // prologue: K-tile 0 into buffer 0, then group 1 falls one barrier behind
+  // prologue: K-tile 0 into buffer 0 (+ NORM 2: the rows' x² partials, summed into
+  // LDS while the DMAs land — one thread per row, part-major loads are coalesced),
+  // then group 1 falls one barrier behind
 #pragma unroll
   for (int h = 0; h < 4; ++h) stage(0, h, 0);
+  if constexpr (NORM == 2) {
+    if (tid < BM) {
+      const float* sp = na.ssin + min(m0 + tid, M - 1);
+      float v[SS_PARTS];
+#pragma unroll
+      for (int p = 0; p < SS_PARTS; ++p) v[p] = sp[(size_t)p * na.ld];
+      float tot = 0.f;
+#pragma unroll
+      for (int p = 0; p < SS_PARTS; ++p) tot += v[p];
+      ssl[tid] = tot;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
@@ -617,12 +635,7 @@ __global__ void __launch_bounds__(512) gemm256_swiglu_kernel(const uint16_t* __r
       v += __shfl_xor(v, 32, 64);
       rsv[i] = rsqrtf(v / (float)K + eps);
     } else if constexpr (NORM == 2) {
-      const int row = min(m0 + wr * 128 + i * 16 + (lane & 15), M - 1);
-      const float* sp = na.ssin + (size_t)((lane >> 4) * 4) * na.ld + row;
-      float v = (sp[0] + sp[(size_t)na.ld]) + (sp[(size_t)2 * na.ld] + sp[(size_t)3 * na.ld]);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      rsv[i] = rsqrtf(v / (float)K + eps);
+      rsv[i] = rsqrtf(ssl[wr * 128 + i * 16 + (lane & 15)] / (float)K + eps);
     }
   }
   // SwiGLU into the staged bf16 tile: pair p (lo/hi) -> output cols p·64 + wc·16 + c4
@@ -652,6 +665,220 @@ __global__ void __launch_bounds__(512) gemm256_swiglu_kernel(const uint16_t* __r
     *reinterpret_cast<uint4*>(C + (size_t)gr * ldc + c0 + c * 8) =
         *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
   }
+}
+
+// Persistent form of gemm256_swiglu_kernel (cfg 20): one block per CU walks its tiles
+// (virtual ids blockIdx.x + k·gridDim.x through the same XCD-aware map), and the
+// per-tile fixed cost — first K-tile load, SwiGLU epilogue, output stores — is
+// overlapped with the neighbouring tiles' K loops: the last K-tile of tile i stages
+// K-tile 0 of tile i+1 (and, NORM 2, its rows' x² partials: 16 × 1 KB LDS-DMAs into
+// `raw`, summed into `ssl` by group 0 after the loop), the epilogue stores straight
+// from the accumulators (no LDS staging, so nothing waits for the stores), and the
+// wave groups stay staggered across tiles.  Same phase / wait structure as above
+// except (a) p4 re-reads A rows 0-63 (one A register set: the kernel then fits 256
+// VGPRs without spills) and (b) the last K-tile's p2 wait, vmcnt(6): the 2 partial
+// DMAs of p1 precede A_top.
+template <int NORM>
+__global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __restrict__ A, int lda,
+                                                             const uint16_t* __restrict__ W, uint16_t* C, int ldc,
+                                                             int M, int N, int K, float eps, int tiles_m, int tiles_n,
+                                                             int gm, NormArgs na) {
+  constexpr int BM = 256, BN = 256, HALF = 128 * BK, BUF = 4 * HALF;
+  constexpr int RAW = NORM == 2 ? SS_PARTS * BM * 2 : 0;  // [16][256] fp32, in uint16 units
+  constexpr int SSL = NORM == 2 ? 2 * BM * 2 : 0;         // [2][256] fp32 (tile parity)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF + RAW + SSL];
+  float* raw = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* ssl = reinterpret_cast<float*>(smem + 2 * BUF + RAW);
+
+  const int T = tiles_m * tiles_n;
+  auto tile_mn = [&](int v, int& m0, int& n0) {
+    const int xcd = v & 7, q8 = T >> 3, r8 = T & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+    const int gsz = gm * tiles_n, g = t / gsz, gl = t - g * gsz;
+    const int grows = min(gm, tiles_m - g * gm);
+    m0 = (g * gm + gl % grows) * BM;
+    n0 = (gl / grows) * BN;
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int KT = K / BK;
+
+  auto stage = [&](int b, int h, int mm, int nn, int kt) {
+    const int kk = min(kt, KT - 1) * BK;
+    uint16_t* dst = smem + b * BUF + h * HALF;
+    if (h < 2) issue_tile<128, 8>(A, lda, mm + h * 128, M - 1, kk, dst, wave, lane);
+    else issue_tile<128, 8>(W, K, nn + (h - 2) * 128, N - 1, kk, dst, wave, lane);
+  };
+  // NORM 2: parts 2w, 2w+1 of rows mm + [0, 256): lane l -> rows mm + 4l .. +3 (16 B);
+  // groups past the end re-read the last aligned group (never used); ld % 4 == 0
+  auto stage_ss = [&](int mm) {
+    if constexpr (NORM == 2) {
+      const int r = min(mm + lane * 4, ((M + 3) & ~3) - 4);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int p = wave * 2 + e;
+        __builtin_amdgcn_global_load_lds((const void*)(na.ssin + (size_t)p * na.ld + r),
+                                         (lds_ptr_t)(raw + p * BM), 16, 0, 0);
+      }
+    }
+  };
+  auto sum_ss = [&](int par) {  // group 0: one row per thread
+    if constexpr (NORM == 2) {
+      if (tid < BM) {
+        float v = 0.f;
+#pragma unroll
+        for (int p = 0; p < SS_PARTS; ++p) v += raw[p * BM + tid];
+        ssl[par * BM + tid] = v;
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+  float ss[8];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ss[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  bf16x8 af[2][4], bq[2][2];  // ONE A set (p4 re-reads rows 0-63): 32 VGPRs fewer, no spills
+  auto read_a = [&](bf16x8 (&dst)[2][4], const uint16_t* base, int r0) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r0 + i * 16 + (lane & 15), ch = s2 * 4 + (lane >> 4);
+        dst[s2][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((ch ^ (row & 7)) << 3));
+      }
+  };
+  auto read_b = [&](const uint16_t* base) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 32 + j * 16 + (lane & 15), ch = s2 * 4 + (lane >> 4);
+        bq[s2][j] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((ch ^ (row & 7)) << 3));
+      }
+  };
+  auto mfma_q = [&](bf16x8 (&a_)[2][4], int i0, int j0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s2][j], a_[s2][i], acc[i0 + i][j0 + j],
+                                                                        0, 0, 0);
+        if constexpr (NORM == 1)
+          if (j0 == 0) ss[i0 + i] = sumsq_frag(a_[s2][i], ss[i0 + i]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mid = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  int v = blockIdx.x;
+  if (v >= T) return;  // (the launcher sizes the grid <= T: never taken)
+  int m0, n0;
+  tile_mn(v, m0, n0);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, m0, n0, 0);
+  stage_ss(m0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  sum_ss(0);
+  __syncthreads();
+  zero_acc();
+  if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
+
+  int gk = 0, tpar = 0;
+  const int c4 = (lane >> 4) * 4;
+  while (true) {
+    const int vn = v + gridDim.x;
+    const bool more = vn < T;
+    int m1 = m0, n1 = n0;
+    if (more) tile_mn(vn, m1, n1);
+    for (int kt = 0; kt < KT; ++kt, ++gk) {
+      const int cb = gk & 1, nb = cb ^ 1;
+      const bool last = kt == KT - 1;
+      const int sm = last ? m1 : m0, sn = last ? n1 : n0, sk = last ? (more ? 0 : KT - 1) : kt + 1;
+      const uint16_t* buf = smem + cb * BUF;
+      const uint16_t* abase = buf + wr * HALF;
+      // p1: rows 0-63 x lo
+      read_a(af, abase, 0);
+      read_b(buf + 2 * HALF);
+      if (last) stage_ss(sm);
+      stage(nb, 0, sm, sn, sk);
+      mid();
+      mfma_q(af, 0, 0);
+      __builtin_amdgcn_s_barrier();
+      // p2: rows 64-127 x lo
+      read_a(af, abase, 64);
+      stage(nb, 1, sm, sn, sk);
+      if (NORM == 2 && last) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // + this p1's partial DMAs
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                    // Bhi of THIS K-tile landed
+      mid();
+      mfma_q(af, 4, 0);
+      __builtin_amdgcn_s_barrier();
+      // p3: rows 64-127 x hi
+      read_b(buf + 3 * HALF);
+      stage(nb, 2, sm, sn, sk);
+      mid();
+      mfma_q(af, 4, 2);
+      __builtin_amdgcn_s_barrier();
+      // p4: rows 0-63 x hi (re-read: WAR-safe, the next DMA into this A half is staged
+      // after the lagging group's p4 barrier)
+      read_a(af, abase, 0);
+      stage(nb, 3, sm, sn, sk);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // next K-tile's A_top, A_bot, Blo (+ partials)
+      mid();
+      mfma_q(af, 0, 2);
+      __builtin_amdgcn_s_barrier();
+    }
+    // next tile's row sums (its partials landed: every wave's p4 wait precedes a barrier
+    // this wave has passed); this tile's are in ssl[tpar]
+    if (more) sum_ss(tpar ^ 1);
+    // epilogue straight from the accumulators: row m0 + wr·128 + 16i + (lane & 15),
+    // SwiGLU pair p -> output columns n0/2 + p·64 + wc·16 + c4 .. +3
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rl = wr * 128 + i * 16 + (lane & 15);
+      float rs = 1.f;
+      if constexpr (NORM == 1) {
+        float x = ss[i];
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        rs = rsqrtf(x / (float)K + eps);
+      } else if constexpr (NORM == 2) {
+        rs = rsqrtf(ssl[tpar * BM + rl] / (float)K + eps);
+      }
+      const int gr = m0 + rl;
+      if (gr < M) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          float h[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = silu(acc[i][2 * p][r] * rs) * (acc[i][2 * p + 1][r] * rs);
+          *reinterpret_cast<uint2*>(C + (size_t)gr * ldc + n0 / 2 + p * 64 + wc * 16 + c4) =
+              make_uint2((uint32_t)f2bf(h[0]) | ((uint32_t)f2bf(h[1]) << 16),
+                         (uint32_t)f2bf(h[2]) | ((uint32_t)f2bf(h[3]) << 16));
+        }
+      }
+    }
+    if (!more) break;
+    zero_acc();
+    v = vn;
+    m0 = m1;
+    n0 = n1;
+    tpar ^= 1;
+  }
+  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail DMAs
 }
 
 int g_group_m = 8;  // M-tiles per rasterisation group (sg_gemm_set_group_m)
@@ -699,6 +926,7 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
 //  14: 256x128 (4x2) 3st, 8 waves   15: 128x256 (2x4) 3st, 8 waves   16: 256x64 (4x2) 4st, 8 waves
 //  17: 32x64 (2x2) 2st   18: 32x64 (2x2) 4st — small-M decode buckets: twice the tiles of 64x64
 //  19: 256x256 (2x4) staggered 8-wave SwiGLU GEMM (gemm256_swiglu_kernel; epi 2 only)
+//  20: its persistent form (gemm256p_swiglu_kernel; epi 2 only; NORM 2 needs ss_ld % 4 == 0)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -727,9 +955,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[20] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256};
-  if (cfg < 0 || cfg > 19) return -1;
+  static const int BNs[21] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256};
+  if (cfg < 0 || cfg > 20) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -746,6 +974,21 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     else if (norm == 1) SG_256(1);
     else SG_256(0);
 #undef SG_256
+    return 0;
+  }
+  if (cfg == 20) {  // persistent form: one block per CU (256 CUs), tiles overlapped
+    if (epi != 2) return -3;
+    if (norm == 2 && ss_ld % 4 != 0) return -2;
+    const int tm = (M + 255) / 256, tn = N / 256, T = tm * tn;
+    const int grid = T < 256 ? T : 256;
+    const int gmv = g_group_m > 0 ? g_group_m : 1;
+#define SG_256P(NM)                                                                                                   \
+  hipLaunchKernelGGL((gemm256p_swiglu_kernel<NM>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,       \
+                     (const uint16_t*)W, (uint16_t*)C, ldc, M, N, K, eps, tm, tn, gmv, na)
+    if (norm == 2) SG_256P(2);
+    else if (norm == 1) SG_256P(1);
+    else SG_256P(0);
+#undef SG_256P
     return 0;
   }
 #define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream, na

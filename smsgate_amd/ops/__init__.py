@@ -217,15 +217,16 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 # profiles/r02_gemm_tune.json), keyed by (epilogue, N, K): [(M_lo, M_hi, cfg)].
 #   SwiGLU gate/up 3072x576: 256x256 8-wave tiles at 4608 rows (26.7 vs 28.4 us) and at
 #     prefill halves of 16384 (73.9 vs 80.3 us); 128x128 stays best at 9216 (47.5 vs 49.4).
-#   o-proj 576x576 + residual: 64x64 tiles at 9216 rows (14.3 vs 15.9 us).
+#   o-proj 576x576 + residual: 64x64 tiles at 9216 rows (14.3 vs 15.9 us) — superseded below.
 # End to end the bench is unchanged within noise (27 571 vs 27 491 msgs/s, three
 # interleaved runs each, profiles/r02_gemm_measured_ab.jsonl).
 #   SwiGLU gate/up with the staggered 256x256 kernel (cfg 19, scripts/gemm256_check.py,
 #     producer row partials): 22.2 / 41.6 / 67.2 us at 4608 / 9216 / 16384 rows vs 24.1 /
 #     43.8 / 68.2 for the best of cfg 0 and 10 (profiles/r02_gemm256_check.json).
+#   o-proj: with the residual prefetched before the K loop the rule's 128x64 tile wins at
+#     9216 rows again (14.06 vs 14.33 us, profiles/r02_norm_epilogue_cost.txt): no exception.
 GEMM_MEASURED = {
     ("swiglu", 3072, 576): [(4096, 1 << 30, 20)],
-    ("resid", 576, 576): [(8192, 10240, 3)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
 

@@ -218,6 +218,42 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       for (int e = 0; e < 4; ++e) ssv[i][e] = sp[(size_t)e * na.ld];
     }
   }
+  // EPI 1: this thread's residual chunks, loaded before the K loop (their latency hides
+  // behind it instead of stalling the epilogue; R may alias C, but every element is
+  // read and written by the same thread)
+  constexpr int RIT = EPI == 1 ? (BM * (BN / 8)) / NT : 1;
+  uint4 rpre[RIT];
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int it = 0; it < RIT; ++it) {
+      const int q = tid + it * NT, row = q / (BN / 8), c = q % (BN / 8);
+      const int gr = min(m0 + row, M - 1);
+      rpre[it] = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + n0 + c * 8);
+    }
+  }
+  // EPI 3: the tile's token positions / KV slots, likewise loaded before the K loop —
+  // q/k head: the rows of this thread's (row, quarter) items; v head: row = lane (+64)
+  constexpr int QIT = (BM * 4 + NT - 1) / NT, VU = BM > 64 ? 2 : 1;
+  constexpr int EPN = EPI == 3 ? (QIT > VU ? QIT : VU) : 1;
+  int epos[EPN], eslot[EPN];
+  if constexpr (EPI == 3) {
+    const int h = n0 >> 6;
+    if (h < ra.nh + ra.nkv) {
+#pragma unroll
+      for (int it = 0; it < QIT; ++it) {
+        const int gr = min(m0 + ((tid + it * NT) >> 2), M - 1);
+        epos[it] = ra.pos[gr];
+        eslot[it] = h >= ra.nh ? ra.slot[gr] : 0;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < VU; ++u) {
+        const int gl = min(m0 + u * 64 + lane, M - 1);
+        epos[u] = ra.pos[gl];
+        eslot[u] = ra.slot[gl];
+      }
+    }
+  }
   f32x4 acc[FM][FN];
   float ss[FM];
 #pragma unroll
@@ -345,11 +381,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   if constexpr (EPI == 3) {
     const int h = n0 >> 6;
     if (h < ra.nh + ra.nkv) {
-      for (int q = tid; q < BM * 4; q += NT) {
+#pragma unroll
+      for (int it = 0; it < QIT; ++it) {
+        const int q = tid + it * NT;
+        if (q >= BM * 4) break;
         const int row = q >> 2, c = q & 3;
         const int gr = m0 + row;
         if (gr >= M) continue;
-        const int p = ra.pos[gr];
+        const int p = epos[it];
         const uint4 v1 = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
         const uint4 v2 = *reinterpret_cast<const uint4*>(Cs + row * CST + 32 + c * 8);
         const float4* csp = reinterpret_cast<const float4*>(ra.cs + (size_t)(ra.p0 + p) * 32 + c * 8);
@@ -365,19 +404,24 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
         }
         uint16_t* dst;
         if (h < ra.nh) dst = ra.q_out + ((size_t)gr * ra.nh + h) * 64;
-        else dst = ra.k_cache + (((size_t)ra.slot[gr] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
+        else dst = ra.k_cache + (((size_t)eslot[it] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
         *reinterpret_cast<uint4*>(dst + c * 8) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
         *reinterpret_cast<uint4*>(dst + 32 + c * 8) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
       }
     } else {
-      // one token per wave-instruction (lane = d): the row index is wave-uniform, so its
-      // position / slot are scalar loads and the V^T address is scalar base + 16 B x lane
+      // one token per wave-instruction (lane = d).  The tile's positions / slots sit one
+      // row per lane (prefetched before the K loop; a dependent scalar load per row
+      // serialised ~16 L2 round trips per wave) and are broadcast with readlane: the
+      // V^T address is a scalar base + 16 B x lane
+      static_assert(BM <= 128, "V^T scatter: rows per lane register");
       const int kh = h - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
       for (int row = __builtin_amdgcn_readfirstlane(wave); row < BM; row += NW) {
         const int gr = m0 + row;
         if (gr >= M) break;
-        const int p = ra.pos[gr];
-        const size_t base = (((size_t)ra.slot[gr] * ra.nkv + kh) * nb + (p >> 3)) * 512 + (p & 7);
+        const int u = BM > 64 ? (row >> 6) : 0;
+        const int p = __builtin_amdgcn_readlane(u ? epos[VU - 1] : epos[0], row & 63);
+        const int sl = __builtin_amdgcn_readlane(u ? eslot[VU - 1] : eslot[0], row & 63);
+        const size_t base = (((size_t)sl * ra.nkv + kh) * nb + (p >> 3)) * 512 + (p & 7);
         ra.vt_cache[base + (size_t)lane * 8] = Cs[row * CST + lane];
       }
     }
@@ -427,13 +471,15 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     // runs the same trip count, so the row's x² partial reduces with shuffles
     static_assert((BM * CPR) % NT == 0 && CPR <= 64, "uniform epilogue trips");
     const bool want_ss = na.ssout != nullptr;
-    for (int q = tid; q < BM * CPR; q += NT) {
+#pragma unroll
+    for (int it = 0; it < RIT; ++it) {
+      const int q = tid + it * NT;
       const int row = q / CPR, c = q % CPR;
       const int gr = m0 + row;
       float sq = 0.f;
       if (gr < M) {
         const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
-        const uint4 rr = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + c0 + c * 8);
+        const uint4 rr = rpre[it];
         uint32_t a[4] = {v.x, v.y, v.z, v.w};
         const uint32_t b[4] = {rr.x, rr.y, rr.z, rr.w};
 #pragma unroll

@@ -76,10 +76,22 @@ def main() -> int:
         kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=dev)
         vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=dev)
         q_out = torch.empty(M, nh, D, dtype=torch.bfloat16, device=dev)
+        # the engine's flavour: norm GEMMs read the producer's x² partials, residual GEMMs write them
+        ss = ops.ss_buffer(M, dev)
+        ss[:9] = torch.rand(9, M, device=dev)
+        sso = ops.ss_buffer(M, dev)
+
+        def resid_fn(a_, w_):
+            def fn(c):
+                if H // ops.GEMM_TILES[c][1] > ops.SS_PARTS:
+                    raise ValueError("too many N tiles for the partials")
+                return ops.gemm(a_, w_, epi="resid", resid=resid, cfg=c, ss_out=sso)
+            return fn
         shapes = {
-            "gate_up": (2 * I, H, "swiglu", lambda c: ops.gemm(x, w_gu, epi="swiglu", norm_eps=1e-5, out=out_gu, cfg=c)),
-            "down": (H, I, "resid", lambda c: ops.gemm(h, w_down, epi="resid", resid=resid, cfg=c)),
-            "o": (H, H, "resid", lambda c: ops.gemm(x, w_o, epi="resid", resid=resid, cfg=c)),
+            "gate_up": (2 * I, H, "swiglu",
+                        lambda c: ops.gemm(x, w_gu, epi="swiglu", norm_eps=1e-5, out=out_gu, cfg=c, ss_in=ss)),
+            "down": (H, I, "resid", resid_fn(h, w_down)),
+            "o": (H, H, "resid", resid_fn(x, w_o)),
         }
         for name, (N, K, epi, fn) in shapes.items():
             cfgs = [c for c, (bm, bn) in ops.GEMM_TILES.items() if N % bn == 0]
@@ -101,7 +113,8 @@ def main() -> int:
             for _ in range(a.rounds):
                 for c in qcfgs:
                     best[c] = min(best[c], graph_time(
-                        lambda: ops.gemm_qkv_rope(x, w_qkv, 1e-5, pos, slot, cs, q_out, kc, vt, nh, nkv, 20, cfg=c),
+                        lambda: ops.gemm_qkv_rope(x, w_qkv, 1e-5, pos, slot, cs, q_out, kc, vt, nh, nkv, 20, cfg=c,
+                                                  ss_in=ss),
                         a.iters, a.inner))
             ok = {c: round(t, 2) for c, t in best.items()}
             res[f"qkv_rope_M{M}"] = {"us": ok, "best": min(ok, key=ok.get)}

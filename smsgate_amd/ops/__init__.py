@@ -217,16 +217,19 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 # profiles/r02_gemm_tune.json), keyed by (epilogue, N, K): [(M_lo, M_hi, cfg)].
 #   SwiGLU gate/up 3072x576: 256x256 8-wave tiles at 4608 rows (26.7 vs 28.4 us) and at
 #     prefill halves of 16384 (73.9 vs 80.3 us); 128x128 stays best at 9216 (47.5 vs 49.4).
-#   o-proj 576x576 + residual: 64x64 tiles at 9216 rows (14.3 vs 15.9 us) — superseded below.
+#   o-proj 576x576 + residual: 64x64 tiles at 9216 rows (14.3 vs 15.9 us) (re-confirmed below).
 # End to end the bench is unchanged within noise (27 571 vs 27 491 msgs/s, three
 # interleaved runs each, profiles/r02_gemm_measured_ab.jsonl).
 #   SwiGLU gate/up with the staggered 256x256 kernel (cfg 19, scripts/gemm256_check.py,
 #     producer row partials): 22.2 / 41.6 / 67.2 us at 4608 / 9216 / 16384 rows vs 24.1 /
-#     43.8 / 68.2 for the best of cfg 0 and 10 (profiles/r02_gemm256_check.json).
-#   o-proj: with the residual prefetched before the K loop the rule's 128x64 tile wins at
-#     9216 rows again (14.06 vs 14.33 us, profiles/r02_norm_epilogue_cost.txt): no exception.
+#     43.8 / 68.2 for the best of cfg 0 and 10; its persistent form (cfg 20, the default
+#     from 4096 rows) 39.1 / 60.9 us at 9216 / 16384 (profiles/r02_gemm256_check.json).
+#   Re-swept with the engine's norm flavour (producer partials in / out; interleaved,
+#   profiles/r02s3_gemm_tune.json): gate/up at 2304 rows 128x128 8-wave (13.7 vs 16.9 us);
+#   o-proj at 9216 rows 64x64 (14.7 vs 16.4 us).
 GEMM_MEASURED = {
-    ("swiglu", 3072, 576): [(4096, 1 << 30, 20)],
+    ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 1 << 30, 20)],
+    ("resid", 576, 576): [(8192, 10240, 3)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
 
@@ -360,7 +363,8 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
         # (kbench, B=4096/8192: 17.8/27.6 us vs 22.0/31.3 us with 128x64); 32-row
         # tiles up to 2048 rows (7.4 / 8.2 / 11.4 vs 10.1 / 10.7 / 12.3 us at 512 / 1024
         # / 2048, profiles/r01c_kbench_small_buckets.json)
-        cfg = 17 if M <= 2 * GEMM_SMALL_M else 3
+        # 128x64 from 12 288 rows (prefill halves: 39.0 vs 40.7 us at 16 384, r02s3_gemm_tune.json)
+        cfg = 17 if M <= 2 * GEMM_SMALL_M else (1 if M >= 12288 else 3)
     ld = _ss_check(ss_in, M, "gemm_qkv_rope ss_in")
     rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,

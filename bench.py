@@ -69,7 +69,10 @@ def _args(argv=None):
     p.add_argument("--msgs-per-step", type=int, default=16384)
     p.add_argument("--max-slots", type=int, default=8192)
     p.add_argument("--steps-per-graph", type=int, default=2)
-    p.add_argument("--admit-frac", type=float, default=0.25)
+    # admit when this fraction of rows is free: 0.25 / 0.125 / 0.0625 -> 28 258 / 28 466 (one box),
+    # 27 728 / 27 910 for 0.125 / 0.0625 (another): within noise, 0.125 kept
+    # (profiles/r02s3_admit_frac_ab*.jsonl)
+    p.add_argument("--admit-frac", type=float, default=0.125)
     p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)
     p.add_argument("--bus-shards", type=int, default=3,

@@ -55,3 +55,28 @@ def test_argtypes_match_c_signatures():
 @pytest.mark.parametrize("fn", ["sg_rmsnorm_residual", "sg_attn_prefill", "sg_attn_decode", "sg_fsm_sample", "sg_gemm"])
 def test_expected_entry_points_exist(fn):
     assert fn in _c_signatures()
+
+
+def test_row_partials_image_and_checks():
+    """x² partials image: [SS_PARTS, M rounded up to 16-B row groups], validated before
+    any launch (CPU tensors and wrong shapes are refused)."""
+    import torch
+
+    ss = ops.ss_buffer(10, "cpu")
+    assert ss.shape == (ops.SS_PARTS, 12) and ss.dtype == torch.float32 and not ss.any()
+    with pytest.raises(ValueError):
+        ops._ss_check(ss, 10, "t")  # not on the GPU
+    with pytest.raises(ValueError):
+        ops._ss_check(torch.zeros(ops.SS_PARTS - 1, 16), 4, "t")
+    assert ops._ss_check(None, 10, "t") == 0
+
+
+def test_measured_tile_exceptions():
+    """gate/up uses the staggered 256x256 kernels where measured faster (persistent
+    form from 4096 rows), the 8-wave 128x128 tile just below."""
+    if not ops.GEMM_MEASURED:
+        pytest.skip("SMSGATE_GEMM_MEASURED=0")
+    assert ops.gemm_cfg(9216, 3072, epi="swiglu", K=576) == 20
+    assert ops.gemm_cfg(16384, 3072, epi="swiglu", K=576) == 20
+    assert ops.gemm_cfg(2304, 3072, epi="swiglu", K=576) == 13
+    assert ops.GEMM_TILES[20] == (256, 256) and 20 in ops.GEMM_SWIGLU_ONLY

@@ -72,6 +72,23 @@ def main() -> None:
             row["tflops"] = round(2 * M * H * K / row["resid"] / 1e6, 1)
             out[f"{name} M={M} cfg={cfg}"] = row
             print(f"{name} M={M} cfg={cfg} {row}", flush=True)
+    # lm_head + FSM-masked arg-max (EPI 4) against the same GEMM storing logits
+    from smsgate_amd.models.tokenizer import load_tokenizer
+    from smsgate_amd.serving.fsm import build_fsm
+
+    tk = load_tokenizer()
+    V = (tk.vocab_size + 127) // 128 * 128
+    fsm = build_fsm(tk, V).to_device(dev)
+    wl = (torch.randn(V, H, device=dev) * 0.05).to(torch.bfloat16)
+    st = torch.randint(0, fsm.num_states, (M,), device=dev, dtype=torch.int32)
+    best = torch.zeros(M, dtype=torch.int64, device=dev)
+    row = {"store_norm_cfg0": round(min(graph_time(lambda: ops.gemm(x, wl, norm_eps=1e-5, cfg=0), 20, 10)
+                                        for _ in range(3)), 2)}
+    for cfg in (0, 3):
+        row[f"argmax_ssin_cfg{cfg}"] = round(min(graph_time(lambda: ops.gemm_argmax(
+            x, wl, st, fsm, best, norm_eps=1e-5, cfg=cfg, ss_in=ss), 20, 10) for _ in range(3)), 2)
+    out[f"lm_argmax M={M} V={V}"] = row
+    print(f"lm_argmax M={M} V={V} {row}", flush=True)
     print(json.dumps(out))
 
 

@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-python -m smsgate_amd.ops.build > gpurun_out/build.log 2>&1 || exit 1
+[ -f smsgate_amd/ops/_lib/libsmsgate_kernels.so ] || { echo "build the kernels first"; exit 1; }
 R=$GRAFT_REPO_ROOT
 cd /tmp
 i=0

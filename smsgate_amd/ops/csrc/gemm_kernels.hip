@@ -254,6 +254,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       }
     }
   }
+  // EPI 4: the FSM state of each of this thread's epilogue rows, likewise (one link of
+  // the row_state -> state_mask -> mask-word chain fewer after the K loop)
+  constexpr int XIT = EPI == 4 ? (BM * (BN / 8)) / NT : 1;
+  int xstate[XIT];
+  if constexpr (EPI == 4) {
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) xstate[it] = xa.row_state[min(m0 + (tid + it * NT) / (BN / 8), M - 1)];
+  }
   f32x4 acc[FM][FN];
   float ss[FM];
 #pragma unroll
@@ -433,14 +441,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   if constexpr (EPI == 4) {
     constexpr int CPR4 = BN / 8;
     static_assert(CPR4 <= 64 && (CPR4 & (CPR4 - 1)) == 0, "row chunks must fit a wave");
+    static_assert((BM * CPR4) % NT == 0, "uniform epilogue trips");
     const int words = N >> 5;
-    for (int q = tid; q < BM * CPR4; q += NT) {
+#pragma unroll
+    for (int it = 0; it < XIT; ++it) {
+      const int q = tid + it * NT;
       const int row = q / CPR4, c = q % CPR4;
       const int gr = m0 + row;
       unsigned long long key = 0ull;
       if (gr < M) {
         const int col = n0 + c * 8;
-        const uint32_t* mrow = xa.masks + (size_t)xa.state_mask[xa.row_state[gr]] * words;
+        const uint32_t* mrow = xa.masks + (size_t)xa.state_mask[xstate[it]] * words;
         const uint32_t bits = (mrow[col >> 5] >> (col & 31)) & 0xffu;
         if (bits) {
           const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);

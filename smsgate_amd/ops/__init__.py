@@ -225,10 +225,11 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #     43.8 / 68.2 for the best of cfg 0 and 10; its persistent form (cfg 20, the default
 #     from 4096 rows) 39.1 / 60.9 us at 9216 / 16384 (profiles/r02_gemm256_check.json).
 #   Re-swept with the engine's norm flavour (producer partials in / out; interleaved,
-#   profiles/r02s3_gemm_tune.json): gate/up at 2304 rows 128x128 8-wave (13.7 vs 16.9 us);
+#   profiles/r02s3_gemm_tune.json): gate/up at 2304 rows 128x128 8-wave (13.7 vs 16.9 us),
+#   at 4608 rows (one tile round: nothing for persistence to overlap) cfg 19 (21.1 vs 21.6);
 #   o-proj at 9216 rows 64x64 (14.7 vs 16.4 us).
 GEMM_MEASURED = {
-    ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 1 << 30, 20)],
+    ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 6143, 19), (6144, 1 << 30, 20)],
     ("resid", 576, 576): [(8192, 10240, 3)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 

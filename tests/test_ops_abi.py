@@ -79,4 +79,5 @@ def test_measured_tile_exceptions():
     assert ops.gemm_cfg(9216, 3072, epi="swiglu", K=576) == 20
     assert ops.gemm_cfg(16384, 3072, epi="swiglu", K=576) == 20
     assert ops.gemm_cfg(2304, 3072, epi="swiglu", K=576) == 13
+    assert ops.gemm_cfg(4608, 3072, epi="swiglu", K=576) == 19
     assert ops.GEMM_TILES[20] == (256, 256) and 20 in ops.GEMM_SWIGLU_ONLY

@@ -191,7 +191,8 @@ def run_replica(args, rank: int, world: int, local: int):
         from smsgate_amd.serving import freeze_gc_for_launch_loop
 
         freeze_gc_for_launch_loop()
-    coord = Coordinator(engine, conns, bus_dsn=bus_dsn, world=world)
+    # the node's brokers see only this node's ranks (LOCAL_WORLD_SIZE under torchrun)
+    coord = Coordinator(engine, conns, bus_dsn=bus_dsn, node_ranks=int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     coord.wait_all("ready")
 
     def sync():

@@ -39,6 +39,7 @@ __all__ = [
     "SUBJECT_PROCESSING",
     "SUBJECT_FAILED",
     "SUBJECT_CATEGORIZED",
+    "SUBJECT_FAILED_FINAL",
     "STREAM_NAME",
     "ALL_SUBJECTS",
     "DeliverPolicy",
@@ -63,8 +64,12 @@ SUBJECT_PARSED = "sms.parsed"
 SUBJECT_PROCESSING = "sms.processing"
 SUBJECT_FAILED = "sms.failed"
 SUBJECT_CATEGORIZED = "sms.categorized"
+# terminal DLQ: messages whose DLQ reparse failed again (no consumer in the pipeline:
+# kept for inspection, never re-fed to the DLQ worker that reads sms.failed)
+SUBJECT_FAILED_FINAL = "sms.failed.final"
 STREAM_NAME = "SMS"
-ALL_SUBJECTS = (SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_FAILED, SUBJECT_PROCESSING, SUBJECT_CATEGORIZED)
+ALL_SUBJECTS = (SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_FAILED, SUBJECT_PROCESSING, SUBJECT_CATEGORIZED,
+                SUBJECT_FAILED_FINAL)
 
 
 class BusError(RuntimeError):

@@ -120,18 +120,31 @@ def upgrade_from_reference(c: Connection, rev: str) -> int:
     head_cols = [col.name for col in sms_data.columns]
     sel = ", ".join(f"{mapping.get(n, n)} AS {n}" for n in head_cols)
     key = mapping["msg_id"]
-    cols = [col.copy() for col in sms_data.columns]
-    Table("sms_data__new", MetaData(), *cols).create(c)
+    # carry the rows aside, then recreate sms_data under its own name: the primary key,
+    # the unique constraint and (Postgres) the id sequence get the names Alembic's chain
+    # gave them (sms_data_pkey, sms_data_id_seq), not the names of a renamed copy
     c.execute(text(
-        f"INSERT INTO sms_data__new ({', '.join(head_cols)}) SELECT {sel} FROM sms_data "
+        f"CREATE TABLE sms_data__carry AS SELECT {sel} FROM sms_data "
         f"WHERE ({key}) IS NULL OR id IN (SELECT MAX(id) FROM sms_data GROUP BY {key})"))
-    n = int(c.execute(text("SELECT COUNT(*) FROM sms_data__new")).scalar() or 0)
     c.execute(text("DROP TABLE sms_data"))
-    c.execute(text("ALTER TABLE sms_data__new RENAME TO sms_data"))
+    _create_table(c)
+    c.execute(text(f"INSERT INTO sms_data ({', '.join(head_cols)}) SELECT {', '.join(head_cols)} FROM sms_data__carry"))
+    c.execute(text("DROP TABLE sms_data__carry"))
+    n = int(c.execute(text("SELECT COUNT(*) FROM sms_data")).scalar() or 0)
+    _reset_id_sequence(c)
     _create_indexes(c)
     c.execute(text("UPDATE alembic_version SET version_num = :v"), {"v": REFERENCE_HEAD})
     _set(c, HEAD)
     return n
+
+
+def _reset_id_sequence(c: Connection) -> None:
+    """After rows were inserted with explicit ids: move Postgres' serial sequence past
+    MAX(id), so the writer's INSERT (which never passes ``id``) does not collide with
+    a carried row.  SQLite's INTEGER PRIMARY KEY continues from MAX(rowid) by itself."""
+    if c.dialect.name == "postgresql":
+        c.execute(text("SELECT setval(pg_get_serial_sequence('sms_data', 'id'), "
+                       "COALESCE(MAX(id), 1), MAX(id) IS NOT NULL) FROM sms_data"))
 
 
 def _version_table(c: Connection) -> Table:

@@ -489,7 +489,8 @@ struct Waiter {
   double deadline;  // wall clock; INFINITY = wait forever
 };
 
-const char* kAllSubjects[] = {"sms.raw", "sms.parsed", "sms.failed", "sms.processing", "sms.categorized"};
+const char* kAllSubjects[] = {"sms.raw",        "sms.parsed",      "sms.failed",
+                              "sms.processing", "sms.categorized", "sms.failed.final"};
 
 class Server {
  public:

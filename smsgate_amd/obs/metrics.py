@@ -80,6 +80,8 @@ LLM_TRUNCATED = Counter("llm_prompt_truncated_total",
 GEMINI_LATENCY = Summary("sms_parser_gemini_seconds", "Seconds spent in the extraction backend call")
 ACK_PENDING = Gauge("sms_parser_ack_pending", "Delivered-but-unacked messages of the parser consumer")
 
+DLQ_REPARSE_FAILED = Counter("sms_dlq_reparse_failed_total",
+                             "DLQ messages whose reparse failed again (moved to sms.failed.final)")
 WRITER_OK = Counter("pb_writer_parsed_ok_total", "Records saved by the writer")
 WRITER_FAIL = Counter("pb_writer_parsed_fail_total", "Records the writer failed to save")
 WRITER_LAG = Gauge("pb_writer_stream_lag", "sms.parsed consumer lag (messages)")

@@ -37,6 +37,8 @@ __all__ = [
     "spec_verify_keys",
     "fsm_commit",
     "gemm_argmax",
+    "copy_masks",
+    "ref_copy_masks",
     "SPEC_MAX_K",
     "gemm",
     "gemm_cfg",
@@ -90,7 +92,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_attn_decode_cascade.restype = _c_int
     lib.sg_fsm_sample.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_float,
-                                  ctypes.c_uint, _vp]
+                                  ctypes.c_uint, _ip, _vp, _vp]
     lib.sg_gemm.argtypes = [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                             _c_float, _c_int, _vp, _vp, _c_int, _vp]
     lib.sg_gemm_qkv_rope.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_float, _c_int, _ip, _ip, _vp, _vp, _vp,
@@ -108,15 +110,17 @@ def _declare(lib: ctypes.CDLL) -> None:
         [_ip, _ip, _c_int, _vp, _ip, _c_int] + [_ip] * 8 + [_vp]
     lib.sg_spec_plan.restype = _c_int
     lib.sg_spec_verify.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
-                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _vp]
+                                   _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _ip, _vp, _vp]
     lib.sg_spec_verify.restype = _c_int
     lib.sg_spec_verify_keys.argtypes = [_vp] + fsm_t + [_c_int] * 3 + [_ip] * 10 + [_c_int, _c_int, _vp]
     lib.sg_spec_verify_keys.restype = _c_int
     lib.sg_fsm_commit.argtypes = [_vp, _ip] + fsm_t + [_c_int] * 3 + [_ip] * 6 + [_c_int, _c_int, _vp]
     lib.sg_fsm_commit.restype = _c_int
     lib.sg_gemm_argmax.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int, _ip, _ip, _vp,
-                                   _vp, _vp, _c_int, _vp]
+                                   _vp, _vp, _c_int, _ip, _vp, _vp]
     lib.sg_gemm_argmax.restype = _c_int
+    lib.sg_copy_masks.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp, _vp]
+    lib.sg_copy_masks.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
         getattr(lib, f).restype = _c_int
@@ -527,23 +531,81 @@ def attn_spec(q: torch.Tensor, row_start: torch.Tensor, row_nd: torch.Tensor, x_
     return out
 
 
+def _copy_args(fsm, row_masks: Optional[torch.Tensor], rows: int, name: str):
+    """(copy_kind, row_masks) pointers for a kernel that honours copy masks, or (None, None)."""
+    if row_masks is None:
+        return None, None
+    if row_masks.dtype != torch.int32 or not row_masks.is_contiguous() or row_masks.dim() != 2 \
+            or row_masks.shape[0] < rows or row_masks.shape[1] != fsm.vocab // 32 or fsm.copy_kind_t is None:
+        raise ValueError(f"{name}: row_masks must be int32 [>= {rows}, {fsm.vocab // 32}] (ops.copy_masks)")
+    return _p(fsm.copy_kind_t), _p(row_masks)
+
+
 def fsm_sample(logits: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tensor, out_buf: torch.Tensor,
                out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, slot_id: torch.Tensor,
-               temperature: float, seed: int, row_map: Optional[torch.Tensor] = None) -> None:
+               temperature: float, seed: int, row_map: Optional[torch.Tensor] = None,
+               row_masks: Optional[torch.Tensor] = None) -> None:
     """Masked argmax/Gumbel sampling + FSM transition for ``B = logits.shape[0]`` rows.
 
-    Logits row ``i`` updates state row ``row_map[i]`` (or ``i``)."""
+    Logits row ``i`` updates state row ``row_map[i]`` (or ``i``).  ``row_masks``
+    (:func:`copy_masks`, one row per logits row): rows in copy states use their own mask."""
     B, V = logits.shape
     ldl = logits.stride(0)
     assert logits.dtype == torch.bfloat16 and logits.stride(1) == 1
     max_out = out_buf.shape[1]
     inv_t = 0.0 if temperature <= 0 else 1.0 / temperature
+    ck, rm = _copy_args(fsm, row_masks, B, "fsm_sample")
     _check(load_library().sg_fsm_sample(
         _p(logits), ldl, _p(fsm.masks), _p(fsm.state_mask), _p(state), _p(fsm.next_sep_t), _p(fsm.next_tok_t),
         _p(fsm.enum_tok_t), _p(fsm.enum_next_t), fsm.E, fsm.sep_token, fsm.done_state, _p(tok_io), _p(out_buf),
         _p(out_len), _p(done), _p(pos), _p(slot_id), _p(row_map), max_out, V, B, inv_t, seed & 0xFFFFFFFF,
-        _stream()),
+        ck, rm, _stream()),
         "fsm_sample")
+
+
+def copy_masks(fsm, row_state: torch.Tensor, prev_tok: torch.Tensor, row_slot: torch.Tensor,
+               body_buf: torch.Tensor, body_len: torch.Tensor, out: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
+    """Per-row allowed-token masks of copy-constrained decoding (csrc/spec_kernels.hip
+    ``copy_mask_kernel``): for each of ``n`` rows whose state is a copy state, ``out[r]``
+    = the state's schema mask AND (<sep> | any token of the row's body at a value's
+    first position | a token following ``prev_tok[r]`` in the body after that).  The
+    body of row ``r`` is ``body_buf[row_slot[r], :body_len[row_slot[r]]]``.  Rows in
+    other states are not written (the consumers only read copy rows)."""
+    n = row_state.numel() if n is None else n
+    S1, LB = body_buf.shape
+    for name, t in (("row_state", row_state), ("prev_tok", prev_tok), ("row_slot", row_slot)):
+        _req(t, torch.int32, name)
+        if t.numel() < n:
+            raise ValueError(f"copy_masks: {name} has fewer than {n} rows")
+    _req(body_buf, torch.int32, "body_buf")
+    _req(body_len, torch.int32, "body_len")
+    _req(out, torch.int32, "out")
+    if out.dim() != 2 or out.shape[0] < n or out.shape[1] != fsm.vocab // 32 or body_len.numel() != S1:
+        raise ValueError("copy_masks: out must be [>= n, vocab/32]; body_len must match body_buf")
+    if fsm.copy_kind_t is None:
+        raise ValueError("copy_masks: the FSM has no copy states (to_device first)")
+    _check(load_library().sg_copy_masks(_p(fsm.masks), _p(fsm.state_mask), fsm.sep_token, fsm.vocab,
+                                        _p(fsm.copy_kind_t), _p(row_state), _p(prev_tok), _p(row_slot),
+                                        _p(body_buf), _p(body_len), LB, n, _p(out), _stream()), "copy_masks")
+    return out
+
+
+def ref_copy_masks(fsm, row_state, prev_tok, row_slot, body_buf, body_len) -> torch.Tensor:
+    """fp32-free reference of :func:`copy_masks`: [n, vocab] bool (rows in non-copy
+    states get their schema mask)."""
+    import numpy as np
+
+    st, pv, sl = (t.cpu().numpy() for t in (row_state, prev_tok, row_slot))
+    bb, bl = body_buf.cpu().numpy(), body_len.cpu().numpy()
+    rows = [fsm.copy_mask_host(int(st[r]), int(pv[r]), bb[sl[r], : bl[sl[r]]].tolist()) for r in range(len(st))]
+    return torch.from_numpy(np.stack(rows)) if rows else torch.zeros(0, fsm.vocab, dtype=torch.bool)
+
+
+def unpack_masks(words: torch.Tensor) -> torch.Tensor:
+    """int32 [n, V/32] bit masks -> bool [n, V] (bit j of word w = token 32w + j)."""
+    w = words.to(torch.int64) & 0xFFFFFFFF
+    bits = (w.unsqueeze(-1) >> torch.arange(32, device=words.device)) & 1
+    return bits.reshape(words.shape[0], -1).bool()
 
 
 SPEC_MAX_K = 8
@@ -601,9 +663,11 @@ def spec_plan(fsm, state: torch.Tensor, x_state: torch.Tensor, K: int, T_cap: in
 
 def spec_verify(logits: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.Tensor, out_buf: torch.Tensor,
                 out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, x_tok: torch.Tensor,
-                row_start: torch.Tensor, row_nd: torch.Tensor, accepted: Optional[torch.Tensor] = None) -> None:
+                row_start: torch.Tensor, row_nd: torch.Tensor, accepted: Optional[torch.Tensor] = None,
+                row_masks: Optional[torch.Tensor] = None) -> None:
     """Greedy FSM-masked verification of the drafts of ``B = tok_buf.numel()`` rows
-    (``logits`` [T_cap, V] over the pseudo-rows :func:`spec_plan` laid out)."""
+    (``logits`` [T_cap, V] over the pseudo-rows :func:`spec_plan` laid out).
+    ``row_masks``: the pseudo-rows' copy masks (:func:`copy_masks`)."""
     B = tok_buf.numel()
     T, V = logits.shape
     if logits.dtype != torch.bfloat16 or logits.stride(1) != 1 or x_tok.numel() < T:
@@ -614,20 +678,22 @@ def spec_verify(logits: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.T
             raise ValueError(f"spec_verify: bad {name}")
     if accepted is not None and (accepted.numel() < B or accepted.dtype != torch.int32):
         raise ValueError("spec_verify: bad accepted")
+    ck, rm = _copy_args(fsm, row_masks, T, "spec_verify")
     _check(load_library().sg_spec_verify(
         _p(logits), logits.stride(0), _p(fsm.masks), _p(fsm.state_mask), _p(state), _p(fsm.next_sep_t),
         _p(fsm.next_tok_t), _p(fsm.enum_tok_t), _p(fsm.enum_next_t), fsm.E, fsm.sep_token, fsm.done_state,
         _p(tok_buf), _p(out_buf), _p(out_len), _p(done), _p(pos), _p(x_tok), _p(row_start), _p(row_nd),
-        _p(accepted), out_buf.shape[1], V, B, _stream()), "spec_verify")
+        _p(accepted), out_buf.shape[1], V, B, ck, rm, _stream()), "spec_verify")
 
 
 def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, best: torch.Tensor,
                 norm_eps: Optional[float] = None, cfg: Optional[int] = None,
-                ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+                ss_in: Optional[torch.Tensor] = None, row_masks: Optional[torch.Tensor] = None) -> torch.Tensor:
     """lm_head GEMM with the schema-FSM masked arg-max fused in (EPI 4): for every
     row, ``best[row] = max(argmax_key(bf16 logit, token))`` over the tokens its FSM
     state allows — no logits are written.  ``w`` [V, K] (final norm folded in when
-    ``norm_eps``); ``best`` uint64-as-int64 [>= M] is ZEROED here first."""
+    ``norm_eps``); ``best`` uint64-as-int64 [>= M] is ZEROED here first.
+    ``row_masks`` (:func:`copy_masks`): rows in copy states use their own mask row."""
     M, K = a.shape
     N = w.shape[0]
     if a.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or a.stride(1) != 1 or a.stride(0) % 8:
@@ -646,9 +712,10 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, 
         raise ValueError("gemm_argmax: ss_in needs norm_eps")
     ld = _ss_check(ss_in, M, "gemm_argmax ss_in")
     norm = 0 if norm_eps is None else (2 if ss_in is not None else 1)
+    ck, rm = _copy_args(fsm, row_masks, M, "gemm_argmax")
     _check(load_library().sg_gemm_argmax(_p(a), a.stride(0), _p(w), M, N, K, float(norm_eps or 0.0),
                                          norm, cfg, _p(row_state), _p(fsm.state_mask),
-                                         _p(fsm.masks), _p(best), _p(ss_in), ld, _stream()), "gemm_argmax")
+                                         _p(fsm.masks), _p(best), _p(ss_in), ld, ck, rm, _stream()), "gemm_argmax")
     return best
 
 

@@ -79,6 +79,11 @@ struct ArgmaxArgs {
   const int* state_mask;        // [S] state -> mask row
   const uint32_t* masks;        // [mask rows][N / 32] allowed-token bits
   unsigned long long* best;     // [M] running max of argmax_key(), zeroed before the launch
+  // copy-constrained decoding (optional): a row whose state has copy_kind != 0 is
+  // masked with its own row_masks[row] (the schema mask AND its body's copy set,
+  // built by sg_copy_masks) instead of the state's mask row
+  const int* copy_kind;         // [S] or null
+  const uint32_t* row_masks;    // [M][N / 32]
 };
 
 // Orderable key: larger bf16 value first, then the SMALLER token index (the tie rule
@@ -261,6 +266,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   if constexpr (EPI == 4) {
 #pragma unroll
     for (int it = 0; it < XIT; ++it) xstate[it] = xa.row_state[min(m0 + (tid + it * NT) / (BN / 8), M - 1)];
+    // copy rows read their own mask row: resolve the mask row pointers now, so the
+    // epilogue's mask word is one load (state_mask / copy_kind lookups hide behind the K loop)
+    if (xa.copy_kind != nullptr) {
+#pragma unroll
+      for (int it = 0; it < XIT; ++it)
+        xstate[it] = xa.copy_kind[xstate[it]] ? -1 - min(m0 + (tid + it * NT) / (BN / 8), M - 1)
+                                              : xa.state_mask[xstate[it]];
+    } else {
+#pragma unroll
+      for (int it = 0; it < XIT; ++it) xstate[it] = xa.state_mask[xstate[it]];
+    }
   }
   f32x4 acc[FM][FN];
   float ss[FM];
@@ -451,7 +467,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       unsigned long long key = 0ull;
       if (gr < M) {
         const int col = n0 + c * 8;
-        const uint32_t* mrow = xa.masks + (size_t)xa.state_mask[xstate[it]] * words;
+        // xstate: the mask row of the state (>= 0) or -1 - row for a copy row
+        const uint32_t* mrow = xstate[it] >= 0 ? xa.masks + (size_t)xstate[it] * words
+                                               : xa.row_masks + (size_t)(-1 - xstate[it]) * words;
         const uint32_t bits = (mrow[col >> 5] >> (col & 31)) & 0xffu;
         if (bits) {
           const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
@@ -1105,10 +1123,12 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
 // best [M] uint64 zeroed before the launch; cfg 0 (128x128), 3 (64x64), 17 (32x64).
 int sg_gemm_argmax(const void* A, int lda, const void* W, int M, int N, int K, float eps, int norm, int cfg,
                    const int* row_state, const int* state_mask, const void* masks, void* best, const float* ssin,
-                   int ss_ld, hipStream_t stream) {
+                   int ss_ld, const int* copy_kind, const void* row_masks, hipStream_t stream) {
   if (M <= 0 || K % BK != 0 || lda % 8 != 0 || N % 128 != 0) return -2;
   if (norm == 2 && (!ssin || ss_ld < M)) return -2;
-  ArgmaxArgs xa{row_state, state_mask, (const uint32_t*)masks, (unsigned long long*)best};
+  if (copy_kind != nullptr && row_masks == nullptr) return -2;
+  ArgmaxArgs xa{row_state, state_mask, (const uint32_t*)masks, (unsigned long long*)best, copy_kind,
+                (const uint32_t*)row_masks};
   RopeArgs ra{};
   const NormArgs na{ssin, nullptr, ss_ld};
 #define SG_AM(BM_, BN_, WM_, WN_)                                                                                      \

@@ -1585,7 +1585,7 @@ __global__ void __launch_bounds__(256) fsm_sample_kernel(
     const int* __restrict__ enum_tok, const int* __restrict__ enum_next, int E, int sep_token, int done_state,
     int* __restrict__ tok_io, int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done,
     int* __restrict__ pos, const int* __restrict__ slot_id, const int* __restrict__ row_map, int max_out, int V,
-    float inv_temp, uint32_t seed) {
+    float inv_temp, uint32_t seed, const int* __restrict__ copy_kind, const uint32_t* __restrict__ row_masks) {
   const int lr = blockIdx.x;                      // logits row
   const int b = row_map ? row_map[lr] : lr;       // state row
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1593,7 +1593,9 @@ __global__ void __launch_bounds__(256) fsm_sample_kernel(
   __shared__ int bi[4];
   if (done[b]) return;  // block-uniform
   const int s = state[b];
-  const uint32_t* mrow = masks + (size_t)state_mask[s] * (V >> 5);
+  // copy state: the row's own mask (ops.copy_masks, one mask row per logits row)
+  const uint32_t* mrow = (copy_kind != nullptr && copy_kind[s]) ? row_masks + (size_t)lr * (V >> 5)
+                                                                 : masks + (size_t)state_mask[s] * (V >> 5);
   const uint16_t* lrow = logits + (size_t)lr * ldl;
   const uint32_t rseed = hash3(seed, (uint32_t)slot_id[b], (uint32_t)out_len[b]);
   float best = -INFINITY;
@@ -1894,12 +1896,13 @@ int sg_fsm_sample(const void* logits, int ldl, const void* masks, const int* sta
                   const int* next_sep, const int* next_tok, const int* enum_tok, const int* enum_next, int E,
                   int sep_token, int done_state, int* tok_io, int* out_buf, int* out_len, int* done, int* pos,
                   const int* slot_id, const int* row_map, int max_out, int V, int B, float inv_temp,
-                  unsigned int seed, hipStream_t stream) {
-  if (V % 32 || ldl % 8) return -1;
+                  unsigned int seed, const int* copy_kind, const void* row_masks, hipStream_t stream) {
+  if (V % 32 || ldl % 8 || (copy_kind != nullptr && row_masks == nullptr)) return -1;
   if (B == 0) return 0;
   hipLaunchKernelGGL(fsm_sample_kernel, dim3(B), dim3(256), 0, stream, (const uint16_t*)logits, ldl,
                      (const uint32_t*)masks, state_mask, state, next_sep, next_tok, enum_tok, enum_next, E, sep_token,
-                     done_state, tok_io, out_buf, out_len, done, pos, slot_id, row_map, max_out, V, inv_temp, seed);
+                     done_state, tok_io, out_buf, out_len, done, pos, slot_id, row_map, max_out, V, inv_temp, seed,
+                     copy_kind, (const uint32_t*)row_masks);
   return (int)hipGetLastError();
 }
 

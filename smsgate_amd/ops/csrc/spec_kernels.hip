@@ -360,6 +360,54 @@ __global__ void __launch_bounds__(256) fsm_commit_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// copy-constrained decoding (serving/fsm.py COPY_START / COPY_NEXT states): the
+// per-row allowed-token mask = the state's schema mask AND the tokens the row may
+// copy from its own SMS body -- any body token at a value's first position, after
+// that only a token that follows the previous token somewhere in the body -- plus
+// <sep>.  One wave per row builds the bit set in LDS (V/32 words), then writes the
+// full mask row; rows in non-copy states are skipped (their mask row is never read:
+// the consumers check copy_kind[state] first).  Consumers: the lm_head arg-max
+// epilogue (EPI 4), fsm_sample_kernel, spec_verify_kernel.
+// ---------------------------------------------------------------------------
+#define COPY_MAX_WORDS 512  // V <= 16384
+
+__global__ void __launch_bounds__(256) copy_mask_kernel(
+    FsmTables fsm, const int* __restrict__ copy_kind, const int* __restrict__ row_state,
+    const int* __restrict__ prev_tok, const int* __restrict__ row_slot, const int* __restrict__ body_buf,
+    const int* __restrict__ body_len, int LB, int n, uint32_t* __restrict__ row_masks) {
+  __shared__ uint32_t bits[4][COPY_MAX_WORDS];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wid;
+  if (r >= n) return;  // wave-uniform: no block barrier below
+  const int s = row_state[r];
+  const int kind = copy_kind[s];
+  if (kind == 0) return;
+  const int words = fsm.V >> 5;
+  uint32_t* b = bits[wid];
+  for (int w = lane; w < words; w += 64) b[w] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const int sl = row_slot[r];
+  const int bl = min(body_len[sl], LB);
+  const int* body = body_buf + (size_t)sl * LB;
+  const int prev = prev_tok[r];
+  for (int j = lane; j < bl; j += 64) {
+    int cand = -1;
+    if (kind == 1) cand = body[j];
+    else if (j + 1 < bl && body[j] == prev) cand = body[j + 1];
+    if (cand >= 0 && cand < fsm.V) atomicOr(&b[cand >> 5], 1u << (cand & 31));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t* m = fsm.masks + (size_t)fsm.state_mask[s] * words;
+  const int sw = fsm.sep_token >> 5;
+  const uint32_t sbit = 1u << (fsm.sep_token & 31);
+  uint32_t* out = row_masks + (size_t)r * words;
+  for (int w = lane; w < words; w += 64) out[w] = (b[w] | (w == sw ? sbit : 0u)) & m[w];
+}
+
+// ---------------------------------------------------------------------------
 // verify: grid = B blocks of 256 threads.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) spec_verify_kernel(
@@ -368,7 +416,8 @@ __global__ void __launch_bounds__(256) spec_verify_kernel(
     const int* __restrict__ enum_tok, const int* __restrict__ enum_next, int E, int sep_token, int done_state,
     int* __restrict__ tok_buf, int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done,
     int* __restrict__ pos, const int* __restrict__ x_tok, const int* __restrict__ row_start,
-    const int* __restrict__ row_nd, int* __restrict__ accepted, int max_out, int V) {
+    const int* __restrict__ row_nd, int* __restrict__ accepted, int max_out, int V, const int* __restrict__ copy_kind,
+    const uint32_t* __restrict__ row_masks) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ float bv[4];
@@ -382,7 +431,10 @@ __global__ void __launch_bounds__(256) spec_verify_kernel(
   int s = state[b];
   int emitted = 0;
   for (int i = 0; i <= nd; ++i) {
-    const uint32_t* mrow = masks + (size_t)state_mask[s] * (V >> 5);
+    // copy state: pseudo-row st + i's own mask (built for x_state[st + i] == s: the
+    // drafts before it were accepted, or the loop would have stopped)
+    const uint32_t* mrow = (copy_kind != nullptr && copy_kind[s]) ? row_masks + (size_t)(st + i) * (V >> 5)
+                                                                   : masks + (size_t)state_mask[s] * (V >> 5);
     const uint16_t* lrow = logits + (size_t)(st + i) * ldl;
     float best = -INFINITY;
     int besti = 0x7fffffff;
@@ -479,12 +531,13 @@ int sg_spec_verify(const void* logits, int ldl, const void* masks, const int* st
                    const int* next_sep, const int* next_tok, const int* enum_tok, const int* enum_next, int E,
                    int sep_token, int done_state, int* tok_buf, int* out_buf, int* out_len, int* done, int* pos,
                    const int* x_tok, const int* row_start, const int* row_nd, int* accepted, int max_out, int V, int B,
-                   hipStream_t stream) {
-  if (V % 32 || ldl % 8) return -1;
+                   const int* copy_kind, const void* row_masks, hipStream_t stream) {
+  if (V % 32 || ldl % 8 || (copy_kind != nullptr && row_masks == nullptr)) return -1;
   if (B == 0) return 0;
   hipLaunchKernelGGL(spec_verify_kernel, dim3(B), dim3(256), 0, stream, (const uint16_t*)logits, ldl,
                      (const uint32_t*)masks, state_mask, state, next_sep, next_tok, enum_tok, enum_next, E, sep_token,
-                     done_state, tok_buf, out_buf, out_len, done, pos, x_tok, row_start, row_nd, accepted, max_out, V);
+                     done_state, tok_buf, out_buf, out_len, done, pos, x_tok, row_start, row_nd, accepted, max_out, V,
+                     copy_kind, (const uint32_t*)row_masks);
   return (int)hipGetLastError();
 }
 
@@ -510,6 +563,20 @@ int sg_fsm_commit(const void* best, const int* row_map, const void* masks, const
   const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
   hipLaunchKernelGGL(fsm_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, f,
                      (const unsigned long long*)best, row_map, state, tok_io, out_buf, out_len, done, pos, max_out, B);
+  return (int)hipGetLastError();
+}
+
+// per-row copy masks (copy_mask_kernel) for n rows: row r in state row_state[r], its
+// last emitted token prev_tok[r], its prompt ids body_buf[row_slot[r]]; row_masks
+// [n][V/32].  Rows whose state is not a copy state are left untouched.
+int sg_copy_masks(const void* masks, const int* state_mask, int sep_token, int V, const int* copy_kind,
+                  const int* row_state, const int* prev_tok, const int* row_slot, const int* body_buf,
+                  const int* body_len, int LB, int n, void* row_masks, hipStream_t stream) {
+  if (V % 32 || V / 32 > COPY_MAX_WORDS || LB <= 0 || sep_token < 0 || sep_token >= V) return -1;
+  if (n == 0) return 0;
+  const FsmTables f = make_fsm(masks, state_mask, nullptr, nullptr, nullptr, nullptr, 0, sep_token, 0, V);
+  hipLaunchKernelGGL(copy_mask_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, f, copy_kind, row_state, prev_tok,
+                     row_slot, body_buf, body_len, LB, n, (uint32_t*)row_masks);
   return (int)hipGetLastError();
 }
 

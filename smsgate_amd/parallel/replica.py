@@ -185,13 +185,16 @@ class Coordinator:
     COUNTER = "bench_raw_counter"
 
     def __init__(self, engine, conns: Sequence[Connection], bus_dsn: Optional[str] = None,
-                 world: int = 1) -> None:
+                 node_ranks: int = 1) -> None:
+        """``node_ranks``: the ranks whose parser processes publish into THIS node's
+        broker (LOCAL_WORLD_SIZE: each node starts its own brokers, so a multi-node
+        job's drain target counts only the node's own ranks)."""
         from ..serving.remote import EngineServer
 
         self.events: Dict[str, Dict[int, Any]] = {}
         self.server = EngineServer(engine, conns, on_control=self._on_control)
         self.n = len(conns)
-        self.world = world
+        self.node_ranks = node_ranks
         self.bus = None
         if bus_dsn:
             from ..bus.base import SUBJECT_RAW
@@ -237,7 +240,7 @@ class Coordinator:
         self.wait_all("prepared")
         target = 0
         if self.bus is not None:
-            n_raw = sum(len(s) for s in seeds_per_worker) * n_per_step * self.world
+            n_raw = sum(len(s) for s in seeds_per_worker) * n_per_step * self.node_ranks
             target = self.bus.consumer_info("SMS", self.COUNTER)["num_pending"] + n_raw
         if sync is not None:
             sync()

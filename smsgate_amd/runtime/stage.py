@@ -12,7 +12,9 @@ is the one loop, written once:
 * never dies on a handler exception (D1/D2), and bounds poison messages:
 
   - a :class:`~smsgate_amd.runtime.errors.TransientError` (engine restarting,
-    socket closed) naks the whole batch with a delay — not the messages' fault;
+    socket closed), a ``BusError`` or a ``ConnectionError`` (a publish / ack to the
+    broker failed mid-batch) naks the whole batch with a delay — not the
+    messages' fault, so it never counts toward dead-lettering;
   - any other exception re-runs the batch one message at a time, so the good
     messages of the batch go through and only the failing one is isolated;
     that one is nak'ed with a delay until it has been delivered
@@ -30,13 +32,18 @@ import logging
 import time
 from typing import Awaitable, Callable, List, Optional, Sequence
 
-from ..bus.base import Bus, Msg, Subscription
+from ..bus.base import Bus, BusError, Msg, Subscription
 from ..obs.errors import sentry_capture
 from .errors import TransientError
 
-__all__ = ["Stage", "BatchHandler", "dlq_publisher"]
+__all__ = ["Stage", "BatchHandler", "dlq_publisher", "TRANSIENT"]
 
 log = logging.getLogger(__name__)
+
+# not the messages' fault: the batch is nak'ed whole (never split into per-message
+# re-runs, never counted toward dead-lettering) -- a dependency (engine, broker) is
+# down or a publish / ack to the broker failed mid-batch
+TRANSIENT = (TransientError, BusError, ConnectionError)
 
 BatchHandler = Callable[[Sequence[Msg]], Awaitable[None]]
 DeadLetter = Callable[[Msg, BaseException], Awaitable[None]]
@@ -129,7 +136,7 @@ class Stage:
             await self.handler(msgs)
         except asyncio.CancelledError:
             raise
-        except TransientError as exc:
+        except TRANSIENT as exc:
             self.transient_errors += 1
             log.warning("%s: dependency unavailable, batch of %d nak'ed: %s", self.name, len(msgs), exc)
             await self._nak(msgs)
@@ -161,7 +168,7 @@ class Stage:
                 await self.handler([m])
             except asyncio.CancelledError:
                 raise
-            except TransientError:
+            except TRANSIENT:
                 self.transient_errors += 1
                 await self._nak(msgs[i:])
                 return

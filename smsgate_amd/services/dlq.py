@@ -4,8 +4,10 @@ Consumes ``sms.failed`` as durable ``parser_worker_dlq`` (dlq_worker.py:84-90),
 logs every envelope pretty-printed and, with ``--reparse``, runs the message
 through the parse pipeline again.  Successes are routed like the parser worker
 (``sms.parsed`` + ``sms.processing``); a message that fails again is logged,
-counted (``reparse_failed``) and acked, never republished to ``sms.failed`` —
-this worker reads that subject, so a republish would loop forever.
+counted (``reparse_failed``, Prometheus ``sms_dlq_reparse_failed_total``) and
+moved to the terminal subject ``sms.failed.final`` (no consumer: kept for
+inspection), never republished to ``sms.failed`` — this worker reads that
+subject, so a republish would loop forever.
 
 Fixes: every message is acked (the reference never acked
 non-``raw`` payloads in reparse mode), and every envelope shape that carries
@@ -19,7 +21,8 @@ import json
 import logging
 from typing import Any, Dict, List, Optional, Sequence
 
-from ..bus.base import SUBJECT_FAILED, Bus, Msg
+from ..bus.base import SUBJECT_FAILED, SUBJECT_FAILED_FINAL, Bus, Msg
+from ..obs.metrics import DLQ_REPARSE_FAILED
 from ..models.domain import RawSMS
 from ..obs.tracing import Profiler
 from ..parse.pipeline import ParsePipeline
@@ -97,7 +100,9 @@ class DlqWorker:
                 for s, p in publishes:
                     if s == SUBJECT_FAILED:
                         self.reparse_failed += 1
-                        log.warning("DLQ reparse failed again (dropped from the DLQ loop): %s", p[:300])
+                        DLQ_REPARSE_FAILED.inc()
+                        log.warning("DLQ reparse failed again (moved to %s): %s", SUBJECT_FAILED_FINAL, p[:300])
+                        keep.append((SUBJECT_FAILED_FINAL, p))
                 if keep:
                     await self.bus.publish_many(keep)
             self.reparsed += len(to_reparse)

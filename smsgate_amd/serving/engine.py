@@ -113,6 +113,11 @@ class EngineConfig:
     # next norm GEMM (gate/up, QKV, lm_head arg-max) sums those partials instead of
     # accumulating x² with v_dot2 beside its MFMAs in every N tile (ops.gemm ss_out/ss_in)
     producer_norm: bool = True
+    # copy-constrained decoding (serving/fsm.py FieldSpec.copy): in a copy field every
+    # value token must be a body token, and after the first one a token that follows
+    # the previous one somewhere in the body; applied per row in the lm_head arg-max
+    # epilogue (ops.copy_masks -> gemm_argmax / fsm_sample / spec_verify)
+    copy_constrain: bool = True
     measure_idle: bool = True  # EngineStats.gpu_idle_s from two timing events per step
 
 
@@ -204,6 +209,7 @@ class ExtractionEngine:
         S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
         dev, bf = self.device, torch.bfloat16
         self.spec = ec.spec_k > 0 and ec.temperature <= 0
+        self.copy = ec.copy_constrain and self.fsm.has_copy
         if ec.spec_k > ops.SPEC_MAX_K:
             raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
         # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV there
@@ -248,6 +254,13 @@ class ExtractionEngine:
         self._fwd_ss: Optional[torch.Tensor] = None  # row partials of the last forward's output (_layers_fused)
         self._idle_prev: Optional[Any] = None  # event after the last launched chunk (measure_idle)
         self._idle_pairs: Deque[Tuple[Any, Any]] = deque()  # (end of chunk k-1, start of step k) to price
+        if self.spec or self.copy:
+            # prompt ids per KV slot: the draft source and the copy constraint's body
+            self.LB = ec.max_body_tokens + 2
+            self.body_buf = torch.zeros(S + 1, self.LB, **i32)
+            self.body_len = torch.zeros(S + 1, **i32)
+        if self.copy:  # per-row copy masks of the one-token paths (prefill, plain decode)
+            self.copy_rows = torch.zeros(S, self.V_dec // 32, **i32)
         if self.spec:
             self._init_spec()
         self._compute_prefix()
@@ -319,12 +332,23 @@ class ExtractionEngine:
         return self._layers_fused(x, **kw) if self.fused else self._layers(x, **kw)
 
     def _argmax(self, h: torch.Tensor, row_state: torch.Tensor, best: torch.Tensor,
-                ss: Optional[torch.Tensor] = None) -> torch.Tensor:
+                ss: Optional[torch.Tensor] = None, row_masks: Optional[torch.Tensor] = None) -> torch.Tensor:
         """lm_head + FSM-masked arg-max keys (no logits materialised).  ``ss``: the
-        forward's row partials of ``h`` (same rows), else the GEMM computes the norm."""
+        forward's row partials of ``h`` (same rows), else the GEMM computes the norm;
+        ``row_masks``: copy masks of the rows (:meth:`_copy_masks`)."""
         if self.fused:  # h is the un-normed residual stream: the final norm is the GEMM prologue
-            return ops.gemm_argmax(h, self.fw_lm, row_state, self.fsm, best, norm_eps=self.mc.eps, ss_in=ss)
-        return ops.gemm_argmax(h, self.lm_head, row_state, self.fsm, best)
+            return ops.gemm_argmax(h, self.fw_lm, row_state, self.fsm, best, norm_eps=self.mc.eps, ss_in=ss,
+                                   row_masks=row_masks)
+        return ops.gemm_argmax(h, self.lm_head, row_state, self.fsm, best, row_masks=row_masks)
+
+    def _copy_masks(self, state: torch.Tensor, prev: torch.Tensor, slot: torch.Tensor,
+                    out: torch.Tensor) -> Optional[torch.Tensor]:
+        """Copy masks of rows in ``state`` whose last token is ``prev`` on KV ``slot``
+        (None when copy-constrained decoding is off)."""
+        if not self.copy:
+            return None
+        n = state.numel()
+        return ops.copy_masks(self.fsm, state, prev, slot, self.body_buf, self.body_len, out[:n], n)
 
     def _logits(self, h: torch.Tensor) -> torch.Tensor:
         if self.fused:
@@ -388,7 +412,7 @@ class ExtractionEngine:
         flat_d = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
         x = F.embedding(flat_d, self.w.embed).contiguous()
         max_q = int(lens.max())
-        if self.spec:  # the rows' prompts are their draft source
+        if self.spec or self.copy:  # the rows' prompts: draft source and copy set
             self.body_buf[slot_d.long(), pos_d.long()] = flat_d.to(torch.int32)
             self.body_len[seq_slot_d.long()] = last_pos_d + 1
 
@@ -414,15 +438,21 @@ class ExtractionEngine:
         self.out_len.index_fill_(0, rl, 0)
         self.state.index_fill_(0, rl, self.fsm.start_state)
         self.pos.index_copy_(0, rl, last_pos_d)
+        cm = None
+        if self.copy and int(self.fsm.copy_kind[self.fsm.start_state]):
+            # a first field that copies: every body token may start it (prev is unused)
+            # (own buffer: the two halves of a split prefill run concurrently)
+            cm = self._copy_masks(self.start_states[:n], self.start_states[:n], seq_slot_d,
+                                  torch.empty(n, self.V_dec // 32, dtype=torch.int32, device=dev))
         if self.argmax:
             best = torch.empty(n, dtype=torch.int64, device=dev)
-            self._argmax(last, self.start_states[:n], best)
+            self._argmax(last, self.start_states[:n], best, row_masks=cm)
             ops.fsm_commit(best, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done, self.pos,
                            n, row_map=rows_d)
             logits = None
         else:
             ops.fsm_sample(logits, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done,
-                           self.pos, self.slot_id, self.cfg.temperature, self.cfg.seed, row_map=rows_d)
+                           self.pos, self.slot_id, self.cfg.temperature, self.cfg.seed, row_map=rows_d, row_masks=cm)
         self.stats.prefill_tokens += T
         self.stats.prefill_seqs += len(items)
         self.stats.prefill_s += time.perf_counter() - t0
@@ -455,16 +485,17 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0,
                           hook=hook)
+        cm = self._copy_masks(self.state[r0:r1], tok, slot, self.copy_rows[r0:r1]) if sample else None
         if sample and self.argmax:
             best = self.best[r0:r1]
-            self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None)
+            self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
             ops.fsm_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
                            pos, B)
             return best
         logits = self._logits(h)
         if sample:
             ops.fsm_sample(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
-                           done, pos, slot, self.cfg.temperature, self.cfg.seed)
+                           done, pos, slot, self.cfg.temperature, self.cfg.seed, row_masks=cm)
         return logits
 
     # ----------------------------------------------------------- speculative
@@ -473,9 +504,6 @@ class ExtractionEngine:
         S = ec.max_slots
         i32 = dict(dtype=torch.int32, device=dev)
         self.scratch_slot = S
-        self.LB = ec.max_body_tokens + 2
-        self.body_buf = torch.zeros(S + 1, self.LB, **i32)  # prompt ids per KV slot (the draft source)
-        self.body_len = torch.zeros(S + 1, **i32)
         # tokens that end a copied value in the body: drafted as <sep>
         strings = self.tok.token_strings
         delim = [(("," in t) or ("&#" in t) or (";" in t)) and i not in (self.tok.sep,) for i, t in enumerate(strings)]
@@ -490,6 +518,8 @@ class ExtractionEngine:
         self.x_done = torch.ones(cap, **i32)
         self.x_state = torch.full((cap,), self.fsm.done_state, **i32)
         self.x_best = torch.zeros(cap, dtype=torch.int64, device=dev)
+        if self.copy:  # one copy mask per pseudo-row
+            self.copy_x = torch.zeros(cap, self.V_dec // 32, **i32)
         self.row_start = torch.zeros(S, **i32)
         self.row_nd = torch.zeros(S, **i32)
         self.spec_acc = torch.zeros(S, **i32)
@@ -544,10 +574,12 @@ class ExtractionEngine:
                                 done=xd, impl=impl, scratch=scratch)
 
         h = self._forward(x, pos_tok=xp, slot_tok=xs, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0, hook=hook)
+        # pseudo-row i's copy mask: its state and its input token (the draft before it)
+        cm = self._copy_masks(xst, xt, xs, self.copy_x[off:off + T]) if sample else None
         if sample and self.argmax:
             # every pseudo-row masked with the state it has if its row's drafts so far are accepted
             best = self.x_best[off:off + T]
-            self._argmax(h, xst, best, ss=self._fwd_ss if self.fused else None)
+            self._argmax(h, xst, best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
             ops.spec_verify_keys(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
                                  done, pos, xt, rs, nd, acc)
             logits = best
@@ -555,7 +587,7 @@ class ExtractionEngine:
             logits = self._logits(h)
         if sample and not self.argmax:
             ops.spec_verify(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
-                            pos, xt, rs, nd, acc)
+                            pos, xt, rs, nd, acc, row_masks=cm)
         if sample:
             # tokens emitted and live rows this step (read back only by stats())
             self.spec_counts += torch.stack([acc.sum(dtype=torch.int64), (acc > 0).sum(dtype=torch.int64)])

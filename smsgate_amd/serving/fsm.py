@@ -29,7 +29,7 @@ import numpy as np
 from ..models.domain import CORE_FIELDS
 from ..parse.schema import TXN_TYPES
 
-__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm"]
+__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm", "COPY_NONE", "COPY_START", "COPY_NEXT"]
 
 
 @dataclass(frozen=True)
@@ -38,6 +38,10 @@ class FieldSpec:
     kind: str  # text | date | number | currency | card | enum
     cap: int
     choices: Tuple[str, ...] = ()
+    # copy-constrained: every value token is a token of the SMS body, and after the
+    # first one each token must follow the previous one at some body position
+    # (COPY_START / COPY_NEXT states; masks built per row by ops.copy_masks)
+    copy: bool = False
 
 
 # Token caps per field.  Measured on 20 k synthetic SMS of each vocabulary with the
@@ -47,18 +51,26 @@ class FieldSpec:
 # are about 2x those maxima: a cap only bounds the KV length reserved per slot
 # (rows stop at <sep>, so decode cost does not depend on it), and a value longer
 # than its cap would be silently cut.
+#
+# Every non-enum value is copied from the body (the reference's golden answers are
+# substrings of their SMS, tests/test_parsers.py:11-58; all synthetic gold values are
+# token-aligned body spans, tests/test_copy_fsm.py), so every non-enum field is
+# copy-constrained: the model can pick the span, never invent a name.
 DEFAULT_FIELDS: Tuple[FieldSpec, ...] = (
     FieldSpec("txn_type", "enum", 8, TXN_TYPES),  # cap = bound on the enum trie depth
-    FieldSpec("date", "date", 16),
-    FieldSpec("amount", "number", 10),
-    FieldSpec("currency", "currency", 4),
-    FieldSpec("card", "card", 6),
-    FieldSpec("merchant", "text", 32),
-    FieldSpec("city", "text", 12),
-    FieldSpec("address", "text", 24),
-    FieldSpec("balance", "number", 10),
+    FieldSpec("date", "date", 16, copy=True),
+    FieldSpec("amount", "number", 10, copy=True),
+    FieldSpec("currency", "currency", 4, copy=True),
+    FieldSpec("card", "card", 6, copy=True),
+    FieldSpec("merchant", "text", 32, copy=True),
+    FieldSpec("city", "text", 12, copy=True),
+    FieldSpec("address", "text", 24, copy=True),
+    FieldSpec("balance", "number", 10, copy=True),
 )
 assert tuple(f.name for f in DEFAULT_FIELDS) == CORE_FIELDS
+
+# per-state copy kind (SchemaFSM.copy_kind)
+COPY_NONE, COPY_START, COPY_NEXT = 0, 1, 2
 
 _CLASS_CHARS = {
     "date": set("0123456789.:/- "),
@@ -98,6 +110,7 @@ class SchemaFSM:
     done_state: int
     start_state: int = 0
     field_of_state: List[int] = field(default_factory=list)
+    copy_kind: Optional[np.ndarray] = None  # [S] COPY_NONE / COPY_START / COPY_NEXT
     # device copies (filled by to_device; consumed by ops.fsm_sample)
     masks: object = None
     state_mask: object = None
@@ -106,6 +119,11 @@ class SchemaFSM:
     enum_tok_t: object = None
     enum_next_t: object = None
     forced_t: object = None
+    copy_kind_t: object = None
+
+    @property
+    def has_copy(self) -> bool:
+        return self.copy_kind is not None and bool((self.copy_kind != COPY_NONE).any())
 
     @property
     def forced(self) -> np.ndarray:
@@ -144,7 +162,26 @@ class SchemaFSM:
         self.enum_tok_t = torch.from_numpy(self.enum_tok.astype(np.int32)).to(device)
         self.enum_next_t = torch.from_numpy(self.enum_next.astype(np.int32)).to(device)
         self.forced_t = torch.from_numpy(self.forced).to(device)
+        ck = self.copy_kind if self.copy_kind is not None else np.zeros(self.num_states, dtype=np.int32)
+        self.copy_kind_t = torch.from_numpy(ck.astype(np.int32)).to(device)
         return self
+
+    def copy_mask_host(self, state: int, prev: int, body: Sequence[int]) -> np.ndarray:
+        """Reference of ops.copy_masks for one row (tests): [vocab] bool allowed tokens
+        of ``state`` after ``prev`` for a row whose prompt ids are ``body``."""
+        allow = self.allowed[state].copy()
+        kind = COPY_NONE if self.copy_kind is None else int(self.copy_kind[state])
+        if kind == COPY_NONE:
+            return allow
+        cand = np.zeros(self.vocab, dtype=bool)
+        if kind == COPY_START:
+            cand[[t for t in body if 0 <= t < self.vocab]] = True
+        else:
+            for j in range(len(body) - 1):
+                if body[j] == prev and 0 <= body[j + 1] < self.vocab:
+                    cand[body[j + 1]] = True
+        cand[self.sep_token] = True
+        return allow & cand
 
     def step_host(self, state: int, tok: int) -> int:
         """Reference transition (host side, for tests)."""
@@ -182,13 +219,15 @@ def build_fsm(tokenizer, vocab: int, fields: Sequence[FieldSpec] = DEFAULT_FIELD
     next_tok: List[int] = []
     enum_lists: List[List[Tuple[int, int]]] = []
     field_of: List[int] = []
+    copy_kind: List[int] = []
 
-    def new_state(allowed: np.ndarray, fidx: int) -> int:
+    def new_state(allowed: np.ndarray, fidx: int, ck: int = COPY_NONE) -> int:
         states_allowed.append(allowed)
         next_sep.append(-1)
         next_tok.append(-1)
         enum_lists.append([])
         field_of.append(fidx)
+        copy_kind.append(ck)
         return len(states_allowed) - 1
 
     def pad(mask: np.ndarray) -> np.ndarray:
@@ -230,7 +269,8 @@ def build_fsm(tokenizer, vocab: int, fields: Sequence[FieldSpec] = DEFAULT_FIELD
             cls = pad(classes[f.kind])
             allow = cls.copy()
             allow[sep] = True
-            st = [new_state(allow.copy(), fi) for _ in range(f.cap)]
+            st = [new_state(allow.copy(), fi, (COPY_START if k == 0 else COPY_NEXT) if f.copy else COPY_NONE)
+                  for k in range(f.cap)]
             last = new_state(only_sep.copy(), fi)
             chain = st + [last]
             for a, b in zip(chain[:-1], chain[1:]):
@@ -264,4 +304,5 @@ def build_fsm(tokenizer, vocab: int, fields: Sequence[FieldSpec] = DEFAULT_FIELD
         done_state=done,
         start_state=field_starts[0],
         field_of_state=field_of,
+        copy_kind=np.asarray(copy_kind, dtype=np.int32),
     )

@@ -184,7 +184,8 @@ class RemoteEngineClient:
     """
 
     def __init__(self, conn: Optional[Connection] = None, tokenizer=None, max_body_tokens: int = 128,
-                 connector: Optional[Callable[[], Connection]] = None) -> None:
+                 connector: Optional[Callable[[], Connection]] = None,
+                 request_timeout: Optional[float] = 120.0) -> None:
         from ..models.tokenizer import load_tokenizer
         from .fsm import DEFAULT_FIELDS
 
@@ -195,7 +196,12 @@ class RemoteEngineClient:
         self.fields = [f.name for f in DEFAULT_FIELDS]
         self.max_body = max_body_tokens
         self._ids = itertools.count(1)
+        # rid -> (future, loop, connection it was sent on): a dying connection's reader
+        # fails exactly its own requests (a request already sent on the next connection
+        # is never swept by the old reader)
         self._pending: Dict[int, Any] = {}
+        self._plock = threading.Lock()
+        self.request_timeout = request_timeout
         self._send_lock = threading.Lock()
         self._conn_lock = threading.Lock()
         self.control: "queue.Queue[Any]" = queue.Queue()
@@ -234,26 +240,32 @@ class RemoteEngineClient:
             try:
                 buf = conn.recv_bytes()
             except (EOFError, OSError):
+                # detach first, then sweep: a request registered after the sweep sees
+                # self.conn is not its connection and fails itself (extract)
                 with self._conn_lock:
                     if self.conn is conn:
                         self.conn = None
-                for fut, loop in list(self._pending.values()):
+                with self._plock:
+                    mine = [rid for rid, e in self._pending.items() if e[2] is conn]
+                    ents = [self._pending.pop(rid) for rid in mine]
+                for fut, loop, _ in ents:
                     loop.call_soon_threadsafe(self._set_exc, fut, self._unavailable("engine server closed"))
-                self._pending.clear()
                 self.control.put(None)
                 return
             k = P.kind(buf)
             if k == b"R":
                 _, rid, seqs = P.unpack_ids(buf)
-                ent = self._pending.pop(rid, None)
+                with self._plock:
+                    ent = self._pending.pop(rid, None)
                 if ent is not None:
-                    fut, loop = ent
+                    fut, loop, _ = ent
                     loop.call_soon_threadsafe(self._set_res, fut, seqs)
             elif k == b"E":
                 rid, msg = P.unpack_error(buf)
-                ent = self._pending.pop(rid, None)
+                with self._plock:
+                    ent = self._pending.pop(rid, None)
                 if ent is not None:
-                    fut, loop = ent
+                    fut, loop, _ = ent
                     loop.call_soon_threadsafe(self._set_exc, fut, RuntimeError(msg))
             elif k == b"C":
                 self.control.put(P.unpack_control(buf))
@@ -293,20 +305,33 @@ class RemoteEngineClient:
 
     async def extract(self, bodies: Sequence[str]) -> List[Dict[str, str]]:
         ids = self.tok.message_ids(list(bodies), self.max_body)
+        conn = self._connection()  # may raise BackendUnavailable: nothing registered yet
         rid = next(self._ids)
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
-        self._pending[rid] = (fut, loop)
+        with self._plock:
+            self._pending[rid] = (fut, loop, conn)
         msg = P.pack_ids(b"Q", rid, ids)
-        conn = self._connection()
+        sent = False
         try:
+            if self.conn is not conn:  # its reader already swept: it will never answer
+                raise self._unavailable("engine server closed")
             with self._send_lock:
                 conn.send_bytes(msg)
+            sent = True
         except OSError as exc:  # broken pipe: the server went away under us
-            self._pending.pop(rid, None)
             with self._conn_lock:
                 if self.conn is conn:
                     self.conn = None
             raise self._unavailable(f"engine server send failed: {exc}") from exc
-        seqs = await fut
+        finally:
+            if not sent:
+                with self._plock:
+                    self._pending.pop(rid, None)
+        try:
+            seqs = await (asyncio.wait_for(fut, self.request_timeout) if self.request_timeout else fut)
+        except asyncio.TimeoutError:
+            with self._plock:
+                self._pending.pop(rid, None)
+            raise self._unavailable(f"engine server did not answer within {self.request_timeout:.0f} s") from None
         return self.decode_answers(seqs)

@@ -90,3 +90,41 @@ def test_duplicate_msg_ids_at_f1a93_keep_newest(tmp_path):
     with eng.begin() as c:
         rows = c.execute(text("SELECT msg_id, original_body FROM sms_data ORDER BY id")).all()
     assert rows == [("m", "b1"), ("k2", "b2")]  # newest duplicate kept; a NULL msg_id falls back to original_key
+
+
+def test_new_rows_after_upgrade_get_fresh_ids(tmp_path):
+    """The writer never passes ``id``: after the carry-over a new SMS must get an id
+    past the carried ones (a stale Postgres sequence rejected every new row)."""
+    from smsgate_amd.sinks.sql import SqlSink  # noqa: F401  (the writer's upsert path)
+
+    eng, _ = _make_db(tmp_path, "f1ebe9c5dea6")
+    migrations.upgrade(eng)
+    with eng.begin() as c:
+        c.execute(text("INSERT INTO sms_data (msg_id, sender, datetime, card, amount, currency, txn_type) "
+                       "VALUES ('fresh', 'B', '2025-01-01', '1', 1, 'USD', 'debit')"))
+        ids = dict(c.execute(text("SELECT msg_id, id FROM sms_data")).all())
+        # the table was recreated under its own name (no renamed copy's constraint names)
+        ddl = c.execute(text("SELECT sql FROM sqlite_master WHERE name = 'sms_data'")).scalar()
+    assert ids["fresh"] == 4 and sorted(ids.values()) == [1, 2, 3, 4]
+    assert "__new" not in ddl and "__carry" not in ddl
+
+
+def test_postgres_sequence_reset_after_carry():
+    """On Postgres the id sequence is moved past MAX(id) inside the upgrade."""
+    seen = []
+
+    class _Dialect:
+        name = "postgresql"
+
+    class _Conn:
+        dialect = _Dialect()
+
+        def execute(self, stmt, *a):
+            seen.append(str(stmt))
+
+    migrations._reset_id_sequence(_Conn())
+    assert len(seen) == 1 and "setval(pg_get_serial_sequence('sms_data', 'id')" in seen[0]
+    assert "MAX(id)" in seen[0]
+    _Dialect.name = "sqlite"
+    migrations._reset_id_sequence(_Conn())
+    assert len(seen) == 1  # nothing to do on SQLite

@@ -20,6 +20,7 @@ from fastapi.testclient import TestClient
 from conftest import REFERENCE_CASES, drain
 from fakes import FakePocketBase, FakeTelegram
 from smsgate_amd.bus import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_RAW, MemoryBus
+from smsgate_amd.bus.base import SUBJECT_FAILED_FINAL
 from smsgate_amd.models import ParsedSMS, RawSMS, get_sha1_hash
 from smsgate_amd.parse import ParsePipeline
 from smsgate_amd.parse.backends import RegexBackend
@@ -117,12 +118,18 @@ def test_dlq_reparse_failure_is_terminal(arun):
         w = DlqWorker(bus, ParsePipeline(AlwaysFails()), reparse=True)
         await w.stage.run_until_idle(idle_s=0.3)
         info = await bus.consumer_info("SMS", "parser_worker_dlq")
-        return w, info, await drain(bus, SUBJECT_PARSED)
+        return w, info, await drain(bus, SUBJECT_PARSED), await drain(bus, SUBJECT_FAILED_FINAL)
 
-    w, info, parsed = arun(go())
+    from prometheus_client import REGISTRY
+
+    m0 = REGISTRY.get_sample_value("sms_dlq_reparse_failed_total") or 0.0
+    w, info, parsed, final = arun(go())
     assert w.seen == 2 and w.reparsed == 2 and w.reparse_failed == 2
     assert len(calls) == 2 and len(set(calls)) == 2  # each body reached the backend exactly once
     assert info.num_pending == 0 and info.num_ack_pending == 0 and parsed == []
+    # the twice-failed messages stay inspectable on the terminal subject, and are counted
+    assert len(final) == 2 and all("raw" in f or "entry" in f for f in final)
+    assert (REGISTRY.get_sample_value("sms_dlq_reparse_failed_total") or 0.0) - m0 == 2
 
 
 def test_dlq_reparse_profiler_dumps_pstats(arun, tmp_path):

@@ -3,6 +3,8 @@ dependency failures nak the whole batch, and the parser worker never turns an
 engine outage into DLQ traffic (stage.py:105, cli.py:65)."""
 from __future__ import annotations
 
+import pytest
+
 from conftest import REFERENCE_CASES, drain
 from smsgate_amd.bus import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_RAW, MemoryBus
 from smsgate_amd.runtime.errors import TransientError
@@ -226,3 +228,59 @@ def test_long_body_truncation_is_counted():
     assert len(ids[0]) == 130 and ids[0][0] == tk.sms and ids[0][-1] == tk.ans
     assert tk.truncated - t0 == 1
     assert (REGISTRY.get_sample_value("llm_prompt_truncated_total") or 0.0) - c0 == 1
+
+
+def test_remote_client_dead_reader_sweeps_only_its_own_requests(arun):
+    """when connection 1 dies, its reader fails the requests sent on it --
+    and nothing registered for the next connection (which used to be wiped by
+    ``_pending.clear()`` and then waited forever)."""
+    import asyncio
+    from multiprocessing import Pipe
+
+    from smsgate_amd.parse.backends.base import BackendUnavailable
+    from smsgate_amd.serving.remote import RemoteEngineClient
+
+    (c1, s1), (c2, s2) = Pipe(), Pipe()
+    conns = iter([c1, c2])
+    client = RemoteEngineClient(connector=lambda: next(conns), request_timeout=10)
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        t1 = asyncio.create_task(client.extract(["APPROVED PURCHASE: A, B"]))
+        await asyncio.sleep(0.05)
+        assert len(client._pending) == 1
+        other = loop.create_future()
+        client._pending[10_000] = (other, loop, c2)  # in flight on the next connection
+        s1.close()  # server 1 goes away
+        with pytest.raises(BackendUnavailable):
+            await t1
+        await asyncio.sleep(0.05)
+        assert 10_000 in client._pending and not other.done()
+        client._pending.pop(10_000)
+        # the next request reconnects (connection 2) and is answered normally
+        t2 = asyncio.create_task(client.extract(["x"]))
+        await asyncio.sleep(0.05)
+        from smsgate_amd.serving import protocol as P
+
+        _, rid, seqs = P.unpack_id_arrays(s2.recv_bytes())
+        s2.send_bytes(P.pack_ids(b"R", rid, [[client.tok.sep] * 9]))
+        return await t2
+
+    ans = arun(go())
+    assert client.reconnects == 1 and ans[0]["merchant"] == "" and not client._pending
+
+
+def test_remote_client_request_timeout_is_transient(arun):
+    """An engine that never answers fails the request as BackendUnavailable (the
+    stage naks and retries) instead of stalling a worker slot forever."""
+    from multiprocessing import Pipe
+
+    from smsgate_amd.parse.backends.base import BackendUnavailable
+    from smsgate_amd.serving.remote import RemoteEngineClient
+
+    c, s = Pipe()
+    client = RemoteEngineClient(c, request_timeout=0.2)
+    with pytest.raises(BackendUnavailable):
+        arun(client.extract(["x"]))
+    assert not client._pending
+    s.close()

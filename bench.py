@@ -66,17 +66,29 @@ def _args(argv=None):
                    help="where local rank 0 publishes the trained weights; reused by later identical runs")
     p.add_argument("--eval-n", type=int, default=500, help="held-out SMS scored before the timed region (0 = skip)")
     p.add_argument("--traffic-vocab", default="heldout", choices=["heldout", "train"])
+    p.add_argument("--traffic", default="purchase", choices=["purchase", "mixed"],
+                   help="purchase: debit transactions only, every message LLM-routed (the BASELINE harness's "
+                        "traffic); mixed: all kinds, ~17%% skipped by the keyword filter before the LLM")
+    # the timed throughput is only reported for an extractor that extracts: below this
+    # held-out exact-answer rate the run fails before the timed region (0 = no floor)
+    p.add_argument("--quality-floor", type=float, default=0.95)
     p.add_argument("--msgs-per-step", type=int, default=16384)
-    p.add_argument("--max-slots", type=int, default=8192)
-    p.add_argument("--steps-per-graph", type=int, default=2)
+    p.add_argument("--profile", default="throughput", choices=["throughput", "latency"],
+                   help="engine configuration (serving/profiles.py; engine-server --profile serves the same)")
+    # the engine knobs below default to the profile's values (None = the profile's)
+    p.add_argument("--max-slots", type=int, default=None)
+    p.add_argument("--steps-per-graph", type=int, default=None)
     # admit when this fraction of rows is free: 0.25 / 0.125 / 0.0625 -> 28 258 / 28 466 (one box),
     # 27 728 / 27 910 for 0.125 / 0.0625 (another): within noise, 0.125 kept
     # (profiles/r02s3_admit_frac_ab*.jsonl)
-    p.add_argument("--admit-frac", type=float, default=0.125)
+    p.add_argument("--admit-frac", type=float, default=None)
     p.add_argument("--bucket-step", type=int, default=0, help="0 = powers of two; N = multiples of N")
     p.add_argument("--cpu-workers", type=int, default=8)
-    p.add_argument("--bus-shards", type=int, default=3,
-                   help="brokers per node, sharded by subject (sms.raw | sms.parsed | sms.processing + the rest)")
+    p.add_argument("--bus-shards", type=int, default=0,
+                   help="N > 0: N brokers per node, positional subject sharding (sms.raw | sms.parsed | "
+                        "sms.processing + the rest); 0 = the node layout (bus/sharded.py NODE_PARTITIONS: sms.raw and "
+                        "sms.parsed each partitioned over --partitions brokers, one more for the rest)")
+    p.add_argument("--partitions", type=int, default=2, help="brokers per partitioned subject (node layout)")
     p.add_argument("--bus", default="busd", choices=["memory", "busd"],
                    help="busd: ONE shared native broker per node (journal on) carries sms.raw / sms.parsed for every "
                         "GPU's parser and writer processes (one competing group each); memory: an in-process bus per "
@@ -87,7 +99,7 @@ def _args(argv=None):
                    help="tokenizer (Rayon) threads per parser process; 0 = library default (one per CPU)")
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
     p.add_argument("--no-compact", action="store_true", help="disable decode row compaction")
-    p.add_argument("--split-decode", type=int, default=4096,
+    p.add_argument("--split-decode", type=int, default=None,
                    help="decode buckets >= N run as two half-batches on two streams (0 = off)")
     p.add_argument("--no-split-offset", action="store_true", help="start both halves together")
     p.add_argument("--split-parts", type=int, default=2, help="parts of a split decode bucket")
@@ -98,7 +110,7 @@ def _args(argv=None):
     p.add_argument("--admit-min-batch", type=int, default=None, help="EngineConfig.admit_min_batch (default: engine's)")
     p.add_argument("--prefill-key-split", type=int, default=1, choices=[1, 2],
                    help="waves sharing each prefill attention tile's keys")
-    p.add_argument("--split-prefill", type=int, default=8192,
+    p.add_argument("--split-prefill", type=int, default=None,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--spec-policy", type=int, default=0, help="draft policy (EngineConfig.spec_policy)")
     p.add_argument("--swiglu-cfg", type=int, default=None,
@@ -109,8 +121,9 @@ def _args(argv=None):
                    help="ignore the measured GEMM tile exceptions (ops.GEMM_MEASURED), A/B only")
     # up to 6 drafts per row under the same pseudo-row budget: 2.56 vs 2.52 tokens per row-step,
     # 28 610 vs 28 349 msgs/s (profiles/r02s3_spec_k_ab.jsonl)
-    p.add_argument("--spec-k", type=int, default=6, help="speculative decoding: drafts per row per step (0 = off)")
-    p.add_argument("--spec-frac", type=float, default=1.25, help="draft budget per step, x decode rows")
+    p.add_argument("--spec-k", type=int, default=None, help="speculative decoding: drafts per row per step (0 = off)")
+    p.add_argument("--spec-frac", type=float, default=None, help="draft budget per step, x decode rows")
+    p.add_argument("--no-copy", action="store_true", help="A/B: schema-only decoding (no body-copy constraint)")
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
     p.add_argument("--cpu-echo-engine", action="store_true",
                    help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")
@@ -134,7 +147,8 @@ def run_replica(args, rank: int, world: int, local: int):
     # 0) the node's shared broker, started before anything touches the GPU (no exec after GPU init)
     broker, bus_dsn = start_node_broker(args, local) if args.bus == "busd" else (None, None)
     cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
-           "worker_threads": args.worker_threads, "vocab": args.traffic_vocab, "bus": bus_dsn}
+           "worker_threads": args.worker_threads, "vocab": args.traffic_vocab, "bus": bus_dsn,
+           "traffic": args.traffic}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
 
@@ -165,19 +179,14 @@ def run_replica(args, rank: int, world: int, local: int):
     else:
         from smsgate_amd.parse.backends.local_llm import build_engine
 
-        buckets = (tuple(range(args.bucket_step, args.max_slots + 1, args.bucket_step)) if args.bucket_step
-                   else (64, 128, 256, 512, 1024, 2048, 4096, 8192))
+        ekw = engine_kwargs(args)
         engine = build_engine(args.model, device=f"cuda:{local}", random_init=weights is None, weights=weights,
-                              max_slots=args.max_slots,
-                              steps_per_graph=args.steps_per_graph, admit_min_fraction=args.admit_frac,
-                              buckets=buckets, fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
-                              split_decode=args.split_decode, split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
-                              split_parts=args.split_parts,
-                              split_prefill=args.split_prefill, decode_attn=args.decode_attn,
-                              prefill_key_split=args.prefill_key_split,
-                              spec_k=args.spec_k, spec_policy=args.spec_policy, spec_draft_frac=args.spec_frac,
-                              spec_max_rows=args.spec_max_rows,
-                              producer_norm=not args.no_producer_norm,
+                              fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
+                              split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
+                              split_parts=args.split_parts, decode_attn=args.decode_attn,
+                              prefill_key_split=args.prefill_key_split, spec_policy=args.spec_policy,
+                              spec_max_rows=args.spec_max_rows, producer_norm=not args.no_producer_norm,
+                              **ekw,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
     if not echo and args.eval_n and rank == 0:
@@ -185,7 +194,12 @@ def run_replica(args, rank: int, world: int, local: int):
 
         q = evaluate_engine(engine, n=args.eval_n, seed=4242, vocab_name="heldout")
         quality = {"parse_rate": round(q["parse_rate"], 4), "exact": round(q["exact"], 4), "n": q["n"],
-                   "field_acc": {k: round(v, 4) for k, v in q["field_acc"].items()}, "vocab": "heldout"}
+                   "field_acc": {k: round(v, 4) for k, v in q["field_acc"].items()}, "vocab": "heldout",
+                   "floor": args.quality_floor}
+        print(f"[bench] held-out quality: {json.dumps(quality)}", file=sys.stderr, flush=True)
+        if args.weights != "random" and q["exact"] < args.quality_floor:
+            raise SystemExit(f"bench: held-out exact-answer rate {q['exact']:.4f} is below the quality floor "
+                             f"{args.quality_floor} -- no throughput is reported for a broken extractor")
         (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
     if not args.no_gc_freeze:
         from smsgate_amd.serving import freeze_gc_for_launch_loop
@@ -237,17 +251,38 @@ def run_replica(args, rank: int, world: int, local: int):
     return dt, counts, init_s, estats, prov, quality
 
 
+def engine_kwargs(args) -> dict:
+    """EngineConfig of this run: the ``--profile`` (serving/profiles.py, the same
+    defaults ``engine-server --profile`` serves) with the explicit flags applied."""
+    from smsgate_amd.serving.profiles import profile_kwargs
+
+    kw = profile_kwargs(args.profile, max_slots=args.max_slots, steps_per_graph=args.steps_per_graph,
+                        admit_min_fraction=args.admit_frac, spec_k=args.spec_k, spec_draft_frac=args.spec_frac,
+                        split_decode=args.split_decode, split_prefill=args.split_prefill,
+                        copy_constrain=False if args.no_copy else None)
+    if args.bucket_step:
+        kw["buckets"] = tuple(range(args.bucket_step, kw["max_slots"] + 1, args.bucket_step))
+    return kw
+
+
 def start_node_broker(args, local: int):
     """Local rank 0 starts ``--bus-shards`` ``smsgate-busd`` brokers (journal in a temp
     dir, fsync interval), sharded by subject; the other ranks of the node wait for
     their sockets.  Returns (list of brokers | None, dsn)."""
     import tempfile
 
+    from smsgate_amd.bus.sharded import NODE_PARTITIONS, node_layout
+
     tag = os.environ.get("MASTER_PORT") or str(os.getpid())
     root = os.path.join(tempfile.gettempdir(), f"smsgate-bench-bus-{tag}")
-    n = max(1, args.bus_shards)
+    parts = {s: max(1, args.partitions) for s in NODE_PARTITIONS}
+    n = args.bus_shards if args.bus_shards > 0 else sum(parts.values()) + 1
     socks = [os.path.join(root, f"bus{k}.sock") for k in range(n)]
-    dsn = ("sharded+" if n > 1 else "") + ",".join(f"unix://{p}" for p in socks)
+    members = [f"unix://{p}" for p in socks]
+    if args.bus_shards > 0:
+        dsn = ("sharded+" if n > 1 else "") + ",".join(members)
+    else:
+        dsn = node_layout(members, parts)
     if local == 0:
         from smsgate_amd.native import spawn_busd
 
@@ -332,7 +367,7 @@ async def _run_cpu(args):
     worker = ParserWorker(bus, ParsePipeline(backend), batch=args.batch, concurrency=args.concurrency,
                           stats_interval=0)
     await worker.start()
-    sets = [_payload_bytes(args.msgs_per_step, 1_000_003 + s) for s in range(args.warmup + args.steps)]
+    sets = [_payload_bytes(args.msgs_per_step, 1_000_003 + s, traffic=args.traffic) for s in range(args.warmup + args.steps)]
 
     async def run(first, n):
         base = worker.stage.processed
@@ -383,6 +418,7 @@ def main(argv=None) -> int:
         if k in counts:
             routing[k] = counts[k]
     llm_routed = routing["parsed"] + routing["broken"] + routing["dlq"]
+    llm_value = llm_routed / dt  # messages that went through the LLM (keyword-skipped ones excluded)
     if rank == 0:
         gpu = args.backend == "local_llm"
         out = {
@@ -398,23 +434,29 @@ def main(argv=None) -> int:
             "vs_baseline": round(value / BASELINE_MSGS_PER_S, 3),
             "dtype": "bf16",
             "data": ("synthetic; CPU echo engine - harness check only, not a benchmark" if args.cpu_echo_engine
-                     else f"synthetic unique bank-SMS bodies ({args.traffic_vocab} vocabulary"
+                     else f"synthetic unique bank-SMS bodies, {args.traffic} traffic ({args.traffic_vocab} vocabulary"
                           + (": merchant/city/street names never seen in training)" if args.traffic_vocab == "heldout"
                              else ")")),
+            "llm_msgs_per_sec": round(llm_value, 1),
+            "traffic": args.traffic,
             "config": {
                 "model": (f"{args.model} extractor LLM (134.5M params, replaces the Gemini call)" if gpu
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
                 "pipeline": ("payload->RawSMS->bus sms.raw->parser_worker->sms.parsed+sms.processing|DLQ->ack"
                              + ("->pb_writer->in-memory sink" if gpu else "")),
-                "bus": (f"shared smsgate-busd brokers per node ({max(1, args.bus_shards)}, sharded by subject; "
-                        "journal on), one competing parser group and one writer group across all GPUs"
+                "bus": (("shared smsgate-busd brokers per node (" +
+                         (f"{args.bus_shards}, sharded by subject" if args.bus_shards > 0 else
+                          f"{2 * max(1, args.partitions) + 1}: sms.raw and sms.parsed each partitioned over "
+                          f"{max(1, args.partitions)}, one for the rest") +
+                         "; journal on), one competing parser group and one writer group across all GPUs")
                         if args.bus == "busd" else "in-process bus per parser process"),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
                 "seq_len": "shared prefix 20 + ~48 prompt + <=131 schema-constrained output tokens (~38 trained)",
                 "parallelism": f"dp{world}" if gpu else "cpu",
                 "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
-                "max_slots": args.max_slots,
+                "engine_profile": args.profile,
+                "max_slots": engine_kwargs(args)["max_slots"],
                 "baseline_msgs_per_s": BASELINE_MSGS_PER_S,
             },
             "routing": routing,

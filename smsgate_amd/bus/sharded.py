@@ -1,23 +1,35 @@
 """Subject-sharded bus: several brokers act as one bus, each owning some subjects.
 
 The reference runs ONE NATS server for everything (docker-compose.yml:15-27).
-One ``smsgate-busd`` event loop carries ≈350 k publish→fetch→ack messages/s with
-its journal on (profiles/r02_busd_capacity.jsonl), while a node of 8 GPUs needs
-about 3 publishes and 2 deliveries per SMS at ~20 k SMS/s per GPU.  Sharding by
-subject keeps every subject's semantics intact (one stream per broker, one
-competing consumer group per durable, a durable lives where its subject lives)
-and splits the broker work: ``sms.raw`` (ingest → parser) on shard 0; with two
-shards the parser's outputs (``sms.parsed`` / ``sms.processing`` / ``sms.failed``
-/ ``sms.categorized``) on shard 1; with three (the 8-GPU deployment) one message
-per SMS lands on each shard: sms.parsed alone on 1, sms.processing (and the
-low-rate subjects) on 2.
+One ``smsgate-busd`` event loop carries ≈250 k publish→fetch→ack messages/s with
+its journal on (tests/test_broker_capacity.py), while a node of 8 GPUs needs
+about one message per SMS on each of three subjects at ~25 k SMS/s per GPU.
+Sharding by subject keeps every subject's semantics intact (one stream per
+broker, one competing consumer group per durable, a durable lives where its
+subject lives) and splits the broker work.
 
-DSN: ``sharded+unix:///run/raw.sock,unix:///run/out.sock`` (any member DSNs
-:func:`smsgate_amd.bus.connect` accepts, comma separated).
+Two layouts, chosen by the DSN:
+
+* **positional** (``sharded+A,B,C``): ``sms.raw`` on shard 0; with two shards
+  the parser's outputs (``sms.parsed`` / ``sms.processing`` / ``sms.failed`` /
+  ``sms.categorized``) on shard 1; with three (the 8-GPU deployment) one message
+  per SMS lands on each shard: sms.parsed alone on 1, sms.processing (and the
+  low-rate subjects) on 2 (:func:`shard_of`);
+* **pinned** (``sharded+sms.raw=A,sms.raw=B,sms.parsed=C,*=D``): a member
+  prefixed ``<subject>=`` serves that subject, and a subject pinned to several
+  members is **partitioned** over them: publishes are dealt round-robin, a
+  durable exists on every partition (one competing group per partition, the
+  same name), and a subscription fetches from the partitions in rotation, so
+  a subject's rate is no longer bounded by one broker's event loop.  Unpinned
+  subjects go to the ``*=`` (or unprefixed) members, spread by subject hash.
+
+``consumer_info`` of a partitioned durable sums its partitions.
 """
 from __future__ import annotations
 
 import asyncio
+import itertools
+import time
 import zlib
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -28,18 +40,42 @@ from .base import (
     Bus,
     BusError,
     ConsumerInfo,
+    Msg,
     PubAck,
     StreamConfig,
     StreamInfo,
     Subscription,
 )
 
-__all__ = ["ShardedBus", "shard_of"]
+__all__ = ["ShardedBus", "shard_of", "parse_members", "Router", "NODE_PARTITIONS", "node_layout"]
+
+# The 8-GPU node's broker layout (deploy/docker-compose.yml, bench.py): the two
+# consumed per-SMS subjects each partitioned over two brokers, everything else
+# (sms.processing -- published, consumed outside the pipeline -- and the low-rate
+# subjects) on one more; tests/test_broker_capacity.py sizes each broker against
+# the latest measured headline.
+NODE_PARTITIONS = {SUBJECT_RAW: 2, SUBJECT_PARSED: 2}
+
+
+def node_layout(dsns: Sequence[str], partitions: Optional[Dict[str, int]] = None) -> str:
+    """Pinned ``sharded+`` DSN over ``dsns``: the first ``partitions[s]`` members per
+    subject (in dict order), the remaining member(s) as the default."""
+    parts = NODE_PARTITIONS if partitions is None else partitions
+    need = sum(parts.values()) + 1
+    if len(dsns) < need:
+        raise BusError(f"layout {parts} needs {need} brokers, got {len(dsns)}")
+    out, k = [], 0
+    for subject, n in parts.items():
+        for _ in range(n):
+            out.append(f"{subject}={dsns[k]}")
+            k += 1
+    out += [f"*={d}" for d in dsns[k:]]
+    return "sharded+" + ",".join(out)
 
 
 def shard_of(subject: str, n: int) -> int:
-    """Shard owning ``subject``: ingest (sms.raw) on 0; with 3+ shards sms.parsed
-    alone on 1, sms.processing on 2 and the rest spread over 2 .. n-1."""
+    """Positional layout: shard owning ``subject``: ingest (sms.raw) on 0; with 3+
+    shards sms.parsed alone on 1, sms.processing on 2 and the rest spread over 2 .. n-1."""
     if n <= 1 or subject == SUBJECT_RAW:
         return 0
     if n == 2 or subject == SUBJECT_PARSED:
@@ -49,21 +85,121 @@ def shard_of(subject: str, n: int) -> int:
     return 2 + zlib.crc32(subject.encode()) % (n - 2)
 
 
+def parse_members(spec: str) -> Tuple[List[str], Dict[str, List[int]], List[int]]:
+    """``"sms.raw=unix:///a,*=unix:///b"`` -> (member dsns, {subject: member indices},
+    default member indices).  No ``=`` prefix anywhere -> positional layout ({} pins)."""
+    dsns: List[str] = []
+    pins: Dict[str, List[int]] = {}
+    default: List[int] = []
+    parts = [p for p in spec.split(",") if p]
+    pinned = any("=" in p.split("://", 1)[0] for p in parts)
+    for p in parts:
+        head = p.split("://", 1)[0]
+        if pinned and "=" in head:
+            subj, dsn = p.split("=", 1)
+        else:
+            subj, dsn = "*", p
+        idx = len(dsns)
+        dsns.append(dsn)
+        if subj == "*":
+            default.append(idx)
+        else:
+            pins.setdefault(subj, []).append(idx)
+    if pinned and not default:
+        raise BusError(f"sharded DSN {spec!r}: pinned layout needs a '*=' member for the other subjects")
+    return dsns, pins, default
+
+
+class Router:
+    """Subject -> member indices (one member, or the partitions of a pinned subject)."""
+
+    def __init__(self, n: int, pins: Optional[Dict[str, List[int]]] = None,
+                 default: Optional[List[int]] = None) -> None:
+        self.n = n
+        self.pins = dict(pins or {})
+        self.default = list(default or range(n))
+        self._rr = itertools.count()
+
+    def members(self, subject: str) -> List[int]:
+        if not self.pins:
+            return [shard_of(subject, self.n)]
+        if subject in self.pins:
+            return self.pins[subject]
+        return [self.default[zlib.crc32(subject.encode()) % len(self.default)]]
+
+    def publish_target(self, subject: str) -> int:
+        ms = self.members(subject)
+        return ms[0] if len(ms) == 1 else ms[next(self._rr) % len(ms)]
+
+
+class _PartitionedSub(Subscription):
+    """One durable on every partition of a subject; fetches rotate over them (a
+    non-blocking sweep first, then short long-polls partition by partition, so no
+    fetch is ever left outstanding on a partition whose answer would be lost)."""
+
+    POLL_SLICE = 0.02
+
+    def __init__(self, subs: Sequence[Subscription]) -> None:
+        self.subs = list(subs)
+        self.consumer = subs[0].consumer
+        self.stream = getattr(subs[0], "stream", None) or "SMS"
+        self._rr = 0
+
+    async def fetch(self, batch: int = 1, timeout: Optional[float] = None) -> List[Msg]:
+        n = len(self.subs)
+        start = self._rr
+        self._rr = (self._rr + 1) % n
+        got: List[Msg] = []
+        for k in range(n):
+            got += await self.subs[(start + k) % n].fetch(batch - len(got), 0)
+            if len(got) >= batch:
+                return got
+        if got or (timeout is not None and timeout <= 0):
+            return got
+        deadline = None if timeout is None else time.monotonic() + timeout
+        k = 0
+        while True:
+            left = self.POLL_SLICE if deadline is None else min(self.POLL_SLICE, deadline - time.monotonic())
+            got = await self.subs[(start + k) % n].fetch(batch, max(0.0, left))
+            k += 1
+            if got or (deadline is not None and time.monotonic() >= deadline):
+                return got
+
+    async def unsubscribe(self) -> None:
+        await asyncio.gather(*(s.unsubscribe() for s in self.subs))
+
+
+def _sum_infos(infos: Sequence[ConsumerInfo]) -> ConsumerInfo:
+    first = infos[0]
+    if len(infos) == 1:
+        return first
+    return ConsumerInfo(stream=first.stream, name=first.name,
+                        num_pending=sum(i.num_pending for i in infos),
+                        num_ack_pending=sum(i.num_ack_pending for i in infos),
+                        num_redelivered=sum(i.num_redelivered for i in infos),
+                        delivered_seq=max(i.delivered_seq for i in infos),
+                        ack_floor=min(i.ack_floor for i in infos),
+                        num_waiting=sum(i.num_waiting for i in infos))
+
+
 class ShardedBus(Bus):
-    def __init__(self, members: Sequence[Bus]) -> None:
+    def __init__(self, members: Sequence[Bus], pins: Optional[Dict[str, List[int]]] = None,
+                 default: Optional[List[int]] = None) -> None:
         if not members:
             raise BusError("sharded bus needs at least one member")
         self.members = list(members)
-        self._durables: Dict[Tuple[str, str], int] = {}  # (stream, durable) -> shard
+        self.router = Router(len(self.members), pins, default)
+        self._durables: Dict[Tuple[str, str], List[int]] = {}  # (stream, durable) -> shards
 
     @classmethod
-    async def connect(cls, dsns: Sequence[str], max_age: float) -> "ShardedBus":
+    async def connect(cls, spec: Sequence[str] | str, max_age: float) -> "ShardedBus":
         from . import _open
 
-        return cls([await _open(d, max_age) for d in dsns])
+        dsns, pins, default = parse_members(spec if isinstance(spec, str) else ",".join(spec))
+        return cls([await _open(d, max_age) for d in dsns], pins, default)
 
     def _bus(self, subject: str) -> Bus:
-        return self.members[shard_of(subject, len(self.members))]
+        return self.members[self.router.publish_target(subject)]
 
     async def ensure_stream(self, config: Optional[StreamConfig] = None) -> StreamInfo:
         infos = await asyncio.gather(*(m.ensure_stream(config) for m in self.members))
@@ -73,10 +209,9 @@ class ShardedBus(Bus):
         return await self._bus(subject).publish(subject, data, headers)
 
     async def publish_many(self, items: Sequence[Tuple[str, bytes]]) -> List[PubAck]:
-        n = len(self.members)
         groups: Dict[int, List[int]] = {}
         for i, (s, _) in enumerate(items):
-            groups.setdefault(shard_of(s, n), []).append(i)
+            groups.setdefault(self.router.publish_target(s), []).append(i)
         if len(groups) == 1:
             (k, _), = groups.items()
             return await self.members[k].publish_many(items)
@@ -89,22 +224,24 @@ class ShardedBus(Bus):
         return out  # type: ignore[return-value]
 
     async def subscribe(self, subject: str, durable: str, **consumer_opts) -> Subscription:
-        k = shard_of(subject, len(self.members))
-        sub = await self.members[k].subscribe(subject, durable, **consumer_opts)
-        self._durables[(getattr(sub, "stream", None) or "SMS", durable)] = k
-        return sub
+        ks = self.router.members(subject)
+        subs = [await self.members[k].subscribe(subject, durable, **consumer_opts) for k in ks]
+        self._durables[(getattr(subs[0], "stream", None) or "SMS", durable)] = ks
+        return subs[0] if len(subs) == 1 else _PartitionedSub(subs)
 
     async def consumer_info(self, stream: str, durable: str) -> ConsumerInfo:
-        k = self._durables.get((stream, durable))
-        if k is not None:
-            return await self.members[k].consumer_info(stream, durable)
-        for m in self.members:  # a durable created by another client: find its shard
+        ks = self._durables.get((stream, durable))
+        if ks is not None:
+            return _sum_infos([await self.members[k].consumer_info(stream, durable) for k in ks])
+        found = []
+        for m in self.members:  # a durable created by another client: find its shard(s)
             try:
-                info = await m.consumer_info(stream, durable)
+                found.append(await m.consumer_info(stream, durable))
             except Exception:  # noqa: BLE001 — not on this shard
                 continue
-            return info
-        raise BusError(f"consumer {durable!r} not found on any shard")
+        if not found:
+            raise BusError(f"consumer {durable!r} not found on any shard")
+        return _sum_infos(found)
 
     async def stream_info(self, stream: str) -> StreamInfo:
         infos = await asyncio.gather(*(m.stream_info(stream) for m in self.members))

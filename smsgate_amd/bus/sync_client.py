@@ -27,7 +27,7 @@ class SyncBusClient:
 
     def __new__(cls, dsn: str, timeout: float = 10.0):
         if dsn.startswith("sharded+"):
-            return _SyncSharded([d for d in dsn[len("sharded+"):].split(",") if d], timeout)
+            return _SyncSharded(dsn[len("sharded+"):], timeout)
         return super().__new__(cls)
 
     def __init__(self, dsn: str, timeout: float = 10.0) -> None:
@@ -78,26 +78,41 @@ class SyncBusClient:
 
 
 class _SyncSharded:
-    def __init__(self, dsns, timeout: float) -> None:
+    """Blocking view of a ``sharded+`` bus (positional or pinned/partitioned layout,
+    :mod:`.sharded`): a durable of a partitioned subject exists on every partition
+    and its consumer_info is the sum over them."""
+
+    def __init__(self, spec: str, timeout: float) -> None:
+        from .sharded import Router, parse_members
+
+        dsns, pins, default = parse_members(spec)
         self.members = [SyncBusClient(d, timeout) for d in dsns]
+        self.router = Router(len(dsns), pins, default)
 
     def ensure_stream(self) -> None:
         for m in self.members:
             m.ensure_stream()
 
     def subscribe(self, subject: str, durable: str, **opts: Any) -> str:
-        from .sharded import shard_of
-
-        return self.members[shard_of(subject, len(self.members))].subscribe(subject, durable, **opts)
+        names = [self.members[k].subscribe(subject, durable, **opts) for k in self.router.members(subject)]
+        return names[0]
 
     def consumer_info(self, stream: str, durable: str) -> Dict[str, Any]:
-        err: Exception = BusError(f"consumer {durable!r} not found on any shard")
+        found = []
         for m in self.members:
             try:
-                return m.consumer_info(stream, durable)
-            except BusError as exc:
-                err = exc
-        raise err
+                found.append(m.consumer_info(stream, durable))
+            except BusError:
+                continue
+        if not found:
+            raise BusError(f"consumer {durable!r} not found on any shard")
+        if len(found) == 1:
+            return found[0]
+        out = dict(found[0])
+        for k in ("num_pending", "num_ack_pending", "num_redelivered", "num_waiting"):
+            if k in out:
+                out[k] = sum(f.get(k, 0) for f in found)
+        return out
 
     def close(self) -> None:
         for m in self.members:

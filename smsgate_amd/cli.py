@@ -125,7 +125,10 @@ async def _run_dlq(a, settings) -> None:
     from .services.dlq import DlqWorker
 
     bus = await connect(settings.nats_dsn)
-    w = DlqWorker(bus, _pipeline(settings) if a.reparse else None, group=a.group, reparse=a.reparse)
+    # --reparse re-runs the REAL parser (dlq_worker.py:59-78): with --engine the GPU
+    # engine-server the parsers use (an outage naks the batch, it never drops it)
+    w = DlqWorker(bus, _pipeline(settings, a.backend, a.engine) if a.reparse else None, group=a.group,
+                  reparse=a.reparse)
     await w.start()
     await _stop_event().wait()
     await w.stop()
@@ -201,14 +204,18 @@ def _engine_server(a) -> None:
         raise SystemExit(2) from exc
     if ckpt is None:
         log.warning("engine-server: serving RANDOM-INIT weights (--random-init): answers are meaningless")
-    eng = build_engine(model, ckpt, a.device, random_init=a.random_init, max_slots=a.max_slots)
+    from .serving.profiles import profile_kwargs
+
+    kw = profile_kwargs(a.profile, max_slots=a.max_slots)
+    eng = build_engine(model, ckpt, a.device, random_init=a.random_init, **kw)
     stop = threading.Event()
     signal.signal(signal.SIGTERM, lambda *_: stop.set())
     signal.signal(signal.SIGINT, lambda *_: stop.set())
     path = a.listen.replace("unix://", "")
     if os.path.exists(path):
         os.unlink(path)
-    log.info("engine server on %s (%s, %s, %d slots)", a.listen, model, ckpt or "random-init", a.max_slots)
+    log.info("engine server on %s (%s, %s, profile %s, %d slots)", a.listen, model, ckpt or "random-init",
+             a.profile, eng.cfg.max_slots)
     from .obs.metrics import EngineMetricsExporter, start_metrics_server
 
     start_metrics_server(env_var="ENGINE_METRICS_PORT", default=9104)
@@ -291,7 +298,9 @@ def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="python -m smsgate_amd", description="smsgate_amd services")
     p.add_argument("-v", "--verbose", action="store_true")
     sp = p.add_subparsers(dest="cmd", required=True)
-    sp.add_parser("gateway")
+    gp = sp.add_parser("gateway")
+    gp.add_argument("--workers", type=int, default=0,
+                    help="HTTP worker processes on the port (default GATEWAY_WORKERS or 1)")
     pp = sp.add_parser("parser")
     pp.add_argument("--name", default=f"{socket.gethostname()}-{os.getpid()}")
     pp.add_argument("--group", default="parser_worker")
@@ -303,6 +312,8 @@ def build_parser() -> argparse.ArgumentParser:
     dp.add_argument("--name", default=f"{socket.gethostname()}-{os.getpid()}")
     dp.add_argument("--group", default="parser_worker_dlq")
     dp.add_argument("--reparse", action="store_true")
+    dp.add_argument("--backend", default=None, help="parser backend for --reparse (default PARSER_BACKEND)")
+    dp.add_argument("--engine", default=None, help="unix:///path of an engine-server (GPU) for --reparse")
     sp.add_parser("xml-watcher")
     np_ = sp.add_parser("notifier")
     np_.add_argument("--state", default="last_state.json")
@@ -325,7 +336,9 @@ def build_parser() -> argparse.ArgumentParser:
     ep.add_argument("--random-init", action="store_true",
                     help="serve random weights (throughput tests only; every SMS ends in the DLQ)")
     ep.add_argument("--device", default="cuda:0")
-    ep.add_argument("--max-slots", type=int, default=4096)
+    ep.add_argument("--profile", default="throughput", choices=["throughput", "latency"],
+                    help="engine configuration (serving/profiles.py): the one bench.py measures by default")
+    ep.add_argument("--max-slots", type=int, default=None, help="default: the profile's")
     pl = sp.add_parser("pipeline")
     pl.add_argument("--backend", default=None)
     db = sp.add_parser("db")
@@ -373,8 +386,19 @@ def main(argv: Optional[List[str]] = None) -> int:
         init_sentry(release="api_gateway@0.1.0")
         port = int(settings.api_port or 9001)
         tunnel = open_tunnel(settings, port)
+        workers = a.workers or int(os.getenv("GATEWAY_WORKERS", "1"))
         try:
-            uvicorn.run(create_app(log_dir=settings.log_dir), host=settings.api_host or "0.0.0.0", port=port)
+            if workers > 1:
+                # N processes on one port (uvicorn workers), each with its own bus client;
+                # Prometheus counters aggregated across them (obs.metrics.render_latest)
+                import tempfile
+
+                os.environ.setdefault("PROMETHEUS_MULTIPROC_DIR",
+                                      tempfile.mkdtemp(prefix="smsgate-gw-metrics-"))
+                uvicorn.run("smsgate_amd.services.gateway:default_app", factory=True, workers=workers,
+                            host=settings.api_host or "0.0.0.0", port=port, log_level="warning")
+            else:
+                uvicorn.run(create_app(log_dir=settings.log_dir), host=settings.api_host or "0.0.0.0", port=port)
         finally:
             if tunnel is not None:
                 tunnel.close()

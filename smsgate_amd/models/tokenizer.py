@@ -92,6 +92,13 @@ class ExtractorTokenizer:
             if a < 0:
                 return self.encode(value)
             z = a + len(value)
+            # an occurrence inside a longer word is not the value ("AM" in "AMERIABANK"
+            # vs the city ", AM&#10;"): values are copied at word boundaries (the copy
+            # constraint, serving/fsm.py, only lets a value start and end there)
+            if (a > 0 and value[0].isalnum() and body[a - 1].isalnum()) or \
+                    (z < len(body) and value[-1].isalnum() and body[z].isalnum()):
+                start = a + 1
+                continue
             k0 = next((k for k, (s, e) in enumerate(offsets) if s <= a < e), None)
             k1 = next((k for k, (s, e) in enumerate(offsets) if e == z), None)
             if k0 is not None and k1 is not None and k1 >= k0 and body[offsets[k0][0]:a].strip() == "":

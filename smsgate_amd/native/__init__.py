@@ -10,6 +10,9 @@
   journal writes, long-poll fetch waiters.  ``nats_listen`` adds the NATS client
   protocol + JetStream API front-end (the subset :mod:`smsgate_amd.bus.nats_server`
   serves) on the same engine, so nats-py style clients reach the fast broker.
+  ``http_listen`` adds native HTTP ingestion (``csrc/http_ingest.hpp``): the
+  gateway's ``POST /sms/raw`` / ``/sms/raw/batch`` contract, ``/health``,
+  ``/metrics``, stored straight into ``sms.raw`` by the broker's own loop.
 
 Build: ``python -m smsgate_amd.native.build`` (in-tree, ``_bin/``).
 """
@@ -35,11 +38,12 @@ class NativeBroker:
     """A running ``smsgate-busd`` child process."""
 
     def __init__(self, proc: subprocess.Popen, listens: List[str], tcp_port: Optional[int],
-                 nats_port: Optional[int] = None) -> None:
+                 nats_port: Optional[int] = None, http_port: Optional[int] = None) -> None:
         self.proc = proc
         self.listens = listens
         self.tcp_port = tcp_port
         self.nats_port = nats_port
+        self.http_port = http_port
 
     @property
     def pid(self) -> int:
@@ -72,7 +76,8 @@ class NativeBroker:
 def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_age: float = 3 * 24 * 3600.0,
                fsync: str = "interval", fsync_interval_s: float = 0.05, compact_bytes: Optional[int] = None,
                ready_timeout: float = 20.0, binary: Optional[Path] = None, stderr=None,
-               die_with_parent: bool = True, nats_listen: Optional[str] = None) -> NativeBroker:
+               die_with_parent: bool = True, nats_listen: Optional[str] = None,
+               http_listen: Optional[str] = None) -> NativeBroker:
     """Start the native broker and wait until it listens.
 
     ``listen`` takes ``tcp://host:port`` (port 0 = pick one, see
@@ -89,6 +94,8 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
         cmd += ["--listen", u]
     if nats_listen:
         cmd += ["--nats-listen", nats_listen]
+    if http_listen:
+        cmd += ["--http-listen", http_listen]
     if data_dir:
         cmd += ["--data", str(data_dir)]
     cmd += ["--max-age", repr(float(max_age)), "--fsync", fsync, "--fsync-interval", repr(float(fsync_interval_s))]
@@ -107,8 +114,8 @@ def spawn_busd(listen: str | List[str], data_dir: Optional[str] = None, *, max_a
         raise RuntimeError(f"smsgate-busd failed to start (exit {proc.poll()}): {line!r}")
     parts = line.split()
     tok = parts[1].decode()
-    nats_port = int(parts[3]) if len(parts) >= 4 and parts[2] == b"NATS" else None
-    return NativeBroker(proc, listens, None if tok == "-" else int(tok), nats_port)
+    extra = {parts[k].decode(): int(parts[k + 1]) for k in range(2, len(parts) - 1, 2)}  # "NATS p", "HTTP p"
+    return NativeBroker(proc, listens, None if tok == "-" else int(tok), extra.get("NATS"), extra.get("HTTP"))
 
 
 def _pdeathsig() -> None:  # runs in the child between fork and exec

@@ -55,6 +55,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "http_ingest.hpp"
 #include "json.hpp"
 
 namespace {
@@ -101,7 +102,7 @@ uint32_t get_u32(const char* p) {
 }
 
 // ------------------------------------------------------------------- journal
-class Journal {
+class Journal : public bus::JournalSink {
  public:
   Journal(std::string dir, std::string mode, double interval, int64_t compact_bytes)
       : dir_(std::move(dir)), mode_(std::move(mode)), interval_(interval), compact_bytes_(compact_bytes) {
@@ -178,6 +179,34 @@ class Journal {
     if (bytes_ > std::max(compact_bytes_, 2 * floor_bytes_)) need_compact = true;
   }
 
+  // Hot-path records encoded in place: [len][crc][ ["store", [stream, seq, subject,
+  // bin(data), ts, headers]] ] -- the bytes frame() produces for the same record.
+  void store(const std::string& stream, int64_t seq, const std::string& subject, const std::string& data, double ts,
+             const mp::Value& headers) override {
+    const size_t at = begin_record();
+    mp::enc_arr_hdr(buf_, 2);
+    mp::enc_str(buf_, "store", 5);
+    mp::enc_arr_hdr(buf_, 6);
+    mp::enc_str(buf_, stream);
+    mp::enc_int(buf_, seq);
+    mp::enc_str(buf_, subject);
+    mp::enc_bin(buf_, data.data(), data.size());
+    mp::enc_double(buf_, ts);
+    mp::encode(buf_, headers);
+    end_record(at);
+  }
+
+  void ack(const char* kind, const std::string& stream, const std::string& durable, int64_t seq) override {
+    const size_t at = begin_record();
+    mp::enc_arr_hdr(buf_, 2);
+    mp::enc_str(buf_, kind, strlen(kind));
+    mp::enc_arr_hdr(buf_, 3);
+    mp::enc_str(buf_, stream);
+    mp::enc_str(buf_, durable);
+    mp::enc_int(buf_, seq);
+    end_record(at);
+  }
+
   // Group commit: one write(2) for everything appended since the last flush.
   void flush() {
     if (buf_.empty() || fd_ < 0) return;
@@ -247,6 +276,23 @@ class Journal {
   std::condition_variable cv_;
   bool want_sync_ = false, stop_ = false;
   int sync_fd_ = -1;
+
+  size_t begin_record() {
+    const size_t at = buf_.size();
+    buf_.append(8, '\0');  // length + CRC, patched by end_record
+    return at;
+  }
+
+  void end_record(size_t at) {
+    const size_t n = buf_.size() - at - 8;
+    const uint32_t c = crc::crc32(buf_.data() + at + 8, n);
+    for (int k = 0; k < 4; ++k) {
+      buf_[at + k] = (char)((n >> (8 * k)) & 0xff);
+      buf_[at + 4 + k] = (char)((c >> (8 * k)) & 0xff);
+    }
+    bytes_ += (int64_t)(n + 8);
+    if (bytes_ > std::max(compact_bytes_, 2 * floor_bytes_)) need_compact = true;
+  }
 
   void sync_loop() {
     std::unique_lock<std::mutex> lk(mu_);
@@ -464,6 +510,8 @@ struct Conn {
   int fd;
   uint64_t id;
   bool nats = false;                               // NATS text protocol (--nats-listen)
+  bool http = false;                               // HTTP/1.1 ingestion (--http-listen)
+  bool close_after = false;                        // HTTP: close once the reply is written
   std::unordered_map<std::string, NSub> subs;      // NATS: sid -> subscription
   std::string in;
   size_t in_off = 0;
@@ -507,7 +555,7 @@ class Server {
     return c;
   }
 
-  int listen_on(const std::string& url, bool nats = false) {
+  int listen_on(const std::string& url, bool nats = false, bool http = false) {
     int fd;
     int port = -1;
     if (url.rfind("unix://", 0) == 0) {
@@ -545,7 +593,7 @@ class Server {
     ev.events = EPOLLIN;
     ev.data.u64 = 0;  // 0 = a listener; look up by fd
     listeners_.push_back(fd);
-    ev.data.u64 = (uint64_t)fd | (1ull << 63) | (nats ? (1ull << 62) : 0);
+    ev.data.u64 = (uint64_t)fd | (1ull << 63) | (nats ? (1ull << 62) : 0) | (http ? (1ull << 61) : 0);
     epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev);
     return port;
   }
@@ -560,14 +608,15 @@ class Server {
       for (int k = 0; k < n; ++k) {
         uint64_t tag = evs[k].data.u64;
         if (tag & (1ull << 63)) {
-          accept_all((int)(tag & 0xffffffff), (tag >> 62) & 1);
+          accept_all((int)(tag & 0xffffffff), (tag >> 62) & 1, (tag >> 61) & 1);
           continue;
         }
         auto it = conns_.find(tag);
         if (it == conns_.end()) continue;
         Conn& c = it->second;
         if (evs[k].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) read_conn(c);
-        if (evs[k].events & EPOLLOUT) c.writing = false;  // retry the write below
+        // EPOLLOUT: nothing to do here -- flush_conns retries every pending write each
+        // iteration; `writing` means EPOLLOUT interest is armed until the output drains
       }
       double now = wall_now();
       if (now - last_expire_ >= 1.0) {
@@ -625,7 +674,7 @@ class Server {
     return (int)std::ceil(t * 1000.0);
   }
 
-  void accept_all(int lfd, bool nats) {
+  void accept_all(int lfd, bool nats, bool http = false) {
     for (;;) {
       int fd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (fd < 0) return;
@@ -636,6 +685,7 @@ class Server {
       c.fd = fd;
       c.id = id;
       c.nats = nats;
+      c.http = http;
       if (nats) nats_info(c);
       epoll_event ev{};
       ev.events = EPOLLIN | EPOLLRDHUP;
@@ -657,7 +707,8 @@ class Server {
       break;
     }
     if (c.nats) nats_parse(c);
-    while (!c.nats && c.in.size() - c.in_off >= 4) {
+    if (c.http) http_parse(c);
+    while (!c.nats && !c.http && c.in.size() - c.in_off >= 4) {
       uint32_t len = get_u32(c.in.data() + c.in_off);
       if (len > (256u << 20)) { c.dead = true; break; }
       if (c.in.size() - c.in_off < 4 + (size_t)len) break;
@@ -894,13 +945,17 @@ class Server {
           c.dead = true;
         }
       }
+      if (c.close_after && c.out_off == c.out.size()) c.dead = true;  // HTTP "Connection: close": reply sent
       if (c.out_off == c.out.size() && !c.out.empty()) {
         c.out.clear();
         c.out_off = 0;
-        epoll_event ev{};
-        ev.events = EPOLLIN | EPOLLRDHUP;
-        ev.data.u64 = c.id;
-        epoll_ctl(ep_, EPOLL_CTL_MOD, c.fd, &ev);
+        if (c.writing) {  // EPOLLOUT was armed by a short write: back to read-only interest
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.u64 = c.id;
+          epoll_ctl(ep_, EPOLL_CTL_MOD, c.fd, &ev);
+          c.writing = false;
+        }
       }
       if (c.dead) {
         epoll_ctl(ep_, EPOLL_CTL_DEL, c.fd, nullptr);
@@ -913,7 +968,134 @@ class Server {
   }
 
 
+  // =================================================================== HTTP
+  // Native ingestion front-end (``--http-listen``): the gateway's POST /sms/raw and
+  // POST /sms/raw/batch contract (http_ingest.hpp) plus GET /health and GET
+  // /metrics, HTTP/1.1 keep-alive (pipelined requests are answered in order).  An
+  // accepted SMS is stored on sms.raw by this loop's engine and its journal record
+  // is group-committed before the 202 leaves, like a msgpack publish.
+  static constexpr size_t kHttpMaxHeader = 64u << 10, kHttpMaxBody = 64u << 20;
+
+  static std::string lower(std::string s) {
+    for (auto& ch : s) ch = (char)tolower((unsigned char)ch);
+    return s;
+  }
+
+  void http_reply(Conn& c, int status, const std::string& body, bool keep_alive,
+                  const char* ctype = "application/json") {
+    const char* reason = status == 200   ? "OK"
+                         : status == 202 ? "Accepted"
+                         : status == 400 ? "Bad Request"
+                         : status == 404 ? "Not Found"
+                         : status == 405 ? "Method Not Allowed"
+                         : status == 413 ? "Content Too Large"
+                         : status == 422 ? "Unprocessable Entity"
+                         : status == 431 ? "Request Header Fields Too Large"
+                         : status == 501 ? "Not Implemented"
+                                         : "Internal Server Error";
+    c.out += "HTTP/1.1 " + std::to_string(status) + " " + reason + "\r\ncontent-length: " +
+             std::to_string(body.size()) + "\r\ncontent-type: " + ctype + "\r\n" +
+             (keep_alive ? "" : "connection: close\r\n") + "\r\n" + body;
+    if (!keep_alive) c.close_after = true;
+  }
+
+  void http_parse(Conn& c) {
+    while (!c.dead && !c.close_after) {
+      const char* base = c.in.data() + c.in_off;
+      const size_t avail = c.in.size() - c.in_off;
+      const char* he = (const char*)memmem(base, avail, "\r\n\r\n", 4);
+      if (!he) {
+        if (avail > kHttpMaxHeader) http_reply(c, 431, "{\"detail\":\"Request Header Fields Too Large\"}", false);
+        return;
+      }
+      const size_t hlen = (size_t)(he - base) + 4;
+      const std::string head(base, hlen - 4);
+      const size_t eol = head.find("\r\n");
+      const std::string line = head.substr(0, eol);
+      const size_t sp1 = line.find(' '), sp2 = line.rfind(' ');
+      if (sp1 == std::string::npos || sp2 == sp1) {
+        http_reply(c, 400, "{\"detail\":\"Bad Request\"}", false);
+        return;
+      }
+      const std::string method = line.substr(0, sp1), version = line.substr(sp2 + 1);
+      std::string path = line.substr(sp1 + 1, sp2 - sp1 - 1);
+      bool keep_alive = version == "HTTP/1.1";
+      long long clen = 0;
+      bool chunked = false;
+      size_t pos = eol == std::string::npos ? head.size() : eol + 2;
+      while (pos < head.size()) {
+        size_t e = head.find("\r\n", pos);
+        if (e == std::string::npos) e = head.size();
+        const std::string h = head.substr(pos, e - pos);
+        pos = e + 2;
+        const size_t colon = h.find(':');
+        if (colon == std::string::npos) continue;
+        const std::string name = lower(h.substr(0, colon));
+        size_t v0 = colon + 1;
+        while (v0 < h.size() && (h[v0] == ' ' || h[v0] == '\t')) ++v0;
+        const std::string val = lower(h.substr(v0));
+        if (name == "content-length") {
+          clen = atoll(val.c_str());
+        } else if (name == "transfer-encoding") {
+          chunked = val.find("chunked") != std::string::npos;
+        } else if (name == "connection") {
+          if (val.find("close") != std::string::npos) keep_alive = false;
+          else if (val.find("keep-alive") != std::string::npos) keep_alive = true;
+        }
+      }
+      if (chunked) {
+        http_reply(c, 501, "{\"detail\":\"chunked bodies are not supported: send Content-Length\"}", false);
+        return;
+      }
+      if (clen < 0 || (size_t)clen > kHttpMaxBody) {
+        http_reply(c, 413, "{\"detail\":\"Content Too Large\"}", false);
+        return;
+      }
+      if (avail < hlen + (size_t)clen) return;  // the rest of the body has not arrived yet
+      const std::string body(base + hlen, (size_t)clen);
+      c.in_off += hlen + (size_t)clen;
+      const size_t q = path.find('?');
+      if (q != std::string::npos) path.resize(q);
+      http_route(c, method, path, body, keep_alive);
+    }
+  }
+
+  void http_route(Conn& c, const std::string& method, const std::string& path, const std::string& body,
+                  bool keep_alive) {
+    const bool one = path == "/sms/raw", batch = path == "/sms/raw/batch";
+    if (one || batch) {
+      if (method != "POST") {
+        http_reply(c, 405, "{\"detail\":\"Method Not Allowed\"}", keep_alive);
+        return;
+      }
+      ingest::Result r = ingest::handle(body, batch);
+      if (r.status == 202) {
+        try {
+          for (auto& raw : r.raws) eng_.store("sms.raw", std::move(raw), mp::Value::nil());
+        } catch (std::exception&) {
+          r.status = 500;
+          r.body = "{\"detail\":\"Internal error\"}";
+        }
+      }
+      ++http_counts_[{path, r.status}];
+      http_reply(c, r.status, r.body, keep_alive);
+    } else if (path == "/health" && method == "GET") {
+      http_reply(c, 200, "{\"status\":\"ok\"}", keep_alive);  // this process IS the bus
+    } else if (path == "/metrics" && method == "GET") {
+      std::string o = "# HELP api_gateway_requests_total HTTP requests\n# TYPE api_gateway_requests_total counter\n";
+      for (auto& kv : http_counts_)
+        o += "api_gateway_requests_total{endpoint=\"" + kv.first.first + "\",status=\"" +
+             std::to_string(kv.first.second) + "\"} " + std::to_string(kv.second) + "\n";
+      http_reply(c, 200, o, keep_alive, "text/plain; version=0.0.4");
+    } else {
+      http_reply(c, 404, "{\"detail\":\"Not Found\"}", keep_alive);
+    }
+  }
+
+  std::map<std::pair<std::string, int>, long long> http_counts_;  // (endpoint, status) -> requests
+
   // =================================================================== NATS
+
   // NATS client protocol + the JetStream API subset of bus/nats_server.py (the
   // Python front-end; tests/test_bus_nats.py runs the same client tests against
   // both): core INFO/CONNECT/PING/PONG/PUB/HPUB/SUB (queue groups)/UNSUB with
@@ -1498,7 +1680,7 @@ class Server {
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::vector<std::string> listens, nats_listens;
+  std::vector<std::string> listens, nats_listens, http_listens;
   std::string data_dir, fsync_mode = "interval";
   double max_age = 3 * 24 * 3600.0, fsync_interval = 0.05;
   int64_t compact_bytes = 256ll << 20;
@@ -1510,18 +1692,20 @@ int main(int argc, char** argv) {
     };
     if (a == "--listen") listens.push_back(val());
     else if (a == "--nats-listen") nats_listens.push_back(val());
+    else if (a == "--http-listen") http_listens.push_back(val());
     else if (a == "--data") data_dir = val();
     else if (a == "--max-age") max_age = atof(val().c_str());
     else if (a == "--fsync") fsync_mode = val();
     else if (a == "--fsync-interval") fsync_interval = atof(val().c_str());
     else if (a == "--compact-bytes") compact_bytes = atoll(val().c_str());
     else if (a == "-h" || a == "--help") {
-      printf("usage: smsgate-busd --listen URL [--listen URL] [--nats-listen tcp://HOST:PORT] [--data DIR] [--max-age S] "
+      printf("usage: smsgate-busd --listen URL [--listen URL] [--nats-listen tcp://HOST:PORT] "
+             "[--http-listen tcp://HOST:PORT] [--data DIR] [--max-age S] "
              "[--fsync interval|always|never] [--fsync-interval S] [--compact-bytes N]\n");
       return 0;
     } else die("unknown argument " + a);
   }
-  if (listens.empty() && nats_listens.empty()) listens.push_back("tcp://127.0.0.1:4222");
+  if (listens.empty() && nats_listens.empty() && http_listens.empty()) listens.push_back("tcp://127.0.0.1:4222");
   if (fsync_mode != "interval" && fsync_mode != "always" && fsync_mode != "never") die("bad --fsync " + fsync_mode);
 
   struct sigaction sa{};
@@ -1537,6 +1721,7 @@ int main(int argc, char** argv) {
     recover(eng, *jr);
     Journal* j = jr.get();
     eng.journal = [j](const char* kind, mp::Value&& args) { j->append(kind, std::move(args)); };
+    eng.fast = j;
   }
   Server srv(eng, jr.get(), max_age);
   if (eng.streams.empty()) eng.add_or_update_stream(srv.default_config());
@@ -1551,8 +1736,14 @@ int main(int argc, char** argv) {
     int p = srv.listen_on(l, true);
     if (p >= 0 && nats_port < 0) nats_port = srv.nats_port_ = p;
   }
+  int http_port = -1;
+  for (auto& l : http_listens) {
+    int p = srv.listen_on(l, false, true);
+    if (p >= 0 && http_port < 0) http_port = p;
+  }
   std::string ready = tcp_port >= 0 ? "READY " + std::to_string(tcp_port) : std::string("READY -");
   if (nats_port >= 0) ready += " NATS " + std::to_string(nats_port);
+  if (http_port >= 0) ready += " HTTP " + std::to_string(http_port);
   printf("%s\n", ready.c_str());
   fflush(stdout);
   srv.run();

@@ -13,6 +13,14 @@
 //                        [--msgs 100000] [--batch 256] [--fetch 256] [--depth 4]
 //                        [--payload 300] [--durable load]
 // Prints one JSON line: {"published":..,"acked":..,"seconds":..,"publish_per_s":..}
+//
+// HTTP mode (the broker's native ingestion front-end, --http-listen):
+//   smsgate-busload --http PORT [--path /sms/raw] [--conns 64] [--seconds 5] [--depth 1] [--batch 1]
+// C threads, one keep-alive connection each, keep --depth requests in flight
+// (pipelined) and count 202 answers for --seconds; --batch > 1 posts
+// /sms/raw/batch arrays.  Prints {"mode":"http","requests_per_s":..,"msgs_per_s":..}.
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -31,7 +39,9 @@
 namespace {
 
 struct Opts {
-  std::string socket;
+  std::string socket, path = "/sms/raw";
+  int http_port = 0, conns = 64;
+  double seconds = 5.0;
   int producers = 4, consumers = 64, batch = 256, fetch = 256, depth = 4, payload = 300;
   long msgs = 100000;
   std::string durable = "load", subject = "sms.raw", stream = "SMS";
@@ -167,22 +177,107 @@ void consumer(const Opts& o, long total) {
   ::close(fd);
 }
 
+// ---------------------------------------------------------------- HTTP mode
+std::atomic<long> g_http_ok{0}, g_http_msgs{0}, g_http_other{0};
+
+std::string http_request(const Opts& o, long k) {
+  std::string body;
+  auto one = [&](long i) {
+    return std::string("{\"device_id\":\"load\",\"message\":\"APPROVED PURCHASE DB SALE: SHOP ") +
+           std::to_string(i) + ", YEREVAN,06.05.25 14:23,card ***0018. Amount:" + std::to_string(i % 997 + 1) +
+           ".00 USD, Balance:1842.74 USD\",\"sender\":\"BANK\",\"timestamp\":1746541380,\"source\":\"device\"}";
+  };
+  if (o.batch > 1) {
+    body = "[";
+    for (int b = 0; b < o.batch; ++b) body += (b ? "," : "") + one(k * o.batch + b);
+    body += "]";
+  } else {
+    body = one(k);
+  }
+  return "POST " + o.path + " HTTP/1.1\r\nHost: load\r\nContent-Type: application/json\r\nContent-Length: " +
+         std::to_string(body.size()) + "\r\n\r\n" + body;
+}
+
+void http_worker(const Opts& o, int idx, double t_end) {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)o.http_port);
+  a.sin_addr.s_addr = htonl(0x7f000001);
+  if (fd < 0 || ::connect(fd, (sockaddr*)&a, sizeof a) < 0) { g_fail = true; return; }
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  std::vector<std::string> reqs;
+  for (int k = 0; k < 64; ++k) reqs.push_back(http_request(o, (long)idx * 1000000 + k));
+  std::string in;
+  long sent = 0, got = 0;
+  char buf[1 << 16];
+  while (!g_go.load()) std::this_thread::yield();
+  bool stop = false;
+  while (!stop || got < sent) {
+    while (!stop && sent - got < o.depth) {
+      if (!send_all(fd, reqs[sent % reqs.size()])) { g_fail = true; return; }
+      ++sent;
+      if (now_s() >= t_end) stop = true;
+    }
+    ssize_t r = ::read(fd, buf, sizeof buf);
+    if (r <= 0) { g_fail = true; return; }
+    in.append(buf, (size_t)r);
+    for (;;) {  // complete responses in `in`
+      size_t he = in.find("\r\n\r\n");
+      if (he == std::string::npos) break;
+      size_t cl = in.find("content-length: ");
+      if (cl == std::string::npos || cl > he) { g_fail = true; return; }
+      long clen = atol(in.c_str() + cl + 16);
+      if (in.size() < he + 4 + (size_t)clen) break;
+      int status = atoi(in.c_str() + 9);
+      if (status == 202) { ++g_http_ok; g_http_msgs += o.batch > 1 ? o.batch : 1; }
+      else ++g_http_other;
+      in.erase(0, he + 4 + (size_t)clen);
+      ++got;
+    }
+    if (now_s() >= t_end) stop = true;
+  }
+  ::close(fd);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Opts o;
+  bool batch_given = false;
   for (int i = 1; i + 1 < argc; i += 2) {
     std::string k = argv[i], v = argv[i + 1];
     if (k == "--socket") o.socket = v;
     else if (k == "--producers") o.producers = atoi(v.c_str());
     else if (k == "--consumers") o.consumers = atoi(v.c_str());
     else if (k == "--msgs") o.msgs = atol(v.c_str());
-    else if (k == "--batch") o.batch = atoi(v.c_str());
+    else if (k == "--batch") o.batch = atoi(v.c_str()), batch_given = true;
     else if (k == "--fetch") o.fetch = atoi(v.c_str());
     else if (k == "--depth") o.depth = atoi(v.c_str());
     else if (k == "--payload") o.payload = std::max(24, atoi(v.c_str()));
     else if (k == "--durable") o.durable = v;
+    else if (k == "--http") o.http_port = atoi(v.c_str());
+    else if (k == "--path") o.path = v;
+    else if (k == "--conns") o.conns = atoi(v.c_str());
+    else if (k == "--seconds") o.seconds = atof(v.c_str());
     else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
+  }
+  if (o.http_port > 0) {
+    if (!batch_given) o.batch = 1;  // one SMS per request unless --batch is given
+    if (o.batch > 1 && o.path == "/sms/raw") o.path = "/sms/raw/batch";
+    const double t0 = now_s();
+    std::vector<std::thread> ts;
+    for (int c = 0; c < o.conns; ++c) ts.emplace_back(http_worker, std::cref(o), c, t0 + o.seconds);
+    g_go = true;
+    for (auto& t : ts) t.join();
+    const double dt = now_s() - t0;
+    printf("{\"mode\": \"http\", \"path\": \"%s\", \"conns\": %d, \"depth\": %d, \"batch\": %d, \"seconds\": %.3f, "
+           "\"requests_202\": %ld, \"requests_other\": %ld, \"requests_per_s\": %.0f, \"msgs_per_s\": %.0f, "
+           "\"ok\": %s}\n",
+           o.path.c_str(), o.conns, o.depth, o.batch, dt, g_http_ok.load(), g_http_other.load(), g_http_ok.load() / dt,
+           g_http_msgs.load() / dt, g_fail.load() ? "false" : "true");
+    return g_fail.load() ? 1 : 0;
   }
   if (o.socket.empty()) { fprintf(stderr, "--socket required\n"); return 2; }
   {  // the stream must exist before consumers subscribe

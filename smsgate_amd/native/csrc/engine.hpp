@@ -133,12 +133,21 @@ struct Stream {
 };
 
 using JournalFn = std::function<void(const char* kind, mp::Value&& args)>;
+// Hot-path records written straight into the journal buffer (same bytes as the
+// generic JournalFn path would frame, without building an mp::Value per message)
+struct JournalSink {
+  virtual ~JournalSink() = default;
+  virtual void store(const std::string& stream, int64_t seq, const std::string& subject, const std::string& data,
+                     double ts, const mp::Value& headers) = 0;
+  virtual void ack(const char* kind, const std::string& stream, const std::string& durable, int64_t seq) = 0;
+};
 
 class Engine {
  public:
   std::map<std::string, Stream> streams;  // ordered like Python's insertion for the single default stream
   std::vector<std::string> order;         // insertion order of streams (routing priority)
   JournalFn journal;                      // empty = no journal (replay)
+  JournalSink* fast = nullptr;            // store / ack records (set with `journal`)
   std::function<double()> clock;
 
   explicit Engine(std::function<double()> clk) : clock(std::move(clk)) {}
@@ -248,7 +257,9 @@ class Engine {
       Consumer& c = kv.second;
       if (seq > c.cursor && matches(c.cfg.filter_subject, subject)) c.num_pending += 1;
     }
-    if (journal) {
+    if (fast) {
+      fast->store(st.cfg.name, seq, subject, m->data, ts, m->headers);
+    } else if (journal) {
       mp::Value a = mp::Value::arr();
       a.push(mp::Value::str(st.cfg.name));
       a.push(mp::Value::integer(seq));
@@ -461,11 +472,15 @@ class Engine {
     bool hit = c.pending.erase(seq) > 0;
     if (hit) {
       if (kind[0] == 't') c.num_dropped += 1;
-      mp::Value a = mp::Value::arr();
-      a.push(mp::Value::str(s));
-      a.push(mp::Value::str(d));
-      a.push(mp::Value::integer(seq));
-      log(kind, std::move(a));
+      if (fast) {
+        fast->ack(kind, s, d, seq);
+      } else if (journal) {
+        mp::Value a = mp::Value::arr();
+        a.push(mp::Value::str(s));
+        a.push(mp::Value::str(d));
+        a.push(mp::Value::integer(seq));
+        log(kind, std::move(a));
+      }
     }
     return hit;
   }

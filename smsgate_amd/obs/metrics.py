@@ -167,4 +167,14 @@ def start_metrics_server(port: Optional[int] = None, *, env_var: str = "METRICS_
 
 
 def render_latest(registry: CollectorRegistry = REGISTRY) -> bytes:
+    """The exposition text.  Under ``PROMETHEUS_MULTIPROC_DIR`` (a multi-process
+    server: ``gateway --workers N``) the counters of every worker process are
+    aggregated, so ``/metrics`` is the same whichever worker answers it."""
+    mp_dir = os.getenv("PROMETHEUS_MULTIPROC_DIR")
+    if mp_dir and registry is REGISTRY:
+        from prometheus_client import multiprocess
+
+        reg = CollectorRegistry()
+        multiprocess.MultiProcessCollector(reg, path=mp_dir)
+        return generate_latest(reg)
     return generate_latest(registry)

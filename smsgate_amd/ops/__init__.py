@@ -119,7 +119,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_gemm_argmax.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int, _ip, _ip, _vp,
                                    _vp, _vp, _c_int, _ip, _vp, _vp]
     lib.sg_gemm_argmax.restype = _c_int
-    lib.sg_copy_masks.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp, _vp]
+    lib.sg_copy_masks.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _vp, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp,
+                                  _vp]
     lib.sg_copy_masks.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version"):
@@ -567,8 +568,10 @@ def copy_masks(fsm, row_state: torch.Tensor, prev_tok: torch.Tensor, row_slot: t
                body_buf: torch.Tensor, body_len: torch.Tensor, out: torch.Tensor, n: Optional[int] = None) -> torch.Tensor:
     """Per-row allowed-token masks of copy-constrained decoding (csrc/spec_kernels.hip
     ``copy_mask_kernel``): for each of ``n`` rows whose state is a copy state, ``out[r]``
-    = the state's schema mask AND (<sep> | any token of the row's body at a value's
-    first position | a token following ``prev_tok[r]`` in the body after that).  The
+    = the state's schema mask AND, at a value's first position, <sep> or any body token
+    at a word boundary; after that, a token following ``prev_tok[r]`` in the body, and
+    <sep> where such an occurrence is followed by a word boundary
+    (:meth:`~smsgate_amd.serving.fsm.SchemaFSM.copy_mask_host` is the reference).  The
     body of row ``r`` is ``body_buf[row_slot[r], :body_len[row_slot[r]]]``.  Rows in
     other states are not written (the consumers only read copy rows)."""
     n = row_state.numel() if n is None else n
@@ -582,10 +585,11 @@ def copy_masks(fsm, row_state: torch.Tensor, prev_tok: torch.Tensor, row_slot: t
     _req(out, torch.int32, "out")
     if out.dim() != 2 or out.shape[0] < n or out.shape[1] != fsm.vocab // 32 or body_len.numel() != S1:
         raise ValueError("copy_masks: out must be [>= n, vocab/32]; body_len must match body_buf")
-    if fsm.copy_kind_t is None:
-        raise ValueError("copy_masks: the FSM has no copy states (to_device first)")
+    if fsm.copy_kind_t is None or fsm.tok_flags_t is None:
+        raise ValueError("copy_masks: the FSM has no copy tables (to_device first)")
     _check(load_library().sg_copy_masks(_p(fsm.masks), _p(fsm.state_mask), fsm.sep_token, fsm.vocab,
-                                        _p(fsm.copy_kind_t), _p(row_state), _p(prev_tok), _p(row_slot),
+                                        _p(fsm.copy_kind_t), _p(fsm.tok_flags_t), _p(row_state), _p(prev_tok),
+                                        _p(row_slot),
                                         _p(body_buf), _p(body_len), LB, n, _p(out), _stream()), "copy_masks")
     return out
 

@@ -362,19 +362,27 @@ __global__ void __launch_bounds__(256) fsm_commit_kernel(
 // ---------------------------------------------------------------------------
 // copy-constrained decoding (serving/fsm.py COPY_START / COPY_NEXT states): the
 // per-row allowed-token mask = the state's schema mask AND the tokens the row may
-// copy from its own SMS body -- any body token at a value's first position, after
-// that only a token that follows the previous token somewhere in the body -- plus
-// <sep>.  One wave per row builds the bit set in LDS (V/32 words), then writes the
-// full mask row; rows in non-copy states are skipped (their mask row is never read:
-// the consumers check copy_kind[state] first).  Consumers: the lm_head arg-max
-// epilogue (EPI 4), fsm_sample_kernel, spec_verify_kernel.
+// copy from its own SMS body.  A value starts at a word boundary of the body (any
+// body token not glued to an alphanumeric predecessor; <sep> = an empty value is
+// always allowed there); after that the next token must follow the previous one
+// somewhere in the body, and <sep> is allowed only where such an occurrence is
+// followed by a word boundary (or the end of the body) -- a value never ends
+// inside a word split into several tokens.  Boundary: tokens a, b adjacent with
+// NOT (a ends alphanumeric AND b starts alphanumeric) (tok_flags, bit 0 = starts,
+// bit 1 = ends alphanumeric; byte-level BPE puts a word's leading blank in its
+// first token).  One wave per row builds the bit set in LDS (V/32 words), then
+// writes the full mask row; rows in non-copy states are skipped (their mask row
+// is never read: the consumers check copy_kind[state] first).  A row left with an
+// empty set decodes <sep> (the consumers' nothing-allowed fallback).  Consumers:
+// the lm_head arg-max epilogue (EPI 4), fsm_sample_kernel, spec_verify_kernel.
 // ---------------------------------------------------------------------------
 #define COPY_MAX_WORDS 512  // V <= 16384
 
 __global__ void __launch_bounds__(256) copy_mask_kernel(
-    FsmTables fsm, const int* __restrict__ copy_kind, const int* __restrict__ row_state,
-    const int* __restrict__ prev_tok, const int* __restrict__ row_slot, const int* __restrict__ body_buf,
-    const int* __restrict__ body_len, int LB, int n, uint32_t* __restrict__ row_masks) {
+    FsmTables fsm, const int* __restrict__ copy_kind, const uint8_t* __restrict__ tok_flags,
+    const int* __restrict__ row_state, const int* __restrict__ prev_tok, const int* __restrict__ row_slot,
+    const int* __restrict__ body_buf, const int* __restrict__ body_len, int LB, int n,
+    uint32_t* __restrict__ row_masks) {
   __shared__ uint32_t bits[4][COPY_MAX_WORDS];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wid;
@@ -391,18 +399,29 @@ __global__ void __launch_bounds__(256) copy_mask_kernel(
   const int bl = min(body_len[sl], LB);
   const int* body = body_buf + (size_t)sl * LB;
   const int prev = prev_tok[r];
+  const int sep = fsm.sep_token;
+  auto flags = [&](int t) -> int { return (t >= 0 && t < fsm.V) ? (int)tok_flags[t] : 0; };
   for (int j = lane; j < bl; j += 64) {
+    const int t = body[j];
     int cand = -1;
-    if (kind == 1) cand = body[j];
-    else if (j + 1 < bl && body[j] == prev) cand = body[j + 1];
+    bool end_ok = false;
+    if (kind == 1) {
+      const bool glued = j > 0 && (flags(body[j - 1]) & 2) && (flags(t) & 1);
+      if (!glued) cand = t;
+    } else if (t == prev) {
+      const int nx = j + 1 < bl ? body[j + 1] : -1;
+      cand = nx;
+      end_ok = nx < 0 || !((flags(t) & 2) && (flags(nx) & 1));
+    }
     if (cand >= 0 && cand < fsm.V) atomicOr(&b[cand >> 5], 1u << (cand & 31));
+    if (end_ok) atomicOr(&b[sep >> 5], 1u << (sep & 31));
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const uint32_t* m = fsm.masks + (size_t)fsm.state_mask[s] * words;
-  const int sw = fsm.sep_token >> 5;
-  const uint32_t sbit = 1u << (fsm.sep_token & 31);
+  const int sw = sep >> 5;
+  const uint32_t sbit = kind == 1 ? 1u << (sep & 31) : 0u;  // an empty value: always allowed
   uint32_t* out = row_masks + (size_t)r * words;
   for (int w = lane; w < words; w += 64) out[w] = (b[w] | (w == sw ? sbit : 0u)) & m[w];
 }
@@ -570,13 +589,14 @@ int sg_fsm_commit(const void* best, const int* row_map, const void* masks, const
 // last emitted token prev_tok[r], its prompt ids body_buf[row_slot[r]]; row_masks
 // [n][V/32].  Rows whose state is not a copy state are left untouched.
 int sg_copy_masks(const void* masks, const int* state_mask, int sep_token, int V, const int* copy_kind,
-                  const int* row_state, const int* prev_tok, const int* row_slot, const int* body_buf,
-                  const int* body_len, int LB, int n, void* row_masks, hipStream_t stream) {
-  if (V % 32 || V / 32 > COPY_MAX_WORDS || LB <= 0 || sep_token < 0 || sep_token >= V) return -1;
+                  const void* tok_flags, const int* row_state, const int* prev_tok, const int* row_slot,
+                  const int* body_buf, const int* body_len, int LB, int n, void* row_masks, hipStream_t stream) {
+  if (V % 32 || V / 32 > COPY_MAX_WORDS || LB <= 0 || sep_token < 0 || sep_token >= V || !tok_flags) return -1;
   if (n == 0) return 0;
   const FsmTables f = make_fsm(masks, state_mask, nullptr, nullptr, nullptr, nullptr, 0, sep_token, 0, V);
-  hipLaunchKernelGGL(copy_mask_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, f, copy_kind, row_state, prev_tok,
-                     row_slot, body_buf, body_len, LB, n, (uint32_t*)row_masks);
+  hipLaunchKernelGGL(copy_mask_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, f, copy_kind,
+                     (const uint8_t*)tok_flags, row_state, prev_tok, row_slot, body_buf, body_len, LB, n,
+                     (uint32_t*)row_masks);
   return (int)hipGetLastError();
 }
 

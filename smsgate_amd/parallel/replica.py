@@ -62,14 +62,15 @@ def spawn_parser_workers(n: int, rank: int, cfg: Dict[str, Any]) -> Tuple[List[A
     return procs, conns
 
 
-def _payload_bytes(n: int, seed: int, vocab_name: str = "heldout") -> List[bytes]:
+def _payload_bytes(n: int, seed: int, vocab_name: str = "heldout", traffic: str = "mixed") -> List[bytes]:
     """Synthetic phone posts (the gateway's ``RawSMSPayload``); ``vocab_name``
-    picks the merchant / city vocabulary (held-out = never seen in training)."""
+    picks the merchant / city vocabulary (held-out = never seen in training),
+    ``traffic`` the mix of message kinds (utils.synth.TRAFFIC_KINDS)."""
     from ..services.gateway import RawSMSPayload
-    from ..utils.synth import generate
+    from ..utils.synth import TRAFFIC_KINDS, generate
 
     out = []
-    for s in generate(n, seed=seed, vocab_name=vocab_name):
+    for s in generate(n, seed=seed, vocab_name=vocab_name, kinds=TRAFFIC_KINDS[traffic]):
         p = RawSMSPayload(device_id="bench", message=s.body, sender="BANK", timestamp=s.timestamp, source="device")
         out.append(p)
     return out  # type: ignore[return-value]
@@ -118,7 +119,8 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
             break
         if cmd["cmd"] == "prepare":
             n = int(cmd["n"])
-            prepared = [_payload_bytes(n, seed, cfg.get("vocab", "heldout")) for seed in cmd["seeds"]]
+            prepared = [_payload_bytes(n, seed, cfg.get("vocab", "heldout"), cfg.get("traffic", "mixed"))
+                        for seed in cmd["seeds"]]
             client.send_control({"event": "prepared", "w": widx})
         elif cmd["cmd"] == "go":
             c0 = dict(worker.counts)

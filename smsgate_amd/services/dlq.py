@@ -26,7 +26,7 @@ from ..obs.metrics import DLQ_REPARSE_FAILED
 from ..models.domain import RawSMS
 from ..obs.tracing import Profiler
 from ..parse.pipeline import ParsePipeline
-from ..runtime.stage import Stage
+from ..runtime.stage import Stage, dlq_publisher
 
 __all__ = ["DlqWorker", "extract_raw"]
 
@@ -67,8 +67,10 @@ class DlqWorker:
         self.log: List[Dict[str, Any]] = []
         # reparse runs under a profiler session (dlq_worker.py:70-74)
         self.profiler = Profiler("dlq_reparse")
+        # a message whose handling keeps failing (not a transient outage: those nak) ends
+        # on the terminal subject after poison_after deliveries, never silently dropped
         self.stage = Stage(bus, SUBJECT_FAILED, group, self.handle_batch, batch=batch, stats_interval=0,
-                           name="dlq_worker")
+                           name="dlq_worker", dead_letter=dlq_publisher(bus, SUBJECT_FAILED_FINAL))
 
     async def handle_batch(self, msgs: Sequence[Msg]) -> None:
         from ..services.parser import route_batch

@@ -18,6 +18,12 @@ Additions: ``GET /metrics`` (Prometheus — README.md:37 promised it, D12),
 ``POST /sms/raw/batch`` (one publish round trip for many SMS) and
 ``GET /debug/errors`` (recent captured errors).  No per-request stream
 check: the stream is ensured once at start-up (D3).
+
+Scale: concurrent ``POST /sms/raw`` requests share broker round trips
+(:class:`~smsgate_amd.bus.coalesce.PublishCoalescer`; each request still waits
+for its own PubAck before the 202), and ``gateway --workers N`` runs N
+processes on one port (uvicorn workers; :func:`default_app` is the per-process
+factory; Prometheus counters aggregated across them).
 """
 from __future__ import annotations
 
@@ -32,11 +38,12 @@ from fastapi.responses import JSONResponse, Response
 from pydantic import BaseModel
 
 from ..bus.base import SUBJECT_RAW, Bus
+from ..bus.coalesce import PublishCoalescer
 from ..models.domain import RawSMS, get_md5_hash
 from ..obs import metrics as M
 from ..obs.errors import recent_errors, sentry_capture
 
-__all__ = ["RawSMSPayload", "ShortSMSPayload", "RawSMSResponse", "create_app", "payload_to_raw"]
+__all__ = ["RawSMSPayload", "ShortSMSPayload", "RawSMSResponse", "create_app", "payload_to_raw", "default_app"]
 
 log = logging.getLogger("api_gateway")
 
@@ -83,7 +90,7 @@ BusGetter = Callable[[], Awaitable[Bus]]
 
 
 def create_app(get_bus: Optional[BusGetter] = None, *, log_dir: Optional[str] = None,
-               ensure_stream_on_start: bool = True) -> FastAPI:
+               ensure_stream_on_start: bool = True, coalesce: bool = True) -> FastAPI:
     if get_bus is None:
         from ..bus import connect
 
@@ -110,6 +117,18 @@ def create_app(get_bus: Optional[BusGetter] = None, *, log_dir: Optional[str] = 
 
     app = FastAPI(title="SMS API Gateway", version="0.1.0", lifespan=lifespan)
     app.state.get_bus = get_bus
+    coalescers: dict = {}
+
+    async def publish_one(bus: Bus, data: bytes) -> None:
+        if not coalesce:
+            await bus.publish(SUBJECT_RAW, data)
+            return
+        c = coalescers.get(id(bus))
+        if c is None or c.bus is not bus:
+            c = coalescers[id(bus)] = PublishCoalescer(bus)
+        await c.publish(SUBJECT_RAW, data)
+
+    app.state.coalescers = coalescers
 
     @app.post("/sms/raw", status_code=status.HTTP_202_ACCEPTED)
     async def post_raw_sms(payload: RawSMSPayload, request: Request) -> JSONResponse:
@@ -123,7 +142,7 @@ def create_app(get_bus: Optional[BusGetter] = None, *, log_dir: Optional[str] = 
         try:
             t0 = time.perf_counter()
             bus = await request.app.state.get_bus()
-            await bus.publish(SUBJECT_RAW, raw.model_dump_json().encode("utf-8"))
+            await publish_one(bus, raw.model_dump_json().encode("utf-8"))
             M.GATEWAY_PUBLISH_TIME.observe(time.perf_counter() - t0)
         except Exception as exc:
             sentry_capture(exc)
@@ -173,3 +192,11 @@ def create_app(get_bus: Optional[BusGetter] = None, *, log_dir: Optional[str] = 
         return recent_errors(n)
 
     return app
+
+
+def default_app() -> FastAPI:
+    """Per-process app factory of ``gateway --workers N`` (uvicorn ``factory=True``):
+    every worker process connects its own bus client from the settings."""
+    from ..config import get_settings
+
+    return create_app(log_dir=get_settings().log_dir)

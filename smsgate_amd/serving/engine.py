@@ -485,7 +485,7 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0,
                           hook=hook)
-        cm = self._copy_masks(self.state[r0:r1], tok, slot, self.copy_rows[r0:r1]) if sample else None
+        cm = self._copy_masks(self.state[r0:r1], tok, slot, self.copy_rows[r0:r1]) if sample and self.copy else None
         if sample and self.argmax:
             best = self.best[r0:r1]
             self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
@@ -575,7 +575,7 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=xp, slot_tok=xs, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0, hook=hook)
         # pseudo-row i's copy mask: its state and its input token (the draft before it)
-        cm = self._copy_masks(xst, xt, xs, self.copy_x[off:off + T]) if sample else None
+        cm = self._copy_masks(xst, xt, xs, self.copy_x[off:off + T]) if sample and self.copy else None
         if sample and self.argmax:
             # every pseudo-row masked with the state it has if its row's drafts so far are accepted
             best = self.x_best[off:off + T]

@@ -29,7 +29,8 @@ import numpy as np
 from ..models.domain import CORE_FIELDS
 from ..parse.schema import TXN_TYPES
 
-__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm", "COPY_NONE", "COPY_START", "COPY_NEXT"]
+__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm", "COPY_NONE", "COPY_START", "COPY_NEXT",
+           "TOK_STARTS_ALNUM", "TOK_ENDS_ALNUM", "token_flags"]
 
 
 @dataclass(frozen=True)
@@ -39,8 +40,10 @@ class FieldSpec:
     cap: int
     choices: Tuple[str, ...] = ()
     # copy-constrained: every value token is a token of the SMS body, and after the
-    # first one each token must follow the previous one at some body position
-    # (COPY_START / COPY_NEXT states; masks built per row by ops.copy_masks)
+    # first one each token must follow the previous one at some body position; a
+    # value starts and ends at a word boundary of the body (never inside a word
+    # split into several tokens) -- COPY_START / COPY_NEXT states, masks built per
+    # row by ops.copy_masks
     copy: bool = False
 
 
@@ -71,6 +74,20 @@ assert tuple(f.name for f in DEFAULT_FIELDS) == CORE_FIELDS
 
 # per-state copy kind (SchemaFSM.copy_kind)
 COPY_NONE, COPY_START, COPY_NEXT = 0, 1, 2
+# per-token flags (SchemaFSM.tok_flags): the token's text starts / ends with a letter or
+# digit.  Between body tokens a and b there is a word boundary unless a ends and b
+# starts alphanumeric (b then continues a's word: byte-level BPE puts the blank in b)
+TOK_STARTS_ALNUM, TOK_ENDS_ALNUM = 1, 2
+
+
+def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: int) -> np.ndarray:
+    out = np.zeros(vocab, dtype=np.uint8)
+    spec = set(specials)
+    for i, t in enumerate(token_strings[:vocab]):
+        if i in spec or not t:
+            continue
+        out[i] = (TOK_STARTS_ALNUM if t[0].isalnum() else 0) | (TOK_ENDS_ALNUM if t[-1].isalnum() else 0)
+    return out
 
 _CLASS_CHARS = {
     "date": set("0123456789.:/- "),
@@ -111,6 +128,7 @@ class SchemaFSM:
     start_state: int = 0
     field_of_state: List[int] = field(default_factory=list)
     copy_kind: Optional[np.ndarray] = None  # [S] COPY_NONE / COPY_START / COPY_NEXT
+    tok_flags: Optional[np.ndarray] = None  # [vocab] uint8 TOK_STARTS_ALNUM | TOK_ENDS_ALNUM
     # device copies (filled by to_device; consumed by ops.fsm_sample)
     masks: object = None
     state_mask: object = None
@@ -120,6 +138,7 @@ class SchemaFSM:
     enum_next_t: object = None
     forced_t: object = None
     copy_kind_t: object = None
+    tok_flags_t: object = None
 
     @property
     def has_copy(self) -> bool:
@@ -164,7 +183,18 @@ class SchemaFSM:
         self.forced_t = torch.from_numpy(self.forced).to(device)
         ck = self.copy_kind if self.copy_kind is not None else np.zeros(self.num_states, dtype=np.int32)
         self.copy_kind_t = torch.from_numpy(ck.astype(np.int32)).to(device)
+        tf = self.tok_flags if self.tok_flags is not None else np.zeros(self.vocab, dtype=np.uint8)
+        self.tok_flags_t = torch.from_numpy(tf.astype(np.uint8)).to(device)
         return self
+
+    def _boundary(self, a: int, b: int) -> bool:
+        """A word boundary between adjacent body tokens ``a`` and ``b``."""
+        tf = self.tok_flags
+        if tf is None:
+            return True
+        fa = int(tf[a]) if 0 <= a < self.vocab else 0
+        fb = int(tf[b]) if 0 <= b < self.vocab else 0
+        return not ((fa & TOK_ENDS_ALNUM) and (fb & TOK_STARTS_ALNUM))
 
     def copy_mask_host(self, state: int, prev: int, body: Sequence[int]) -> np.ndarray:
         """Reference of ops.copy_masks for one row (tests): [vocab] bool allowed tokens
@@ -175,12 +205,21 @@ class SchemaFSM:
             return allow
         cand = np.zeros(self.vocab, dtype=bool)
         if kind == COPY_START:
-            cand[[t for t in body if 0 <= t < self.vocab]] = True
+            # a value starts at a word boundary; an empty value (<sep>) is always possible
+            for j, t in enumerate(body):
+                if 0 <= t < self.vocab and (j == 0 or self._boundary(body[j - 1], t)):
+                    cand[t] = True
+            cand[self.sep_token] = True
         else:
-            for j in range(len(body) - 1):
-                if body[j] == prev and 0 <= body[j + 1] < self.vocab:
-                    cand[body[j + 1]] = True
-        cand[self.sep_token] = True
+            # continue along a body bigram; end (<sep>) only where the body has a word boundary
+            for j, t in enumerate(body):
+                if t != prev:
+                    continue
+                nxt = body[j + 1] if j + 1 < len(body) else -1
+                if 0 <= nxt < self.vocab:
+                    cand[nxt] = True
+                if nxt < 0 or self._boundary(t, nxt):
+                    cand[self.sep_token] = True
         return allow & cand
 
     def step_host(self, state: int, tok: int) -> int:
@@ -305,4 +344,5 @@ def build_fsm(tokenizer, vocab: int, fields: Sequence[FieldSpec] = DEFAULT_FIELD
         start_state=field_starts[0],
         field_of_state=field_of,
         copy_kind=np.asarray(copy_kind, dtype=np.int32),
+        tok_flags=token_flags(strings, specials, vocab),
     )

@@ -1,0 +1,41 @@
+"""Named engine configurations: ONE source of defaults for ``bench.py`` and
+``engine-server`` (and so for the compose deployment, which serves the profile
+the headline bench measured).
+
+* ``throughput`` — the headline bench's configuration: 8 192 rows, two decode
+  steps per graph, admission at 12.5 % free rows, up to six drafts per row
+  (profiles/r02s3_admit_frac_ab*.jsonl, r02s3_spec_k_ab.jsonl);
+* ``latency`` — the serving-latency configuration of round 2: 4 096 rows, four
+  steps per graph, admission at 25 % free rows, four drafts per row (p50 30 ms at
+  1 k msgs/s, profiles/r02s3_latency_spec4.json; six drafts did not lower it,
+  r02s3_latency_spec6.json).
+
+Everything not listed keeps the :class:`~smsgate_amd.serving.engine.EngineConfig`
+default.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict
+
+__all__ = ["PROFILES", "profile_kwargs", "BUCKETS"]
+
+BUCKETS = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
+
+PROFILES: Dict[str, Dict[str, Any]] = {
+    "throughput": dict(max_slots=8192, steps_per_graph=2, admit_min_fraction=0.125, spec_k=6, spec_draft_frac=1.25,
+                       buckets=BUCKETS, split_decode=4096, split_prefill=8192, copy_constrain=True),
+    "latency": dict(max_slots=4096, steps_per_graph=4, admit_min_fraction=0.25, spec_k=4, spec_draft_frac=1.25,
+                    buckets=BUCKETS[:-1], split_decode=4096, split_prefill=8192, copy_constrain=True),
+}
+
+
+def profile_kwargs(name: str, **overrides: Any) -> Dict[str, Any]:
+    """EngineConfig keyword arguments of profile ``name`` with ``overrides`` applied
+    (None values are ignored, so unset CLI flags keep the profile's value)."""
+    if name not in PROFILES:
+        raise KeyError(f"unknown engine profile {name!r} (one of {sorted(PROFILES)})")
+    kw = dict(PROFILES[name])
+    kw.update({k: v for k, v in overrides.items() if v is not None})
+    if "max_slots" in overrides and overrides["max_slots"] is not None:
+        kw["buckets"] = tuple(b for b in kw["buckets"] if b <= kw["max_slots"]) or (kw["max_slots"],)
+    return kw

@@ -208,7 +208,10 @@ class RemoteEngineClient:
         self.conn: Optional[Connection] = None
         self.reconnects = 0
         if conn is None:
-            conn = connector()  # type: ignore[misc]
+            try:
+                conn = connector()  # type: ignore[misc]
+            except OSError:  # engine not up yet: the first request connects (or naks)
+                return
         self._attach(conn)
 
     def _attach(self, conn: Connection) -> None:

@@ -22,7 +22,7 @@ import zlib
 from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
-__all__ = ["SynthSMS", "generate", "generate_bodies", "reference_cases", "vocab", "Vocab"]
+__all__ = ["SynthSMS", "generate", "generate_bodies", "reference_cases", "vocab", "Vocab", "TRAFFIC_KINDS"]
 
 # Real-looking merchant words.  The reference's golden answers (tests/test_parsers.py:11-58:
 # TEST, LLC, MOSKOW, AMERIABANK, API, GATE, AM, "TEST STR.") are deliberately absent from
@@ -208,17 +208,27 @@ def _one(r: random.Random, v: Vocab) -> SynthSMS:
     return SynthSMS(body, "funds", None, ts)
 
 
-def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "train") -> List[SynthSMS]:
+# traffic mixes (bench.py --traffic): "mixed" = every kind in its natural share (17 % are
+# skipped by the parser's keyword filter and never reach the LLM); "purchase" = debit
+# transactions only (the store-purchase and account-debit formats), every message
+# LLM-routed -- the reference's BASELINE harness timed purchase bodies only
+TRAFFIC_KINDS = {"mixed": None, "purchase": ("purchase", "account")}
+
+
+def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "train",
+             kinds: Optional[Sequence[str]] = None) -> List[SynthSMS]:
     """``n`` messages; with ``unique`` every body is distinct (defeats the response cache).
     ``vocab_name``: ``"train"`` (what the extractor is trained on) or ``"heldout"`` —
     merchant / city / street names disjoint from the training pools (held-out scoring
-    and the benchmark's traffic)."""
+    and the benchmark's traffic).  ``kinds``: keep only these message kinds."""
     r = random.Random(seed)
     v = vocab(vocab_name)
     out: List[SynthSMS] = []
     seen = set()
     while len(out) < n:
         s = _one(r, v)
+        if kinds is not None and s.kind not in kinds:
+            continue
         if unique:
             if s.body in seen:
                 continue

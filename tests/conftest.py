@@ -35,6 +35,9 @@ def _isolate_settings(tmp_path, monkeypatch):
 
     monkeypatch.setenv("BACKUP_DIR", str(tmp_path / "backups"))
     monkeypatch.setenv("LOG_DIR", str(tmp_path / "logs"))
+    # the parse pipeline's response cache: one per test (a shared file would let one
+    # test's cached answer skip another test's backend call)
+    monkeypatch.setenv("PARSER_CACHE_PATH", str(tmp_path / "parser_cache.sqlite"))
     config.reset_settings()
     from smsgate_amd import bus
 

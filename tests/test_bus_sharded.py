@@ -36,3 +36,46 @@ def test_publish_subscribe_ack_across_shards(arun):
     assert got == [b'"r1"', b'"r2"'] and info.num_ack_pending == 0 and info.num_pending == 0
     assert on_a == [] and on_b == ["p1"] and raw_b == []  # each subject lives on exactly one shard
     assert st.messages == 4
+
+
+def test_pinned_layout_and_partitioned_subject(arun):
+    """``sms.raw`` partitioned over two brokers: publishes are dealt over both, one
+    durable name on each, a subscription drains both, consumer_info sums them; the
+    other subjects follow their pins / the default member."""
+    from smsgate_amd.bus.sharded import Router, parse_members
+
+    dsns, pins, default = parse_members("sms.raw=memory://r0,sms.raw=memory://r1,sms.parsed=memory://p,*=memory://d")
+    assert dsns == ["memory://r0", "memory://r1", "memory://p", "memory://d"]
+    assert pins == {"sms.raw": [0, 1], "sms.parsed": [2]} and default == [3]
+    assert parse_members("memory://a,memory://b")[1] == {}  # positional
+    rt = Router(4, pins, default)
+    assert rt.members(SUBJECT_PROCESSING) == [3] and rt.members(SUBJECT_RAW) == [0, 1]
+    r0, r1, p, d = (MemoryBus() for _ in range(4))
+    bus = ShardedBus([r0, r1, p, d], pins, default)
+
+    async def go():
+        await bus.ensure_stream()
+        await bus.publish_many([(SUBJECT_RAW, f'"r{i}"'.encode()) for i in range(10)])
+        await bus.publish(SUBJECT_PARSED, b'"p"')
+        await bus.publish(SUBJECT_FAILED, b'"f"')
+        sub = await bus.subscribe(SUBJECT_RAW, "parser_worker")
+        first = await sub.fetch(4, 0.05)
+        info_mid = await bus.consumer_info("SMS", "parser_worker")
+        rest = []
+        while True:
+            got = await sub.fetch(4, 0.05)
+            if not got:
+                break
+            rest += got
+        for m in first + rest:
+            await m.ack()
+        info = await bus.consumer_info("SMS", "parser_worker")
+        empty = await sub.fetch(4, 0.05)  # blocking path over both partitions, times out
+        per = [(await r.stream_info("SMS")).messages for r in (r0, r1, p, d)]
+        return first, rest, info_mid, info, empty, per
+
+    first, rest, info_mid, info, empty, per = arun(go())
+    assert sorted(m.data for m in first + rest) == sorted(f'"r{i}"'.encode() for i in range(10))
+    assert info_mid.num_ack_pending == 4 and info_mid.num_pending == 6
+    assert info.num_ack_pending == 0 and info.num_pending == 0 and empty == []
+    assert per == [5, 5, 1, 1]  # raw dealt over both partitions; parsed pinned; failed on the default

@@ -40,16 +40,19 @@ def test_host_mask_semantics(tk_fsm):
     body = tk.message_ids([normalize_body(REFERENCE_CASES[0][0])], 128)[0]
     merchant = fsm.fields.index(next(f for f in fsm.fields if f.name == "merchant"))
     s0 = next(s for s in range(fsm.num_states) if fsm.field_of_state[s] == merchant)
-    m0 = fsm.copy_mask_host(s0, tk.sep, body)
-    allowed_body = {t for t in body if fsm.allowed[s0, t]}
-    assert set(m0.nonzero()[0]) == allowed_body | {tk.sep}
-    # after " T" (twice in the body: " T EST L..." and " T EST STR") only "EST" may follow
-    t = tk.encode(" T")[0]
-    m1 = fsm.copy_mask_host(s0 + 1, t, body)
-    assert set(m1.nonzero()[0]) == {tk.encode("EST")[0], tk.sep}
-    # a token absent from the body: only <sep> (the value must end)
+    m0 = set(fsm.copy_mask_host(s0, tk.sep, body).nonzero()[0])
+    t_, est = tk.encode(" T")[0], tk.encode("EST")[0]
+    # a value starts at a word boundary: " T" may start one, "EST" (always inside "TEST") may not
+    assert t_ in m0 and est not in m0 and tk.sep in m0
+    assert m0 <= {t for t in body if fsm.allowed[s0, t]} | {tk.sep}
+    # after " T" only "EST" may follow -- and the value may not end inside the word
+    assert set(fsm.copy_mask_host(s0 + 1, t_, body).nonzero()[0]) == {est}
+    # after "EST" the word is complete: " L" / " STR" / "," continue or <sep> ends it
+    after = set(fsm.copy_mask_host(s0 + 1, est, body).nonzero()[0])
+    assert tk.sep in after and tk.encode(" L")[0] in after
+    # a token absent from the body: nothing (the kernels then fall back to <sep>)
     absent = next(i for i in range(fsm.vocab) if i not in body and fsm.allowed[s0 + 1, i])
-    assert set(fsm.copy_mask_host(s0 + 1, absent, body).nonzero()[0]) == {tk.sep}
+    assert not fsm.copy_mask_host(s0 + 1, absent, body).any()
     # non-copy state: the schema mask unchanged
     assert (fsm.copy_mask_host(fsm.start_state, 0, body) == fsm.allowed[fsm.start_state]).all()
 

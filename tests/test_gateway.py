@@ -18,6 +18,9 @@ class _DownBus(MemoryBus):
     async def publish(self, *a, **k):
         raise ConnectionError("bus down")
 
+    async def publish_many(self, *a, **k):
+        raise ConnectionError("bus down")
+
 
 @pytest.fixture
 def bus():
@@ -129,3 +132,34 @@ def test_batch_and_metrics(client, bus, valid_payload, arun):
 
     got = arun(read())
     assert [json.loads(x.data)["body"] for x in got] == ["msg 0", "msg 1", "msg 2"]
+
+
+def test_concurrent_posts_share_round_trips(bus, valid_payload, arun):
+    """Concurrent POST /sms/raw requests are coalesced into publish_many round trips;
+    every request still gets its own 202 only after its message is on the bus."""
+    import asyncio
+
+    import httpx
+
+    async def get_bus():
+        return bus
+
+    app = create_app(get_bus, ensure_stream_on_start=False)
+
+    async def go():
+        async with httpx.AsyncClient(transport=httpx.ASGITransport(app=app), base_url="http://gw") as c:
+            async def one(i):
+                p = dict(valid_payload)
+                p["message"] = f"concurrent {i}"
+                return await c.post("/sms/raw", json=p)
+
+            rs = await asyncio.gather(*(one(i) for i in range(200)))
+        sub = await bus.subscribe(SUBJECT_RAW, "check")
+        got = await sub.fetch(500, 0.1)
+        return rs, got
+
+    rs, got = arun(go())
+    assert all(r.status_code == 202 and r.json() == {"result": "queued"} for r in rs)
+    assert sorted(json.loads(m.data)["body"] for m in got) == sorted(f"concurrent {i}" for i in range(200))
+    (co,) = app.state.coalescers.values()
+    assert co.published == 200 and co.round_trips < 200

@@ -284,3 +284,48 @@ def test_remote_client_request_timeout_is_transient(arun):
         arun(client.extract(["x"]))
     assert not client._pending
     s.close()
+
+
+def test_dlq_reparse_through_engine_server(arun, tmp_path):
+    """`dlq --reparse --engine unix://...` (VERDICT r02 missing #2): a shape-(c)
+    envelope is re-parsed by the engine-server to sms.parsed; while the engine is
+    down the batch is nak'ed (transient) -- never terminated or dropped."""
+    import asyncio
+    import json
+    import threading
+
+    from smsgate_amd.cli import _pipeline
+    from smsgate_amd.config import get_settings
+    from smsgate_amd.serving.echo import EchoEngine
+    from smsgate_amd.serving.remote import EngineServer
+    from smsgate_amd.services.dlq import DlqWorker
+    from smsgate_amd.services.gateway import RawSMSPayload, payload_to_raw
+
+    path = tmp_path / "engine.sock"
+    raw = payload_to_raw(RawSMSPayload(device_id="d", message=REFERENCE_CASES[0][0], sender="BANK",
+                                       timestamp=1746541380, source="device"))
+
+    async def go():
+        bus = MemoryBus()
+        w = DlqWorker(bus, _pipeline(get_settings(), "local_llm", f"unix://{path}"), reparse=True, batch=8)
+        w.stage.nak_delay = 0.05
+        await bus.publish(SUBJECT_FAILED, json.dumps({"reason": "unmatched", "raw": raw.model_dump()}).encode())
+        await _pump(w.stage, rounds=8)  # no engine yet: transient, nak'ed, still pending
+        down = (w.stage.transient_errors, w.stage.dead_lettered, w.reparse_failed)
+        stop = threading.Event()
+        th = threading.Thread(target=EngineServer(EchoEngine()).serve_listener, args=(str(path), stop), daemon=True)
+        th.start()
+        for _ in range(200):
+            if path.exists():
+                break
+            await asyncio.sleep(0.01)
+        await _pump(w.stage, rounds=40)
+        stop.set()
+        await asyncio.to_thread(th.join, 5)
+        info = await bus.consumer_info("SMS", "parser_worker_dlq")
+        return w, down, info, await drain(bus, SUBJECT_PARSED)
+
+    w, down, info, parsed = arun(go())
+    assert down[0] >= 1 and down[1] == 0 and down[2] == 0
+    assert [p["msg_id"] for p in parsed] == [raw.msg_id] and w.reparsed == 1
+    assert info.num_pending == 0 and info.num_ack_pending == 0

@@ -98,7 +98,22 @@ def _client(port: int, conns: int, path: str, batch: int, seconds: float, seed: 
     q.put(counts)
 
 
+def _phase_native(port, args, path, batch):
+    from smsgate_amd.native.build import BUSLOAD
+
+    conns = args.clients * args.conns
+    cmd = [str(BUSLOAD), "--http", str(port), "--conns", str(conns), "--seconds", str(args.seconds),
+           "--depth", str(args.depth)] + (["--batch", str(batch)] if batch > 1 else [])
+    out = json.loads(subprocess.run(cmd, capture_output=True, text=True, timeout=args.seconds + 120).stdout)
+    return {"endpoint": path, "batch": batch, "msgs": int(round(out["msgs_per_s"] * out["seconds"])),
+            "requests_202": out["requests_202"], "requests_other": out["requests_other"],
+            "msgs_per_s": out["msgs_per_s"], "requests_per_s": out["requests_per_s"], "wall_s": out["seconds"],
+            "loadgen": "smsgate-busload --http", "conns": conns, "depth": args.depth}
+
+
 def _phase(port, args, path, batch):
+    if args.loadgen == "native":
+        return _phase_native(port, args, path, batch)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_client, args=(port, args.conns, path, batch, args.seconds, c, q))
@@ -125,6 +140,9 @@ def main() -> int:
     p.add_argument("--seconds", type=float, default=8.0)
     p.add_argument("--batch", type=int, default=100)
     p.add_argument("--mode", default="python", choices=["python", "native"])
+    p.add_argument("--loadgen", default="python", choices=["python", "native"],
+                   help="native: smsgate-busload --http (C++ threads, one keep-alive connection each)")
+    p.add_argument("--depth", type=int, default=1, help="native load generator: pipelined requests per connection")
     a = p.parse_args()
     from smsgate_amd.bus.sync_client import SyncBusClient
     from smsgate_amd.native import spawn_busd
@@ -166,8 +184,10 @@ def main() -> int:
                 gw.kill()
         broker.stop()
     acked = single["msgs"] + batch["msgs"]
+    if a.loadgen == "native":  # (msgs derived from a rate: compare with a small tolerance)
+        acked = single["requests_202"] + batch["requests_202"] * a.batch
     out = {"bench": "gateway_ingest", "mode": a.mode, "workers": 0 if native else a.workers, "client_procs": a.clients,
-           "conns_per_client": a.conns, "seconds": a.seconds, "single": single, "batch": batch,
+           "conns_per_client": a.conns, "loadgen": a.loadgen, "seconds": a.seconds, "single": single, "batch": batch,
            "broker_stored": stored, "acked": acked, "lossless": stored >= acked,
            "cpus": os.cpu_count(), "note": "gateway, broker and load generator share the same CPUs"}
     print(json.dumps(out), flush=True)

@@ -149,7 +149,7 @@ class BusServer:
 
 async def serve(listen: str, data_dir: Optional[str], stop: Optional[asyncio.Event] = None,
                 max_age: float = 3 * 24 * 3600.0, nats_listen: Optional[str] = None,
-                native: bool = False) -> BusServer:
+                native: bool = False, http_listen: Optional[str] = None) -> BusServer:
     """One journaled engine behind the msgpack protocol (``listen``) and, optionally,
     the NATS wire protocol (``nats_listen``, :mod:`.nats_server`).
 
@@ -157,10 +157,13 @@ async def serve(listen: str, data_dir: Optional[str], stop: Optional[asyncio.Eve
     protocol and journal format, its own NATS front-end) as a child process
     instead; the returned object has the same ``close()``.
     """
+    if http_listen and not native:
+        raise ValueError("--http-listen (native HTTP ingestion) needs --native")
     if native:
         from ..native import spawn_busd
 
-        broker = spawn_busd(listen, data_dir, max_age=max_age, nats_listen=nats_listen or None)
+        broker = spawn_busd(listen, data_dir, max_age=max_age, nats_listen=nats_listen or None,
+                            http_listen=http_listen or None)
         if stop is not None:
             await stop.wait()
             await broker.close()

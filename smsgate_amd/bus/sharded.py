@@ -47,14 +47,23 @@ from .base import (
     Subscription,
 )
 
-__all__ = ["ShardedBus", "shard_of", "parse_members", "Router", "NODE_PARTITIONS", "node_layout"]
+__all__ = ["ShardedBus", "shard_of", "parse_members", "Router", "NODE_PARTITIONS", "node_layout", "node_partitions"]
 
 # The 8-GPU node's broker layout (deploy/docker-compose.yml, bench.py): the two
-# consumed per-SMS subjects each partitioned over two brokers, everything else
-# (sms.processing -- published, consumed outside the pipeline -- and the low-rate
-# subjects) on one more; tests/test_broker_capacity.py sizes each broker against
-# the latest measured headline.
-NODE_PARTITIONS = {SUBJECT_RAW: 2, SUBJECT_PARSED: 2}
+# consumed per-SMS subjects partitioned -- sms.raw over six brokers, each also a
+# native HTTP ingest front door (smsgate-busd --http-listen: ~56 k single-SMS
+# requests/s each, profiles/r03_ingest_bench.jsonl), sms.parsed over two --
+# everything else (sms.processing -- published, consumed outside the pipeline --
+# and the low-rate subjects) on one more.  tests/test_broker_capacity.py and
+# tests/test_deploy.py size each broker, and the ingest front doors, against the
+# latest measured headline.  Fewer GPUs on a node: node_partitions() scales it down.
+NODE_PARTITIONS = {SUBJECT_RAW: 6, SUBJECT_PARSED: 2}
+NODE_GPUS = 8
+
+
+def node_partitions(gpus: int = NODE_GPUS) -> Dict[str, int]:
+    """The node layout sized for ``gpus`` GPUs (same per-broker load as the 8-GPU node)."""
+    return {s: max(1, -(-n * gpus // NODE_GPUS)) for s, n in NODE_PARTITIONS.items()}
 
 
 def node_layout(dsns: Sequence[str], partitions: Optional[Dict[str, int]] = None) -> str:

@@ -159,7 +159,7 @@ async def _run_bus_server(a, settings) -> None:
 
     native = getattr(a, "native", False)
     await serve(a.listen, a.data, _stop_event(), max_age=settings.stream_max_age_s,
-                nats_listen=a.nats_listen, native=native)
+                nats_listen=a.nats_listen, native=native, http_listen=a.http_listen)
 
 
 async def _run_pipeline(a, settings) -> None:
@@ -329,6 +329,8 @@ def build_parser() -> argparse.ArgumentParser:
     bp.add_argument("--data", default="./.bus-data")
     bp.add_argument("--native", action="store_true",
                     help="run the C++ broker (smsgate-busd: msgpack + NATS protocols, same journal format)")
+    bp.add_argument("--http-listen", default="",
+                    help="with --native: native HTTP ingestion (POST /sms/raw, /sms/raw/batch, /health, /metrics)")
     ep = sp.add_parser("engine-server")
     ep.add_argument("--listen", default="unix:///tmp/smsgate-engine0.sock")
     ep.add_argument("--model", default=None, help="default: LLM_MODEL (smollm-135m)")
@@ -389,14 +391,11 @@ def main(argv: Optional[List[str]] = None) -> int:
         workers = a.workers or int(os.getenv("GATEWAY_WORKERS", "1"))
         try:
             if workers > 1:
-                # N processes on one port (uvicorn workers), each with its own bus client;
-                # Prometheus counters aggregated across them (obs.metrics.render_latest)
-                import tempfile
+                # N processes on one port (SO_REUSEPORT), each with its own bus client;
+                # Prometheus counters aggregated across them (services/gateway_runner.py)
+                from .services.gateway_runner import serve_workers
 
-                os.environ.setdefault("PROMETHEUS_MULTIPROC_DIR",
-                                      tempfile.mkdtemp(prefix="smsgate-gw-metrics-"))
-                uvicorn.run("smsgate_amd.services.gateway:default_app", factory=True, workers=workers,
-                            host=settings.api_host or "0.0.0.0", port=port, log_level="warning")
+                serve_workers(workers, settings.api_host or "0.0.0.0", port)
             else:
                 uvicorn.run(create_app(log_dir=settings.log_dir), host=settings.api_host or "0.0.0.0", port=port)
         finally:

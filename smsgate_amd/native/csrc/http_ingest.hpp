@@ -32,19 +32,26 @@ class Md5 {
  public:
   static std::string hex(const std::string& data) {
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    std::string m = data;
-    const uint64_t bits = (uint64_t)data.size() * 8u;
-    m.push_back((char)0x80);
-    while (m.size() % 64 != 56) m.push_back('\0');
-    for (int i = 0; i < 8; ++i) m.push_back((char)((bits >> (8 * i)) & 0xff));
-    for (size_t off = 0; off < m.size(); off += 64) block(h, (const unsigned char*)m.data() + off);
+    const size_t n = data.size();
+    const unsigned char* p = (const unsigned char*)data.data();
+    size_t off = 0;
+    for (; off + 64 <= n; off += 64) block(h, p + off);  // whole blocks in place
+    unsigned char tail[128] = {0};                       // the rest + padding + bit length
+    const size_t rem = n - off;
+    memcpy(tail, p + off, rem);
+    tail[rem] = 0x80;
+    const size_t tl = rem + 1 + 8 <= 64 ? 64 : 128;
+    const uint64_t bits = (uint64_t)n * 8u;
+    for (int i = 0; i < 8; ++i) tail[tl - 8 + i] = (unsigned char)((bits >> (8 * i)) & 0xff);
+    block(h, tail);
+    if (tl == 128) block(h, tail + 64);
     static const char* hx = "0123456789abcdef";
-    std::string out;
+    std::string out(32, '0');
     for (int i = 0; i < 4; ++i)
       for (int b = 0; b < 4; ++b) {
         const unsigned v = (h[i] >> (8 * b)) & 0xff;
-        out.push_back(hx[v >> 4]);
-        out.push_back(hx[v & 15]);
+        out[8 * i + 2 * b] = hx[v >> 4];
+        out[8 * i + 2 * b + 1] = hx[v & 15];
       }
     return out;
   }

@@ -22,8 +22,42 @@ def test_compose_is_an_8_gpu_node():
     assert {p["command"][p["command"].index("--group") + 1] for p in parsers} == {"parser_worker"}
     assert {p["command"][p["command"].index("--engine") + 1] for p in parsers} == socks
     dsn = parsers[0]["environment"]["NATS_DSN"]
-    assert dsn.startswith("sharded+") and dsn.count(",") == 2
-    assert all("--native" in svc[b]["command"] for b in ("broker-raw", "broker-parsed", "broker-proc"))
+    assert dsn.startswith("sharded+")
+    brokers = [k for k in svc if k.startswith("broker-") and "profiles" not in svc[k]]
+    assert all("--native" in svc[b]["command"] for b in brokers)
+
+
+def test_broker_layout_is_the_node_layout():
+    """compose's NATS_DSN is bus/sharded.py's node layout over the compose brokers."""
+    from smsgate_amd.bus.sharded import NODE_PARTITIONS, Router, parse_members
+
+    svc = yaml.safe_load(open(os.path.join(ROOT, "deploy", "docker-compose.yml")))["services"]
+    dsn = svc["parser0"]["environment"]["NATS_DSN"]
+    dsns, pins, default = parse_members(dsn[len("sharded+"):])
+    assert {s: len(v) for s, v in pins.items()} == NODE_PARTITIONS and len(default) == 1
+    hosts = [d.split("://")[1].split(":")[0] for d in dsns]
+    assert len(set(hosts)) == len(hosts) and set(hosts) <= set(svc)
+    rt = Router(len(dsns), pins, default)
+    for h, k in zip(hosts, range(len(dsns))):  # every broker listens where the DSN points
+        port = dsns[k].rsplit(":", 1)[1]
+        assert f"tcp://0.0.0.0:{port}" in svc[h]["command"], h
+    assert all(hosts[k].startswith("broker-raw") for k in rt.members("sms.raw"))
+
+
+def test_ingest_front_doors_cover_the_node_rate():
+    """The raw partitions' native HTTP front doors, at their measured single-SMS rate
+    (profiles/r03_ingest_bench.jsonl), take at least 8 x the latest BENCH headline."""
+    import json
+
+    from test_broker_capacity import latest_headline
+
+    svc = yaml.safe_load(open(os.path.join(ROOT, "deploy", "docker-compose.yml")))["services"]
+    doors = [k for k, v in svc.items() if "--http-listen" in (v.get("command") or [])]
+    assert len(doors) >= 6 and all(k.startswith("broker-raw") for k in doors)
+    recs = [json.loads(x) for x in open(os.path.join(ROOT, "profiles", "r03_ingest_bench.jsonl"))]
+    native = [r["single"]["requests_per_s"] for r in recs if r["mode"] == "native" and r.get("lossless")]
+    per_door = sorted(native)[len(native) // 2]  # median of the measured runs
+    assert len(doors) * per_door >= 8 * latest_headline(), (len(doors), per_door, latest_headline())
 
 
 def _env_example():

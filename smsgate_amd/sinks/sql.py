@@ -24,11 +24,25 @@ __all__ = ["SqlSink", "make_engine"]
 
 
 def make_engine(url: str, **kw: Any) -> Engine:
+    """SQLAlchemy engine; a file-backed SQLite database runs in WAL mode with
+    ``synchronous=NORMAL`` (readers -- MCP tools, the notifier -- never block the
+    writer, and a commit costs no fsync of the main file: scripts/sink_bench.py)."""
     if url.startswith("sqlite"):
         kw.setdefault("connect_args", {"check_same_thread": False})
     else:
         kw.setdefault("pool_size", 10)  # db/session.py:9
-    return create_engine(url, **kw)
+    eng = create_engine(url, **kw)
+    if url.startswith("sqlite") and ":memory:" not in url and url not in ("sqlite://", "sqlite:///"):
+        from sqlalchemy import event
+
+        @event.listens_for(eng, "connect")
+        def _wal(dbapi_conn, _record):  # noqa: ANN001
+            cur = dbapi_conn.cursor()
+            cur.execute("PRAGMA journal_mode=WAL")
+            cur.execute("PRAGMA synchronous=NORMAL")
+            cur.close()
+
+    return eng
 
 
 def _insert_for(engine: Engine):
@@ -48,6 +62,12 @@ class SqlSink(Sink):
         self.url = url
         self.engine = engine or make_engine(url)
         self._insert = _insert_for(self.engine)
+        stmt = self._insert(sms_data)
+        # the columns every row carries (parsed_to_row), so executemany binds all of them
+        self._upsert_stmt = stmt.on_conflict_do_update(
+            index_elements=["msg_id"],
+            set_={c.name: stmt.excluded[c.name] for c in sms_data.columns if c.name not in UPSERT_EXCLUDED},
+        )
         if migrate:
             migrations.upgrade(self.engine)
 
@@ -55,17 +75,15 @@ class SqlSink(Sink):
     def upsert_rows_sync(self, rows: List[Dict[str, Any]]) -> None:
         if not rows:
             return
-        # Deduplicate inside one statement (ON CONFLICT can't touch a row twice).
+        # Deduplicate inside one batch (ON CONFLICT can't touch a row twice in one statement).
         by_id: Dict[Any, Dict[str, Any]] = {}
         for r in rows:
             by_id[r["msg_id"]] = r
-        stmt = self._insert(sms_data).values(list(by_id.values()))
-        stmt = stmt.on_conflict_do_update(
-            index_elements=["msg_id"],
-            set_={c.name: stmt.excluded[c.name] for c in sms_data.columns if c.name not in UPSERT_EXCLUDED},
-        )
+        # one compiled statement, executed with the batch as parameter sets (DBAPI
+        # executemany / SQLAlchemy insertmanyvalues): compiling a VALUES list of 512 rows
+        # per batch cost ~0.3 ms per row on SQLite (3 k rows/s, scripts/sink_bench.py)
         with self.engine.begin() as conn:
-            conn.execute(stmt)
+            conn.execute(self._upsert_stmt, list(by_id.values()))
 
     async def upsert_many(self, records: Sequence[ParsedSMS]) -> None:
         rows = [parsed_to_row(r) for r in records]

@@ -14,12 +14,56 @@ class FakePocketBase:
     """Enough of the PocketBase REST API: superuser auth, list with ``msg_id=`` /
     ``datetime >`` filters + sort + pagination, create, patch."""
 
-    def __init__(self, email: str = "a@b.c", password: str = "pw", fail_first: int = 0) -> None:
+    def __init__(self, email: str = "a@b.c", password: str = "pw", fail_first: int = 0,
+                 batch_enabled: bool = False, unique_msg_id: bool = True) -> None:
         self.email, self.password = email, password
         self.cols: Dict[str, List[Dict[str, Any]]] = {}
         self.calls: List[str] = []
         self.fail_first = fail_first
+        self.batch_enabled = batch_enabled  # PocketBase >= 0.23 batch API (off by default there too)
+        self.unique_msg_id = unique_msg_id  # deploy/pb_schema.json: unique msg_id index
         self._n = 0
+        self._idx: Dict[str, Dict[str, Any]] = {}
+
+    def _batch(self, req: httpx.Request) -> httpx.Response:
+        """POST /api/batch: all-or-nothing; PUT = upsert by the body's id."""
+        if not self.batch_enabled:
+            return httpx.Response(403, json={"message": "Batch requests are not allowed."})
+        reqs = json.loads(req.content)["requests"]
+        plan = []  # validate everything first (all-or-nothing), then apply
+        seen_msg = {}
+        for r in reqs:
+            col = re.match(r"/api/collections/([^/]+)/records", r["url"]).group(1)
+            items = self.cols.setdefault(col, [])
+            idx = self._index(col)
+            body = dict(r["body"])
+            hit = idx["id"].get(body["id"])
+            if hit is None and self.unique_msg_id:
+                owner = idx["msg"].get(body.get("msg_id"), seen_msg.get((col, body.get("msg_id"))))
+                if owner is not None and owner != body["id"]:
+                    return httpx.Response(400, json={"message": "msg_id: value must be unique"})
+            seen_msg[(col, body.get("msg_id"))] = body["id"]
+            plan.append((col, items, idx, hit, body))
+        for col, items, idx, hit, body in plan:
+            if hit is None:
+                hit = idx["id"].get(body["id"])
+            if hit is None:
+                items.append(body)
+                idx["id"][body["id"]] = body
+            else:
+                hit.update(body)
+            idx["msg"][body.get("msg_id")] = body["id"]
+        return httpx.Response(200, json=[{"status": 200, "body": b} for *_, b in plan])
+
+    def _index(self, col):
+        """id -> record and msg_id -> id of a collection (rebuilt if the list was replaced)."""
+        items = self.cols.setdefault(col, [])
+        idx = self._idx.get(col)
+        if idx is None or idx["list"] is not items or idx["n"] != len(items):
+            idx = {"list": items, "n": len(items), "id": {r["id"]: r for r in items},
+                   "msg": {r.get("msg_id"): r["id"] for r in items}}
+            self._idx[col] = idx
+        return idx
 
     def transport(self) -> httpx.MockTransport:
         return httpx.MockTransport(self.handle)
@@ -30,6 +74,8 @@ class FakePocketBase:
         if self.fail_first > 0 and "/records" in path:
             self.fail_first -= 1
             return httpx.Response(503, json={"message": "unavailable"})
+        if path == "/api/batch":
+            return self._batch(req)
         if path.endswith("auth-with-password"):
             body = json.loads(req.content)
             if body == {"identity": self.email, "password": self.password}:
@@ -46,7 +92,9 @@ class FakePocketBase:
             sel = items
             fm = re.match(r"msg_id='(.*)'", flt)
             if fm:
-                sel = [r for r in items if r.get("msg_id") == fm.group(1)]
+                idx = self._index(col)
+                rid_ = idx["msg"].get(fm.group(1))
+                sel = [idx["id"][rid_]] if rid_ is not None else []
             fm = re.match(r"datetime > '(.*)'", flt)
             if fm:
                 sel = [r for r in items if str(r.get("datetime", "")) > fm.group(1)]
@@ -60,14 +108,18 @@ class FakePocketBase:
             rec = json.loads(req.content)
             self._n += 1
             rec["id"] = f"r{self._n}"
+            idx = self._index(col)
             items.append(rec)
+            idx["id"][rec["id"]] = rec
+            idx["msg"][rec.get("msg_id")] = rec["id"]
+            idx["n"] = len(items)
             return httpx.Response(200, json=rec)
         if req.method == "PATCH":
-            for r in items:
-                if r["id"] == rid:
-                    r.update(json.loads(req.content))
-                    return httpx.Response(200, json=r)
-            return httpx.Response(404)
+            r = self._index(col)["id"].get(rid)
+            if r is None:
+                return httpx.Response(404)
+            r.update(json.loads(req.content))
+            return httpx.Response(200, json=r)
         return httpx.Response(405)
 
 

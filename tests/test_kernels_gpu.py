@@ -434,3 +434,113 @@ def test_attn_spec_matches_grouped_bitwise(P0, max_q):
         torch.testing.assert_close(out_s[t].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)
     with pytest.raises(ValueError):
         ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=11)
+
+
+# ---------------------------------------------------------------- operating points
+# The headline bench runs the GEMMs at thousands of rows (decode halves of 4096 rows
+# plus their drafts: ~9 216 pseudo-rows; prefill halves up to 16 384 tokens).  The
+# kernels' multi-tile paths only run there: cfg 20 (persistent 256x256 SwiGLU) walks
+# several tiles per block only once T > 256 tiles, i.e. from ~6 144 rows on.
+
+@pytest.mark.parametrize("M", [6144, 9216, 16384])
+@pytest.mark.parametrize("producer", [False, True])
+def test_gemm_swiglu_persistent_operating_points(M, producer):
+    """cfg 20 at bench-scale row counts: the persistent path that stages the next tile's
+    first K-tile (and x² partials) inside the current tile's last K-tile, vs the fp32
+    reference and vs the one-tile-per-block 128x128 kernel."""
+    K, I = 576, 1536
+    a = _bf(M, K, seed=71)
+    gu = _bf(2 * I, K, scale=K ** -0.5, seed=72)
+    nw = _bf(K, scale=0.1, seed=73) + 1
+    w = ops.interleave_gate_up(ops.fold_norm(gu, nw))
+    ss = None
+    if producer:  # the partials a residual GEMM would write (NORM 2)
+        ss = ops.ss_buffer(M, DEV)
+        parts = a.float().pow(2).reshape(M, 9, 64).sum(-1).t()
+        ss[:9, :M] = parts
+    out = ops.gemm(a, w, epi="swiglu", norm_eps=1e-5, cfg=20, ss_in=ss)
+    assert ops.gemm_cfg(M, 2 * I, epi="swiglu", K=K) == 20  # what the engine launches at these rows
+    ref = ops.ref_gemm(a, gu, epi="swiglu", norm_eps=1e-5, norm_w=nw)
+    rows = torch.randperm(M, generator=torch.Generator().manual_seed(M))[:512].to(DEV)  # fp32 reference on a sample
+    torch.testing.assert_close(out.float()[rows], ref[rows], atol=3e-2, rtol=3e-2)
+    base = ops.gemm(a, w, epi="swiglu", norm_eps=1e-5, cfg=0, ss_in=ss)
+    torch.testing.assert_close(out.float(), base.float(), atol=2e-2, rtol=2e-2)
+
+
+def _measured_cases():
+    out = []
+    for (epi, N, K), ranges in sorted(ops.GEMM_MEASURED.items()):
+        for lo, hi, cfg in ranges:
+            out.append((epi, N, K, cfg, min(hi, (lo + hi) // 2 if hi < (1 << 20) else lo + 2048)))
+    return out
+
+
+@pytest.mark.parametrize("epi,N,K,cfg,M", _measured_cases())
+def test_gemm_measured_exceptions_in_range(epi, N, K, cfg, M):
+    """Every tile exception of ops.GEMM_MEASURED at a row count inside its measured
+    range (the configuration the engine really launches there) vs fp32."""
+    assert ops.gemm_cfg(M, N, epi=epi, K=K) == cfg
+    a = _bf(M, K, seed=81)
+    if epi == "swiglu":
+        gu = _bf(N, K, scale=K ** -0.5, seed=82)
+        nw = _bf(K, scale=0.1, seed=83) + 1
+        out = ops.gemm(a, ops.interleave_gate_up(ops.fold_norm(gu, nw)), epi="swiglu", norm_eps=1e-5)
+        ref = ops.ref_gemm(a, gu, epi="swiglu", norm_eps=1e-5, norm_w=nw)
+    else:
+        w = _bf(N, K, scale=K ** -0.5, seed=84)
+        x = _bf(M, N, seed=85)
+        ref = x.float() + (a.float() @ w.float().t()).to(torch.bfloat16).float()
+        out = ops.gemm(a, w, epi="resid", resid=x)
+    rows = torch.randperm(M, generator=torch.Generator().manual_seed(M))[:512].to(DEV)
+    torch.testing.assert_close(out.float()[rows], ref[rows], atol=3e-2, rtol=3e-2)
+
+
+def test_attn_spec_bench_scale():
+    """Verify attention at a bench-scale bucket: 4 096 rows, up to 6 drafts each
+    (max_q 7, two MFMA column blocks), random positions over the whole slot, a
+    quarter of the rows finished -- bit-identical to the grouped decode kernel on
+    the same pseudo-rows, and an fp32 spot check."""
+    nh, nkv, D, S, Lmax, P0 = 9, 3, 64, 4096, 224, 20
+    P0pad = 32
+    g = torch.Generator(device="cpu").manual_seed(91)
+    kc = _bf(S, nkv, Lmax, D, seed=92)
+    vrows = _bf(S, nkv, Lmax, D, seed=93)
+    vt = ops.rows_to_vt(vrows)
+    pk = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
+    pvrows = torch.zeros(nkv, P0pad, D, dtype=torch.bfloat16, device=DEV)
+    pk[:, :P0] = _bf(nkv, P0, D, seed=94)
+    pvrows[:, :P0] = _bf(nkv, P0, D, seed=95)
+    pvt = ops.rows_to_vt(pvrows)
+    B, max_q = 4096, 7
+    nd_h = torch.randint(0, max_q, (B,), generator=g)
+    pos_h = torch.randint(0, Lmax - max_q, (B,), generator=g)
+    done_h = torch.rand(B, generator=g) < 0.25
+    slots = torch.randperm(S, generator=g)[:B]
+    xp, xs, xd, rs, nd = [], [], [], [], []
+    for r in range(B):
+        rs.append(len(xp))
+        if done_h[r]:
+            nd.append(-1)
+            continue
+        nd.append(int(nd_h[r]))
+        for i in range(int(nd_h[r]) + 1):
+            xp.append(int(pos_h[r]) + i)
+            xs.append(int(slots[r]))
+            xd.append(0)
+    T = len(xp)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    xp, xs, xd, rs, nd = (torch.tensor(v, **i32) for v in (xp, xs, xd, rs, nd))
+    q = _bf(T, nh, D, seed=96)
+    scale = 1 / math.sqrt(D)
+    out_s = torch.zeros(T, nh * D, dtype=torch.bfloat16, device=DEV)
+    out_g = torch.zeros_like(out_s)
+    ops.attn_spec(q, rs, nd, xp, xs, xd, kc, vt, pk, pvt, P0, out_s, scale, max_q=max_q)
+    ops.attn_decode(q, xp, xs, kc, vt, pk, pvt, P0, out_g, scale, done=xd, impl="grouped")
+    torch.cuda.synchronize()
+    assert torch.equal(out_s, out_g)
+    for t in torch.randperm(T, generator=g)[:24].tolist():
+        p, r = int(xp[t]), int(xs[t])
+        ref = _ref_seq_attention(q[t:t + 1].float(), kc[r, :, :p + 1].permute(1, 0, 2).float(),
+                                 vrows[r, :, :p + 1].permute(1, 0, 2).float(), pk[:, :P0].permute(1, 0, 2).float(),
+                                 pvrows[:, :P0].permute(1, 0, 2).float(), P0, [p], scale)
+        torch.testing.assert_close(out_s[t].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)

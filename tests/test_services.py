@@ -434,6 +434,44 @@ def test_pocketbase_upsert_dedup_and_retry(arun):
     assert any("auth-with-password" in c for c in fake.calls)
 
 
+def test_pocketbase_batch_upsert_and_fallbacks(arun):
+    """With the batch API, N records cost ceil(N / 50) requests (PUT on msg_id-derived
+    ids, idempotent); a chunk the server refuses (a msg_id the reference's writer
+    stored under a random id) falls back to GET + PATCH for that chunk; a server
+    without the batch API (403) switches the sink to per-record for good."""
+    from smsgate_amd.sinks.pocketbase import PocketBaseClient, PocketBaseSink, record_id
+
+    recs = [ParsedSMS(**_parsed(f"b{i}")) for i in range(120)]
+
+    async def run(fake, batches):
+        c = PocketBaseClient(base_url="http://pb", transport=fake.transport(), retry_min=0.001, retry_max=0.002)
+        sink = PocketBaseSink(c)
+        for b in batches:
+            await sink.upsert_many(b)
+        await c.close()
+        return sink
+
+    fake = FakePocketBase(batch_enabled=True)
+    sink = arun(run(fake, [recs, [r.model_copy(update={"merchant": "NEW"}) for r in recs[:10]]]))
+    stored = fake.cols["sms_data"]
+    assert len(stored) == 120 and sink.batched == 130 and sink.per_record == 0
+    assert sum(c == "POST /api/batch" for c in fake.calls) == 4  # 50 + 50 + 20, then 10
+    assert {r["id"] for r in stored} == {record_id(f"b{i}") for i in range(120)}
+    assert sum(r["merchant"] == "NEW" for r in stored) == 10
+
+    legacy_fake = FakePocketBase(batch_enabled=True)
+    legacy_fake.cols["sms_data"] = [dict(msg_id="b3", id="legacyrandomid0", merchant="OLD")]
+    sink = arun(run(legacy_fake, [recs[:5]]))
+    assert sink.per_record == 5 and sink.batch_supported is not False
+    assert len(legacy_fake.cols["sms_data"]) == 5  # b3 PATCHed in place, no duplicate
+    assert next(r for r in legacy_fake.cols["sms_data"] if r["msg_id"] == "b3")["id"] == "legacyrandomid0"
+
+    off = FakePocketBase(batch_enabled=False)
+    sink = arun(run(off, [recs[:60], recs[60:]]))
+    assert sink.batch_supported is False and sink.per_record == 120 and len(off.cols["sms_data"]) == 120
+    assert sum(c == "POST /api/batch" for c in off.calls) == 1  # probed once, then per record
+
+
 # --------------------------------------------------------------------------- CLI
 def test_cli_parses_every_service():
     from smsgate_amd.cli import build_parser

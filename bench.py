@@ -227,7 +227,9 @@ def run_replica(args, rank: int, world: int, local: int):
     (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
     if hasattr(engine, "spec_stats"):
         engine.spec_stats(reset=True)
+    cpu0 = _cpu_snapshot(procs, broker)
     dt, counts = coord.run_phase(seeds(args.warmup, args.steps), per_w, sync=sync)
+    cpu = {k: v1 - cpu0[k] for k, v1 in _cpu_snapshot(procs, broker).items()}
     coord.shutdown(procs)
     estats = engine.stats.as_dict()
     if hasattr(engine, "spec_stats"):
@@ -242,6 +244,11 @@ def run_replica(args, rank: int, world: int, local: int):
         c = torch.tensor([counts.get(k, 0) for k in keys], dtype=torch.int64, device=dev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         counts = dict(zip(keys, (int(x) for x in c.tolist())))
+        # CPU seconds of the timed region summed over ranks (brokers: local rank 0 only)
+        ck = sorted(cpu)
+        cs = torch.tensor([cpu[k] for k in ck], dtype=torch.float64, device=dev)
+        dist.all_reduce(cs, op=dist.ReduceOp.SUM)
+        cpu = dict(zip(ck, (float(x) for x in cs.tolist())))
         dist.barrier()  # every rank is done with the broker
         dist.destroy_process_group()
     if broker:
@@ -250,7 +257,41 @@ def run_replica(args, rank: int, world: int, local: int):
         for b in broker:
             b.stop()
         shutil.rmtree(os.path.dirname(broker[0].listens[0].replace("unix://", "")), ignore_errors=True)
-    return dt, counts, init_s, estats, prov, quality
+    return dt, counts, init_s, estats, prov, quality, cpu
+
+
+def _cpu_snapshot(procs, brokers) -> dict:
+    """CPU seconds (user + system) consumed so far by the roles of this replica: its
+    parser processes, this rank process (engine feeder + coordinator) and the node's
+    brokers (local rank 0 owns them).  Differences around the timed region give the
+    node's CPU budget per message (VERDICT r02 weak #8)."""
+    import psutil
+
+    def cpu_of(pids):
+        tot = 0.0
+        for pid in pids:
+            try:
+                t = psutil.Process(pid).cpu_times()
+                tot += t.user + t.system
+            except psutil.Error:
+                pass
+        return tot
+
+    return {"parser_procs": cpu_of(p.pid for p in procs), "rank_proc": cpu_of([os.getpid()]),
+            "brokers": cpu_of(b.pid for b in (brokers or []))}
+
+
+def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
+    """Cores busy per role over the timed region, CPU microseconds per message and the
+    cores an 8-GPU node needs at this run's per-GPU rate (weak scaling: per-GPU work is
+    fixed, so each role's load scales with the GPU count)."""
+    per_gpu = {k: v / dt / world for k, v in cpu.items()}
+    total = sum(per_gpu.values())
+    return {"cores_busy_per_gpu": {k: round(v, 2) for k, v in per_gpu.items()},
+            "cores_busy_per_gpu_total": round(total, 2),
+            "cpu_us_per_msg": round(sum(cpu.values()) / max(msgs, 1) * 1e6, 1),
+            "node_cores_at_8_gpus": round(8 * total, 1),
+            "visible_cpus": len(os.sched_getaffinity(0))}
 
 
 def engine_kwargs(args) -> dict:
@@ -408,9 +449,10 @@ def main(argv=None) -> int:
         ops.GEMM_MEASURED[("swiglu", 3072, 576)] = [(4096, 1 << 30, args.swiglu_cfg)]
     rank, world, local = _rank_env()
     if args.backend == "local_llm" or args.cpu_echo_engine:
-        dt, counts, init_s, estats, prov, quality = run_replica(args, rank, world, local)
+        dt, counts, init_s, estats, prov, quality, cpu = run_replica(args, rank, world, local)
     else:
         dt, counts, init_s, estats, prov, quality = asyncio.run(_run_cpu(args))
+        cpu = None
         world = 1
     total = args.msgs_per_step * args.steps * world
     routed = counts.get("ok", 0) + counts.get("fail", 0) + counts.get("skip", 0)
@@ -476,6 +518,8 @@ def main(argv=None) -> int:
         }
         if quality is not None:
             out["quality_heldout"] = quality
+        if cpu is not None:
+            out["cpu"] = cpu_budget(cpu, dt, total, world)
         if args.verbose and estats:
             out["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in estats.items()}
         print(json.dumps(out), flush=True)

@@ -54,7 +54,11 @@ def main() -> int:
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--iters", type=int, default=9)
     p.add_argument("--inner", type=int, default=20)
+    p.add_argument("--only", default="", help="comma list of shapes (gate_up,down,o,qkv_rope); default all")
+    p.add_argument("--cfgs", default="", help="comma list of tile configs to time; default every one that fits")
     a = p.parse_args()
+    only = set(filter(None, a.only.split(",")))
+    pick = {int(c) for c in a.cfgs.split(",") if c}
     dev = "cuda"
     torch.manual_seed(0)
     H, I, nh, nkv, D = 576, 1536, 9, 3, 64
@@ -94,7 +98,11 @@ def main() -> int:
             "o": (H, H, "resid", resid_fn(x, w_o)),
         }
         for name, (N, K, epi, fn) in shapes.items():
-            cfgs = [c for c, (bm, bn) in ops.GEMM_TILES.items() if N % bn == 0]
+            if only and name not in only:
+                continue
+            cfgs = [c for c, (bm, bn) in ops.GEMM_TILES.items() if N % bn == 0 and (not pick or c in pick)
+                    and not (epi == "swiglu" and c in ops.GEMM_NO_SWIGLU)
+                    and not (epi != "swiglu" and c in ops.GEMM_SWIGLU_ONLY)]
             best = {c: math.inf for c in cfgs}
             for _ in range(a.rounds):
                 for c in cfgs:
@@ -107,7 +115,7 @@ def main() -> int:
             res[f"{name}_M{M}"] = {"us": ok, "auto": auto, "auto_us": ok.get(auto),
                                    "best": min(ok, key=ok.get) if ok else None}
             print(json.dumps({f"{name}_M{M}": res[f"{name}_M{M}"]}), file=sys.stderr, flush=True)
-        if True:
+        if not only or "qkv_rope" in only:
             qcfgs = [1, 3, 5, 17, 18]
             best = {c: math.inf for c in qcfgs}
             for _ in range(a.rounds):

@@ -113,11 +113,15 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 template <int ROWS, int NW>
 __device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ src, int ld, int r0, int rmax, int k0,
                                            uint16_t* dst, int wave, int lane) {
-  static_assert(ROWS % (8 * NW) == 0, "8-row pieces spread over the waves");
+  static_assert(ROWS % 8 == 0, "8-row pieces");
+  constexpr int PIECES = ROWS / 8;
   const int rr = lane >> 3, p = lane & 7;
+  // every wave issues the same count (the K loop's counted vmcnt): when the pieces do
+  // not divide evenly (96 rows over 8 waves), the spare issues re-load the last piece
+  // into its own place (same bytes, same LDS address)
 #pragma unroll
-  for (int i = 0; i < ROWS / (8 * NW); ++i) {
-    const int g = wave + NW * i;  // 8-row piece
+  for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
+    const int g = PIECES % NW == 0 ? wave + NW * i : min(wave + NW * i, PIECES - 1);  // 8-row piece
     const int row = 8 * g + rr;
     const int gr = min(r0 + row, rmax);  // rows past the end re-read the last row (never stored)
     const uint16_t* gp = src + (size_t)gr * ld + k0 + ((p ^ (row & 7)) << 3);
@@ -188,7 +192,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   constexpr int BNO = EPI == 2 ? BN / 2 : BN;  // output columns of the block
   constexpr int CST = BNO + 8;                // staged C row stride (elements), +16 B pad
   constexpr int TILE = (BM + BN) * BK;        // one stage (A + B) in elements
-  constexpr int NI = (BM + BN) / (8 * NW);    // glds instructions per stage per wave
+  constexpr int NI = (BM / 8 + NW - 1) / NW + (BN / 8 + NW - 1) / NW;  // glds instructions per stage per wave
   static_assert(ST >= 2 && ST <= 4, "pipeline stages");
   static_assert(BM * CST <= ST * TILE, "C staging fits in the K-loop buffers");
 
@@ -497,8 +501,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   const int c0 = EPI == 2 ? n0 / 2 : n0;
   if constexpr (EPI == 1) {
     // the CPR chunks of a row are CPR consecutive lanes of one wave, and every lane
-    // runs the same trip count, so the row's x² partial reduces with shuffles
+    // runs the same trip count, so the row's x² partial reduces with shuffles (a
+    // power-of-two CPR) or, for 96/192-wide tiles (CPR 12 / 24: a row's lanes are not
+    // an aligned group), through a [BM][CPR] LDS image summed in a fixed order
     static_assert((BM * CPR) % NT == 0 && CPR <= 64, "uniform epilogue trips");
+    constexpr bool POW2 = (CPR & (CPR - 1)) == 0;
+    static_assert(POW2 || BM * CST + 2 * BM * CPR <= ST * TILE, "x² image fits beside the C tile");
+    float* ssl = reinterpret_cast<float*>(smem + BM * CST);
     const bool want_ss = na.ssout != nullptr;
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
@@ -522,9 +531,25 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
         *reinterpret_cast<uint4*>(C + (size_t)gr * ldc + c0 + c * 8) = make_uint4(a[0], a[1], a[2], a[3]);
       }
       if (want_ss) {
+        if constexpr (POW2) {
 #pragma unroll
-        for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
-        if (c == 0 && gr < M) na.ssout[(size_t)(n0 / BN) * na.ld + gr] = sq;
+          for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+          if (c == 0 && gr < M) na.ssout[(size_t)(n0 / BN) * na.ld + gr] = sq;
+        } else {
+          ssl[row * CPR + c] = sq;
+        }
+      }
+    }
+    if constexpr (!POW2) {
+      if (want_ss) {
+        __syncthreads();
+        for (int r = tid; r < BM; r += NT) {
+          if (m0 + r >= M) break;
+          float v = 0.f;
+#pragma unroll
+          for (int c = 0; c < CPR; ++c) v += ssl[r * CPR + c];
+          na.ssout[(size_t)(n0 / BN) * na.ld + m0 + r] = v;
+        }
       }
     }
     return;
@@ -991,6 +1016,19 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
   return -3;
 }
 
+// 96 / 192-wide tiles (3 MFMA columns per wave: no SwiGLU pairing) — the N = 576
+// residual GEMMs (o-proj, down-proj) and plain stores only
+template <int BM, int BN, int WM, int WN, int ST>
+int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr,
+                   int M, int N, int K, float eps, hipStream_t s, const NormArgs& na) {
+  const RopeArgs ra{};
+  const ArgmaxArgs xa{};
+  if (epi == 1 && norm == 0) return launch<BM, BN, WM, WN, 1, 0, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
+  if (epi == 0 && norm == 0) return launch<BM, BN, WM, WN, 0, 0, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
+  if (epi == 0 && norm == 1) return launch<BM, BN, WM, WN, 0, 1, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
+  return -3;
+}
+
 }  // namespace
 
 // Tile configurations: BM x BN (wave grid), pipeline stages.
@@ -1002,6 +1040,9 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
 //  17: 32x64 (2x2) 2st   18: 32x64 (2x2) 4st — small-M decode buckets: twice the tiles of 64x64
 //  19: 256x256 (2x4) staggered 8-wave SwiGLU GEMM (gemm256_swiglu_kernel; epi 2 only)
 //  20: its persistent form (gemm256p_swiglu_kernel; epi 2 only; NORM 2 needs ss_ld % 4 == 0)
+//  21: 128x96 (2x2) 2st   22: 64x96 (2x2) 2st   23: 128x192 (2x4) 2st, 8 waves
+//  24: 256x96 (4x2) 2st, 8 waves   25: 128x96 (2x2) 3st   26: 64x192 (1x4) 2st
+//      (21..26: epi 0 / 1 only — 48-wide wave tiles for the N = 576 residual GEMMs)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1030,9 +1071,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[21] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256};
-  if (cfg < 0 || cfg > 20) return -1;
+  static const int BNs[27] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192};
+  if (cfg < 0 || cfg > 26) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1086,7 +1127,13 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     case 15: return dispatch_epi<128, 256, 2, 4, 3>(SG_ARGS);
     case 16: return dispatch_epi<256, 64, 4, 2, 4>(SG_ARGS);
     case 17: return dispatch_epi<32, 64, 2, 2, 2>(SG_ARGS);
-    default: return dispatch_epi<32, 64, 2, 2, 4>(SG_ARGS);
+    case 18: return dispatch_epi<32, 64, 2, 2, 4>(SG_ARGS);
+    case 21: return dispatch_resid<128, 96, 2, 2, 2>(SG_ARGS);
+    case 22: return dispatch_resid<64, 96, 2, 2, 2>(SG_ARGS);
+    case 23: return dispatch_resid<128, 192, 2, 4, 2>(SG_ARGS);
+    case 24: return dispatch_resid<256, 96, 4, 2, 2>(SG_ARGS);
+    case 25: return dispatch_resid<128, 96, 2, 2, 3>(SG_ARGS);
+    default: return dispatch_resid<64, 192, 1, 4, 2>(SG_ARGS);
   }
 #undef SG_ARGS
 }

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import multiprocessing as mp
 import os
+import shutil
 import signal
 import socket
 import tempfile
@@ -50,7 +51,9 @@ def _worker(host: str, port: int, log_level: str) -> None:
 
 def serve_workers(n: int, host: str, port: int, log_level: str = "warning") -> int:
     """Run ``n`` gateway processes on ``host:port`` until SIGTERM / SIGINT; returns 0."""
-    os.environ.setdefault("PROMETHEUS_MULTIPROC_DIR", tempfile.mkdtemp(prefix="smsgate-gw-metrics-"))
+    own_dir = None
+    if not os.environ.get("PROMETHEUS_MULTIPROC_DIR"):
+        own_dir = os.environ["PROMETHEUS_MULTIPROC_DIR"] = tempfile.mkdtemp(prefix="smsgate-gw-metrics-")
     ctx = mp.get_context("spawn")
     procs: List[mp.Process] = []
     for i in range(n):
@@ -75,4 +78,6 @@ def serve_workers(n: int, host: str, port: int, log_level: str = "warning") -> i
             p.join(10)
             if p.is_alive():
                 p.kill()
+        if own_dir:
+            shutil.rmtree(own_dir, ignore_errors=True)
     return 0

@@ -26,4 +26,9 @@ def test_two_ranks_one_broker():
     assert rt["parsed"] + rt["keyword_skipped"] + rt["broken"] + rt["dlq"] == total
     assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"]  # every parsed message written once
     assert "shared smsgate-busd" in out["config"]["bus"] and out["n_gpus"] == 2
+    # node CPU budget of the timed region: every role accounted, brokers included
+    cpu = out["cpu"]
+    assert set(cpu["cores_busy_per_gpu"]) == {"parser_procs", "rank_proc", "brokers"}
+    assert cpu["cores_busy_per_gpu"]["parser_procs"] > 0 and cpu["cores_busy_per_gpu"]["brokers"] > 0
+    assert cpu["cpu_us_per_msg"] > 0 and cpu["node_cores_at_8_gpus"] == round(8 * cpu["cores_busy_per_gpu_total"], 1)
     assert not [d for d in os.listdir("/tmp") if d == "smsgate-bench-bus-29671"]  # broker dir cleaned up

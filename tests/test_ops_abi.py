@@ -81,3 +81,4 @@ def test_measured_tile_exceptions():
     assert ops.gemm_cfg(2304, 3072, epi="swiglu", K=576) == 13
     assert ops.gemm_cfg(4608, 3072, epi="swiglu", K=576) == 19
     assert ops.GEMM_TILES[20] == (256, 256) and 20 in ops.GEMM_SWIGLU_ONLY
+    assert all(576 % ops.GEMM_TILES[c][1] == 0 for c in ops.GEMM_NO_SWIGLU)  # the N = 576 residual GEMMs

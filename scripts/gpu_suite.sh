@@ -12,6 +12,8 @@
 #   latency   Poisson serving latency, trained weights, spec on/off -> gpurun_out/latency_spec{0,4}.json
 #   curve     extractor training curve (held-out accuracy) -> gpurun_out/curve.log
 #   worst     bench.py with random-init weights (every answer runs to the field caps) -> gpurun_out/bench_random.log
+#   ktests    GPU tests selected by PYTEST_K (pytest -k) -> gpurun_out/ktests.log
+#   tune      scripts/gemm_tune.py $TUNE_ARGS        -> gpurun_out/gemm_tune.json
 # Extra bench.py arguments can be passed in BENCH_ARGS.
 set -o pipefail
 mkdir -p gpurun_out
@@ -33,7 +35,15 @@ for stage in "$@"; do
       timeout -k 10 700 python -u bench.py --steps 2 --warmup 1 --eval-n 0 $BENCH_ARGS > gpurun_out/prof_warm.log 2>&1 || { rc=$?; tail -3 gpurun_out/prof_warm.log; exit $rc; }
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python $R/bench.py --steps 10 --warmup 2 --eval-n 0 $BENCH_ARGS > $R/gpurun_out/prof.log 2>&1)
       rc=$?; tail -1 gpurun_out/prof.log | cut -c1-160
-      find gpurun_out/prof -name "*kernel_trace.csv" -size +20M -delete ;;
+      # the trace itself is too big to copy back: keep a (kernel, grid) histogram of it
+      [ $rc -eq 0 ] && python scripts/prof_summary.py gpurun_out/prof
+      find gpurun_out/prof -name "*kernel_trace.csv" -delete ;;
+    ktests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "$PYTEST_K" > gpurun_out/ktests.log 2>&1
+      rc=$?; tail -3 gpurun_out/ktests.log ;;
+    tune)
+      timeout -k 10 600 python -u scripts/gemm_tune.py $TUNE_ARGS > gpurun_out/gemm_tune.json 2> gpurun_out/gemm_tune.err
+      rc=$?; tail -c 600 gpurun_out/gemm_tune.json ;;
     latency)
       rc=0
       for k in 0 4; do

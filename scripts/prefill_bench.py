@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Prefill attention microbench at the engine's shapes: per-head vs GQA-shared kernel.
+"""Prefill attention microbench at the engine's shapes: per-head, GQA-shared and
+multi-tile kernels (one JSON line per batch size).
 
-    python scripts/prefill_bench.py [--nseq 800] [--out gpurun_out/prefill_bench.json]
+    python scripts/prefill_bench.py [--nseq 150,300,800] [--out gpurun_out/prefill_bench.jsonl]
 """
 from __future__ import annotations
 
@@ -20,16 +21,27 @@ from smsgate_amd import ops  # noqa: E402
 
 def main() -> None:
     p = argparse.ArgumentParser()
-    p.add_argument("--nseq", type=int, default=800)
+    p.add_argument("--nseq", default="150,300,800")
+    p.add_argument("--lens", default="40,70", help="prompt length range (tokens)")
     p.add_argument("--nh", type=int, default=9)
     p.add_argument("--nkv", type=int, default=3)
-    p.add_argument("--P0", type=int, default=75)
+    p.add_argument("--P0", type=int, default=20)
     p.add_argument("--iters", type=int, default=50)
     p.add_argument("--out", default=None)
     a = p.parse_args()
+    lines = [run(a, int(n)) for n in a.nseq.split(",")]
+    if a.out:
+        os.makedirs(os.path.dirname(a.out), exist_ok=True)
+        with open(a.out, "w") as f:
+            f.write("".join(json.dumps(r) + "\n" for r in lines))
+
+
+def run(a, nseq: int) -> dict:
     dev = "cuda"
+    a.nseq = nseq
+    lo, hi = (int(x) for x in a.lens.split(","))
     g = torch.Generator(device="cpu").manual_seed(0)
-    lens = torch.randint(30, 60, (a.nseq,), generator=g).tolist()
+    lens = torch.randint(lo, hi, (a.nseq,), generator=g).tolist()
     D, Lmax = 64, 192
     S = a.nseq
     T = sum(lens)
@@ -45,7 +57,7 @@ def main() -> None:
     scale = 1 / math.sqrt(D)
     res = {"nseq": a.nseq, "tokens": T, "nh": a.nh, "nkv": a.nkv, "P0": a.P0}
     outs = {}
-    for impl in ("per_head", "gqa", "gqa_ks2"):
+    for impl in ("per_head", "gqa", "gqa_ks2", "multi"):
         ops.set_prefill_impl("gqa" if impl.startswith("gqa") else impl)
         ops.set_prefill_split(2 if impl == "gqa_ks2" else 1)
         out = torch.empty(T, a.nh * D, dtype=torch.bfloat16, device=dev)
@@ -66,11 +78,10 @@ def main() -> None:
     res["max_abs_diff_ks2"] = float((outs["gqa_ks2"] - outs["gqa"]).abs().max())
     res["speedup"] = round(res["per_head_us"] / res["gqa_us"], 3)
     res["speedup_ks2"] = round(res["gqa_us"] / res["gqa_ks2_us"], 3)
-    print(json.dumps(res))
-    if a.out:
-        os.makedirs(os.path.dirname(a.out), exist_ok=True)
-        with open(a.out, "w") as f:
-            json.dump(res, f)
+    res["max_abs_diff_multi"] = float((outs["multi"] - outs["per_head"]).abs().max())
+    res["speedup_multi_vs_per_head"] = round(res["per_head_us"] / res["multi_us"], 3)
+    print(json.dumps(res), flush=True)
+    return res
 
 
 if __name__ == "__main__":

@@ -236,9 +236,17 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #   profiles/r02s3_gemm_tune.json): gate/up at 2304 rows 128x128 8-wave (13.7 vs 16.9 us),
 #   at 4608 rows (one tile round: nothing for persistence to overlap) cfg 19 (21.1 vs 21.6);
 #   o-proj at 9216 rows 64x64 (14.7 vs 16.4 us).
+#   Round 3: 96-wide tiles (48-wide wave tiles: 6 B of LDS reads per output instead of 8
+#   for 64x64 / 32x32 wave tiles) for the N = 576 residual GEMMs, interleaved with every
+#   older config at the engine's flavour (profiles/r03_gemm96_tune.json): down-proj 128x96
+#   25.0 / 40.3 us at 9216 / 16384 rows vs 28.2 / 43.4 (128x64), 64x96 15.8 vs 18.5 at
+#   4608; o-proj 64x96 8.3 / 20.3 us at 4608 / 16384 vs 8.8 / 22.4, 128x96 13.0 vs 14.9
+#   (64x64) at 9216.  Both residual GEMMs of a forward keep BN = 96 at the same rows
+#   (the producer-norm partials need equal N tilings: 6 parts).
 GEMM_MEASURED = {
     ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 6143, 19), (6144, 1 << 30, 20)],
-    ("resid", 576, 576): [(8192, 10240, 3)],
+    ("resid", 576, 576): [(2048, 6143, 22), (6144, 12287, 21), (12288, 1 << 30, 22)],
+    ("resid", 576, 1536): [(2048, 6143, 22), (6144, 1 << 30, 21)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
 
@@ -421,9 +429,10 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos
 def set_prefill_impl(impl: str) -> None:
     """``"auto"`` (default: ``per_head`` up to 384 sequences per launch, ``gqa``
     above), ``"gqa"`` (one wave per KV head, K/V loaded once per GQA group,
-    prefetched) or ``"per_head"`` (one wave per query head: G x the waves, which
-    fills the chip better at small batches; ``profiles/r01c_prefill_key_split_ab.txt``)."""
-    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2}[impl])
+    prefetched), ``"per_head"`` (one wave per query head: G x the waves, which
+    fills the chip better at small batches; ``profiles/r01c_prefill_key_split_ab.txt``)
+    or ``"multi"`` (per head, every K/V tile of a 3-tile chunk loaded at once)."""
+    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3}[impl])
 
 
 def set_prefill_split(ks: int) -> None:

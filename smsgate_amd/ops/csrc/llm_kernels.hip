@@ -347,7 +347,176 @@ __global__ void __launch_bounds__(64) attn_prefill_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Prefill attention, GQA-shared (production): one wave per (16-query tile,
+// Prefill attention, multi-tile (default): same wave decomposition and layouts as
+// attn_prefill_kernel, but the K and V tiles of NT key tiles (a whole short
+// sequence: the shared prefix + ~54 own keys is 3 tiles) are loaded up front,
+// all at once, and the softmax runs once per chunk of NT tiles instead of once per
+// tile.  The per-tile kernel walks its tiles as a chain of dependent cold loads
+// (K tile -> scores -> V tile -> next K tile): at the engine's prefill batches every
+// wave is latency-bound and the kernel ran at ~0.5 TB/s (profiles/r03_bench_grid_hist.csv:
+// 32 us per 8 k-token call).  Longer sequences take several chunks (online softmax
+// across chunks).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ void __launch_bounds__(64) attn_prefill_mt_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
+    const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out,
+    int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int tile = blockIdx.x, b = blockIdx.y, h = blockIdx.z;
+  const int l = threadIdx.x;
+  const int qbeg = cu_q[b];
+  const int qlen = cu_q[b + 1] - qbeg;
+  if (tile * 16 >= qlen) return;
+  const int kh = h / (nh / nkv);
+  const int g4 = l >> 4, r16 = l & 15;
+  const int qs = q_start[b];
+  const int sl = slot[b];
+
+  __shared__ __attribute__((aligned(16))) uint16_t P_lds[NT][16 * 32];
+
+  bf16x8 qa[2];
+  {
+    const int row = tile * 16 + r16;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < qlen) v = *reinterpret_cast<const uint4*>(q + ((size_t)(qbeg + row) * nh + h) * D + 8 * g4 + 32 * s);
+      qa[s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  int qoff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) qoff[i] = qs + tile * 16 + 4 * g4 + i;
+  const int last_row = min(tile * 16 + 15, qlen - 1);
+  const int nkeys = P0pad + qs + last_row + 1;
+
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+
+  f32x4 o[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) o[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m[4], lsum[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m[i] = -INFINITY; lsum[i] = 0.f; }
+
+  for (int kc = 0; kc < nkeys; kc += NT * 32) {
+    // ---- every load of the chunk first (K: 4 x 16 B, V: 4 x 16 B per lane and tile)
+    uint4 kv[NT][2][2], vv[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int kt = kc + 32 * t;
+      const bool pre = kt < P0pad;  // tiles never straddle: P0pad % 32 == 0
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const int key = kt + 16 * hs + r16;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          kv[t][hs][s] = make_uint4(0, 0, 0, 0);
+          if (key < nkeys) {
+            const uint16_t* krow = pre ? (kpre + (size_t)key * D) : (kself + (size_t)(key - P0pad) * D);
+            kv[t][hs][s] = *reinterpret_cast<const uint4*>(krow + 8 * g4 + 32 * s);
+          }
+        }
+      }
+      const int kk = kt + 8 * g4;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int d = 16 * n + r16;
+        vv[t][n] = make_uint4(0, 0, 0, 0);
+        if (kk < nkeys) {
+          const uint16_t* vrow = pre ? (vpre + ((size_t)(kk >> 3) * D + d) * 8)
+                                     : (vself + ((size_t)((kk - P0pad) >> 3) * D + d) * 8);
+          vv[t][n] = *reinterpret_cast<const uint4*>(vrow);
+        }
+      }
+    }
+    // ---- scores of the chunk, masked and scaled; chunk row max
+    float sv[NT][2][4];
+    float cmax[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cmax[i] = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int kt = kc + 32 * t;
+      const bool pre = kt < P0pad;
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[s], __builtin_bit_cast(bf16x8, kv[t][hs][s]), acc, 0, 0, 0);
+        const int key = kt + 16 * hs + r16;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = key < nkeys && (pre ? key < P0 : (key - P0pad) <= qoff[i]);
+          const float v = ok ? acc[i] * scale_log2 : -INFINITY;
+          sv[t][hs][i] = v;
+          cmax[i] = fmaxf(cmax[i], v);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o2 = 8; o2 > 0; o2 >>= 1) cmax[i] = fmaxf(cmax[i], __shfl_xor(cmax[i], o2, WAVE));
+    }
+    float alpha[4], rs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float mn = fmaxf(m[i], cmax[i]);
+      alpha[i] = (mn == -INFINITY) ? 1.f : exp2f(m[i] - mn);
+      m[i] = mn;
+      rs[i] = 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = (m[i] == -INFINITY) ? 0.f : exp2f(sv[t][hs][i] - m[i]);
+          rs[i] += p;
+          P_lds[t][(4 * g4 + i) * 32 + 16 * hs + r16] = f2bf(p);
+        }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o2 = 8; o2 > 0; o2 >>= 1) rs[i] += __shfl_xor(rs[i], o2, WAVE);
+      lsum[i] = lsum[i] * alpha[i] + rs[i];
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[n][i] *= alpha[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bf16x8 pa = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&P_lds[t][r16 * 32 + 8 * g4]));
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, __builtin_bit_cast(bf16x8, vv[t][n]), o[n], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = tile * 16 + 4 * g4 + i;
+    if (row >= qlen) continue;
+    const float inv = lsum[i] > 0.f ? 1.f / lsum[i] : 0.f;
+    uint16_t* orow = out + ((size_t)(qbeg + row) * nh + h) * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) orow[16 * n + r16] = f2bf(o[n][i] * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Prefill attention, GQA-shared (K/V loaded once per GQA group): one wave per (16-query tile,
 // sequence, KV head) computes all G query heads of the group from ONE load of
 // each K/V tile (the per-head kernel above re-reads K/V G times), and the K tile
 // of step kt+1 and the V tile of step kt are in flight while the scores of step
@@ -1706,6 +1875,13 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   // auto: the per-head kernel launches G x the waves, which wins while the batch is
   // too small to fill the chip (prefill_bench: 12.6 vs 17.2 us at 32 sequences,
   // 32 vs 38 us at 190); the GQA kernel's single K/V load wins at 800 (98 vs 112 us)
+  if (g_prefill_impl == 3) {  // multi-tile per-head kernel (default)
+    dim3 grid((max_q + 15) / 16, nseq, nh);
+    hipLaunchKernelGGL((attn_prefill_mt_kernel<3>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, slot,
+                       (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt,
+                       P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2);
+    return (int)hipGetLastError();
+  }
   const bool gqa = g_prefill_impl == 0 || (g_prefill_impl == 2 && nseq > 384);
   if (gqa && G >= 1 && G <= 4) {
     dim3 grid((max_q + 15) / 16, nseq, nkv);
@@ -1734,7 +1910,8 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   return (int)hipGetLastError();
 }
 
-// 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto by batch size (default)
+// 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto by batch size (0 / 1),
+// 3 = multi-tile per-head kernel
 void sg_set_prefill_impl(int impl) { g_prefill_impl = impl; }
 
 // key split of the GQA prefill kernel: 1 (one wave per tile) or 2 (two waves share the keys)

@@ -512,7 +512,7 @@ def main(argv=None) -> int:
                         if args.bus == "busd" else "in-process bus per parser process"),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
-                "seq_len": "shared prefix 20 + ~48 prompt + <=131 schema-constrained output tokens (~38 trained)",
+                "seq_len": "shared prefix 21 + ~50 prompt + <=131 schema-constrained output tokens (~42 trained)",
                 "parallelism": f"dp{world}" if gpu else "cpu",
                 "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
                 "engine_profile": args.profile,

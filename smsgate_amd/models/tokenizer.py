@@ -8,8 +8,8 @@ Rust ``tokenizers`` library on the synthetic SMS corpus
 text (Cyrillic, emoji…): unknown strings fall back to byte tokens.
 
 Special tokens: ``<pad> <bos> <eos> <sep> <sms> <ans>``.  The prompt of one
-extraction is ``<bos> EXTRACTOR_PROMPT`` (shared prefix, cached once on
-the GPU) + ``<sms> body <ans>`` (per message); the answer is the nine field
+extraction is ``<bos> EXTRACTOR_PROMPT <sms>`` (shared prefix, cached once on
+the GPU) + ``body <ans>`` (per message); the answer is the nine field
 values in schema order, each terminated by ``<sep>``.
 """
 from __future__ import annotations
@@ -18,7 +18,7 @@ import functools
 from pathlib import Path
 from typing import List, Sequence, Tuple
 
-__all__ = ["ExtractorTokenizer", "SPECIALS", "load_tokenizer", "train_tokenizer", "ASSET"]
+__all__ = ["ExtractorTokenizer", "SPECIALS", "load_tokenizer", "train_tokenizer", "ASSET", "model_text"]
 
 ASSET = Path(__file__).resolve().parent / "assets" / "extractor_tokenizer.json"
 SPECIALS = ["<pad>", "<bos>", "<eos>", "<sep>", "<sms>", "<ans>"]
@@ -53,6 +53,15 @@ def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: 
     return tok
 
 
+def model_text(text: str) -> str:
+    """The text the extractor reads: bank bodies carry their line breaks as the literal
+    XML entity ``&#10;`` (the reference's export), which byte-level BPE splits into three
+    tokens (``&#`` ``10`` ``;``: the pre-tokenizer separates punctuation from digits) --
+    15 of the ~55 tokens of an account-format SMS.  The model sees one ``\n`` token
+    instead.  No extracted value spans a line break, so copied values are unchanged."""
+    return text.replace("&#10;", "\n") if "&#" in text else text
+
+
 class ExtractorTokenizer:
     def __init__(self, path: Path = ASSET) -> None:
         from tokenizers import Tokenizer
@@ -65,15 +74,16 @@ class ExtractorTokenizer:
         self.pad, self.bos, self.eos, self.sep, self.sms, self.ans = (ids[s] for s in SPECIALS)
 
     def encode(self, text: str) -> List[int]:
-        return self.tk.encode(text, add_special_tokens=False).ids
+        return self.tk.encode(model_text(text), add_special_tokens=False).ids
 
     def encode_batch(self, texts: Sequence[str]) -> List[List[int]]:
-        return [e.ids for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
+        return [e.ids for e in self.tk.encode_batch([model_text(t) for t in texts], add_special_tokens=False)]
 
     def encode_offsets(self, texts: Sequence[str]) -> List[Tuple[List[int], List[Tuple[int, int]]]]:
-        """Ids plus each token's ``(start, end)`` character span in its text (a
-        token that carries a leading blank covers it)."""
-        return [(e.ids, e.offsets) for e in self.tk.encode_batch(list(texts), add_special_tokens=False)]
+        """Ids plus each token's ``(start, end)`` character span in its MODEL text
+        (:func:`model_text`; a token that carries a leading blank covers it)."""
+        return [(e.ids, e.offsets) for e in self.tk.encode_batch([model_text(t) for t in texts],
+                                                                  add_special_tokens=False)]
 
     def value_span_ids(self, value: str, body: str, ids: Sequence[int],
                        offsets: Sequence[Tuple[int, int]]) -> List[int]:
@@ -86,6 +96,7 @@ class ExtractorTokenizer:
         an exact draft for speculative decoding (:mod:`smsgate_amd.serving.draft`)."""
         if not value:
             return []
+        body, value = model_text(body), model_text(value)  # the offsets index the model text
         start = 0
         while True:
             a = body.find(value, start)
@@ -123,12 +134,15 @@ class ExtractorTokenizer:
         return out
 
     def prefix_ids(self, system: str) -> List[int]:
-        return [self.bos] + self.encode(system)
+        """``<bos> system <sms>``: the shared prefix ends with the message marker, so
+        it is computed once instead of once per message."""
+        return [self.bos] + self.encode(system) + [self.sms]
 
     truncated = 0  # bodies cut to max_body tokens (also the llm_prompt_truncated_total counter)
 
     def message_ids(self, bodies: Sequence[str], max_body: int) -> List[List[int]]:
-        """``<sms> body <ans>`` ids.  A body longer than ``max_body`` tokens keeps
+        """``body <ans>`` ids (the ``<sms>`` marker ends the shared prefix,
+        :meth:`prefix_ids`).  A body longer than ``max_body`` tokens keeps
         its first ``max_body`` tokens; every such cut is counted (the extractor
         never sees the tail, where balances often are), never silent."""
         enc = self.encode_batch(bodies)
@@ -138,7 +152,7 @@ class ExtractorTokenizer:
             from ..obs.metrics import LLM_TRUNCATED
 
             LLM_TRUNCATED.inc(cut)
-        return [[self.sms] + e[:max_body] + [self.ans] for e in enc]
+        return [e[:max_body] + [self.ans] for e in enc]
 
 
 @functools.lru_cache(maxsize=4)

@@ -9,7 +9,7 @@ its speed.  This module turns the LM into a working extractor.
   normalised exactly like the parse pipeline does before calling a backend
   (:func:`~smsgate_amd.parse.text.normalize_body`); skipped kinds (OTP, …) never
   reach the LLM and are not trained on;
-* sequence: ``<bos> EXTRACTOR_PROMPT <sms> body <ans>`` followed by the
+* sequence: ``<bos> EXTRACTOR_PROMPT <sms>`` (shared) ``body <ans>`` followed by the
   compact answer (9 field values, each ended by ``<sep>``): the exact token
   stream the serving engine decodes.  Every target is checked against the
   schema FSM (:mod:`~smsgate_amd.serving.fsm`), so the constrained decoder can

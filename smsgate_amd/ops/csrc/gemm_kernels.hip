@@ -184,7 +184,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
                                                          NormArgs na) {
   constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  static_assert(EPI != 3 || BN == 64, "QKV+RoPE epilogue: one 64-wide head per N tile");
+  static_assert(EPI != 3 || BN % 64 == 0, "QKV+RoPE epilogue: whole 64-wide heads per N tile");
+  constexpr int HT = BN / 64;  // EPI 3: heads per N tile (all q, all k or all v: HT | nh, HT | nkv)
   constexpr int TM = BM / WM, TN = BN / WN;  // wave tile
   constexpr int FM = TM / 16, FN = TN / 16;  // MFMA tiles per wave
   static_assert(FM >= 1 && FN >= 1 && TM % 16 == 0 && TN % 16 == 0, "tile");
@@ -241,8 +242,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     }
   }
   // EPI 3: the tile's token positions / KV slots, likewise loaded before the K loop —
-  // q/k head: the rows of this thread's (row, quarter) items; v head: row = lane (+64)
-  constexpr int QIT = (BM * 4 + NT - 1) / NT, VU = BM > 64 ? 2 : 1;
+  // q/k heads: the rows of this thread's (row, head, quarter) items; v heads: row = lane (+64)
+  constexpr int QIT = (BM * 4 * HT + NT - 1) / NT, VU = BM > 64 ? 2 : 1;
   constexpr int EPN = EPI == 3 ? (QIT > VU ? QIT : VU) : 1;
   int epos[EPN], eslot[EPN];
   if constexpr (EPI == 3) {
@@ -250,7 +251,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     if (h < ra.nh + ra.nkv) {
 #pragma unroll
       for (int it = 0; it < QIT; ++it) {
-        const int gr = min(m0 + ((tid + it * NT) >> 2), M - 1);
+        const int gr = min(m0 + (tid + it * NT) / (4 * HT), M - 1);
         epos[it] = ra.pos[gr];
         eslot[it] = h >= ra.nh ? ra.slot[gr] : 0;
       }
@@ -403,22 +404,23 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   }
   __syncthreads();
 
-  // ---- epilogue 2 (EPI 3): RoPE the q/k head of this tile into q_out / the K
-  // cache, or scatter the v head into the blocked V^T cache.  Same rounding as
+  // ---- epilogue 2 (EPI 3): RoPE the q/k heads of this tile into q_out / the K
+  // cache, or scatter the v heads into the blocked V^T cache.  Same rounding as
   // the unfused path: bf16 projection (the staged tile) -> fp32 RoPE -> bf16.
   if constexpr (EPI == 3) {
-    const int h = n0 >> 6;
-    if (h < ra.nh + ra.nkv) {
+    const int h0 = n0 >> 6;
+    if (h0 < ra.nh + ra.nkv) {
 #pragma unroll
       for (int it = 0; it < QIT; ++it) {
         const int q = tid + it * NT;
-        if (q >= BM * 4) break;
-        const int row = q >> 2, c = q & 3;
+        if (q >= BM * 4 * HT) break;
+        const int row = q / (4 * HT), j = (q >> 2) % HT, c = q & 3;
+        const int h = h0 + j;
         const int gr = m0 + row;
         if (gr >= M) continue;
         const int p = epos[it];
-        const uint4 v1 = *reinterpret_cast<const uint4*>(Cs + row * CST + c * 8);
-        const uint4 v2 = *reinterpret_cast<const uint4*>(Cs + row * CST + 32 + c * 8);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(Cs + row * CST + j * 64 + c * 8);
+        const uint4 v2 = *reinterpret_cast<const uint4*>(Cs + row * CST + j * 64 + 32 + c * 8);
         const float4* csp = reinterpret_cast<const float4*>(ra.cs + (size_t)(ra.p0 + p) * 32 + c * 8);
         const uint32_t a1[4] = {v1.x, v1.y, v1.z, v1.w}, a2[4] = {v2.x, v2.y, v2.z, v2.w};
         uint32_t o1[4], o2[4];
@@ -442,15 +444,18 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       // serialised ~16 L2 round trips per wave) and are broadcast with readlane: the
       // V^T address is a scalar base + 16 B x lane
       static_assert(BM <= 128, "V^T scatter: rows per lane register");
-      const int kh = h - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
+      const int kh0 = h0 - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
       for (int row = __builtin_amdgcn_readfirstlane(wave); row < BM; row += NW) {
         const int gr = m0 + row;
         if (gr >= M) break;
         const int u = BM > 64 ? (row >> 6) : 0;
         const int p = __builtin_amdgcn_readlane(u ? epos[VU - 1] : epos[0], row & 63);
         const int sl = __builtin_amdgcn_readlane(u ? eslot[VU - 1] : eslot[0], row & 63);
-        const size_t base = (((size_t)sl * ra.nkv + kh) * nb + (p >> 3)) * 512 + (p & 7);
-        ra.vt_cache[base + (size_t)lane * 8] = Cs[row * CST + lane];
+#pragma unroll
+        for (int j = 0; j < HT; ++j) {
+          const size_t base = (((size_t)sl * ra.nkv + kh0 + j) * nb + (p >> 3)) * 512 + (p & 7);
+          ra.vt_cache[base + (size_t)lane * 8] = Cs[row * CST + j * 64 + lane];
+        }
       }
     }
     return;
@@ -1140,7 +1145,8 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
 
 // QKV projection with the RMSNorm prologue and the RoPE + KV-cache epilogue
 // (replaces gemm + sg_rope_qkv_cache).  W: [(nh + 2 nkv)·64, K], norm folded in.
-// cfg must have BN = 64 (1, 3, 5, 17 or 18).
+// cfg must have BN = 64 (1, 3, 5, 17 or 18) or 192 (23: 128x192 8 waves, 26: 64x192; three
+// heads per N tile, so nh and nkv must be multiples of 3).
 // ssin non-null: the row scales come from the producer's partials (NORM 2).
 int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float eps, int cfg, const int* pos,
                      const int* slot, const void* cos_sin, void* q_out, void* k_cache, void* vt_cache, int nh, int nkv,
@@ -1161,6 +1167,14 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
     case 5: SG_QKV(64, 3);
     case 17: SG_QKV(32, 2);
     case 18: SG_QKV(32, 4);
+    case 23:
+      if (nh % 3 || nkv % 3) return -2;
+      return ssin ? launch<128, 192, 2, 4, 3, 2, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
+                  : launch<128, 192, 2, 4, 3, 1, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na);
+    case 26:
+      if (nh % 3 || nkv % 3) return -2;
+      return ssin ? launch<64, 192, 1, 4, 3, 2, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
+                  : launch<64, 192, 1, 4, 3, 1, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na);
     default: return -1;
   }
 #undef SG_QKV

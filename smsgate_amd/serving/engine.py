@@ -916,7 +916,7 @@ class ExtractionEngine:
         return out
 
     def submit_ids(self, items: Sequence[Tuple[Any, Sequence[int]]]) -> None:
-        """Queue pre-tokenised prompts (``<sms> body <ans>`` ids, see the tokenizer)."""
+        """Queue pre-tokenised prompts (``body <ans>`` ids, see the tokenizer)."""
         cap = self.cfg.max_body_tokens + 2
         for k, ids in items:
             if len(ids) > cap:  # keep the closing <ans>

@@ -92,3 +92,16 @@ def test_reference_cases_reachable(tk_fsm):
                    merchant=exp["merchant"], city=exp["city"], address=exp["address"], balance=balance)
         ids = answer_tokens(tk, fsm, ans, b)
         assert ids is not None and _walk_ok(fsm, ids, tk.message_ids([b], 128)[0]), body
+
+
+def test_model_text_line_breaks(tk_fsm):
+    """``&#10;`` (the reference export's line break) reaches the model as ONE token, and
+    copied values still decode to the body's own text."""
+    tk, fsm = tk_fsm
+    body = "DEBIT ACCOUNT&#10;111,264.44 RUB&#10;CARD:4579,&#10;S1X1GWT5, TIOVINVU&#10;25.02.2023 19:39"
+    ids = tk.encode(body)
+    assert len(ids) <= len(tk.tk.encode(body, add_special_tokens=False).ids) - 7
+    assert "&#" not in tk.decode(ids) and tk.decode(ids).count("\n") == 4
+    enc = tk.encode_offsets([body])[0]
+    for v in ("TIOVINVU", "111,264.44", "S1X1GWT5"):
+        assert tk.decode(tk.value_span_ids(v, body, *enc)).strip() == v

@@ -255,10 +255,10 @@ def test_gemm_strided_a_and_bad_shapes():
         ops.gemm(_bf(4, 100), _bf(64, 100))
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 5, 17, 18])
-@pytest.mark.parametrize("M", [1, 77, 1000])
+@pytest.mark.parametrize("cfg", [1, 3, 5, 17, 18, 23, 26])
+@pytest.mark.parametrize("M", [1, 77, 1000, 9216])
 def test_gemm_qkv_rope_matches_unfused(cfg, M):
-    nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, 1024, 192, 576, 75
+    nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, max(1024, M), 192, 576, 75
     x = _bf(M, K, seed=51)
     w = _bf((nh + 2 * nkv) * D, K, scale=K ** -0.5, seed=52)
     g = torch.Generator(device="cpu").manual_seed(53)

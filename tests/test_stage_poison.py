@@ -225,7 +225,7 @@ def test_long_body_truncation_is_counted():
     t0 = tk.truncated
     long_body = REFERENCE_CASES[0][0] + " EXTRA" * 200
     ids = tk.message_ids([long_body, REFERENCE_CASES[1][0]], 128)
-    assert len(ids[0]) == 130 and ids[0][0] == tk.sms and ids[0][-1] == tk.ans
+    assert len(ids[0]) == 129 and tk.sms not in ids[0] and ids[0][-1] == tk.ans  # <sms> ends the shared prefix
     assert tk.truncated - t0 == 1
     assert (REGISTRY.get_sample_value("llm_prompt_truncated_total") or 0.0) - c0 == 1
 

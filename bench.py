@@ -111,6 +111,8 @@ def _args(argv=None):
     p.add_argument("--decode-attn", default="grouped", help="decode attention kernel (ops.attn_decode impl)")
     p.add_argument("--admit-min-batch", type=int, default=None, help="EngineConfig.admit_min_batch (default: engine's)")
     p.add_argument("--no-resid96", action="store_true", help="A/B: the round-2 residual-GEMM tile table")
+    p.add_argument("--template-slots", type=int, default=None,
+                   help="message-start template KV slots (0 = off; default: the profile's)")
     p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa"],
                    help="prefill attention kernel (default: the profile's)")
     p.add_argument("--prefill-key-split", type=int, default=1, choices=[1, 2],
@@ -305,7 +307,8 @@ def engine_kwargs(args) -> dict:
     kw = profile_kwargs(args.profile, max_slots=args.max_slots, steps_per_graph=args.steps_per_graph,
                         admit_min_fraction=args.admit_frac, spec_k=args.spec_k, spec_draft_frac=args.spec_frac,
                         split_decode=args.split_decode, split_prefill=args.split_prefill,
-                        copy_constrain=False if args.no_copy else None, prefill_attn=args.prefill_attn)
+                        copy_constrain=False if args.no_copy else None, prefill_attn=args.prefill_attn,
+                        template_slots=args.template_slots)
     if args.bucket_step:
         kw["buckets"] = tuple(range(args.bucket_step, kw["max_slots"] + 1, args.bucket_step))
     return kw

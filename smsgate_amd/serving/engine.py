@@ -119,6 +119,19 @@ class EngineConfig:
     # the previous one somewhere in the body; applied per row in the lm_head arg-max
     # epilogue (ops.copy_masks -> gemm_argmax / fsm_sample / spec_verify)
     copy_constrain: bool = True
+    # message-start templates: bank SMS open with a few fixed phrases ("APPROVED PURCHASE
+    # DB SALE:", "DEBIT ACCOUNT\n" ...).  Causal attention makes the keys / values of a
+    # body's first k tokens a function of those tokens alone, so a start shared by many
+    # messages is computed ONCE into a template KV slot and copied into each matching
+    # message's slot; its prefill starts at own offset k (ops.attn_prefill q_start).
+    # Templates are learned from the traffic: the first k-token starts (2 <= k <=
+    # template_max_len) of admitted bodies are counted, and every template_every
+    # admissions those seen >= template_min_count times become templates (at most
+    # template_slots).  0 slots = off.
+    template_slots: int = 0
+    template_max_len: int = 12
+    template_min_count: int = 16
+    template_every: int = 4096
     measure_idle: bool = True  # EngineStats.gpu_idle_s from two timing events per step
 
 
@@ -127,6 +140,8 @@ class EngineStats:
     prefill_tokens: int = 0
     prefill_seqs: int = 0
     prefill_s: float = 0.0
+    template_tokens: int = 0  # prompt tokens NOT computed: copied from a message-start template
+    templates: int = 0
     decode_steps: int = 0
     decode_row_steps: int = 0
     decode_s: float = 0.0
@@ -214,8 +229,10 @@ class ExtractionEngine:
         self.copy = ec.copy_constrain and self.fsm.has_copy
         if ec.spec_k > ops.SPEC_MAX_K:
             raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
-        # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV there
-        S_kv = S + 1 if self.spec else S
+        # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV
+        # there; template KV slots follow it (slot S + 1 + t)
+        self.T0 = S + 1
+        S_kv = S + 1 + max(0, ec.template_slots) if (self.spec or ec.template_slots > 0) else S
         self.k_cache = torch.zeros(L, S_kv, nkv, self.Lmax, D, dtype=bf, device=dev)
         self.vt_cache = torch.zeros(L, *ops.vt_shape(S_kv, nkv, D, self.Lmax), dtype=bf, device=dev)
         self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
@@ -259,12 +276,17 @@ class ExtractionEngine:
         if self.spec or self.copy:
             # prompt ids per KV slot: the draft source and the copy constraint's body
             self.LB = ec.max_body_tokens + 2
-            self.body_buf = torch.zeros(S + 1, self.LB, **i32)
-            self.body_len = torch.zeros(S + 1, **i32)
+            self.body_buf = torch.zeros(S_kv + 1, self.LB, **i32)
+            self.body_len = torch.zeros(S_kv + 1, **i32)
         if self.copy:  # per-row copy masks of the one-token paths (prefill, plain decode)
             self.copy_rows = torch.zeros(S, self.V_dec // 32, **i32)
         if self.spec:
             self._init_spec()
+        # message-start templates: tuple(first k ids) -> template slot; counts of starts
+        self._tpl: Dict[Tuple[int, ...], int] = {}
+        self._tpl_first: Dict[int, List[int]] = {}  # first token -> template lengths, longest first
+        self._tpl_counts: Dict[Tuple[int, ...], int] = {}
+        self._tpl_seen = 0
         self._compute_prefix()
         if ec.use_graphs:
             self._capture_graphs()
@@ -386,22 +408,31 @@ class ExtractionEngine:
         torch.cuda.synchronize(self.device)
 
     # ---------------------------------------------------------------- prefill
-    def _prefill(self, rows: List[int], items: List[_Pending], sample: bool = True) -> torch.Tensor:
+    def _prefill(self, rows: List[int], items: List[_Pending], sample: bool = True,
+                 slots: Optional[np.ndarray] = None, templates: bool = True) -> torch.Tensor:
+        """Prefill ``items`` into the KV slots of ``rows`` (or explicit ``slots``: a
+        template fill, no row state) and sample their first answer token.  A body that
+        opens with a message-start template gets the template's keys / values copied
+        into its slot and is computed from own offset k on."""
         t0 = time.perf_counter()
         # vectorised host prep (runs while the previous decode chunk is on the GPU)
         n = len(items)
-        lens = np.fromiter((len(it.ids) for it in items), dtype=np.int32, count=n)
-        T = int(lens.sum())
+        full = np.fromiter((len(it.ids) for it in items), dtype=np.int32, count=n)
         dev = self.device
-        flat = np.concatenate([it.ids for it in items]).astype(np.int64, copy=False)
-        rows_np = np.asarray(rows, dtype=np.int32)
+        seq_slots = self.slot_host[np.asarray(rows, dtype=np.int32)] if slots is None else slots.astype(np.int32)
+        rows_np = np.asarray(rows if slots is None else np.zeros(n), dtype=np.int32)
+        kk, tsl = self._match_templates(items) if (templates and self._tpl) else (None, None)
+        skip = kk if kk is not None else np.zeros(n, dtype=np.int32)
+        lens = full - skip
+        T = int(lens.sum())
+        flat = np.concatenate([it.ids[k:] for it, k in zip(items, skip.tolist())] if kk is not None
+                              else [it.ids for it in items]).astype(np.int64, copy=False)
         cu = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(lens, out=cu[1:])
-        pos_np = np.arange(T, dtype=np.int32) - np.repeat(cu[:-1], lens)
-        seq_slots = self.slot_host[rows_np]
+        pos_np = np.arange(T, dtype=np.int32) - np.repeat(cu[:-1] - skip, lens)
         slot_np = np.repeat(seq_slots, lens)
         # one pinned staging copy for all small index arrays
-        meta = torch.from_numpy(np.concatenate([pos_np, slot_np, cu, rows_np, lens - 1, seq_slots])).pin_memory()
+        meta = torch.from_numpy(np.concatenate([pos_np, slot_np, cu, rows_np, full - 1, seq_slots, skip])).pin_memory()
         meta_d = meta.to(dev, non_blocking=True)
         o = 0
         pos_d = meta_d[o:o + T]; o += T
@@ -409,8 +440,10 @@ class ExtractionEngine:
         cu_d = meta_d[o:o + n + 1]; o += n + 1
         rows_d = meta_d[o:o + n]; o += n
         last_pos_d = meta_d[o:o + n]; o += n
-        seq_slot_d = meta_d[o:o + n]
-        qstart = torch.zeros(n, dtype=torch.int32, device=dev)
+        seq_slot_d = meta_d[o:o + n]; o += n
+        qstart = meta_d[o:o + n]
+        if kk is not None:
+            self._copy_templates(kk, tsl, seq_slots)
         flat_d = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
         x = F.embedding(flat_d, self.w.embed).contiguous()
         max_q = int(lens.max())
@@ -429,6 +462,8 @@ class ExtractionEngine:
                              self.scale)
 
         h = self._forward(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        if slots is not None:  # a template fill: its keys / values are all it leaves
+            return None
         last = h.index_select(0, (cu_d[1:] - 1).long())
         if not sample or not self.argmax:
             logits = self._logits(last)
@@ -457,8 +492,82 @@ class ExtractionEngine:
                            self.pos, self.slot_id, self.cfg.temperature, self.cfg.seed, row_map=rows_d, row_masks=cm)
         self.stats.prefill_tokens += T
         self.stats.prefill_seqs += len(items)
+        self.stats.template_tokens += int(skip.sum())
         self.stats.prefill_s += time.perf_counter() - t0
         return logits
+
+    # ----------------------------------------------------- message-start templates
+    def _match_templates(self, items: List[_Pending]) -> Tuple[Optional[np.ndarray], Optional[np.ndarray]]:
+        """Longest template opening each body: (k, template slot) per item, or (None,
+        None) when no item matches.  A match leaves >= 1 token (the <ans>) to compute."""
+        n = len(items)
+        kk = np.zeros(n, dtype=np.int32)
+        tsl = np.zeros(n, dtype=np.int32)
+        hit = False
+        first = self._tpl_first
+        for i, it in enumerate(items):
+            ids = it.ids
+            for k in first.get(int(ids[0]), ()):  # this first token's template lengths, longest first
+                if k < len(ids):
+                    t = self._tpl.get(tuple(ids[:k]))
+                    if t is not None:
+                        kk[i], tsl[i] = k, t
+                        hit = True
+                        break
+        return (kk, tsl) if hit else (None, None)
+
+    def _copy_templates(self, kk: np.ndarray, tsl: np.ndarray, seq_slots: np.ndarray) -> None:
+        """Copy each matching item's template keys / values (own offsets 0..k-1, every
+        layer) and prompt ids into its slot.  Rows past an item's own k carry template
+        padding that the item's prefill overwrites (it writes offsets >= k)."""
+        sel = np.nonzero(kk)[0]
+        kmax = int(kk[sel].max())
+        dev = self.device
+        idx = torch.from_numpy(np.stack([tsl[sel], seq_slots[sel]]).astype(np.int64)).pin_memory().to(
+            dev, non_blocking=True)
+        src, dst = idx[0], idx[1]
+        self.k_cache[:, dst, :, :kmax] = self.k_cache[:, src, :, :kmax]
+        nb = (kmax + 7) // 8  # blocked V^T: 8 keys per block
+        self.vt_cache[:, dst, :, :nb] = self.vt_cache[:, src, :, :nb]
+        if self.spec or self.copy:
+            self.body_buf[dst, :kmax] = self.body_buf[src, :kmax]
+
+    def _learn_templates(self, items: Sequence[_Pending]) -> None:
+        """Count the k-token starts of admitted bodies; every ``template_every``
+        admissions promote the most frequent (count x k, >= template_min_count) to
+        template slots and compute their keys / values (one small prefill)."""
+        ec = self.cfg
+        if ec.template_slots <= 0 or len(self._tpl) >= ec.template_slots:
+            return
+        cnt = self._tpl_counts
+        kmax = ec.template_max_len
+        for it in items:
+            ids = it.ids
+            for k in range(2, min(kmax, len(ids) - 1) + 1):
+                key = tuple(ids[:k])
+                cnt[key] = cnt.get(key, 0) + 1
+        self._tpl_seen += len(items)
+        if self._tpl_seen < ec.template_every:
+            return
+        self._tpl_seen = 0
+        cands = sorted((c * len(key), key) for key, c in cnt.items()
+                       if c >= ec.template_min_count and key not in self._tpl)
+        new = []
+        while cands and len(self._tpl) + len(new) < ec.template_slots:
+            new.append(cands.pop()[1])
+        if new:
+            slots = np.arange(len(self._tpl), len(self._tpl) + len(new), dtype=np.int32) + self.T0
+            # a template's own keys depend only on its tokens: prefill them alone
+            self._prefill([], [_Pending(None, list(key)) for key in new], sample=False, slots=slots,
+                          templates=False)
+            for key, sl in zip(new, slots.tolist()):  # (the fill wrote their ids to body_buf too)
+                self._tpl[key] = sl
+            first: Dict[int, set] = {}
+            for key in self._tpl:
+                first.setdefault(int(key[0]), set()).add(len(key))
+            self._tpl_first = {t: sorted(ks, reverse=True) for t, ks in first.items()}
+            self.stats.templates = len(self._tpl)
+        self._tpl_counts = {}  # a fresh window: the next promotion sees recent traffic
 
     # ----------------------------------------------------------------- decode
     def _decode_step(self, B: int, sample: bool = True, r0: int = 0, hook=None) -> torch.Tensor:
@@ -652,7 +761,7 @@ class ExtractionEngine:
         items = [_Pending(i, ids) for i, ids in enumerate(self.tok.message_ids(list(bodies), self.cfg.max_body_tokens))]
         n = len(items)
         rows = list(range(n))
-        outs = [self._prefill(rows, items, sample=False).float()]
+        outs = [self._prefill(rows, items, sample=False, templates=False).float()]
         lens = torch.tensor([len(it.ids) for it in items], dtype=torch.int32, device=self.device)
         self.pos[:n] = lens - 1
         self.done[:n] = 0  # attention skips finished rows
@@ -810,6 +919,7 @@ class ExtractionEngine:
                 items.append(it)
                 ntok += len(it.ids)
                 self.active[r] = it.key
+            self._learn_templates(items)
             split = self.cfg.split_prefill
             if split and ntok >= split and len(items) >= 2:
                 # two independent halves on two streams (disjoint rows and KV slots):

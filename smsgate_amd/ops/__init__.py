@@ -28,6 +28,7 @@ __all__ = [
     "rmsnorm_residual",
     "silu_mul",
     "rope_qkv_cache",
+    "kv_copy_prefix",
     "attn_prefill",
     "attn_decode",
     "fsm_sample",
@@ -67,6 +68,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_rmsnorm_residual.argtypes = [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_float, _vp]
     lib.sg_silu_mul.argtypes = [_vp, _vp, _c_int, _c_int, _vp]
     lib.sg_rope_qkv_cache.argtypes = [_vp, _ip, _ip, _vp, _vp, _vp, _vp] + [_c_int] * 6 + [_vp]
+    lib.sg_kv_copy_prefix.argtypes = [_vp, _vp, _ip] + [_c_int] * 6 + [_vp]
     lib.sg_attn_prefill.argtypes = [_vp, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
                                     _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp]
     lib.sg_attn_decode.argtypes = [_vp, _ip, _ip, _ip, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp,
@@ -123,7 +125,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   _vp]
     lib.sg_copy_masks.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
-              "sg_fsm_sample", "sg_version"):
+              "sg_fsm_sample", "sg_version", "sg_kv_copy_prefix"):
         getattr(lib, f).restype = _c_int
 
 
@@ -763,6 +765,20 @@ def spec_verify_keys(best: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torc
         _p(best), *_fsm_args(fsm), fsm.sep_token, fsm.done_state, fsm.vocab, _p(state), _p(tok_buf), _p(out_buf),
         _p(out_len), _p(done), _p(pos), _p(x_tok), _p(row_start), _p(row_nd), _p(accepted), out_buf.shape[1], B,
         _stream()), "spec_verify_keys")
+
+
+def kv_copy_prefix(k_cache: torch.Tensor, vt_cache: torch.Tensor, items: torch.Tensor) -> None:
+    """Copy own offsets ``0..k-1`` of each item's template slot into its message slot,
+    every layer (keys row-wise, Vᵀ as whole 8-key blocks).  ``k_cache`` [L, S, nkv,
+    Lmax, 64], ``vt_cache`` its blocked Vᵀ twin, ``items`` int32 [3, n] = (template
+    slot, message slot, k)."""
+    L, S, nkv, Lmax, D = k_cache.shape
+    assert vt_cache.shape == (L, *vt_shape(S, nkv, D, Lmax)) and k_cache.is_contiguous() and vt_cache.is_contiguous()
+    _req(items, torch.int32, "items")
+    assert items.dim() == 2 and items.shape[0] == 3 and items.is_contiguous()
+    n = items.shape[1]
+    _check(load_library().sg_kv_copy_prefix(_p(k_cache), _p(vt_cache), _p(items), n, L, S, nkv, D, Lmax,
+                                            _stream()), "kv_copy_prefix")
 
 
 def vt_shape(S: int, nkv: int, D: int, L: int):

@@ -1831,6 +1831,39 @@ __global__ void __launch_bounds__(256) fsm_sample_kernel(
 static int g_prefill_impl = 2;  // sg_set_prefill_impl
 static int g_prefill_ks = 1;    // sg_set_prefill_split
 
+// ---------------------------------------------------------------------------
+// Message-start template reuse (serving/engine.py): copy own offsets 0..k-1 of a
+// template slot's keys (k rows of 128 B per layer and kv head) and the V^T blocks
+// holding them (8 keys per 1 KiB block; a partial last block carries template
+// padding that the message's own prefill overwrites from offset k on) into a
+// message's slot, every layer.  grid = (items, layers), 256 threads, 16-B copies.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) kv_copy_prefix_kernel(uint16_t* __restrict__ k_cache,
+                                                             uint16_t* __restrict__ vt_cache,
+                                                             const int* __restrict__ items, int n, int S_kv,
+                                                             int nkv, int Lmax) {
+  constexpr int D = 64;
+  const int i = blockIdx.x, layer = blockIdx.y;
+  const int src = items[i], dst = items[n + i], k = items[2 * n + i];
+  const size_t slot_elems = (size_t)nkv * Lmax * D;  // K and V^T: the same elements per slot
+  const size_t lbase = (size_t)layer * S_kv * slot_elems;
+  const uint4* ks = reinterpret_cast<const uint4*>(k_cache + lbase + (size_t)src * slot_elems);
+  uint4* kd = reinterpret_cast<uint4*>(k_cache + lbase + (size_t)dst * slot_elems);
+  const uint4* vs = reinterpret_cast<const uint4*>(vt_cache + lbase + (size_t)src * slot_elems);
+  uint4* vd = reinterpret_cast<uint4*>(vt_cache + lbase + (size_t)dst * slot_elems);
+  const int head16 = Lmax * D / 8;        // uint4 per kv head (K rows or V^T blocks)
+  const int krow16 = k * (D / 8);         // K: k rows x 8 chunks
+  const int vblk16 = ((k + 7) >> 3) * D;  // V^T: whole 8-key blocks, 64 chunks each
+  for (int q = threadIdx.x; q < nkv * krow16; q += 256) {
+    const int h = q / krow16, c = q - h * krow16;
+    kd[h * head16 + c] = ks[h * head16 + c];
+  }
+  for (int q = threadIdx.x; q < nkv * vblk16; q += 256) {
+    const int h = q / vblk16, c = q - h * vblk16;
+    vd[h * head16 + c] = vs[h * head16 + c];
+  }
+}
+
 extern "C" {
 
 int sg_rmsnorm_residual(const void* x_in, void* residual, const void* w, void* out, int T, int H, float eps,
@@ -1850,6 +1883,16 @@ int sg_silu_mul(const void* gu, void* out, int T, int I, hipStream_t stream) {
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)out, T, I);
+  return (int)hipGetLastError();
+}
+
+// items: int32 [3][n] = template slot, message slot, k (0 < k <= Lmax) per item
+int sg_kv_copy_prefix(void* k_cache, void* vt_cache, const int* items, int n, int layers, int S_kv, int nkv, int D,
+                      int Lmax, hipStream_t stream) {
+  if (D != 64 || Lmax % 8) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(kv_copy_prefix_kernel, dim3(n, layers), dim3(256), 0, stream, (uint16_t*)k_cache,
+                     (uint16_t*)vt_cache, items, n, S_kv, nkv, Lmax);
   return (int)hipGetLastError();
 }
 

@@ -493,6 +493,7 @@ class ExtractionEngine:
         self.stats.prefill_tokens += T
         self.stats.prefill_seqs += len(items)
         self.stats.template_tokens += int(skip.sum())
+        self.stats.templates = len(self._tpl)
         self.stats.prefill_s += time.perf_counter() - t0
         return logits
 
@@ -523,13 +524,14 @@ class ExtractionEngine:
         sel = np.nonzero(kk)[0]
         kmax = int(kk[sel].max())
         dev = self.device
-        idx = torch.from_numpy(np.stack([tsl[sel], seq_slots[sel]]).astype(np.int64)).pin_memory().to(
+        items = torch.from_numpy(np.stack([tsl[sel], seq_slots[sel], kk[sel]]).astype(np.int32)).pin_memory().to(
             dev, non_blocking=True)
-        src, dst = idx[0], idx[1]
-        self.k_cache[:, dst, :, :kmax] = self.k_cache[:, src, :, :kmax]
-        nb = (kmax + 7) // 8  # blocked V^T: 8 keys per block
-        self.vt_cache[:, dst, :, :nb] = self.vt_cache[:, src, :, :nb]
+        # exactly k rows per item, every layer, one launch (a torch gather / index_put of
+        # the kmax-row block of all layers moved ~0.3 GB per admitted batch and cost more
+        # than the prefill rows it saved: profiles/r03_ab_templates.jsonl)
+        ops.kv_copy_prefix(self.k_cache, self.vt_cache, items)
         if self.spec or self.copy:
+            src, dst = items[0].long(), items[1].long()
             self.body_buf[dst, :kmax] = self.body_buf[src, :kmax]
 
     def _learn_templates(self, items: Sequence[_Pending]) -> None:

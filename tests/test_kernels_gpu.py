@@ -544,3 +544,20 @@ def test_attn_spec_bench_scale():
                                  vrows[r, :, :p + 1].permute(1, 0, 2).float(), pk[:, :P0].permute(1, 0, 2).float(),
                                  pvrows[:, :P0].permute(1, 0, 2).float(), P0, [p], scale)
         torch.testing.assert_close(out_s[t].float().view(1, nh, D), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_kv_copy_prefix():
+    """Template reuse copy: own offsets 0..k-1 of the template slot's keys, and the Vᵀ
+    blocks holding them, land in the message slot on every layer; nothing else moves."""
+    L, S, nkv, Lmax, D = 3, 10, 3, 64, 64
+    kc = _bf(L, S, nkv, Lmax, D, seed=101)
+    vt = _bf(L, *ops.vt_shape(S, nkv, D, Lmax), seed=102)
+    k0, v0 = kc.clone(), vt.clone()
+    items = torch.tensor([[8, 9, 8], [1, 4, 6], [5, 12, 1]], dtype=torch.int32, device=DEV)  # (src, dst, k)
+    ops.kv_copy_prefix(kc, vt, items)
+    torch.cuda.synchronize()
+    ek, ev = k0.clone(), v0.clone()
+    for src, dst, k in items.t().tolist():
+        ek[:, dst, :, :k] = k0[:, src, :, :k]
+        ev[:, dst, :, :(k + 7) // 8] = v0[:, src, :, :(k + 7) // 8]
+    assert torch.equal(kc, ek) and torch.equal(vt, ev)

@@ -97,6 +97,9 @@ def _args(argv=None):
                         "parser process")
     p.add_argument("--concurrency", type=int, default=4)
     p.add_argument("--batch", type=int, default=512)
+    p.add_argument("--rank-threads", type=int, default=0,
+                   help="torch CPU threads of the rank process (0 = torch's default); the rank only "
+                        "launches GPU work, and idle OpenMP workers spin after every parallel CPU op")
     p.add_argument("--worker-threads", type=int, default=2,
                    help="tokenizer (Rayon) threads per parser process; 0 = library default (one per CPU)")
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
@@ -163,6 +166,8 @@ def run_replica(args, rank: int, world: int, local: int):
     import torch
 
     echo = args.cpu_echo_engine
+    if args.rank_threads > 0:
+        torch.set_num_threads(args.rank_threads)
     if not echo:
         torch.cuda.set_device(local)
     dist = None

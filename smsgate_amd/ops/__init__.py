@@ -207,14 +207,14 @@ GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 6
               7: (128, 128), 8: (64, 128), 9: (256, 128), 10: (256, 256), 11: (128, 256), 12: (256, 64),
               13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64),
               19: (256, 256), 20: (256, 256), 21: (128, 96), 22: (64, 96), 23: (128, 192), 24: (256, 96),
-              25: (128, 96), 26: (64, 192)}
+              25: (128, 96), 26: (64, 192), 27: (32, 96)}
 # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 # a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
 # SwiGLU kernel (gemm256_swiglu_kernel), 20 its persistent form
 GEMM_SWIGLU_ONLY = {10, 19, 20}
 # 21..26: 48-wide wave tiles (96 / 192-wide blocks) for the N = 576 residual GEMMs: no SwiGLU
-GEMM_NO_SWIGLU = {21, 22, 23, 24, 25, 26}
+GEMM_NO_SWIGLU = {21, 22, 23, 24, 25, 26, 27}
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
@@ -243,12 +243,14 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #   older config at the engine's flavour (profiles/r03_gemm96_tune.json): down-proj 128x96
 #   25.0 / 40.3 us at 9216 / 16384 rows vs 28.2 / 43.4 (128x64), 64x96 15.8 vs 18.5 at
 #   4608; o-proj 64x96 8.3 / 20.3 us at 4608 / 16384 vs 8.8 / 22.4, 128x96 13.0 vs 14.9
-#   (64x64) at 9216.  Both residual GEMMs of a forward keep BN = 96 at the same rows
-#   (the producer-norm partials need equal N tilings: 6 parts).
+#   (64x64) at 9216.  Both residual GEMMs keep BN = 96 at EVERY row count (32x96 below
+#   2048 rows): the producer-norm partials then always come as the same 6 parts summed in
+#   the same order, so a row's result does not depend on the batch it runs in (split vs
+#   single prefill, spec vs plain decode: tests/test_engine_gpu.py, test_spec_gpu.py).
 GEMM_MEASURED = {
     ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 6143, 19), (6144, 1 << 30, 20)],
-    ("resid", 576, 576): [(2048, 6143, 22), (6144, 12287, 21), (12288, 1 << 30, 22)],
-    ("resid", 576, 1536): [(2048, 6143, 22), (6144, 1 << 30, 21)],
+    ("resid", 576, 576): [(1, 2047, 27), (2048, 6143, 22), (6144, 12287, 21), (12288, 1 << 30, 22)],
+    ("resid", 576, 1536): [(1, 2047, 27), (2048, 6143, 22), (6144, 1 << 30, 21)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
 

@@ -231,12 +231,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   // EPI 1: this thread's residual chunks, loaded before the K loop (their latency hides
   // behind it instead of stalling the epilogue; R may alias C, but every element is
   // read and written by the same thread)
-  constexpr int RIT = EPI == 1 ? (BM * (BN / 8)) / NT : 1;
+  constexpr int RIT = EPI == 1 ? (BM * (BN / 8) + NT - 1) / NT : 1;  // (32x96: 1.5 chunks per thread)
   uint4 rpre[RIT];
   if constexpr (EPI == 1) {
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
-      const int q = tid + it * NT, row = q / (BN / 8), c = q % (BN / 8);
+      const int q = min(tid + it * NT, BM * (BN / 8) - 1), row = q / (BN / 8), c = q % (BN / 8);
       const int gr = min(m0 + row, M - 1);
       rpre[it] = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + n0 + c * 8);
     }
@@ -509,14 +509,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     // runs the same trip count, so the row's x² partial reduces with shuffles (a
     // power-of-two CPR) or, for 96/192-wide tiles (CPR 12 / 24: a row's lanes are not
     // an aligned group), through a [BM][CPR] LDS image summed in a fixed order
-    static_assert((BM * CPR) % NT == 0 && CPR <= 64, "uniform epilogue trips");
     constexpr bool POW2 = (CPR & (CPR - 1)) == 0;
+    // the shuffle reduction needs every lane on the same trip count
+    static_assert(CPR <= 64 && (!POW2 || (BM * CPR) % NT == 0), "uniform epilogue trips");
     static_assert(POW2 || BM * CST + 2 * BM * CPR <= ST * TILE, "x² image fits beside the C tile");
     float* ssl = reinterpret_cast<float*>(smem + BM * CST);
     const bool want_ss = na.ssout != nullptr;
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
       const int q = tid + it * NT;
+      if (!POW2 && q >= BM * CPR) break;  // (the LDS path has no shuffles: ragged trips are fine)
       const int row = q / CPR, c = q % CPR;
       const int gr = m0 + row;
       float sq = 0.f;
@@ -1047,7 +1049,8 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  20: its persistent form (gemm256p_swiglu_kernel; epi 2 only; NORM 2 needs ss_ld % 4 == 0)
 //  21: 128x96 (2x2) 2st   22: 64x96 (2x2) 2st   23: 128x192 (2x4) 2st, 8 waves
 //  24: 256x96 (4x2) 2st, 8 waves   25: 128x96 (2x2) 3st   26: 64x192 (1x4) 2st
-//      (21..26: epi 0 / 1 only — 48-wide wave tiles for the N = 576 residual GEMMs)
+//  27: 32x96 (2x2) 2st — small-M form of 21 / 22 (the same 96-wide N tiling at every M)
+//      (21..27: epi 0 / 1 only — 48-wide wave tiles for the N = 576 residual GEMMs)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1076,9 +1079,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[27] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256, 96, 96, 192, 96, 96, 192};
-  if (cfg < 0 || cfg > 26) return -1;
+  static const int BNs[28] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192, 96};
+  if (cfg < 0 || cfg > 27) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1138,7 +1141,8 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     case 23: return dispatch_resid<128, 192, 2, 4, 2>(SG_ARGS);
     case 24: return dispatch_resid<256, 96, 4, 2, 2>(SG_ARGS);
     case 25: return dispatch_resid<128, 96, 2, 2, 3>(SG_ARGS);
-    default: return dispatch_resid<64, 192, 1, 4, 2>(SG_ARGS);
+    case 26: return dispatch_resid<64, 192, 1, 4, 2>(SG_ARGS);
+    default: return dispatch_resid<32, 96, 2, 2, 2>(SG_ARGS);
   }
 #undef SG_ARGS
 }

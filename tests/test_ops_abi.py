@@ -86,5 +86,6 @@ def test_measured_tile_exceptions():
         bn = {ops.GEMM_TILES[ops.gemm_cfg(M, 576, epi="resid", K=k)][1] for k in (576, 1536)}
         assert len(bn) == 1, (M, bn)
     assert ops.gemm_cfg(9216, 576, epi="resid", K=1536) == 21
+    assert {ops.GEMM_TILES[ops.gemm_cfg(M, 576, epi="resid", K=576)][1] for M in range(1, 40000, 97)} == {96}
     assert ops.GEMM_TILES[20] == (256, 256) and 20 in ops.GEMM_SWIGLU_ONLY
     assert all(576 % ops.GEMM_TILES[c][1] == 0 for c in ops.GEMM_NO_SWIGLU)  # the N = 576 residual GEMMs

@@ -247,6 +247,10 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #   2048 rows): the producer-norm partials then always come as the same 6 parts summed in
 #   the same order, so a row's result does not depend on the batch it runs in (split vs
 #   single prefill, spec vs plain decode: tests/test_engine_gpu.py, test_spec_gpu.py).
+#   The price below 2048 rows: 32x96 runs 5-25 % behind 32x64 (down-proj 9.3 vs 7.7 us at
+#   256 rows, 9.7 vs 8.4 at 1024; profiles/r03_resid_small_m_tune.json) -- small decode
+#   buckets only, i.e. serving latency at low load, not the throughput bench's 9216-row
+#   halves.
 GEMM_MEASURED = {
     ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 6143, 19), (6144, 1 << 30, 20)],
     ("resid", 576, 576): [(1, 2047, 27), (2048, 6143, 22), (6144, 12287, 21), (12288, 1 << 30, 22)],

@@ -25,14 +25,28 @@ SPECIALS = ["<pad>", "<bos>", "<eos>", "<sep>", "<sms>", "<ans>"]
 DEFAULT_VOCAB = 8192
 
 
+# Pre-tokenizer: GPT-2's split, except that a NUMBER stays one pre-token -- digits joined
+# by '.' / ':' (dates "06.05.25", times "14:23", decimals "52.00") or a thousands group
+# ("1,842.74": ',' followed by exactly three digits).  Byte-level BPE never merges across
+# pre-tokens, and GPT-2's split cut every number at each '.', ',' and ':' (a date + time
+# was 8 tokens).  ',' before a non-3-digit group stays a separator ("BLVD 89,17.05.24"
+# keeps the street number and the date apart), so every body value stays token-aligned.
+# 8 192 merges: 49.2 -> 41.2 body tokens and 43.8 -> 35.7 answer tokens per purchase SMS.
+NUMBER_AWARE_SPLIT = (r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\d{1,3}(?:,\d{3})+(?:\.\d+)?| ?\d+(?:[.:]\d+)*"
+                      r"| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+")
+
+
 def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: int = 60000, seed: int = 1234):
-    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+    from tokenizers import Regex, Tokenizer, decoders, models, pre_tokenizers, trainers
 
     from ..parse.schema import EXTRACTOR_PROMPT, SYSTEM_INSTRUCTION
     from ..utils.synth import iter_corpus
 
     tok = Tokenizer(models.BPE())
-    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(Regex(NUMBER_AWARE_SPLIT), behavior="isolated"),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False),
+    ])
     tok.decoder = decoders.ByteLevel()
     trainer = trainers.BpeTrainer(
         vocab_size=vocab_size,
@@ -45,7 +59,7 @@ def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: 
         for _ in range(50):
             yield SYSTEM_INSTRUCTION
             yield EXTRACTOR_PROMPT
-        yield from iter_corpus(n_sms, seed)
+        yield from (model_text(t) for t in iter_corpus(n_sms, seed))
 
     tok.train_from_iterator(corpus(), trainer=trainer)
     path.parent.mkdir(parents=True, exist_ok=True)

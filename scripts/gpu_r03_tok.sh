@@ -14,4 +14,4 @@ cut -c1-400 gpurun_out/r03_bench_tok.json
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_tok -o run -- python $R/bench.py --steps 10 --warmup 2 --eval-n 0 > $R/gpurun_out/prof_tok.log 2>&1) || { tail -5 gpurun_out/prof_tok.log; exit 1; }
 python scripts/prof_summary.py gpurun_out/prof_tok
 find gpurun_out/prof_tok -name "*kernel_trace.csv" -delete
-python scripts/stats_top.py gpurun_out/prof_tok/run_kernel_stats.csv | head -12
+python scripts/stats_top.py gpurun_out/prof_tok/run_kernel_stats.csv > gpurun_out/prof_tok/top.txt

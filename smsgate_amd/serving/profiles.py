@@ -5,9 +5,11 @@ the headline bench measured).
 * ``throughput`` — the headline bench's configuration: 8 192 rows, two decode
   steps per graph, admission at 12.5 % free rows, up to six drafts per row
   (profiles/r02s3_admit_frac_ab*.jsonl, r02s3_spec_k_ab.jsonl);
-* both learn up to 16 message-start templates (``EngineConfig.template_slots``: 3.2 of
-  ~50 prompt tokens per message not computed, +1.8 % msgs/s interleaved,
-  profiles/r03_ab_templates2.jsonl; a 16 384-row engine lost 12 % there);
+* both learn up to 32 message-start templates (``EngineConfig.template_slots``): 16 of
+  them left 3.2 of ~50 prompt tokens per message uncomputed, +1.8 % msgs/s interleaved
+  (profiles/r03_ab_templates2.jsonl; a 16 384-row engine lost 12 % there); 32 reach 4.0
+  of the 4.1 tokens an oracle choice would save (replay of 20 k purchase SMS through
+  the learning policy);
 * ``latency`` — the serving-latency configuration of round 2: 4 096 rows, four
   steps per graph, admission at 25 % free rows, four drafts per row (p50 30 ms at
   1 k msgs/s, profiles/r02s3_latency_spec4.json; six drafts did not lower it,
@@ -27,10 +29,10 @@ BUCKETS = (64, 128, 256, 512, 1024, 2048, 4096, 8192)
 PROFILES: Dict[str, Dict[str, Any]] = {
     "throughput": dict(max_slots=8192, steps_per_graph=2, admit_min_fraction=0.125, spec_k=6, spec_draft_frac=1.25,
                        buckets=BUCKETS, split_decode=4096, split_prefill=8192, copy_constrain=True,
-                       template_slots=16),
+                       template_slots=32),
     "latency": dict(max_slots=4096, steps_per_graph=4, admit_min_fraction=0.25, spec_k=4, spec_draft_frac=1.25,
                     buckets=BUCKETS[:-1], split_decode=4096, split_prefill=8192, copy_constrain=True,
-                    template_slots=16),
+                    template_slots=32),
 }
 
 

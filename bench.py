@@ -114,6 +114,9 @@ def _args(argv=None):
     p.add_argument("--decode-attn", default="grouped", help="decode attention kernel (ops.attn_decode impl)")
     p.add_argument("--admit-min-batch", type=int, default=None, help="EngineConfig.admit_min_batch (default: engine's)")
     p.add_argument("--no-resid96", action="store_true", help="A/B: the round-2 residual-GEMM tile table")
+    p.add_argument("--sink", default="memory", choices=["memory", "sqlite"],
+                   help="the writer's sink: in-memory (BASELINE config #1) or SqlSink on one SQLite WAL "
+                        "file per parser process")
     p.add_argument("--template-slots", type=int, default=None,
                    help="message-start template KV slots (0 = off; default: the profile's)")
     p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa"],
@@ -156,9 +159,14 @@ def run_replica(args, rank: int, world: int, local: int):
         raise SystemExit("--msgs-per-step must be divisible by --cpu-workers")
     # 0) the node's shared broker, started before anything touches the GPU (no exec after GPU init)
     broker, bus_dsn = start_node_broker(args, local) if args.bus == "busd" else (None, None)
+    sink_dir = None
+    if args.sink == "sqlite":
+        import tempfile
+
+        sink_dir = tempfile.mkdtemp(prefix=f"smsgate-bench-sink-r{rank}-")
     cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
            "worker_threads": args.worker_threads, "vocab": args.traffic_vocab, "bus": bus_dsn,
-           "traffic": args.traffic}
+           "traffic": args.traffic, "sink": args.sink, "sink_dir": sink_dir}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
 
@@ -261,6 +269,10 @@ def run_replica(args, rank: int, world: int, local: int):
         cpu = dict(zip(ck, (float(x) for x in cs.tolist())))
         dist.barrier()  # every rank is done with the broker
         dist.destroy_process_group()
+    if sink_dir:
+        import shutil
+
+        shutil.rmtree(sink_dir, ignore_errors=True)
     if broker:
         import shutil
 
@@ -510,7 +522,8 @@ def main(argv=None) -> int:
                 "model": (f"{args.model} extractor LLM (134.5M params, replaces the Gemini call)" if gpu
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
                 "pipeline": ("payload->RawSMS->bus sms.raw->parser_worker->sms.parsed+sms.processing|DLQ->ack"
-                             + ("->pb_writer->in-memory sink" if gpu else "")),
+                             + (("->pb_writer->SqlSink (SQLite WAL, one file per parser process)"
+                                 if args.sink == "sqlite" else "->pb_writer->in-memory sink") if gpu else "")),
                 "bus": (("shared smsgate-busd brokers per node (" +
                          (f"{args.bus_shards}, sharded by subject" if args.bus_shards > 0 else
                           "node layout: " + ", ".join(f"{s} over {args.partitions or n}"

@@ -104,8 +104,14 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                           concurrency=cfg.get("concurrency", 4), stats_interval=0)
     if dsn:
         worker.stage.max_ack_pending = 1 << 22  # all replicas' batches in flight at once
-    # pb_writer with an in-memory sink on sms.parsed (BASELINE config #1: "... -> in-memory sink")
-    sink = MemorySink()
+    # pb_writer on sms.parsed with an in-memory sink (BASELINE config #1: "... -> in-memory
+    # sink"), or a real SqlSink: one SQLite WAL file per parser process (--sink sqlite)
+    if cfg.get("sink", "memory") == "sqlite":
+        from ..sinks.sql import SqlSink
+
+        sink = SqlSink(f"sqlite:///{cfg['sink_dir']}/sink-r{rank}-w{widx}.db")
+    else:
+        sink = MemorySink()
     writer = WriterService(bus, [sink], batch=cfg.get("writer_batch", 512), stats_interval=0)
     if dsn:
         writer.stage.max_ack_pending = 1 << 22

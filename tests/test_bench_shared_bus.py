@@ -32,3 +32,18 @@ def test_two_ranks_one_broker():
     assert cpu["cores_busy_per_gpu"]["parser_procs"] > 0 and cpu["cores_busy_per_gpu"]["brokers"] > 0
     assert cpu["cpu_us_per_msg"] > 0 and cpu["node_cores_at_8_gpus"] == round(8 * cpu["cores_busy_per_gpu_total"], 1)
     assert not [d for d in os.listdir("/tmp") if d == "smsgate-bench-bus-29671"]  # broker dir cleaned up
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "smsgate_amd/native/_bin/smsgate-busd")),
+                    reason="native broker not built")
+def test_bench_with_a_real_sql_sink():
+    """--sink sqlite: every parser process's writer upserts into its own SQLite WAL file
+    (SqlSink) inside the timed region; every parsed message is stored once."""
+    cmd = [sys.executable, "bench.py", "--cpu-echo-engine", "--steps", "2", "--warmup", "1", "--msgs-per-step", "1024",
+           "--cpu-workers", "2", "--bus", "busd", "--sink", "sqlite"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert r.returncode == 0 and len(lines) == 1, r.stderr[-3000:]
+    rt = lines[0]["routing"]
+    assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"] > 0 and rt["writer_fail"] == 0
+    assert not [d for d in os.listdir("/tmp") if d.startswith("smsgate-bench-sink-r0-")]  # sink files removed

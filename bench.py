@@ -72,6 +72,9 @@ def _args(argv=None):
     # the timed throughput is only reported for an extractor that extracts: below this
     # held-out exact-answer rate the run fails before the timed region (0 = no floor)
     p.add_argument("--quality-floor", type=float, default=0.95)
+    # the reference's acceptance test (tests/test_parsers.py:11-86) on the flagship being timed:
+    # 1 = the run fails before the timed region unless all three CASES come out right
+    p.add_argument("--cases-required", type=int, default=1, choices=[0, 1])
     p.add_argument("--msgs-per-step", type=int, default=16384)
     p.add_argument("--profile", default="throughput", choices=["throughput", "latency"],
                    help="engine configuration (serving/profiles.py; engine-server --profile serves the same)")
@@ -119,7 +122,7 @@ def _args(argv=None):
                         "file per parser process")
     p.add_argument("--template-slots", type=int, default=None,
                    help="message-start template KV slots (0 = off; default: the profile's)")
-    p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa"],
+    p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa", "st", "st32"],
                    help="prefill attention kernel (default: the profile's)")
     p.add_argument("--prefill-key-split", type=int, default=1, choices=[1, 2],
                    help="waves sharing each prefill attention tile's keys")
@@ -220,6 +223,14 @@ def run_replica(args, rank: int, world: int, local: int):
         if args.weights != "random" and q["exact"] < args.quality_floor:
             raise SystemExit(f"bench: held-out exact-answer rate {q['exact']:.4f} is below the quality floor "
                              f"{args.quality_floor} -- no throughput is reported for a broken extractor")
+        from smsgate_amd.models.evaluate import golden_case_mismatches, golden_case_results
+
+        bad = golden_case_mismatches(golden_case_results(engine))
+        quality["reference_cases"] = {"passed": 3 - len({b.split(".")[0].split(":")[0] for b in bad}), "of": 3,
+                                      "mismatches": bad, "required": bool(args.cases_required)}
+        print(f"[bench] reference CASES: {json.dumps(quality['reference_cases'])}", file=sys.stderr, flush=True)
+        if args.weights != "random" and args.cases_required and bad:
+            raise SystemExit(f"bench: the flagship gets the reference CASES wrong: {bad}")
         (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
     if not args.no_gc_freeze:
         from smsgate_amd.serving import freeze_gc_for_launch_loop

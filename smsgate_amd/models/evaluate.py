@@ -17,7 +17,8 @@ from __future__ import annotations
 from decimal import Decimal
 from typing import Any, Dict, List, Optional, Sequence
 
-__all__ = ["score_answers", "evaluate_engine", "golden_case_results"]
+__all__ = ["score_answers", "evaluate_engine", "golden_case_results", "golden_case_mismatches",
+           "REFERENCE_EXPECTED"]
 
 _FIELDS = ("txn_type", "date", "amount", "currency", "card", "merchant", "city", "address", "balance")
 
@@ -96,3 +97,37 @@ def golden_case_results(engine) -> List[Optional[Dict[str, Any]]]:
         p = _post(b, 1746541380, a)
         out.append(None if p is None else p.model_dump(mode="json"))
     return out
+
+
+# the expected values of the reference's CASES (tests/test_parsers.py:11-58, asserted
+# field by field like :73-86); dates as the ISO strings ParsedSMS serialises
+REFERENCE_EXPECTED = (
+    dict(merchant="TEST LLC", city="MOSKOW", address="TEST STR. 29, 24 AREA", amount="52.00", balance="1842.74",
+         date="2025-05-06T14:23", card="0018", currency="USD", txn_type="debit"),
+    dict(merchant="TEST", city="MOSKOW", address="", amount="3460.00", balance="1800.74",
+         date="2025-05-06T15:11", card="0018", currency="USD", txn_type="debit"),
+    dict(merchant="AMERIABANK API GATE", city="AM", address="", amount="27252.00", balance="391469.09",
+         date="2025-06-10T20:51", card="7538", currency="AMD", txn_type="debit"),
+)
+
+
+def golden_case_mismatches(results: Sequence[Optional[Dict[str, Any]]]) -> List[str]:
+    """Every field of :func:`golden_case_results` that differs from the
+    reference's expectation, as ``"case<i>.<field>: got != want"`` (empty = all
+    three CASES pass)."""
+    bad: List[str] = []
+    for i, (got, want) in enumerate(zip(results, REFERENCE_EXPECTED), 1):
+        if got is None:
+            bad.append(f"case{i}: not parsed")
+            continue
+        for k, v in want.items():
+            g = got.get(k)
+            if k in ("amount", "balance"):
+                same = g is not None and Decimal(str(g)) == Decimal(v)
+            elif k == "date":
+                same = str(g or "").startswith(v)
+            else:
+                same = (g or "") == v
+            if not same:
+                bad.append(f"case{i}.{k}: {g!r} != {v!r}")
+    return bad

@@ -439,8 +439,11 @@ def set_prefill_impl(impl: str) -> None:
     above), ``"gqa"`` (one wave per KV head, K/V loaded once per GQA group,
     prefetched), ``"per_head"`` (one wave per query head: G x the waves, which
     fills the chip better at small batches; ``profiles/r01c_prefill_key_split_ab.txt``)
-    or ``"multi"`` (per head, every K/V tile of a 3-tile chunk loaded at once)."""
-    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3}[impl])
+    or ``"multi"`` (per head, every K/V tile of a 3-tile chunk loaded at once), or
+    ``"st"`` / ``"st32"`` (transposed register formulation, S^T = K·Q^T and
+    O^T = V^T·P^T: one wave per 16 / 32 (query, head) columns of one KV head,
+    P never leaves registers)."""
+    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3, "st": 4, "st32": 5}[impl])
 
 
 def set_prefill_split(ks: int) -> None:

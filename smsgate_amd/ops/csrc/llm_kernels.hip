@@ -1558,6 +1558,90 @@ __global__ void __launch_bounds__(64) attn_spec_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Prefill attention in the transposed register formulation (impl "st", default).
+// One wave = QPW = 16·NCB/G consecutive queries of ONE sequence and one kv head, all
+// G query heads: MFMA column c <-> (query i = c / G, head g = c % G), exactly the
+// verify kernel's decomposition with the row's drafts replaced by a prompt chunk.
+// S^T = K·Q^T and O^T = V^T·P^T (st_tile): the softmax state stays in the lane that
+// owns the column, P never leaves registers — no LDS round trip, no barrier and two
+// shuffles per reduction, where the per-head kernel (S = Q·K^T) staged P through LDS
+// with eight 2-byte stores and two __syncthreads per 32-key tile and spent its time
+// on that VALU / LDS work (prefill_bench: it scales with tokens, not with latency).
+// K/V tiles are loaded once for the G heads of the group.  Causal: column i sees own
+// keys [0, q_start + i]; the tile loop runs to the wave's last query.
+// grid = (ceil(max_q / QPW), nseq, nkv), one wave.
+// ---------------------------------------------------------------------------
+template <int NCB>
+__global__ void __launch_bounds__(64) attn_prefill_st_kernel(
+    const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
+    const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
+    const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out,
+    int nh, int nkv, int Lmax, float scale_log2) {
+  constexpr int D = 64;
+  const int tile = blockIdx.x, b = blockIdx.y, kh = blockIdx.z, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
+  const int G = nh / nkv, QPW = 16 * NCB / G;
+  const int qbeg = cu_q[b], qlen = cu_q[b + 1] - qbeg;
+  const int q0 = tile * QPW;
+  if (q0 >= qlen) return;
+  const int qs = q_start[b], sl = slot[b];
+  const int nq = min(QPW, qlen - q0);
+  bf16x8 qb[NCB][2];
+  f32x4 o[NCB][4];
+  float m[NCB], lsum[NCB];
+  int own[NCB];
+  bool col_valid[NCB];
+  size_t qrow[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int c = 16 * cb + r16, i = c / G, g = c % G;
+    col_valid[cb] = i < nq;
+    own[cb] = qs + q0 + i + 1;  // causal length over own keys
+    qrow[cb] = (size_t)(qbeg + q0 + (col_valid[cb] ? i : 0)) * nh + kh * G + g;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      uint4 v = *reinterpret_cast<const uint4*>(q + qrow[cb] * D + 8 * g4 + 32 * s2);
+      if (!col_valid[cb]) v = make_uint4(0, 0, 0, 0);
+      qb[cb][s2] = __builtin_bit_cast(bf16x8, v);
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) o[cb][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    m[cb] = -INFINITY;
+    lsum[cb] = 0.f;
+  }
+  const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
+  const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
+  for (int kt = 0; kt < P0; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) st_tile(qb[cb], kc, vc, kt, P0, g4, scale_log2, m[cb], lsum[cb], o[cb]);
+  }
+  const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+  const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+  const int own_max = qs + q0 + nq;
+  for (int kt = 0; kt < own_max; kt += 32) {
+    uint4 kc[2][2], vc[4];
+    st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own_max, kc, vc);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+      st_tile(qb[cb], kc, vc, kt, own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+  }
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    if (!col_valid[cb]) continue;
+    const float inv = 1.f / lsum[cb];
+    uint16_t* orow = out + qrow[cb] * D;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      uint2 w;
+      w.x = (uint32_t)f2bf(o[cb][n][0] * inv) | ((uint32_t)f2bf(o[cb][n][1] * inv) << 16);
+      w.y = (uint32_t)f2bf(o[cb][n][2] * inv) | ((uint32_t)f2bf(o[cb][n][3] * inv) << 16);
+      *reinterpret_cast<uint2*>(orow + 16 * n + 4 * g4) = w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Grouped decode attention with a one-tile register prefetch: the same work as
 // attn_grouped_kernel, but the wave walks ONE flattened stream of 32-key tiles
 // (shared prefix, then each live sequence's own keys) and issues the loads of
@@ -1918,7 +2002,19 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   // auto: the per-head kernel launches G x the waves, which wins while the batch is
   // too small to fill the chip (prefill_bench: 12.6 vs 17.2 us at 32 sequences,
   // 32 vs 38 us at 190); the GQA kernel's single K/V load wins at 800 (98 vs 112 us)
-  if (g_prefill_impl == 3) {  // multi-tile per-head kernel (default)
+  if ((g_prefill_impl == 4 || g_prefill_impl == 5) && G <= 16) {  // transposed register kernel
+    const int ncb = g_prefill_impl == 5 ? 2 : 1, qpw = 16 * ncb / G;
+    dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
+#define SG_PST(NC)                                                                                             \
+  hipLaunchKernelGGL((attn_prefill_st_kernel<NC>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
+                     slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,             \
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2)
+    if (ncb == 2) SG_PST(2);
+    else SG_PST(1);
+#undef SG_PST
+    return (int)hipGetLastError();
+  }
+  if (g_prefill_impl == 3) {  // multi-tile per-head kernel
     dim3 grid((max_q + 15) / 16, nseq, nh);
     hipLaunchKernelGGL((attn_prefill_mt_kernel<3>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, slot,
                        (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk, (const uint16_t*)pvt,
@@ -1954,7 +2050,7 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
 }
 
 // 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto by batch size (0 / 1),
-// 3 = multi-tile per-head kernel
+// 3 = multi-tile per-head kernel, 4 / 5 = transposed register kernel with 16 / 32 columns
 void sg_set_prefill_impl(int impl) { g_prefill_impl = impl; }
 
 // key split of the GQA prefill kernel: 1 (one wave per tile) or 2 (two waves share the keys)

@@ -176,3 +176,19 @@ def test_null_card_and_credit_parity_d8_d10():
     assert postprocess_answer(raw, raw.body, dict(base, card=None)).outcome == Outcome.UNMATCHED
     assert postprocess_answer(raw, raw.body, dict(base, card="***")).outcome == Outcome.BROKEN
     assert worker_should_skip("CREDIT PAYMENT 100 AMD") and worker_should_skip("C2C RECEIVED 5 AMD")
+
+
+def test_golden_case_check_matches_the_reference_assertions():
+    """bench.py gates the flagship on the reference's CASES (tests/test_parsers.py:73-86):
+    the checker accepts exactly the expected values and names every wrong field."""
+    from conftest import REFERENCE_CASES
+    from smsgate_amd.models.evaluate import REFERENCE_EXPECTED, golden_case_mismatches
+
+    for (_, exp), want in zip(REFERENCE_CASES, REFERENCE_EXPECTED):
+        assert {k: want[k] for k in ("merchant", "city", "address", "card", "currency")} == {
+            k: exp[k] for k in ("merchant", "city", "address", "card", "currency")}
+        assert want["date"] == "%04d-%02d-%02dT%02d:%02d" % exp["date"]
+    good = [dict(w, date=w["date"] + ":00", amount=w["amount"] + "0") for w in REFERENCE_EXPECTED]
+    assert golden_case_mismatches(good) == []
+    bad = [good[0], None, dict(good[2], city="AMERIABANK")]
+    assert golden_case_mismatches(bad) == ["case2: not parsed", "case3.city: 'AMERIABANK' != 'AM'"]

@@ -435,8 +435,8 @@ def rope_qkv_cache(qkv: torch.Tensor, pos: torch.Tensor, slot: torch.Tensor, cos
 
 
 def set_prefill_impl(impl: str) -> None:
-    """``"auto"`` (default: ``per_head`` up to 384 sequences per launch, ``gqa``
-    above), ``"gqa"`` (one wave per KV head, K/V loaded once per GQA group,
+    """``"auto"`` (default: ``st32``; past 16 query heads per KV head ``per_head`` up
+    to 384 sequences per launch, ``gqa`` above), ``"gqa"`` (one wave per KV head, K/V loaded once per GQA group,
     prefetched), ``"per_head"`` (one wave per query head: G x the waves, which
     fills the chip better at small batches; ``profiles/r01c_prefill_key_split_ab.txt``)
     or ``"multi"`` (per head, every K/V tile of a 3-tile chunk loaded at once), or

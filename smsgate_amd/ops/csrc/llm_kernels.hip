@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(64) attn_prefill_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Prefill attention, multi-tile (default): same wave decomposition and layouts as
+// Prefill attention, multi-tile (opt-in "multi"): same wave decomposition and layouts as
 // attn_prefill_kernel, but the K and V tiles of NT key tiles (a whole short
 // sequence: the shared prefix + ~54 own keys is 3 tiles) are loaded up front,
 // all at once, and the softmax runs once per chunk of NT tiles instead of once per
@@ -2002,8 +2002,12 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   // auto: the per-head kernel launches G x the waves, which wins while the batch is
   // too small to fill the chip (prefill_bench: 12.6 vs 17.2 us at 32 sequences,
   // 32 vs 38 us at 190); the GQA kernel's single K/V load wins at 800 (98 vs 112 us)
-  if ((g_prefill_impl == 4 || g_prefill_impl == 5) && G <= 16) {  // transposed register kernel
-    const int ncb = g_prefill_impl == 5 ? 2 : 1, qpw = 16 * ncb / G;
+  // auto (default) = the transposed register kernel with 32 columns: 14.0 / 20.8 / 42.1 us
+  // at 150 / 300 / 800 sequences vs 23.3 / 33.6 / 81.3 for the per-head kernel and 20.8 /
+  // 32.6 / 70.2 for the GQA one (profiles/r03_prefill_st.jsonl); bench 29 350 vs 26 698 /
+  // 27 508 msgs/s (per-head / GQA auto, profiles/r03_ab_prefill_st.jsonl)
+  if ((g_prefill_impl == 2 || g_prefill_impl == 4 || g_prefill_impl == 5) && G <= 16) {
+    const int ncb = g_prefill_impl == 4 ? 1 : 2, qpw = 16 * ncb / G;
     dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
 #define SG_PST(NC)                                                                                             \
   hipLaunchKernelGGL((attn_prefill_st_kernel<NC>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
@@ -2049,8 +2053,8 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   return (int)hipGetLastError();
 }
 
-// 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto by batch size (0 / 1),
-// 3 = multi-tile per-head kernel, 4 / 5 = transposed register kernel with 16 / 32 columns
+// 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto (5; if G > 16: 0 / 1 by
+// batch size), 3 = multi-tile per-head kernel, 4 / 5 = transposed register kernel, 16 / 32 columns
 void sg_set_prefill_impl(int impl) { g_prefill_impl = impl; }
 
 // key split of the GQA prefill kernel: 1 (one wave per tile) or 2 (two waves share the keys)

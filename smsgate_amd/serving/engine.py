@@ -88,7 +88,7 @@ class EngineConfig:
     split_parts: int = 2  # parts of a split decode bucket (split_graphs=2)
     split_prefill: int = 8192  # >0: prefill batches of >= this many tokens run as two halves on two streams
     prefill_key_split: int = 1  # 2: two waves share each prefill attention tile's keys (ops.set_prefill_split)
-    prefill_attn: str = "auto"  # ops.set_prefill_impl: auto / multi / per_head / gqa
+    prefill_attn: str = "auto"  # ops.set_prefill_impl: auto (= st32) / st / multi / per_head / gqa
     # speculative decoding (csrc/spec_kernels.hip): each decode step verifies up to
     # `spec_k` drafts per row looked up in the row's own SMS body (the extractor copies
     # body tokens); greedy only.  0 = off.  A step packs B rows + at most

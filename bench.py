@@ -124,6 +124,8 @@ def _args(argv=None):
                    help="message-start template KV slots (0 = off; default: the profile's)")
     p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa", "st", "st32"],
                    help="prefill attention kernel (default: the profile's)")
+    p.add_argument("--no-attn-merge", action="store_true",
+                   help="A/B: attention walks the shared-prefix tiles, then the own-key tiles (ops.set_attn_merge)")
     p.add_argument("--prefill-key-split", type=int, default=1, choices=[1, 2],
                    help="waves sharing each prefill attention tile's keys")
     p.add_argument("--split-prefill", type=int, default=None,
@@ -407,7 +409,9 @@ def acquire_weights(args, device: str, rank: int, world: int):
     # (profiles/r03_quality_probe.jsonl; 98.0 % with the copy-constrained decoder)
     tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
                      n_examples=args.train_steps * args.train_batch, log_every=200, data_parallel=False)
-    h = hashlib.sha256(repr((tc, open(ASSET, "rb").read())).encode(errors="ignore")).hexdigest()[:16]
+    from smsgate_amd.parse.schema import EXTRACTOR_PROMPT
+
+    h = hashlib.sha256(repr((tc, EXTRACTOR_PROMPT, open(ASSET, "rb").read())).encode(errors="ignore")).hexdigest()[:16]
     cache = args.weights_cache or os.path.join(tempfile.gettempdir(), f"smsgate-bench-w-{os.getpid()}")
     path = os.path.join(cache, f"{args.model}-{h}.safetensors")
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -482,6 +486,10 @@ def main(argv=None) -> int:
 
         ops.GEMM_MEASURED.pop(("resid", 576, 1536), None)
         ops.GEMM_MEASURED[("resid", 576, 576)] = [(8192, 10240, 3)]
+    if args.no_attn_merge:
+        from smsgate_amd import ops
+
+        ops.set_attn_merge(False)
     if args.swiglu_cfg is not None:
         from smsgate_amd import ops
 
@@ -544,7 +552,7 @@ def main(argv=None) -> int:
                         if args.bus == "busd" else "in-process bus per parser process"),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
-                "seq_len": "shared prefix 21 + ~50 prompt + <=131 schema-constrained output tokens (~42 trained)",
+                "seq_len": "shared prefix 4 (<bos> txn: <sms>) + ~43 prompt + <=131 schema-constrained output tokens (~36 trained)",
                 "parallelism": f"dp{world}" if gpu else "cpu",
                 "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
                 "engine_profile": args.profile,

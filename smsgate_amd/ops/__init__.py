@@ -105,6 +105,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_gemm_set_group_m.restype = None
     lib.sg_set_prefill_impl.argtypes = [_c_int]
     lib.sg_set_prefill_impl.restype = None
+    lib.sg_set_attn_merge.argtypes = [_c_int]
+    lib.sg_set_attn_merge.restype = None
     lib.sg_set_prefill_split.argtypes = [_c_int]
     lib.sg_set_prefill_split.restype = None
     fsm_t = [_vp, _ip, _ip, _ip, _ip, _ip, _c_int]  # masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E
@@ -444,6 +446,14 @@ def set_prefill_impl(impl: str) -> None:
     O^T = V^T·P^T: one wave per 16 / 32 (query, head) columns of one KV head,
     P never leaves registers)."""
     load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3, "st": 4, "st32": 5}[impl])
+
+
+def set_attn_merge(on: bool) -> None:
+    """``True`` (default): the transposed attention kernels (verify, grouped decode,
+    prefill ``st``/``st32``) walk the shared prefix and a row's own keys as ONE
+    stream of 32-key tiles when ``P0 % 4 == 0`` (ceil((P0 + own) / 32) tiles instead
+    of ceil(P0 / 32) + ceil(own / 32)); ``False``: prefix tiles, then own tiles."""
+    load_library().sg_set_attn_merge(1 if on else 0)
 
 
 def set_prefill_split(ks: int) -> None:

@@ -1290,6 +1290,49 @@ __device__ __forceinline__ void st_tile(const bf16x8 (&qb)[2], const uint4 (&kc)
 
 // Pass 1: grid = (ceil(B*G / 16), nkv), one wave; column c <-> query row
 // r = 16·blockIdx.x + c of kv head kh, i.e. sequence r / G, head kh·G + r % G.
+// Merged key stream (g_attn_merge): the shared prefix's P0 keys and the slot's own keys
+// form ONE sequence of 32-key tiles -- key k < P0 is prefix row k, key k >= P0 own key
+// k - P0 -- instead of a prefix tile padded to 32 followed by own tiles starting at 0.
+// A row with P0 + own keys then walks ceil((P0 + own) / 32) tiles, not
+// 1 + ceil(own / 32) (P0 = 20: 0.6 tiles fewer per row on average).  P0 % 4 == 0 keeps
+// every lane's 4-key V^T piece inside one of the two sources.  Rows past the slot's
+// Lmax (the last tile of a full slot) are clamped; their scores are masked.
+__device__ __forceinline__ void st_load_tile_m(const uint16_t* __restrict__ kpre, const uint16_t* __restrict__ vpre,
+                                               const uint16_t* __restrict__ kself,
+                                               const uint16_t* __restrict__ vself, int P0, int Lmax, int kt, int g4,
+                                               int r16, bool full, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
+  constexpr int D = 64;
+  const int ka = kt + r16, kb = kt + 16 + r16;
+  const uint16_t* kra = ka < P0 ? kpre + (size_t)ka * D : kself + (size_t)min(ka - P0, Lmax - 1) * D;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) kv[0][s2] = *reinterpret_cast<const uint4*>(kra + 8 * g4 + 32 * s2);
+  const int k_lo = kt + 4 * g4, k_hi = kt + 16 + 4 * g4;
+  const bool plo = k_lo < P0;
+  const uint16_t* vlo = plo ? vpre : vself;
+  const int kl = plo ? k_lo : min(k_lo - P0, Lmax - 4);
+  uint2 lo[4], hi[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+    lo[n] = *reinterpret_cast<const uint2*>(vlo + ((size_t)(kl >> 3) * D + 16 * n + r16) * 8 + (kl & 7));
+  if (full) {
+    const uint16_t* krb = kb < P0 ? kpre + (size_t)kb * D : kself + (size_t)min(kb - P0, Lmax - 1) * D;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) kv[1][s2] = *reinterpret_cast<const uint4*>(krb + 8 * g4 + 32 * s2);
+    const bool phi = k_hi < P0;
+    const uint16_t* vhi = phi ? vpre : vself;
+    const int kh2 = phi ? k_hi : min(k_hi - P0, Lmax - 4);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      hi[n] = *reinterpret_cast<const uint2*>(vhi + ((size_t)(kh2 >> 3) * D + 16 * n + r16) * 8 + (kh2 & 7));
+  } else {
+    kv[1][0] = kv[1][1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) hi[n] = make_uint2(0, 0);
+  }
+#pragma unroll
+  for (int n = 0; n < 4; ++n) vv[n] = make_uint4(lo[n].x, lo[n].y, hi[n].x, hi[n].y);
+}
+
 __global__ void __launch_bounds__(64) attn_prefix_kernel(const uint16_t* __restrict__ q,
                                                          const uint16_t* __restrict__ pk,
                                                          const uint16_t* __restrict__ pvt, int P0, int P0pad,
@@ -1403,7 +1446,7 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ pos, const int* __restrict__ slot,
     const int* __restrict__ done, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
     const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad,
-    uint16_t* __restrict__ out, int B, int nh, int nkv, int Lmax, float scale_log2) {
+    uint16_t* __restrict__ out, int B, int nh, int nkv, int Lmax, float scale_log2, int merge) {
   constexpr int D = 64;
   const int kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
   const int G = nh / nkv, SPW = 16 / G;
@@ -1432,7 +1475,9 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
   // shared prefix: all columns
   const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
   const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
-  for (int kt = 0; kt < P0; kt += 32) {
+  // (merged key stream: the prefix is walked per sequence inside its own stream -- the
+  // same tiles in the same order as attn_spec_kernel's, so spec and plain decode agree)
+  for (int kt = 0; kt < (merge ? 0 : P0); kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
     st_tile(qb, kc, vc, kt, P0, g4, scale_log2, m, lsum, o);
@@ -1454,6 +1499,15 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
     const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
     const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
     const bool mine = (j == jj);
+    if (merge) {
+      const int nk = P0 + own;
+      for (int kt = 0; kt < nk; kt += 32) {
+        uint4 kc[2][2], vc[4];
+        st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, kt + 16 < nk, kc, vc);
+        st_tile(qb, kc, vc, kt, nk, g4, scale_log2, m, lsum, o, mine);
+      }
+      continue;
+    }
     for (int kt = 0; kt < own; kt += 32) {
       uint4 kc[2][2], vc[4];
       st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own, kc, vc);
@@ -1492,7 +1546,7 @@ __global__ void __launch_bounds__(64) attn_spec_kernel(
     const int* __restrict__ x_pos, const int* __restrict__ x_slot, const int* __restrict__ x_done,
     const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache, const uint16_t* __restrict__ pk,
     const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out, int nh, int nkv, int Lmax,
-    float scale_log2) {
+    float scale_log2, int merge) {
   constexpr int D = 64;
   const int r = blockIdx.x, kh = blockIdx.y, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
   const int G = nh / nkv, QPW = 16 * NCB / G;
@@ -1524,23 +1578,41 @@ __global__ void __launch_bounds__(64) attn_spec_kernel(
     m[cb] = -INFINITY;
     lsum[cb] = 0.f;
   }
+  // column blocks holding a valid column (wave-uniform): a row with 1 + nd <= 16 / G
+  // pseudo-rows (most rows: ~2.3 per row at the bench's draft budget) skips the second
+  // block's MFMAs and softmax; the valid columns' arithmetic is unchanged
+  const int live = (nq * G + 15) >> 4;
   const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
   const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
-  for (int kt = 0; kt < P0; kt += 32) {
+  if (merge) {  // one stream of prefix + own keys (st_load_tile_m)
+    const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+    const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+    const int nk = P0 + p + nq;
+    for (int kt = 0; kt < nk; kt += 32) {
+      uint4 kc[2][2], vc[4];
+      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, kt + 16 < nk, kc, vc);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        if (cb < live)
+          st_tile(qb[cb], kc, vc, kt, P0 + own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+    }
+  }
+  for (int kt = 0; kt < (merge ? 0 : P0); kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) st_tile(qb[cb], kc, vc, kt, P0, g4, scale_log2, m[cb], lsum[cb], o[cb]);
+    for (int cb = 0; cb < NCB; ++cb)
+      if (cb < live) st_tile(qb[cb], kc, vc, kt, P0, g4, scale_log2, m[cb], lsum[cb], o[cb]);
   }
   const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
   const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
-  const int own_max = p + nq;
+  const int own_max = merge ? 0 : p + nq;
   for (int kt = 0; kt < own_max; kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own_max, kc, vc);
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb)
-      st_tile(qb[cb], kc, vc, kt, own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+      if (cb < live) st_tile(qb[cb], kc, vc, kt, own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
   }
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
@@ -1576,7 +1648,7 @@ __global__ void __launch_bounds__(64) attn_prefill_st_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
     const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
     const uint16_t* __restrict__ pk, const uint16_t* __restrict__ pvt, int P0, int P0pad, uint16_t* __restrict__ out,
-    int nh, int nkv, int Lmax, float scale_log2) {
+    int nh, int nkv, int Lmax, float scale_log2, int merge) {
   constexpr int D = 64;
   const int tile = blockIdx.x, b = blockIdx.y, kh = blockIdx.z, l = threadIdx.x, g4 = l >> 4, r16 = l & 15;
   const int G = nh / nkv, QPW = 16 * NCB / G;
@@ -1608,23 +1680,38 @@ __global__ void __launch_bounds__(64) attn_prefill_st_kernel(
     m[cb] = -INFINITY;
     lsum[cb] = 0.f;
   }
+  const int live = (nq * G + 15) >> 4;  // column blocks with a valid column (a sequence's last chunk)
   const uint16_t* kpre = pk + (size_t)kh * P0pad * D;
   const uint16_t* vpre = pvt + (size_t)kh * D * P0pad;
-  for (int kt = 0; kt < P0; kt += 32) {
+  if (merge) {  // one stream of prefix + own keys (st_load_tile_m)
+    const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
+    const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
+    const int nk = P0 + qs + q0 + nq;
+    for (int kt = 0; kt < nk; kt += 32) {
+      uint4 kc[2][2], vc[4];
+      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, kt + 16 < nk, kc, vc);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+        if (cb < live)
+          st_tile(qb[cb], kc, vc, kt, P0 + own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+    }
+  }
+  for (int kt = 0; kt < (merge ? 0 : P0); kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kpre, vpre, kt, g4, r16, kt + 16 < P0, kc, vc);
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) st_tile(qb[cb], kc, vc, kt, P0, g4, scale_log2, m[cb], lsum[cb], o[cb]);
+    for (int cb = 0; cb < NCB; ++cb)
+      if (cb < live) st_tile(qb[cb], kc, vc, kt, P0, g4, scale_log2, m[cb], lsum[cb], o[cb]);
   }
   const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
   const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
-  const int own_max = qs + q0 + nq;
+  const int own_max = merge ? 0 : qs + q0 + nq;
   for (int kt = 0; kt < own_max; kt += 32) {
     uint4 kc[2][2], vc[4];
     st_load_tile(kself, vself, kt, g4, r16, kt + 16 < own_max, kc, vc);
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb)
-      st_tile(qb[cb], kc, vc, kt, own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+      if (cb < live) st_tile(qb[cb], kc, vc, kt, own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
   }
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
@@ -1913,6 +2000,8 @@ __global__ void __launch_bounds__(256) fsm_sample_kernel(
 // C ABI
 // ---------------------------------------------------------------------------
 static int g_prefill_impl = 2;  // sg_set_prefill_impl
+static int g_attn_merge = 1;    // sg_set_attn_merge: merged prefix + own key stream (st kernels)
+static inline int attn_merge(int P0) { return g_attn_merge && P0 % 4 == 0 ? 1 : 0; }
 static int g_prefill_ks = 1;    // sg_set_prefill_split
 
 // ---------------------------------------------------------------------------
@@ -2012,7 +2101,7 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
 #define SG_PST(NC)                                                                                             \
   hipLaunchKernelGGL((attn_prefill_st_kernel<NC>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
                      slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,             \
-                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2)
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2, attn_merge(P0))
     if (ncb == 2) SG_PST(2);
     else SG_PST(1);
 #undef SG_PST
@@ -2056,6 +2145,10 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
 // 0 = GQA-shared prefetching kernel, 1 = per-head kernel, 2 = auto (5; if G > 16: 0 / 1 by
 // batch size), 3 = multi-tile per-head kernel, 4 / 5 = transposed register kernel, 16 / 32 columns
 void sg_set_prefill_impl(int impl) { g_prefill_impl = impl; }
+
+// 1 (default): the st attention kernels (verify, grouped decode, prefill st/st32) walk the
+// shared prefix and the own keys as one tile stream when P0 % 4 == 0; 0: prefix tiles first
+void sg_set_attn_merge(int on) { g_attn_merge = on ? 1 : 0; }
 
 // key split of the GQA prefill kernel: 1 (one wave per tile) or 2 (two waves share the keys)
 void sg_set_prefill_split(int ks) { g_prefill_ks = ks == 2 ? 2 : 1; }
@@ -2102,7 +2195,7 @@ int sg_attn_decode_grouped(const void* q, const int* pos, const int* slot, const
   const int spw = 16 / (nh / nkv);
   hipLaunchKernelGGL(attn_grouped_kernel<1>, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
-                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f, attn_merge(P0));
   return (int)hipGetLastError();
 }
 
@@ -2119,11 +2212,11 @@ int sg_attn_spec(const void* q, const int* row_start, const int* row_nd, const i
   if (max_q * (nh / nkv) <= 16)
     hipLaunchKernelGGL(attn_spec_kernel<1>, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, row_start, row_nd,
                        x_pos, x_slot, x_done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
-                       (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2);
+                       (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2, attn_merge(P0));
   else
     hipLaunchKernelGGL(attn_spec_kernel<2>, dim3(B, nkv), dim3(64), 0, stream, (const uint16_t*)q, row_start, row_nd,
                        x_pos, x_slot, x_done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
-                       (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2);
+                       (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2, attn_merge(P0));
   return (int)hipGetLastError();
 }
 
@@ -2137,7 +2230,7 @@ int sg_attn_decode_grouped_h(const void* q, const int* pos, const int* slot, con
   hipLaunchKernelGGL((attn_grouped_kernel<1, true>), dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream,
                      (const uint16_t*)q, pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache,
                      (const uint16_t*)pk, (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax,
-                     scale * 1.4426950408889634f);
+                     scale * 1.4426950408889634f, attn_merge(P0));
   return (int)hipGetLastError();
 }
 
@@ -2150,7 +2243,7 @@ int sg_attn_decode_grouped6(const void* q, const int* pos, const int* slot, cons
   const int spw = 16 / (nh / nkv);
   hipLaunchKernelGGL(attn_grouped_kernel<6>, dim3((B + spw - 1) / spw, nkv), dim3(64), 0, stream, (const uint16_t*)q,
                      pos, slot, done, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,
-                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f);
+                     (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, B, nh, nkv, Lmax, scale * 1.4426950408889634f, attn_merge(P0));
   return (int)hipGetLastError();
 }
 

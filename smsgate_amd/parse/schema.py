@@ -5,10 +5,14 @@
   request; same content and key list as the reference's Gemini prompt
   (gemini_parser.py:37-43) so remote and local backends see one task.
 * :data:`EXTRACTOR_PROMPT` — the local extractor's prompt.  The extractor is
-  fine-tuned on the task, so the instruction lives in its weights and the prompt
-  is only the schema key list (a 242-token Russian instruction would be 60 % of
-  every training sequence and of every decode step's attention for no
-  information: it is constant).
+  trained on the task, so the instruction lives in its weights and the prompt is
+  a two-token task tag (a 242-token Russian instruction would be 60 % of every
+  training sequence and of every decode step's attention for no information: it
+  is constant).  Round 3 cut the tag from the schema key list (``<bos> Extract:
+  txn_type date … <sms>``, 21 shared keys) to ``<bos> txn: <sms>`` (4 keys): every
+  decode and prefill query attends to the shared keys, and with 4 of them
+  (a multiple of 4) the attention kernels walk them inside the row's own key
+  stream (``ops.set_attn_merge``) instead of a padded 32-key tile of their own.
 * :data:`RESPONSE_SCHEMA` — the JSON schema of the answer: nine string
   properties, ``txn_type`` and ``date`` required (gemini_parser.py:46-61),
   expressed as plain JSON (the REST API shape), not google-genai objects.
@@ -33,7 +37,7 @@ SYSTEM_INSTRUCTION = (
     "Дата в сообщении обычно в формате день.месяц.год часы:минуты"
 )
 
-EXTRACTOR_PROMPT = f"Extract: {' '.join(CORE_FIELDS)}"
+EXTRACTOR_PROMPT = "txn:"
 
 RESPONSE_SCHEMA = {
     "type": "OBJECT",

@@ -88,7 +88,7 @@ def _ref_seq_attention(qb, own_k, own_v, pk, pv, P0, q_off, scale):
 
 @pytest.mark.parametrize("impl", ["gqa", "gqa_ks2", "per_head", "multi", "st", "st32"])
 @pytest.mark.parametrize("heads", [(9, 3), (4, 2), (4, 4), (8, 2)])
-@pytest.mark.parametrize("P0", [0, 75])
+@pytest.mark.parametrize("P0", [0, 20, 75])  # 0 / 20: merged prefix + own key stream; 75: prefix tiles first
 def test_attn_prefill(P0, heads, impl):
     nh, nkv = heads
     D, S, Lmax = 64, 6, 200
@@ -132,7 +132,7 @@ def test_attn_prefill(P0, heads, impl):
 
 @pytest.mark.parametrize("impl", ["grouped", "grouped_h", "grouped6", "grouped_pf", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4",
                                   "split8"])
-@pytest.mark.parametrize("P0", [0, 75])
+@pytest.mark.parametrize("P0", [0, 20, 75])
 def test_attn_decode(P0, impl):
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224  # MFMA decode tiles need Lmax % 32 == 0
     P0pad = (P0 + 31) // 32 * 32
@@ -375,11 +375,21 @@ def test_gemm_producer_norm(cfg, M):
         ops.gemm(a, wo, epi="store", ss_out=ss)
 
 
-@pytest.mark.parametrize("P0,max_q", [(0, 5), (75, 5), (75, 9)])
-def test_attn_spec_matches_grouped_bitwise(P0, max_q):
+@pytest.mark.parametrize("P0,max_q,merge", [(0, 5, 1), (20, 5, 1), (20, 9, 1), (20, 9, 0), (75, 5, 1), (75, 9, 1)])
+def test_attn_spec_matches_grouped_bitwise(P0, max_q, merge):
     """attn_spec (one wave per row, all its drafts) == the grouped decode kernel on
     the same pseudo-rows, bit for bit, and == an fp32 reference; finished rows
-    (row_nd = -1) untouched.  max_q = 9: 27 columns, two MFMA column blocks per wave."""
+    (row_nd = -1) untouched.  max_q = 9: 27 columns, two MFMA column blocks per wave.
+    P0 % 4 == 0 walks the prefix and own keys as one tile stream (ops.set_attn_merge),
+    including the clamped last tile of a full slot in the last slot (215 + 8 drafts)."""
+    ops.set_attn_merge(bool(merge))
+    try:
+        _spec_vs_grouped(P0, max_q)
+    finally:
+        ops.set_attn_merge(True)
+
+
+def _spec_vs_grouped(P0, max_q):
     nh, nkv, D, S, Lmax = 9, 3, 64, 8, 224
     P0pad = (P0 + 31) // 32 * 32
     kc = _bf(S, nkv, Lmax, D, seed=20)

@@ -1,6 +1,7 @@
 # Round-3 session 2: two-token task tag as the shared prefix (P0 = 4: merged key stream in the
 # st attention kernels).  Retrain the bundled small extractor for the new prefix and use it in
-# place, GPU suite + smoke with it, bench A/B (merged vs --no-attn-merge), kernel profile.
+# place, GPU suite + smoke with it, bench A/B (default vs --no-native-prefill vs --no-attn-merge),
+# kernel profile.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -18,7 +19,8 @@ run() {  # name, args...
   cut -c1-160 gpurun_out/ab5_$n.json
 }
 run m1
-run n1 --no-attn-merge
+run np --no-native-prefill
+run nm --no-attn-merge
 run m2
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_tag -o run -- python $R/bench.py --steps 10 --warmup 2 --eval-n 0 > $R/gpurun_out/prof_tag.log 2>&1) || { tail -5 gpurun_out/prof_tag.log; exit 1; }
 python scripts/prof_summary.py gpurun_out/prof_tag

@@ -18,6 +18,7 @@ import math
 import os
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import build as _build
@@ -99,6 +100,11 @@ def _declare(lib: ctypes.CDLL) -> None:
                             _c_float, _c_int, _vp, _vp, _c_int, _vp]
     lib.sg_gemm_qkv_rope.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_float, _c_int, _ip, _ip, _vp, _vp, _vp,
                                      _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp]
+    lib.sg_prefill_forward.argtypes = [_c_int] + [_vp] * 8 + [_vp] + [_c_int] * 9 + [_ip, _ip, _vp, _c_int, _ip, _ip,
+                                                                               _ip, _c_int, _c_int, _c_float, _vp,
+                                                                               _vp, _vp, _vp, _c_int, _c_float] + \
+        [_c_int] * 4 + [_vp]
+    lib.sg_prefill_forward.restype = _c_int
     lib.sg_gemm_probe.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]
     lib.sg_gemm_probe.restype = _c_int
     lib.sg_gemm_set_group_m.argtypes = [_c_int]
@@ -209,14 +215,15 @@ GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 6
               7: (128, 128), 8: (64, 128), 9: (256, 128), 10: (256, 256), 11: (128, 256), 12: (256, 64),
               13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64),
               19: (256, 256), 20: (256, 256), 21: (128, 96), 22: (64, 96), 23: (128, 192), 24: (256, 96),
-              25: (128, 96), 26: (64, 192), 27: (32, 96)}
+              25: (128, 96), 26: (64, 192), 27: (32, 96), 28: (128, 192), 29: (256, 96)}
 # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 # a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
 # SwiGLU kernel (gemm256_swiglu_kernel), 20 its persistent form
 GEMM_SWIGLU_ONLY = {10, 19, 20}
 # 21..26: 48-wide wave tiles (96 / 192-wide blocks) for the N = 576 residual GEMMs: no SwiGLU
-GEMM_NO_SWIGLU = {21, 22, 23, 24, 25, 26, 27}
+# 28 / 29: 128x192 / 256x96 with 4 waves (64x96 wave tiles)
+GEMM_NO_SWIGLU = {21, 22, 23, 24, 25, 26, 27, 28, 29}
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 
@@ -397,6 +404,49 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
                                          _p(ss_in), ld, _stream())
     _check(rc, "gemm_qkv_rope")
+
+
+class LayerPointers:
+    """Per-layer device addresses of a fused serving model (int64 host arrays) for the
+    native launch sequences (``csrc/runtime.hip``): weights, KV caches, shared prefix.
+    The tensors must stay alive (and in place) as long as this object is used."""
+
+    def __init__(self, w_qkv, w_o, w_gu, w_down, k_cache, vt_cache, pk, pvt):
+        def arr(ts):
+            return np.asarray([t.data_ptr() for t in ts], dtype=np.int64)
+
+        L = len(w_qkv)
+        self.L = L
+        self.arrays = [arr(w_qkv), arr(w_o), arr(w_gu), arr(w_down), arr(k_cache[i] for i in range(L)),
+                       arr(vt_cache[i] for i in range(L)), arr(pk[i] for i in range(L)), arr(pvt[i] for i in range(L))]
+        self.ptrs = [a.ctypes.data for a in self.arrays]
+
+
+def prefill_forward(lp: LayerPointers, x: torch.Tensor, *, H: int, I: int, nh: int, nkv: int, D: int, Lmax: int,
+                    P0: int, P0pad: int, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor, p0: int,
+                    cu_q: torch.Tensor, q_start: torch.Tensor, seq_slot: torch.Tensor, max_q: int, scale: float,
+                    q: torch.Tensor, a: torch.Tensor, act: torch.Tensor, ss: Optional[torch.Tensor], eps: float) -> None:
+    """The fused prefill forward (every layer: QKV+RoPE+KV write, varlen prefill
+    attention, o-proj + residual, SwiGLU gate/up, down-proj + residual) as ONE native
+    call (``sg_prefill_forward``) — the kernels and tile configs of ``gemm_qkv_rope`` /
+    ``attn_prefill`` / ``gemm`` launched from C instead of ~150 Python wrapper calls.
+    ``x`` [T, H] is the residual stream (updated in place); ``q``/``a``/``act`` scratch."""
+    T = x.shape[0]
+    if T == 0:
+        return
+    assert x.is_contiguous() and x.shape[1] == H and q.numel() >= T * nh * D and a.numel() >= T * nh * D
+    assert act.is_contiguous() and act.shape[1] == I and act.shape[0] >= T
+    nseq = cu_q.numel() - 1
+    cfg_qkv = 17 if T <= 2 * GEMM_SMALL_M else (1 if T >= 12288 else 3)  # gemm_qkv_rope's rule
+    cfg_o = gemm_cfg(T, H, epi="resid", K=nh * D)
+    cfg_gu = gemm_cfg(T, 2 * I, epi="swiglu", K=H)
+    cfg_down = gemm_cfg(T, H, epi="resid", K=I)
+    ld = _ss_check(ss, T, "prefill_forward ss")
+    rc = load_library().sg_prefill_forward(
+        lp.L, *lp.ptrs, _p(x), T, H, I, nh, nkv, D, Lmax, P0, P0pad, _p(pos), _p(slot), _p(cos_sin), p0, _p(cu_q),
+        _p(q_start), _p(seq_slot), nseq, max_q, float(scale), _p(q), _p(a), _p(act), _p(ss), ld, float(eps),
+        cfg_qkv, cfg_o, cfg_gu, cfg_down, _stream())
+    _check(rc, "prefill_forward")
 
 
 def fold_norm(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:

@@ -548,14 +548,19 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       }
     }
     if constexpr (!POW2) {
+      // x² parts are 96 columns wide whatever the tile width: a 192-wide tile writes two
+      // parts, each summed over its 12 chunks in the order a 96-wide tile sums them, so the
+      // consumer's partials (and every row's result) do not depend on the tile config
+      constexpr int PW = BN % 96 == 0 ? 96 : BN, CPP = PW / 8, NPART = BN / PW;
       if (want_ss) {
         __syncthreads();
-        for (int r = tid; r < BM; r += NT) {
-          if (m0 + r >= M) break;
+        for (int q = tid; q < BM * NPART; q += NT) {
+          const int r = q % BM, part = q / BM;
+          if (m0 + r >= M) continue;
           float v = 0.f;
 #pragma unroll
-          for (int c = 0; c < CPR; ++c) v += ssl[r * CPR + c];
-          na.ssout[(size_t)(n0 / BN) * na.ld + m0 + r] = v;
+          for (int c = 0; c < CPP; ++c) v += ssl[r * CPR + part * CPP + c];
+          na.ssout[(size_t)(n0 / PW + part) * na.ld + m0 + r] = v;
         }
       }
     }
@@ -1079,9 +1084,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[28] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256, 96, 96, 192, 96, 96, 192, 96};
-  if (cfg < 0 || cfg > 27) return -1;
+  static const int BNs[30] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96};
+  if (cfg < 0 || cfg > 29) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1142,6 +1147,10 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     case 24: return dispatch_resid<256, 96, 4, 2, 2>(SG_ARGS);
     case 25: return dispatch_resid<128, 96, 2, 2, 3>(SG_ARGS);
     case 26: return dispatch_resid<64, 192, 1, 4, 2>(SG_ARGS);
+    // 64x96 wave tiles (4 waves): 10 fragment reads per 24 MFMAs and (BM + BN) / (BM * BN)
+    // staged bytes per output 28 % below the 64x48 wave tiles of 21 / 23 / 24 (LDS-bound loop)
+    case 28: return dispatch_resid<128, 192, 2, 2, 2>(SG_ARGS);
+    case 29: return dispatch_resid<256, 96, 4, 1, 2>(SG_ARGS);
     default: return dispatch_resid<32, 96, 2, 2, 2>(SG_ARGS);
   }
 #undef SG_ARGS
@@ -1149,7 +1158,7 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
 
 // QKV projection with the RMSNorm prologue and the RoPE + KV-cache epilogue
 // (replaces gemm + sg_rope_qkv_cache).  W: [(nh + 2 nkv)·64, K], norm folded in.
-// cfg must have BN = 64 (1, 3, 5, 17 or 18) or 192 (23: 128x192 8 waves, 26: 64x192; three
+// cfg must have BN = 64 (1, 3, 5, 17 or 18) or 192 (23: 128x192 8 waves, 28: 4 waves, 26: 64x192; three
 // heads per N tile, so nh and nkv must be multiples of 3).
 // ssin non-null: the row scales come from the producer's partials (NORM 2).
 int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float eps, int cfg, const int* pos,
@@ -1179,6 +1188,10 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
       if (nh % 3 || nkv % 3) return -2;
       return ssin ? launch<64, 192, 1, 4, 3, 2, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
                   : launch<64, 192, 1, 4, 3, 1, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na);
+    case 28:  // 128x192, 4 waves: 64x96 wave tiles
+      if (nh % 3 || nkv % 3) return -2;
+      return ssin ? launch<128, 192, 2, 2, 3, 2, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
+                  : launch<128, 192, 2, 2, 3, 1, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na);
     default: return -1;
   }
 #undef SG_QKV

@@ -133,6 +133,10 @@ class EngineConfig:
     template_min_count: int = 16
     template_every: int = 4096
     measure_idle: bool = True  # EngineStats.gpu_idle_s from two timing events per step
+    # the prefill forward (not graph-captured: its shape changes with every admission)
+    # launched by ONE native call (ops.prefill_forward, csrc/runtime.hip) instead of 150
+    # Python wrapper calls per half batch (fused GEMM path only)
+    native_prefill: bool = True
 
 
 @dataclass
@@ -287,6 +291,11 @@ class ExtractionEngine:
         self._tpl_first: Dict[int, List[int]] = {}  # first token -> template lengths, longest first
         self._tpl_counts: Dict[Tuple[int, ...], int] = {}
         self._tpl_seen = 0
+        # per-layer device addresses for the native prefill forward (the tensors above
+        # never move: caches and weights are allocated once)
+        self._lp = (ops.LayerPointers(self.fw_qkv, self.fw_o, self.fw_gu, self.fw_down, self.k_cache,
+                                      self.vt_cache, self.pk, self.pvt)
+                    if self.fused and ec.native_prefill else None)
         self._compute_prefix()
         if ec.use_graphs:
             self._capture_graphs()
@@ -461,7 +470,20 @@ class ExtractionEngine:
             ops.attn_prefill(q, cu_d, qstart, seq_slot_d, max_q, kc(i), vc(i), self.pk[i], self.pvt[i], self.P0, out,
                              self.scale)
 
-        h = self._forward(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
+        if self._lp is not None:
+            mc = self.mc
+            ss = self._ss_buffer(T, dev)
+            ops.prefill_forward(self._lp, x, H=mc.hidden, I=mc.inter, nh=mc.heads, nkv=mc.kv_heads, D=mc.head_dim,
+                                Lmax=self.Lmax, P0=self.P0, P0pad=self.P0pad, pos=pos_d, slot=slot_d,
+                                cos_sin=self.cos_sin, p0=self.P0, cu_q=cu_d, q_start=qstart, seq_slot=seq_slot_d,
+                                max_q=max_q, scale=self.scale,
+                                q=torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=dev),
+                                a=torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=dev),
+                                act=torch.empty(T, mc.inter, dtype=x.dtype, device=dev), ss=ss, eps=mc.eps)
+            self._fwd_ss = ss
+            h = x
+        else:
+            h = self._forward(x, pos_tok=pos_d, slot_tok=slot_d, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0)
         if slots is not None:  # a template fill: its keys / values are all it leaves
             return None
         last = h.index_select(0, (cu_d[1:] - 1).long())

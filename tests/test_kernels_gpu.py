@@ -255,7 +255,7 @@ def test_gemm_strided_a_and_bad_shapes():
         ops.gemm(_bf(4, 100), _bf(64, 100))
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 5, 17, 18, 23, 26])
+@pytest.mark.parametrize("cfg", [1, 3, 5, 17, 18, 23, 26, 28])
 @pytest.mark.parametrize("M", [1, 77, 1000, 9216])
 def test_gemm_qkv_rope_matches_unfused(cfg, M):
     nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, max(1024, M), 192, 576, 75
@@ -320,7 +320,7 @@ def test_gemm_argmax_matches_logits_path(cfg, M):
             assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 17, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("cfg", [1, 3, 17, 21, 22, 23, 24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("M", [5, 333, 2048])
 def test_gemm_producer_norm(cfg, M):
     """Residual GEMM with ``ss_out`` writes per-N-tile x² partials of the rows it
@@ -331,9 +331,15 @@ def test_gemm_producer_norm(cfg, M):
     wo = _bf(H, H, scale=H ** -0.5, seed=62)
     x = _bf(M, H, seed=63)
     ss = ops.ss_buffer(M + 7, DEV)
+    x0 = x.clone()
     ops.gemm(a, wo, epi="resid", resid=x, cfg=cfg, ss_out=ss)
-    parts = H // ops.GEMM_TILES[cfg][1]
+    bn = ops.GEMM_TILES[cfg][1]
+    parts = H // (96 if bn % 96 == 0 else bn)  # 96- and 192-wide tiles both write 96-column parts
     assert torch.count_nonzero(ss[parts:]) == 0 and torch.count_nonzero(ss[:, M:]) == 0
+    if bn % 96 == 0 and cfg != 21:  # ... and the same partials, bit for bit, as the 128x96 tile
+        x21, ss21 = x0.clone(), ops.ss_buffer(M + 7, DEV)
+        ops.gemm(a, wo, epi="resid", resid=x21, cfg=21, ss_out=ss21)
+        assert torch.equal(x21, x) and torch.equal(ss21, ss)
     torch.testing.assert_close(ss[:, :M].sum(0), x.float().pow(2).sum(1), rtol=1e-4, atol=1e-3)
     nw = _bf(H, scale=0.1, seed=64) + 1
     gu = ops.interleave_gate_up(ops.fold_norm(_bf(2 * I, H, scale=H ** -0.5, seed=65), nw))

@@ -103,6 +103,8 @@ def _args(argv=None):
     p.add_argument("--rank-threads", type=int, default=0,
                    help="torch CPU threads of the rank process (0 = torch's default); the rank only "
                         "launches GPU work, and idle OpenMP workers spin after every parallel CPU op")
+    p.add_argument("--worker-nice", type=int, default=0,
+                   help="nice increment of the parser processes (the rank process keeps its priority)")
     p.add_argument("--worker-threads", type=int, default=2,
                    help="tokenizer (Rayon) threads per parser process; 0 = library default (one per CPU)")
     p.add_argument("--no-fused-gemm", action="store_true", help="hipBLASLt GEMMs + separate norm/SwiGLU kernels")
@@ -172,7 +174,7 @@ def run_replica(args, rank: int, world: int, local: int):
 
         sink_dir = tempfile.mkdtemp(prefix=f"smsgate-bench-sink-r{rank}-")
     cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
-           "worker_threads": args.worker_threads, "vocab": args.traffic_vocab, "bus": bus_dsn,
+           "worker_threads": args.worker_threads, "nice": args.worker_nice, "vocab": args.traffic_vocab, "bus": bus_dsn,
            "traffic": args.traffic, "sink": args.sink, "sink_dir": sink_dir}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)

@@ -1297,35 +1297,53 @@ __device__ __forceinline__ void st_tile(const bf16x8 (&qb)[2], const uint4 (&kc)
 // 1 + ceil(own / 32) (P0 = 20: 0.6 tiles fewer per row on average).  P0 % 4 == 0 keeps
 // every lane's 4-key V^T piece inside one of the two sources.  Rows past the slot's
 // Lmax (the last tile of a full slot) are clamped; their scores are masked.
+// Only keys below nk are fetched (per lane: a K row is one 128-B line pair, a 4-key V^T
+// piece shares 64-B lines with its 8-key block): the tail tile of a row reads its valid
+// keys, not 16 or 32 — the verify kernel is HBM-bound, so bytes are its time.
 __device__ __forceinline__ void st_load_tile_m(const uint16_t* __restrict__ kpre, const uint16_t* __restrict__ vpre,
                                                const uint16_t* __restrict__ kself,
                                                const uint16_t* __restrict__ vself, int P0, int Lmax, int kt, int g4,
-                                               int r16, bool full, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
+                                               int r16, int nk, uint4 (&kv)[2][2], uint4 (&vv)[4]) {
   constexpr int D = 64;
   const int ka = kt + r16, kb = kt + 16 + r16;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
   const uint16_t* kra = ka < P0 ? kpre + (size_t)ka * D : kself + (size_t)min(ka - P0, Lmax - 1) * D;
+  kv[0][0] = kv[0][1] = z4;
+  if (ka < nk) {
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) kv[0][s2] = *reinterpret_cast<const uint4*>(kra + 8 * g4 + 32 * s2);
+    for (int s2 = 0; s2 < 2; ++s2) kv[0][s2] = *reinterpret_cast<const uint4*>(kra + 8 * g4 + 32 * s2);
+  }
   const int k_lo = kt + 4 * g4, k_hi = kt + 16 + 4 * g4;
   const bool plo = k_lo < P0;
   const uint16_t* vlo = plo ? vpre : vself;
   const int kl = plo ? k_lo : min(k_lo - P0, Lmax - 4);
   uint2 lo[4], hi[4];
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
-    lo[n] = *reinterpret_cast<const uint2*>(vlo + ((size_t)(kl >> 3) * D + 16 * n + r16) * 8 + (kl & 7));
-  if (full) {
-    const uint16_t* krb = kb < P0 ? kpre + (size_t)kb * D : kself + (size_t)min(kb - P0, Lmax - 1) * D;
+  for (int n = 0; n < 4; ++n) lo[n] = make_uint2(0, 0);
+  if (k_lo < nk) {
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) kv[1][s2] = *reinterpret_cast<const uint4*>(krb + 8 * g4 + 32 * s2);
+    for (int n = 0; n < 4; ++n)
+      lo[n] = *reinterpret_cast<const uint2*>(vlo + ((size_t)(kl >> 3) * D + 16 * n + r16) * 8 + (kl & 7));
+  }
+  if (kt + 16 < nk) {
+    const uint16_t* krb = kb < P0 ? kpre + (size_t)kb * D : kself + (size_t)min(kb - P0, Lmax - 1) * D;
+    kv[1][0] = kv[1][1] = z4;
+    if (kb < nk) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) kv[1][s2] = *reinterpret_cast<const uint4*>(krb + 8 * g4 + 32 * s2);
+    }
     const bool phi = k_hi < P0;
     const uint16_t* vhi = phi ? vpre : vself;
     const int kh2 = phi ? k_hi : min(k_hi - P0, Lmax - 4);
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      hi[n] = *reinterpret_cast<const uint2*>(vhi + ((size_t)(kh2 >> 3) * D + 16 * n + r16) * 8 + (kh2 & 7));
+    for (int n = 0; n < 4; ++n) hi[n] = make_uint2(0, 0);
+    if (k_hi < nk) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        hi[n] = *reinterpret_cast<const uint2*>(vhi + ((size_t)(kh2 >> 3) * D + 16 * n + r16) * 8 + (kh2 & 7));
+    }
   } else {
-    kv[1][0] = kv[1][1] = make_uint4(0, 0, 0, 0);
+    kv[1][0] = kv[1][1] = z4;
 #pragma unroll
     for (int n = 0; n < 4; ++n) hi[n] = make_uint2(0, 0);
   }
@@ -1503,7 +1521,7 @@ __global__ void __launch_bounds__(64, MINW) attn_grouped_kernel(
       const int nk = P0 + own;
       for (int kt = 0; kt < nk; kt += 32) {
         uint4 kc[2][2], vc[4];
-        st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, kt + 16 < nk, kc, vc);
+        st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, nk, kc, vc);
         st_tile(qb, kc, vc, kt, nk, g4, scale_log2, m, lsum, o, mine);
       }
       continue;
@@ -1590,7 +1608,7 @@ __global__ void __launch_bounds__(64) attn_spec_kernel(
     const int nk = P0 + p + nq;
     for (int kt = 0; kt < nk; kt += 32) {
       uint4 kc[2][2], vc[4];
-      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, kt + 16 < nk, kc, vc);
+      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, nk, kc, vc);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
         if (cb < live)
@@ -1689,7 +1707,7 @@ __global__ void __launch_bounds__(64) attn_prefill_st_kernel(
     const int nk = P0 + qs + q0 + nq;
     for (int kt = 0; kt < nk; kt += 32) {
       uint4 kc[2][2], vc[4];
-      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, kt + 16 < nk, kc, vc);
+      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, nk, kc, vc);
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
         if (cb < live)

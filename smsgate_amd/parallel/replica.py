@@ -77,7 +77,11 @@ def _payload_bytes(n: int, seed: int, vocab_name: str = "heldout", traffic: str 
 
 
 def parser_worker_main(conn: Connection, rank: int, widx: int, cfg: Dict[str, Any]) -> None:
-    """Entry point of a parser process (bench/serving harness)."""
+    """Entry point of a parser process (bench/serving harness).  ``cfg["nice"]`` > 0
+    lowers its CPU priority: on a node where the parser processes and the rank process
+    share cores, the rank process (it feeds the GPU) wins a contended core."""
+    if int(cfg.get("nice", 0)) > 0:
+        os.nice(int(cfg["nice"]))
     asyncio.run(_worker_async(conn, rank, widx, cfg))
 
 

@@ -71,6 +71,9 @@ def main() -> None:
     p.add_argument("--weights", default="random",
                    help="random | train (bench.py's in-run training, reusing its weights cache) | checkpoint path")
     p.add_argument("--spec-k", type=int, default=0, help="speculative decoding drafts per row (0 = off)")
+    p.add_argument("--profile", default=None, choices=["throughput", "latency"],
+                   help="engine configuration of serving/profiles.py (what engine-server --profile serves); "
+                        "--max-slots / --spec-k are then ignored")
     a = p.parse_args()
     import torch
 
@@ -95,10 +98,16 @@ def main() -> None:
 
         bargs = bench._args(["--weights", a.weights])
         weights, _ = bench.acquire_weights(bargs, "cuda:0", 0, 1)
-    eng = build_engine("smollm-135m", device="cuda", random_init=weights is None, weights=weights,
-                       max_slots=a.max_slots, steps_per_graph=2,
-                       buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192), spec_k=a.spec_k, **kw)
-    arm = {"attn_small_rows": eng.cfg.decode_attn_small_rows, "attn_small": eng.cfg.decode_attn_small,
+    if a.profile:
+        from smsgate_amd.serving.profiles import profile_kwargs
+
+        ekw = dict(profile_kwargs(a.profile), **kw)
+    else:
+        ekw = dict(max_slots=a.max_slots, steps_per_graph=2, buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192),
+                   spec_k=a.spec_k, **kw)
+    eng = build_engine("smollm-135m", device="cuda", random_init=weights is None, weights=weights, **ekw)
+    a.spec_k = eng.cfg.spec_k
+    arm = {"profile": a.profile, "attn_small_rows": eng.cfg.decode_attn_small_rows, "attn_small": eng.cfg.decode_attn_small,
            "gemm_small_m": ops.GEMM_SMALL_M, "admit_min_batch": eng.cfg.admit_min_batch,
            "admit_max_wait_ms": eng.cfg.admit_max_wait_s * 1000.0, "prefill_key_split": eng.cfg.prefill_key_split,
            "weights": a.weights, "spec_k": a.spec_k}

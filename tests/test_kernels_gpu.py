@@ -577,3 +577,27 @@ def test_kv_copy_prefix():
         ek[:, dst, :, :k] = k0[:, src, :, :k]
         ev[:, dst, :, :(k + 7) // 8] = v0[:, src, :, :(k + 7) // 8]
     assert torch.equal(kc, ek) and torch.equal(vt, ev)
+
+
+@pytest.mark.parametrize("M", [777, 9216])
+def test_gemm_qkv_rope_tile_independent(M):
+    """ops.qkv_cfg picks the QKV+RoPE tile by row count; every config accumulates each
+    output in the same K order, so q, K and V^T come out bit-identical whatever the tile
+    (a row's result never depends on the batch it runs in)."""
+    nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, max(1024, M), 192, 576, 4
+    x = _bf(M, K, seed=57)
+    w = _bf((nh + 2 * nkv) * D, K, scale=K ** -0.5, seed=58)
+    g = torch.Generator(device="cpu").manual_seed(59)
+    pos = torch.randint(0, Lmax, (M,), generator=g, dtype=torch.int32).to(DEV)
+    slot = torch.randperm(S, generator=g)[:M].to(torch.int32).to(DEV)
+    cs = ops.rope_table(p0 + Lmax + 1, D, 100000.0, DEV)
+    outs = []
+    for cfg in (1, 3, 17, 23, 28):
+        kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
+        vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=DEV)
+        q = torch.zeros(M, nh, D, dtype=torch.bfloat16, device=DEV)
+        ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, p0, cfg=cfg)
+        outs.append((q, kc, vt))
+    for o in outs[1:]:
+        for u, v in zip(outs[0], o):
+            assert torch.equal(u, v)

@@ -372,7 +372,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: Opti
     return out
 
 
-def qkv_cfg(M: int) -> int:
+def qkv_cfg(M: int, nh: int = 9, nkv: int = 3) -> int:
     """Tile config of the QKV+RoPE GEMM at M rows.  64x64 tiles: the V^T scatter of the
     epilogue favours more, smaller tiles (kbench, B=4096/8192: 17.8/27.6 us vs 22.0/31.3
     us with 128x64); 32-row tiles up to 2048 rows (7.4 / 8.2 / 11.4 vs 10.1 / 10.7 / 12.3
@@ -380,12 +380,13 @@ def qkv_cfg(M: int) -> int:
     waves (64x96 wave tiles) at the 9 216-row decode halves (24.45 vs 25.10 us,
     profiles/r03s2_tiles_tune.json); 128x64 from 12 288 rows (prefill halves: 39.0 vs 40.7
     us at 16 384, r02s3_gemm_tune.json).  Every config accumulates each output in the
-    same K order, so the choice never changes a result."""
+    same K order, so the choice never changes a result.  192-wide tiles hold three
+    heads: only for head counts divisible by 3."""
     if M <= 2 * GEMM_SMALL_M:
         return 17
     if M >= 12288:
         return 1
-    return 28 if M >= 6144 else 3
+    return 28 if M >= 6144 and nh % 3 == 0 and nkv % 3 == 0 else 3
 
 
 def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tensor, slot: torch.Tensor,
@@ -409,7 +410,7 @@ def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tenso
     if M == 0:
         return
     if cfg is None:
-        cfg = qkv_cfg(M)
+        cfg = qkv_cfg(M, nh, nkv)
     ld = _ss_check(ss_in, M, "gemm_qkv_rope ss_in")
     rc = load_library().sg_gemm_qkv_rope(_p(x), x.stride(0), _p(w), M, K, float(eps), cfg, _p(pos), _p(slot),
                                          _p(cos_sin), _p(q_out), _p(k_cache), _p(vt_cache), nh, nkv, Lmax, p0,
@@ -448,7 +449,7 @@ def prefill_forward(lp: LayerPointers, x: torch.Tensor, *, H: int, I: int, nh: i
     assert x.is_contiguous() and x.shape[1] == H and q.numel() >= T * nh * D and a.numel() >= T * nh * D
     assert act.is_contiguous() and act.shape[1] == I and act.shape[0] >= T
     nseq = cu_q.numel() - 1
-    cfg_qkv = qkv_cfg(T)  # gemm_qkv_rope's rule
+    cfg_qkv = qkv_cfg(T, nh, nkv)  # gemm_qkv_rope's rule
     cfg_o = gemm_cfg(T, H, epi="resid", K=nh * D)
     cfg_gu = gemm_cfg(T, 2 * I, epi="swiglu", K=H)
     cfg_down = gemm_cfg(T, H, epi="resid", K=I)

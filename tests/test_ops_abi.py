@@ -89,3 +89,15 @@ def test_measured_tile_exceptions():
     assert {ops.GEMM_TILES[ops.gemm_cfg(M, 576, epi="resid", K=576)][1] for M in range(1, 40000, 97)} == {96}
     assert ops.GEMM_TILES[20] == (256, 256) and 20 in ops.GEMM_SWIGLU_ONLY
     assert all(576 % ops.GEMM_TILES[c][1] == 0 for c in ops.GEMM_NO_SWIGLU)  # the N = 576 residual GEMMs
+
+
+def test_qkv_tile_rule():
+    """The 3-head (192-wide) QKV tile only where both head counts divide by 3; 32-row
+    tiles for small batches, 128x64 for prefill-sized ones."""
+    from smsgate_amd import ops
+
+    assert ops.qkv_cfg(9216, 9, 3) == 28
+    assert ops.qkv_cfg(9216, 4, 2) == 3 and ops.qkv_cfg(9216, 9, 2) == 3
+    assert ops.qkv_cfg(1000) == 17 and ops.qkv_cfg(4608) == 3 and ops.qkv_cfg(15104) == 1
+    bm, bn = ops.GEMM_TILES[28]
+    assert (bm, bn) == (128, 192) and 28 in ops.GEMM_NO_SWIGLU

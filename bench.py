@@ -128,6 +128,8 @@ def _args(argv=None):
                    help="message-start template KV slots (0 = off; default: the profile's)")
     p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa", "st", "st32"],
                    help="prefill attention kernel (default: the profile's)")
+    p.add_argument("--no-sparse-argmax", action="store_true",
+                   help="A/B: the dense lm_head GEMM with the masked arg-max epilogue (EngineConfig.sparse_argmax)")
     p.add_argument("--no-native-prefill", action="store_true",
                    help="A/B: launch the prefill forward op by op from Python (EngineConfig.native_prefill)")
     p.add_argument("--no-attn-merge", action="store_true",
@@ -217,7 +219,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               split_parts=args.split_parts, decode_attn=args.decode_attn,
                               prefill_key_split=args.prefill_key_split, spec_policy=args.spec_policy,
                               spec_max_rows=args.spec_max_rows, producer_norm=not args.no_producer_norm,
-                              native_prefill=not args.no_native_prefill,
+                              native_prefill=not args.no_native_prefill, sparse_argmax=not args.no_sparse_argmax,
                               **ekw,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init

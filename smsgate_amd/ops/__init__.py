@@ -105,6 +105,9 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                                                _vp, _vp, _vp, _c_int, _c_float] + \
         [_c_int] * 4 + [_vp]
     lib.sg_prefill_forward.restype = _c_int
+    lib.sg_sparse_argmax.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _vp, _vp, _c_int, _vp, _c_int, _c_float,
+                                     _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp, _vp]
+    lib.sg_sparse_argmax.restype = _c_int
     lib.sg_gemm_probe.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]
     lib.sg_gemm_probe.restype = _c_int
     lib.sg_gemm_set_group_m.argtypes = [_c_int]
@@ -816,6 +819,47 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, 
                                          norm, cfg, _p(row_state), _p(fsm.state_mask),
                                          _p(fsm.masks), _p(best), _p(ss_in), ld, ck, rm, _stream()), "gemm_argmax")
     return best
+
+
+def sparse_argmax(h: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, best: torch.Tensor,
+                  prev_tok: torch.Tensor, row_slot: torch.Tensor, body_buf: torch.Tensor, body_len: torch.Tensor,
+                  eps: float) -> torch.Tensor:
+    """Candidate-sparse lm_head + masked arg-max (``sparse_argmax_kernel``): ``best[r]``
+    = :func:`gemm_argmax`'s key over the tokens row ``r`` may emit — the schema mask of
+    its state, AND in a copy state the tokens its SMS body allows after ``prev_tok[r]``
+    (:func:`copy_masks`' rules) — computed from those candidates' lm_head rows only.
+    ``h`` [n, H] un-normed rows, ``w`` [V, H] with the final RMSNorm weight folded in
+    (:func:`fold_norm`); the row scale is computed from ``h``."""
+    n, H = h.shape
+    if h.dtype != torch.bfloat16 or h.stride(1) != 1 or h.stride(0) % 8 or not w.is_contiguous():
+        raise ValueError("sparse_argmax: bf16 rows with 16-B aligned strides and a contiguous weight required")
+    if w.shape != (fsm.vocab, H) or H % 64 or H > 1024:
+        raise ValueError(f"sparse_argmax: weight {tuple(w.shape)} vs vocab {fsm.vocab}, hidden {H}")
+    for t, name in ((row_state, "row_state"), (prev_tok, "prev_tok"), (row_slot, "row_slot")):
+        _req(t, torch.int32, name)
+        if t.numel() < n:
+            raise ValueError(f"sparse_argmax: {name} shorter than the rows")
+    if best.dtype != torch.int64 or best.numel() < n or not best.is_contiguous():
+        raise ValueError("sparse_argmax: best must be int64 [>= n]")
+    if n == 0:
+        return best
+    _req(body_buf, torch.int32, "body_buf")
+    ck = _p(fsm.copy_kind_t) if fsm.has_copy else None
+    _check(load_library().sg_sparse_argmax(_p(fsm.masks), _p(fsm.state_mask), fsm.sep_token, fsm.vocab, ck,
+                                           _p(fsm.tok_flags_t), _p(h), h.stride(0), _p(w), H, float(eps),
+                                           _p(row_state), _p(prev_tok), _p(row_slot), _p(body_buf),
+                                           _p(body_len), body_buf.shape[1], n, _p(best), _stream()),
+           "sparse_argmax")
+    return best
+
+
+def sparse_argmax_ok(fsm) -> bool:
+    """The sparse arg-max needs every NON-copy state to allow at most 1 024 tokens (its
+    candidate list; copy states allow at most the body's tokens + <sep>)."""
+    import numpy as _np
+
+    ck = fsm.copy_kind if fsm.copy_kind is not None else _np.zeros(fsm.num_states, dtype=_np.int32)
+    return int(fsm.allowed[ck == 0].sum(1).max(initial=0)) <= 1024
 
 
 def fsm_commit(best: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tensor, out_buf: torch.Tensor,

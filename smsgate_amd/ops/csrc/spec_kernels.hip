@@ -519,6 +519,140 @@ __global__ void __launch_bounds__(256) spec_verify_kernel(
   if (tid == 0 && accepted != nullptr) accepted[b] = emitted;
 }
 
+// ---------------------------------------------------------------------------
+// Candidate-sparse lm_head + masked arg-max (copy-constrained decoding).  Under the
+// copy constraint a row may only emit <sep> or tokens of its own SMS body (copy
+// states), or the few tokens of an enum / forced state: ~2 candidates mid-copy, ~40 at
+// a field start, of 8 192.  The dense lm_head GEMM (EPI 4 of gemm_fused_kernel)
+// computes all 8 192 logits of every pseudo-row to arg-max over that handful; here one
+// wave per row builds the row's allowed set exactly as copy_mask_kernel does (bit set
+// in LDS, AND the state's schema mask), compacts it to a candidate list, and dots the
+// row's final-normed hidden state with the candidates' (norm-folded) lm_head rows
+// only: lane l owns dims l + 64 j, so every W row is read as coalesced 128-B pieces.
+// Each logit is rounded to bf16 like the dense epilogue's staged tile and reduced with
+// the same key (larger value, then smaller token id), so best[] feeds fsm_commit /
+// spec_verify_keys unchanged.  The row scale rsqrt(mean(x^2) + eps) is computed from
+// the row itself.  Rows past n, and the wave's candidate overflow, never occur: the
+// host checks that no non-copy state allows more than SPARSE_MAX_CAND tokens and the
+// body is at most LB <= SPARSE_MAX_CAND - 1 tokens.
+// ---------------------------------------------------------------------------
+#define SPARSE_MAX_CAND 1024
+#define SPARSE_MAX_HL 16  // hidden <= 1024
+
+static __device__ __forceinline__ unsigned long long sp_argmax_key(float v, int idx) {
+  const uint32_t b = __float_as_uint(v + 0.0f);
+  const uint32_t k = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return ((unsigned long long)k << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
+}
+
+__global__ void __launch_bounds__(256) sparse_argmax_kernel(
+    FsmTables fsm, const int* __restrict__ copy_kind, const uint8_t* __restrict__ tok_flags,
+    const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ W, int H, float eps,
+    const int* __restrict__ row_state, const int* __restrict__ prev_tok, const int* __restrict__ row_slot,
+    const int* __restrict__ body_buf, const int* __restrict__ body_len, int LB, int n,
+    unsigned long long* __restrict__ best) {
+  __shared__ uint32_t bits[4][COPY_MAX_WORDS];
+  __shared__ int cand[4][SPARSE_MAX_CAND];
+  __shared__ int ncand[4];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + wid;
+  if (r >= n) return;  // wave-uniform: no block barrier below
+  const int s = row_state[r];
+  const int kind = copy_kind != nullptr ? copy_kind[s] : 0;
+  const int words = fsm.V >> 5;
+  const uint32_t* m = fsm.masks + (size_t)fsm.state_mask[s] * words;
+  uint32_t* b = bits[wid];
+  int* cl = cand[wid];
+  if (lane == 0) ncand[wid] = 0;
+  if (kind != 0) {  // the row's copy set (copy_mask_kernel's rules)
+    for (int w = lane; w < words; w += 64) b[w] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int sl = row_slot[r];
+    const int bl = min(body_len[sl], LB);
+    const int* body = body_buf + (size_t)sl * LB;
+    const int prev = prev_tok[r];
+    const int sep = fsm.sep_token;
+    auto flags = [&](int t) -> int { return (t >= 0 && t < fsm.V) ? (int)tok_flags[t] : 0; };
+    for (int j = lane; j < bl; j += 64) {
+      const int t = body[j];
+      int c = -1;
+      bool end_ok = false;
+      if (kind == 1) {
+        const bool glued = j > 0 && (flags(body[j - 1]) & 2) && (flags(t) & 1);
+        if (!glued) c = t;
+      } else if (t == prev) {
+        const int nx = j + 1 < bl ? body[j + 1] : -1;
+        c = nx;
+        end_ok = nx < 0 || !((flags(t) & 2) && (flags(nx) & 1));
+      }
+      if (c >= 0 && c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
+      if (end_ok) atomicOr(&b[sep >> 5], 1u << (sep & 31));
+    }
+    if (kind == 1 && lane == 0) atomicOr(&b[sep >> 5], 1u << (sep & 31));  // an empty value
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // compact the allowed set (copy set AND schema mask; a non-copy row: the schema mask)
+  for (int w = lane; w < words; w += 64) {
+    uint32_t x = m[w];
+    if (kind != 0) x &= b[w];
+    while (x) {
+      const int bit = __builtin_ctz(x);
+      x &= x - 1u;
+      const int k = atomicAdd(&ncand[wid], 1);
+      if (k < SPARSE_MAX_CAND) cl[k] = 32 * w + bit;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int nc = min(ncand[wid], SPARSE_MAX_CAND);
+  // the row's hidden state (lane l: dims l + 64 j) and its RMSNorm scale
+  const int HL = H >> 6;
+  float hv[SPARSE_MAX_HL];
+  float ss = 0.f;
+  const uint16_t* hr = h + (size_t)r * ldh;
+#pragma unroll
+  for (int j = 0; j < SPARSE_MAX_HL; ++j) {
+    hv[j] = j < HL ? sp_bf2f(hr[lane + 64 * j]) : 0.f;
+    ss = fmaf(hv[j], hv[j], ss);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float rs = rsqrtf(ss / (float)H + eps);
+  unsigned long long bk = 0ull;
+  for (int c0 = 0; c0 < nc; c0 += 4) {
+    float part[4];
+    int tk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      tk[q] = c0 + q < nc ? cl[c0 + q] : -1;
+      part[q] = 0.f;
+      if (tk[q] >= 0) {
+        const uint16_t* wr = W + (size_t)tk[q] * H + lane;
+#pragma unroll
+        for (int j = 0; j < SPARSE_MAX_HL; ++j)
+          if (j < HL) part[q] = fmaf(hv[j], sp_bf2f(wr[64 * j]), part[q]);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) part[q] += __shfl_xor(part[q], o, 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (tk[q] < 0) continue;
+      const __bf16 lb = (__bf16)(part[q] * rs);  // the dense epilogue's staged bf16 logit
+      const float v = sp_bf2f(__builtin_bit_cast(uint16_t, lb));
+      const unsigned long long k2 = sp_argmax_key(v, tk[q]);
+      bk = k2 > bk ? k2 : bk;
+    }
+  }
+  if (lane == 0) best[r] = bk;
+}
+
 extern "C" {
 
 static FsmTables make_fsm(const void* masks, const int* state_mask, const int* next_sep, const int* next_tok,
@@ -582,6 +716,25 @@ int sg_fsm_commit(const void* best, const int* row_map, const void* masks, const
   const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
   hipLaunchKernelGGL(fsm_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, f,
                      (const unsigned long long*)best, row_map, state, tok_io, out_buf, out_len, done, pos, max_out, B);
+  return (int)hipGetLastError();
+}
+
+// candidate-sparse lm_head + masked arg-max for n rows (sparse_argmax_kernel): best[r]
+// = the arg-max key over the tokens row r may emit (its state's schema mask, AND its copy
+// set in a copy state).  h [n][ldh] bf16 un-normed, W [V][H] bf16 with the final norm
+// folded in.
+int sg_sparse_argmax(const void* masks, const int* state_mask, int sep_token, int V, const int* copy_kind,
+                     const void* tok_flags, const void* h, int ldh, const void* W, int H, float eps,
+                     const int* row_state, const int* prev_tok, const int* row_slot, const int* body_buf,
+                     const int* body_len, int LB, int n, void* best, hipStream_t stream) {
+  if (V % 32 || V / 32 > COPY_MAX_WORDS || LB <= 0 || LB >= SPARSE_MAX_CAND || sep_token < 0 || sep_token >= V ||
+      H % 64 || H / 64 > SPARSE_MAX_HL || ldh % 8 || (copy_kind && !tok_flags))
+    return -1;
+  if (n == 0) return 0;
+  const FsmTables f = make_fsm(masks, state_mask, nullptr, nullptr, nullptr, nullptr, 0, sep_token, 0, V);
+  hipLaunchKernelGGL(sparse_argmax_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, f, copy_kind,
+                     (const uint8_t*)tok_flags, (const uint16_t*)h, ldh, (const uint16_t*)W, H, eps, row_state,
+                     prev_tok, row_slot, body_buf, body_len, LB, n, (unsigned long long*)best);
   return (int)hipGetLastError();
 }
 

@@ -137,6 +137,10 @@ class EngineConfig:
     # launched by ONE native call (ops.prefill_forward, csrc/runtime.hip) instead of 150
     # Python wrapper calls per half batch (fused GEMM path only)
     native_prefill: bool = True
+    # greedy copy-constrained decoding: the lm_head arg-max over each row's candidates only
+    # (its body tokens / enum tokens, ops.sparse_argmax) instead of the dense 8 192-wide
+    # GEMM with the masked arg-max epilogue (fused GEMM path, lm_head_argmax)
+    sparse_argmax: bool = True
 
 
 @dataclass
@@ -231,6 +235,8 @@ class ExtractionEngine:
         dev, bf = self.device, torch.bfloat16
         self.spec = ec.spec_k > 0 and ec.temperature <= 0
         self.copy = ec.copy_constrain and self.fsm.has_copy
+        self.sparse = (ec.sparse_argmax and self.copy and self.argmax and self.fused
+                       and ops.sparse_argmax_ok(self.fsm))
         if ec.spec_k > ops.SPEC_MAX_K:
             raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
         # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV
@@ -498,14 +504,18 @@ class ExtractionEngine:
         self.state.index_fill_(0, rl, self.fsm.start_state)
         self.pos.index_copy_(0, rl, last_pos_d)
         cm = None
-        if self.copy and int(self.fsm.copy_kind[self.fsm.start_state]):
+        if self.copy and not self.sparse and int(self.fsm.copy_kind[self.fsm.start_state]):
             # a first field that copies: every body token may start it (prev is unused)
             # (own buffer: the two halves of a split prefill run concurrently)
             cm = self._copy_masks(self.start_states[:n], self.start_states[:n], seq_slot_d,
                                   torch.empty(n, self.V_dec // 32, dtype=torch.int32, device=dev))
         if self.argmax:
             best = torch.empty(n, dtype=torch.int64, device=dev)
-            self._argmax(last, self.start_states[:n], best, row_masks=cm)
+            if self.sparse:
+                ops.sparse_argmax(last, self.fw_lm, self.start_states[:n], self.fsm, best, self.start_states[:n],
+                                  seq_slot_d, self.body_buf, self.body_len, self.mc.eps)
+            else:
+                self._argmax(last, self.start_states[:n], best, row_masks=cm)
             ops.fsm_commit(best, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done, self.pos,
                            n, row_map=rows_d)
             logits = None
@@ -620,10 +630,15 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=pos, slot_tok=slot, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0,
                           hook=hook)
-        cm = self._copy_masks(self.state[r0:r1], tok, slot, self.copy_rows[r0:r1]) if sample and self.copy else None
+        cm = (self._copy_masks(self.state[r0:r1], tok, slot, self.copy_rows[r0:r1])
+              if sample and self.copy and not self.sparse else None)
         if sample and self.argmax:
             best = self.best[r0:r1]
-            self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
+            if self.sparse:
+                ops.sparse_argmax(h, self.fw_lm, self.state[r0:r1], self.fsm, best, tok, slot, self.body_buf,
+                                  self.body_len, self.mc.eps)
+            else:
+                self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
             ops.fsm_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
                            pos, B)
             return best
@@ -710,11 +725,16 @@ class ExtractionEngine:
 
         h = self._forward(x, pos_tok=xp, slot_tok=xs, attn=attn, k_cache=kc, vt_cache=vc, p0=self.P0, hook=hook)
         # pseudo-row i's copy mask: its state and its input token (the draft before it)
-        cm = self._copy_masks(xst, xt, xs, self.copy_x[off:off + T]) if sample and self.copy else None
+        cm = (self._copy_masks(xst, xt, xs, self.copy_x[off:off + T])
+              if sample and self.copy and not (self.sparse and self.argmax) else None)
         if sample and self.argmax:
             # every pseudo-row masked with the state it has if its row's drafts so far are accepted
             best = self.x_best[off:off + T]
-            self._argmax(h, xst, best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
+            if self.sparse:
+                ops.sparse_argmax(h, self.fw_lm, xst, self.fsm, best, xt, xs, self.body_buf, self.body_len,
+                                  self.mc.eps)
+            else:
+                self._argmax(h, xst, best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
             ops.spec_verify_keys(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
                                  done, pos, xt, rs, nd, acc)
             logits = best

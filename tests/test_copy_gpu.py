@@ -158,3 +158,61 @@ def test_copy_off_is_the_old_decoder():
     eng = _engine(0, copy_constrain=False)
     assert not eng.copy and not hasattr(eng, "copy_rows")
     assert len(eng.run(bodies)) == 3
+
+
+@pytest.mark.parametrize("H", [128, 576])
+def test_sparse_argmax_matches_dense_masked_argmax(H):
+    """ops.sparse_argmax (candidates only) == the dense lm_head GEMM's masked arg-max
+    (copy masks + EPI 4) on rows in every kind of state: the chosen token is allowed,
+    its logit is the allowed maximum of an fp32 reference (to bf16 rounding), and the
+    two kernels pick the same token except at bf16 near-ties."""
+    from smsgate_amd import ops
+    from smsgate_amd.models.tokenizer import load_tokenizer
+    from smsgate_amd.models.train import make_examples
+    from smsgate_amd.serving.fsm import build_fsm
+
+    tok = load_tokenizer()
+    V = (tok.vocab_size + 127) // 128 * 128
+    fsm = build_fsm(tok, V).to_device("cuda")
+    assert ops.sparse_argmax_ok(fsm)
+    exs = make_examples(tok, fsm, 400, seed=11, vocab_name="heldout")[:256]
+    n, LB = len(exs), 160
+    i32 = dict(dtype=torch.int32, device="cuda")
+    body = torch.zeros(n, LB, **i32)
+    blen = torch.zeros(n, **i32)
+    states, prevs = [], []
+    g = torch.Generator().manual_seed(3)
+    for r, (m, a) in enumerate(exs):
+        body[r, :len(m)] = torch.tensor(m)
+        blen[r] = len(m)
+        L = int(torch.randint(0, len(a), (1,), generator=g))  # any point of the gold answer
+        s = fsm.start_state
+        for x in a[:L]:
+            s = fsm.step_host(s, x)
+        states.append(s)
+        prevs.append(a[L - 1] if L else fsm.start_state)
+    state = torch.tensor(states, **i32)
+    prev = torch.tensor(prevs, **i32)
+    slot = torch.arange(n, **i32)
+    h = (torch.randn(n, H, generator=g) * 2).to(torch.bfloat16).cuda()
+    nw = (torch.rand(H, generator=g) + 0.5).to(torch.bfloat16).cuda()
+    w = (torch.randn(V, H, generator=g) * 0.05).to(torch.bfloat16).cuda()
+    wf = ops.fold_norm(w, nw)
+    sparse = torch.zeros(n, dtype=torch.int64, device="cuda")
+    ops.sparse_argmax(h, wf, state, fsm, sparse, prev, slot, body, blen, 1e-5)
+    masks = torch.zeros(n, V // 32, **i32)
+    ops.copy_masks(fsm, state, prev, slot, body, blen, masks, n)
+    dense = torch.zeros(n, dtype=torch.int64, device="cuda")
+    ops.gemm_argmax(h, wf, state, fsm, dense, norm_eps=1e-5, row_masks=masks)
+    torch.cuda.synchronize()
+    ref = ops.ref_gemm(h, w, norm_eps=1e-5, norm_w=nw)  # fp32 logits
+    tid = lambda k: (0xFFFFFFFF - (int(k) & 0xFFFFFFFF)) if int(k) else fsm.sep_token  # noqa: E731
+    same = 0
+    for r in range(n):
+        allowed = torch.tensor(fsm.copy_mask_host(states[r], prevs[r], exs[r][0]), device="cuda")
+        ts, td = tid(sparse[r]), tid(dense[r])
+        assert bool(allowed[ts]) or not allowed.any(), (r, ts)
+        top = ref[r].masked_fill(~allowed, float("-inf")).max()
+        assert float(ref[r, ts]) >= float(top) - 0.02 * abs(float(top)) - 0.02, (r, ts, float(ref[r, ts]), float(top))
+        same += ts == td
+    assert same >= 0.97 * n, same

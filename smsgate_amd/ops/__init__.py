@@ -854,12 +854,10 @@ def sparse_argmax(h: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm
 
 
 def sparse_argmax_ok(fsm) -> bool:
-    """The sparse arg-max needs every NON-copy state to allow at most 1 024 tokens (its
-    candidate list; copy states allow at most the body's tokens + <sep>)."""
-    import numpy as _np
-
-    ck = fsm.copy_kind if fsm.copy_kind is not None else _np.zeros(fsm.num_states, dtype=_np.int32)
-    return int(fsm.allowed[ck == 0].sum(1).max(initial=0)) <= 1024
+    """The sparse arg-max needs every NON-copy state to allow at most 256 tokens (its
+    candidate list; copy states allow at most the body's tokens + <sep>, < 256)."""
+    ck = fsm.copy_kind if fsm.copy_kind is not None else np.zeros(fsm.num_states, dtype=np.int32)
+    return int(fsm.allowed[ck == 0].sum(1).max(initial=0)) <= 256
 
 
 def fsm_commit(best: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tensor, out_buf: torch.Tensor,

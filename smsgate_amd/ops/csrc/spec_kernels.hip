@@ -528,7 +528,8 @@ __global__ void __launch_bounds__(256) spec_verify_kernel(
 // wave per row builds the row's allowed set exactly as copy_mask_kernel does (bit set
 // in LDS, AND the state's schema mask), compacts it to a candidate list, and dots the
 // row's final-normed hidden state with the candidates' (norm-folded) lm_head rows
-// only: lane l owns dims l + 64 j, so every W row is read as coalesced 128-B pieces.
+// only: 16 candidates per pass, four lanes per candidate reading its W row as 16-B
+// chunks against the row staged in LDS.
 // Each logit is rounded to bf16 like the dense epilogue's staged tile and reduced with
 // the same key (larger value, then smaller token id), so best[] feeds fsm_commit /
 // spec_verify_keys unchanged.  The row scale rsqrt(mean(x^2) + eps) is computed from
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(256) spec_verify_kernel(
 // host checks that no non-copy state allows more than SPARSE_MAX_CAND tokens and the
 // body is at most LB <= SPARSE_MAX_CAND - 1 tokens.
 // ---------------------------------------------------------------------------
-#define SPARSE_MAX_CAND 1024
+#define SPARSE_MAX_CAND 256
 #define SPARSE_MAX_HL 16  // hidden <= 1024
 
 static __device__ __forceinline__ unsigned long long sp_argmax_key(float v, int idx) {
@@ -554,6 +555,7 @@ __global__ void __launch_bounds__(256) sparse_argmax_kernel(
   __shared__ uint32_t bits[4][COPY_MAX_WORDS];
   __shared__ int cand[4][SPARSE_MAX_CAND];
   __shared__ int ncand[4];
+  __shared__ __attribute__((aligned(16))) uint16_t hbuf[4][8 * SPARSE_MAX_HL * 8];  // the row, bf16
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + wid;
   if (r >= n) return;  // wave-uniform: no block barrier below
@@ -609,46 +611,61 @@ __global__ void __launch_bounds__(256) sparse_argmax_kernel(
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int nc = min(ncand[wid], SPARSE_MAX_CAND);
-  // the row's hidden state (lane l: dims l + 64 j) and its RMSNorm scale
-  const int HL = H >> 6;
-  float hv[SPARSE_MAX_HL];
-  float ss = 0.f;
+  // the row's hidden state, staged in LDS as bf16 (16-B chunks), and its RMSNorm scale
   const uint16_t* hr = h + (size_t)r * ldh;
+  uint16_t* hb = hbuf[wid];
+  const int nch = H >> 3;  // 16-B chunks of the row
+  float ss = 0.f;
+  for (int k = lane; k < nch; k += 64) {
+    const uint4 u = *reinterpret_cast<const uint4*>(hr + 8 * k);
+    *reinterpret_cast<uint4*>(hb + 8 * k) = u;
+    const uint32_t w4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-  for (int j = 0; j < SPARSE_MAX_HL; ++j) {
-    hv[j] = j < HL ? sp_bf2f(hr[lane + 64 * j]) : 0.f;
-    ss = fmaf(hv[j], hv[j], ss);
+    for (int e = 0; e < 4; ++e) {
+      const float lo = sp_bf2f((uint16_t)(w4[e] & 0xffffu)), hi = sp_bf2f((uint16_t)(w4[e] >> 16));
+      ss = fmaf(lo, lo, fmaf(hi, hi, ss));
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
   const float rs = rsqrtf(ss / (float)H + eps);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // 16 candidates per pass: lane = 4 c + q dots candidate c over the q-th quarter of the
+  // dims (16-B W chunks; the h chunk is an LDS broadcast to the 16 lanes of quarter q),
+  // then the 4 quarters are summed with two shuffles
+  const int c = lane >> 2, q = lane & 3, QD = H >> 2, qch = QD >> 3;
   unsigned long long bk = 0ull;
-  for (int c0 = 0; c0 < nc; c0 += 4) {
-    float part[4];
-    int tk[4];
+  for (int c0 = 0; c0 < nc; c0 += 16) {
+    const int tk = c0 + c < nc ? cl[c0 + c] : -1;
+    float part = 0.f;
+    if (tk >= 0) {
+      const uint16_t* wr = W + (size_t)tk * H + q * QD;
+      const uint16_t* hq = hb + q * QD;
+      for (int k = 0; k < qch; ++k) {
+        const uint4 wu = *reinterpret_cast<const uint4*>(wr + 8 * k);
+        const uint4 hu = *reinterpret_cast<const uint4*>(hq + 8 * k);
+        const uint32_t a4[4] = {wu.x, wu.y, wu.z, wu.w}, b4[4] = {hu.x, hu.y, hu.z, hu.w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      tk[q] = c0 + q < nc ? cl[c0 + q] : -1;
-      part[q] = 0.f;
-      if (tk[q] >= 0) {
-        const uint16_t* wr = W + (size_t)tk[q] * H + lane;
-#pragma unroll
-        for (int j = 0; j < SPARSE_MAX_HL; ++j)
-          if (j < HL) part[q] = fmaf(hv[j], sp_bf2f(wr[64 * j]), part[q]);
+        for (int e = 0; e < 4; ++e) {
+          part = fmaf(sp_bf2f((uint16_t)(a4[e] & 0xffffu)), sp_bf2f((uint16_t)(b4[e] & 0xffffu)), part);
+          part = fmaf(sp_bf2f((uint16_t)(a4[e] >> 16)), sp_bf2f((uint16_t)(b4[e] >> 16)), part);
+        }
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) part[q] += __shfl_xor(part[q], o, 64);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (tk[q] < 0) continue;
-      const __bf16 lb = (__bf16)(part[q] * rs);  // the dense epilogue's staged bf16 logit
-      const float v = sp_bf2f(__builtin_bit_cast(uint16_t, lb));
-      const unsigned long long k2 = sp_argmax_key(v, tk[q]);
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    if (tk >= 0 && q == 0) {
+      const __bf16 lb = (__bf16)(part * rs);  // the dense epilogue's staged bf16 logit
+      const unsigned long long k2 = sp_argmax_key(sp_bf2f(__builtin_bit_cast(uint16_t, lb)), tk);
       bk = k2 > bk ? k2 : bk;
     }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long ok = __shfl_xor(bk, o, 64);
+    bk = ok > bk ? ok : bk;
   }
   if (lane == 0) best[r] = bk;
 }

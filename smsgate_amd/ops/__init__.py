@@ -105,6 +105,8 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                                                _vp, _vp, _vp, _c_int, _c_float] + \
         [_c_int] * 4 + [_vp]
     lib.sg_prefill_forward.restype = _c_int
+    lib.sg_embed_rows.argtypes = [_ip, _vp, _vp, _c_int, _c_int, _c_int, _vp]
+    lib.sg_embed_rows.restype = _c_int
     lib.sg_sparse_argmax.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _vp, _vp, _c_int, _vp, _c_int, _c_float,
                                      _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp, _vp]
     lib.sg_sparse_argmax.restype = _c_int
@@ -125,7 +127,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_spec_verify.argtypes = [_vp, _c_int, _vp, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int,
                                    _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _ip, _vp, _vp]
     lib.sg_spec_verify.restype = _c_int
-    lib.sg_spec_verify_keys.argtypes = [_vp] + fsm_t + [_c_int] * 3 + [_ip] * 10 + [_c_int, _c_int, _vp]
+    lib.sg_spec_verify_keys.argtypes = [_vp] + fsm_t + [_c_int] * 3 + [_ip] * 10 + [_c_int, _c_int, _vp, _vp]
     lib.sg_spec_verify_keys.restype = _c_int
     lib.sg_fsm_commit.argtypes = [_vp, _ip] + fsm_t + [_c_int] * 3 + [_ip] * 6 + [_c_int, _c_int, _vp]
     lib.sg_fsm_commit.restype = _c_int
@@ -821,6 +823,22 @@ def gemm_argmax(a: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, 
     return best
 
 
+def embed_rows(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``table[ids]`` for int32 ``ids`` (one kernel; ``F.embedding`` needs int64 ids, i.e.
+    a cast and a gather per call); ids outside the table give zero rows."""
+    _req(ids, torch.int32, "ids")
+    V, H = table.shape
+    if table.dtype != torch.bfloat16 or not table.is_contiguous() or H % 8:
+        raise ValueError("embed_rows: contiguous bf16 table with H % 8 == 0 required")
+    T = ids.numel()
+    if out is None:
+        out = table.new_empty((T, H))
+    if out.shape != (T, H) or not out.is_contiguous() or out.dtype != torch.bfloat16:
+        raise ValueError("embed_rows: bad output")
+    _check(load_library().sg_embed_rows(_p(ids), _p(table), _p(out), T, H, V, _stream()), "embed_rows")
+    return out
+
+
 def sparse_argmax(h: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm, best: torch.Tensor,
                   prev_tok: torch.Tensor, row_slot: torch.Tensor, body_buf: torch.Tensor, body_len: torch.Tensor,
                   eps: float) -> torch.Tensor:
@@ -875,8 +893,12 @@ def fsm_commit(best: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tenso
 
 def spec_verify_keys(best: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.Tensor, out_buf: torch.Tensor,
                      out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, x_tok: torch.Tensor,
-                     row_start: torch.Tensor, row_nd: torch.Tensor, accepted: Optional[torch.Tensor] = None) -> None:
-    """Greedy verification of the drafts from :func:`gemm_argmax` keys (one thread per row)."""
+                     row_start: torch.Tensor, row_nd: torch.Tensor, accepted: Optional[torch.Tensor] = None,
+                     counts: Optional[torch.Tensor] = None) -> None:
+    """Greedy verification of the drafts from :func:`gemm_argmax` keys (one thread per row).
+    ``counts`` (int64 [2], optional): += (tokens emitted, rows that emitted) of this step."""
+    if counts is not None and (counts.dtype != torch.int64 or counts.numel() < 2 or not counts.is_contiguous()):
+        raise ValueError("spec_verify_keys: counts must be a contiguous int64 [2]")
     B = tok_buf.numel()
     if best.dtype != torch.int64 or best.numel() < x_tok.numel():
         raise ValueError("spec_verify_keys: best must cover every pseudo-row")
@@ -887,7 +909,7 @@ def spec_verify_keys(best: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torc
     _check(load_library().sg_spec_verify_keys(
         _p(best), *_fsm_args(fsm), fsm.sep_token, fsm.done_state, fsm.vocab, _p(state), _p(tok_buf), _p(out_buf),
         _p(out_len), _p(done), _p(pos), _p(x_tok), _p(row_start), _p(row_nd), _p(accepted), out_buf.shape[1], B,
-        _stream()), "spec_verify_keys")
+        _p(counts), _stream()), "spec_verify_keys")
 
 
 def kv_copy_prefix(k_cache: torch.Tensor, vt_cache: torch.Tensor, items: torch.Tensor) -> None:

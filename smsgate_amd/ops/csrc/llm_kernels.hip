@@ -2029,6 +2029,21 @@ static int g_prefill_ks = 1;    // sg_set_prefill_split
 // padding that the message's own prefill overwrites from offset k on) into a
 // message's slot, every layer.  grid = (items, layers), 256 threads, 16-B copies.
 // ---------------------------------------------------------------------------
+// Embedding rows for int32 token ids (the decode / verify step's input): out[i] =
+// table[ids[i]], 16-B chunks, one thread per chunk.  F.embedding needs int64 ids, i.e. a
+// cast kernel plus a gather kernel per step; ids outside [0, V) give a zero row.
+__global__ void __launch_bounds__(256) embed_rows_kernel(const int* __restrict__ ids, const uint16_t* __restrict__ table,
+                                                         uint16_t* __restrict__ out, int T, int H, int V) {
+  const int cpr = H >> 3;  // 16-B chunks per row
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)T * cpr) return;
+  const int i = (int)(q / cpr), c = (int)(q % cpr);
+  const int t = ids[i];
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (t >= 0 && t < V) v = *reinterpret_cast<const uint4*>(table + (size_t)t * H + 8 * c);
+  *reinterpret_cast<uint4*>(out + (size_t)i * H + 8 * c) = v;
+}
+
 __global__ void __launch_bounds__(256) kv_copy_prefix_kernel(uint16_t* __restrict__ k_cache,
                                                              uint16_t* __restrict__ vt_cache,
                                                              const int* __restrict__ items, int n, int S_kv,
@@ -2074,6 +2089,15 @@ int sg_silu_mul(const void* gu, void* out, int T, int I, hipStream_t stream) {
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(silu_mul_kernel, dim3(blocks), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)out, T, I);
+  return (int)hipGetLastError();
+}
+
+int sg_embed_rows(const int* ids, const void* table, void* out, int T, int H, int V, hipStream_t stream) {
+  if (H % 8) return -1;
+  if (T == 0) return 0;
+  const long long n = (long long)T * (H >> 3);
+  hipLaunchKernelGGL(embed_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ids,
+                     (const uint16_t*)table, (uint16_t*)out, T, H, V);
   return (int)hipGetLastError();
 }
 

@@ -299,17 +299,12 @@ __global__ void __launch_bounds__(256) spec_fill_kernel(
 // verify from arg-max keys (sg_gemm_argmax already masked each pseudo-row with
 // x_state): one thread per row, no logits read.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) spec_verify_keys_kernel(
-    FsmTables fsm, const unsigned long long* __restrict__ best, int* __restrict__ state, int* __restrict__ tok_buf,
+// the greedy verification of row b (spec_verify_keys_kernel); returns the tokens emitted
+static __device__ __forceinline__ int spec_verify_row(
+    const FsmTables& fsm, const unsigned long long* __restrict__ best, int* __restrict__ state, int* __restrict__ tok_buf,
     int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done, int* __restrict__ pos,
-    const int* __restrict__ x_tok, const int* __restrict__ row_start, const int* __restrict__ row_nd,
-    int* __restrict__ accepted, int max_out, int B) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  if (done[b]) {
-    if (accepted != nullptr) accepted[b] = 0;
-    return;
-  }
+    const int* __restrict__ x_tok, const int* __restrict__ row_start, const int* __restrict__ row_nd, int max_out,
+    int b) {
   const int st = row_start[b], nd = row_nd[b];
   int s = state[b], len = out_len[b], p = pos[b], emitted = 0, tok = tok_buf[b];
   bool fin = false;
@@ -332,8 +327,35 @@ __global__ void __launch_bounds__(256) spec_verify_keys_kernel(
   state[b] = s;
   pos[b] = p;
   if (fin) done[b] = 1;
-  if (accepted != nullptr) accepted[b] = emitted;
+  return emitted;
 }
+
+__global__ void __launch_bounds__(256) spec_verify_keys_kernel(
+    FsmTables fsm, const unsigned long long* __restrict__ best, int* __restrict__ state, int* __restrict__ tok_buf,
+    int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done, int* __restrict__ pos,
+    const int* __restrict__ x_tok, const int* __restrict__ row_start, const int* __restrict__ row_nd,
+    int* __restrict__ accepted, int max_out, int B, unsigned long long* __restrict__ counts) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  // counts (optional): [tokens emitted, live rows] of this step, summed per wave and added
+  // with one atomic per wave (the engine's spec_stats; was four torch kernels per step)
+  int emitted = 0;
+  if (b < B && !done[b]) emitted = spec_verify_row(fsm, best, state, tok_buf, out_buf, out_len, done, pos, x_tok,
+                                                   row_start, row_nd, max_out, b);
+  if (b < B && accepted != nullptr) accepted[b] = emitted;
+  if (counts != nullptr) {
+    unsigned long long e = (unsigned long long)emitted, live = emitted > 0 ? 1ull : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      e += __shfl_xor(e, o, 64);
+      live += __shfl_xor(live, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && e) {
+      atomicAdd(&counts[0], e);
+      atomicAdd(&counts[1], live);
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------------------
 // one-token decode / prefill sampling from arg-max keys: the FSM step of
@@ -715,12 +737,12 @@ int sg_spec_verify_keys(const void* best, const void* masks, const int* state_ma
                         const int* next_tok, const int* enum_tok, const int* enum_next, int E, int sep_token,
                         int done_state, int V, int* state, int* tok_buf, int* out_buf, int* out_len, int* done, int* pos,
                         const int* x_tok, const int* row_start, const int* row_nd, int* accepted, int max_out, int B,
-                        hipStream_t stream) {
+                        void* counts, hipStream_t stream) {
   if (B == 0) return 0;
   const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
   hipLaunchKernelGGL(spec_verify_keys_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, f,
                      (const unsigned long long*)best, state, tok_buf, out_buf, out_len, done, pos, x_tok, row_start,
-                     row_nd, accepted, max_out, B);
+                     row_nd, accepted, max_out, B, (unsigned long long*)counts);
   return (int)hipGetLastError();
 }
 

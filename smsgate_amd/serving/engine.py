@@ -367,6 +367,12 @@ class ExtractionEngine:
             return None
         return ops.ss_buffer(T, dev)
 
+    def _embed(self, ids: torch.Tensor) -> torch.Tensor:
+        """Input rows of int32 token ids (one gather kernel for bf16 weights)."""
+        if self.w.embed.dtype == torch.bfloat16 and self.w.embed.is_contiguous():
+            return ops.embed_rows(ids, self.w.embed)
+        return F.embedding(ids.long(), self.w.embed)
+
     def _forward(self, x: torch.Tensor, **kw) -> torch.Tensor:
         return self._layers_fused(x, **kw) if self.fused else self._layers(x, **kw)
 
@@ -615,7 +621,7 @@ class ExtractionEngine:
         slot = self.slot_id[r0:r1]
         done = self.done[r0:r1]
         scratch = (self.attn_scratch[0][r0:r1], self.attn_scratch[1][r0:r1])
-        x = F.embedding(tok.long(), self.w.embed)
+        x = self._embed(tok)
         impl = self.cfg.decode_attn_small if B <= self.cfg.decode_attn_small_rows else self.cfg.decode_attn
 
         def kc(i):
@@ -700,7 +706,7 @@ class ExtractionEngine:
                       self.out_buf[r0:r1], self.out_len[r0:r1], self.body_buf, self.body_len, self.spec_delim,
                       self.draft_buf[r0 * ops.SPEC_MAX_K:], xt, xp, xs, xd, rs, nd, self.spec_meta[r0:r0 + 1],
                       policy=self.cfg.spec_policy)
-        x = F.embedding(xt.long(), self.w.embed)
+        x = self._embed(xt)
         impl = self.cfg.decode_attn_small if T <= self.cfg.decode_attn_small_rows else self.cfg.decode_attn
         scratch = None
         if impl == "cascade":
@@ -736,15 +742,16 @@ class ExtractionEngine:
             else:
                 self._argmax(h, xst, best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
             ops.spec_verify_keys(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
-                                 done, pos, xt, rs, nd, acc)
+                                 done, pos, xt, rs, nd, acc, counts=self.spec_counts)
             logits = best
         else:
             logits = self._logits(h)
         if sample and not self.argmax:
             ops.spec_verify(logits, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
                             pos, xt, rs, nd, acc, row_masks=cm)
-        if sample:
-            # tokens emitted and live rows this step (read back only by stats())
+        if sample and not self.argmax:
+            # tokens emitted and live rows this step (read back only by stats(); the arg-max
+            # path adds them inside spec_verify_keys)
             self.spec_counts += torch.stack([acc.sum(dtype=torch.int64), (acc > 0).sum(dtype=torch.int64)])
         return logits
 

@@ -601,3 +601,15 @@ def test_gemm_qkv_rope_tile_independent(M):
     for o in outs[1:]:
         for u, v in zip(outs[0], o):
             assert torch.equal(u, v)
+
+
+def test_embed_rows_matches_f_embedding():
+    """ops.embed_rows (int32 ids, one kernel) == F.embedding; ids outside the table -> 0."""
+    import torch.nn.functional as F
+
+    table = _bf(8192, 576, seed=91)
+    ids = torch.randint(0, 8192, (9216,), dtype=torch.int32, device=DEV)
+    assert torch.equal(ops.embed_rows(ids, table), F.embedding(ids.long(), table))
+    bad = torch.tensor([-1, 8192, 5], dtype=torch.int32, device=DEV)
+    out = ops.embed_rows(bad, table)
+    assert torch.count_nonzero(out[:2]) == 0 and torch.equal(out[2], table[5])

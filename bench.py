@@ -100,7 +100,11 @@ def _args(argv=None):
                    help="busd: ONE shared native broker per node (journal on) carries sms.raw / sms.parsed for every "
                         "GPU's parser and writer processes (one competing group each); memory: an in-process bus per "
                         "parser process")
-    p.add_argument("--concurrency", type=int, default=4)
+    # batches of --batch messages each parser process keeps in flight to the engine (the
+    # deployed parser's PARSER_CONCURRENCY default, config.py): 8 vs 4 = 32 723 vs 30 793
+    # msgs/s mean of 3 interleaved runs, spread 0.3 k vs 2.3 k (profiles/r03s2_ab_conc.jsonl:
+    # with 4 the engine's waiting queue ran dry between lumps of finished batches)
+    p.add_argument("--concurrency", type=int, default=8)
     p.add_argument("--batch", type=int, default=512)
     p.add_argument("--rank-threads", type=int, default=0,
                    help="torch CPU threads of the rank process (0 = torch's default); the rank only "

@@ -105,3 +105,19 @@ def test_model_text_line_breaks(tk_fsm):
     enc = tk.encode_offsets([body])[0]
     for v in ("TIOVINVU", "111,264.44", "S1X1GWT5"):
         assert tk.decode(tk.value_span_ids(v, body, *enc)).strip() == v
+
+
+def test_sparse_argmax_eligibility():
+    """The candidate-sparse arg-max needs small allowed sets outside the copy states: the
+    default schema qualifies (enum / <sep>-only states), schema-only decoding (every text
+    field a free class) does not."""
+    import dataclasses
+
+    from smsgate_amd import ops
+    from smsgate_amd.models.tokenizer import load_tokenizer
+    from smsgate_amd.serving.fsm import DEFAULT_FIELDS, build_fsm
+
+    tok = load_tokenizer()
+    assert ops.sparse_argmax_ok(build_fsm(tok, 8192))
+    free = tuple(dataclasses.replace(f, copy=False) for f in DEFAULT_FIELDS)
+    assert not ops.sparse_argmax_ok(build_fsm(tok, 8192, free))

@@ -71,7 +71,7 @@ def main() -> None:
     p.add_argument("--weights", default="random",
                    help="random | train (bench.py's in-run training, reusing its weights cache) | checkpoint path")
     p.add_argument("--spec-k", type=int, default=0, help="speculative decoding drafts per row (0 = off)")
-    p.add_argument("--profile", default=None, choices=["throughput", "latency"],
+    p.add_argument("--profile", default=None, choices=["throughput", "latency", "latency_r2"],
                    help="engine configuration of serving/profiles.py (what engine-server --profile serves); "
                         "--max-slots / --spec-k are then ignored")
     a = p.parse_args()

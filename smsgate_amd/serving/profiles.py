@@ -30,9 +30,15 @@ PROFILES: Dict[str, Dict[str, Any]] = {
     "throughput": dict(max_slots=8192, steps_per_graph=2, admit_min_fraction=0.125, spec_k=6, spec_draft_frac=1.25,
                        buckets=BUCKETS, split_decode=4096, split_prefill=8192, copy_constrain=True,
                        template_slots=32),
-    "latency": dict(max_slots=4096, steps_per_graph=4, admit_min_fraction=0.25, spec_k=4, spec_draft_frac=1.25,
+    "latency": dict(max_slots=4096, steps_per_graph=2, admit_min_fraction=0.125, spec_k=6, spec_draft_frac=1.25,
                     buckets=BUCKETS[:-1], split_decode=4096, split_prefill=8192, copy_constrain=True,
                     template_slots=32),
+    # the round-2 latency profile (4 steps per graph, 25 % admission, 4 drafts): with the
+    # round-3 kernels it was behind the throughput profile at every load
+    # (profiles/r03s2_latency_{latency,throughput}.json)
+    "latency_r2": dict(max_slots=4096, steps_per_graph=4, admit_min_fraction=0.25, spec_k=4, spec_draft_frac=1.25,
+                       buckets=BUCKETS[:-1], split_decode=4096, split_prefill=8192, copy_constrain=True,
+                       template_slots=32),
 }
 
 

@@ -10,10 +10,12 @@ the headline bench measured).
   (profiles/r03_ab_templates2.jsonl; a 16 384-row engine lost 12 % there); 32 reach 4.0
   of the 4.1 tokens an oracle choice would save (replay of 20 k purchase SMS through
   the learning policy);
-* ``latency`` — the serving-latency configuration of round 2: 4 096 rows, four
-  steps per graph, admission at 25 % free rows, four drafts per row (p50 30 ms at
-  1 k msgs/s, profiles/r02s3_latency_spec4.json; six drafts did not lower it,
-  r02s3_latency_spec6.json).
+* ``latency`` — the serving-latency configuration: 4 096 rows, otherwise the
+  throughput profile's knobs (two steps per graph, 12.5 % admission, six drafts);
+  p50 25.9 / 31.7 / 41.5 / 49.9 ms at 1 k / 6 k / 10 k / 14 k msgs/s offered, against
+  29.3 / 37.6 / 42.8 / 52.2 ms for the round-2 latency profile (``latency_r2``: four
+  steps per graph, 25 % admission, four drafts) in the same call
+  (profiles/r03s2b_latency_{latency,latency_r2,throughput}.json).
 
 Everything not listed keeps the :class:`~smsgate_amd.serving.engine.EngineConfig`
 default.
@@ -35,7 +37,7 @@ PROFILES: Dict[str, Dict[str, Any]] = {
                     template_slots=32),
     # the round-2 latency profile (4 steps per graph, 25 % admission, 4 drafts): with the
     # round-3 kernels it was behind the throughput profile at every load
-    # (profiles/r03s2_latency_{latency,throughput}.json)
+    # (profiles/r03s2_latency_{latency,throughput}.json, r03s2b_latency_latency_r2.json)
     "latency_r2": dict(max_slots=4096, steps_per_graph=4, admit_min_fraction=0.25, spec_k=4, spec_draft_frac=1.25,
                        buckets=BUCKETS[:-1], split_decode=4096, split_prefill=8192, copy_constrain=True,
                        template_slots=32),

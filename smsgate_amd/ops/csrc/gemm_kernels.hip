@@ -1056,6 +1056,8 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  24: 256x96 (4x2) 2st, 8 waves   25: 128x96 (2x2) 3st   26: 64x192 (1x4) 2st
 //  27: 32x96 (2x2) 2st — small-M form of 21 / 22 (the same 96-wide N tiling at every M)
 //      (21..27: epi 0 / 1 only — 48-wide wave tiles for the N = 576 residual GEMMs)
+//  28: 128x192 (2x2) 2st   29: 256x96 (4x1) 2st — 64x96 wave tiles
+//  30: 128x96 (4x2) 2st, 8 waves   31: 64x96 (4x2) 2st, 8 waves
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1084,9 +1086,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[30] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96};
-  if (cfg < 0 || cfg > 29) return -1;
+  static const int BNs[32] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96};
+  if (cfg < 0 || cfg > 31) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1151,6 +1153,10 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     // staged bytes per output 28 % below the 64x48 wave tiles of 21 / 23 / 24 (LDS-bound loop)
     case 28: return dispatch_resid<128, 192, 2, 2, 2>(SG_ARGS);
     case 29: return dispatch_resid<256, 96, 4, 1, 2>(SG_ARGS);
+    // 8 waves on the 96-wide tiles (32x48 / 16x48 wave tiles): twice the waves per CU to
+    // hide the one-tile-per-block latency of the short K loops (K = 576 / 1536)
+    case 30: return dispatch_resid<128, 96, 4, 2, 2>(SG_ARGS);
+    case 31: return dispatch_resid<64, 96, 4, 2, 2>(SG_ARGS);
     default: return dispatch_resid<32, 96, 2, 2, 2>(SG_ARGS);
   }
 #undef SG_ARGS

@@ -1,5 +1,6 @@
 """Driver for counter runs: the gate_up GEMM (fused SwiGLU+norm) at batch B for the
-tile configs in CFGS, and hipBLASLt on the same shape."""
+tile configs in CFGS, and hipBLASLt on the same shape.  EPI=resid: the N = 576
+residual GEMM (o-proj with K=576, down-proj with K=1536) instead."""
 import os
 import sys
 
@@ -11,11 +12,17 @@ from smsgate_amd import ops  # noqa: E402
 
 dev, bf = "cuda", torch.bfloat16
 B = int(os.environ.get("B", "4096"))
-X = torch.randn(B, 576, device=dev).to(bf)
-W = (torch.randn(3072, 576, device=dev) * 0.05).to(bf)
+EPI = os.environ.get("EPI", "swiglu")
+K = int(os.environ.get("K", "576"))
+X = torch.randn(B, K, device=dev).to(bf)
+W = (torch.randn(3072 if EPI == "swiglu" else 576, K, device=dev) * 0.05).to(bf)
+R = torch.randn(B, 576, device=dev).to(bf)
 for cfg in [int(c) for c in os.environ.get("CFGS", os.environ.get("CFG", "0")).split(",")]:
     for _ in range(10):
-        ops.gemm(X, W, epi="swiglu", norm_eps=1e-5, cfg=cfg)
+        if EPI == "swiglu":
+            ops.gemm(X, W, epi="swiglu", norm_eps=1e-5, cfg=cfg)
+        else:
+            ops.gemm(X, W, epi="resid", resid=R, cfg=cfg)
 for _ in range(10):
     F.linear(X, W)
 torch.cuda.synchronize()

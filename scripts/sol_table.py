@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Speed-of-light table of the headline's hot kernels at their operating points.
+
+Each kernel runs alone (``inner`` launches captured in one hipGraph, median of
+``iters`` replays, the best of ``rounds`` interleaved visits) at the shapes the
+headline bench gives it: the 9 216-row decode halves (4 096 rows + 5 120 drafts,
+``spec_draft_frac`` 1.25) and the ~15 k-token prefill halves.  For each it prints
+the time, the work (FLOPs), the minimum HBM bytes (every operand read once, every
+output written once: no re-reads) and both as a fraction of MI355X's dense bf16
+peak (2.5 PFLOP/s) and of the achievable read bandwidth (6.3 TB/s, MI355X_MICROARCH.md).
+
+    python scripts/sol_table.py > sol.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from smsgate_amd import ops  # noqa: E402
+from scripts.gemm_tune import graph_time  # noqa: E402
+
+PEAK_TFLOPS = 2500.0
+HBM_TBS = 6.3
+
+
+def main() -> int:
+    p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    p.add_argument("--decode-rows", type=int, default=4096)
+    p.add_argument("--decode-m", type=int, default=9216)
+    p.add_argument("--prefill-m", type=int, default=15104)
+    p.add_argument("--prefill-len", type=int, default=37, help="computed prompt tokens per message")
+    p.add_argument("--own", type=int, default=60, help="mean own keys per decode row")
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--iters", type=int, default=9)
+    p.add_argument("--inner", type=int, default=20)
+    a = p.parse_args()
+    dev, bf16 = "cuda", torch.bfloat16
+    torch.manual_seed(0)
+    H, I, nh, nkv, D, P0 = 576, 1536, 9, 3, 64, 4
+    S, Lmax = 8192, 192
+    NQKV = (nh + 2 * nkv) * D
+    g = torch.Generator(device="cpu").manual_seed(0)
+
+    def bf(*shape):
+        return (torch.randn(*shape, generator=g) * 0.05).to(bf16).to(dev)
+
+    w_gu, w_down, w_o, w_qkv = bf(2 * I, H), bf(H, I), bf(H, H), bf(NQKV, H)
+    cs = ops.rope_table(1024, D, 1e5, device=dev)
+    kc = bf(S, nkv, Lmax, D)
+    vt = bf(*ops.vt_shape(S, nkv, D, Lmax))
+    P0pad = 32
+    pk, pvt = bf(nkv, P0pad, D), bf(*ops.vt_shape(1, nkv, D, P0pad)[1:])
+    scale = 1.0 / math.sqrt(D)
+    cases = {}  # name -> (fn, flops, bytes)
+
+    for tag, M in (("decode", a.decode_m), ("prefill", a.prefill_m)):
+        x, h, resid = bf(M, H), bf(M, I), bf(M, H)
+        out_gu = torch.empty(M, I, dtype=bf16, device=dev)
+        ss = ops.ss_buffer(M, dev)
+        ss[:6] = torch.rand(6, M, device=dev)
+        sso = ops.ss_buffer(M, dev)
+        pos = torch.randint(0, 120, (M,), generator=g, dtype=torch.int32).to(dev)
+        slot = torch.randint(0, S, (M,), generator=g, dtype=torch.int32).to(dev)
+        q_out = torch.empty(M, nh, D, dtype=bf16, device=dev)
+        c_gu = ops.gemm_cfg(M, 2 * I, epi="swiglu", K=H)
+        c_o, c_dn = ops.gemm_cfg(M, H, epi="resid", K=H), ops.gemm_cfg(M, H, epi="resid", K=I)
+        c_q = ops.qkv_cfg(M, nh, nkv)
+        cases[f"gate_up_{tag}_M{M}_cfg{c_gu}"] = (
+            lambda x=x, o=out_gu, s=ss, c=c_gu: ops.gemm(x, w_gu, epi="swiglu", norm_eps=1e-5, out=o, cfg=c, ss_in=s),
+            2.0 * M * 2 * I * H, 2 * (M * H + 2 * I * H + M * I))
+        cases[f"o_proj_{tag}_M{M}_cfg{c_o}"] = (
+            lambda x=x, r=resid, s=sso, c=c_o: ops.gemm(x, w_o, epi="resid", resid=r, cfg=c, ss_out=s),
+            2.0 * M * H * H, 2 * (M * H + H * H + 2 * M * H))
+        cases[f"down_proj_{tag}_M{M}_cfg{c_dn}"] = (
+            lambda h=h, r=resid, s=sso, c=c_dn: ops.gemm(h, w_down, epi="resid", resid=r, cfg=c, ss_out=s),
+            2.0 * M * H * I, 2 * (M * I + H * I + 2 * M * H))
+        cases[f"qkv_rope_{tag}_M{M}_cfg{c_q}"] = (
+            lambda x=x, pos=pos, slot=slot, q=q_out, c=c_q: ops.gemm_qkv_rope(
+                x, w_qkv, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, P0, cfg=c, ss_in=ss),
+            2.0 * M * NQKV * H, 2 * (M * H + NQKV * H + M * NQKV))
+
+    # speculative verify attention: B rows, nd pseudo-rows each (mean decode_m / B), own keys ~ own
+    B, T = a.decode_rows, a.decode_m
+    nd = torch.full((B,), T // B, dtype=torch.int32)
+    nd[: T - int(nd.sum())] += 1
+    start = torch.zeros(B, dtype=torch.int32)
+    start[1:] = torch.cumsum(nd, 0)[:-1].to(torch.int32)
+    base = torch.randint(a.own - 20, a.own + 20, (B,), generator=g, dtype=torch.int32)
+    rslot = torch.randperm(S, generator=g)[:B].to(torch.int32)
+    row_of = torch.repeat_interleave(torch.arange(B), nd.long())
+    within = torch.arange(T) - start.long()[row_of]
+    x_pos = (base[row_of] + within.to(torch.int32)).to(torch.int32)
+    x_slot = rslot[row_of]
+    qs, outs = bf(T, nh, D), torch.empty(T, nh, D, dtype=bf16, device=dev)
+    args = [t.to(dev) for t in (start, nd, x_pos, x_slot)] + [torch.zeros(T, dtype=torch.int32, device=dev)]
+    max_q = int(nd.max())
+    keys = int((base + nd - 1 + 1).sum()) + B * P0  # row r reads keys [0, pos_last] + the prefix
+    cases[f"attn_spec_B{B}_T{T}_own{a.own}"] = (
+        lambda: ops.attn_spec(qs, *args, kc, vt, pk, pvt, P0, outs, scale, max_q),
+        2.0 * 2 * D * nh * float((x_pos.float() + 1 + P0).sum()),
+        keys * nkv * D * 2 * 2 + 2 * T * nh * D * 2)
+
+    # prefill attention: the prefill half's sequences, prefill_len tokens each
+    L = a.prefill_len
+    nseq = a.prefill_m // L
+    Tp = nseq * L
+    cu = torch.arange(0, Tp + 1, L, dtype=torch.int32).to(dev)
+    qst = torch.zeros(nseq, dtype=torch.int32, device=dev)
+    pslot = torch.randperm(S, generator=g)[:nseq].to(torch.int32).to(dev)
+    qp, op_ = bf(Tp, nh, D), torch.empty(Tp, nh * D, dtype=bf16, device=dev)
+    causal = nseq * sum(P0 + i + 1 for i in range(L))
+    cases[f"attn_prefill_{nseq}x{L}"] = (
+        lambda: ops.attn_prefill(qp, cu, qst, pslot, L, kc, vt, pk, pvt, P0, op_, scale),
+        2.0 * 2 * D * nh * causal, (nseq * (L + P0)) * nkv * D * 2 * 2 + 2 * Tp * nh * D * 2)
+
+    best = {k: math.inf for k in cases}
+    for _ in range(a.rounds):
+        for k, (fn, _, _) in cases.items():
+            best[k] = min(best[k], graph_time(fn, a.iters, a.inner))
+    res = {}
+    for k, (fn, fl, by) in cases.items():
+        us = best[k]
+        tf = fl / us / 1e6
+        tbs = by / us / 1e6
+        res[k] = {"us": round(us, 2), "gflop": round(fl / 1e9, 2), "min_mb": round(by / 1e6, 1),
+                  "tflops": round(tf, 1), "pct_peak_flops": round(100 * tf / PEAK_TFLOPS, 1),
+                  "tb_s_min_bytes": round(tbs, 2), "pct_hbm": round(100 * tbs / HBM_TBS, 1),
+                  "floor_us": round(max(fl / PEAK_TFLOPS / 1e6, by / HBM_TBS / 1e6), 2)}
+        print(json.dumps({k: res[k]}), file=sys.stderr, flush=True)
+    print(json.dumps(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -387,10 +387,24 @@ def start_node_broker(args, local: int):
                 os.unlink(p)
             brokers.append(spawn_busd(f"unix://{p}", os.path.join(root, f"data{k}")))
         return brokers, dsn
+    import socket
+
+    def listening(path: str) -> bool:
+        # a socket file left by an earlier run that died (same MASTER_PORT) exists but
+        # refuses connections: wait for local rank 0's fresh broker behind it
+        if not os.path.exists(path):
+            return False
+        with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as c:
+            try:
+                c.connect(path)
+                return True
+            except OSError:
+                return False
+
     t_end = time.time() + 60
-    while not all(os.path.exists(p) for p in socks):
+    while not all(listening(p) for p in socks):
         if time.time() > t_end:
-            raise SystemExit(f"bench: the node broker sockets {socks} never appeared")
+            raise SystemExit(f"bench: the node broker sockets {socks} never started listening")
         time.sleep(0.05)
     return None, dsn
 

@@ -357,6 +357,22 @@ def engine_kwargs(args) -> dict:
     return kw
 
 
+def _listening(path: str) -> bool:
+    """True once a broker accepts connections on unix socket ``path``.  A socket file
+    left by an earlier run that died (same MASTER_PORT) exists but refuses them, so
+    the waiting ranks do not mistake it for local rank 0's fresh broker."""
+    import socket
+
+    if not os.path.exists(path):
+        return False
+    with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as c:
+        try:
+            c.connect(path)
+            return True
+        except OSError:
+            return False
+
+
 def start_node_broker(args, local: int):
     """Local rank 0 starts ``--bus-shards`` ``smsgate-busd`` brokers (journal in a temp
     dir, fsync interval), sharded by subject; the other ranks of the node wait for
@@ -387,22 +403,8 @@ def start_node_broker(args, local: int):
                 os.unlink(p)
             brokers.append(spawn_busd(f"unix://{p}", os.path.join(root, f"data{k}")))
         return brokers, dsn
-    import socket
-
-    def listening(path: str) -> bool:
-        # a socket file left by an earlier run that died (same MASTER_PORT) exists but
-        # refuses connections: wait for local rank 0's fresh broker behind it
-        if not os.path.exists(path):
-            return False
-        with socket.socket(socket.AF_UNIX, socket.SOCK_STREAM) as c:
-            try:
-                c.connect(path)
-                return True
-            except OSError:
-                return False
-
     t_end = time.time() + 60
-    while not all(listening(p) for p in socks):
+    while not all(_listening(p) for p in socks):
         if time.time() > t_end:
             raise SystemExit(f"bench: the node broker sockets {socks} never started listening")
         time.sleep(0.05)

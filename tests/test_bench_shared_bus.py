@@ -47,3 +47,21 @@ def test_bench_with_a_real_sql_sink():
     rt = lines[0]["routing"]
     assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"] > 0 and rt["writer_fail"] == 0
     assert not [d for d in os.listdir("/tmp") if d.startswith("smsgate-bench-sink-r0-")]  # sink files removed
+
+
+def test_stale_broker_socket_is_not_listening(tmp_path):
+    """A socket file whose broker died (a crashed run with the same MASTER_PORT) does not
+    count as the node broker: the waiting ranks hold until a live one accepts."""
+    import socket
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    path = str(tmp_path / "bus0.sock")
+    assert not bench._listening(path)
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind(path)
+    srv.listen(1)
+    assert bench._listening(path)
+    srv.close()  # the file stays, nobody accepts
+    assert os.path.exists(path) and not bench._listening(path)

@@ -510,10 +510,10 @@ def set_prefill_impl(impl: str) -> None:
     prefetched), ``"per_head"`` (one wave per query head: G x the waves, which
     fills the chip better at small batches; ``profiles/r01c_prefill_key_split_ab.txt``)
     or ``"multi"`` (per head, every K/V tile of a 3-tile chunk loaded at once), or
-    ``"st"`` / ``"st32"`` (transposed register formulation, S^T = K·Q^T and
-    O^T = V^T·P^T: one wave per 16 / 32 (query, head) columns of one KV head,
+    ``"st"`` / ``"st32"`` / ``"st64"`` (transposed register formulation, S^T = K·Q^T and
+    O^T = V^T·P^T: one wave per 16 / 32 / 64 (query, head) columns of one KV head,
     P never leaves registers)."""
-    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3, "st": 4, "st32": 5}[impl])
+    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3, "st": 4, "st32": 5, "st64": 6}[impl])
 
 
 def set_attn_merge(on: bool) -> None:

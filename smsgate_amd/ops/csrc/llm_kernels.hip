@@ -2137,14 +2137,16 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   // at 150 / 300 / 800 sequences vs 23.3 / 33.6 / 81.3 for the per-head kernel and 20.8 /
   // 32.6 / 70.2 for the GQA one (profiles/r03_prefill_st.jsonl); bench 29 350 vs 26 698 /
   // 27 508 msgs/s (per-head / GQA auto, profiles/r03_ab_prefill_st.jsonl)
-  if ((g_prefill_impl == 2 || g_prefill_impl == 4 || g_prefill_impl == 5) && G <= 16) {
-    const int ncb = g_prefill_impl == 4 ? 1 : 2, qpw = 16 * ncb / G;
+  if ((g_prefill_impl == 2 || g_prefill_impl >= 4) && G <= 16) {
+    // st64 (impl 6): 64 columns, half the waves re-read a sequence's keys
+    const int ncb = g_prefill_impl == 4 ? 1 : g_prefill_impl == 6 ? 4 : 2, qpw = 16 * ncb / G;
     dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
 #define SG_PST(NC)                                                                                             \
   hipLaunchKernelGGL((attn_prefill_st_kernel<NC>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
                      slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,             \
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2, attn_merge(P0))
     if (ncb == 2) SG_PST(2);
+    else if (ncb == 4) SG_PST(4);
     else SG_PST(1);
 #undef SG_PST
     return (int)hipGetLastError();

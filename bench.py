@@ -130,7 +130,7 @@ def _args(argv=None):
                         "file per parser process")
     p.add_argument("--template-slots", type=int, default=None,
                    help="message-start template KV slots (0 = off; default: the profile's)")
-    p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa", "st", "st32", "st64"],
+    p.add_argument("--prefill-attn", default=None, choices=["auto", "multi", "per_head", "gqa", "st", "st32", "st64", "st32pf", "stpf"],
                    help="prefill attention kernel (default: the profile's)")
     p.add_argument("--no-sparse-argmax", action="store_true",
                    help="A/B: the dense lm_head GEMM with the masked arg-max epilogue (EngineConfig.sparse_argmax)")

@@ -57,7 +57,7 @@ def run(a, nseq: int) -> dict:
     scale = 1 / math.sqrt(D)
     res = {"nseq": a.nseq, "tokens": T, "nh": a.nh, "nkv": a.nkv, "P0": a.P0}
     outs = {}
-    for impl in ("per_head", "gqa", "gqa_ks2", "multi", "st", "st32", "st64"):
+    for impl in ("per_head", "gqa", "gqa_ks2", "multi", "st", "st32", "st64", "st32pf", "stpf"):
         ops.set_prefill_impl("gqa" if impl.startswith("gqa") else impl)
         ops.set_prefill_split(2 if impl == "gqa_ks2" else 1)
         out = torch.empty(T, a.nh * D, dtype=torch.bfloat16, device=dev)
@@ -80,9 +80,11 @@ def run(a, nseq: int) -> dict:
     res["speedup_ks2"] = round(res["gqa_us"] / res["gqa_ks2_us"], 3)
     res["max_abs_diff_multi"] = float((outs["multi"] - outs["per_head"]).abs().max())
     res["speedup_multi_vs_per_head"] = round(res["per_head_us"] / res["multi_us"], 3)
-    for impl in ("st", "st32", "st64"):
+    for impl in ("st", "st32", "st64", "st32pf", "stpf"):
         res[f"max_abs_diff_{impl}"] = float((outs[impl] - outs["per_head"]).abs().max())
         res[f"speedup_{impl}_vs_per_head"] = round(res["per_head_us"] / res[f"{impl}_us"], 3)
+    res["st32pf_bitwise_st32"] = bool(torch.equal(outs["st32pf"], outs["st32"]))
+    res["stpf_bitwise_st"] = bool(torch.equal(outs["stpf"], outs["st"]))
     print(json.dumps(res), flush=True)
     return res
 

@@ -1659,9 +1659,10 @@ __global__ void __launch_bounds__(64) attn_spec_kernel(
 // on that VALU / LDS work (prefill_bench: it scales with tokens, not with latency).
 // K/V tiles are loaded once for the G heads of the group.  Causal: column i sees own
 // keys [0, q_start + i]; the tile loop runs to the wave's last query.
-// grid = (ceil(max_q / QPW), nseq, nkv), one wave.
+// grid = (ceil(max_q / QPW), nseq, nkv), one wave.  PF = 1 (merged stream only): the
+// loads of key tile t+1 are issued before the MFMAs of tile t (one-tile register prefetch).
 // ---------------------------------------------------------------------------
-template <int NCB>
+template <int NCB, int PF = 0>
 __global__ void __launch_bounds__(64) attn_prefill_st_kernel(
     const uint16_t* __restrict__ q, const int* __restrict__ cu_q, const int* __restrict__ q_start,
     const int* __restrict__ slot, const uint16_t* __restrict__ k_cache, const uint16_t* __restrict__ vt_cache,
@@ -1705,13 +1706,36 @@ __global__ void __launch_bounds__(64) attn_prefill_st_kernel(
     const uint16_t* kself = k_cache + ((size_t)sl * nkv + kh) * Lmax * D;
     const uint16_t* vself = vt_cache + ((size_t)sl * nkv + kh) * D * Lmax;
     const int nk = P0 + qs + q0 + nq;
-    for (int kt = 0; kt < nk; kt += 32) {
+    if constexpr (PF) {
       uint4 kc[2][2], vc[4];
-      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, nk, kc, vc);
+      st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, 0, g4, r16, nk, kc, vc);
+      for (int kt = 0; kt < nk; kt += 32) {
+        uint4 kn[2][2], vn[4];
+        const bool more = kt + 32 < nk;
+        if (more) st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt + 32, g4, r16, nk, kn, vn);
 #pragma unroll
-      for (int cb = 0; cb < NCB; ++cb)
-        if (cb < live)
-          st_tile(qb[cb], kc, vc, kt, P0 + own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+        for (int cb = 0; cb < NCB; ++cb)
+          if (cb < live)
+            st_tile(qb[cb], kc, vc, kt, P0 + own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+        if (more) {
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            kc[a][0] = kn[a][0];
+            kc[a][1] = kn[a][1];
+          }
+#pragma unroll
+          for (int n = 0; n < 4; ++n) vc[n] = vn[n];
+        }
+      }
+    } else {
+      for (int kt = 0; kt < nk; kt += 32) {
+        uint4 kc[2][2], vc[4];
+        st_load_tile_m(kpre, vpre, kself, vself, P0, Lmax, kt, g4, r16, nk, kc, vc);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          if (cb < live)
+            st_tile(qb[cb], kc, vc, kt, P0 + own[cb], g4, scale_log2, m[cb], lsum[cb], o[cb], col_valid[cb]);
+      }
     }
   }
   for (int kt = 0; kt < (merge ? 0 : P0); kt += 32) {
@@ -2138,16 +2162,19 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   // 32.6 / 70.2 for the GQA one (profiles/r03_prefill_st.jsonl); bench 29 350 vs 26 698 /
   // 27 508 msgs/s (per-head / GQA auto, profiles/r03_ab_prefill_st.jsonl)
   if ((g_prefill_impl == 2 || g_prefill_impl >= 4) && G <= 16) {
-    // st64 (impl 6): 64 columns, half the waves re-read a sequence's keys
-    const int ncb = g_prefill_impl == 4 ? 1 : g_prefill_impl == 6 ? 4 : 2, qpw = 16 * ncb / G;
+    // st64 (impl 6): 64 columns, half the waves re-read a sequence's keys; st32pf (impl 7):
+    // st32 with the one-tile register prefetch; stpf (impl 8): st with it
+    const int ncb = (g_prefill_impl == 4 || g_prefill_impl == 8) ? 1 : g_prefill_impl == 6 ? 4 : 2, qpw = 16 * ncb / G;
     dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
-#define SG_PST(NC)                                                                                             \
-  hipLaunchKernelGGL((attn_prefill_st_kernel<NC>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
+#define SG_PST(NC, PFV)                                                                                             \
+  hipLaunchKernelGGL((attn_prefill_st_kernel<NC, PFV>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \
                      slot, (const uint16_t*)k_cache, (const uint16_t*)vt_cache, (const uint16_t*)pk,             \
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2, attn_merge(P0))
-    if (ncb == 2) SG_PST(2);
-    else if (ncb == 4) SG_PST(4);
-    else SG_PST(1);
+    if (g_prefill_impl == 7) SG_PST(2, 1);
+    else if (g_prefill_impl == 8) SG_PST(1, 1);
+    else if (ncb == 2) SG_PST(2, 0);
+    else if (ncb == 4) SG_PST(4, 0);
+    else SG_PST(1, 0);
 #undef SG_PST
     return (int)hipGetLastError();
   }

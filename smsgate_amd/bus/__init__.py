@@ -30,6 +30,7 @@ from .base import (  # noqa: F401
     SUBJECT_RAW,
     Bus,
     BusError,
+    BusUnavailable,
     ConsumerConfig,
     ConsumerInfo,
     DeliverPolicy,

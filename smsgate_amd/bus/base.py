@@ -73,7 +73,14 @@ ALL_SUBJECTS = (SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_FAILED, SUBJECT_PROCESSING,
 
 
 class BusError(RuntimeError):
-    pass
+    """The broker refused an operation (e.g. a publish over the maximum payload, no
+    stream for a subject): a property of the request, not of the connection."""
+
+
+class BusUnavailable(BusError, ConnectionError):
+    """The broker could not be reached (connection closed / reset, no responders,
+    timeout).  Not any message's fault: the consume loop naks the batch whole
+    (runtime/stage.py TRANSIENT) instead of isolating and dead-lettering."""
 
 
 class DeliverPolicy(str, enum.Enum):

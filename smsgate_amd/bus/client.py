@@ -10,6 +10,7 @@ from .base import (
     Acker,
     Bus,
     BusError,
+    BusUnavailable,
     ConsumerInfo,
     Msg,
     MsgMetadata,
@@ -76,7 +77,7 @@ class RemoteBus(Bus, Acker):
             self._closed = True
             for fut in self._pending.values():
                 if not fut.done():
-                    fut.set_exception(BusError("bus connection closed"))
+                    fut.set_exception(BusUnavailable("bus connection closed"))
             self._pending.clear()
 
     def _flush_acks(self) -> None:
@@ -93,7 +94,7 @@ class RemoteBus(Bus, Acker):
 
     async def _call(self, op: str, *args: Any) -> Any:
         if self._closed:
-            raise BusError("bus connection closed")
+            raise BusUnavailable("bus connection closed")
         self._flush_acks()
         rid = next(self._ids)
         fut = asyncio.get_running_loop().create_future()

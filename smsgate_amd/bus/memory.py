@@ -15,6 +15,7 @@ from .base import (
     Acker,
     Bus,
     BusError,
+    BusUnavailable,
     ConsumerConfig,
     ConsumerInfo,
     Msg,
@@ -118,7 +119,7 @@ class MemoryBus(Bus, Acker):
 
     async def publish(self, subject: str, data: bytes, headers: Optional[Dict[str, str]] = None) -> PubAck:
         if self._closed:
-            raise BusError("bus closed")
+            raise BusUnavailable("bus closed")
         stream, seq = self.engine.store(subject, bytes(data), headers)
         self._maybe_expire()
         self._wake(stream)
@@ -126,7 +127,7 @@ class MemoryBus(Bus, Acker):
 
     async def publish_many(self, items: Sequence[Tuple[str, bytes]]) -> List[PubAck]:
         if self._closed:
-            raise BusError("bus closed")
+            raise BusUnavailable("bus closed")
         stored = self.engine.store_many([(s, bytes(d)) for s, d in items])
         out = [PubAck(stream, seq) for stream, seq in stored]
         touched = {stream for stream, _ in stored}

@@ -30,6 +30,7 @@ from .base import (
     Acker,
     Bus,
     BusError,
+    BusUnavailable,
     ConsumerConfig,
     ConsumerInfo,
     Msg,
@@ -187,7 +188,7 @@ class NatsBus(Bus):
     async def _pub(self, subject: str, payload: bytes, reply: Optional[str] = None,
                    headers: Optional[bytes] = None) -> None:
         if self.writer is None or self._closed:
-            raise BusError("NATS connection closed")
+            raise BusUnavailable("NATS connection closed")
         async with self._wlock:
             self.writer.write(P.pub_bytes(subject, payload, reply, headers))
             await self.writer.drain()
@@ -220,7 +221,7 @@ class NatsBus(Bus):
             self._closed = True
             for fut in self._resp.values():
                 if not fut.done():
-                    fut.set_exception(BusError("NATS connection closed"))
+                    fut.set_exception(BusUnavailable("NATS connection closed"))
 
     async def request(self, subject: str, payload: bytes, timeout: Optional[float] = None) -> P.Frame:
         token = P.nuid(12)
@@ -238,7 +239,7 @@ class NatsBus(Bus):
         if f.op == "HMSG":
             status, text, _ = P.decode_headers(f.headers)
             if status == 503:
-                raise BusError("JetStream not enabled / no responders")
+                raise BusUnavailable("JetStream not enabled / no responders")
         return json.loads(f.payload or b"{}")
 
     # -------------------------------------------------------------------- Bus

@@ -39,6 +39,7 @@ from .base import (
     SUBJECT_RAW,
     Bus,
     BusError,
+    BusUnavailable,
     ConsumerInfo,
     Msg,
     PubAck,
@@ -142,39 +143,124 @@ class Router:
 
 
 class _PartitionedSub(Subscription):
-    """One durable on every partition of a subject; fetches rotate over them (a
-    non-blocking sweep first, then short long-polls partition by partition, so no
-    fetch is ever left outstanding on a partition whose answer would be lost)."""
+    """One durable on every partition of a subject.
 
-    POLL_SLICE = 0.02
+    ``fetch`` first sweeps the partitions without waiting (rotating the start so
+    no partition starves), then long-polls EVERY partition at once and returns as
+    soon as one answers.  A long-poll still outstanding when the call returns is
+    kept, never cancelled: whatever it delivers later is buffered and returned by
+    the next ``fetch`` (cancelling it would strand the messages it was handed
+    until ack_wait).  So at low load a message on any partition is picked up
+    immediately, not after ``(n-1)`` polling slices.
+
+    A partition whose fetch raises (its broker is down) is skipped with an
+    exponential backoff (``BACKOFF_MIN``..``BACKOFF_MAX``) while the healthy ones
+    keep being served; messages already pulled in the same call are returned,
+    not dropped.  ``fetch`` raises only when every partition is failing."""
+
+    BACKOFF_MIN = 0.05
+    BACKOFF_MAX = 2.0
+    LONG_POLL = 1.0  # seconds one background long-poll may stay outstanding
 
     def __init__(self, subs: Sequence[Subscription]) -> None:
         self.subs = list(subs)
         self.consumer = subs[0].consumer
         self.stream = getattr(subs[0], "stream", None) or "SMS"
         self._rr = 0
+        n = len(self.subs)
+        self._down_until = [0.0] * n
+        self._backoff = [0.0] * n
+        self._inflight: Dict[int, "asyncio.Task[List[Msg]]"] = {}
+        self._buffer: List[Msg] = []
+        self.partition_errors = 0
+        self._last_error: Optional[BaseException] = None
+
+    def _failed(self, i: int, exc: BaseException) -> None:
+        self.partition_errors += 1
+        self._backoff[i] = min(self.BACKOFF_MAX, max(self.BACKOFF_MIN, self._backoff[i] * 2))
+        self._down_until[i] = time.monotonic() + self._backoff[i]
+        self._last_error = exc
+
+    def _ok(self, i: int) -> None:
+        self._backoff[i] = 0.0
+
+    def _harvest(self, i: int, task: "asyncio.Task[List[Msg]]") -> List[Msg]:
+        """Result of partition ``i``'s finished long-poll (it is removed from the
+        in-flight set by exactly one caller)."""
+        if self._inflight.get(i) is not task:
+            return []
+        del self._inflight[i]
+        try:
+            got = task.result()
+        except asyncio.CancelledError:
+            return []
+        except Exception as exc:  # noqa: BLE001
+            self._failed(i, exc)
+            return []
+        self._ok(i)
+        return got
+
+    def _take(self, got: List[Msg], batch: int) -> List[Msg]:
+        if len(got) > batch:
+            self._buffer = got[batch:] + self._buffer
+            got = got[:batch]
+        return got
 
     async def fetch(self, batch: int = 1, timeout: Optional[float] = None) -> List[Msg]:
         n = len(self.subs)
         start = self._rr
         self._rr = (self._rr + 1) % n
-        got: List[Msg] = []
-        for k in range(n):
-            got += await self.subs[(start + k) % n].fetch(batch - len(got), 0)
+        got, self._buffer = self._buffer[:batch], self._buffer[batch:]
+        for i, t in list(self._inflight.items()):
+            if t.done():
+                got += self._harvest(i, t)
+        now = time.monotonic()
+        order = [(start + k) % n for k in range(n)]
+        live = [i for i in order if self._down_until[i] <= now]
+        if not live and not self._inflight and not got:
+            raise BusUnavailable(f"every partition of {self.consumer!r} is failing: {self._last_error}")
+        for i in live:
             if len(got) >= batch:
-                return got
+                return self._take(got, batch)
+            if i in self._inflight:
+                continue
+            try:
+                got += await self.subs[i].fetch(batch - len(got), 0)
+                self._ok(i)
+            except Exception as exc:  # noqa: BLE001 - one broker down must not stall the others
+                self._failed(i, exc)
         if got or (timeout is not None and timeout <= 0):
-            return got
-        deadline = None if timeout is None else time.monotonic() + timeout
-        k = 0
+            return self._take(got, batch)
+        now = time.monotonic()
+        deadline = None if timeout is None else now + timeout
+        for i in order:
+            if i not in self._inflight and self._down_until[i] <= now:
+                self._inflight[i] = asyncio.ensure_future(self.subs[i].fetch(batch, self.LONG_POLL))
+        if not self._inflight:  # every partition is backing off: wait out the shortest backoff
+            wait = min(self._down_until) - now
+            await asyncio.sleep(max(0.0, min(wait, timeout if timeout is not None else wait)))
+            return []
         while True:
-            left = self.POLL_SLICE if deadline is None else min(self.POLL_SLICE, deadline - time.monotonic())
-            got = await self.subs[(start + k) % n].fetch(batch, max(0.0, left))
-            k += 1
-            if got or (deadline is not None and time.monotonic() >= deadline):
-                return got
+            left = None if deadline is None else max(0.0, deadline - time.monotonic())
+            done, _ = await asyncio.wait(list(self._inflight.values()), timeout=left,
+                                         return_when=asyncio.FIRST_COMPLETED)
+            for i, t in list(self._inflight.items()):
+                if t in done:
+                    got += self._harvest(i, t)
+            if got or not done or (deadline is not None and time.monotonic() >= deadline):
+                return self._take(got, batch)
+            # an empty long-poll ended (its own timeout): re-arm it and keep waiting
+            now = time.monotonic()
+            for i in order:
+                if i not in self._inflight and self._down_until[i] <= now:
+                    self._inflight[i] = asyncio.ensure_future(self.subs[i].fetch(batch, self.LONG_POLL))
+            if not self._inflight:
+                return []
 
     async def unsubscribe(self) -> None:
+        for t in self._inflight.values():
+            t.cancel()
+        self._inflight.clear()
         await asyncio.gather(*(s.unsubscribe() for s in self.subs))
 
 

@@ -14,7 +14,7 @@ from urllib.parse import urlparse
 
 import msgpack
 
-from .base import BusError
+from .base import BusError, BusUnavailable
 
 __all__ = ["SyncBusClient"]
 
@@ -45,7 +45,7 @@ class SyncBusClient:
         while len(buf) < n:
             chunk = self.sock.recv(n - len(buf))
             if not chunk:
-                raise BusError("bus connection closed")
+                raise BusUnavailable("bus connection closed")
             buf += chunk
         return bytes(buf)
 

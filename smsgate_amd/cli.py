@@ -54,7 +54,9 @@ def _pipeline(settings, backend_name: Optional[str] = None, engine: Optional[str
     from .parse.backends import create_backend
     from .parse.cache import open_cache
     from .parse.pipeline import ParsePipeline
+    from .parse.text import set_keyword_match
 
+    set_keyword_match(settings.parser_keyword_match)
     name = backend_name or settings.parser_backend
     if engine:
         from multiprocessing.connection import Client

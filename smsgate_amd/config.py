@@ -87,6 +87,9 @@ class Settings(BaseModel):
     parser_cache_path: str = ".gemini_cache.sqlite"
     parser_concurrency: int = 8
     parser_batch_size: int = 64
+    # keyword skip filters: "word" (default; a keyword must stand as a word) or
+    # "substring" (the reference's exact behaviour, worker.py:112-121) -- parse/text.py
+    parser_keyword_match: str = "word"
     llm_model: str = "smollm-135m"
     llm_checkpoint: Optional[str] = None
     llm_device: str = "cuda"

@@ -32,8 +32,10 @@ DEFAULT_VOCAB = 8192
 # was 8 tokens).  ',' before a non-3-digit group stays a separator ("BLVD 89,17.05.24"
 # keeps the street number and the date apart), so every body value stays token-aligned.
 # 8 192 merges: 49.2 -> 41.2 body tokens and 43.8 -> 35.7 answer tokens per purchase SMS.
+# Currency symbols are pre-tokens of their own (never glued to neighbouring
+# punctuation: "-£574.33", "BAL:$52.00"), so a copied currency is token-aligned.
 NUMBER_AWARE_SPLIT = (r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\d{1,3}(?:,\d{3})+(?:\.\d+)?| ?\d+(?:[.:]\d+)*"
-                      r"| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+")
+                      r"| ?[$€£₽₾֏]| ?[^\s\p{L}\p{N}$€£₽₾֏]+|\s+(?!\S)|\s+")
 
 
 def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: int = 60000, seed: int = 1234):
@@ -91,7 +93,9 @@ class ExtractorTokenizer:
         return self.tk.encode(model_text(text), add_special_tokens=False).ids
 
     def encode_batch(self, texts: Sequence[str]) -> List[List[int]]:
-        return [e.ids for e in self.tk.encode_batch([model_text(t) for t in texts], add_special_tokens=False)]
+        # the offset-free batch encoder: same ids, ~25 % less work (offsets are only
+        # needed for training targets, encode_offsets)
+        return [e.ids for e in self.tk.encode_batch_fast([model_text(t) for t in texts], add_special_tokens=False)]
 
     def encode_offsets(self, texts: Sequence[str]) -> List[Tuple[List[int], List[Tuple[int, int]]]]:
         """Ids plus each token's ``(start, end)`` character span in its MODEL text
@@ -125,7 +129,9 @@ class ExtractorTokenizer:
                 start = a + 1
                 continue
             k0 = next((k for k, (s, e) in enumerate(offsets) if s <= a < e), None)
-            k1 = next((k for k, (s, e) in enumerate(offsets) if e == z), None)
+            # the LAST token ending at z: a character split over several byte-level
+            # tokens (Cyrillic, symbols) gives each piece the character's whole span
+            k1 = max((k for k, (s, e) in enumerate(offsets) if e == z), default=None)
             if k0 is not None and k1 is not None and k1 >= k0 and body[offsets[k0][0]:a].strip() == "":
                 span = list(ids[k0:k1 + 1])
                 if self.decode(span).strip() == value:
@@ -134,6 +140,43 @@ class ExtractorTokenizer:
 
     def decode(self, ids: Sequence[int]) -> str:
         return self.tk.decode(list(ids), skip_special_tokens=True)
+
+    @functools.cached_property
+    def token_bytes(self) -> List[bytes]:
+        """The raw bytes of every id (specials -> ``b""``): byte-level BPE tokens are
+        byte strings, so a value decodes as ``b"".join(...).decode("utf-8", "replace")``
+        -- identical to :meth:`decode` (tests/test_families.py pins it) without a
+        round trip through the library per value."""
+        u2b = {c: b for b, c in _bytes_to_unicode().items()}
+        out = [b""] * self.vocab_size
+        for s, i in self.tk.get_vocab().items():
+            if s not in SPECIALS and i < self.vocab_size:
+                out[i] = bytes(u2b[c] for c in s)
+        return out
+
+    def decode_fields(self, seqs: Sequence[Sequence[int]], nfields: int) -> List[List[str]]:
+        """Answer token sequences -> ``nfields`` stripped strings each (split at
+        ``<sep>``; a missing field is ``""``; tokens after the last field are dropped)."""
+        tb = self.token_bytes
+        sep = self.sep
+        out: List[List[str]] = []
+        for toks in seqs:
+            vals: List[str] = []
+            cur: List[bytes] = []
+            for t in toks:
+                if t == sep:
+                    vals.append(b"".join(cur).decode("utf-8", "replace").strip())
+                    if len(vals) == nfields:
+                        break
+                    cur = []
+                else:
+                    cur.append(tb[t])
+            else:
+                if len(vals) < nfields:
+                    vals.append(b"".join(cur).decode("utf-8", "replace").strip())
+            vals += [""] * (nfields - len(vals))
+            out.append(vals)
+        return out
 
     def decode_batch(self, seqs: Sequence[Sequence[int]]) -> List[str]:
         return self.tk.decode_batch([list(s) for s in seqs], skip_special_tokens=True)
@@ -167,6 +210,19 @@ class ExtractorTokenizer:
 
             LLM_TRUNCATED.inc(cut)
         return [e[:max_body] + [self.ans] for e in enc]
+
+
+def _bytes_to_unicode() -> dict:
+    """GPT-2's byte <-> printable-character table (the ByteLevel pre-tokenizer's alphabet)."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + list(range(ord("®"), ord("ÿ") + 1))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, (chr(c) for c in cs)))
 
 
 @functools.lru_cache(maxsize=4)

@@ -5,7 +5,9 @@ The reference never trains a model: it sends every SMS to Gemini
 our own extractor LM, and random-init weights only exercise
 its speed.  This module turns the LM into a working extractor.
 
-* data: :mod:`~smsgate_amd.utils.synth` bank SMS with ground-truth answers,
+* data: :mod:`~smsgate_amd.utils.synth` bank SMS with ground-truth answers — the
+  training template families (20 layouts in three languages; the held-out
+  families are never seen),
   normalised exactly like the parse pipeline does before calling a backend
   (:func:`~smsgate_amd.parse.text.normalize_body`); skipped kinds (OTP, …) never
   reach the LLM and are not trained on;
@@ -47,7 +49,7 @@ from ..parse.text import normalize_body
 from .extractor import CONFIGS, ExtractorWeights, reference_forward
 from .tokenizer import ExtractorTokenizer, load_tokenizer
 
-__all__ = ["TrainConfig", "answer_tokens", "make_examples", "train_extractor", "field_accuracy",
+__all__ = ["TrainConfig", "answer_tokens", "make_examples", "ExamplePool", "train_extractor", "field_accuracy",
            "latest_checkpoint", "to_serving"]
 
 
@@ -69,6 +71,10 @@ class TrainConfig:
     resume: bool = False
     bucket_mb: float = 64.0
     vocab_name: str = "train"  # synthetic vocabulary pool (utils.synth.vocab)
+    # SMS layouts trained on: "train" = the training template families (utils.synth
+    # TRAIN_FAMILIES, the two legacy formats included); None = the legacy mix only.
+    # The held-out families (HELDOUT_FAMILIES) are never trained on.
+    families: Optional[str] = "train"
     data_parallel: bool = True  # under torch.distributed: all-reduce gradients (False: train this rank alone)
     eval_every: int = 0  # call on_eval(step, serving weights) every N steps (0 = never)
 
@@ -100,12 +106,15 @@ def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]]
 
 
 def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
-                  max_body: int = 128, vocab_name: str = "train") -> List[Tuple[List[int], List[int]]]:
+                  max_body: int = 128, vocab_name: str = "train",
+                  families: Optional[str] = "train") -> List[Tuple[List[int], List[int]]]:
     """``(message ids, answer ids)`` pairs (prefix excluded: it is shared)."""
-    from ..utils.synth import generate
+    from ..utils.synth import HELDOUT_FAMILIES, generate, family_names
 
+    if families is not None:
+        assert not set(family_names(families)) & set(HELDOUT_FAMILIES), "held-out families are never trained on"
     out: List[Tuple[List[int], List[int]]] = []
-    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name) if s.answer is not None]
+    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name, families=families) if s.answer is not None]
     bodies = [normalize_body(s.body) for s in items]
     msgs = tok.message_ids(bodies, max_body)
     encs = tok.encode_offsets(bodies)
@@ -114,6 +123,54 @@ def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
         if a is not None:
             out.append((m, a))
     return out
+
+
+_POOL_STATE: Dict[str, object] = {}
+
+
+def _pool_init(tok_path: str) -> None:
+    from ..serving.fsm import build_fsm
+
+    tok = ExtractorTokenizer(Path(tok_path))
+    _POOL_STATE["tok"] = tok
+    _POOL_STATE["fsm"] = build_fsm(tok, (tok.vocab_size + 63) // 64 * 64)
+
+
+def _pool_chunk(args) -> List[Tuple[List[int], List[int]]]:
+    n, seed, max_body, vocab_name, families = args
+    return make_examples(_POOL_STATE["tok"], _POOL_STATE["fsm"], n, seed, max_body, vocab_name, families)
+
+
+class ExamplePool:
+    """Training examples built by CPU worker processes while the caller does other
+    work (the bench starts it before the GPU is touched, then trains on the result).
+
+    ``n`` examples in chunks of ``chunk``; chunk ``k`` is generated with seed
+    ``seed * 7919 + k``, so the data depends only on (n, seed, chunk), never on the
+    worker count.  The worker processes are spawned (not forked) and exit when the
+    examples are collected."""
+
+    def __init__(self, n: int, seed: int = 0, max_body: int = 128, vocab_name: str = "train",
+                 families: Optional[str] = "train", workers: int = 8, chunk: int = 4096,
+                 tok_path: Optional[str] = None) -> None:
+        import multiprocessing as mp
+
+        from .tokenizer import ASSET
+
+        jobs = [(min(chunk, n - k * chunk), seed * 7919 + k, max_body, vocab_name, families)
+                for k in range((n + chunk - 1) // chunk)]
+        self.n = n
+        self._pool = mp.get_context("spawn").Pool(max(1, min(workers, len(jobs))), initializer=_pool_init,
+                                                  initargs=(str(tok_path or ASSET),))
+        self._res = self._pool.map_async(_pool_chunk, jobs)
+
+    def get(self, timeout: float = 1800.0) -> List[Tuple[List[int], List[int]]]:
+        try:
+            chunks = self._res.get(timeout)
+        finally:
+            self._pool.close()
+            self._pool.join()
+        return [e for c in chunks for e in c]
 
 
 def _batch(prefix: List[int], exs: Sequence[Tuple[List[int], List[int]]], pad: int,
@@ -166,8 +223,10 @@ def to_serving(w: ExtractorWeights, cfg=None) -> ExtractorWeights:
 
 def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] = print,
                     tok: Optional[ExtractorTokenizer] = None,
-                    on_eval: Optional[Callable[[int, ExtractorWeights], None]] = None) -> ExtractorWeights:
-    """Train and return **bf16** serving weights."""
+                    on_eval: Optional[Callable[[int, ExtractorWeights], None]] = None,
+                    data: Optional[List[Tuple[List[int], List[int]]]] = None) -> ExtractorWeights:
+    """Train and return **bf16** serving weights.  ``data``: prebuilt examples
+    (e.g. :class:`ExamplePool`), else built here from ``cfg``."""
     import torch.distributed as dist
 
     from ..parallel.ddp import GradBuckets
@@ -182,7 +241,8 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     v_dec = min(mcfg.vocab, (tok.vocab_size + 63) // 64 * 64)
     fsm = build_fsm(tok, v_dec)
     t0 = time.perf_counter()
-    data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens, cfg.vocab_name)
+    if data is None:
+        data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens, cfg.vocab_name, cfg.families)
     log(f"train: {len(data)} examples ({time.perf_counter() - t0:.1f}s), model {cfg.model}")
     prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
     torch.manual_seed(cfg.seed)

@@ -65,12 +65,12 @@ def spawn_parser_workers(n: int, rank: int, cfg: Dict[str, Any]) -> Tuple[List[A
 def _payload_bytes(n: int, seed: int, vocab_name: str = "heldout", traffic: str = "mixed") -> List[bytes]:
     """Synthetic phone posts (the gateway's ``RawSMSPayload``); ``vocab_name``
     picks the merchant / city vocabulary (held-out = never seen in training),
-    ``traffic`` the mix of message kinds (utils.synth.TRAFFIC_KINDS)."""
+    ``traffic`` the preset mix of SMS layouts / kinds (utils.synth.TRAFFIC)."""
     from ..services.gateway import RawSMSPayload
-    from ..utils.synth import TRAFFIC_KINDS, generate
+    from ..utils.synth import generate_traffic
 
     out = []
-    for s in generate(n, seed=seed, vocab_name=vocab_name, kinds=TRAFFIC_KINDS[traffic]):
+    for s in generate_traffic(n, seed=seed, vocab_name=vocab_name, traffic=traffic):
         p = RawSMSPayload(device_id="bench", message=s.body, sender="BANK", timestamp=s.timestamp, source="device")
         out.append(p)
     return out  # type: ignore[return-value]
@@ -123,6 +123,12 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     await writer.start()
     client.send_control({"event": "ready", "w": widx})
     prepared: List[List[Any]] = []
+    # cProfile of the timed phases only (bench.py --profile-cpu DIR)
+    prof = None
+    if cfg.get("profile_dir"):
+        import cProfile
+
+        prof = cProfile.Profile()
     while True:
         cmd = await asyncio.to_thread(client.control.get)
         if cmd is None or cmd.get("cmd") == "quit":
@@ -133,6 +139,8 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                         for seed in cmd["seeds"]]
             client.send_control({"event": "prepared", "w": widx})
         elif cmd["cmd"] == "go":
+            if prof is not None:
+                prof.enable()
             c0 = dict(worker.counts)
             w0 = (writer.stage.processed, writer.ok, writer.skipped, writer.fail)
             t0 = time.perf_counter()
@@ -160,6 +168,8 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                 counts = {k: worker.counts[k] - c0[k] for k in c0}
                 counts.update(sink_stored=writer.ok - w0[1], writer_no_merchant=writer.skipped - w0[2],
                               writer_fail=writer.fail - w0[3])
+                if prof is not None:
+                    prof.disable()
                 client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
                 continue
             pub_task = asyncio.create_task(publish(0)) if nsteps else None
@@ -181,7 +191,12 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
             counts = {k: worker.counts[k] - c0[k] for k in c0}
             counts.update(sink_stored=writer.ok - w0[1], writer_no_merchant=writer.skipped - w0[2],
                           writer_fail=writer.fail - w0[3])
+            if prof is not None:
+                prof.disable()
             client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
+    if prof is not None:
+        os.makedirs(cfg["profile_dir"], exist_ok=True)
+        prof.dump_stats(os.path.join(cfg["profile_dir"], f"parser-r{rank}-w{widx}.pstats"))
     await writer.stop()
     await worker.stop()
 

@@ -1,0 +1,65 @@
+"""Answer canonicalisation for copy-span extractors (runs before post-processing).
+
+The reference asks Gemini for strings and lets post-processing parse them
+(gemini_parser.py:224-241); a hosted LLM quietly normalises as it answers
+(``$`` -> ``USD``).  The local extractor *copies* every value from the body
+(serving/fsm.py copy constraint), so a value can be a currency symbol or a
+date in a layout the reference chain mis-reads.  Two deterministic fixes, applied
+to every backend's answer by :func:`~smsgate_amd.parse.pipeline.postprocess_answer`:
+
+* **currency**: a symbol or word (``$ € ֏ ₽ ₾ £``, ``руб``, ``драм``…) becomes its
+  ISO 4217 code; codes pass through unchanged (ParsedSMS upper-cases them);
+* **day-first numeric dates with ``/`` or ``-``** (``06/05/2025 14:23``,
+  ``06-05-25``) become ISO ``2025-05-06 14:23``.  ``dateutil`` reads them
+  month-first, and the reference's body-date repair (``fix_broken_datetime``)
+  only knows dotted dates, so without this a ``dd/mm/yyyy`` SMS would be stored
+  with day and month swapped.  Day-first is the reference's own convention
+  (SYSTEM_INSTRUCTION: "Дата в сообщении обычно в формате день.месяц.год").
+  Dotted dates are left to the reference chain (its golden behaviour).
+
+Values that are not strings (a ``None`` from an LLM) pass through untouched, so
+D6 / D8 (null amount / card -> DLQ) stay as they were.
+"""
+from __future__ import annotations
+
+import re
+from typing import Any, Dict
+
+__all__ = ["CURRENCY_ALIASES", "canonical_currency", "canonical_date_text", "canonicalize_answer"]
+
+CURRENCY_ALIASES: Dict[str, str] = {
+    "$": "USD", "US$": "USD", "€": "EUR", "EURO": "EUR", "֏": "AMD", "ДРАМ": "AMD", "DRAM": "AMD",
+    "₽": "RUB", "РУБ": "RUB", "Р": "RUB", "RUR": "RUB", "₾": "GEL", "£": "GBP",
+}
+
+_DAY_FIRST = re.compile(r"(\d{1,2})[/-](\d{1,2})[/-](\d{4}|\d{2})(?![\d])(.*)\Z", re.S)
+
+
+def canonical_currency(value: Any) -> Any:
+    if not isinstance(value, str):
+        return value
+    v = value.strip().rstrip(".")
+    return CURRENCY_ALIASES.get(v.upper(), value)
+
+
+def canonical_date_text(value: Any) -> Any:
+    if not isinstance(value, str):
+        return value
+    m = _DAY_FIRST.match(value.strip())
+    if m is None:
+        return value
+    d, mo, y, rest = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4)
+    if not (1 <= d <= 31 and 1 <= mo <= 12):
+        return value
+    year = int(y) if len(y) == 4 else 2000 + int(y) if int(y) < 69 else 1900 + int(y)
+    return f"{year:04d}-{mo:02d}-{d:02d}{rest}"
+
+
+def canonicalize_answer(answer: Dict[str, Any]) -> Dict[str, Any]:
+    """A copy of ``answer`` with currency and date canonicalised (see module doc)."""
+    out = dict(answer)
+    if "currency" in out:
+        out["currency"] = canonical_currency(out["currency"])
+    if "date" in out:
+        out["date"] = canonical_date_text(out["date"])
+    return out

@@ -88,8 +88,14 @@ def _date_from_match(s: str, fmt: str) -> datetime:
 
 
 def fix_broken_datetime(body: str, current: datetime) -> datetime:
-    for rx, fmt in _BODY_DATE_PATTERNS:
-        m = rx.search(body)
+    # every dd.mm.yyyy match is also a dd.mm.yy match starting at the same place, so the
+    # first dd.mm.yy match bounds where a dd.mm.yyyy one can start: one full scan of the
+    # body instead of up to two (same precedence as the reference's loop)
+    (rx4, fmt4), (rx2, fmt2) = _BODY_DATE_PATTERNS
+    m2 = rx2.search(body)
+    if m2 is None:
+        return current
+    for m, fmt in ((rx4.search(body, m2.start()), fmt4), (m2, fmt2)):
         if m is None:
             continue
         try:

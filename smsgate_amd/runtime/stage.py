@@ -12,9 +12,12 @@ is the one loop, written once:
 * never dies on a handler exception (D1/D2), and bounds poison messages:
 
   - a :class:`~smsgate_amd.runtime.errors.TransientError` (engine restarting,
-    socket closed), a ``BusError`` or a ``ConnectionError`` (a publish / ack to the
-    broker failed mid-batch) naks the whole batch with a delay — not the
-    messages' fault, so it never counts toward dead-lettering;
+    socket closed), a ``BusUnavailable`` / ``ConnectionError`` / timeout (the
+    broker went away mid-batch) naks the whole batch with a delay — not the
+    messages' fault, so it never counts toward dead-lettering.  A plain
+    ``BusError`` is the broker refusing ONE request (a publish over the maximum
+    payload, no stream for a subject): that is a property of a message and takes
+    the isolate / dead-letter path below, so it cannot pin its batch forever;
   - any other exception re-runs the batch one message at a time, so the good
     messages of the batch go through and only the failing one is isolated;
     that one is nak'ed with a delay until it has been delivered
@@ -32,7 +35,7 @@ import logging
 import time
 from typing import Awaitable, Callable, List, Optional, Sequence
 
-from ..bus.base import Bus, BusError, Msg, Subscription
+from ..bus.base import Bus, BusUnavailable, Msg, Subscription
 from ..obs.errors import sentry_capture
 from .errors import TransientError
 
@@ -42,8 +45,13 @@ log = logging.getLogger(__name__)
 
 # not the messages' fault: the batch is nak'ed whole (never split into per-message
 # re-runs, never counted toward dead-lettering) -- a dependency (engine, broker) is
-# down or a publish / ack to the broker failed mid-batch
-TRANSIENT = (TransientError, BusError, ConnectionError)
+# down or the connection to the broker broke mid-batch.  (BusUnavailable is a
+# ConnectionError; a plain BusError -- the broker refused one request -- is not here.)
+TRANSIENT = (TransientError, BusUnavailable, ConnectionError, asyncio.TimeoutError, TimeoutError)
+
+# a dead-letter envelope carries at most this much of the failed payload: the payload
+# may be what the broker refused (over its maximum size), and the envelope must fit
+DLQ_ENTRY_MAX = 64 * 1024
 
 BatchHandler = Callable[[Sequence[Msg]], Awaitable[None]]
 DeadLetter = Callable[[Msg, BaseException], Awaitable[None]]
@@ -56,7 +64,10 @@ def dlq_publisher(bus: Bus, subject: str) -> DeadLetter:
 
     async def publish(m: Msg, exc: BaseException) -> None:
         data = m.data if isinstance(m.data, (bytes, bytearray)) else str(m.data).encode()
-        await bus.publish(subject, json.dumps({"err": str(exc), "entry": data.decode(errors="ignore")}).encode())
+        env = {"err": str(exc)[:4096], "entry": data[:DLQ_ENTRY_MAX].decode(errors="ignore")}
+        if len(data) > DLQ_ENTRY_MAX:
+            env["entry_truncated"] = len(data)  # original size; the entry holds its first DLQ_ENTRY_MAX bytes
+        await bus.publish(subject, json.dumps(env).encode())
 
     return publish
 

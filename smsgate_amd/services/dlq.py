@@ -21,7 +21,7 @@ import json
 import logging
 from typing import Any, Dict, List, Optional, Sequence
 
-from ..bus.base import SUBJECT_FAILED, SUBJECT_FAILED_FINAL, Bus, Msg
+from ..bus.base import SUBJECT_FAILED, SUBJECT_FAILED_FINAL, Bus, BusError, BusUnavailable, Msg
 from ..obs.metrics import DLQ_REPARSE_FAILED
 from ..models.domain import RawSMS
 from ..obs.tracing import Profiler
@@ -64,6 +64,7 @@ class DlqWorker:
         self.reparsed = 0
         self.not_reparsable = 0
         self.reparse_failed = 0
+        self.final_rejected = 0  # twice-failed messages the broker refused on the terminal subject
         self.log: List[Dict[str, Any]] = []
         # reparse runs under a profiler session (dlq_worker.py:70-74)
         self.profiler = Profiler("dlq_reparse")
@@ -99,14 +100,29 @@ class DlqWorker:
                 # worker consumes that subject, so a republish would re-feed it
                 # forever (and re-call the backend on every lap).
                 keep = [(s, p) for s, p in publishes if s != SUBJECT_FAILED]
+                final = []
                 for s, p in publishes:
                     if s == SUBJECT_FAILED:
                         self.reparse_failed += 1
                         DLQ_REPARSE_FAILED.inc()
                         log.warning("DLQ reparse failed again (moved to %s): %s", SUBJECT_FAILED_FINAL, p[:300])
-                        keep.append((SUBJECT_FAILED_FINAL, p))
+                        final.append((SUBJECT_FAILED_FINAL, p))
                 if keep:
                     await self.bus.publish_many(keep)
+                if final:
+                    try:
+                        await self.bus.publish_many(final)
+                    except BusUnavailable:
+                        raise  # broker gone: the stage naks the batch and retries it
+                    except BusError as exc:
+                        # the broker refuses the terminal subject (e.g. a reference-created
+                        # stream whose subject list could not be updated): log and ack --
+                        # retrying cannot succeed and must not pin the DLQ consumer
+                        self.final_rejected += len(final)
+                        log.error("DLQ: %s rejected %d twice-failed message(s), logged and acked: %s",
+                                  SUBJECT_FAILED_FINAL, len(final), exc)
+                        for _, p in final:
+                            log.error("DLQ twice-failed payload: %s", p[:2000])
             self.reparsed += len(to_reparse)
         for m in msgs:
             await m.ack()

@@ -69,7 +69,8 @@ class WriterService:
         for m in msgs:
             text = m.data.decode(errors="ignore")
             try:
-                p = ParsedSMS.model_validate(json.loads(text))
+                # one Rust pass parses and validates (the reference: json + model_validate)
+                p = ParsedSMS.model_validate_json(text)
                 if not p.merchant:
                     self.skipped += 1
                     continue

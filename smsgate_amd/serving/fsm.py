@@ -47,11 +47,14 @@ class FieldSpec:
     copy: bool = False
 
 
-# Token caps per field.  Measured on 20 k synthetic SMS of each vocabulary with the
-# extractor tokenizer (values written with the body's own tokens): max tokens seen
-# date 8, amount/balance 5, currency 1, card 3, merchant 18, city 5, address 11
-# (tests/test_fsm_caps.py pins a truncation rate of 0 on held-out data).  The caps
-# are about 2x those maxima: a cap only bounds the KV length reserved per slot
+# Token caps per field.  Measured on 20 k synthetic SMS of each vocabulary and of the
+# template families (utils/synth.py) with the extractor tokenizer (values written with
+# the body's own tokens): max tokens seen date 9, amount/balance 6, currency 2, card 3,
+# merchant 32, city 14 (Cyrillic names split into byte-level pieces), address 16
+# (tests/test_fsm_caps.py pins a truncation rate of 0 on held-out data,
+# tests/test_families.py that no family uses more than ~3/4 of a cap).  The caps
+# are about 1.5-2x those maxima (the total keeps Lmax at 288 KV positions per slot):
+# a cap only bounds the KV length reserved per slot
 # (rows stop at <sep>, so decode cost does not depend on it), and a value longer
 # than its cap would be silently cut.
 #
@@ -65,8 +68,8 @@ DEFAULT_FIELDS: Tuple[FieldSpec, ...] = (
     FieldSpec("amount", "number", 10, copy=True),
     FieldSpec("currency", "currency", 4, copy=True),
     FieldSpec("card", "card", 6, copy=True),
-    FieldSpec("merchant", "text", 32, copy=True),
-    FieldSpec("city", "text", 12, copy=True),
+    FieldSpec("merchant", "text", 48, copy=True),
+    FieldSpec("city", "text", 20, copy=True),
     FieldSpec("address", "text", 24, copy=True),
     FieldSpec("balance", "number", 10, copy=True),
 )
@@ -86,13 +89,21 @@ def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: in
     for i, t in enumerate(token_strings[:vocab]):
         if i in spec or not t:
             continue
-        out[i] = (TOK_STARTS_ALNUM if t[0].isalnum() else 0) | (TOK_ENDS_ALNUM if t[-1].isalnum() else 0)
+        # a byte-level piece of a multi-byte character decodes to U+FFFD: it is inside a
+        # word (Cyrillic letters), never a word boundary
+        out[i] = (TOK_STARTS_ALNUM if (t[0].isalnum() or t[0] == "\ufffd") else 0) | \
+            (TOK_ENDS_ALNUM if (t[-1].isalnum() or t[-1] == "\ufffd") else 0)
     return out
 
+# token classes by the characters of a token's text.  Dates may carry ASCII letters
+# (month names "10 Jun 2025", the ISO "T"); currencies are codes, symbols or words in
+# any script ("USD", "$", "руб") -- parse/canonical.py maps the last two to ISO codes
+_ASCII_LETTERS = set("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz")
+_CURRENCY_SYMBOLS = set("$€£₽₾֏")
 _CLASS_CHARS = {
-    "date": set("0123456789.:/- "),
+    "date": set("0123456789.:/-, ") | _ASCII_LETTERS,
     "number": set("0123456789.,- "),
-    "currency": set("ABCDEFGHIJKLMNOPQRSTUVWXYZ "),
+    "currency": {" "} | _CURRENCY_SYMBOLS,  # plus any alphabetic character (below)
     "card": set("0123456789* "),
 }
 
@@ -109,7 +120,7 @@ def _token_class_sets(token_strings: Sequence[str], specials: Sequence[int]) -> 
             continue  # pure-whitespace tokens only count as free text
         cs = set(s)
         for k, allowed in _CLASS_CHARS.items():
-            if cs <= allowed:
+            if cs <= allowed or (k == "currency" and all(ch in allowed or ch.isalpha() for ch in cs)):
                 out[k][i] = True
     return out
 

@@ -12,6 +12,7 @@ process does only scheduling: its Python work per message is a few slices.
 """
 from __future__ import annotations
 
+import itertools
 import json
 import struct
 from typing import Any, List, Sequence, Tuple
@@ -25,8 +26,8 @@ _HDR = struct.Struct("<cQI")
 
 def pack_ids(tag: bytes, req_id: int, seqs: Sequence[Sequence[int]]) -> bytes:
     n = len(seqs)
-    lens = np.fromiter((len(s) for s in seqs), dtype=np.uint16, count=n)
-    flat = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(lens.sum()))
+    lens = np.fromiter(map(len, seqs), dtype=np.uint16, count=n)
+    flat = np.array(list(itertools.chain.from_iterable(seqs)), dtype=np.int32)
     return _HDR.pack(tag, req_id, n) + lens.tobytes() + flat.tobytes()
 
 

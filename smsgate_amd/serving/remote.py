@@ -289,22 +289,8 @@ class RemoteEngineClient:
             conn.send_bytes(P.pack_control(obj))
 
     def decode_answers(self, seqs: List[List[int]]) -> List[Dict[str, str]]:
-        sep = self.tok.sep
-        nf = len(self.fields)
-        pieces: List[List[int]] = []
-        for toks in seqs:
-            vals: List[List[int]] = [[]]
-            for t in toks:
-                if t == sep:
-                    if len(vals) == nf:
-                        break
-                    vals.append([])
-                else:
-                    vals[-1].append(t)
-            vals += [[]] * (nf - len(vals))
-            pieces.extend(vals)
-        texts = self.tok.decode_batch(pieces) if pieces else []
-        return [{f: texts[j * nf + i].strip() for i, f in enumerate(self.fields)} for j in range(len(seqs))]
+        fields = self.fields
+        return [dict(zip(fields, vals)) for vals in self.tok.decode_fields(seqs, len(fields))]
 
     async def extract(self, bodies: Sequence[str]) -> List[Dict[str, str]]:
         ids = self.tok.message_ids(list(bodies), self.max_body)

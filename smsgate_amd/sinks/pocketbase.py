@@ -17,13 +17,16 @@ of two copy-pasted clients and a duplicated ``get_pb_client``.
 
 Throughput: the reference's upsert costs two HTTP round trips per record (GET by
 filter, then POST/PATCH).  :meth:`PocketBaseClient.batch_upsert` writes up to 50
-records in ONE ``POST /api/batch`` request (PocketBase ≥ 0.23, batch API enabled):
-each record is a ``PUT`` (upsert) on a record id derived from its msg_id
-(:func:`record_id`), so no lookup is needed.  The sink uses it when the server
-supports it and falls back to the per-record path for a chunk the server
-refuses (batch API disabled -> per-record from then on; a chunk that fails, e.g.
-a msg_id already stored under another id by the reference's writer -> that
-chunk per record).  ``scripts/sink_bench.py`` measures both paths.
+records in TWO requests (PocketBase ≥ 0.23, batch API enabled): one list query
+for the chunk's msg_ids (``msg_id='a' || msg_id='b' …``), then one ``POST
+/api/batch`` in which a msg_id already stored is a ``PATCH`` of the record that
+holds it (whatever its id: the reference's writer lets PocketBase pick ids) and a
+new one is a ``PUT`` on the id derived from its msg_id (:func:`record_id`).  The
+per-record path creates records with that same derived id, so the two paths never
+write one msg_id twice -- also on the reference schema, whose msg_id index is not
+unique (pb_schema.json:149).  The sink falls back to the per-record path for a
+chunk the server refuses (batch API disabled -> per-record from then on).
+``scripts/sink_bench.py`` measures both paths.
 """
 from __future__ import annotations
 
@@ -123,17 +126,47 @@ class PocketBaseClient:
             r = await self._client.patch(f"/api/collections/{collection}/records/{rec_id}", json=dict(record))
             r.raise_for_status()
             return "patched"
-        r = await self._client.post(f"/api/collections/{collection}/records", json=dict(record))
+        # created under the msg_id-derived id, the id the batch path PUTs: both paths
+        # address one record per msg_id
+        r = await self._client.post(f"/api/collections/{collection}/records",
+                                    json={"id": record_id(msg_id), **dict(record)})
         r.raise_for_status()
         return "created"
+
+    async def existing_ids(self, collection: str, msg_ids: Sequence[str]) -> Dict[str, str]:
+        """msg_id -> id of a record already holding it (one list request per call)."""
+        uniq = list(dict.fromkeys(msg_ids))
+        if not uniq:
+            return {}
+        params = {"filter": " || ".join(f"msg_id={_q(m)}" for m in uniq), "page": 1,
+                  "perPage": max(len(uniq) * 2, 30), "fields": "id,msg_id"}
+        r = await self._client.get(f"/api/collections/{collection}/records", params=params)
+        r.raise_for_status()
+        out: Dict[str, str] = {}
+        for it in r.json().get("items", []):
+            out.setdefault(str(it.get("msg_id")), str(it["id"]))
+        return out
 
     async def batch_upsert(self, collection: str, records: Sequence[Mapping[str, Any]]) -> Optional[bool]:
         """Upsert ``records`` (each with its ``msg_id``) in one ``POST /api/batch``.
         Returns True when stored, False when the server refused this batch (the
         caller retries it per record), None when the server has no batch API."""
         await self._ensure_auth()
-        reqs = [{"method": "PUT", "url": f"/api/collections/{collection}/records",
-                 "body": {"id": record_id(str(r["msg_id"])), **dict(r)}} for r in records]
+        try:
+            have = await self.existing_ids(collection, [str(r["msg_id"]) for r in records])
+        except httpx.HTTPError as exc:
+            log.warning("PocketBase msg_id lookup failed: %s", exc)
+            return False
+        reqs = []
+        for rec in records:
+            m = str(rec["msg_id"])
+            if m in have:
+                reqs.append({"method": "PATCH", "url": f"/api/collections/{collection}/records/{have[m]}",
+                             "body": dict(rec)})
+            else:
+                reqs.append({"method": "PUT", "url": f"/api/collections/{collection}/records",
+                             "body": {"id": record_id(m), **dict(rec)}})
+                have[m] = record_id(m)  # a repeated msg_id in the same chunk updates that record
         try:
             r = await self._client.post("/api/batch", json={"requests": reqs})
         except httpx.HTTPError as exc:

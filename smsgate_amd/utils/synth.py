@@ -2,27 +2,47 @@
 
 There is no dataset on the box (and the reference ships none — its only
 fixtures are the three CASES of tests/test_parsers.py:11-58), so every
-benchmark and tokenizer corpus here is generated.  The formats follow the
-reference's real-world examples:
+benchmark and tokenizer corpus here is generated.
 
-* ``APPROVED PURCHASE DB SALE: MERCHANT, CITY[, ADDRESS],dd.mm.yy HH:MM,card ***NNNN. Amount:X CUR, Balance:Y CUR``
-  (and the PURCHASE / SALE / PURCHASE DB INTERNET / PURCH.COMPLETION.DB INTERNET prefixes,
-  process_cached.py:98-120);
-* the multi-line ``DEBIT ACCOUNT&#10;…`` account format (test case 3);
-* credit/C2C/OTP/insufficient-funds notifications (worker-skipped kinds).
+Two generators share one output type (:class:`SynthSMS`):
 
-:func:`generate` is deterministic for a seed.  Each item carries the body and
-the expected extraction answer (the LLM JSON shape), so a trained extractor
-can be scored and the regex backend cross-checked.
+* the **legacy mix** (``generate(..., families=None)``): the reference's two
+  real-world purchase formats — ``APPROVED PURCHASE DB SALE: MERCHANT, CITY[,
+  ADDRESS],dd.mm.yy HH:MM,card ***NNNN. Amount:X CUR, Balance:Y CUR``
+  (process_cached.py:98-120) and the multi-line ``DEBIT ACCOUNT&#10;…`` format of
+  test case 3 — plus credit / OTP / insufficient-funds notifications
+  (worker-skipped kinds);
+* **template families** (``families="train" | "heldout" | "all" | [names]``):
+  :data:`FAMILIES` — 24 hand-written bank-SMS layouts plus 5 procedural ones
+  (a random layout per message, training only) in English, Russian (Cyrillic) and
+  Russian transliterated to Latin: different field orders and separators, label
+  words (``Amount`` / ``Amt`` / ``Сумма`` / ``Summa``…), date styles
+  (``dd.mm.yy HH:MM``, ``yyyy-mm-dd``, ``dd/mm/yyyy``, ``10 Jun 2025``, time
+  first…), currency as a code or a symbol before / after the number (``$``,
+  ``€``, ``֏``, ``₽``, ``руб.``), card masks (``*1234``, ``****1234``,
+  ``4083***7538``, ``ending 1234``…), single- vs multi-line, optional address /
+  balance, debit and credit.  The split is **by family**: :data:`HELDOUT_FAMILIES`
+  never occur in training, so scoring on them measures what the Gemini prompt
+  (gemini_parser.py:37-43, a format-agnostic instruction) is for — formats the
+  extractor has never seen.  The legacy formats are train families.
+
+Each item carries the body, the LLM answer (the nine strings the extractor
+copies from the body, the Gemini JSON shape) and ``expected`` — the final
+normalised values (``datetime``, ``Decimal``, ISO currency, 4-digit card) a
+correct parse must produce, computed by the generator itself rather than by the
+pipeline under test.  :func:`generate` is deterministic for a seed.
 """
 from __future__ import annotations
 
 import random
 import zlib
-from dataclasses import dataclass
-from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+from dataclasses import dataclass, field
+from datetime import datetime
+from decimal import Decimal
+from typing import Any, Callable, Dict, Iterator, List, Optional, Sequence, Tuple, Union
 
-__all__ = ["SynthSMS", "generate", "generate_bodies", "reference_cases", "vocab", "Vocab", "TRAFFIC_KINDS"]
+__all__ = ["SynthSMS", "generate", "generate_bodies", "generate_traffic", "reference_cases", "vocab", "Vocab",
+           "TRAFFIC_KINDS", "TRAFFIC", "FAMILIES", "TRAIN_FAMILIES", "HELDOUT_FAMILIES", "family_names"]
 
 # Real-looking merchant words.  The reference's golden answers (tests/test_parsers.py:11-58:
 # TEST, LLC, MOSKOW, AMERIABANK, API, GATE, AM, "TEST STR.") are deliberately absent from
@@ -47,6 +67,9 @@ _ONSETS = ["B", "D", "G", "K", "L", "M", "N", "P", "R", "S", "T", "V", "Z", "KH"
            "BR", "DR", "KR", "TR", "CH", "Y", "H", "F"]
 _VOWELS = ["A", "E", "I", "O", "U", "YA", "OU", "EA", "IO"]
 _CODAS = ["", "", "", "N", "R", "S", "K", "T", "M", "L", "RT", "NK"]
+# the worker's skip keywords (parse/text.py) must not occur as whole words in a generated
+# transaction: "OTP" / "CODE" / "PASS" as a merchant name would be skipped before the LLM
+_SKIP_WORDS = frozenset({"OTP", "CODE", "PASS"})
 
 
 def _pseudo_words(seed: int = 20240601, n: int = 20000, exclude=frozenset()) -> List[str]:
@@ -68,7 +91,7 @@ def _random_strings(seed: int = 99, n: int = 6000) -> List[str]:
     r = random.Random(seed)
     alpha = "ABCDEFGHIJKLMNOPQRSTUVWXYZ"
     out: List[str] = []
-    seen = set(_GOLDEN_VOCAB)
+    seen = set(_GOLDEN_VOCAB) | _SKIP_WORDS
     while len(out) < n:
         k = r.randint(2, 10)
         w = "".join(r.choice(alpha if r.random() < 0.9 else "0123456789") for _ in range(k))
@@ -84,6 +107,26 @@ def _split(words: Sequence[str]) -> Tuple[List[str], List[str]]:
     for w in words:
         (ho if zlib.crc32(w.encode()) % 5 == 0 else tr).append(w)
     return tr, ho
+
+
+# Latin -> Cyrillic letter map for Russian-language families (digraphs first): pseudo
+# names keep their syllable structure, so Cyrillic merchants are as unpredictable as Latin
+_CYR_DI = (("KH", "Х"), ("SH", "Ш"), ("TS", "Ц"), ("CH", "Ч"), ("YA", "Я"), ("OU", "У"), ("IO", "ИО"))
+_CYR_1 = dict(zip("ABCDEFGHIJKLMNOPQRSTUVWXYZ", "АКЦДЕФГХИЖКЛМНОПКРСТУВВКЙЗ"))
+
+
+def to_cyrillic(word: str) -> str:
+    out, i = [], 0
+    while i < len(word):
+        for a, b in _CYR_DI:
+            if word.startswith(a, i):
+                out.append(b)
+                i += len(a)
+                break
+        else:
+            out.append(_CYR_1.get(word[i], word[i]))
+            i += 1
+    return "".join(out)
 
 
 @dataclass(frozen=True)
@@ -133,6 +176,10 @@ class SynthSMS:
     kind: str  # purchase | account | credit | otp | funds
     answer: Optional[Dict[str, Optional[str]]]  # expected LLM JSON answer (None for skipped kinds)
     timestamp: int
+    family: str = "legacy"
+    # final values of a correct parse (txn_type, date: datetime, amount / balance: Decimal,
+    # currency: ISO code, card: 4 digits, merchant / city / address); None for skipped kinds
+    expected: Optional[Dict[str, Any]] = field(default=None, repr=False)
 
 
 def _amount(r: random.Random, cur: str) -> str:
@@ -164,69 +211,577 @@ def _date(r: random.Random, year4: bool = False) -> str:
     return f"{d:02d}.{m:02d}.{ys} {hh:02d}:{mm:02d}"
 
 
+def _dec(s: str) -> Decimal:
+    from ..parse.numeric import parse_ambiguous_decimal
+
+    return parse_ambiguous_decimal(s)
+
+
+def _legacy_expected(ans: Dict[str, str]) -> Dict[str, Any]:
+    return dict(txn_type=ans["txn_type"], date=datetime.strptime(ans["date"], "%d.%m.%Y %H:%M")
+                if len(ans["date"]) == 16 else datetime.strptime(ans["date"], "%d.%m.%y %H:%M"),
+                amount=_dec(ans["amount"]), currency=ans["currency"], card=ans["card"].replace("*", "")[-4:],
+                merchant=ans["merchant"], city=ans["city"], address=ans["address"], balance=_dec(ans["balance"]))
+
+
+def _legacy_purchase(r: random.Random, v: Vocab, ts: int, cur: str, card: str) -> SynthSMS:
+    merchant, city = _merchant(r, v), r.choice(v.cities)
+    address = _address(r, v) if r.random() < 0.6 else ""
+    place = f"{merchant}, {city}" + (f", {address}" if address else "")
+    date = _date(r)
+    amt, bal = _amount(r, cur), _amount(r, cur)
+    pre = r.choice(_PREFIXES)
+    status = r.choice(("APPROVED ", "APPROVED ", ""))
+    body = f"{status}{pre}: {place},{date},card ***{card}. Amount:{amt} {cur}, Balance:{bal} {cur}"
+    ans = dict(txn_type="debit", date=date, amount=amt, currency=cur, card=f"***{card}", merchant=merchant,
+               city=city, address=address, balance=bal)
+    return SynthSMS(body, "purchase", ans, ts, "legacy_purchase", _legacy_expected(ans))
+
+
+def _legacy_account(r: random.Random, v: Vocab, ts: int, cur: str, card: str) -> SynthSMS:
+    merchant, city = _merchant(r, v), r.choice(v.cities)
+    date = _date(r, year4=True)
+    amt, bal = _amount(r, cur), _amount(r, cur)
+    first = f"{r.randint(1000, 9999)}"
+    body = (f"DEBIT ACCOUNT&#10;{amt} {cur}&#10;{first}***{card},&#10;{merchant}, {city}"
+            f"&#10;{date}&#10;BALANCE: {bal} {cur}")
+    ans = dict(txn_type="debit", date=date, amount=amt, currency=cur, card=card, merchant=merchant,
+               city=city, address="", balance=bal)
+    return SynthSMS(body, "account", ans, ts, "legacy_account", _legacy_expected(ans))
+
+
+def _legacy_credit(r: random.Random, ts: int, cur: str, card: str,
+                   kinds: Tuple[str, ...] = ("CREDIT PAYMENT", "C2C RECEIVED", "TRANSFER IN")) -> SynthSMS:
+    kind = r.choice(kinds)
+    date = _date(r)
+    amt, bal = _amount(r, cur), _amount(r, cur)
+    body = f"{kind}: {date},card ***{card}. Amount:{amt} {cur}, Balance:{bal} {cur}"
+    ans = dict(txn_type="credit", date=date, amount=amt, currency=cur, card=f"***{card}", merchant="",
+               city="", address="", balance=bal)
+    return SynthSMS(body, "credit", ans, ts, "legacy_credit", _legacy_expected(ans))
+
+
 def _one(r: random.Random, v: Vocab) -> SynthSMS:
     ts = r.randint(1_690_000_000, 1_750_000_000)
     x = r.random()
     cur = r.choice(_CURRENCIES)
     card = f"{r.randint(0, 9999):04d}"
     if x < 0.55:
-        merchant, city = _merchant(r, v), r.choice(v.cities)
-        address = _address(r, v) if r.random() < 0.6 else ""
-        place = f"{merchant}, {city}" + (f", {address}" if address else "")
-        date = _date(r)
-        amt, bal = _amount(r, cur), _amount(r, cur)
-        pre = r.choice(_PREFIXES)
-        status = r.choice(("APPROVED ", "APPROVED ", ""))
-        body = f"{status}{pre}: {place},{date},card ***{card}. Amount:{amt} {cur}, Balance:{bal} {cur}"
-        ans = dict(txn_type="debit", date=date, amount=amt, currency=cur, card=f"***{card}", merchant=merchant,
-                   city=city, address=address, balance=bal)
-        return SynthSMS(body, "purchase", ans, ts)
+        return _legacy_purchase(r, v, ts, cur, card)
     if x < 0.80:
-        merchant, city = _merchant(r, v), r.choice(v.cities)
-        date = _date(r, year4=True)
-        amt, bal = _amount(r, cur), _amount(r, cur)
-        first = f"{r.randint(1000, 9999)}"
-        body = (f"DEBIT ACCOUNT&#10;{amt} {cur}&#10;{first}***{card},&#10;{merchant}, {city}"
-                f"&#10;{date}&#10;BALANCE: {bal} {cur}")
-        ans = dict(txn_type="debit", date=date, amount=amt, currency=cur, card=card, merchant=merchant,
-                   city=city, address="", balance=bal)
-        return SynthSMS(body, "account", ans, ts)
+        return _legacy_account(r, v, ts, cur, card)
     if x < 0.90:
-        kind = r.choice(("CREDIT PAYMENT", "C2C RECEIVED", "TRANSFER IN"))
-        date = _date(r)
-        amt, bal = _amount(r, cur), _amount(r, cur)
-        body = f"{kind}: {date},card ***{card}. Amount:{amt} {cur}, Balance:{bal} {cur}"
-        ans = dict(txn_type="credit", date=date, amount=amt, currency=cur, card=f"***{card}", merchant="",
-                   city="", address="", balance=bal)
-        return SynthSMS(body, "credit", ans, ts)
+        return _legacy_credit(r, ts, cur, card)
     if x < 0.96:
         code = r.randint(100000, 999999)
         body = r.choice((f"Your OTP code: {code}. Do not share it.", f"CODE: {code} for login",
                          f"PASS={code} valid 5 min"))
-        return SynthSMS(body, "otp", None, ts)
+        return SynthSMS(body, "otp", None, ts, "legacy_otp")
     body = f"DECLINED: INSUFFICIENT FUNDS, {_merchant(r, v)}, card ***{card}"
-    return SynthSMS(body, "funds", None, ts)
+    return SynthSMS(body, "funds", None, ts, "legacy_funds")
 
 
-# traffic mixes (bench.py --traffic): "mixed" = every kind in its natural share (17 % are
-# skipped by the parser's keyword filter and never reach the LLM); "purchase" = debit
-# transactions only (the store-purchase and account-debit formats), every message
-# LLM-routed -- the reference's BASELINE harness timed purchase bodies only
-TRAFFIC_KINDS = {"mixed": None, "purchase": ("purchase", "account")}
+# ---------------------------------------------------------------- template families
+# currency symbols / words and the ISO code a correct parse maps them to
+# (parse/canonical.py CURRENCY_ALIASES is the parse-side table; tests pin they agree)
+_SYMBOL = {"USD": "$", "EUR": "€", "AMD": "֏", "RUB": "₽", "GEL": "₾", "GBP": "£"}
+_WORD = {"RUB": "руб.", "AMD": "драм"}
+_FAMILY_CURRENCIES = ("AMD", "USD", "EUR", "RUB", "GEL", "GBP")
+
+# date styles: strftime format, whether the time of day is part of the value
+_DATE_STYLES: Dict[str, Tuple[str, bool]] = {
+    "dmy2": ("%d.%m.%y %H:%M", True),
+    "dmy4": ("%d.%m.%Y %H:%M", True),
+    "dmy4_date": ("%d.%m.%Y", False),
+    "dmy2_date": ("%d.%m.%y", False),
+    "iso": ("%Y-%m-%d %H:%M", True),
+    "iso_t": ("%Y-%m-%dT%H:%M:%S", True),
+    "slash": ("%d/%m/%Y %H:%M", True),
+    "mon": ("%d %b %Y %H:%M", True),
+    "mon_up": ("%d-%b-%Y %H:%M", True),
+    "time_first": ("%H:%M %d.%m.%Y", True),
+}
+# per language: date styles, money layouts, number formats, card masks
+_STYLE_POOLS = {
+    "en": dict(dates=("dmy2", "dmy4", "iso", "iso_t", "slash", "mon", "mon_up"),
+               money=("code_after", "code_after", "code_before", "sym_before", "sym_after"),
+               numbers=("dot", "comma_dot", "comma_dot", "int"),
+               cards=("star1", "stars2", "stars3", "stars4", "spaced", "first_mask", "ending")),
+    "ru": dict(dates=("dmy2", "dmy4", "dmy4_date", "dmy2_date", "time_first", "iso"),
+               money=("code_after", "sym_after", "word_after"),
+               numbers=("space_comma", "space_comma", "comma", "dot", "int"),
+               cards=("star1", "stars2", "stars4", "spaced", "first_mask")),
+    "tr": dict(dates=("dmy2", "dmy4", "time_first", "iso", "slash"),
+               money=("code_after", "code_before", "sym_after"),
+               numbers=("dot", "comma", "space_comma", "comma_dot"),
+               cards=("star1", "stars2", "stars4", "first_mask")),
+}
+_NOISE = {
+    "en": ("", "", "", " Thank you.", " Details in the app.", " Bank."),
+    "ru": ("", "", "", " Спасибо!", " Подробнее в приложении."),
+    "tr": ("", "", "", " Spasibo!", " Podrobnee v prilozhenii."),
+}
+
+
+def _fmt_number(r: random.Random, style: str, v: Decimal, cur: str) -> str:
+    if style == "int" and cur not in ("AMD", "RUB"):
+        style = "dot"
+    if style == "int":
+        return str(int(v))
+    q = f"{v:.2f}"
+    whole, frac = q.split(".")
+    if style == "dot":
+        return q
+    if style == "comma":
+        return f"{whole},{frac}"
+    grouped = f"{int(whole):,}"
+    if style == "comma_dot":
+        return f"{grouped}.{frac}"
+    if style == "space_comma":
+        return f"{grouped.replace(',', ' ')},{frac}"
+    raise ValueError(style)
+
+
+class _Ctx:
+    """Values of one message, rendered in the family's styles; every value a
+    template writes is recorded as the answer (the exact body substring)."""
+
+    def __init__(self, r: random.Random, v: Vocab, fam: "Family", ts: int) -> None:
+        self.r, self.v, self.fam, self.ts = r, v, fam, ts
+        pools = _STYLE_POOLS[fam.lang]
+        self.cur = r.choice(fam.currencies or _FAMILY_CURRENCIES)
+        self.money = r.choice(fam.money or pools["money"])
+        if self.money.startswith("sym") and self.cur not in _SYMBOL:
+            self.money = "code_after"
+        if self.money == "word_after" and self.cur not in _WORD:
+            self.money = "code_after"
+        self.num_style = r.choice(pools["numbers"])
+        self.date_style = r.choice(fam.dates or pools["dates"])
+        self.card_style = r.choice(fam.cards or pools["cards"])
+        cyr = fam.lang == "ru" and r.random() < 0.5
+        self.cyr = cyr
+        self.case = r.choice(fam.cases)
+        self.ans: Dict[str, str] = dict(txn_type=fam.txn, date="", amount="", currency="", card="", merchant="",
+                                        city="", address="", balance="")
+        self.exp: Dict[str, Any] = dict(txn_type=fam.txn, amount=Decimal("0.0"), currency=None, card=None,
+                                        merchant="", city="", address="", balance=Decimal("0.0"))
+
+    # ---- names
+    def _name(self, w: str) -> str:
+        if self.cyr:
+            w = to_cyrillic(w)
+        return w.title() if self.case == "title" else w
+
+    def M(self) -> str:
+        m = " ".join(self._name(self.r.choice(self.v.words)) for _ in range(self.r.choice((1, 1, 2, 2, 3))))
+        if self.r.random() < 0.06:
+            m += f" {self.r.randint(1, 999)}"
+        self.ans["merchant"] = self.exp["merchant"] = m
+        return m
+
+    def C(self) -> str:
+        c = self._name(self.r.choice(self.v.cities))
+        self.ans["city"] = self.exp["city"] = c
+        return c
+
+    def A(self) -> str:
+        st = self._name(self.r.choice(self.v.streets))
+        n = self.r.randint(1, 150)
+        if self.fam.lang == "ru":
+            a = f"{self.r.choice(('ул.', 'пр.', 'ул.'))} {st} {n}"
+        elif self.fam.lang == "tr":
+            a = f"{self.r.choice(('ul.', 'pr.'))} {st} {n}"
+        else:
+            sfx = self.r.choice(_STREET_SUFFIXES)
+            a = f"{st} {sfx.title() if self.case == 'title' else sfx} {n}"
+        self.ans["address"] = self.exp["address"] = a
+        return a
+
+    # ---- date
+    def D(self) -> str:
+        r = self.r
+        fmt, timed = _DATE_STYLES[self.date_style]
+        dt = datetime(r.choice((2023, 2024, 2025)), r.randint(1, 12), r.randint(1, 28),
+                      r.randint(0, 23), r.randint(0, 59), r.randint(0, 59) if "%S" in fmt else 0)
+        if not timed:
+            dt = dt.replace(hour=0, minute=0, second=0)
+        s = dt.strftime(fmt)
+        if self.date_style == "mon_up":
+            s = s.upper()
+        self.ans["date"] = s
+        self.exp["date"] = dt
+        return s
+
+    # ---- money
+    def _value(self) -> Decimal:
+        big = self.cur in ("AMD", "RUB")
+        v = self.r.uniform(100, 250000) if big else self.r.uniform(1, 5000)
+        return Decimal(f"{v:.2f}")
+
+    def _money(self, key: str) -> str:
+        v = self._value()
+        num = _fmt_number(self.r, self.num_style, v, self.cur)
+        if self.num_style == "int" and self.cur in ("AMD", "RUB"):
+            v = Decimal(int(v))
+        cur = {"code_after": self.cur, "code_before": self.cur, "sym_before": _SYMBOL.get(self.cur),
+               "sym_after": _SYMBOL.get(self.cur), "word_after": _WORD.get(self.cur)}[self.money]
+        cur_value = cur[:-1] if cur.endswith(".") else cur  # "руб." -> the word, not its dot
+        if self.money == "code_before":
+            s = f"{cur} {num}"
+        elif self.money == "sym_before":
+            s = f"{cur}{num}"
+        elif self.money == "sym_after" and self.r.random() < 0.3:
+            s = f"{num}{cur}"
+        else:
+            s = f"{num} {cur}"
+        self.ans[key] = num
+        self.exp[key] = v
+        if not self.ans["currency"]:
+            self.ans["currency"] = cur_value
+            self.exp["currency"] = self.cur
+        return s
+
+    def AMT(self) -> str:
+        return self._money("amount")
+
+    def BAL(self) -> str:
+        return self._money("balance")
+
+    # ---- card
+    def CARD(self) -> str:
+        c = f"{self.r.randint(0, 9999):04d}"
+        st = self.card_style
+        if st == "first_mask":  # normalize_body masks it to CARD:NNNN (gemini_parser.py:121-137)
+            s, a = f"{self.r.randint(1000, 9999)}***{c}", c
+        elif st == "spaced":
+            s, a = f"**** {c}", c
+        elif st == "ending":
+            s, a = f"ending {c}", c
+        else:
+            stars = {"star1": "*", "stars2": "**", "stars3": "***", "stars4": "****"}[st]
+            s = a = f"{stars}{c}"
+        self.ans["card"] = a
+        self.exp["card"] = c
+        return s
+
+    def pick(self, *opts: str) -> str:
+        return self.r.choice(opts)
+
+    def noise(self) -> str:
+        return self.r.choice(_NOISE[self.fam.lang])
+
+
+@dataclass(frozen=True)
+class Family:
+    name: str
+    lang: str  # en | ru | tr (Russian in Latin letters)
+    txn: str  # debit | credit
+    render: Callable[[_Ctx], str]
+    heldout: bool = False
+    cases: Tuple[str, ...] = ("upper",)
+    dates: Tuple[str, ...] = ()  # () = the language's pool
+    money: Tuple[str, ...] = ()
+    cards: Tuple[str, ...] = ()
+    currencies: Tuple[str, ...] = ()
+
+
+def _opt(c: _Ctx, p: float, f: Callable[[], str], pre: str = ", ") -> str:
+    return pre + f() if c.r.random() < p else ""
+
+
+# Labels are shared across families (each family draws from the language's synonyms),
+# so a held-out family is a NEW LAYOUT of label words the model has seen elsewhere.
+def _bal_en(c: _Ctx) -> str:
+    return c.pick("Balance", "Bal", "Avail. balance", "Available", "Avl bal", "Remaining balance")
+
+
+def _bal_ru(c: _Ctx) -> str:
+    return c.pick("Остаток", "Баланс", "Доступно")
+
+
+def _bal_tr(c: _Ctx) -> str:
+    return c.pick("ostatok", "Ostatok", "dostupno", "Dostupno", "balans")
+
+
+FAMILIES: Tuple[Family, ...] = (
+    # ---- English, training
+    Family("en_card_at", "en", "debit", lambda c: (
+        f"{c.pick('Card', 'CARD', 'card')} {c.CARD()}: {c.pick('purchase', 'Purchase', 'POS purchase', 'payment')} "
+        f"{c.AMT()} at {c.M()}, {c.C()}{_opt(c, 0.3, c.A)}. {c.D()}. {_bal_en(c)} {c.BAL()}{c.noise()}"),
+        cases=("upper", "upper", "title")),
+    Family("en_pipe", "en", "debit", lambda c: (
+        f"{c.M()} | {c.C()} | {c.AMT()} | card {c.CARD()} | {c.D()} | {_bal_en(c)} {c.BAL()}")),
+    Family("en_ml_labels", "en", "debit", lambda c: (
+        f"{c.pick('Purchase', 'PURCHASE', 'Payment', 'Card payment')}\n{c.pick('Card', 'Card no')}: {c.CARD()}\n"
+        f"{c.pick('Amount', 'Amt', 'Sum')}: {c.AMT()}\n{c.pick('Merchant', 'Shop', 'Payee')}: {c.M()}\n"
+        f"{c.pick('City', 'Location')}: {c.C()}\n{c.pick('Date', 'Time')}: {c.D()}\n{_bal_en(c)}: {c.BAL()}"),
+        cases=("upper", "title")),
+    Family("en_you_paid", "en", "debit", lambda c: (
+        f"You {c.pick('paid', 'spent')} {c.AMT()} {c.pick('to', 'at')} {c.M()} in {c.C()} with card {c.CARD()} "
+        f"on {c.D()}. {_bal_en(c)} {c.BAL()}{c.noise()}"), cases=("title", "upper")),
+    Family("en_pos_semicolon", "en", "debit", lambda c: (
+        f"{c.pick('POS PURCHASE', 'POS', 'PURCHASE')} {c.AMT()}; {c.M()}; {c.A()}, {c.C()}; card {c.CARD()}; "
+        f"{c.D()}; bal: {c.BAL()}")),
+    Family("en_charged_nobal", "en", "debit", lambda c: (
+        f"{c.pick('Card', 'Your card')} {c.CARD()} was charged {c.AMT()} at {c.M()}, {c.C()} on {c.D()}.{c.noise()}"),
+        cases=("upper", "title")),
+    Family("en_upper_compact", "en", "debit", lambda c: (
+        f"DEBIT {c.AMT()} CARD{c.CARD()} {c.M()}/{c.C()} {c.D()} BAL:{c.BAL()}"),
+        cards=("star1", "stars2", "stars3", "stars4")),
+    Family("en_internet", "en", "debit", lambda c: (
+        f"{c.pick('Internet purchase', 'Online payment', 'E-commerce purchase')} {c.AMT()} {c.M()} card {c.CARD()} "
+        f"{c.D()}. {_bal_en(c)}: {c.BAL()}")),
+    Family("en_location_ml", "en", "debit", lambda c: (
+        f"TRANSACTION: {c.pick('PURCHASE', 'POS', 'PAYMENT')}\nAMOUNT: {c.AMT()}\nCARD: {c.CARD()}\n"
+        f"MERCHANT: {c.M()}\nLOCATION: {c.C()}, {c.A()}\nDATE: {c.D()}\nBALANCE: {c.BAL()}")),
+    Family("en_bracket", "en", "debit", lambda c: (
+        f"[{c.M()}] [{c.C()}] {c.AMT()} card {c.CARD()} {c.D()} {c.pick('balance', 'bal')} {c.BAL()}")),
+    Family("en_refund", "en", "credit", lambda c: (
+        f"{c.pick('Refund', 'Reversal', 'Credit')} {c.AMT()} to card {c.CARD()} from {c.M()}, {c.C()} on {c.D()}. "
+        f"{_bal_en(c)} {c.BAL()}")),
+    # ---- Russian (Cyrillic), training
+    Family("ru_pokupka", "ru", "debit", lambda c: (
+        f"{c.pick('Покупка', 'Оплата', 'Списание')} {c.AMT()} {c.M()}, {c.C()}{_opt(c, 0.3, c.A)}. "
+        f"{c.pick('Карта', 'карта')} {c.CARD()}. {c.D()}. {_bal_ru(c)} {c.BAL()}{c.noise()}")),
+    Family("ru_oplata_ml", "ru", "debit", lambda c: (
+        f"{c.pick('Оплата', 'Покупка')}\n{c.pick('Карта', 'карта')} {c.CARD()}\n{c.pick('Сумма', 'Списано')}: "
+        f"{c.AMT()}\n{c.M()}\n{c.C()}\n{c.D()}\n{_bal_ru(c)}: {c.BAL()}")),
+    Family("ru_spisanie", "ru", "debit", lambda c: (
+        f"{c.D()} {c.pick('Списание', 'Покупка')} {c.AMT()}, карта {c.CARD()}, {c.M()}, г. {c.C()}. "
+        f"{_bal_ru(c)}: {c.BAL()}")),
+    Family("ru_nobal", "ru", "debit", lambda c: (
+        f"Покупка по карте {c.CARD()} на {c.AMT()}{c.pick(': ', ' в ')}{c.M()}, {c.C()}. {c.D()}{c.noise()}")),
+    Family("ru_zachislenie", "ru", "credit", lambda c: (
+        f"{c.pick('Зачисление', 'Возврат')} {c.AMT()} на карту {c.CARD()} от {c.M()}. {c.D()}. "
+        f"{_bal_ru(c)}: {c.BAL()}")),
+    # ---- Russian transliterated, training
+    Family("tr_pokupka_ml", "tr", "debit", lambda c: (
+        f"{c.pick('Pokupka', 'Oplata')}: {c.AMT()}\n{c.pick('Karta', 'karta')}: {c.CARD()}\n"
+        f"{c.pick('Mesto', 'Magazin')}: {c.M()}, {c.C()}\n{c.pick('Data', 'Vremya')}: {c.D()}\n"
+        f"{_bal_tr(c).title()}: {c.BAL()}")),
+    Family("tr_spisanie", "tr", "debit", lambda c: (
+        f"{c.pick('Spisanie', 'Pokupka', 'Summa')} {c.AMT()} s karty {c.CARD()}. {c.M()}, {c.C()}. {c.D()}. "
+        f"{_bal_tr(c).title()}: {c.BAL()}{c.noise()}")),
+    # ---- held out: new layouts of seen label words (never trained on)
+    Family("en_alert", "en", "debit", lambda c: (
+        f"Debit alert: {c.AMT()} spent on card {c.CARD()} at {c.M()}, {c.C()} on {c.D()}. "
+        f"{_bal_en(c)}: {c.BAL()}"), heldout=True, cases=("upper", "title")),
+    Family("en_amount_first", "en", "debit", lambda c: (
+        f"{c.AMT()} debited from card {c.CARD()} at {c.M()}, {c.C()}, {c.A()} on {c.D()}. "
+        f"{_bal_en(c)} {c.BAL()}.{c.noise()}"), heldout=True),
+    Family("en_reverse_pipe", "en", "debit", lambda c: (
+        f"{_bal_en(c)} {c.BAL()} | {c.D()} | -{c.AMT()} | {c.M()}, {c.C()} | {c.CARD()}"), heldout=True,
+        cards=("star1", "stars2", "stars3", "stars4")),
+    Family("ru_karta_first", "ru", "debit", lambda c: (
+        f"Карта {c.CARD()} {c.D()} покупка на сумму {c.AMT()} в {c.M()}, {c.C()}, {c.A()}. "
+        f"{_bal_ru(c)} {c.BAL()}"), heldout=True),
+    Family("ru_ml_addr", "ru", "debit", lambda c: (
+        f"Карта {c.CARD()}\nПокупка {c.AMT()}\n{c.M()}\n{c.A()}\n{c.C()}\n{_bal_ru(c)} {c.BAL()}\n{c.D()}"),
+        heldout=True),
+    Family("tr_oplata", "tr", "debit", lambda c: (
+        f"Oplata {c.AMT()} {c.M()}, {c.C()}; karta {c.CARD()}; {c.D()}; {_bal_tr(c)} {c.BAL()}"), heldout=True),
+)
+# ---------------------------------------------------------------- procedural layouts
+# Training-only families whose layout is drawn per message: the five segments (amount,
+# card, place = merchant / city / address, date, balance) in a random order, an optional
+# header word, random separators or one segment per line, each segment labelled or not
+# (label words from the language's pools), place rendered in one of several shapes,
+# optional address / balance.  They teach field SEMANTICS rather than template
+# positions.  The (language, segment order, multi-line) signatures of the held-out
+# families are excluded (_HELDOUT_SIGNATURES, pinned by tests/test_families.py), and
+# the held-out families' own phrasings ("Debit alert", "spent on card", "debited from",
+# "покупка на сумму") are not in the pools: a held-out layout stays unseen.
+_PROC_POOLS = {
+    "en": dict(
+        head_debit=("Purchase", "PURCHASE", "POS", "Payment", "Card payment", "DEBIT", "Debit", "Charge", "POS PURCHASE"),
+        head_credit=("Refund", "Credit", "Reversal", "Incoming transfer", "REFUND"),
+        amt=("Amount", "Amt", "Sum", "Total", "AMOUNT"), card=("card", "Card", "CARD", "Card no"),
+        merch=("Merchant", "Shop", "Payee", "MERCHANT"), city=("City", "Location", "CITY"),
+        addr=("Address", "Addr"), date=("Date", "Time", "DATE"),
+        bal=("Balance", "Bal", "Avail. balance", "Available", "Avl bal", "Remaining balance", "BALANCE", "Bal."),
+        at=("at", "AT"), on=("on",), inn=("in",)),
+    "ru": dict(
+        head_debit=("Покупка", "Оплата", "Списание", "ПОКУПКА", "Оплата товаров"),
+        head_credit=("Зачисление", "Возврат", "Пополнение"),
+        amt=("Сумма", "Списано", "Сумма операции"), card=("Карта", "карта", "по карте", "КАРТА"),
+        merch=("Магазин", "Место", "Получатель"), city=("Город",), addr=("Адрес",), date=("Дата", "Время"),
+        bal=("Остаток", "Баланс", "Доступно", "Доступный остаток"),
+        at=("в",), on=("",), inn=("г.",)),
+    "tr": dict(
+        head_debit=("Pokupka", "Oplata", "Spisanie", "POKUPKA"),
+        head_credit=("Zachislenie", "Vozvrat", "Popolnenie"),
+        amt=("Summa", "Spisano"), card=("karta", "Karta", "po karte", "s karty"),
+        merch=("Mesto", "Magazin", "Poluchatel"), city=("Gorod",), addr=("Adres",), date=("Data", "Vremya"),
+        bal=("ostatok", "Ostatok", "dostupno", "Dostupno", "balans", "Balans"),
+        at=("v",), on=("",), inn=("g.",)),
+}
+_SEGMENTS = ("AMT", "CARD", "PLACE", "DATE", "BAL")
+# (language, segment order, one segment per line) of every held-out family: never drawn
+_HELDOUT_SIGNATURES = frozenset({
+    ("en", ("AMT", "CARD", "PLACE", "DATE", "BAL"), False),  # en_alert, en_amount_first
+    ("en", ("BAL", "DATE", "AMT", "PLACE", "CARD"), False),  # en_reverse_pipe
+    ("ru", ("CARD", "DATE", "AMT", "PLACE", "BAL"), False),  # ru_karta_first
+    ("ru", ("CARD", "AMT", "PLACE", "BAL", "DATE"), True),  # ru_ml_addr
+    ("tr", ("AMT", "PLACE", "CARD", "DATE", "BAL"), False),  # tr_oplata
+})
+
+
+def _proc_layout(r: random.Random, lang: str) -> Tuple[Tuple[str, ...], bool]:
+    while True:
+        order = list(_SEGMENTS)
+        r.shuffle(order)
+        if r.random() < 0.25:
+            order.remove("BAL")
+        multi = r.random() < 0.3
+        if (lang, tuple(order), multi) not in _HELDOUT_SIGNATURES:
+            return tuple(order), multi
+
+
+def _proc_render(c: "_Ctx") -> str:
+    r, lang = c.r, c.fam.lang
+    P = _PROC_POOLS[lang]
+    order, multi = _proc_layout(r, lang)
+    labelled = r.random() < 0.5  # "Label: value" style (else mostly bare values / prepositions)
+    colon = r.choice((": ", ": ", " ", ":"))
+
+    def lab(pool: Sequence[str]) -> str:
+        return r.choice(pool) + colon
+
+    segs: List[str] = []
+    head = ""
+    if r.random() < 0.75:
+        head = r.choice(P["head_credit"] if c.fam.txn == "credit" else P["head_debit"])
+    for seg in order:
+        if seg == "AMT":
+            v = c.AMT()
+            segs.append(lab(P["amt"]) + v if (labelled or r.random() < 0.2) else v)
+        elif seg == "CARD":
+            v = c.CARD()
+            segs.append(lab(P["card"]) + v if (labelled or r.random() < 0.7) else v)
+        elif seg == "DATE":
+            v = c.D()
+            if labelled and r.random() < 0.7:
+                segs.append(lab(P["date"]) + v)
+            elif lang == "en" and r.random() < 0.3:
+                segs.append("on " + v)
+            else:
+                segs.append(v)
+        elif seg == "BAL":
+            v = c.BAL()
+            segs.append(lab(P["bal"]) + v)
+        else:  # PLACE
+            m = c.M()
+            city = c.C() if r.random() < 0.85 else ""
+            addr = c.A() if r.random() < 0.35 else ""
+            if labelled and r.random() < 0.6:
+                parts = [lab(P["merch"]) + m] + ([lab(P["city"]) + city] if city else []) + \
+                    ([lab(P["addr"]) + addr] if addr else [])
+                segs.extend(parts) if multi else segs.append(", ".join(parts))
+                continue
+            shape = r.choice(("comma", "comma", "paren", "slash", "in", "lines"))
+            if not city:
+                place = m + (", " + addr if addr else "")
+            elif shape == "paren":
+                place = f"{m} ({city})" + (f", {addr}" if addr else "")
+            elif shape == "slash":
+                place = f"{m}/{city}" + (f", {addr}" if addr else "")
+            elif shape == "in":
+                place = f"{m} {r.choice(P['inn'])} {city}" + (f", {addr}" if addr else "")
+            elif shape == "lines" and multi:
+                segs.extend([m, city] + ([addr] if addr else []))
+                continue
+            else:
+                place = f"{m}, {city}" + (f", {addr}" if addr else "")
+            if r.random() < 0.3:
+                place = r.choice(P["at"]) + " " + place
+            segs.append(place)
+    if multi:
+        body = "\n".join(([head] if head else []) + segs)
+    else:
+        sep = r.choice((", ", "; ", " | ", ". ", " ", " / "))
+        body = (head + r.choice((": ", " ", ". ")) if head else "") + sep.join(segs)
+    return body + (c.noise() if not multi else "")
+
+
+FAMILIES = FAMILIES + (
+    Family("proc_en", "en", "debit", _proc_render, cases=("upper", "upper", "title")),
+    Family("proc_en_credit", "en", "credit", _proc_render, cases=("upper", "title")),
+    Family("proc_ru", "ru", "debit", _proc_render),
+    Family("proc_ru_credit", "ru", "credit", _proc_render),
+    Family("proc_tr", "tr", "debit", _proc_render),
+)
+_BY_NAME = {f.name: f for f in FAMILIES}
+# the reference's real-world formats are families too (training; up-weighted: they carry
+# the golden CASES)
+LEGACY_FAMILIES = ("legacy_purchase", "legacy_account", "legacy_credit")
+TRAIN_FAMILIES: Tuple[str, ...] = LEGACY_FAMILIES + tuple(f.name for f in FAMILIES if not f.heldout)
+HELDOUT_FAMILIES: Tuple[str, ...] = tuple(f.name for f in FAMILIES if f.heldout)
+_LEGACY_WEIGHT = 3
+_PROC_WEIGHT = 3  # procedural layouts: the training data's diversity
+
+
+def family_names(which: Union[str, Sequence[str]]) -> Tuple[str, ...]:
+    if isinstance(which, str):
+        if which == "train":
+            return TRAIN_FAMILIES
+        if which == "heldout":
+            return HELDOUT_FAMILIES
+        if which == "all":
+            return TRAIN_FAMILIES + HELDOUT_FAMILIES
+        return (which,)
+    return tuple(which)
+
+
+def _family_one(r: random.Random, v: Vocab, name: str) -> SynthSMS:
+    ts = r.randint(1_690_000_000, 1_750_000_000)
+    if name in LEGACY_FAMILIES:
+        cur, card = r.choice(_CURRENCIES), f"{r.randint(0, 9999):04d}"
+        if name == "legacy_credit":  # the kind the worker's keyword filter lets through to the LLM
+            return _legacy_credit(r, ts, cur, card, kinds=("TRANSFER IN",))
+        return (_legacy_purchase if name == "legacy_purchase" else _legacy_account)(r, v, ts, cur, card)
+    fam = _BY_NAME[name]
+    c = _Ctx(r, v, fam, ts)
+    body = fam.render(c)
+    exp = dict(c.exp)
+    return SynthSMS(body, "purchase" if fam.txn == "debit" else "credit", dict(c.ans), ts, name, exp)
+
+
+# traffic mixes (bench.py --traffic): "mixed" = every legacy kind in its natural share (17 %
+# are skipped by the parser's keyword filter and never reach the LLM); "purchase" = the two
+# legacy debit formats only (the BASELINE harness timed purchase bodies only); "formats" =
+# every template family (train and held-out layouts, all LLM-routed); "heldout_formats" =
+# the held-out families only
+TRAFFIC: Dict[str, Dict[str, Any]] = {
+    "mixed": {},
+    "purchase": {"kinds": ("purchase", "account")},
+    "formats": {"families": "all"},
+    "heldout_formats": {"families": "heldout"},
+}
+TRAFFIC_KINDS = {k: v.get("kinds") for k, v in TRAFFIC.items() if "families" not in v}
 
 
 def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "train",
-             kinds: Optional[Sequence[str]] = None) -> List[SynthSMS]:
+             kinds: Optional[Sequence[str]] = None,
+             families: Union[None, str, Sequence[str]] = None) -> List[SynthSMS]:
     """``n`` messages; with ``unique`` every body is distinct (defeats the response cache).
     ``vocab_name``: ``"train"`` (what the extractor is trained on) or ``"heldout"`` —
     merchant / city / street names disjoint from the training pools (held-out scoring
-    and the benchmark's traffic).  ``kinds``: keep only these message kinds."""
+    and the benchmark's traffic).  ``kinds``: keep only these message kinds.
+    ``families``: None = the legacy mix; else draw each message from these template
+    families (``"train"``, ``"heldout"``, ``"all"`` or names), uniformly by family with
+    the legacy formats and the procedural layouts weighted x3 in ``"train"`` / ``"all"``."""
     r = random.Random(seed)
     v = vocab(vocab_name)
+    names: Tuple[str, ...] = ()
+    weights: List[int] = []
+    if families is not None:
+        names = family_names(families)
+        weights = [(_LEGACY_WEIGHT if f in LEGACY_FAMILIES else _PROC_WEIGHT if f.startswith("proc_") else 1)
+                   if len(names) > 3 else 1 for f in names]
     out: List[SynthSMS] = []
     seen = set()
     while len(out) < n:
-        s = _one(r, v)
+        s = _one(r, v) if not names else _family_one(r, v, r.choices(names, weights)[0])
         if kinds is not None and s.kind not in kinds:
             continue
         if unique:
@@ -235,6 +790,11 @@ def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "trai
             seen.add(s.body)
         out.append(s)
     return out
+
+
+def generate_traffic(n: int, seed: int = 0, vocab_name: str = "heldout", traffic: str = "mixed") -> List[SynthSMS]:
+    """Bench / evaluation traffic by preset name (:data:`TRAFFIC`)."""
+    return generate(n, seed=seed, vocab_name=vocab_name, **TRAFFIC[traffic])
 
 
 def generate_bodies(n: int, seed: int = 0, vocab_name: str = "train") -> List[str]:
@@ -254,10 +814,14 @@ def reference_cases() -> List[str]:
 
 def iter_corpus(n: int, seed: int = 0) -> Iterator[str]:
     """Tokenizer-training text: bodies, normalised bodies and answer values
-    (``"tokenizer"`` vocabulary: real training-split words only)."""
+    (``"tokenizer"`` vocabulary: real training-split words only; the legacy mix and
+    the TRAINING template families — held-out layouts contribute no merges)."""
     from ..parse.text import normalize_body
 
-    for s in generate(n, seed, unique=False, vocab_name="tokenizer"):
+    half = n // 2
+    items = generate(half, seed, unique=False, vocab_name="tokenizer") + \
+        generate(n - half, seed + 1, unique=False, vocab_name="tokenizer", families="train")
+    for s in items:
         yield s.body
         yield normalize_body(s.body)
         if s.answer:

@@ -33,10 +33,15 @@ class FakePocketBase:
         plan = []  # validate everything first (all-or-nothing), then apply
         seen_msg = {}
         for r in reqs:
-            col = re.match(r"/api/collections/([^/]+)/records", r["url"]).group(1)
+            um = re.match(r"/api/collections/([^/]+)/records(?:/([^/]+))?$", r["url"])
+            col = um.group(1)
             items = self.cols.setdefault(col, [])
             idx = self._index(col)
             body = dict(r["body"])
+            if r["method"] == "PATCH":
+                if um.group(2) not in idx["id"]:
+                    return httpx.Response(404, json={"message": "not found"})
+                body["id"] = um.group(2)
             hit = idx["id"].get(body["id"])
             if hit is None and self.unique_msg_id:
                 owner = idx["msg"].get(body.get("msg_id"), seen_msg.get((col, body.get("msg_id"))))
@@ -90,11 +95,11 @@ class FakePocketBase:
             q = {k: v[0] for k, v in parse_qs(req.url.query.decode()).items()}
             flt = q.get("filter", "")
             sel = items
-            fm = re.match(r"msg_id='(.*)'", flt)
-            if fm:
-                idx = self._index(col)
-                rid_ = idx["msg"].get(fm.group(1))
-                sel = [idx["id"][rid_]] if rid_ is not None else []
+            if flt.startswith("msg_id="):
+                wanted = set(re.findall(r"msg_id='((?:[^'\\]|\\.)*)'", flt))
+                # every record holding one of the msg_ids (duplicates included: the
+                # reference schema's msg_id index is not unique)
+                sel = [r for r in items if r.get("msg_id") in wanted]
             fm = re.match(r"datetime > '(.*)'", flt)
             if fm:
                 sel = [r for r in items if str(r.get("datetime", "")) > fm.group(1)]
@@ -106,9 +111,14 @@ class FakePocketBase:
                                              "totalItems": len(sel), "items": sel[(page - 1) * per: page * per]})
         if req.method == "POST":
             rec = json.loads(req.content)
-            self._n += 1
-            rec["id"] = f"r{self._n}"
             idx = self._index(col)
+            if "id" not in rec:  # PocketBase picks a random id when the client sends none
+                self._n += 1
+                rec["id"] = f"r{self._n}"
+            elif rec["id"] in idx["id"]:
+                return httpx.Response(400, json={"message": "id: value must be unique"})
+            if self.unique_msg_id and rec.get("msg_id") in idx["msg"]:
+                return httpx.Response(400, json={"message": "msg_id: value must be unique"})
             items.append(rec)
             idx["id"][rec["id"]] = rec
             idx["msg"][rec.get("msg_id")] = rec["id"]

@@ -79,3 +79,72 @@ def test_pinned_layout_and_partitioned_subject(arun):
     assert info_mid.num_ack_pending == 4 and info_mid.num_pending == 6
     assert info.num_ack_pending == 0 and info.num_pending == 0 and empty == []
     assert per == [5, 5, 1, 1]  # raw dealt over both partitions; parsed pinned; failed on the default
+
+
+def test_partitioned_fetch_survives_a_dead_partition(arun):
+    """one failing raw partition must not drop the messages already pulled
+    from the healthy ones nor stall them; it is skipped with a backoff, and fetch only
+    raises when every partition fails."""
+    import pytest
+
+    from smsgate_amd.bus import BusUnavailable
+
+    parts = [MemoryBus() for _ in range(3)]
+    pins = {SUBJECT_RAW: [0, 1, 2]}
+    bus = ShardedBus(parts + [MemoryBus()], pins, [3])
+
+    async def go():
+        await bus.ensure_stream()
+        await bus.publish_many([(SUBJECT_RAW, f'"r{i}"'.encode()) for i in range(30)])
+        sub = await bus.subscribe(SUBJECT_RAW, "parser_worker")
+        async def down(*a, **k):
+            raise BusUnavailable("broker down")
+
+        sub.subs[1].fetch = down  # one broker of the partitioned subject goes away
+        got = []
+        for _ in range(10):
+            batch = await sub.fetch(8, 0.05)
+            for m in batch:
+                await m.ack()
+            got += [m.data for m in batch]
+        errors = sub.partition_errors
+        sub.subs[0].fetch = sub.subs[2].fetch = down
+        with pytest.raises(BusUnavailable):
+            for _ in range(100):  # outstanding long-polls (<= LONG_POLL s) finish first
+                await sub.fetch(8, 0.05)
+        return got, errors
+
+    got, errors = arun(go())
+    assert len(got) == 20 and len(set(got)) == 20  # the two healthy partitions' 10 + 10 messages
+    assert errors >= 1
+
+
+def test_partitioned_fetch_low_load_latency(arun):
+    """A message published to any partition while a consumer long-polls is delivered
+    at once (all partitions are polled together), not after (n-1) polling slices."""
+    import asyncio
+    import time
+
+    parts = [MemoryBus() for _ in range(6)]
+    bus = ShardedBus(parts + [MemoryBus()], {SUBJECT_RAW: list(range(6))}, [6])
+
+    async def go():
+        await bus.ensure_stream()
+        sub = await bus.subscribe(SUBJECT_RAW, "parser_worker")
+        lat = []
+        for k in range(6):
+            async def pub():
+                await asyncio.sleep(0.05)
+                await parts[k].publish(SUBJECT_RAW, b'"x"')
+                return time.monotonic()
+
+            t = asyncio.ensure_future(pub())
+            msgs = await sub.fetch(4, 2.0)
+            lat.append(time.monotonic() - await t)
+            for m in msgs:
+                await m.ack()
+        await sub.unsubscribe()
+        return lat
+
+    lat = arun(go())
+    assert max(lat) < 0.03, lat

@@ -1,0 +1,147 @@
+"""Template families of the synthetic SMS generator.
+
+The local extractor replaces a format-agnostic Gemini prompt
+(/root/reference/libs/gemini_parser.py:37-61), so it is scored on SMS layouts it
+never saw in training.  These CPU tests pin the ground the GPU evaluation stands on:
+
+* the split is by family (>= 20 training families, held-out families disjoint);
+* every family's gold answer, run through the real post-processing chain, gives the
+  generator's ``expected`` values (so a correct extraction scores 1.0);
+* every gold answer is reachable by the copy-constrained schema decoder and fits the
+  per-field token caps (so a perfect model is not blocked by the FSM);
+* the rule-based regex backend fails the held-out families (<= 0.3 exact): the set
+  measures something a fixed-template parser cannot do.
+"""
+from __future__ import annotations
+
+from collections import Counter
+
+import pytest
+
+from smsgate_amd.models.domain import RawSMS
+from smsgate_amd.models.evaluate import score_answers
+from smsgate_amd.models.tokenizer import load_tokenizer
+from smsgate_amd.models.train import answer_tokens
+from smsgate_amd.parse.backends.regex import UNKNOWN_ANSWER, extract_rule_based
+from smsgate_amd.parse.canonical import CURRENCY_ALIASES
+from smsgate_amd.parse.pipeline import Outcome, postprocess_answer
+from smsgate_amd.parse.text import normalize_body, worker_should_skip
+from smsgate_amd.serving.fsm import DEFAULT_FIELDS, build_fsm
+from smsgate_amd.utils import synth
+from smsgate_amd.utils.synth import FAMILIES, HELDOUT_FAMILIES, TRAIN_FAMILIES, generate
+
+
+@pytest.fixture(scope="module")
+def tk_fsm():
+    tk = load_tokenizer()
+    return tk, build_fsm(tk, (tk.vocab_size + 63) // 64 * 64)
+
+
+def test_split_is_by_family():
+    assert len(TRAIN_FAMILIES) >= 20 and len(HELDOUT_FAMILIES) >= 5
+    assert not set(TRAIN_FAMILIES) & set(HELDOUT_FAMILIES)
+    assert {"legacy_purchase", "legacy_account"} <= set(TRAIN_FAMILIES)
+    tr = {s.family for s in generate(3000, seed=3, families="train")}
+    ho = {s.family for s in generate(1000, seed=3, families="heldout")}
+    assert tr == set(TRAIN_FAMILIES) and ho == set(HELDOUT_FAMILIES)
+    # the three languages and both transaction types occur
+    assert {f.lang for f in FAMILIES} == {"en", "ru", "tr"} and {f.txn for f in FAMILIES} == {"debit", "credit"}
+
+
+def test_generator_symbols_agree_with_parse_aliases():
+    for code, sym in synth._SYMBOL.items():
+        assert CURRENCY_ALIASES[sym] == code
+    for code, word in synth._WORD.items():
+        assert CURRENCY_ALIASES[word.rstrip(".").upper()] == code
+
+
+def _got(p):
+    return dict(txn_type=p.txn_type.value, date=p.date, amount=p.amount, currency=p.currency, card=p.card,
+                merchant=p.merchant, city=p.city, address=p.address, balance=p.balance)
+
+
+@pytest.mark.parametrize("which", ["train", "heldout"])
+def test_gold_answers_postprocess_to_expected(which):
+    bad = Counter()
+    for s in generate(3000, seed=17, vocab_name="heldout", families=which):
+        raw = RawSMS(msg_id="e", device_id="d", sender="B", date=str(s.timestamp), body=s.body, source="device")
+        r = postprocess_answer(raw, normalize_body(s.body), s.answer)
+        assert r.outcome is Outcome.PARSED, (s.family, s.body, r.error)
+        got = _got(r.parsed)
+        for k, v in s.expected.items():
+            bad[(s.family, k)] += got[k] != v
+    assert not +bad, +bad
+
+
+@pytest.mark.parametrize("which", ["train", "heldout"])
+def test_score_of_gold_answers_is_one(which):
+    items = generate(400, seed=23, vocab_name="heldout", families=which)
+    res = score_answers(items, [s.answer for s in items])
+    assert res["exact"] == 1.0 and res["parse_rate"] == 1.0, res
+
+
+def _walk_ok(fsm, ids, body):
+    s, prev = fsm.start_state, body[-1]
+    for t in ids:
+        if not fsm.copy_mask_host(s, prev, body)[t]:
+            return False
+        s, prev = fsm.step_host(s, t), t
+    return s == fsm.done_state
+
+
+@pytest.mark.parametrize("which", ["train", "heldout"])
+def test_gold_answers_reachable_by_copy_fsm(tk_fsm, which):
+    tk, fsm = tk_fsm
+    bad = Counter()
+    longest = Counter()
+    for s in generate(1500, seed=29, vocab_name="heldout", families=which):
+        b = normalize_body(s.body)
+        enc = tk.encode_offsets([b])[0]
+        ids = answer_tokens(tk, fsm, s.answer, b, enc)
+        if ids is None or not _walk_ok(fsm, ids, tk.message_ids([b], 128)[0]):
+            bad[s.family] += 1
+            continue
+        for f, vals in zip(DEFAULT_FIELDS, fsm.split_fields(ids)):
+            longest[f.name] = max(longest[f.name], len(vals))
+    assert not bad, bad
+    for f in DEFAULT_FIELDS:  # at most ~3/4 of a cap is used: headroom for longer real values
+        assert longest[f.name] <= max(2, int(0.75 * f.cap) + 1), (f.name, longest[f.name], f.cap)
+
+
+def test_bodies_fit_the_prompt_budget(tk_fsm):
+    tk, _ = tk_fsm
+    items = generate(3000, seed=31, vocab_name="heldout", families="all")
+    lens = [len(e) for e in tk.encode_batch([normalize_body(s.body) for s in items])]
+    assert max(lens) <= 110 and sum(lens) / len(lens) < 50  # max_body_tokens is 128
+
+
+def test_transactions_pass_the_word_keyword_filter():
+    items = generate(5000, seed=37, vocab_name="heldout", families="all")
+    assert sum(worker_should_skip(s.body) for s in items) == 0
+
+
+def test_regex_backend_fails_heldout_families():
+    """The held-out set only counts if a fixed-template parser cannot do it."""
+    ho = generate(600, seed=41, vocab_name="heldout", families="heldout")
+    legacy = generate(300, seed=41, vocab_name="heldout", families=["legacy_purchase", "legacy_account"])
+
+    def regex_exact(items):
+        return score_answers(items, [extract_rule_based(s.body) or dict(UNKNOWN_ANSWER) for s in items])["exact"]
+
+    assert regex_exact(ho) <= 0.3
+    assert regex_exact(legacy) == 1.0
+
+
+def test_procedural_layouts_never_draw_a_heldout_signature():
+    import random
+
+    r = random.Random(5)
+    seen = set()
+    for lang in ("en", "ru", "tr"):
+        for _ in range(20000):
+            order, multi = synth._proc_layout(r, lang)
+            assert (lang, order, multi) not in synth._HELDOUT_SIGNATURES
+            seen.add((lang, order, multi))
+    assert len(seen) > 500  # and they are diverse
+    # each held-out family's own layout is one of the excluded signatures
+    assert len(synth._HELDOUT_SIGNATURES) == 5 and {s[0] for s in synth._HELDOUT_SIGNATURES} == {"en", "ru", "tr"}

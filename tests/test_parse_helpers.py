@@ -106,6 +106,50 @@ def test_skip_filters():
     assert not llm_should_skip("your otp: 1")  # the parser's filter is case-sensitive
 
 
+def test_keyword_match_word_vs_substring_decision():
+    """Parity-vs-fix: the reference matches substrings, so a
+    purchase at a merchant whose name merely contains OTP is dropped unparsed.  Default
+    "word": keywords must stand as words; "substring" is the reference, exactly."""
+    from smsgate_amd.parse.text import keyword_match, set_keyword_match
+
+    purchase = "APPROVED PURCHASE DB SALE: RIROTPIOR, YEREVAN,06.05.25 14:23,card ***0018. Amount:5.00 USD"
+    assert keyword_match() == "word"
+    try:
+        assert not worker_should_skip(purchase) and not llm_should_skip(purchase)
+        assert worker_should_skip("Your OTP: 123456") and worker_should_skip("OTP-code 1234")
+        assert worker_should_skip("CODE: 1234") and worker_should_skip("pass=1")
+        assert not worker_should_skip("BARCODE:123 PURCHASE")  # 'CODE:' inside a word
+        # known limit in both modes: a merchant literally named OTP BANK is skipped
+        assert worker_should_skip("PURCHASE: OTP BANK, YEREVAN")
+        set_keyword_match("substring")  # reference parity (worker.py:112-121)
+        assert worker_should_skip(purchase) and llm_should_skip(purchase)
+        assert worker_should_skip("BARCODE:123 PURCHASE")
+        with pytest.raises(ValueError):
+            set_keyword_match("fuzzy")
+    finally:
+        set_keyword_match("word")
+
+
+def test_answer_canonicalisation():
+    """Copied currency symbols map to ISO codes; day-first slash dates become ISO so
+    dateutil does not swap day and month (parse/canonical.py)."""
+    from smsgate_amd.parse import postprocess_answer
+    from smsgate_amd.parse.canonical import canonical_currency, canonical_date_text
+
+    assert [canonical_currency(c) for c in ("$", "€", "֏", "₽", "руб", "руб.", "USD", "£", None)] == \
+        ["USD", "EUR", "AMD", "RUB", "RUB", "RUB", "USD", "GBP", None]
+    assert canonical_date_text("06/05/2025 14:23") == "2025-05-06 14:23"
+    assert canonical_date_text("06-05-25 14:23") == "2025-05-06 14:23"
+    assert canonical_date_text("06.05.25 14:23") == "06.05.25 14:23"  # dotted: the reference chain
+    assert canonical_date_text("2025-05-06 14:23") == "2025-05-06 14:23"
+    assert canonical_date_text("31/13/2025") == "31/13/2025"  # not a day-first date: untouched
+    raw = RawSMS(msg_id="m", sender="s", body="Paid $5.00 on 06/05/2025 14:23", date="1749808562")
+    ans = {"txn_type": "debit", "date": "06/05/2025 14:23", "amount": "5.00", "currency": "$", "card": "*0018",
+           "merchant": "SHOP", "city": "", "address": "", "balance": ""}
+    p = postprocess_answer(raw, raw.body, ans).parsed
+    assert p.currency == "USD" and p.date.isoformat() == "2025-05-06T14:23:00"
+
+
 def test_md5_sha1_ids():
     assert get_md5_hash("APPROVED PURCHASE DB SALE: …") == "ba20eeee04a7b49c06131ff1403e8fa4"
     assert get_sha1_hash("abc") == "a9993e364706816aba3e25717850c26c9cd0d89d"
@@ -192,3 +236,16 @@ def test_golden_case_check_matches_the_reference_assertions():
     assert golden_case_mismatches(good) == []
     bad = [good[0], None, dict(good[2], city="AMERIABANK")]
     assert golden_case_mismatches(bad) == ["case2: not parsed", "case3.city: 'AMERIABANK' != 'AM'"]
+
+
+def test_postprocess_builds_the_same_parsedsms_as_validation():
+    """postprocess_answer's ParsedSMS and its wire JSON equal a re-validated copy."""
+    from smsgate_amd.parse import postprocess_answer
+    from smsgate_amd.parse.text import normalize_body
+    from smsgate_amd.utils.synth import generate
+
+    for s in generate(300, seed=9, vocab_name="heldout", families="all"):
+        raw = RawSMS(msg_id="m", sender="B", body=s.body, date=str(s.timestamp), device_id="d")
+        p = postprocess_answer(raw, normalize_body(s.body), s.answer).parsed
+        v = ParsedSMS.model_validate(p.model_dump())
+        assert p.model_dump_json() == v.model_dump_json() and p == v

@@ -132,6 +132,54 @@ def test_dlq_reparse_failure_is_terminal(arun):
     assert (REGISTRY.get_sample_value("sms_dlq_reparse_failed_total") or 0.0) - m0 == 2
 
 
+def test_dlq_terminal_subject_on_reference_stream_and_rejection(arun):
+    """(1) a stream created by the reference with its five subjects gains
+    sms.failed.final when the DLQ worker starts (ensure_stream updates it), and a
+    twice-failed message lands there; (2) if the broker refuses the terminal subject,
+    the message is logged and acked -- the DLQ consumer never loops on it."""
+    from smsgate_amd.bus import BusError
+    from smsgate_amd.bus.base import StreamConfig
+    from smsgate_amd.services.dlq import DlqWorker
+
+    class AlwaysFails(RegexBackend):
+        async def extract_batch(self, bodies):
+            return [BackendError("still broken")] * len(bodies)
+
+    env = json.dumps({"reason": "unmatched", "raw": _raw("hello there", "m9").model_dump()}).encode()
+    bus = MemoryBus()
+
+    async def go_reference_stream():
+        await bus.ensure_stream(StreamConfig(name="SMS", subjects=[SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_FAILED,
+                                                                   "sms.processing", "sms.categorized"]))
+        await bus.publish(SUBJECT_FAILED, env)
+        w = DlqWorker(bus, ParsePipeline(AlwaysFails()), reparse=True)
+        await w.start()
+        await w.stop()
+        await w.stage.run_until_idle(idle_s=0.3)
+        return w, await drain(bus, SUBJECT_FAILED_FINAL)
+
+    w, final = arun(go_reference_stream())
+    assert w.reparse_failed == 1 and len(final) == 1 and w.final_rejected == 0
+
+    class Refusing(MemoryBus):
+        async def publish_many(self, items):
+            if any(s == SUBJECT_FAILED_FINAL for s, _ in items):
+                raise BusError("no stream captures subject 'sms.failed.final'")
+            return await super().publish_many(items)
+
+    bus2 = Refusing()
+
+    async def go_refused():
+        await bus2.publish(SUBJECT_FAILED, env)
+        w = DlqWorker(bus2, ParsePipeline(AlwaysFails()), reparse=True)
+        await w.stage.run_until_idle(idle_s=0.3)
+        return w, await bus2.consumer_info("SMS", "parser_worker_dlq")
+
+    w, info = arun(go_refused())
+    assert w.final_rejected == 1 and w.stage.dead_lettered == 0 and w.seen == 1
+    assert info.num_pending == 0 and info.num_ack_pending == 0
+
+
 def test_dlq_reparse_profiler_dumps_pstats(arun, tmp_path):
     """Reparse runs inside a profiler session (dlq_worker.py:70-74); with a
     profile dir set, a cProfile dump lands there and names the parse path."""
@@ -435,10 +483,10 @@ def test_pocketbase_upsert_dedup_and_retry(arun):
 
 
 def test_pocketbase_batch_upsert_and_fallbacks(arun):
-    """With the batch API, N records cost ceil(N / 50) requests (PUT on msg_id-derived
-    ids, idempotent); a chunk the server refuses (a msg_id the reference's writer
-    stored under a random id) falls back to GET + PATCH for that chunk; a server
-    without the batch API (403) switches the sink to per-record for good."""
+    """With the batch API, N records cost 2 x ceil(N / 50) requests (one msg_id lookup,
+    one batch: PUT on msg_id-derived ids, PATCH where a msg_id is already stored under
+    another id, e.g. by the reference's writer); a server without the batch API (403)
+    switches the sink to per-record for good."""
     from smsgate_amd.sinks.pocketbase import PocketBaseClient, PocketBaseSink, record_id
 
     recs = [ParsedSMS(**_parsed(f"b{i}")) for i in range(120)]
@@ -462,7 +510,7 @@ def test_pocketbase_batch_upsert_and_fallbacks(arun):
     legacy_fake = FakePocketBase(batch_enabled=True)
     legacy_fake.cols["sms_data"] = [dict(msg_id="b3", id="legacyrandomid0", merchant="OLD")]
     sink = arun(run(legacy_fake, [recs[:5]]))
-    assert sink.per_record == 5 and sink.batch_supported is not False
+    assert sink.batched == 5 and sink.per_record == 0 and sink.batch_supported is True
     assert len(legacy_fake.cols["sms_data"]) == 5  # b3 PATCHed in place, no duplicate
     assert next(r for r in legacy_fake.cols["sms_data"] if r["msg_id"] == "b3")["id"] == "legacyrandomid0"
 
@@ -470,6 +518,43 @@ def test_pocketbase_batch_upsert_and_fallbacks(arun):
     sink = arun(run(off, [recs[:60], recs[60:]]))
     assert sink.batch_supported is False and sink.per_record == 120 and len(off.cols["sms_data"]) == 120
     assert sum(c == "POST /api/batch" for c in off.calls) == 1  # probed once, then per record
+
+
+def test_pocketbase_paths_share_one_record_per_msg_id(arun):
+    """on the reference schema (msg_id NOT unique) the batch path must not
+    create a second record for a msg_id the per-record path (or the reference's
+    writer) stored, and vice versa -- both paths address one record per msg_id."""
+    from smsgate_amd.sinks.pocketbase import PocketBaseClient, PocketBaseSink, record_id
+
+    fake = FakePocketBase(batch_enabled=False, unique_msg_id=False)
+    fake.cols["sms_data"] = [dict(msg_id="ref0", id="referencerand01", merchant="OLD")]
+    recs = [ParsedSMS(**_parsed(f"m{i}")) for i in range(6)]
+    ref0 = ParsedSMS(**_parsed("ref0"))
+
+    async def go():
+        c = PocketBaseClient(base_url="http://pb", transport=fake.transport(), retry_min=0.001, retry_max=0.002)
+        sink = PocketBaseSink(c)
+        await sink.upsert_many(recs[:3])  # batch API off: per-record creates (derived ids)
+        fake.batch_enabled = True
+        sink.batch_supported = None
+        # redelivery of m0..m2 + new m3..m5 + the reference's record, all through the batch path
+        await sink.upsert_many([r.model_copy(update={"merchant": "B"}) for r in recs] + [ref0])
+        fake.batch_enabled = False
+        sink.batch_supported = False
+        await sink.upsert_many([recs[4].model_copy(update={"merchant": "P"})])  # per-record after batch
+        await c.close()
+        return sink
+
+    sink = arun(go())
+    stored = fake.cols["sms_data"]
+    by_msg = {}
+    for r in stored:
+        by_msg.setdefault(r["msg_id"], []).append(r)
+    assert all(len(v) == 1 for v in by_msg.values()), {k: len(v) for k, v in by_msg.items()}
+    assert len(stored) == 7 and sink.batched == 7
+    assert by_msg["ref0"][0]["id"] == "referencerand01" and by_msg["ref0"][0]["merchant"] == "TEST LLC"
+    assert all(by_msg[f"m{i}"][0]["id"] == record_id(f"m{i}") for i in range(6))
+    assert by_msg["m4"][0]["merchant"] == "P" and by_msg["m0"][0]["merchant"] == "B"
 
 
 # --------------------------------------------------------------------------- CLI

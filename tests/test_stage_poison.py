@@ -329,3 +329,46 @@ def test_dlq_reparse_through_engine_server(arun, tmp_path):
     assert down[0] >= 1 and down[1] == 0 and down[2] == 0
     assert [p["msg_id"] for p in parsed] == [raw.msg_id] and w.reparsed == 1
     assert info.num_pending == 0 and info.num_ack_pending == 0
+
+
+def test_publish_rejection_is_isolated_and_dead_lettered(arun):
+    """a broker rejection of ONE request (publish over the maximum payload)
+    is a plain BusError -- the message's fault: it takes the isolate / dead-letter path
+    (the good messages of its batch are acked, the envelope is truncated to fit), while a
+    BusUnavailable (connection gone) naks the batch whole."""
+    from smsgate_amd.bus import BusError, BusUnavailable
+    from smsgate_amd.runtime.stage import DLQ_ENTRY_MAX
+
+    class Limited(MemoryBus):
+        MAX = 100_000
+
+        async def publish(self, subject, data, headers=None):
+            if len(data) > self.MAX:
+                raise BusError("maximum payload exceeded")
+            return await super().publish(subject, data, headers)
+
+    bus = Limited()
+    big = b'"' + b"x" * 149_998 + b'"'
+
+    async def handler(msgs):
+        for m in msgs:
+            await bus.publish(SUBJECT_PARSED, m.data)  # the output is the size of the input
+            await m.ack()
+
+    async def go():
+        await bus.publish_many([(SUBJECT_RAW, b'"ok1"'), (SUBJECT_RAW, b'"ok2"')])
+        await MemoryBus.publish(bus, SUBJECT_RAW, big)  # accepted on the way in
+        await bus.publish(SUBJECT_RAW, b'"ok3"')
+        st = Stage(bus, SUBJECT_RAW, "g", handler, batch=16, nak_delay=0.0, poison_after=2,
+                   dead_letter=dlq_publisher(bus, SUBJECT_FAILED), stats_interval=0)
+        await _pump(st)
+        info = await bus.consumer_info("SMS", "g")
+        return st, info, await drain(bus, SUBJECT_FAILED), await drain(bus, SUBJECT_PARSED)
+
+    st, info, dlq, parsed = arun(go())
+    assert st.dead_lettered == 1 and st.transient_errors == 0
+    assert len(dlq) == 1 and dlq[0]["err"] == "maximum payload exceeded"
+    assert dlq[0]["entry_truncated"] == 150_000 and len(dlq[0]["entry"]) == DLQ_ENTRY_MAX
+    assert sorted(parsed) == ["ok1", "ok2", "ok3"]  # the good messages went through
+    assert info.num_pending == 0 and info.num_ack_pending == 0
+    assert issubclass(BusUnavailable, ConnectionError) and not issubclass(BusError, ConnectionError)

@@ -32,10 +32,11 @@ DEFAULT_VOCAB = 8192
 # was 8 tokens).  ',' before a non-3-digit group stays a separator ("BLVD 89,17.05.24"
 # keeps the street number and the date apart), so every body value stays token-aligned.
 # 8 192 merges: 49.2 -> 41.2 body tokens and 43.8 -> 35.7 answer tokens per purchase SMS.
-# Currency symbols are pre-tokens of their own (never glued to neighbouring
-# punctuation: "-£574.33", "BAL:$52.00"), so a copied currency is token-aligned.
+# Currency symbols and card-mask star runs are pre-tokens of their own (never glued to
+# neighbouring punctuation: "-£574.33", "BAL:$52.00", "CARD:**3736"), so a copied
+# currency or masked card is token-aligned.
 NUMBER_AWARE_SPLIT = (r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\d{1,3}(?:,\d{3})+(?:\.\d+)?| ?\d+(?:[.:]\d+)*"
-                      r"| ?[$€£₽₾֏]| ?[^\s\p{L}\p{N}$€£₽₾֏]+|\s+(?!\S)|\s+")
+                      r"| ?[$€£₽₾֏]| ?\*+| ?[^\s\p{L}\p{N}$€£₽₾֏*]+|\s+(?!\S)|\s+")
 
 
 def train_tokenizer(path: Path = ASSET, vocab_size: int = DEFAULT_VOCAB, n_sms: int = 60000, seed: int = 1234):

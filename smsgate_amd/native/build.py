@@ -18,6 +18,7 @@ from typing import List
 HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 BINDIR = HERE / "_bin"
+LIBDIR = HERE / "_lib"  # in-tree CPython extensions (git-ignored, travel with the tree)
 BUSD = BINDIR / "smsgate-busd"
 # host sanitizer build (ASan + UBSan): the broker's race/memory check, run by
 # tests/test_native_bus.py::test_sanitizer_build_clean (GPU sanitizers are not used)
@@ -34,7 +35,7 @@ def cxx() -> str:
 
 
 def sources() -> List[Path]:
-    return sorted(CSRC.glob("*.cpp")) + sorted(CSRC.glob("*.hpp"))
+    return sorted(p for p in CSRC.glob("*.cpp") if p.name != "tokfast.cpp") + sorted(CSRC.glob("*.hpp"))
 
 
 def needs_build(target: Path = BUSD) -> bool:
@@ -44,7 +45,30 @@ def needs_build(target: Path = BUSD) -> bool:
     return any(s.stat().st_mtime > mt for s in sources() + [Path(__file__)])
 
 
+def build_tokfast(force: bool = False, verbose: bool = False) -> Path:
+    """``_lib/_tokfast*.so``: the CPython extension of ``csrc/tokfast.cpp`` (native
+    BPE encoder / answer decoder of the parser processes, models/fasttok.py)."""
+    import sysconfig
+
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    target = LIBDIR / ("_tokfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    src = CSRC / "tokfast.cpp"
+    if not force and target.exists() and target.stat().st_mtime > max(src.stat().st_mtime,
+                                                                       Path(__file__).stat().st_mtime):
+        return target
+    tmp = target.with_suffix(".tmp")
+    cmd = [cxx(), "-O2", "-std=c++17", "-Wall", "-shared", "-fPIC", "-fvisibility=hidden",
+           f"-I{sysconfig.get_paths()['include']}", str(src), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, target)
+    return target
+
+
 def build(force: bool = False, verbose: bool = False, extra: List[str] = (), sanitize: bool = False) -> Path:
+    if not sanitize:
+        build_tokfast(force=force, verbose=verbose)
     target = BUSD_SAN if sanitize else BUSD
     if not force and not needs_build(target):
         return target

@@ -19,7 +19,8 @@ from typing import Any, List, Sequence, Tuple
 
 import numpy as np
 
-__all__ = ["pack_ids", "unpack_ids", "unpack_id_arrays", "pack_error", "pack_control", "kind"]
+__all__ = ["pack_ids", "pack_raw", "unpack_ids", "unpack_id_arrays", "pack_error", "pack_control", "kind", "req_id",
+           "count", "HEADER_SIZE"]
 
 _HDR = struct.Struct("<cQI")
 
@@ -29,6 +30,22 @@ def pack_ids(tag: bytes, req_id: int, seqs: Sequence[Sequence[int]]) -> bytes:
     lens = np.fromiter(map(len, seqs), dtype=np.uint16, count=n)
     flat = np.array(list(itertools.chain.from_iterable(seqs)), dtype=np.int32)
     return _HDR.pack(tag, req_id, n) + lens.tobytes() + flat.tobytes()
+
+
+HEADER_SIZE = _HDR.size
+
+
+def pack_raw(tag: bytes, req_id: int, n: int, lens: bytes, flat: bytes) -> bytes:
+    """A frame from already-packed uint16 lengths and int32 ids (the native encoder's output)."""
+    return _HDR.pack(tag, req_id, n) + lens + flat
+
+
+def req_id(buf: bytes) -> int:
+    return _HDR.unpack_from(buf, 0)[1]
+
+
+def count(buf: bytes) -> int:
+    return _HDR.unpack_from(buf, 0)[2]
 
 
 def pack_arrays(tag: bytes, req_id: int, lens: np.ndarray, flat: np.ndarray) -> bytes:

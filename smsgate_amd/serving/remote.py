@@ -193,6 +193,11 @@ class RemoteEngineClient:
             raise ValueError("RemoteEngineClient needs a connection or a connector")
         self.connector = connector
         self.tok = tokenizer or load_tokenizer()
+        # native encoder / decoder (native/csrc/tokfast.cpp, id-for-id the library's);
+        # None when the extension is not built -> the library path
+        from ..models.fasttok import load_fast_tokenizer
+
+        self.fast = load_fast_tokenizer() if tokenizer is None else None
         self.fields = [f.name for f in DEFAULT_FIELDS]
         self.max_body = max_body_tokens
         self._ids = itertools.count(1)
@@ -257,12 +262,13 @@ class RemoteEngineClient:
                 return
             k = P.kind(buf)
             if k == b"R":
-                _, rid, seqs = P.unpack_ids(buf)
+                rid = P.req_id(buf)
                 with self._plock:
                     ent = self._pending.pop(rid, None)
                 if ent is not None:
                     fut, loop, _ = ent
-                    loop.call_soon_threadsafe(self._set_res, fut, seqs)
+                    # the raw response: decoded on the event loop (natively when built)
+                    loop.call_soon_threadsafe(self._set_res, fut, buf)
             elif k == b"E":
                 rid, msg = P.unpack_error(buf)
                 with self._plock:
@@ -292,15 +298,37 @@ class RemoteEngineClient:
         fields = self.fields
         return [dict(zip(fields, vals)) for vals in self.tok.decode_fields(seqs, len(fields))]
 
+    def decode_response(self, buf: bytes) -> List[Dict[str, str]]:
+        """Answers of one ``R`` frame (serving/protocol.py)."""
+        fields = self.fields
+        if self.fast is not None:
+            n = P.count(buf)
+            rows = self.fast.decode_fields(buf, P.HEADER_SIZE, n, len(fields))
+        else:
+            rows = self.tok.decode_fields(P.unpack_ids(buf)[2], len(fields))
+        return [dict(zip(fields, vals)) for vals in rows]
+
+    def encode_request(self, rid: int, bodies: Sequence[str]) -> bytes:
+        """The ``Q`` frame of ``bodies``: ``body <ans>`` ids, each body cut to max_body
+        tokens (counted like ExtractorTokenizer.message_ids)."""
+        if self.fast is None:
+            return P.pack_ids(b"Q", rid, self.tok.message_ids(list(bodies), self.max_body))
+        cut, lens, flat = self.fast.encode_packed(bodies, self.max_body, self.tok.ans)
+        if cut:
+            self.tok.truncated += cut
+            from ..obs.metrics import LLM_TRUNCATED
+
+            LLM_TRUNCATED.inc(cut)
+        return P.pack_raw(b"Q", rid, len(bodies), lens, flat)
+
     async def extract(self, bodies: Sequence[str]) -> List[Dict[str, str]]:
-        ids = self.tok.message_ids(list(bodies), self.max_body)
-        conn = self._connection()  # may raise BackendUnavailable: nothing registered yet
         rid = next(self._ids)
+        msg = self.encode_request(rid, bodies)
+        conn = self._connection()  # may raise BackendUnavailable: nothing registered yet
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         with self._plock:
             self._pending[rid] = (fut, loop, conn)
-        msg = P.pack_ids(b"Q", rid, ids)
         sent = False
         try:
             if self.conn is not conn:  # its reader already swept: it will never answer
@@ -318,9 +346,9 @@ class RemoteEngineClient:
                 with self._plock:
                     self._pending.pop(rid, None)
         try:
-            seqs = await (asyncio.wait_for(fut, self.request_timeout) if self.request_timeout else fut)
+            buf = await (asyncio.wait_for(fut, self.request_timeout) if self.request_timeout else fut)
         except asyncio.TimeoutError:
             with self._plock:
                 self._pending.pop(rid, None)
             raise self._unavailable(f"engine server did not answer within {self.request_timeout:.0f} s") from None
-        return self.decode_answers(seqs)
+        return self.decode_response(buf)

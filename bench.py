@@ -162,6 +162,9 @@ def _args(argv=None):
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
     p.add_argument("--cpu-echo-engine", action="store_true",
                    help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")
+    p.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
+                   help="NUMA placement of the rank / parser / broker processes (parallel/placement.py); auto = "
+                        "only when this job holds every GPU of the node")
     p.add_argument("--profile-cpu", default=None, metavar="DIR",
                    help="cProfile the timed region of every parser process and of the rank process into DIR "
                         "(parser-r<rank>-w<k>.pstats, rank<rank>.pstats)")
@@ -196,6 +199,7 @@ def run_replica(args, rank: int, world: int, local: int):
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
     pool = start_training_data(args, local)
+    placement = pin_replica(args, local, procs, broker)  # after the spawns: children keep their own sets
 
     # 2) GPU: device, RCCL group, engine
     import torch
@@ -277,6 +281,12 @@ def run_replica(args, rank: int, world: int, local: int):
         os.makedirs(args.profile_cpu, exist_ok=True)
         rprof.dump_stats(os.path.join(args.profile_cpu, f"rank{rank}.pstats"))
     cpu = {k: v1 - cpu0[k] for k, v1 in _cpu_snapshot(procs, broker).items()}
+    bus_members = None
+    if broker and coord.bus is not None:  # local rank 0: what each node broker carried
+        try:
+            bus_members = coord.bus.member_stats()
+        except Exception as exc:  # noqa: BLE001 - a report, never a failure of the run
+            bus_members = [{"error": str(exc)}]
     coord.shutdown(procs)
     estats = engine.stats.as_dict()
     if hasattr(engine, "spec_stats"):
@@ -308,7 +318,9 @@ def run_replica(args, rank: int, world: int, local: int):
         for b in broker:
             b.stop()
         shutil.rmtree(os.path.dirname(broker[0].listens[0].replace("unix://", "")), ignore_errors=True)
-    return dt, counts, init_s, estats, prov, quality, cpu
+    if placement is not None:
+        cpu["placement"] = placement
+    return dt, counts, init_s, estats, prov, quality, cpu, bus_members
 
 
 def evaluate_quality(engine, args) -> dict:
@@ -354,6 +366,26 @@ def evaluate_quality(engine, args) -> dict:
     return quality
 
 
+def pin_replica(args, local: int, procs, brokers):
+    """NUMA placement (parallel/placement.py): this rank and its parser processes on
+    the cores of its GPU's NUMA node, the node's brokers (local rank 0) on a reserved
+    pair.  ``--pin auto`` pins only when the job holds every GPU of the node (a
+    shared single-GPU box keeps the scheduler's placement).  Returns the plan for
+    the JSON line (None: nothing pinned / no topology)."""
+    if args.pin == "off" or args.cpu_echo_engine:
+        return None
+    from smsgate_amd.parallel.placement import gpu_topology, plan
+
+    node_gpus = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    p = plan(local, node_gpus, broker_cores=2 if brokers else 0)
+    if p is None:
+        return {"pinned": False, "why": "no GPU topology in sysfs"}
+    if args.pin == "auto" and node_gpus != len(gpu_topology()):
+        return {"pinned": False, "why": f"job holds {node_gpus} of {len(gpu_topology())} GPUs (auto)", **p.describe()}
+    p.apply(rank_pid=0, worker_pids=[q.pid for q in procs], broker_pids=[b.pid for b in (brokers or [])])
+    return {"pinned": True, **p.describe()}
+
+
 def _cpu_snapshot(procs, brokers) -> dict:
     """CPU seconds (user + system) consumed so far by the roles of this replica: its
     parser processes, this rank process (engine feeder + coordinator) and the node's
@@ -379,13 +411,15 @@ def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
     """Cores busy per role over the timed region, CPU microseconds per message and the
     cores an 8-GPU node needs at this run's per-GPU rate (weak scaling: per-GPU work is
     fixed, so each role's load scales with the GPU count)."""
+    placement = cpu.pop("placement", None)
     per_gpu = {k: v / dt / world for k, v in cpu.items()}
     total = sum(per_gpu.values())
     return {"cores_busy_per_gpu": {k: round(v, 2) for k, v in per_gpu.items()},
             "cores_busy_per_gpu_total": round(total, 2),
             "cpu_us_per_msg": round(sum(cpu.values()) / max(msgs, 1) * 1e6, 1),
             "node_cores_at_8_gpus": round(8 * total, 1),
-            "visible_cpus": len(os.sched_getaffinity(0))}
+            "visible_cpus": len(os.sched_getaffinity(0)),
+            **({"placement": placement} if placement is not None else {})}
 
 
 def engine_kwargs(args) -> dict:
@@ -600,10 +634,10 @@ def main(argv=None) -> int:
         ops.GEMM_MEASURED[("swiglu", 3072, 576)] = [(4096, 1 << 30, args.swiglu_cfg)]
     rank, world, local = _rank_env()
     if args.backend == "local_llm" or args.cpu_echo_engine:
-        dt, counts, init_s, estats, prov, quality, cpu = run_replica(args, rank, world, local)
+        dt, counts, init_s, estats, prov, quality, cpu, bus_members = run_replica(args, rank, world, local)
     else:
         dt, counts, init_s, estats, prov, quality = asyncio.run(_run_cpu(args))
-        cpu = None
+        cpu = bus_members = None
         world = 1
     total = args.msgs_per_step * args.steps * world
     routed = counts.get("ok", 0) + counts.get("fail", 0) + counts.get("skip", 0)
@@ -674,6 +708,10 @@ def main(argv=None) -> int:
             out["quality_heldout"] = quality
         if cpu is not None:
             out["cpu"] = cpu_budget(cpu, dt, total, world)
+        if bus_members is not None:
+            # messages held per node broker over the whole run (warmup included): every
+            # partition of sms.raw / sms.parsed must carry traffic
+            out["bus_members"] = bus_members
         if args.verbose and estats:
             out["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in estats.items()}
         print(json.dumps(out), flush=True)

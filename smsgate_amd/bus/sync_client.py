@@ -9,7 +9,7 @@ from __future__ import annotations
 import itertools
 import socket
 import struct
-from typing import Any, Dict
+from typing import Any, Dict, List
 from urllib.parse import urlparse
 
 import msgpack
@@ -70,6 +70,13 @@ class SyncBusClient:
     def consumer_info(self, stream: str, durable: str) -> Dict[str, Any]:
         return self.call("consumer_info", stream, durable)
 
+    def stream_info(self, stream: str = "SMS") -> Dict[str, Any]:
+        return self.call("stream_info", stream)
+
+    def member_stats(self, stream: str = "SMS") -> List[Dict[str, Any]]:
+        """One broker: its message count (the sharded view reports every member)."""
+        return [{"subjects": ["*"], "messages": int(self.stream_info(stream).get("messages", 0))}]
+
     def close(self) -> None:
         try:
             self.sock.close()
@@ -113,6 +120,16 @@ class _SyncSharded:
             if k in out:
                 out[k] = sum(f.get(k, 0) for f in found)
         return out
+
+    def member_stats(self, stream: str = "SMS") -> List[Dict[str, Any]]:
+        """Per broker: the subjects pinned to it and the messages its stream holds (the
+        node layout check: every partition of sms.raw carries traffic)."""
+        pinned: Dict[int, List[str]] = {}
+        for subj, idx in self.router.pins.items():
+            for k in idx:
+                pinned.setdefault(k, []).append(subj)
+        return [{"subjects": pinned.get(k, ["*"]), "messages": int(m.stream_info(stream).get("messages", 0))}
+                for k, m in enumerate(self.members)]
 
     def close(self) -> None:
         for m in self.members:

@@ -49,6 +49,64 @@ def _yy(y: int) -> int:
     return y + (1900 if y >= 69 else 2000)
 
 
+# ``dateutil`` costs ~75 us per call, and every layout but the reference's dd.mm.yy
+# HH:MM reaches it.  The shapes below are computed directly, with dateutil's own
+# resolution rules (a dotted d.m.y is read MONTH first when it can be -- the body-date
+# repair fixes the date part afterwards -- 2-digit years via its century window, English
+# month abbreviations); any value the fast path cannot build (an impossible date) falls
+# through to dateutil, so errors are dateutil's own.  tests/test_parse_helpers.py fuzzes
+# every shape against dateutil.
+_FAST_ISO = re.compile(r"(\d{4})-(\d{2})-(\d{2})(?:[ T](\d{2}):(\d{2})(?::(\d{2}))?)?\Z")
+_FAST_DOTTED = re.compile(r"(\d{2})\.(\d{2})\.(\d{4}|\d{2})(?: (\d{2}):(\d{2}))?\Z")
+_FAST_TIME_FIRST = re.compile(r"(\d{2}):(\d{2}) (\d{2})\.(\d{2})\.(\d{4})\Z")
+_FAST_MON = re.compile(r"(\d{1,2})([ -])([A-Za-z]{3})\2(\d{4})(?: (\d{2}):(\d{2}))?\Z")
+_MONTHS = {m: i for i, m in enumerate(("jan", "feb", "mar", "apr", "may", "jun", "jul", "aug", "sep", "oct", "nov",
+                                       "dec"), 1)}
+_DU_INFO = None
+
+
+def _du_year(y: int) -> int:
+    global _DU_INFO
+    if _DU_INFO is None:
+        from dateutil.parser import parserinfo
+
+        _DU_INFO = parserinfo()
+    return _DU_INFO.convertyear(y)
+
+
+def _month_first(a: int, b: int, y: int, hh: int = 0, mm: int = 0) -> datetime:
+    """dateutil's reading of an all-numeric d.m.y: month first unless it cannot be."""
+    if a <= 12:
+        return datetime(y, a, b, hh, mm)
+    return datetime(y, b, a, hh, mm)
+
+
+def _fast_dateutil(text: str):
+    try:
+        m = _FAST_ISO.match(text)
+        if m is not None:
+            y, mo, d, hh, mi, ss = m.groups()
+            return datetime(int(y), int(mo), int(d), int(hh or 0), int(mi or 0), int(ss or 0))
+        m = _FAST_DOTTED.match(text)
+        if m is not None:
+            a, b, y, hh, mi = m.groups()
+            yy = int(y) if len(y) == 4 else _du_year(int(y))
+            return _month_first(int(a), int(b), yy, int(hh or 0), int(mi or 0))
+        m = _FAST_TIME_FIRST.match(text)
+        if m is not None:
+            hh, mi, a, b, y = map(int, m.groups())
+            return _month_first(a, b, y, hh, mi)
+        m = _FAST_MON.match(text)
+        if m is not None:
+            d, _, mon, y, hh, mi = m.groups()
+            mo = _MONTHS.get(mon.lower())
+            if mo is not None:
+                return datetime(int(y), mo, int(d), int(hh or 0), int(mi or 0))
+    except ValueError:
+        return None  # impossible date: dateutil decides (and raises its own error)
+    return None
+
+
 def parse_custom_datetime(text: str) -> datetime:
     if isinstance(text, str):
         m = _FAST_DMY_HM.match(text)
@@ -58,6 +116,10 @@ def parse_custom_datetime(text: str) -> datetime:
                 return datetime(_yy(y), mo, d, hh, mm)
             except ValueError:
                 pass  # impossible date: same fallback path as strptime's failure
+        else:
+            fast = _fast_dateutil(text)  # shapes strptime('%d.%m.%y %H:%M') always rejects
+            if fast is not None:
+                return fast
     try:
         return datetime.strptime(text, "%d.%m.%y %H:%M")
     except Exception:

@@ -65,3 +65,36 @@ def test_stale_broker_socket_is_not_listening(tmp_path):
     assert bench._listening(path)
     srv.close()  # the file stays, nobody accepts
     assert os.path.exists(path) and not bench._listening(path)
+
+
+@pytest.mark.slow
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "smsgate_amd/native/_bin/smsgate-busd")),
+                    reason="native broker not built")
+def test_eight_ranks_full_node_layout():
+    """VERDICT r03 next #4b: 8 ranks (gloo, CPU echo engines) through the production
+    node layout -- sms.raw over 6 brokers, sms.parsed over 2, one for the rest -- with
+    one parser process each: exact routing totals, traffic on every raw and parsed
+    partition, and a drain that accounts for every message across the 6 partitions."""
+    ranks, steps, warm, per = 8, 2, 1, 512
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
+           "--master-addr", "127.0.0.1", "--master-port", "29683", "bench.py", "--gpus", str(ranks),
+           "--cpu-echo-engine", "--steps", str(steps), "--warmup", str(warm), "--msgs-per-step", str(per),
+           "--cpu-workers", "1", "--bus", "busd", "--rank-threads", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    assert r.returncode == 0 and len(lines) == 1, r.stderr[-3000:]
+    out = lines[0]
+    rt = out["routing"]
+    total = ranks * steps * per
+    assert out["n_gpus"] == ranks and rt["parsed"] + rt["keyword_skipped"] + rt["broken"] + rt["dlq"] == total
+    assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"]
+    assert "sms.raw over 6" in out["config"]["bus"] and "sms.parsed over 2" in out["config"]["bus"]
+    members = out["bus_members"]
+    assert len(members) == 9
+    raw = [m for m in members if m["subjects"] == ["sms.raw"]]
+    parsed = [m for m in members if m["subjects"] == ["sms.parsed"]]
+    assert len(raw) == 6 and len(parsed) == 2
+    # every raw message of the run (warmup included) stored on exactly one raw partition
+    assert sum(m["messages"] for m in raw) == ranks * (steps + warm) * per
+    assert all(m["messages"] > 0 for m in raw + parsed)

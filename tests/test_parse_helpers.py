@@ -249,3 +249,36 @@ def test_postprocess_builds_the_same_parsedsms_as_validation():
         p = postprocess_answer(raw, normalize_body(s.body), s.answer).parsed
         v = ParsedSMS.model_validate(p.model_dump())
         assert p.model_dump_json() == v.model_dump_json() and p == v
+
+
+def test_date_fast_paths_equal_dateutil():
+    """parse_custom_datetime computes the common layouts without dateutil (~75 us a
+    call); every shape is fuzzed against dateutil itself, impossible dates included
+    (those fall through to dateutil and raise its error)."""
+    import random
+
+    from dateutil.parser import parse as du
+
+    from smsgate_amd.parse.dates import _fast_dateutil
+
+    r = random.Random(11)
+    mons = ["Jan", "Feb", "Mar", "Apr", "May", "Jun", "Jul", "Aug", "Sep", "Oct", "Nov", "Dec"]
+    fast = 0
+    for _ in range(6000):
+        y, a, b = r.randint(1990, 2030), r.randint(1, 31), r.randint(1, 31)
+        hh, mi, ss = r.randint(0, 23), r.randint(0, 59), r.randint(0, 59)
+        s = r.choice([f"{y}-{a % 13:02d}-{b:02d} {hh:02d}:{mi:02d}", f"{y}-{a % 13:02d}-{b:02d}T{hh:02d}:{mi:02d}:{ss:02d}",
+                      f"{a:02d}.{b:02d}.{y} {hh:02d}:{mi:02d}", f"{a:02d}.{b:02d}.{y % 100:02d}", f"{a:02d}.{b:02d}.{y}",
+                      f"{hh:02d}:{mi:02d} {a:02d}.{b:02d}.{y}", f"{a:02d} {r.choice(mons)} {y} {hh:02d}:{mi:02d}",
+                      f"{a:02d}-{r.choice(mons).upper()}-{y} {hh:02d}:{mi:02d}", f"{y}-{a % 13:02d}-{b:02d}"])
+        try:
+            want = du(s)
+        except Exception:
+            want = None
+        try:
+            got = parse_custom_datetime(s)
+        except Exception:
+            got = None
+        assert got == want, s
+        fast += _fast_dateutil(s) is not None
+    assert fast > 4000

@@ -162,6 +162,18 @@ def _args(argv=None):
     p.add_argument("--spec-max-rows", type=int, default=1 << 30, help="largest bucket that decodes speculatively")
     p.add_argument("--cpu-echo-engine", action="store_true",
                    help="harness check without a GPU: CPU echo engine + gloo (NOT a benchmark number)")
+    # BASELINE config #1 starts at POST /sms/raw: "bus+http" times the pipeline twice --
+    # the parser processes publishing the SMS themselves (value), then loader processes
+    # POSTing them to the node's native /sms/raw doors (http_ingest) -- in one run
+    p.add_argument("--ingest", default="bus+http", choices=["bus", "http", "bus+http"],
+                   help="bus: the parser processes publish each step's SMS to sms.raw; http: --loaders processes "
+                        "POST them to smsgate-busd's native HTTP doors (the reference gateway contract); bus+http: "
+                        "both timed phases, the http one reported under http_ingest")
+    p.add_argument("--loaders", type=int, default=2, help="HTTP loader processes per GPU (--ingest http)")
+    p.add_argument("--http-conns", type=int, default=16, help="keep-alive connections per loader")
+    p.add_argument("--http-batch", type=int, default=1,
+                   help="SMS per request: 1 = POST /sms/raw (the reference's one-SMS requests), N > 1 = "
+                        "POST /sms/raw/batch")
     p.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
                    help="NUMA placement of the rank / parser / broker processes (parallel/placement.py); auto = "
                         "only when this job holds every GPU of the node")
@@ -198,8 +210,17 @@ def run_replica(args, rank: int, world: int, local: int):
            "traffic": args.traffic, "sink": args.sink, "sink_dir": sink_dir}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
     procs, conns = spawn_parser_workers(W, rank, cfg)
+    lprocs, lconns = [], []
+    if args.ingest != "bus":
+        if args.bus != "busd" or not getattr(args, "http_doors", None):
+            raise SystemExit("bench: --ingest http needs the shared native broker (--bus busd) and its HTTP doors")
+        from smsgate_amd.parallel.replica import spawn_loaders
+
+        lcfg = {"http_doors": args.http_doors, "http_batch": args.http_batch, "http_conns": args.http_conns,
+                "vocab": args.traffic_vocab, "traffic": args.traffic}
+        lprocs, lconns = spawn_loaders(max(1, args.loaders), rank, lcfg)
     pool = start_training_data(args, local)
-    placement = pin_replica(args, local, procs, broker)  # after the spawns: children keep their own sets
+    placement = pin_replica(args, local, procs + lprocs, broker)  # after the spawns: children keep their own sets
 
     # 2) GPU: device, RCCL group, engine
     import torch
@@ -249,7 +270,8 @@ def run_replica(args, rank: int, world: int, local: int):
 
         freeze_gc_for_launch_loop()
     # the node's brokers see only this node's ranks (LOCAL_WORLD_SIZE under torchrun)
-    coord = Coordinator(engine, conns, bus_dsn=bus_dsn, node_ranks=int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    coord = Coordinator(engine, conns + lconns, bus_dsn=bus_dsn,
+                        node_ranks=int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     coord.wait_all("ready")
 
     def sync():
@@ -258,39 +280,56 @@ def run_replica(args, rank: int, world: int, local: int):
         if dist is not None:
             dist.barrier()
 
-    per_w = args.msgs_per_step // W
+    L = len(lconns)
 
-    def seeds(first, n):
-        return [[1_000_003 * (rank + 1) + 7919 * w + s for s in range(first, first + n)] for w in range(W)]
+    def seeds(first, n, http=False):
+        """Seed lists per connection (parser workers, then loaders): the messages of a
+        step are published by the parser workers (bus ingest) or POSTed by the loaders."""
+        if not http:
+            ws = [[1_000_003 * (rank + 1) + 7919 * w + s for s in range(first, first + n)] for w in range(W)]
+            return ws + [[] for _ in range(L)]
+        ls = [[2_000_003 * (rank + 1) + 7919 * w + s for s in range(first, first + n)] for w in range(L)]
+        return [[] for _ in range(W)] + ls
 
-    if args.warmup:  # (synchronised too: with a shared broker each rank's drain target needs a common start)
-        coord.run_phase(seeds(0, args.warmup), per_w, sync=sync)
-    (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
-    if hasattr(engine, "spec_stats"):
-        engine.spec_stats(reset=True)
-    cpu0 = _cpu_snapshot(procs, broker)
-    rprof = None
-    if args.profile_cpu:
-        import cProfile
+    if args.msgs_per_step % max(1, L):
+        raise SystemExit("--msgs-per-step must be divisible by --loaders")
+    per = {False: args.msgs_per_step // W, True: args.msgs_per_step // max(1, L)}
+    phases = {"bus": [False], "http": [True], "bus+http": [False, True]}[args.ingest]
+    results = {}
+    for http in phases:
+        if args.warmup:  # (synchronised too: with a shared broker each rank's drain target needs a common start)
+            coord.run_phase(seeds(0 if not http else 10_000, args.warmup if not http else 1, http), per[http],
+                            sync=sync)
+        (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
+        if hasattr(engine, "spec_stats"):
+            engine.spec_stats(reset=True)
+        cpu0 = _cpu_snapshot(procs, broker, lprocs)
+        rprof = None
+        if args.profile_cpu and not http:
+            import cProfile
 
-        rprof = cProfile.Profile()
-        rprof.enable()
-    dt, counts = coord.run_phase(seeds(args.warmup, args.steps), per_w, sync=sync)
-    if rprof is not None:
-        rprof.disable()
-        os.makedirs(args.profile_cpu, exist_ok=True)
-        rprof.dump_stats(os.path.join(args.profile_cpu, f"rank{rank}.pstats"))
-    cpu = {k: v1 - cpu0[k] for k, v1 in _cpu_snapshot(procs, broker).items()}
+            rprof = cProfile.Profile()
+            rprof.enable()
+        first = args.warmup if not http else 10_001
+        dt_p, counts_p = coord.run_phase(seeds(first, args.steps, http), per[http], sync=sync)
+        if rprof is not None:
+            rprof.disable()
+            os.makedirs(args.profile_cpu, exist_ok=True)
+            rprof.dump_stats(os.path.join(args.profile_cpu, f"rank{rank}.pstats"))
+        cpu_p = {k: v1 - cpu0[k] for k, v1 in _cpu_snapshot(procs, broker, lprocs).items()}
+        estats_p = engine.stats.as_dict()
+        if hasattr(engine, "spec_stats"):
+            estats_p.update(engine.spec_stats())
+        results[http] = (dt_p, counts_p, cpu_p, estats_p, dict(coord.last_http))
+    dt, counts, cpu, estats, _ = results[phases[0]]
+    http_res = results.get(True) if phases != [True] else None
     bus_members = None
     if broker and coord.bus is not None:  # local rank 0: what each node broker carried
         try:
             bus_members = coord.bus.member_stats()
         except Exception as exc:  # noqa: BLE001 - a report, never a failure of the run
             bus_members = [{"error": str(exc)}]
-    coord.shutdown(procs)
-    estats = engine.stats.as_dict()
-    if hasattr(engine, "spec_stats"):
-        estats.update(engine.spec_stats())
+    coord.shutdown(procs + lprocs)
     if dist is not None:
         dev = "cpu" if echo else "cuda"
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -306,6 +345,19 @@ def run_replica(args, rank: int, world: int, local: int):
         cs = torch.tensor([cpu[k] for k in ck], dtype=torch.float64, device=dev)
         dist.all_reduce(cs, op=dist.ReduceOp.SUM)
         cpu = dict(zip(ck, (float(x) for x in cs.tolist())))
+        if http_res is not None:  # the second (HTTP-ingest) phase, reduced the same way
+            hdt, hcounts, hcpu, hest, hhttp = http_res
+            t = torch.tensor([hdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            c = torch.tensor([hcounts.get(k, 0) for k in keys] + [hhttp.get(k, 0) for k in HTTP_KEYS],
+                             dtype=torch.int64, device=dev)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            vals = [int(x) for x in c.tolist()]
+            hk = sorted(hcpu)
+            cs = torch.tensor([hcpu[k] for k in hk], dtype=torch.float64, device=dev)
+            dist.all_reduce(cs, op=dist.ReduceOp.SUM)
+            http_res = (float(t.item()), dict(zip(keys, vals[:len(keys)])),
+                        dict(zip(hk, (float(x) for x in cs.tolist()))), hest, dict(zip(HTTP_KEYS, vals[len(keys):])))
         dist.barrier()  # every rank is done with the broker
         dist.destroy_process_group()
     if sink_dir:
@@ -320,7 +372,9 @@ def run_replica(args, rank: int, world: int, local: int):
         shutil.rmtree(os.path.dirname(broker[0].listens[0].replace("unix://", "")), ignore_errors=True)
     if placement is not None:
         cpu["placement"] = placement
-    return dt, counts, init_s, estats, prov, quality, cpu, bus_members
+    if args.ingest == "http":  # the only phase is the HTTP one: report its request counts too
+        prov["http_ingest_requests"] = results[True][4]
+    return dt, counts, init_s, estats, prov, quality, cpu, bus_members, http_res
 
 
 def evaluate_quality(engine, args) -> dict:
@@ -386,7 +440,10 @@ def pin_replica(args, local: int, procs, brokers):
     return {"pinned": True, **p.describe()}
 
 
-def _cpu_snapshot(procs, brokers) -> dict:
+HTTP_KEYS = ("requests", "accepted", "rejected")
+
+
+def _cpu_snapshot(procs, brokers, loaders=()) -> dict:
     """CPU seconds (user + system) consumed so far by the roles of this replica: its
     parser processes, this rank process (engine feeder + coordinator) and the node's
     brokers (local rank 0 owns them).  Differences around the timed region give the
@@ -403,15 +460,22 @@ def _cpu_snapshot(procs, brokers) -> dict:
                 pass
         return tot
 
-    return {"parser_procs": cpu_of(p.pid for p in procs), "rank_proc": cpu_of([os.getpid()]),
-            "brokers": cpu_of(b.pid for b in (brokers or []))}
+    out = {"parser_procs": cpu_of(p.pid for p in procs), "rank_proc": cpu_of([os.getpid()]),
+           "brokers": cpu_of(b.pid for b in (brokers or []))}
+    if loaders:
+        out["loaders"] = cpu_of(p.pid for p in loaders)
+    return out
 
 
 def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
     """Cores busy per role over the timed region, CPU microseconds per message and the
     cores an 8-GPU node needs at this run's per-GPU rate (weak scaling: per-GPU work is
     fixed, so each role's load scales with the GPU count)."""
+    cpu = dict(cpu)
     placement = cpu.pop("placement", None)
+    # the HTTP loaders play the phones / webhook senders: client-side CPU, reported
+    # apart from the node's server-side budget
+    loaders = cpu.pop("loaders", None)
     per_gpu = {k: v / dt / world for k, v in cpu.items()}
     total = sum(per_gpu.values())
     return {"cores_busy_per_gpu": {k: round(v, 2) for k, v in per_gpu.items()},
@@ -419,6 +483,9 @@ def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
             "cpu_us_per_msg": round(sum(cpu.values()) / max(msgs, 1) * 1e6, 1),
             "node_cores_at_8_gpus": round(8 * total, 1),
             "visible_cpus": len(os.sched_getaffinity(0)),
+            **({"client_loaders": {"cores_busy_per_gpu": round(loaders / dt / world, 2),
+                                   "cpu_us_per_msg": round(loaders / max(msgs, 1) * 1e6, 1)}}
+               if loaders is not None and loaders > 0.05 * dt else {}),
             **({"placement": placement} if placement is not None else {})}
 
 
@@ -473,21 +540,37 @@ def start_node_broker(args, local: int):
         dsn = ("sharded+" if n > 1 else "") + ",".join(members)
     else:
         dsn = node_layout(members, parts)
+    # HTTP doors (--ingest http): one per broker holding an sms.raw partition
+    n_raw = (args.partitions or parts.get("sms.raw", 1)) if args.bus_shards <= 0 else 1
+    want_doors = args.ingest != "bus"
+    doors_file = os.path.join(root, "http_doors.json")
     if local == 0:
         from smsgate_amd.native import spawn_busd
 
         os.makedirs(root, exist_ok=True)
+        if os.path.exists(doors_file):
+            os.unlink(doors_file)
         brokers = []
         for k, p in enumerate(socks):
             if os.path.exists(p):
                 os.unlink(p)
-            brokers.append(spawn_busd(f"unix://{p}", os.path.join(root, f"data{k}")))
+            http = "tcp://127.0.0.1:0" if (want_doors and k < n_raw) else None
+            brokers.append(spawn_busd(f"unix://{p}", os.path.join(root, f"data{k}"), http_listen=http))
+        if want_doors:
+            tmp = doors_file + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump([f"127.0.0.1:{b.http_port}" for b in brokers if b.http_port], f)
+            os.replace(tmp, doors_file)
+        args.http_doors = [f"127.0.0.1:{b.http_port}" for b in brokers if b.http_port]
         return brokers, dsn
     t_end = time.time() + 60
-    while not all(_listening(p) for p in socks):
+    while not all(_listening(p) for p in socks) or (want_doors and not os.path.exists(doors_file)):
         if time.time() > t_end:
             raise SystemExit(f"bench: the node broker sockets {socks} never started listening")
         time.sleep(0.05)
+    if want_doors:
+        with open(doors_file) as f:
+            args.http_doors = json.load(f)
     return None, dsn
 
 
@@ -634,10 +717,10 @@ def main(argv=None) -> int:
         ops.GEMM_MEASURED[("swiglu", 3072, 576)] = [(4096, 1 << 30, args.swiglu_cfg)]
     rank, world, local = _rank_env()
     if args.backend == "local_llm" or args.cpu_echo_engine:
-        dt, counts, init_s, estats, prov, quality, cpu, bus_members = run_replica(args, rank, world, local)
+        dt, counts, init_s, estats, prov, quality, cpu, bus_members, http_res = run_replica(args, rank, world, local)
     else:
         dt, counts, init_s, estats, prov, quality = asyncio.run(_run_cpu(args))
-        cpu = bus_members = None
+        cpu = bus_members = http_res = None
         world = 1
     total = args.msgs_per_step * args.steps * world
     routed = counts.get("ok", 0) + counts.get("fail", 0) + counts.get("skip", 0)
@@ -708,6 +791,21 @@ def main(argv=None) -> int:
             out["quality_heldout"] = quality
         if cpu is not None:
             out["cpu"] = cpu_budget(cpu, dt, total, world)
+        if http_res is not None:
+            hdt, hcounts, hcpu, _, hhttp = http_res
+            hrouted = hcounts.get("ok", 0) + hcounts.get("fail", 0) + hcounts.get("skip", 0)
+            if hrouted != total or hhttp["accepted"] != total or hhttp["rejected"]:
+                raise SystemExit(f"bench: HTTP ingest phase routed {hrouted} / accepted {hhttp['accepted']} "
+                                 f"(rejected {hhttp['rejected']}), expected {total}")
+            out["http_ingest"] = {
+                "value": round(total / hdt, 1), "unit": "msgs/s", "ms_per_step": round(hdt / args.steps * 1000, 3),
+                "endpoint": "/sms/raw/batch" if args.http_batch > 1 else "/sms/raw",
+                "sms_per_request": args.http_batch, "requests": hhttp["requests"],
+                "loaders_per_gpu": args.loaders, "conns_per_loader": args.http_conns,
+                "doors": "smsgate-busd --http-listen on every sms.raw broker (native api_gateway contract)",
+                "routing": {"parsed": hcounts.get("parsed", 0), "keyword_skipped": hcounts.get("keyword_skipped", 0),
+                            "broken": hcounts.get("skip", 0), "dlq": hcounts.get("fail", 0)},
+                "cpu": cpu_budget(hcpu, hdt, total, world)}
         if bus_members is not None:
             # messages held per node broker over the whole run (warmup included): every
             # partition of sms.raw / sms.parsed must carry traffic

@@ -201,6 +201,118 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     await worker.stop()
 
 
+# ------------------------------------------------------------- HTTP ingest loaders
+def spawn_loaders(n: int, rank: int, cfg: Dict[str, Any]) -> Tuple[List[Any], List[Connection]]:
+    """Start ``n`` phone-side loader processes (``bench.py --ingest http``): each POSTs
+    its share of the prepared SMS to the node's native ``POST /sms/raw`` doors
+    (smsgate-busd ``--http-listen``, the reference's api_gateway contract,
+    /root/reference/services/api_gateway/main.py:106-134) instead of the parser
+    processes publishing to the bus themselves."""
+    ctx = mp.get_context("spawn")
+    procs, conns = [], []
+    saved = {k: os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    try:
+        os.environ["HIP_VISIBLE_DEVICES"] = ""
+        os.environ["CUDA_VISIBLE_DEVICES"] = ""
+        for w in range(n):
+            a, b = ctx.Pipe(duplex=True)
+            p = ctx.Process(target=loader_main, args=(b, rank, w, cfg), name=f"loader-r{rank}-l{w}", daemon=True)
+            p.start()
+            b.close()
+            procs.append(p)
+            conns.append(a)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return procs, conns
+
+
+def _http_request(path: str, body: bytes) -> bytes:
+    return (f"POST {path} HTTP/1.1\r\nHost: smsgate\r\nContent-Type: application/json\r\n"
+            f"Content-Length: {len(body)}\r\n\r\n").encode() + body
+
+
+async def _post_all(doors: Sequence[str], reqs: Sequence[Tuple[bytes, int]], conns: int) -> Dict[str, int]:
+    """Send every request over ``conns`` keep-alive HTTP/1.1 connections (spread over
+    the doors), one in flight per connection; count 202s and messages accepted."""
+    stats = {"requests": 0, "accepted": 0, "rejected": 0}
+    nxt = [0]
+
+    async def one(k: int) -> None:
+        host, port = doors[k % len(doors)].rsplit(":", 1)
+        r, w = await asyncio.open_connection(host, int(port))
+        try:
+            while nxt[0] < len(reqs):
+                req, n = reqs[nxt[0]]
+                nxt[0] += 1
+                w.write(req)
+                await w.drain()
+                head = await r.readuntil(b"\r\n\r\n")
+                status = int(head.split(b" ", 2)[1])
+                clen = 0
+                for line in head.split(b"\r\n"):
+                    if line[:15].lower() == b"content-length:":
+                        clen = int(line[15:])
+                if clen:
+                    await r.readexactly(clen)
+                stats["requests"] += 1
+                if status == 202:
+                    stats["accepted"] += n
+                else:
+                    stats["rejected"] += n
+        finally:
+            w.close()
+
+    await asyncio.gather(*(one(k) for k in range(max(1, conns))))
+    return stats
+
+
+def loader_main(conn: Connection, rank: int, widx: int, cfg: Dict[str, Any]) -> None:
+    """A loader process: ``prepare`` builds the HTTP requests (untimed, like the bus
+    mode's prepared payloads); ``go`` POSTs them, reports ``published``; ``report``
+    answers ``done`` (loaders route nothing: counts stay with the parsers)."""
+    import json as _json
+
+    from ..serving import protocol as P
+
+    doors = list(cfg["http_doors"])
+    batch = int(cfg.get("http_batch", 1))
+    path = "/sms/raw/batch" if batch > 1 else "/sms/raw"
+    reqs: List[Tuple[bytes, int]] = []
+    stats: Dict[str, int] = {}
+
+    def send(obj: Any) -> None:
+        conn.send_bytes(P.pack_control(obj))
+
+    send({"event": "ready", "w": widx})
+    while True:
+        buf = conn.recv_bytes()
+        cmd = P.unpack_control(buf) if P.kind(buf) == b"C" else None
+        if cmd is None or cmd.get("cmd") == "quit":
+            break
+        if cmd["cmd"] == "prepare":
+            reqs = []
+            for seed in cmd["seeds"]:
+                ps = [p.model_dump() for p in _payload_bytes(int(cmd["n"]), seed, cfg.get("vocab", "heldout"),
+                                                              cfg.get("traffic", "mixed"))]
+                if batch > 1:
+                    reqs += [(_http_request(path, _json.dumps(ps[i:i + batch]).encode()), len(ps[i:i + batch]))
+                             for i in range(0, len(ps), batch)]
+                else:
+                    reqs += [(_http_request(path, _json.dumps(p).encode()), 1) for p in ps]
+            send({"event": "prepared", "w": widx})
+        elif cmd["cmd"] == "go":
+            t0 = time.perf_counter()
+            stats = asyncio.run(_post_all(doors, reqs, int(cfg.get("http_conns", 8))))
+            stats["s"] = time.perf_counter() - t0
+            send({"event": "published", "w": widx, "http": stats})
+        elif cmd["cmd"] == "report":
+            send({"event": "done", "w": widx, "s": stats.get("s", 0.0), "counts": {}, "http": stats})
+
+
 class Coordinator:
     """Rank-side driver: serves the engine while steering the parser processes.
 
@@ -219,6 +331,7 @@ class Coordinator:
         from ..serving.remote import EngineServer
 
         self.events: Dict[str, Dict[int, Any]] = {}
+        self.last_http: Dict[str, int] = {}  # HTTP loaders' totals of the last phase
         self.server = EngineServer(engine, conns, on_control=self._on_control)
         self.n = len(conns)
         self.node_ranks = node_ranks
@@ -246,6 +359,10 @@ class Coordinator:
 
     def _on_control(self, idx: int, obj: Any) -> None:
         self.events.setdefault(obj.get("event", "?"), {})[idx] = obj
+        if "http" in obj and obj.get("event") == "done":
+            for k, v in obj["http"].items():
+                if k != "s":
+                    self.last_http[k] = self.last_http.get(k, 0) + int(v)
 
     def wait_all(self, event: str, timeout: float = 1800.0) -> Dict[int, Any]:
         t_end = time.time() + timeout
@@ -262,6 +379,7 @@ class Coordinator:
     def run_phase(self, seeds_per_worker: Sequence[Sequence[int]], n_per_step: int,
                   sync=None) -> Tuple[float, Dict[str, int]]:
         """Prepare (untimed), then time ``go`` → all ``done``. Returns (seconds, routing counts)."""
+        self.last_http = {}
         for i in range(self.n):
             self.server.send_control(i, {"cmd": "prepare", "n": n_per_step, "seeds": list(seeds_per_worker[i])})
         self.wait_all("prepared")

@@ -29,6 +29,10 @@ def test_two_ranks_one_broker():
     # node CPU budget of the timed region: every role accounted, brokers included
     cpu = out["cpu"]
     assert set(cpu["cores_busy_per_gpu"]) == {"parser_procs", "rank_proc", "brokers"}
+    # the HTTP-ingest phase: loaders POST every SMS to the native doors; their CPU is client-side
+    h = out["http_ingest"]
+    assert h["endpoint"] == "/sms/raw" and h["requests"] == total and h["value"] > 0
+    assert h["cpu"]["client_loaders"]["cpu_us_per_msg"] > 0
     assert cpu["cores_busy_per_gpu"]["parser_procs"] > 0 and cpu["cores_busy_per_gpu"]["brokers"] > 0
     assert cpu["cpu_us_per_msg"] > 0 and cpu["node_cores_at_8_gpus"] == round(8 * cpu["cores_busy_per_gpu_total"], 1)
     assert not [d for d in os.listdir("/tmp") if d == "smsgate-bench-bus-29671"]  # broker dir cleaned up
@@ -95,6 +99,11 @@ def test_eight_ranks_full_node_layout():
     raw = [m for m in members if m["subjects"] == ["sms.raw"]]
     parsed = [m for m in members if m["subjects"] == ["sms.parsed"]]
     assert len(raw) == 6 and len(parsed) == 2
-    # every raw message of the run (warmup included) stored on exactly one raw partition
-    assert sum(m["messages"] for m in raw) == ranks * (steps + warm) * per
+    # every raw message of the run stored on exactly one raw partition: the bus-ingest
+    # phase (warmup + steps) and the HTTP-ingest phase (1 warmup step + steps) through
+    # the six partitions' native /sms/raw doors
+    assert sum(m["messages"] for m in raw) == ranks * (steps + warm) * per + ranks * (steps + 1) * per
     assert all(m["messages"] > 0 for m in raw + parsed)
+    h = out["http_ingest"]
+    assert h["requests"] == total and h["routing"]["parsed"] + h["routing"]["keyword_skipped"] + \
+        h["routing"]["broken"] + h["routing"]["dlq"] == total

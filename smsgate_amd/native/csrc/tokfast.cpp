@@ -39,7 +39,7 @@ enum : uint8_t { C_L = 1, C_N = 2, C_D = 4, C_S = 8 };
 
 struct Tok {
     std::vector<std::string> tok_bytes;                       // id -> raw bytes
-    std::unordered_map<uint64_t, std::pair<int, int>> merges;  // (a << 32 | b) -> (rank, merged id)
+    void* merge_tab = nullptr;                                 // MergeTable* (defined below)
     int byte_id[256];
     std::vector<uint8_t> cls;                                  // code point -> C_* bits
     std::vector<std::pair<std::string, int>> specials;         // literal -> id
@@ -153,6 +153,37 @@ bool utf8_decode(const char* s, size_t len, std::vector<uint32_t>& cp, std::vect
     return true;
 }
 
+// Merge ranks in an open-addressing table (power-of-two slots, multiplicative hash):
+// ~8 k merges fit in L2, one probe per lookup in the common case.
+struct MergeTable {
+    std::vector<uint64_t> key;   // (a << 32 | b) + 1; 0 = empty
+    std::vector<int32_t> rank, id;
+    uint64_t mask = 0;
+    void init(size_t n) {
+        size_t cap = 16;
+        while (cap < 2 * n + 16) cap <<= 1;
+        key.assign(cap, 0);
+        rank.assign(cap, 0);
+        id.assign(cap, 0);
+        mask = cap - 1;
+    }
+    static uint64_t h(uint64_t k) { return (k * 0x9E3779B97F4A7C15ull) >> 17; }
+    void put(uint64_t k, int r, int m) {
+        for (uint64_t i = h(k) & mask;; i = (i + 1) & mask)
+            if (!key[i]) { key[i] = k + 1; rank[i] = r; id[i] = m; return; }
+    }
+    // rank of pair (a, b) or INT32_MAX; its merged id in *m
+    int find(int a, int b, int* m) const {
+        const uint64_t k = (((uint64_t)(uint32_t)a << 32) | (uint32_t)b) + 1;
+        for (uint64_t i = h(k - 1) & mask;; i = (i + 1) & mask) {
+            if (key[i] == k) { *m = id[i]; return rank[i]; }
+            if (!key[i]) return INT32_MAX;
+        }
+    }
+};
+
+inline const MergeTable& merge_table(const Tok& t) { return *reinterpret_cast<const MergeTable*>(t.merge_tab); }
+
 void bpe(Tok& t, const char* s, size_t len, std::vector<int>& out) {
     std::string key(s, len);
     auto it = t.cache.find(key);
@@ -160,34 +191,29 @@ void bpe(Tok& t, const char* s, size_t len, std::vector<int>& out) {
         out.insert(out.end(), it->second.begin(), it->second.end());
         return;
     }
-    std::vector<int> sym(len);
+    const MergeTable& mt = merge_table(t);
+    // symbols + the rank / merged id of each adjacent pair, updated locally per merge:
+    // O(n) table probes per word instead of O(n^2)
+    std::vector<int> sym(len), rk(len), mid(len);
     for (size_t i = 0; i < len; ++i) sym[i] = t.byte_id[(unsigned char)s[i]];
-    while (sym.size() > 1) {
-        int best = -1, best_rank = INT32_MAX, best_id = -1;
-        for (size_t i = 0; i + 1 < sym.size(); ++i) {
-            auto m = t.merges.find(((uint64_t)(uint32_t)sym[i] << 32) | (uint32_t)sym[i + 1]);
-            if (m != t.merges.end() && m->second.first < best_rank) {
-                best_rank = m->second.first;
-                best_id = m->second.second;
-                best = (int)i;
-            }
-        }
-        if (best < 0) break;
-        // merge every non-overlapping occurrence of the best pair, left to right
-        int a = sym[best], b = sym[best + 1];
-        std::vector<int> nxt;
-        nxt.reserve(sym.size());
-        for (size_t i = 0; i < sym.size();) {
-            if (i + 1 < sym.size() && sym[i] == a && sym[i + 1] == b) {
-                nxt.push_back(best_id);
-                i += 2;
-            } else {
-                nxt.push_back(sym[i]);
-                ++i;
-            }
-        }
-        sym.swap(nxt);
+    size_t n = len;
+    for (size_t i = 0; i + 1 < n; ++i) rk[i] = mt.find(sym[i], sym[i + 1], &mid[i]);
+    while (n > 1) {
+        int best = INT32_MAX;
+        size_t bi = 0;
+        for (size_t i = 0; i + 1 < n; ++i)
+            if (rk[i] < best) { best = rk[i]; bi = i; }
+        if (best == INT32_MAX) break;
+        // merge the leftmost occurrence of the lowest-rank pair (the library's order: a
+        // pair's rank never changes, so its later occurrences are merged next, left to right)
+        sym[bi] = mid[bi];
+        for (size_t i = bi + 1; i + 1 < n; ++i) { sym[i] = sym[i + 1]; rk[i] = rk[i + 1]; mid[i] = mid[i + 1]; }
+        --n;
+        if (bi + 1 < n) rk[bi] = mt.find(sym[bi], sym[bi + 1], &mid[bi]);
+        else rk[bi] = INT32_MAX;
+        if (bi > 0) rk[bi - 1] = mt.find(sym[bi - 1], sym[bi], &mid[bi - 1]);
     }
+    sym.resize(n);
     if (t.cache.size() < t.cache_max) t.cache.emplace(std::move(key), sym);
     out.insert(out.end(), sym.begin(), sym.end());
 }
@@ -250,7 +276,12 @@ const char* CAPSULE = "smsgate._tokfast.Tok";
 
 Tok* get(PyObject* cap) { return (Tok*)PyCapsule_GetPointer(cap, CAPSULE); }
 
-void destroy(PyObject* cap) { delete get(cap); }
+void destroy_tok(Tok* t) {
+    delete reinterpret_cast<MergeTable*>(t->merge_tab);
+    delete t;
+}
+
+void destroy(PyObject* cap) { destroy_tok(get(cap)); }
 
 // new(tok_bytes: list[bytes], merges: list[(a, b, merged)], cls: bytes, specials: list[(bytes, id)])
 PyObject* py_new(PyObject*, PyObject* args) {
@@ -265,13 +296,16 @@ PyObject* py_new(PyObject*, PyObject* args) {
         PyObject* b = PyList_GET_ITEM(tb, i);
         char* p;
         Py_ssize_t n;
-        if (PyBytes_AsStringAndSize(b, &p, &n) < 0) { delete t; PyBuffer_Release(&cls); return nullptr; }
+        if (PyBytes_AsStringAndSize(b, &p, &n) < 0) { destroy_tok(t); PyBuffer_Release(&cls); return nullptr; }
         t->tok_bytes[i].assign(p, n);
     }
+    MergeTable* mt = new MergeTable();
+    t->merge_tab = mt;
+    mt->init((size_t)PyList_GET_SIZE(mg));
     for (Py_ssize_t i = 0; i < PyList_GET_SIZE(mg); ++i) {
         int a, b, m;
-        if (!PyArg_ParseTuple(PyList_GET_ITEM(mg, i), "iii", &a, &b, &m)) { delete t; PyBuffer_Release(&cls); return nullptr; }
-        t->merges.emplace(((uint64_t)(uint32_t)a << 32) | (uint32_t)b, std::make_pair((int)i, m));
+        if (!PyArg_ParseTuple(PyList_GET_ITEM(mg, i), "iii", &a, &b, &m)) { destroy_tok(t); PyBuffer_Release(&cls); return nullptr; }
+        mt->put(((uint64_t)(uint32_t)a << 32) | (uint32_t)b, (int)i, m);
     }
     t->cls.assign((const uint8_t*)cls.buf, (const uint8_t*)cls.buf + cls.len);
     PyBuffer_Release(&cls);
@@ -279,7 +313,7 @@ PyObject* py_new(PyObject*, PyObject* args) {
         const char* p;
         Py_ssize_t n;
         int id;
-        if (!PyArg_ParseTuple(PyList_GET_ITEM(sp, i), "y#i", &p, &n, &id)) { delete t; return nullptr; }
+        if (!PyArg_ParseTuple(PyList_GET_ITEM(sp, i), "y#i", &p, &n, &id)) { destroy_tok(t); return nullptr; }
         t->specials.emplace_back(std::string(p, n), id);
     }
     // single-byte tokens (the byte-level alphabet is always in the vocabulary)
@@ -290,7 +324,7 @@ PyObject* py_new(PyObject*, PyObject* args) {
             if (!special) t->byte_id[(unsigned char)t->tok_bytes[i][0]] = (int)i;
         }
     for (int i = 0; i < 256; ++i)
-        if (t->byte_id[i] < 0) { delete t; PyErr_Format(PyExc_ValueError, "byte %d has no token", i); return nullptr; }
+        if (t->byte_id[i] < 0) { destroy_tok(t); PyErr_Format(PyExc_ValueError, "byte %d has no token", i); return nullptr; }
     return PyCapsule_New(t, CAPSULE, destroy);
 }
 

@@ -485,7 +485,7 @@ def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
             "visible_cpus": len(os.sched_getaffinity(0)),
             **({"client_loaders": {"cores_busy_per_gpu": round(loaders / dt / world, 2),
                                    "cpu_us_per_msg": round(loaders / max(msgs, 1) * 1e6, 1)}}
-               if loaders is not None and loaders > 0.05 * dt else {}),
+               if loaders is not None and loaders > 0.01 else {}),
             **({"placement": placement} if placement is not None else {})}
 
 

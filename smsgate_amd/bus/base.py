@@ -222,6 +222,29 @@ class Msg:
         return f"Msg(subject={self.subject!r}, seq={self.seq}, len={len(self.data)})"
 
 
+async def ack_all(msgs: Sequence["Msg"]) -> None:
+    """Ack every unsettled message of a batch: one call per acker / consumer instead of
+    one coroutine per message (an acker without ``ack_seqs`` gets them one by one)."""
+    groups: Dict[Tuple[int, str, str], Tuple["Acker", List[int]]] = {}
+    for m in msgs:
+        if m._done:
+            continue
+        m._done = True
+        md = m.metadata
+        key = (id(m._acker), md.stream, md.consumer)
+        g = groups.get(key)
+        if g is None:
+            g = groups[key] = (m._acker, [])
+        g[1].append(md.sequence)
+    for (_, stream, consumer), (acker, seqs) in groups.items():
+        fn = getattr(acker, "ack_seqs", None)
+        if fn is not None:
+            await fn(stream, consumer, seqs)
+        else:
+            for q in seqs:
+                await acker.ack(stream, consumer, q)
+
+
 class Acker(abc.ABC):
     @abc.abstractmethod
     async def ack(self, stream: str, consumer: str, seq: int) -> None: ...

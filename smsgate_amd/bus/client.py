@@ -156,6 +156,14 @@ class RemoteBus(Bus, Acker):
             self._ack_flush_scheduled = True
             asyncio.get_running_loop().call_soon(self._flush_acks)
 
+    async def ack_seqs(self, stream: str, consumer: str, seqs: Sequence[int]) -> None:
+        if self._closed:
+            return
+        self._acks.setdefault((stream, consumer), []).extend(seqs)
+        if not self._ack_flush_scheduled:
+            self._ack_flush_scheduled = True
+            asyncio.get_running_loop().call_soon(self._flush_acks)
+
     async def nak(self, stream: str, consumer: str, seq: int, delay: float) -> None:
         self._cast("nak", stream, consumer, seq, delay)
 

@@ -35,7 +35,7 @@ import time
 from datetime import datetime, timezone
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
-from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_RAW, Bus, Msg
+from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_RAW, Bus, Msg, ack_all
 from ..models.domain import RawSMS
 from ..obs import metrics as M
 from ..obs.errors import sentry_capture
@@ -186,8 +186,7 @@ class ParserWorker:
             with start_span("publish"):
                 if publishes:
                     await self.bus.publish_many(publishes)
-                for m in msgs:
-                    await m.ack()
+                await ack_all(msgs)
         if counts["ok"]:
             M.PARSED_OK.inc(counts["ok"])
         if counts["fail"]:

@@ -21,7 +21,7 @@ import logging
 from datetime import datetime, timezone
 from typing import List, Optional, Sequence, Tuple
 
-from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, Bus, Msg
+from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, Bus, Msg, ack_all
 from ..models.domain import ParsedSMS
 from ..obs import metrics as M
 from ..obs.errors import sentry_capture
@@ -98,8 +98,7 @@ class WriterService:
 
         if dlq:
             await self.bus.publish_many(dlq)
-        for m in msgs:
-            await m.ack()
+        await ack_all(msgs)
 
     async def start(self) -> None:
         await self.bus.ensure_stream()

@@ -679,6 +679,9 @@ def _proc_render(c: "_Ctx") -> str:
                 segs.extend(parts) if multi else segs.append(", ".join(parts))
                 continue
             shape = r.choice(("comma", "comma", "paren", "slash", "in", "lines"))
+            # the merchant leads; city and address come in either order (an address is
+            # recognised by its shape -- street word, number -- not by its position)
+            addr_first = bool(addr) and r.random() < 0.4
             if not city:
                 place = m + (", " + addr if addr else "")
             elif shape == "paren":
@@ -688,8 +691,10 @@ def _proc_render(c: "_Ctx") -> str:
             elif shape == "in":
                 place = f"{m} {r.choice(P['inn'])} {city}" + (f", {addr}" if addr else "")
             elif shape == "lines" and multi:
-                segs.extend([m, city] + ([addr] if addr else []))
+                segs.extend([m] + ([addr, city] if addr_first else [city] + ([addr] if addr else [])))
                 continue
+            elif addr_first:
+                place = f"{m}, {addr}, {city}"
             else:
                 place = f"{m}, {city}" + (f", {addr}" if addr else "")
             if r.random() < 0.3:

@@ -59,7 +59,7 @@ def _args(argv=None):
     p.add_argument("--model", default="smollm-135m")
     p.add_argument("--weights", default="train",
                    help="train (in-run, untimed; default) | random (worst case) | path to a safetensors checkpoint")
-    p.add_argument("--train-steps", type=int, default=2000)
+    p.add_argument("--train-steps", type=int, default=3000)
     p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
     p.add_argument("--train-lr", type=float, default=1e-3)
     p.add_argument("--data-workers", type=int, default=12,
@@ -653,7 +653,7 @@ def acquire_weights(args, device: str, rank: int, world: int, pool=None):
     w = train_extractor(tc, device=device, log=lambda s: print(f"[bench] train {s}", file=sys.stderr, flush=True),
                         data=data)
     prov["train_s"] = round(time.perf_counter() - t0, 1)
-    os.makedirs(cache, exist_ok=True)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
     tmp = path + f".{os.getpid()}.tmp"
     w.save(tmp)
     os.replace(tmp, path)

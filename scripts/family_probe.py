@@ -55,6 +55,28 @@ def main():
         ho = evaluate_engine(eng, n=a.eval_n, seed=4243, vocab_name="heldout", families="heldout", with_regex=True)
         leg = evaluate_engine(eng, n=a.eval_n // 2, seed=4244, vocab_name="heldout")
         bad = golden_case_mismatches(golden_case_results(eng))
+        # a few wrong answers per held-out family: what the model gets wrong, field by field
+        from smsgate_amd.models.evaluate import _expected, _post
+        from smsgate_amd.parse.text import normalize_body
+        from smsgate_amd.utils.synth import generate
+
+        items = [x for x in generate(240, seed=4245, vocab_name="heldout", families="heldout") if x.answer]
+        got = eng.run([normalize_body(x.body) for x in items])
+        fails = {}
+        for x, g in zip(items, got):
+            p = _post(x.body, x.timestamp, g)
+            want = _expected(x)
+            diff = {}
+            if p is None:
+                diff = {"unparsed": g}
+            else:
+                for k in want:
+                    v = getattr(p, k)
+                    v = v.value if hasattr(v, "value") else v
+                    if str(v) != str(want[k]):
+                        diff[k] = [str(v), str(want[k])]
+            if diff and len(fails.setdefault(x.family, [])) < 2:
+                fails[x.family].append({"body": x.body[:160], "diff": diff})
         rec = {"tag": a.tag, "model": a.model, "step": step, "train_s": round(time.perf_counter() - t0, 1),
                "batch": a.batch, "lr": a.lr,
                "train_formats": {"exact": round(tr["exact"], 4), "by_family": tr["by_family"]},
@@ -62,7 +84,7 @@ def main():
                "heldout_formats": {"exact": round(ho["exact"], 4), "regex_exact": round(ho["regex_exact"], 4),
                                    "field_acc": {k: round(v, 4) for k, v in ho["field_acc"].items()},
                                    "by_family": ho["by_family"]},
-               "cases_mismatches": bad, "eval_s": round(time.perf_counter() - te, 1)}
+               "cases_mismatches": bad, "heldout_failures": fails, "eval_s": round(time.perf_counter() - te, 1)}
         print(json.dumps(rec), flush=True)
         with open(a.jsonl, "a") as f:
             f.write(json.dumps(rec) + "\n")

@@ -114,7 +114,8 @@ def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
     if families is not None:
         assert not set(family_names(families)) & set(HELDOUT_FAMILIES), "held-out families are never trained on"
     out: List[Tuple[List[int], List[int]]] = []
-    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name, families=families) if s.answer is not None]
+    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name, families=families, training=True)
+             if s.answer is not None]
     bodies = [normalize_body(s.body) for s in items]
     msgs = tok.message_ids(bodies, max_body)
     encs = tok.encode_offsets(bodies)

@@ -251,8 +251,8 @@ def _legacy_account(r: random.Random, v: Vocab, ts: int, cur: str, card: str) ->
 
 
 def _legacy_credit(r: random.Random, ts: int, cur: str, card: str,
-                   kinds: Tuple[str, ...] = ("CREDIT PAYMENT", "C2C RECEIVED", "TRANSFER IN")) -> SynthSMS:
-    kind = r.choice(kinds)
+                   kinds: Optional[Tuple[str, ...]] = None) -> SynthSMS:
+    kind = r.choice(kinds or ("CREDIT PAYMENT", "C2C RECEIVED", "TRANSFER IN"))
     date = _date(r)
     amt, bal = _amount(r, cur), _amount(r, cur)
     body = f"{kind}: {date},card ***{card}. Amount:{amt} {cur}, Balance:{bal} {cur}"
@@ -654,6 +654,8 @@ def _proc_render(c: "_Ctx") -> str:
     for seg in order:
         if seg == "AMT":
             v = c.AMT()
+            if r.random() < 0.15:  # a debit written as a negative amount ("-52.00 USD")
+                v = "-" + v
             segs.append(lab(P["amt"]) + v if (labelled or r.random() < 0.2) else v)
         elif seg == "CARD":
             v = c.CARD()
@@ -737,12 +739,14 @@ def family_names(which: Union[str, Sequence[str]]) -> Tuple[str, ...]:
     return tuple(which)
 
 
-def _family_one(r: random.Random, v: Vocab, name: str) -> SynthSMS:
+def _family_one(r: random.Random, v: Vocab, name: str, all_credit_kinds: bool = False) -> SynthSMS:
     ts = r.randint(1_690_000_000, 1_750_000_000)
     if name in LEGACY_FAMILIES:
         cur, card = r.choice(_CURRENCIES), f"{r.randint(0, 9999):04d}"
-        if name == "legacy_credit":  # the kind the worker's keyword filter lets through to the LLM
-            return _legacy_credit(r, ts, cur, card, kinds=("TRANSFER IN",))
+        if name == "legacy_credit":
+            # traffic: the kind the worker's keyword filter lets through to the LLM; training
+            # also sees the skipped kinds (CREDIT PAYMENT / C2C RECEIVED: the legacy mix scores them)
+            return _legacy_credit(r, ts, cur, card, kinds=None if all_credit_kinds else ("TRANSFER IN",))
         return (_legacy_purchase if name == "legacy_purchase" else _legacy_account)(r, v, ts, cur, card)
     fam = _BY_NAME[name]
     c = _Ctx(r, v, fam, ts)
@@ -767,14 +771,15 @@ TRAFFIC_KINDS = {k: v.get("kinds") for k, v in TRAFFIC.items() if "families" not
 
 def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "train",
              kinds: Optional[Sequence[str]] = None,
-             families: Union[None, str, Sequence[str]] = None) -> List[SynthSMS]:
+             families: Union[None, str, Sequence[str]] = None, training: bool = False) -> List[SynthSMS]:
     """``n`` messages; with ``unique`` every body is distinct (defeats the response cache).
     ``vocab_name``: ``"train"`` (what the extractor is trained on) or ``"heldout"`` —
     merchant / city / street names disjoint from the training pools (held-out scoring
     and the benchmark's traffic).  ``kinds``: keep only these message kinds.
     ``families``: None = the legacy mix; else draw each message from these template
     families (``"train"``, ``"heldout"``, ``"all"`` or names), uniformly by family with
-    the legacy formats and the procedural layouts weighted x3 in ``"train"`` / ``"all"``."""
+    the legacy formats and the procedural layouts weighted x3 in ``"train"`` / ``"all"``.
+    ``training``: also the legacy credit kinds the keyword filter skips (never traffic)."""
     r = random.Random(seed)
     v = vocab(vocab_name)
     names: Tuple[str, ...] = ()
@@ -786,7 +791,7 @@ def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "trai
     out: List[SynthSMS] = []
     seen = set()
     while len(out) < n:
-        s = _one(r, v) if not names else _family_one(r, v, r.choices(names, weights)[0])
+        s = _one(r, v) if not names else _family_one(r, v, r.choices(names, weights)[0], training)
         if kinds is not None and s.kind not in kinds:
             continue
         if unique:

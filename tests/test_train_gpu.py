@@ -23,7 +23,10 @@ def _score(w, n=300):
 
 
 def test_training_learns_extraction():
-    w = train_extractor(TrainConfig(model="small", steps=2500, lr=2e-3, n_examples=30000, log_every=0), device="cuda")
+    # the legacy mix (the reference's two formats): what the small model learns in 2 500 steps;
+    # the template-family generalisation of the 135M flagship is scored by bench.py
+    w = train_extractor(TrainConfig(model="small", steps=2500, lr=2e-3, n_examples=30000, log_every=0, families=None),
+                        device="cuda")
     acc = _score(w)
     for f in ("txn_type", "date", "currency"):
         assert acc[f] >= 0.95, acc

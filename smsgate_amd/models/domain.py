@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import hashlib
+import json
 from decimal import Decimal
 from enum import Enum
 from typing import Literal, Optional
@@ -32,6 +33,8 @@ __all__ = [
     "get_sha1_hash",
     "PARSER_VERSION_LLM",
     "CORE_FIELDS",
+    "parsed_wire",
+    "raw_wire",
 ]
 
 PARSER_VERSION_LLM = "llm-0.2.0"  # gemini_parser.py:267
@@ -91,6 +94,35 @@ class ParsedSMS(BaseModel):
     @field_serializer("date", when_used="json")
     def _iso(self, v: _dt.datetime) -> str:
         return v.isoformat()
+
+
+_JSON = json.JSONEncoder(ensure_ascii=False, separators=(",", ":")).encode
+
+
+def parsed_wire(p: "ParsedSMS") -> bytes:
+    """``p.model_dump_json().encode()`` without pydantic's per-field Python serializers
+    (~2x faster): the same keys in the same order, ``isoformat`` dates, ``str``
+    decimals, UTF-8 kept and the same escapes (tests/test_parse_helpers.py fuzzes the
+    equality); anything the fast path cannot encode (a lone surrogate) falls back."""
+    try:
+        return _JSON({
+            "msg_id": p.msg_id, "device_id": p.device_id, "sender": p.sender, "date": p.date.isoformat(),
+            "raw_body": p.raw_body, "txn_type": p.txn_type.value if isinstance(p.txn_type, TxnType) else p.txn_type,
+            "amount": None if p.amount is None else str(p.amount), "currency": p.currency, "card": p.card,
+            "merchant": p.merchant, "city": p.city, "address": p.address,
+            "balance": None if p.balance is None else str(p.balance), "parser_version": p.parser_version,
+        }).encode("utf-8")
+    except (UnicodeEncodeError, TypeError, AttributeError, ValueError):
+        return p.model_dump_json().encode("utf-8")
+
+
+def raw_wire(r: "RawSMS") -> bytes:
+    """``r.model_dump_json().encode()``, fast path (see :func:`parsed_wire`)."""
+    try:
+        return _JSON({"msg_id": r.msg_id, "sender": r.sender, "body": r.body, "date": r.date,
+                      "device_id": r.device_id, "source": r.source}).encode("utf-8")
+    except (UnicodeEncodeError, TypeError, ValueError):
+        return r.model_dump_json().encode("utf-8")
 
 
 class ParsedSmsCore(BaseModel):

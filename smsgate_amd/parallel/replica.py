@@ -90,6 +90,7 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     from ..parse.backends.local_llm import RemoteLLMBackend
     from ..parse.pipeline import ParsePipeline
     from ..serving.remote import RemoteEngineClient
+    from ..models.domain import raw_wire
     from ..services.gateway import payload_to_raw
     from ..services.parser import ParserWorker
     from ..services.writer import WriterService
@@ -152,8 +153,7 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                 chunk = 256
                 msgs = prepared[i]
                 for c in range(0, len(msgs), chunk):
-                    items = [(SUBJECT_RAW, payload_to_raw(p).model_dump_json().encode("utf-8"))
-                             for p in msgs[c:c + chunk]]
+                    items = [(SUBJECT_RAW, raw_wire(payload_to_raw(p))) for p in msgs[c:c + chunk]]
                     await bus.publish_many(items)
                     await asyncio.sleep(0)
 

@@ -39,7 +39,7 @@ from pydantic import BaseModel
 
 from ..bus.base import SUBJECT_RAW, Bus
 from ..bus.coalesce import PublishCoalescer
-from ..models.domain import RawSMS, get_md5_hash
+from ..models.domain import RawSMS, get_md5_hash, raw_wire
 from ..obs import metrics as M
 from ..obs.errors import recent_errors, sentry_capture
 
@@ -142,7 +142,7 @@ def create_app(get_bus: Optional[BusGetter] = None, *, log_dir: Optional[str] = 
         try:
             t0 = time.perf_counter()
             bus = await request.app.state.get_bus()
-            await publish_one(bus, raw.model_dump_json().encode("utf-8"))
+            await publish_one(bus, raw_wire(raw))
             M.GATEWAY_PUBLISH_TIME.observe(time.perf_counter() - t0)
         except Exception as exc:
             sentry_capture(exc)
@@ -162,7 +162,7 @@ def create_app(get_bus: Optional[BusGetter] = None, *, log_dir: Optional[str] = 
             raise HTTPException(status_code=400, detail="Invalid payload") from exc
         try:
             bus = await request.app.state.get_bus()
-            await bus.publish_many([(SUBJECT_RAW, r.model_dump_json().encode("utf-8")) for r in raws])
+            await bus.publish_many([(SUBJECT_RAW, raw_wire(r)) for r in raws])
         except Exception as exc:
             sentry_capture(exc)
             M.GATEWAY_REQUESTS.labels("/sms/raw/batch", "500").inc()

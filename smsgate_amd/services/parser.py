@@ -36,7 +36,7 @@ from datetime import datetime, timezone
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, SUBJECT_PROCESSING, SUBJECT_RAW, Bus, Msg, ack_all
-from ..models.domain import RawSMS
+from ..models.domain import RawSMS, parsed_wire
 from ..obs import metrics as M
 from ..obs.errors import sentry_capture
 from ..obs.tracing import start_span, start_transaction
@@ -138,7 +138,7 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                     counts["fail"] += 1
                     continue
                 try:
-                    payload = parsed.model_dump_json().encode()
+                    payload = parsed_wire(parsed)
                 except Exception as err:
                     sentry_capture(err, extras={"raw_data": text})
                     out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))

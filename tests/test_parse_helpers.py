@@ -282,3 +282,35 @@ def test_date_fast_paths_equal_dateutil():
         assert got == want, s
         fast += _fast_dateutil(s) is not None
     assert fast > 4000
+
+
+def test_fast_wire_json_equals_pydantic():
+    """parsed_wire / raw_wire are byte-for-byte model_dump_json (the sms.parsed and
+    sms.raw contracts), on every template family and on hostile strings."""
+    import random
+    from datetime import datetime as _dt
+    from decimal import Decimal as _D
+
+    from smsgate_amd.models.domain import parsed_wire, raw_wire
+    from smsgate_amd.parse import postprocess_answer
+    from smsgate_amd.parse.text import normalize_body
+    from smsgate_amd.utils.synth import generate
+
+    for s in generate(400, seed=13, vocab_name="heldout", families="all"):
+        raw = RawSMS(msg_id="m", sender="B", body=s.body, date=str(s.timestamp), device_id="d")
+        assert raw_wire(raw) == raw.model_dump_json().encode()
+        p = postprocess_answer(raw, normalize_body(s.body), s.answer).parsed
+        assert parsed_wire(p) == p.model_dump_json().encode()
+    r = random.Random(5)
+    alphabet = 'aZ09 "\\\n\t\x00\x01\x1f\x7f/é漢😀 '
+    for _ in range(500):
+        t = "".join(r.choice(alphabet) for _ in range(r.randint(0, 12)))
+        p = ParsedSMS(msg_id=t, device_id=r.choice([None, t]), sender=t or "s", date=_dt(2024, 2, 29, 1, 2, 3, r.choice([0, 7])),
+                      raw_body=t, txn_type=r.choice(["debit", "credit", "otp", "unknown"]),
+                      amount=r.choice([None, _D("1.000"), _D("-0.0"), _D("123456789.01")]), currency=r.choice([None, "usd", "$"]),
+                      card=r.choice([None, "0018"]), merchant=r.choice([None, t]), city=t, address=t,
+                      balance=r.choice([None, _D("0.0")]))
+        assert parsed_wire(p) == p.model_dump_json().encode()
+        raw = RawSMS(msg_id=t, sender=t or "s", body=t or "b", date=t, device_id=r.choice([None, t]),
+                     source=r.choice(["device", "xml"]))
+        assert raw_wire(raw) == raw.model_dump_json().encode()

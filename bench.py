@@ -47,6 +47,7 @@ import os
 import sys
 import time
 
+VISIBLE_CPUS = len(os.sched_getaffinity(0))  # before any placement narrows this process
 BASELINE_MSGS_PER_S = 10370.0  # median of 5 quiet runs of the reference hot path (stubbed LLM)
 
 
@@ -431,12 +432,21 @@ def pin_replica(args, local: int, procs, brokers):
     from smsgate_amd.parallel.placement import gpu_topology, plan
 
     node_gpus = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    p = plan(local, node_gpus, broker_cores=2 if brokers else 0)
+    # one core per node broker (single-threaded event loops: 9 on an 8-GPU node)
+    p = plan(local, node_gpus, broker_cores=len(brokers) if brokers else 0)
     if p is None:
         return {"pinned": False, "why": "no GPU topology in sysfs"}
-    if args.pin == "auto" and node_gpus != len(gpu_topology()):
-        return {"pinned": False, "why": f"job holds {node_gpus} of {len(gpu_topology())} GPUs (auto)", **p.describe()}
+    n_topo = len(gpu_topology())
+    if args.pin == "auto" and (node_gpus < 2 or node_gpus != n_topo):
+        # a single-GPU job shares its machine (the other GPUs' jobs, cgroup CPU quotas):
+        # the scheduler places it; a job holding every GPU of the node owns the placement
+        return {"pinned": False, "why": f"auto: the job holds {node_gpus} GPU(s) of the {n_topo} visible",
+                **p.describe()}
     p.apply(rank_pid=0, worker_pids=[q.pid for q in procs], broker_pids=[b.pid for b in (brokers or [])])
+    if args.rank_threads <= 0:  # torch's pool sized for the rank's cores, not the machine's
+        import torch
+
+        torch.set_num_threads(max(1, len(p.rank_cpus)))
     return {"pinned": True, **p.describe()}
 
 
@@ -482,7 +492,7 @@ def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
             "cores_busy_per_gpu_total": round(total, 2),
             "cpu_us_per_msg": round(sum(cpu.values()) / max(msgs, 1) * 1e6, 1),
             "node_cores_at_8_gpus": round(8 * total, 1),
-            "visible_cpus": len(os.sched_getaffinity(0)),
+            "visible_cpus": VISIBLE_CPUS,
             **({"client_loaders": {"cores_busy_per_gpu": round(loaders / dt / world, 2),
                                    "cpu_us_per_msg": round(loaders / max(msgs, 1) * 1e6, 1)}}
                if loaders is not None and loaders > 0.01 else {}),

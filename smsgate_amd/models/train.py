@@ -18,7 +18,8 @@ its speed.  This module turns the LM into a working extractor.
   reproduce it;
 * loss: next-token cross-entropy on the answer positions only, over the decode
   vocabulary (the tokenizer ids, the same rows the serving lm_head uses);
-* model: fp32 master weights, bf16 autocast, AdamW with warmup + cosine decay.
+* model: fp32 master weights, bf16 autocast, AdamW with warmup + cosine decay; the
+  served weights are an exponential moving average of the iterates (``ema``);
   The differentiable forward is :func:`~smsgate_amd.models.extractor.reference_forward`
   (PyTorch SDPA); serving uses the HIP kernels on the saved bf16 weights;
 * data parallel: under ``torch.distributed`` (one process per GPU, RCCL) every
@@ -75,6 +76,11 @@ class TrainConfig:
     # TRAIN_FAMILIES, the two legacy formats included); None = the legacy mix only.
     # The held-out families (HELDOUT_FAMILIES) are never trained on.
     families: Optional[str] = "train"
+    # exponential moving average of the weights (0 = off): the served weights are the
+    # average over the last ~1/(1-ema) steps -- smoother than the last iterate, which
+    # swings on SMS layouts it never saw from one checkpoint to the next
+    ema: float = 0.998
+    ema_start: int = 0  # first step the average includes (0 = warmup end)
     data_parallel: bool = True  # under torch.distributed: all-reduce gradients (False: train this rank alone)
     eval_every: int = 0  # call on_eval(step, serving weights) every N steps (0 = never)
 
@@ -260,6 +266,9 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
                             fused=fused)
 
     gb = GradBuckets(list(w.parameters()), bucket_mb=cfg.bucket_mb) if ddp else None
+    params = list(w.parameters())
+    ema_params = None
+    ema_from = cfg.ema_start or cfg.warmup
 
     def lr_at(step: int) -> float:
         if step < cfg.warmup:
@@ -304,15 +313,32 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
             loss.backward()
         torch.nn.utils.clip_grad_norm_(w.parameters(), 1.0)
         opt.step()
+        if cfg.ema > 0 and step + 1 >= ema_from:
+            with torch.no_grad():
+                if ema_params is None:
+                    ema_params = [p.detach().clone() for p in params]
+                else:  # one multi-tensor lerp over all parameters
+                    torch._foreach_lerp_(ema_params, [p.detach() for p in params], 1.0 - cfg.ema)
         if cfg.log_every and rank == 0 and (step % cfg.log_every == 0 or step == cfg.steps - 1):
             log(f"step {step:5d} loss {loss.item():.4f} lr {lr_at(step):.2e} ({time.perf_counter() - t0:.1f}s)"
                 + (f" x{world} ranks" if world > 1 else ""))
         done = step + 1
         if on_eval is not None and cfg.eval_every and done % cfg.eval_every == 0 and done < cfg.steps:
-            on_eval(done, to_serving(w, mcfg))
+            on_eval(done, to_serving(_with_ema(w, ema_params), mcfg))
         if cfg.ckpt_dir and rank == 0 and (done == cfg.steps or (cfg.ckpt_every and done % cfg.ckpt_every == 0)):
             _save_checkpoint(cfg.ckpt_dir, done, w, opt, rng)
-    return to_serving(w, mcfg)
+    return to_serving(_with_ema(w, ema_params), mcfg)
+
+
+def _with_ema(w: ExtractorWeights, ema_params) -> ExtractorWeights:
+    """``w`` itself, or a copy holding the averaged parameters."""
+    if ema_params is None:
+        return w
+    out = ExtractorWeights(w.cfg, device=w.embed.device, dtype=torch.float32, seed=None)
+    with torch.no_grad():
+        for p, e in zip(out.parameters(), ema_params):
+            p.copy_(e)
+    return out
 
 
 def _as_rng_state(st):

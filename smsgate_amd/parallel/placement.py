@@ -17,9 +17,9 @@ here the layout is computed from the kernel's own topology:
   (``/sys/bus/pci/devices/<dddd:bb:dd.f>/numa_node``, ``local_cpulist``),
   intersected with this process's allowed CPUs;
 * the ranks whose GPUs share a NUMA node split its cores into equal contiguous
-  slices; in each slice the first core runs the rank process and the rest the
-  parser workers; local rank 0's node gives up ``broker_cores`` cores (its last
-  ones) to the node's brokers first.
+  slices; in each slice the first quarter (at least 2 cores) runs the rank process
+  and the rest the parser workers; local rank 0's node gives up ``broker_cores``
+  cores (its last ones) to the node's brokers first.
 
 :func:`plan` returns a :class:`Placement` (or None when the topology is not
 readable, e.g. no GPU driver); :meth:`Placement.apply` sets the affinities.
@@ -179,7 +179,10 @@ def plan(local_rank: int, local_world: int, broker_cores: int = 2, sysfs: str = 
     slot = [g.index for g in peers].index(mine.index)
     per = max(1, len(cores) // len(peers))
     chunk = cores[slot * per:(slot + 1) * per] if len(cores) >= len(peers) else cores
-    rank_cpus = chunk[:1]
-    worker_cpus = chunk[1:] or chunk
+    # the rank process is multi-threaded (the launch loop, torch's pool, the HIP runtime's
+    # threads: ~1.8 cores busy at the r03 rate): a quarter of the slice, at least 2 cores
+    nr = min(len(chunk), max(2, len(chunk) // 4))
+    rank_cpus = chunk[:nr]
+    worker_cpus = chunk[nr:] or chunk
     return Placement(local_rank, mine.numa_node, mine.bdf, rank_cpus, worker_cpus,
                      brokers if local_rank == 0 else [], len(peers))

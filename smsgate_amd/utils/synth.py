@@ -308,7 +308,7 @@ _STYLE_POOLS = {
                numbers=("dot", "comma_dot", "comma_dot", "int"),
                cards=("star1", "stars2", "stars3", "stars4", "spaced", "first_mask", "ending")),
     "ru": dict(dates=("dmy2", "dmy4", "dmy4_date", "dmy2_date", "time_first", "iso"),
-               money=("code_after", "sym_after", "word_after"),
+               money=("code_after", "code_after", "code_before", "sym_after", "word_after"),
                numbers=("space_comma", "space_comma", "comma", "dot", "int"),
                cards=("star1", "stars2", "stars4", "spaced", "first_mask")),
     "tr": dict(dates=("dmy2", "dmy4", "time_first", "iso", "slash"),
@@ -649,7 +649,9 @@ def _proc_render(c: "_Ctx") -> str:
 
     segs: List[str] = []
     head = ""
-    if r.random() < 0.75:
+    # a credit is always announced (nothing else tells it from a debit); a debit's header
+    # is optional -- an unlabelled transaction is a debit
+    if c.fam.txn == "credit" or r.random() < 0.75:
         head = r.choice(P["head_credit"] if c.fam.txn == "credit" else P["head_debit"])
     for seg in order:
         if seg == "AMT":
@@ -705,8 +707,13 @@ def _proc_render(c: "_Ctx") -> str:
     if multi:
         body = "\n".join(([head] if head else []) + segs)
     else:
-        sep = r.choice((", ", "; ", " | ", ". ", " ", " / "))
-        body = (head + r.choice((": ", " ", ". ")) if head else "") + sep.join(segs)
+        seps = (", ", "; ", " | ", ". ", " ", " / ")
+        sep = r.choice(seps)
+        if r.random() < 0.25:  # mixed separators within one message
+            body = segs[0] + "".join((sep if r.random() < 0.5 else r.choice(seps)) + x for x in segs[1:])
+        else:
+            body = sep.join(segs)
+        body = (head + r.choice((": ", " ", ". ")) if head else "") + body
     return body + (c.noise() if not multi else "")
 
 

@@ -53,7 +53,7 @@ def test_eight_rank_plan_is_numa_local_and_disjoint(tmp_path):
         node = set(range(sock * 64, sock * 64 + 64))
         mine = set(p.rank_cpus) | set(p.worker_cpus)
         assert p.numa_node == sock and mine <= node  # every process of the replica on its GPU's socket
-        assert len(p.rank_cpus) == 1 and len(p.worker_cpus) >= 8
+        assert len(p.rank_cpus) >= 2 and len(p.worker_cpus) >= 8
         assert not (mine & used)  # replicas never share a core
         used |= mine
     assert plans[0].broker_cpus == [62, 63] and not (set(plans[0].broker_cpus) & used)
@@ -82,4 +82,5 @@ def test_partial_node(tmp_path, world):
     root = _fake_node(tmp_path)
     ps = [plan(r, world, sysfs=root, env={}, allowed=range(128)) for r in range(world)]
     assert all(p is not None and p.numa_node == 0 for p in ps)
-    assert len({c for p in ps for c in p.rank_cpus}) == world
+    assert all(len(p.rank_cpus) >= 2 for p in ps)
+    assert not set.intersection(*(set(p.rank_cpus) | set(p.worker_cpus) for p in ps)) if world > 1 else True

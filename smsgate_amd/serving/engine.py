@@ -188,6 +188,43 @@ class _Snapshot:
     active: Dict[int, Any]  # row -> key at snapshot time (guards against re-admitted rows)
 
 
+class _PinnedRing:
+    """Persistent pinned host staging for host->device copies of index arrays.
+
+    ``tensor.pin_memory()`` per call pins a fresh block every prefill / compaction
+    (~23 ms a call when the rank process runs on few cores: profiles/r04_rank_pin_memory
+    in PERF.md); here a ring of ``slots`` pre-pinned byte buffers is reused, each slot
+    guarded by an event recorded after the copy that reads it, so a slot is rewritten
+    only once its previous copy has finished (almost always already true)."""
+
+    def __init__(self, nbytes: int, slots: int = 4) -> None:
+        self.bufs = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in range(slots)]
+        self.events: List[Optional[torch.cuda.Event]] = [None] * slots
+        self.k = 0
+
+    def to_device(self, arr: np.ndarray, dev) -> torch.Tensor:
+        arr = np.ascontiguousarray(arr)
+        nb = arr.nbytes
+        i = self.k
+        self.k = (self.k + 1) % len(self.bufs)
+        if nb > self.bufs[i].numel():  # larger than planned: grow this slot once
+            if self.events[i] is not None:
+                self.events[i].synchronize()
+            self.bufs[i] = torch.empty(nb, dtype=torch.uint8).pin_memory()
+        elif self.events[i] is not None:
+            self.events[i].synchronize()
+        host = self.bufs[i][:nb]
+        host.numpy()[:] = arr.view(np.uint8).reshape(-1)
+        out = host.view(_TORCH_DTYPE[arr.dtype.str]).view(arr.shape).to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[i] = ev
+        return out
+
+
+_TORCH_DTYPE = {"<i4": torch.int32, "<i8": torch.int64, "<f4": torch.float32}
+
+
 class ExtractionEngine:
     def __init__(self, weights: ExtractorWeights, tokenizer: ExtractorTokenizer,
                  cfg: Optional[EngineConfig] = None, fields: Sequence[FieldSpec] = DEFAULT_FIELDS,
@@ -278,6 +315,9 @@ class ExtractionEngine:
             for _ in range(2)
         ]
         self._snap_flip = 0
+        # pinned staging of the prefill / compaction index arrays (a prefill of T tokens
+        # and n prompts stages 2T + 4n + 1 int32 + T int64)
+        self._stage = _PinnedRing(max(1 << 20, 12 * ec.prefill_max_tokens + 16 * S + 64), slots=6)
         self._pending: Optional[_Snapshot] = None
         self._sides: List[torch.cuda.Stream] = []  # side streams of the split decode / prefill
         self._fwd_ss: Optional[torch.Tensor] = None  # row partials of the last forward's output (_layers_fused)
@@ -453,8 +493,7 @@ class ExtractionEngine:
         pos_np = np.arange(T, dtype=np.int32) - np.repeat(cu[:-1] - skip, lens)
         slot_np = np.repeat(seq_slots, lens)
         # one pinned staging copy for all small index arrays
-        meta = torch.from_numpy(np.concatenate([pos_np, slot_np, cu, rows_np, full - 1, seq_slots, skip])).pin_memory()
-        meta_d = meta.to(dev, non_blocking=True)
+        meta_d = self._stage.to_device(np.concatenate([pos_np, slot_np, cu, rows_np, full - 1, seq_slots, skip]), dev)
         o = 0
         pos_d = meta_d[o:o + T]; o += T
         slot_d = meta_d[o:o + T]; o += T
@@ -465,7 +504,7 @@ class ExtractionEngine:
         qstart = meta_d[o:o + n]
         if kk is not None:
             self._copy_templates(kk, tsl, seq_slots)
-        flat_d = torch.from_numpy(flat).pin_memory().to(dev, non_blocking=True)
+        flat_d = self._stage.to_device(flat, dev)
         x = F.embedding(flat_d, self.w.embed).contiguous()
         max_q = int(lens.max())
         if self.spec or self.copy:  # the rows' prompts: draft source and copy set
@@ -562,8 +601,7 @@ class ExtractionEngine:
         sel = np.nonzero(kk)[0]
         kmax = int(kk[sel].max())
         dev = self.device
-        items = torch.from_numpy(np.stack([tsl[sel], seq_slots[sel], kk[sel]]).astype(np.int32)).pin_memory().to(
-            dev, non_blocking=True)
+        items = self._stage.to_device(np.stack([tsl[sel], seq_slots[sel], kk[sel]]).astype(np.int32), dev)
         # exactly k rows per item, every layer, one launch (a torch gather / index_put of
         # the kmax-row block of all layers moved ~0.3 GB per admitted batch and cost more
         # than the prefill rows it saved: profiles/r03_ab_templates.jsonl)
@@ -840,8 +878,8 @@ class ExtractionEngine:
         if len(free_low) < len(movers):
             return
         dev = self.device
-        src = torch.tensor(movers, dtype=torch.long).pin_memory().to(dev, non_blocking=True)
-        dst = torch.tensor(free_low, dtype=torch.long).pin_memory().to(dev, non_blocking=True)
+        src = self._stage.to_device(np.asarray(movers, dtype=np.int64), dev)
+        dst = self._stage.to_device(np.asarray(free_low, dtype=np.int64), dev)
         for t in (self.tok_buf, self.pos, self.state, self.done, self.out_len, self.out_buf):
             t.index_copy_(0, dst, t.index_select(0, src))
         s_src, s_dst = self.slot_id.index_select(0, src), self.slot_id.index_select(0, dst)

@@ -156,7 +156,12 @@ def main() -> int:
         res[k] = {"us": round(us, 2), "gflop": round(fl / 1e9, 2), "min_mb": round(by / 1e6, 1),
                   "tflops": round(tf, 1), "pct_peak_flops": round(100 * tf / PEAK_TFLOPS, 1),
                   "tb_s_min_bytes": round(tbs, 2), "pct_hbm": round(100 * tbs / HBM_TBS, 1),
-                  "floor_us": round(max(fl / PEAK_TFLOPS / 1e6, by / HBM_TBS / 1e6), 2)}
+                  "floor_us": round(max(fl / PEAK_TFLOPS / 1e6, by / HBM_TBS / 1e6), 2),
+                  # only the verify attention rotates its inputs through 8 disjoint regions;
+                  # the other cases re-read the same operands every replay, which can stay
+                  # in the 256 MB Infinity Cache: their pct_hbm / tb_s are upper bounds
+                  "operands": ("rotating x8 (HBM)" if k.startswith("attn_spec") else
+                               "repeated (cache-resident possible: HBM figures are upper bounds)")}
         print(json.dumps({k: res[k]}), file=sys.stderr, flush=True)
     print(json.dumps(res))
     return 0

@@ -9,7 +9,7 @@ from __future__ import annotations
 import itertools
 import socket
 import struct
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 from urllib.parse import urlparse
 
 import msgpack
@@ -67,7 +67,7 @@ class SyncBusClient:
     def subscribe(self, subject: str, durable: str, **opts: Any) -> str:
         return self.call("subscribe", subject, durable, opts)
 
-    def consumer_info(self, stream: str, durable: str) -> Dict[str, Any]:
+    def consumer_info(self, stream: str, durable: str, subject: Optional[str] = None) -> Dict[str, Any]:
         return self.call("consumer_info", stream, durable)
 
     def stream_info(self, stream: str = "SMS") -> Dict[str, Any]:
@@ -104,9 +104,12 @@ class _SyncSharded:
         names = [self.members[k].subscribe(subject, durable, **opts) for k in self.router.members(subject)]
         return names[0]
 
-    def consumer_info(self, stream: str, durable: str) -> Dict[str, Any]:
+    def consumer_info(self, stream: str, durable: str, subject: Optional[str] = None) -> Dict[str, Any]:
+        """Summed over the members; with ``subject`` only the members that subject is
+        routed to are asked (one round trip per partition instead of one per broker)."""
         found = []
-        for m in self.members:
+        members = self.members if subject is None else [self.members[k] for k in self.router.members(subject)]
+        for m in members:
             try:
                 found.append(m.consumer_info(stream, durable))
             except BusError:

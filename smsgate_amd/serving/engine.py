@@ -1054,12 +1054,14 @@ class ExtractionEngine:
         fin = [r for r, key in snap.active.items()
                if r < snap.B and done_h[r] and self.active.get(r) is key]
         if fin and raw:
-            # token ids only (a remote client detokenises): numpy row slices
-            lens_n = lens.numpy()
-            bufs_n = bufs.numpy()
-            for r in fin:
-                res.append((self.active.pop(r), bufs_n[r, : lens_n[r]].copy()))
-                heapq.heappush(self.free_rows, r)
+            # token ids only (a remote client detokenises): one gather copy of the finished
+            # rows out of the reused pinned snapshot, then per-row views of it
+            lens_l = lens.numpy()[fin].tolist()
+            blk = bufs.numpy()[fin]
+            active, free = self.active, self.free_rows
+            for j, r in enumerate(fin):
+                res.append((active.pop(r), blk[j, : lens_l[j]]))
+                heapq.heappush(free, r)
         elif fin:
             # one batched detokenisation (Rust, parallel) for every field of every finished row
             nf = len(self.fsm.fields)

@@ -74,7 +74,10 @@ def unpack_id_arrays(buf: bytes) -> Tuple[bytes, int, List[np.ndarray]]:
     lens = np.frombuffer(buf, dtype=np.uint16, count=n, offset=off)
     off += 2 * n
     flat = np.frombuffer(buf, dtype=np.int32, count=int(lens.sum()), offset=off).copy()
-    return tag, req_id, np.split(flat, np.cumsum(lens[:-1], dtype=np.int64)) if n else []
+    # plain slices (views of the one copy): np.split costs ~3 us per piece (array_split +
+    # swapaxes per sub-array) on the GPU feeder's loop
+    ends = np.cumsum(lens, dtype=np.int64).tolist()
+    return tag, req_id, [flat[a:b] for a, b in zip([0] + ends[:-1], ends)]
 
 
 def pack_error(req_id: int, msg: str) -> bytes:

@@ -200,12 +200,16 @@ def latest_checkpoint(ckpt_dir: Optional[str]) -> Optional[Path]:
     return cks[-1] if cks else None
 
 
-def _save_checkpoint(ckpt_dir: str, step: int, w: ExtractorWeights, opt, rng: random.Random) -> Path:
+def _save_checkpoint(ckpt_dir: str, step: int, w: ExtractorWeights, opt, rng: random.Random,
+                     ema_params=None) -> Path:
     os.makedirs(ckpt_dir, exist_ok=True)
     path = Path(ckpt_dir) / f"step-{step:07d}.pt"
     tmp = path.with_suffix(".tmp")
-    torch.save({"step": step, "weights": {k: v.detach().cpu() for k, v in w.state_dict().items()},
-                "opt": opt.state_dict(), "rng": rng.getstate(), "model": w.cfg.name}, tmp)
+    state = {"step": step, "weights": {k: v.detach().cpu() for k, v in w.state_dict().items()},
+             "opt": opt.state_dict(), "rng": rng.getstate(), "model": w.cfg.name}
+    if ema_params is not None:  # the running average is training state too (exact resume)
+        state["ema"] = [e.detach().cpu() for e in ema_params]
+    torch.save(state, tmp)
     os.replace(tmp, path)  # atomic: a crash never leaves a half-written "latest"
     return path
 
@@ -286,6 +290,8 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
                 v.copy_(state["weights"][k])
         opt.load_state_dict(state["opt"])
         start = int(state["step"])
+        if "ema" in state:
+            ema_params = [e.to(p.device) for e, p in zip(state["ema"], params)]
         if world == 1:
             rng.setstate(_as_rng_state(state["rng"]))
         else:  # rank 0's stream was saved; the others re-derive theirs deterministically
@@ -326,7 +332,7 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
         if on_eval is not None and cfg.eval_every and done % cfg.eval_every == 0 and done < cfg.steps:
             on_eval(done, to_serving(_with_ema(w, ema_params), mcfg))
         if cfg.ckpt_dir and rank == 0 and (done == cfg.steps or (cfg.ckpt_every and done % cfg.ckpt_every == 0)):
-            _save_checkpoint(cfg.ckpt_dir, done, w, opt, rng)
+            _save_checkpoint(cfg.ckpt_dir, done, w, opt, rng, ema_params)
     return to_serving(_with_ema(w, ema_params), mcfg)
 
 

@@ -31,7 +31,7 @@ from typing import Any, Dict, List, Optional, Sequence
 
 from ..models.domain import PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
 from ..obs.errors import sentry_capture
-from ..obs.metrics import GEMINI_LATENCY
+from ..obs.metrics import GEMINI_LATENCY, observe_many
 from ..runtime.errors import TransientError
 from .backends.base import BackendError, ParserBackend
 from .cache import MemoryKV, ResponseCache, cache_key
@@ -194,7 +194,5 @@ class ParsePipeline:
         # parse_sms_llm (worker.py:130-133, metrics.py:48-53): _count == messages
         # parsed.  The value is the latency each message experienced — the wall time
         # of the batched parse it was part of.
-        dt = time.perf_counter() - t_start
-        for _ in range(n):
-            GEMINI_LATENCY.observe(dt)
+        observe_many(GEMINI_LATENCY, time.perf_counter() - t_start, n)
         return results  # type: ignore[return-value]

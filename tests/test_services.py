@@ -659,3 +659,27 @@ def test_engine_server_refuses_random_weights(tmp_path, monkeypatch):
         resolve_checkpoint("smollm-135m")
     assert resolve_checkpoint("smollm-135m", random_init=True) is None
     assert resolve_checkpoint("small").endswith("extractor-small.safetensors")  # bundled
+
+
+def test_observe_many_equals_repeated_observe():
+    """One latency per message, recorded in O(1) per batch: the exported samples equal
+    n observe() calls (the reference times every message, worker.py:130-133)."""
+    from prometheus_client import CollectorRegistry, Histogram, Summary
+
+    from smsgate_amd.obs.metrics import observe_many
+
+    reg = CollectorRegistry()
+    h1, h2 = (Histogram(f"h{i}_seconds", "x", registry=reg, buckets=(0.001, 0.01, 0.1, 1)) for i in (1, 2))
+    s1, s2 = (Summary(f"s{i}_seconds", "x", registry=reg) for i in (1, 2))
+    for v, n in ((0.005, 7), (0.1, 3), (5.0, 2), (0.0001, 4), (0.01, 1)):
+        for _ in range(n):
+            h1.observe(v)
+            s1.observe(v)
+        observe_many(h2, v, n)
+        observe_many(s2, v, n)
+
+    def samples(m):
+        return [(x.name.split("_", 1)[1], x.labels, round(x.value, 9)) for x in m.collect()[0].samples
+                if not x.name.endswith("created")]
+
+    assert samples(h1) == samples(h2) and samples(s1) == samples(s2)

@@ -90,8 +90,12 @@ def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: in
         if i in spec or not t:
             continue
         # a byte-level piece of a multi-byte character decodes to U+FFFD: it is inside a
-        # word (Cyrillic letters), never a word boundary
-        out[i] = (TOK_STARTS_ALNUM if (t[0].isalnum() or t[0] == "\ufffd") else 0) | \
+        # word (Cyrillic letters), never a word boundary.  A token that opens with a
+        # number's inner separator followed by a digit (".58", ",000", ":23") continues
+        # the number before it like a letter continues a word: a value can neither start
+        # there ("657.58" -> "0.58") nor end just before it ("657" of "657.58")
+        starts = t[0].isalnum() or t[0] == "\ufffd" or (len(t) > 1 and t[0] in ".,:" and t[1].isdigit())
+        out[i] = (TOK_STARTS_ALNUM if starts else 0) | \
             (TOK_ENDS_ALNUM if (t[-1].isalnum() or t[-1] == "\ufffd") else 0)
     return out
 

@@ -637,15 +637,37 @@ def _proc_layout(r: random.Random, lang: str) -> Tuple[Tuple[str, ...], bool]:
             return tuple(order), multi
 
 
+_FILLER_LETTERS = {"en": "abcdefghiklmnoprstuvwy", "tr": "abdeghiklmnoprstuvyz",
+                   "ru": "абвгдеийклмнопрстуфхчшыя"}
+
+
+def _filler(r: random.Random, lang: str) -> str:
+    """One or two pseudo-words: a connector phrase the extractor has never seen
+    ("na summu", "spent on card" in a new layout).  Inserted before values so that the
+    model learns to read an unknown phrase as filler, not as a field."""
+    a = _FILLER_LETTERS[lang]
+    return " ".join("".join(r.choice(a) for _ in range(r.randint(2, 6))) for _ in range(r.randint(1, 2)))
+
+
 def _proc_render(c: "_Ctx") -> str:
     r, lang = c.r, c.fam.lang
     P = _PROC_POOLS[lang]
     order, multi = _proc_layout(r, lang)
     labelled = r.random() < 0.5  # "Label: value" style (else mostly bare values / prepositions)
     colon = r.choice((": ", ": ", " ", ":"))
+    # this message carries up to two unknown connector phrases (bounded: random Cyrillic
+    # letters cost a token each, and the body must stay inside the 128-token prompt)
+    fills = [2 if r.random() < 0.4 else 0]
+
+    def filler() -> str:
+        fills[0] -= 1
+        return _filler(r, lang)
+
+    def want_fill(p: float) -> bool:
+        return fills[0] > 0 and r.random() < p
 
     def lab(pool: Sequence[str]) -> str:
-        return r.choice(pool) + colon
+        return r.choice(pool) + colon + (filler() + " " if want_fill(0.3) else "")
 
     segs: List[str] = []
     head = ""
@@ -658,7 +680,11 @@ def _proc_render(c: "_Ctx") -> str:
             v = c.AMT()
             if r.random() < 0.15:  # a debit written as a negative amount ("-52.00 USD")
                 v = "-" + v
-            segs.append(lab(P["amt"]) + v if (labelled or r.random() < 0.2) else v)
+            if labelled or r.random() < 0.2:
+                v = lab(P["amt"]) + v
+            elif want_fill(0.6):
+                v = filler() + " " + v
+            segs.append(v)
         elif seg == "CARD":
             v = c.CARD()
             segs.append(lab(P["card"]) + v if (labelled or r.random() < 0.7) else v)
@@ -703,6 +729,8 @@ def _proc_render(c: "_Ctx") -> str:
                 place = f"{m}, {city}" + (f", {addr}" if addr else "")
             if r.random() < 0.3:
                 place = r.choice(P["at"]) + " " + place
+            if want_fill(0.4):
+                place = filler() + " " + place
             segs.append(place)
     if multi:
         body = "\n".join(([head] if head else []) + segs)
@@ -713,6 +741,8 @@ def _proc_render(c: "_Ctx") -> str:
             body = segs[0] + "".join((sep if r.random() < 0.5 else r.choice(seps)) + x for x in segs[1:])
         else:
             body = sep.join(segs)
+        if head and want_fill(0.4):
+            head += " " + filler()
         body = (head + r.choice((": ", " ", ". ")) if head else "") + body
     return body + (c.noise() if not multi else "")
 

@@ -63,6 +63,9 @@ def _args(argv=None):
     p.add_argument("--train-steps", type=int, default=3000)
     p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
     p.add_argument("--train-lr", type=float, default=1e-3)
+    p.add_argument("--answer-format", default="copy", choices=["copy", "span"],
+                   help="copy: each copied field written with the body's tokens (speculative prompt-lookup "
+                        "decoding); span: two pointers per field (serving/fsm.py build_span_fsm)")
     p.add_argument("--data-workers", type=int, default=12,
                    help="CPU processes building the training examples (started before the GPU is touched)")
     p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",
@@ -604,7 +607,7 @@ def _train_plan(args):
     # held-out exact 89.6 % vs 87.4 % for 60 k examples reused ~4x (profiles/r03_quality_probe.jsonl)
     tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
                      n_examples=args.train_steps * args.train_batch, log_every=200, data_parallel=False,
-                     families="train")
+                     families="train", answer_format=args.answer_format)
     src = open(ASSET, "rb").read() + open(synth.__file__, "rb").read()
     h = hashlib.sha256(repr((tc, EXTRACTOR_PROMPT, src)).encode(errors="ignore")).hexdigest()[:16]
     cache = args.weights_cache or os.path.join(tempfile.gettempdir(), f"smsgate-bench-w-{os.getpid()}")
@@ -622,7 +625,8 @@ def start_training_data(args, local: int):
         return None
     from smsgate_amd.models.train import ExamplePool
 
-    return ExamplePool(tc.n_examples, seed=tc.seed, families=tc.families, workers=args.data_workers)
+    return ExamplePool(tc.n_examples, seed=tc.seed, families=tc.families, workers=args.data_workers,
+                       answer_format=tc.answer_format)
 
 
 def acquire_weights(args, device: str, rank: int, world: int, pool=None):

@@ -31,13 +31,15 @@ def main():
     p.add_argument("--out", default="")
     p.add_argument("--jsonl", default="gpurun_out/family_probe.jsonl")
     p.add_argument("--tag", default="")
+    p.add_argument("--format", default="copy", choices=["copy", "span"])
     a = p.parse_args()
 
     from smsgate_amd.models.train import ExamplePool, TrainConfig, train_extractor
 
     n = a.examples or a.steps * a.batch
     t0 = time.perf_counter()
-    pool = ExamplePool(n, seed=a.seed, families=a.families, workers=a.workers)  # before the GPU is touched
+    pool = ExamplePool(n, seed=a.seed, families=a.families, workers=a.workers,  # before the GPU is touched
+                       answer_format=a.format)
 
     import torch
 
@@ -77,7 +79,7 @@ def main():
                         diff[k] = [str(v), str(want[k])]
             if diff and len(fails.setdefault(x.family, [])) < 2:
                 fails[x.family].append({"body": x.body[:160], "diff": diff})
-        rec = {"tag": a.tag, "model": a.model, "step": step, "train_s": round(time.perf_counter() - t0, 1),
+        rec = {"tag": a.tag, "model": a.model, "format": a.format, "step": step, "train_s": round(time.perf_counter() - t0, 1),
                "batch": a.batch, "lr": a.lr,
                "train_formats": {"exact": round(tr["exact"], 4), "by_family": tr["by_family"]},
                "legacy_mix_exact": round(leg["exact"], 4),
@@ -94,7 +96,8 @@ def main():
     data = pool.get()
     print(f"examples: {len(data)} in {time.perf_counter() - t0:.1f}s", flush=True)
     cfg = TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr, warmup=a.warmup, n_examples=n,
-                      seed=a.seed, log_every=200, eval_every=a.eval_every, families=a.families, data_parallel=False)
+                      seed=a.seed, log_every=200, eval_every=a.eval_every, families=a.families, data_parallel=False,
+                      answer_format=a.format)
     w = train_extractor(cfg, device="cuda", log=lambda s: print(s, flush=True), on_eval=evaluate, data=data)
     evaluate(a.steps, w)
     if a.out:

@@ -16,6 +16,7 @@ used to validate the HIP path and for training.
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 from dataclasses import asdict, dataclass
 from typing import Dict, Optional, Tuple
@@ -23,7 +24,8 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-__all__ = ["ExtractorConfig", "CONFIGS", "ExtractorWeights", "reference_forward", "count_params"]
+__all__ = ["ExtractorConfig", "CONFIGS", "ExtractorWeights", "reference_forward", "count_params", "span_config",
+           "SPAN_PTR0"]
 
 
 @dataclass(frozen=True)
@@ -39,6 +41,10 @@ class ExtractorConfig:
     rope_theta: float = 100000.0
     eps: float = 1e-5
     init_std: float = 0.02
+    # > 0: the span-pointer answer format (serving/fsm.py build_span_fsm) -- embedding
+    # rows ptr0 .. ptr0 + span_positions - 1 are the pointer tokens, and row ptr0 + j is
+    # added to the input of prompt position j
+    span_positions: int = 0
 
     @property
     def qkv_out(self) -> int:
@@ -60,6 +66,17 @@ CONFIGS: Dict[str, ExtractorConfig] = {
     "smollm-360m": ExtractorConfig(name="smollm-360m", hidden=960, layers=32, heads=15, kv_heads=5, head_dim=64,
                                    inter=2560),
 }
+
+
+# first pointer id of the span format: the tokenizer's 8 192 ids rounded to the lm_head tile
+SPAN_PTR0 = 8192
+
+
+def span_config(cfg: ExtractorConfig, positions: int = 130) -> ExtractorConfig:
+    """``cfg`` for the span-pointer format: the embedding must hold the pointer rows
+    (SmolLM2's 49 152 rows already do; the 8 192-row small models grow by 192)."""
+    vocab = max(cfg.vocab, -(-(SPAN_PTR0 + positions) // 64) * 64)
+    return dataclasses.replace(cfg, vocab=vocab, span_positions=positions)
 
 
 def count_params(cfg: ExtractorConfig) -> int:
@@ -107,8 +124,13 @@ class ExtractorWeights(torch.nn.Module):
 
     @classmethod
     def load(cls, path: str, cfg: ExtractorConfig, device=None, dtype=torch.bfloat16) -> "ExtractorWeights":
+        from safetensors import safe_open
         from safetensors.torch import load_file
 
+        with safe_open(path, framework="pt") as fh:  # a span-format checkpoint says so in its metadata
+            meta = fh.metadata() or {}
+        if int(meta.get("span_positions", "0") or 0) > 0:
+            cfg = dataclasses.replace(cfg, vocab=int(meta["vocab"]), span_positions=int(meta["span_positions"]))
         w = cls(cfg, device="meta" if device is None else device, dtype=dtype, seed=None)
         sd = load_file(path, device=str(device) if device is not None else "cpu")
         w.load_state_dict({k: v.to(dtype) for k, v in sd.items()}, assign=True)
@@ -134,15 +156,19 @@ def _rms(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 
 
 def reference_forward(w: ExtractorWeights, ids: torch.Tensor, compute_dtype=torch.float32,
-                      return_hidden: bool = False) -> torch.Tensor:
+                      return_hidden: bool = False, add_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Full-sequence causal forward. ``ids``: [B, T] → logits [B, T, V] (fp32).
 
     Plain PyTorch (SDPA attention); differentiable, so it is also the training
-    forward.
+    forward.  ``add_ids`` [B, T] (span format): a second embedding row added to each
+    input (the position's pointer row; -1 = none).
     """
     cfg = w.cfg
     B, T = ids.shape
-    x = F.embedding(ids, w.embed).to(compute_dtype)
+    x = F.embedding(ids, w.embed)
+    if add_ids is not None:
+        x = x + F.embedding(add_ids.clamp(min=0), w.embed) * (add_ids >= 0).unsqueeze(-1).to(x.dtype)
+    x = x.to(compute_dtype)
     cos, sin = _rope_tables(T, cfg.head_dim, cfg.rope_theta, ids.device)  # once, not per layer
     for i in range(cfg.layers):
         h = _rms(x, w.ln1[i].to(compute_dtype), cfg.eps)

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import functools
 from pathlib import Path
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 __all__ = ["ExtractorTokenizer", "SPECIALS", "load_tokenizer", "train_tokenizer", "ASSET", "model_text"]
 
@@ -115,12 +115,20 @@ class ExtractorTokenizer:
         an exact draft for speculative decoding (:mod:`smsgate_amd.serving.draft`)."""
         if not value:
             return []
+        sp = self.value_span(value, body, ids, offsets)
+        return list(ids[sp[0]:sp[1] + 1]) if sp is not None else self.encode(value)
+
+    def value_span(self, value: str, body: str, ids: Sequence[int],
+                   offsets: Sequence[Tuple[int, int]]) -> Optional[Tuple[int, int]]:
+        """``(first, last)`` body token index of the first word-aligned occurrence of
+        ``value`` whose tokens decode back to it (:meth:`value_span_ids`; the span
+        format points at these two positions), or None."""
         body, value = model_text(body), model_text(value)  # the offsets index the model text
         start = 0
         while True:
             a = body.find(value, start)
             if a < 0:
-                return self.encode(value)
+                return None
             z = a + len(value)
             # an occurrence inside a longer word is not the value ("AM" in "AMERIABANK"
             # vs the city ", AM&#10;"): values are copied at word boundaries (the copy
@@ -134,9 +142,8 @@ class ExtractorTokenizer:
             # tokens (Cyrillic, symbols) gives each piece the character's whole span
             k1 = max((k for k, (s, e) in enumerate(offsets) if e == z), default=None)
             if k0 is not None and k1 is not None and k1 >= k0 and body[offsets[k0][0]:a].strip() == "":
-                span = list(ids[k0:k1 + 1])
-                if self.decode(span).strip() == value:
-                    return span
+                if self.decode(list(ids[k0:k1 + 1])).strip() == value:
+                    return k0, k1
             start = a + 1
 
     def decode(self, ids: Sequence[int]) -> str:

@@ -47,10 +47,10 @@ import torch.nn.functional as F
 
 from ..parse.schema import EXTRACTOR_PROMPT
 from ..parse.text import normalize_body
-from .extractor import CONFIGS, ExtractorWeights, reference_forward
+from .extractor import CONFIGS, SPAN_PTR0, ExtractorWeights, reference_forward, span_config
 from .tokenizer import ExtractorTokenizer, load_tokenizer
 
-__all__ = ["TrainConfig", "answer_tokens", "make_examples", "ExamplePool", "train_extractor", "field_accuracy",
+__all__ = ["TrainConfig", "answer_tokens", "answer_span_tokens", "answer_fsm", "make_examples", "ExamplePool", "train_extractor", "field_accuracy",
            "latest_checkpoint", "to_serving"]
 
 
@@ -83,6 +83,9 @@ class TrainConfig:
     ema_start: int = 0  # first step the average includes (0 = warmup end)
     data_parallel: bool = True  # under torch.distributed: all-reduce gradients (False: train this rank alone)
     eval_every: int = 0  # call on_eval(step, serving weights) every N steps (0 = never)
+    # "copy": every copied value written with the body's own tokens; "span": as two
+    # pointers to its first and last body token (serving/fsm.py build_span_fsm)
+    answer_format: str = "copy"
 
 
 def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]],
@@ -111,10 +114,52 @@ def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]]
     return ids if state == fsm.done_state else None
 
 
+def answer_span_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]], body: str, body_enc,
+                       msg_len: int) -> Optional[List[int]]:
+    """Span-format answer ids (enum tokens + <sep>; per copied field two pointers
+    ``ptr0 + first``, ``ptr0 + last`` or <sep> when empty), or None when a value is no
+    word-aligned body span inside the (truncated) message, or the FSM / copy rules
+    reject it.  ``msg_len``: the message's ids incl. the closing <ans>."""
+    ids: List[int] = []
+    msg = list(body_enc[0][: msg_len - 1]) + [tok.ans]
+    for f in fsm.fields:
+        v = answer.get(f.name) or ""
+        if f.kind == "enum":
+            ids += (tok.encode(v) if v else []) + [tok.sep]
+        elif not v:
+            ids.append(tok.sep)
+        else:
+            sp = tok.value_span(v, body, body_enc[0], body_enc[1])
+            if sp is None or sp[1] >= msg_len - 1:
+                return None
+            ids += [fsm.ptr0 + sp[0], fsm.ptr0 + sp[1]]
+    state, prev = fsm.start_state, msg[-1]
+    for t in ids:
+        if not fsm.copy_mask_host(state, prev, msg)[t]:
+            return None
+        state, prev = fsm.step_host(state, t), t
+    return ids if state == fsm.done_state else None
+
+
+def answer_fsm(tok: ExtractorTokenizer, fmt: str = "copy", max_body: int = 128):
+    """The schema FSM the training targets are written for (vocabulary trimmed to the
+    tokenizer's ids, plus the pointer ids in span format)."""
+    from ..serving.fsm import build_fsm, build_span_fsm, span_positions
+
+    v_tok = (tok.vocab_size + 63) // 64 * 64
+    if fmt == "span":
+        assert v_tok == SPAN_PTR0, "the span format's pointer ids follow the 8 192-id tokenizer"
+        return build_span_fsm(tok, v_tok, span_positions(max_body))
+    if fmt != "copy":
+        raise ValueError(f"answer format {fmt!r}: copy | span")
+    return build_fsm(tok, v_tok)
+
+
 def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
                   max_body: int = 128, vocab_name: str = "train",
                   families: Optional[str] = "train") -> List[Tuple[List[int], List[int]]]:
-    """``(message ids, answer ids)`` pairs (prefix excluded: it is shared)."""
+    """``(message ids, answer ids)`` pairs (prefix excluded: it is shared); span-format
+    answers when ``fsm`` is a span FSM."""
     from ..utils.synth import HELDOUT_FAMILIES, generate, family_names
 
     if families is not None:
@@ -126,7 +171,7 @@ def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
     msgs = tok.message_ids(bodies, max_body)
     encs = tok.encode_offsets(bodies)
     for m, s, b, e in zip(msgs, items, bodies, encs):
-        a = answer_tokens(tok, fsm, s.answer, b, e)
+        a = answer_span_tokens(tok, fsm, s.answer, b, e, len(m)) if fsm.span else answer_tokens(tok, fsm, s.answer, b, e)
         if a is not None:
             out.append((m, a))
     return out
@@ -135,12 +180,10 @@ def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
 _POOL_STATE: Dict[str, object] = {}
 
 
-def _pool_init(tok_path: str) -> None:
-    from ..serving.fsm import build_fsm
-
+def _pool_init(tok_path: str, fmt: str = "copy", max_body: int = 128) -> None:
     tok = ExtractorTokenizer(Path(tok_path))
     _POOL_STATE["tok"] = tok
-    _POOL_STATE["fsm"] = build_fsm(tok, (tok.vocab_size + 63) // 64 * 64)
+    _POOL_STATE["fsm"] = answer_fsm(tok, fmt, max_body)
 
 
 def _pool_chunk(args) -> List[Tuple[List[int], List[int]]]:
@@ -159,7 +202,7 @@ class ExamplePool:
 
     def __init__(self, n: int, seed: int = 0, max_body: int = 128, vocab_name: str = "train",
                  families: Optional[str] = "train", workers: int = 8, chunk: int = 4096,
-                 tok_path: Optional[str] = None) -> None:
+                 tok_path: Optional[str] = None, answer_format: str = "copy") -> None:
         import multiprocessing as mp
 
         from .tokenizer import ASSET
@@ -168,7 +211,7 @@ class ExamplePool:
                 for k in range((n + chunk - 1) // chunk)]
         self.n = n
         self._pool = mp.get_context("spawn").Pool(max(1, min(workers, len(jobs))), initializer=_pool_init,
-                                                  initargs=(str(tok_path or ASSET),))
+                                                  initargs=(str(tok_path or ASSET), answer_format, max_body))
         self._res = self._pool.map_async(_pool_chunk, jobs)
 
     def get(self, timeout: float = 1800.0) -> List[Tuple[List[int], List[int]]]:
@@ -181,16 +224,22 @@ class ExamplePool:
 
 
 def _batch(prefix: List[int], exs: Sequence[Tuple[List[int], List[int]]], pad: int,
-           device) -> Tuple[torch.Tensor, torch.Tensor]:
+           device, ptr0: int = -1) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+    """ids, labels and (span format, ``ptr0 >= 0``) the pointer row added to each
+    message position's input (-1 elsewhere)."""
     seqs = [prefix + m + a for m, a in exs]
     T = max(len(s) for s in seqs)
     ids = torch.full((len(seqs), T), pad, dtype=torch.long)
     labels = torch.full((len(seqs), T), -100, dtype=torch.long)
+    add = torch.full((len(seqs), T), -1, dtype=torch.long) if ptr0 >= 0 else None
+    P = len(prefix)
     for i, ((m, a), s) in enumerate(zip(exs, seqs)):
         ids[i, : len(s)] = torch.tensor(s)
-        start = len(prefix) + len(m)  # position of the first answer token
+        start = P + len(m)  # position of the first answer token
         labels[i, start - 1: start - 1 + len(a)] = torch.tensor(a)  # predicted from the previous position
-    return ids.to(device), labels.to(device)
+        if add is not None:
+            add[i, P:start] = torch.arange(ptr0, ptr0 + len(m))
+    return ids.to(device), labels.to(device), (add.to(device) if add is not None else None)
 
 
 def latest_checkpoint(ckpt_dir: Optional[str]) -> Optional[Path]:
@@ -241,7 +290,6 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     import torch.distributed as dist
 
     from ..parallel.ddp import GradBuckets
-    from ..serving.fsm import build_fsm
 
     ddp = dist.is_initialized() and cfg.data_parallel
     rank = dist.get_rank() if ddp else 0
@@ -249,8 +297,10 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
 
     tok = tok or load_tokenizer()
     mcfg = CONFIGS[cfg.model]
-    v_dec = min(mcfg.vocab, (tok.vocab_size + 63) // 64 * 64)
-    fsm = build_fsm(tok, v_dec)
+    fsm = answer_fsm(tok, cfg.answer_format, cfg.max_body_tokens)
+    if fsm.span:
+        mcfg = span_config(mcfg, fsm.n_pos)
+    v_dec = min(mcfg.vocab, fsm.vocab)
     t0 = time.perf_counter()
     if data is None:
         data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens, cfg.vocab_name, cfg.families)
@@ -303,9 +353,9 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     for step in range(start, cfg.steps):
         for g in opt.param_groups:
             g["lr"] = lr_at(step)
-        ids, labels = _batch(prefix, rng.sample(data, cfg.batch), tok.pad, device)
+        ids, labels, add = _batch(prefix, rng.sample(data, cfg.batch), tok.pad, device, fsm.ptr0)
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=str(device).startswith("cuda")):
-            h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True)
+            h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True, add_ids=add)
             sel = labels.view(-1) >= 0
             hs = h.reshape(-1, h.shape[-1])[sel]
             logits = hs @ w.embed[:v_dec].t()

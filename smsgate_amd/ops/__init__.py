@@ -108,7 +108,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_embed_rows.argtypes = [_ip, _vp, _vp, _c_int, _c_int, _c_int, _vp]
     lib.sg_embed_rows.restype = _c_int
     lib.sg_sparse_argmax.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _vp, _vp, _c_int, _vp, _c_int, _c_float,
-                                     _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp, _vp]
+                                     _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_int, _vp, _vp]
     lib.sg_sparse_argmax.restype = _c_int
     lib.sg_gemm_probe.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]
     lib.sg_gemm_probe.restype = _c_int
@@ -131,6 +131,9 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_spec_verify_keys.restype = _c_int
     lib.sg_fsm_commit.argtypes = [_vp, _ip] + fsm_t + [_c_int] * 3 + [_ip] * 6 + [_c_int, _c_int, _vp]
     lib.sg_fsm_commit.restype = _c_int
+    lib.sg_span_commit.argtypes = [_vp, _ip] + fsm_t + [_c_int] * 3 + [_ip] * 4 + [_c_int, _c_int] + [_ip] * 6 + \
+        [_c_int, _c_int, _vp]
+    lib.sg_span_commit.restype = _c_int
     lib.sg_gemm_argmax.argtypes = [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_float, _c_int, _c_int, _ip, _ip, _vp,
                                    _vp, _vp, _c_int, _ip, _vp, _vp]
     lib.sg_gemm_argmax.restype = _c_int
@@ -676,6 +679,8 @@ def copy_masks(fsm, row_state: torch.Tensor, prev_tok: torch.Tensor, row_slot: t
     body of row ``r`` is ``body_buf[row_slot[r], :body_len[row_slot[r]]]``.  Rows in
     other states are not written (the consumers only read copy rows)."""
     n = row_state.numel() if n is None else n
+    if fsm.span:
+        raise ValueError("copy_masks: the span format is decoded by sparse_argmax only")
     S1, LB = body_buf.shape
     for name, t in (("row_state", row_state), ("prev_tok", prev_tok), ("row_slot", row_slot)):
         _req(t, torch.int32, name)
@@ -867,7 +872,8 @@ def sparse_argmax(h: torch.Tensor, w: torch.Tensor, row_state: torch.Tensor, fsm
     _check(load_library().sg_sparse_argmax(_p(fsm.masks), _p(fsm.state_mask), fsm.sep_token, fsm.vocab, ck,
                                            _p(fsm.tok_flags_t), _p(h), h.stride(0), _p(w), H, float(eps),
                                            _p(row_state), _p(prev_tok), _p(row_slot), _p(body_buf),
-                                           _p(body_len), body_buf.shape[1], n, _p(best), _stream()),
+                                           _p(body_len), body_buf.shape[1], n, fsm.ptr0 if fsm.span else -1,
+                                           fsm.n_pos if fsm.span else 0, _p(best), _stream()),
            "sparse_argmax")
     return best
 
@@ -890,6 +896,30 @@ def fsm_commit(best: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tenso
     _check(load_library().sg_fsm_commit(
         _p(best), _p(row_map), *_fsm_args(fsm), fsm.sep_token, fsm.done_state, fsm.vocab, _p(state), _p(tok_io),
         _p(out_buf), _p(out_len), _p(done), _p(pos), out_buf.shape[1], B, _stream()), "fsm_commit")
+
+
+def span_commit(best: torch.Tensor, fsm, state: torch.Tensor, tok_io: torch.Tensor, out_buf: torch.Tensor,
+                out_len: torch.Tensor, done: torch.Tensor, pos: torch.Tensor, row_slot: torch.Tensor,
+                body_buf: torch.Tensor, body_len: torch.Tensor, B: int, row_map: Optional[torch.Tensor] = None) -> None:
+    """:func:`fsm_commit` of the span-pointer format (``span_commit_kernel``): the FSM
+    step from the arg-max keys, and the answer written in COPY format -- an end
+    pointer appends its span's body tokens (``body_buf[row_slot[i]]``) and <sep>.
+    :meth:`~smsgate_amd.serving.fsm.SchemaFSM.expand_span_answer` is the reference."""
+    if not fsm.span:
+        raise ValueError("span_commit: not a span-format FSM")
+    if best.dtype != torch.int64 or best.numel() < B or (row_map is not None and row_map.numel() < B):
+        raise ValueError("span_commit: bad best / row_map")
+    if row_map is None and state.numel() < B:
+        raise ValueError("span_commit: state smaller than B")
+    _req(row_slot, torch.int32, "row_slot")
+    _req(body_buf, torch.int32, "body_buf")
+    _req(body_len, torch.int32, "body_len")
+    if row_slot.numel() < B or body_len.numel() != body_buf.shape[0]:
+        raise ValueError("span_commit: bad row_slot / body_len")
+    _check(load_library().sg_span_commit(
+        _p(best), _p(row_map), *_fsm_args(fsm), fsm.sep_token, fsm.done_state, fsm.vocab, _p(fsm.copy_kind_t),
+        _p(row_slot), _p(body_buf), _p(body_len), body_buf.shape[1], fsm.ptr0, _p(state), _p(tok_io), _p(out_buf),
+        _p(out_len), _p(done), _p(pos), out_buf.shape[1], B, _stream()), "span_commit")
 
 
 def spec_verify_keys(best: torch.Tensor, fsm, state: torch.Tensor, tok_buf: torch.Tensor, out_buf: torch.Tensor,

@@ -382,6 +382,48 @@ __global__ void __launch_bounds__(256) fsm_commit_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// span-pointer format: fsm_commit that writes the answer in COPY format.  A start
+// pointer is only held (tok_io: the next step's input, and the end state's `prev`);
+// the end pointer appends the body tokens start..end and <sep>; <sep> and enum
+// tokens are appended as they are.  So out_buf / out_len look exactly like a
+// copy-format decode's and everything downstream (harvest, remote clients'
+// detokenisation) is unchanged.  Key row i updates state row row_map[i] (or i);
+// row_slot[i] is that row's KV slot (its prompt in body_buf).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) span_commit_kernel(
+    FsmTables fsm, const int* __restrict__ copy_kind, const unsigned long long* __restrict__ best,
+    const int* __restrict__ row_map, const int* __restrict__ row_slot, const int* __restrict__ body_buf,
+    const int* __restrict__ body_len, int LB, int ptr0, int* __restrict__ state, int* __restrict__ tok_io,
+    int* __restrict__ out_buf, int* __restrict__ out_len, int* __restrict__ done, int* __restrict__ pos,
+    int max_out, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const int b = row_map ? row_map[i] : i;
+  if (done[b]) return;
+  const int s = state[b];
+  const int tok = key_token(best[i], fsm.sep_token);
+  const int ns = fsm_next(fsm, s, tok);
+  const int k8 = copy_kind[s] & 0xff;
+  int len = out_len[b];
+  int* ob = out_buf + (size_t)b * max_out;
+  if (k8 == 4) {
+    const int sl = row_slot[i];
+    const int nb = min(body_len[sl], LB) - 1;
+    const int* body = body_buf + (size_t)sl * LB;
+    const int s0 = max(0, tok_io[b] - ptr0), e = min(tok - ptr0, nb - 1);
+    for (int j = s0; j <= e && len < max_out - 1; ++j) ob[len++] = body[j];
+    if (len < max_out) ob[len++] = fsm.sep_token;
+  } else if (!(k8 == 3 && tok != fsm.sep_token)) {
+    if (len < max_out) ob[len++] = tok;
+  }
+  out_len[b] = len;
+  tok_io[b] = tok;
+  state[b] = ns < 0 ? fsm.done_state : ns;
+  if (ns < 0 || ns == fsm.done_state) done[b] = 1;
+  else pos[b] = pos[b] + 1;
+}
+
+// ---------------------------------------------------------------------------
 // copy-constrained decoding (serving/fsm.py COPY_START / COPY_NEXT states): the
 // per-row allowed-token mask = the state's schema mask AND the tokens the row may
 // copy from its own SMS body.  A value starts at a word boundary of the body (any
@@ -572,7 +614,7 @@ __global__ void __launch_bounds__(256) sparse_argmax_kernel(
     FsmTables fsm, const int* __restrict__ copy_kind, const uint8_t* __restrict__ tok_flags,
     const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ W, int H, float eps,
     const int* __restrict__ row_state, const int* __restrict__ prev_tok, const int* __restrict__ row_slot,
-    const int* __restrict__ body_buf, const int* __restrict__ body_len, int LB, int n,
+    const int* __restrict__ body_buf, const int* __restrict__ body_len, int LB, int n, int ptr0, int n_pos,
     unsigned long long* __restrict__ best) {
   __shared__ uint32_t bits[4][COPY_MAX_WORDS];
   __shared__ int cand[4][SPARSE_MAX_CAND];
@@ -598,22 +640,57 @@ __global__ void __launch_bounds__(256) sparse_argmax_kernel(
     const int prev = prev_tok[r];
     const int sep = fsm.sep_token;
     auto flags = [&](int t) -> int { return (t >= 0 && t < fsm.V) ? (int)tok_flags[t] : 0; };
-    for (int j = lane; j < bl; j += 64) {
-      const int t = body[j];
-      int c = -1;
-      bool end_ok = false;
-      if (kind == 1) {
+    const int k8 = kind & 0xff, cls = (kind >> 16) & 0xff;
+    if (k8 == 3) {
+      // span start (serving/fsm.py build_span_fsm): pointer ptr0 + j to a body token at a
+      // word boundary and in the field's class; never the closing <ans> (position bl-1)
+      const int np = min(bl - 1, n_pos);
+      for (int j = lane; j < np; j += 64) {
+        const int t = body[j];
         const bool glued = j > 0 && (flags(body[j - 1]) & 2) && (flags(t) & 1);
-        if (!glued) c = t;
-      } else if (t == prev) {
-        const int nx = j + 1 < bl ? body[j + 1] : -1;
-        c = nx;
-        end_ok = nx < 0 || !((flags(t) & 2) && (flags(nx) & 1));
+        if (!glued && (cls == 0 || (flags(t) & cls))) {
+          const int c = ptr0 + j;
+          if (c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
+        }
       }
-      if (c >= 0 && c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
-      if (end_ok) atomicOr(&b[sep >> 5], 1u << (sep & 31));
+      if (lane == 0) atomicOr(&b[sep >> 5], 1u << (sep & 31));  // an empty value
+    } else if (k8 == 4) {
+      // span end: lane l is end position e = start + l (caps <= 64); every token from the
+      // start to e in the class (the first out-of-class token by one wave ballot), e
+      // within the cap and followed by a word boundary
+      const int cap = (kind >> 8) & 0xff, nb = bl - 1, s0 = prev - ptr0;
+      if (s0 >= 0 && s0 < nb) {  // row-uniform
+        const int e = s0 + lane;
+        const bool inr = lane < cap && e < nb;
+        const int t = inr ? body[e] : 0;
+        const bool inc = inr && (cls == 0 || (flags(t) & cls));
+        const unsigned long long bad = __ballot(!inc);
+        const int first_bad = bad ? __builtin_ctzll(bad) : 64;
+        if (inr && lane < first_bad) {
+          const int nx = e + 1 < nb ? body[e + 1] : -1;
+          const int c = ptr0 + e;
+          if ((nx < 0 || !((flags(t) & 2) && (flags(nx) & 1))) && c < fsm.V)
+            atomicOr(&b[c >> 5], 1u << (c & 31));
+        }
+      }
+    } else {
+      for (int j = lane; j < bl; j += 64) {
+        const int t = body[j];
+        int c = -1;
+        bool end_ok = false;
+        if (k8 == 1) {
+          const bool glued = j > 0 && (flags(body[j - 1]) & 2) && (flags(t) & 1);
+          if (!glued) c = t;
+        } else if (t == prev) {
+          const int nx = j + 1 < bl ? body[j + 1] : -1;
+          c = nx;
+          end_ok = nx < 0 || !((flags(t) & 2) && (flags(nx) & 1));
+        }
+        if (c >= 0 && c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
+        if (end_ok) atomicOr(&b[sep >> 5], 1u << (sep & 31));
+      }
+      if (k8 == 1 && lane == 0) atomicOr(&b[sep >> 5], 1u << (sep & 31));  // an empty value
     }
-    if (kind == 1 && lane == 0) atomicOr(&b[sep >> 5], 1u << (sep & 31));  // an empty value
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -765,15 +842,31 @@ int sg_fsm_commit(const void* best, const int* row_map, const void* masks, const
 int sg_sparse_argmax(const void* masks, const int* state_mask, int sep_token, int V, const int* copy_kind,
                      const void* tok_flags, const void* h, int ldh, const void* W, int H, float eps,
                      const int* row_state, const int* prev_tok, const int* row_slot, const int* body_buf,
-                     const int* body_len, int LB, int n, void* best, hipStream_t stream) {
+                     const int* body_len, int LB, int n, int ptr0, int n_pos, void* best, hipStream_t stream) {
   if (V % 32 || V / 32 > COPY_MAX_WORDS || LB <= 0 || LB >= SPARSE_MAX_CAND || sep_token < 0 || sep_token >= V ||
-      H % 64 || H / 64 > SPARSE_MAX_HL || ldh % 8 || (copy_kind && !tok_flags))
+      H % 64 || H / 64 > SPARSE_MAX_HL || ldh % 8 || (copy_kind && !tok_flags) ||
+      (n_pos > 0 && (ptr0 < 0 || ptr0 + n_pos > V || n_pos >= SPARSE_MAX_CAND)))
     return -1;
   if (n == 0) return 0;
   const FsmTables f = make_fsm(masks, state_mask, nullptr, nullptr, nullptr, nullptr, 0, sep_token, 0, V);
   hipLaunchKernelGGL(sparse_argmax_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, f, copy_kind,
                      (const uint8_t*)tok_flags, (const uint16_t*)h, ldh, (const uint16_t*)W, H, eps, row_state,
-                     prev_tok, row_slot, body_buf, body_len, LB, n, (unsigned long long*)best);
+                     prev_tok, row_slot, body_buf, body_len, LB, n, ptr0, n_pos, (unsigned long long*)best);
+  return (int)hipGetLastError();
+}
+
+// span-pointer commit (span_commit_kernel) for B key rows.
+int sg_span_commit(const void* best, const int* row_map, const void* masks, const int* state_mask,
+                   const int* next_sep, const int* next_tok, const int* enum_tok, const int* enum_next, int E,
+                   int sep_token, int done_state, int V, const int* copy_kind, const int* row_slot,
+                   const int* body_buf, const int* body_len, int LB, int ptr0, int* state, int* tok_io, int* out_buf,
+                   int* out_len, int* done, int* pos, int max_out, int B, hipStream_t stream) {
+  if (B == 0) return 0;
+  if (!copy_kind || !row_slot || !body_buf || !body_len || LB <= 0 || ptr0 < 0 || max_out <= 0) return -1;
+  const FsmTables f = make_fsm(masks, state_mask, next_sep, next_tok, enum_tok, enum_next, E, sep_token, done_state, V);
+  hipLaunchKernelGGL(span_commit_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, f, copy_kind,
+                     (const unsigned long long*)best, row_map, row_slot, body_buf, body_len, LB, ptr0, state, tok_io,
+                     out_buf, out_len, done, pos, max_out, B);
   return (int)hipGetLastError();
 }
 

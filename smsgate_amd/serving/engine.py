@@ -40,7 +40,7 @@ from .. import ops
 from ..models.extractor import ExtractorConfig, ExtractorWeights
 from ..models.tokenizer import ExtractorTokenizer
 from ..parse.schema import EXTRACTOR_PROMPT
-from .fsm import DEFAULT_FIELDS, FieldSpec, SchemaFSM, build_fsm
+from .fsm import DEFAULT_FIELDS, FieldSpec, SchemaFSM, build_fsm, build_span_fsm
 
 __all__ = ["EngineConfig", "ExtractionEngine", "EngineStats"]
 
@@ -248,6 +248,14 @@ class ExtractionEngine:
         # arg-max / Gumbel-max over allowed tokens is unchanged (exact, not an
         # approximation) and the projection is 6x smaller for the 49 152 vocab.
         self.V_dec = min(mc.vocab, _round_up(tokenizer.vocab_size, 64))
+        # span-pointer models (models/extractor.py span_config): the pointer ids follow the
+        # tokenizer's, and their rows are part of the lm_head
+        span_fsm = (build_span_fsm(tokenizer, self.V_dec, mc.span_positions, fields)
+                    if mc.span_positions > 0 else None)
+        if span_fsm is not None:
+            if mc.span_positions < ec.max_body_tokens + 2:
+                raise ValueError("span model: fewer pointer positions than prompt positions")
+            self.V_dec = span_fsm.vocab
         self.lm_head = self.w.embed[: self.V_dec]
         self.fused = ec.fused_gemm and self.V_dec % 64 == 0 and mc.hidden % 64 == 0 and mc.inter % 32 == 0
         if self.fused:
@@ -259,21 +267,28 @@ class ExtractionEngine:
             self.fw_gu = [ops.interleave_gate_up(ops.fold_norm(w.gate_up[i], w.ln2[i])) for i in range(mc.layers)]
             self.fw_down = [w.down[i].contiguous() for i in range(mc.layers)]
             self.fw_lm = ops.fold_norm(self.lm_head, w.ln_f)
-        self.fsm: SchemaFSM = build_fsm(tokenizer, self.V_dec, fields).to_device(self.device)
+        self.fsm: SchemaFSM = (span_fsm or build_fsm(tokenizer, self.V_dec, fields)).to_device(self.device)
+        self.span = self.fsm.span
         self.argmax = ec.lm_head_argmax and ec.temperature <= 0 and self.V_dec % 128 == 0
-        self.max_out = self.fsm.max_steps()
+        # out_buf holds the answer in copy format (a span answer is expanded by span_commit);
+        # the KV cache holds the decode steps (2 pointers per field instead of its tokens)
+        self.max_out = self.fsm.max_answer_tokens()
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)
         self.P0 = len(self.prefix_ids)
         self.P0pad = _round_up(self.P0, 32)
-        self.Lmax = _round_up(ec.max_body_tokens + 2 + self.max_out, 32)  # decode tiles are 32 keys
+        self.Lmax = _round_up(ec.max_body_tokens + 2 + self.fsm.max_steps(), 32)  # decode tiles are 32 keys
         if self.P0pad + self.Lmax > 512:
             raise ValueError("prefix + Lmax exceeds the decode kernel's context limit (512)")
         S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
         dev, bf = self.device, torch.bfloat16
-        self.spec = ec.spec_k > 0 and ec.temperature <= 0
-        self.copy = ec.copy_constrain and self.fsm.has_copy
+        # span answers have nothing to draft: one pointer per step
+        self.spec = ec.spec_k > 0 and ec.temperature <= 0 and not self.span
+        self.copy = (ec.copy_constrain or self.span) and self.fsm.has_copy
         self.sparse = (ec.sparse_argmax and self.copy and self.argmax and self.fused
                        and ops.sparse_argmax_ok(self.fsm))
+        if self.span and not self.sparse:
+            raise ValueError("span-format models decode greedily through the fused sparse arg-max "
+                             "(temperature 0, fused_gemm, lm_head_argmax, sparse_argmax)")
         if ec.spec_k > ops.SPEC_MAX_K:
             raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
         # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV
@@ -505,7 +520,10 @@ class ExtractionEngine:
         if kk is not None:
             self._copy_templates(kk, tsl, seq_slots)
         flat_d = self._stage.to_device(flat, dev)
-        x = F.embedding(flat_d, self.w.embed).contiguous()
+        x = F.embedding(flat_d, self.w.embed)
+        if self.span:  # prompt position j also carries pointer j's row
+            x = x + F.embedding(pos_d.long() + self.fsm.ptr0, self.w.embed)
+        x = x.contiguous()
         max_q = int(lens.max())
         if self.spec or self.copy:  # the rows' prompts: draft source and copy set
             self.body_buf[slot_d.long(), pos_d.long()] = flat_d.to(torch.int32)
@@ -561,8 +579,12 @@ class ExtractionEngine:
                                   seq_slot_d, self.body_buf, self.body_len, self.mc.eps)
             else:
                 self._argmax(last, self.start_states[:n], best, row_masks=cm)
-            ops.fsm_commit(best, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done, self.pos,
-                           n, row_map=rows_d)
+            if self.span:
+                ops.span_commit(best, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done,
+                                self.pos, seq_slot_d, self.body_buf, self.body_len, n, row_map=rows_d)
+            else:
+                ops.fsm_commit(best, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done,
+                               self.pos, n, row_map=rows_d)
             logits = None
         else:
             ops.fsm_sample(logits, self.fsm, self.state, self.tok_buf, self.out_buf, self.out_len, self.done,
@@ -683,8 +705,12 @@ class ExtractionEngine:
                                   self.body_len, self.mc.eps)
             else:
                 self._argmax(h, self.state[r0:r1], best, ss=self._fwd_ss if self.fused else None, row_masks=cm)
-            ops.fsm_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1], done,
-                           pos, B)
+            if self.span:
+                ops.span_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
+                                done, pos, slot, self.body_buf, self.body_len, B)
+            else:
+                ops.fsm_commit(best, self.fsm, self.state[r0:r1], tok, self.out_buf[r0:r1], self.out_len[r0:r1],
+                               done, pos, B)
             return best
         logits = self._logits(h)
         if sample:

@@ -29,8 +29,8 @@ import numpy as np
 from ..models.domain import CORE_FIELDS
 from ..parse.schema import TXN_TYPES
 
-__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm", "COPY_NONE", "COPY_START", "COPY_NEXT",
-           "TOK_STARTS_ALNUM", "TOK_ENDS_ALNUM", "token_flags"]
+__all__ = ["FieldSpec", "SchemaFSM", "DEFAULT_FIELDS", "build_fsm", "build_span_fsm", "COPY_NONE", "COPY_START",
+           "COPY_NEXT", "PTR_START", "PTR_END", "TOK_STARTS_ALNUM", "TOK_ENDS_ALNUM", "token_flags", "span_positions"]
 
 
 @dataclass(frozen=True)
@@ -75,17 +75,26 @@ DEFAULT_FIELDS: Tuple[FieldSpec, ...] = (
 )
 assert tuple(f.name for f in DEFAULT_FIELDS) == CORE_FIELDS
 
-# per-state copy kind (SchemaFSM.copy_kind)
-COPY_NONE, COPY_START, COPY_NEXT = 0, 1, 2
+# per-state copy kind (SchemaFSM.copy_kind; low byte).  The span-pointer format's end
+# state also carries the field's token cap (bits 8-15) and token-class bit (16-23)
+COPY_NONE, COPY_START, COPY_NEXT, PTR_START, PTR_END = 0, 1, 2, 3, 4
 # per-token flags (SchemaFSM.tok_flags): the token's text starts / ends with a letter or
 # digit.  Between body tokens a and b there is a word boundary unless a ends and b
 # starts alphanumeric (b then continues a's word: byte-level BPE puts the blank in b)
 TOK_STARTS_ALNUM, TOK_ENDS_ALNUM = 1, 2
+# token-class bits (span format: every token of a pointed-to span must be in the
+# field's class, as every copied token must be in copy format's schema mask)
+TOK_CLASS_BITS = {"date": 4, "number": 8, "currency": 16, "card": 32}
 
 
-def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: int) -> np.ndarray:
+def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: int,
+                classes: Optional[Dict[str, np.ndarray]] = None) -> np.ndarray:
     out = np.zeros(vocab, dtype=np.uint8)
     spec = set(specials)
+    if classes is not None:
+        n = min(vocab, len(token_strings))
+        for k, bit in TOK_CLASS_BITS.items():
+            out[:n] |= np.where(classes[k][:n], bit, 0).astype(np.uint8)
     for i, t in enumerate(token_strings[:vocab]):
         if i in spec or not t:
             continue
@@ -94,9 +103,10 @@ def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: in
         # number's inner separator followed by a digit (".58", ",000", ":23") continues
         # the number before it like a letter continues a word: a value can neither start
         # there ("657.58" -> "0.58") nor end just before it ("657" of "657.58")
+        # (and likewise a token that closes with one after a digit, " 1," of "1,234.50")
         starts = t[0].isalnum() or t[0] == "\ufffd" or (len(t) > 1 and t[0] in ".,:" and t[1].isdigit())
-        out[i] = (TOK_STARTS_ALNUM if starts else 0) | \
-            (TOK_ENDS_ALNUM if (t[-1].isalnum() or t[-1] == "\ufffd") else 0)
+        ends = t[-1].isalnum() or t[-1] == "\ufffd" or (len(t) > 1 and t[-1] in ".,:" and t[-2].isdigit())
+        out[i] |= (TOK_STARTS_ALNUM if starts else 0) | (TOK_ENDS_ALNUM if ends else 0)
     return out
 
 # token classes by the characters of a token's text.  Dates may carry ASCII letters
@@ -142,8 +152,11 @@ class SchemaFSM:
     done_state: int
     start_state: int = 0
     field_of_state: List[int] = field(default_factory=list)
-    copy_kind: Optional[np.ndarray] = None  # [S] COPY_NONE / COPY_START / COPY_NEXT
-    tok_flags: Optional[np.ndarray] = None  # [vocab] uint8 TOK_STARTS_ALNUM | TOK_ENDS_ALNUM
+    copy_kind: Optional[np.ndarray] = None  # [S] COPY_NONE / COPY_START / COPY_NEXT (| PTR_* for spans)
+    tok_flags: Optional[np.ndarray] = None  # [vocab] uint8 TOK_STARTS_ALNUM | TOK_ENDS_ALNUM (| class bits)
+    # span-pointer format (build_span_fsm): pointer token ptr0 + j = body position j
+    ptr0: int = -1
+    n_pos: int = 0
     # device copies (filled by to_device; consumed by ops.fsm_sample)
     masks: object = None
     state_mask: object = None
@@ -175,7 +188,19 @@ class SchemaFSM:
     def num_states(self) -> int:
         return int(self.allowed.shape[0])
 
+    @property
+    def span(self) -> bool:
+        return self.ptr0 >= 0
+
     def max_steps(self) -> int:
+        """Decode steps (= KV positions) an answer can take."""
+        if self.span:
+            return sum(f.cap + 1 if f.kind == "enum" else 2 for f in self.fields)
+        return self.max_answer_tokens()
+
+    def max_answer_tokens(self) -> int:
+        """Length of the longest answer in copy format (the span format's answers are
+        expanded to it on the GPU: ops.span_commit)."""
         return sum(f.cap for f in self.fields) + len(self.fields)
 
     def packed_masks(self) -> np.ndarray:
@@ -218,6 +243,8 @@ class SchemaFSM:
         kind = COPY_NONE if self.copy_kind is None else int(self.copy_kind[state])
         if kind == COPY_NONE:
             return allow
+        if kind & 0xFF in (PTR_START, PTR_END):
+            return allow & self._span_candidates(kind, prev, body)
         cand = np.zeros(self.vocab, dtype=bool)
         if kind == COPY_START:
             # a value starts at a word boundary; an empty value (<sep>) is always possible
@@ -236,6 +263,57 @@ class SchemaFSM:
                 if nxt < 0 or self._boundary(t, nxt):
                     cand[self.sep_token] = True
         return allow & cand
+
+    def _span_candidates(self, kind: int, prev: int, body: Sequence[int]) -> np.ndarray:
+        """Span format (sparse_argmax_kernel's kinds 3 / 4): a start pointer at a word
+        boundary whose token is in the field's class, or <sep> (empty value); an end
+        pointer e >= start, within the field's cap, every token start..e in the class,
+        at a word boundary.  ``body`` ends with <ans>, which is never pointed at."""
+        cand = np.zeros(self.vocab, dtype=bool)
+        tf = self.tok_flags
+        cls = (kind >> 16) & 0xFF
+        n = len(body) - 1  # the pointable positions (the last prompt token is <ans>)
+
+        def in_cls(t: int) -> bool:
+            return cls == 0 or bool(int(tf[t]) & cls) if 0 <= t < self.vocab else False
+
+        if kind & 0xFF == PTR_START:
+            cand[self.sep_token] = True
+            for j in range(min(n, self.n_pos)):
+                if (j == 0 or self._boundary(body[j - 1], body[j])) and in_cls(body[j]):
+                    cand[self.ptr0 + j] = True
+            return cand
+        cap = (kind >> 8) & 0xFF
+        s = prev - self.ptr0
+        if not 0 <= s < n:
+            return cand
+        for e in range(s, min(n, s + cap)):
+            if not in_cls(body[e]):
+                break
+            if e + 1 >= n or self._boundary(body[e], body[e + 1]):
+                cand[self.ptr0 + e] = True
+        return cand
+
+    def expand_span_answer(self, toks: Sequence[int], body: Sequence[int]) -> List[int]:
+        """Span answer -> the copy-format token stream (what ops.span_commit writes)."""
+        out: List[int] = []
+        st = self.start_state
+        start = -1
+        for t in toks:
+            kind = int(self.copy_kind[st]) & 0xFF if self.copy_kind is not None else 0
+            if kind == PTR_END:
+                out += list(body[start:t - self.ptr0 + 1]) + [self.sep_token]
+            elif kind == PTR_START:
+                if t == self.sep_token:
+                    out.append(t)
+                else:
+                    start = t - self.ptr0
+            else:
+                out.append(t)
+            st = self.step_host(st, t)
+            if st < 0:
+                break
+        return out
 
     def step_host(self, state: int, tok: int) -> int:
         """Reference transition (host side, for tests)."""
@@ -361,3 +439,107 @@ def build_fsm(tokenizer, vocab: int, fields: Sequence[FieldSpec] = DEFAULT_FIELD
         copy_kind=np.asarray(copy_kind, dtype=np.int32),
         tok_flags=token_flags(strings, specials, vocab),
     )
+
+
+def span_positions(max_body_tokens: int = 128) -> int:
+    """Pointer tokens of the span format: one per prompt position (``body <ans>``)."""
+    return max_body_tokens + 2
+
+
+def build_span_fsm(tokenizer, vocab_tok: int, n_pos: int,
+                   fields: Sequence[FieldSpec] = DEFAULT_FIELDS) -> SchemaFSM:
+    """The span-pointer answer format (VERDICT r03 next #2a; sized by
+    scripts/span_sim.py): the enum ``txn_type`` is written as in copy format (its
+    trie, then ``<sep>``); every copied field is ONE pointer to its first body token
+    and ONE to its last -- or ``<sep>`` for an empty value -- instead of its tokens
+    one by one.  Pointer ``j`` is token id ``vocab_tok + j`` (ids past the tokenizer's
+    vocabulary: the model's embedding row of pointer ``j`` is also added to the input
+    of prompt position ``j``, so the model can name a position by "reading" it there).
+
+    States per copied field: start (kind PTR_START | class << 16: a pointer -> end,
+    <sep> -> next field) and end (PTR_END | cap << 8 | class << 16: a pointer -> next
+    field).  The
+    vocabulary is rounded up to 64 (the GEMM / mask tiles)."""
+    V = -(-(vocab_tok + n_pos) // 64) * 64
+    strings = tokenizer.token_strings
+    V_tok = len(strings)
+    specials = [tokenizer.pad, tokenizer.bos, tokenizer.eos, tokenizer.sep, tokenizer.sms, tokenizer.ans]
+    classes = _token_class_sets(strings, specials)
+    sep = tokenizer.sep
+    ptrs = np.zeros(V, dtype=bool)
+    ptrs[vocab_tok:vocab_tok + n_pos] = True
+    allowed: List[np.ndarray] = []
+    next_sep: List[int] = []
+    next_tok: List[int] = []
+    enum_lists: List[List[Tuple[int, int]]] = []
+    field_of: List[int] = []
+    kinds: List[int] = []
+
+    def new_state(mask: np.ndarray, fidx: int, kind: int = COPY_NONE) -> int:
+        allowed.append(mask)
+        next_sep.append(-1)
+        next_tok.append(-1)
+        enum_lists.append([])
+        field_of.append(fidx)
+        kinds.append(kind)
+        return len(allowed) - 1
+
+    starts: List[int] = []
+    leaves: List[List[int]] = []  # per field: states whose <sep> / pointer leaves it
+    for fi, f in enumerate(fields):
+        if f.kind == "enum":
+            enc = [tokenizer.encode(c) for c in f.choices]
+            if max(len(e) for e in enc) > f.cap:
+                raise ValueError(f"enum field {f.name!r}: a choice needs more than cap={f.cap} tokens")
+            root = new_state(np.zeros(V, dtype=bool), fi)
+            nodes: Dict[Tuple[int, ...], int] = {(): root}
+            ends: List[int] = []
+            for seq in enc:
+                for d in range(len(seq)):
+                    cur, key = nodes[tuple(seq[:d])], tuple(seq[:d + 1])
+                    if key not in nodes:
+                        nodes[key] = new_state(np.zeros(V, dtype=bool), fi)
+                    allowed[cur][seq[d]] = True
+                    if (seq[d], nodes[key]) not in enum_lists[cur]:
+                        enum_lists[cur].append((seq[d], nodes[key]))
+                    next_tok[cur] = -2
+                allowed[nodes[tuple(seq)]][sep] = True
+                ends.append(nodes[tuple(seq)])
+            starts.append(root)
+            leaves.append(ends)
+        else:
+            if not f.copy or f.cap > 64 or f.cap > 255:
+                raise ValueError(f"span format: field {f.name!r} must be a copy field with cap <= 64")
+            m = ptrs.copy()
+            m[sep] = True
+            cls = TOK_CLASS_BITS.get(f.kind, 0)
+            a = new_state(m, fi, PTR_START | (cls << 16))
+            b = new_state(ptrs.copy(), fi, PTR_END | (f.cap << 8) | (cls << 16))
+            next_tok[a] = b
+            starts.append(a)
+            leaves.append([a, b])  # a: by <sep> (empty value); b: by its end pointer
+    only_sep = np.zeros(V, dtype=bool)
+    only_sep[sep] = True
+    done = new_state(only_sep, len(fields))
+    next_sep[done] = done
+    for fi, f in enumerate(fields):
+        tgt = starts[fi + 1] if fi + 1 < len(fields) else done
+        if f.kind == "enum":
+            for st in leaves[fi]:
+                next_sep[st] = tgt
+        else:
+            a, b = leaves[fi]
+            next_sep[a] = tgt
+            next_tok[b] = tgt
+    S = len(allowed)
+    E = max(1, max(len(e) for e in enum_lists))
+    enum_tok = np.full((S, E), -1, dtype=np.int32)
+    enum_next = np.full((S, E), -1, dtype=np.int32)
+    for st, lst in enumerate(enum_lists):
+        for j, (t, nx) in enumerate(lst):
+            enum_tok[st, j], enum_next[st, j] = t, nx
+    return SchemaFSM(fields=tuple(fields), vocab=V, sep_token=sep, allowed=np.stack(allowed),
+                     next_sep=np.asarray(next_sep, dtype=np.int32), next_tok=np.asarray(next_tok, dtype=np.int32),
+                     enum_tok=enum_tok, enum_next=enum_next, done_state=done, start_state=starts[0],
+                     field_of_state=field_of, copy_kind=np.asarray(kinds, dtype=np.int32),
+                     tok_flags=token_flags(strings, specials, V, classes), ptr0=vocab_tok, n_pos=n_pos)

@@ -34,7 +34,7 @@ def test_two_ranks_one_broker():
     assert h["endpoint"] == "/sms/raw" and h["requests"] == total and h["value"] > 0
     assert h["cpu"].get("client_loaders", {"cpu_us_per_msg": 1})["cpu_us_per_msg"] > 0
     assert cpu["cores_busy_per_gpu"]["parser_procs"] > 0 and cpu["cores_busy_per_gpu"]["brokers"] > 0
-    assert cpu["cpu_us_per_msg"] > 0 and cpu["node_cores_at_8_gpus"] == round(8 * cpu["cores_busy_per_gpu_total"], 1)
+    assert cpu["cpu_us_per_msg"] > 0 and abs(cpu["node_cores_at_8_gpus"] - 8 * cpu["cores_busy_per_gpu_total"]) <= 0.1  # (from unrounded)
     assert not [d for d in os.listdir("/tmp") if d == "smsgate-bench-bus-29671"]  # broker dir cleaned up
 
 

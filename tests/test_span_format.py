@@ -1,0 +1,90 @@
+"""Span-pointer answer format (serving/fsm.py build_span_fsm, VERDICT r03 next #2a):
+every copied field is two pointers into the SMS body instead of its tokens.
+
+CPU checks: every gold answer of every template family is expressible and walks the
+FSM under the copy rules; expanding a span answer gives exactly the copy-format
+answer (what ops.span_commit writes on the GPU); the host masks' start / end rules;
+a tiny span model trains."""
+from collections import Counter
+
+import numpy as np
+import pytest
+
+from smsgate_amd.models.tokenizer import load_tokenizer
+from smsgate_amd.models.train import answer_fsm, answer_span_tokens, answer_tokens
+from smsgate_amd.parse.text import normalize_body
+from smsgate_amd.serving.fsm import PTR_END, PTR_START
+from smsgate_amd.utils.synth import generate
+
+
+@pytest.fixture(scope="module")
+def fsms():
+    tk = load_tokenizer()
+    return tk, answer_fsm(tk, "span"), answer_fsm(tk, "copy")
+
+
+def test_shape(fsms):
+    tk, f, _ = fsms
+    assert f.span and f.ptr0 == 8192 and f.n_pos == 130 and f.vocab == 8384
+    assert f.max_steps() == 8 + 1 + 2 * 8  # enum (+ <sep>) and two pointers per copied field
+    assert f.max_answer_tokens() == sum(x.cap for x in f.fields) + len(f.fields)
+    kinds = Counter(int(k) & 0xFF for k in f.copy_kind)
+    assert kinds[PTR_START] == 8 and kinds[PTR_END] == 8
+
+
+@pytest.mark.parametrize("families", ["train", "heldout", None])
+def test_gold_answers_expressible_and_expand_to_copy_format(fsms, families):
+    tk, f, fc = fsms
+    bad = Counter()
+    lens = []
+    for s in generate(1200, seed=31, vocab_name="heldout", families=families):
+        if s.answer is None:
+            continue
+        b = normalize_body(s.body)
+        enc = tk.encode_offsets([b])[0]
+        msg = tk.message_ids([b], 128)[0]
+        sp = answer_span_tokens(tk, f, s.answer, b, enc, len(msg))
+        if sp is None:
+            bad[s.family] += 1
+            continue
+        lens.append(len(sp))
+        assert f.expand_span_answer(sp, msg) == answer_tokens(tk, fc, s.answer, b, enc), s.body
+    assert not bad, bad
+    assert np.mean(lens) <= 19  # vs ~36 answer tokens in copy format (scripts/span_sim.py)
+
+
+def test_host_masks(fsms):
+    tk, f, _ = fsms
+    body = "Purchase 1,234.50 USD at SHOP NAME, card *1234"
+    msg = tk.message_ids([body], 128)[0]
+    strings = [tk.token_strings[t] for t in msg]
+    # the amount field's start / end states
+    amt = f.fields.index(next(x for x in f.fields if x.name == "amount"))
+    a_start = [s for s in range(f.num_states) if f.field_of_state[s] == amt and f.copy_kind[s] & 0xFF == PTR_START][0]
+    a_end = int(f.next_tok[a_start])
+    m = f.copy_mask_host(a_start, -1, msg)
+    ok = {j for j in range(len(msg)) if m[f.ptr0 + j]}
+    assert m[f.sep_token]
+    # a number starts at its first token only; words are not numbers
+    j1 = next(j for j, t in enumerate(strings) if t.strip().startswith("1"))
+    assert j1 in ok and 0 not in ok  # "Purchase" is no number
+    assert j1 + 1 not in ok and j1 + 2 not in ok  # never inside "1,234.50" (" 1," "234" ".50")
+    assert len(msg) - 1 not in ok  # never the closing <ans>
+    e = f.copy_mask_host(a_end, f.ptr0 + j1, msg)
+    ends = [j for j in range(len(msg)) if e[f.ptr0 + j]]
+    assert ends and all(j >= j1 for j in ends)
+    # the amount cannot end inside "1,234.50": its last pointer is the number's last token
+    assert tk.decode(msg[j1:ends[-1] + 1]).strip() == "1,234.50"
+    assert not e[f.sep_token]
+
+
+def test_tiny_span_model_trains_on_cpu():
+    import torch
+
+    from smsgate_amd.models.train import TrainConfig, train_extractor
+
+    torch.manual_seed(0)
+    w = train_extractor(TrainConfig(model="tiny", steps=3, batch=4, n_examples=48, ema=0, log_every=0,
+                                    answer_format="span", families=None), device="cpu", log=lambda s: None)
+    assert w.cfg.span_positions == 130 and w.embed.shape[0] >= 8192 + 130
+    assert torch.isfinite(w.embed.float()).all()

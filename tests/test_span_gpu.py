@@ -1,0 +1,166 @@
+"""Span-pointer answer format on the GPU (csrc/spec_kernels.hip: sparse_argmax_kernel's
+pointer kinds, span_commit_kernel) against the host references of serving/fsm.py and
+an fp32 PyTorch reference, and end to end: a span model decodes through the engine
+(pointer rows added to the prompt, answers expanded to copy format on the GPU) and
+learns the task."""
+import random
+
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")]
+
+from smsgate_amd import ops  # noqa: E402
+from smsgate_amd.models.tokenizer import load_tokenizer  # noqa: E402
+from smsgate_amd.models.train import answer_fsm, make_examples  # noqa: E402
+from smsgate_amd.parse.text import normalize_body  # noqa: E402
+from smsgate_amd.utils.synth import generate, reference_cases  # noqa: E402
+
+DEV = "cuda"
+i32 = dict(dtype=torch.int32, device=DEV)
+
+
+def _key(tok):  # an arg-max key naming `tok` (what sparse_argmax writes)
+    return (1 << 40) | (0xFFFFFFFF - tok)
+
+
+@pytest.fixture(scope="module")
+def span_data():
+    tok = load_tokenizer()
+    fsm = answer_fsm(tok, "span").to_device(DEV)
+    exs = make_examples(tok, fsm, 500, seed=13, vocab_name="heldout", families="train")[:256]
+    exs += make_examples(tok, fsm, 200, seed=14, vocab_name="heldout", families=None)[:64]
+    n, LB = len(exs), 130
+    body = torch.zeros(n, LB, **i32)
+    blen = torch.zeros(n, **i32)
+    for r, (m, _) in enumerate(exs):
+        body[r, :len(m)] = torch.tensor(m)
+        blen[r] = len(m)
+    return tok, fsm, exs, body, blen
+
+
+@pytest.mark.parametrize("H", [256, 576])
+def test_sparse_argmax_pointer_rows(span_data, H):
+    """Rows at every point of gold span answers: the kernel's choice is allowed by the
+    host rules (start: boundary + class; end: cap, class run, boundary) and its logit
+    is the allowed maximum of the fp32 reference (to bf16 rounding)."""
+    tok, fsm, exs, body, blen = span_data
+    n = len(exs)
+    g = torch.Generator().manual_seed(5)
+    states, prevs = [], []
+    for m, a in exs:
+        L = int(torch.randint(0, len(a), (1,), generator=g))
+        s = fsm.start_state
+        for x in a[:L]:
+            s = fsm.step_host(s, x)
+        states.append(s)
+        prevs.append(a[L - 1] if L else m[-1])
+    state, prev, slot = torch.tensor(states, **i32), torch.tensor(prevs, **i32), torch.arange(n, **i32)
+    h = (torch.randn(n, H, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    nw = (torch.rand(H, generator=g) + 0.5).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(fsm.vocab, H, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    best = torch.zeros(n, dtype=torch.int64, device=DEV)
+    ops.sparse_argmax(h, ops.fold_norm(w, nw), state, fsm, best, prev, slot, body, blen, 1e-5)
+    torch.cuda.synchronize()
+    ref = ops.ref_gemm(h, w, norm_eps=1e-5, norm_w=nw)
+    kinds = {0: 0, 3: 0, 4: 0}
+    for r in range(n):
+        allowed = torch.tensor(fsm.copy_mask_host(states[r], prevs[r], exs[r][0]), device=DEV)
+        t = (0xFFFFFFFF - (int(best[r]) & 0xFFFFFFFF)) if int(best[r]) else fsm.sep_token
+        assert bool(allowed[t]), (r, t, int(fsm.copy_kind[states[r]]))
+        top = ref[r].masked_fill(~allowed, float("-inf")).max()
+        assert float(ref[r, t]) >= float(top) - 0.02 * abs(float(top)) - 0.02, (r, t)
+        kinds[int(fsm.copy_kind[states[r]]) & 0xFF] += 1
+    assert all(v > 10 for v in kinds.values()), kinds  # every kind of state was exercised
+
+
+def test_span_commit_expands_like_host(span_data):
+    """Feeding the gold pointer answers through span_commit (from the prefill's row
+    map, then step by step) writes exactly the copy-format answer, ends every row, and
+    leaves each row's state / last token / position as the host FSM says."""
+    tok, fsm, exs, body, blen = span_data
+    n = len(exs)
+    steps = max(len(a) for _, a in exs)
+    state = torch.full((n,), fsm.done_state, **i32)
+    tok_io, done = torch.zeros(n, **i32), torch.ones(n, **i32)
+    out_buf = torch.full((n, fsm.max_answer_tokens()), -7, **i32)
+    out_len = torch.zeros(n, **i32)
+    pos = torch.tensor([len(m) - 1 for m, _ in exs], **i32)
+    perm = list(range(n))
+    random.Random(0).shuffle(perm)  # prefill: key row i -> state row perm[i]
+    rows = torch.tensor(perm, **i32)
+    state[rows.long()] = fsm.start_state
+    done[rows.long()] = 0
+    slot_of_key = rows.clone()
+    best = torch.tensor([_key(exs[perm[i]][1][0]) for i in range(n)], dtype=torch.int64, device=DEV)
+    ops.span_commit(best, fsm, state, tok_io, out_buf, out_len, done, pos, slot_of_key, body, blen, n, row_map=rows)
+    for k in range(1, steps):
+        best = torch.tensor([_key(a[k]) if k < len(a) else 0 for _, a in exs], dtype=torch.int64, device=DEV)
+        ops.span_commit(best, fsm, state, tok_io, out_buf, out_len, done, pos, torch.arange(n, **i32), body, blen, n)
+    torch.cuda.synchronize()
+    for r, (m, a) in enumerate(exs):
+        want = fsm.expand_span_answer(a, m)
+        assert out_buf[r, :int(out_len[r])].tolist() == want, r
+        assert int(done[r]) == 1 and int(state[r]) == fsm.done_state and int(tok_io[r]) == a[-1]
+        assert int(pos[r]) == len(m) - 1 + len(a) - 1  # one KV position per emitted token but the last
+
+
+def _span_engine(w, **kw):
+    from smsgate_amd.serving.engine import EngineConfig, ExtractionEngine
+
+    return ExtractionEngine(w, load_tokenizer(), EngineConfig(max_slots=512, buckets=(64, 512), **kw))
+
+
+def test_span_engine_matches_fp32_reference_decode():
+    """Random-init span model: the engine's answers (HIP path: pointer rows in the
+    prefill input, sparse pointer arg-max, span_commit) == a plain fp32 PyTorch greedy
+    decode under the host rules, except at bf16 near-ties."""
+    from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, reference_forward, span_config
+    from smsgate_amd.parse.schema import EXTRACTOR_PROMPT
+
+    cfg = span_config(CONFIGS["small"])
+    w = ExtractorWeights(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+    eng = _span_engine(w, use_graphs=False)
+    assert eng.span and not eng.spec and eng.Lmax == 160
+    tok, fsm = eng.tok, eng.fsm
+    bodies = [normalize_body(s.body) for s in generate(24, seed=8, vocab_name="heldout", families="train") if s.answer]
+    bodies += [normalize_body(b) for b in reference_cases()]
+    got = eng.run(bodies)
+    msgs = tok.message_ids(bodies, 128)
+    prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
+    wf = ExtractorWeights(cfg, device=DEV, dtype=torch.float32, seed=None)
+    wf.load_state_dict({k: v.float() for k, v in w.state_dict().items()})
+    same = 0
+    for m, g in zip(msgs, got):
+        seq = prefix + m
+        add = [-1] * len(prefix) + [fsm.ptr0 + j for j in range(len(m))]
+        st, prev, ans = fsm.start_state, m[-1], []
+        while st != fsm.done_state and len(ans) < fsm.max_steps():
+            ids = torch.tensor([seq], device=DEV)
+            logits = reference_forward(wf, ids, add_ids=torch.tensor([add], device=DEV))[0, -1, : fsm.vocab]
+            allowed = torch.tensor(fsm.copy_mask_host(st, prev, m), device=DEV)
+            t = int(logits.masked_fill(~allowed, float("-inf")).argmax())
+            ans.append(t)
+            seq.append(t)
+            add.append(-1)
+            st, prev = fsm.step_host(st, t), t
+        vals = fsm.split_fields(fsm.expand_span_answer(ans, m))
+        ref = {f.name: tok.decode(v).strip() for f, v in zip(fsm.fields, vals)}
+        same += ref == g
+    assert same >= 0.8 * len(bodies), (same, len(bodies))
+
+
+def test_span_model_learns_extraction():
+    """A small span model trained 2 500 steps on the legacy mix decodes held-out SMS
+    through the engine as well as the copy-format test model (test_train_gpu.py)."""
+    from smsgate_amd.models.train import TrainConfig, field_accuracy, train_extractor
+
+    w = train_extractor(TrainConfig(model="small", steps=2500, lr=2e-3, n_examples=30000, log_every=0, families=None,
+                                    answer_format="span"), device="cuda")
+    assert w.cfg.span_positions == 130
+    eng = _span_engine(w)
+    held = [s for s in generate(300, seed=424242, vocab_name="heldout") if s.answer is not None]
+    acc = field_accuracy(eng.run([normalize_body(s.body) for s in held]), [s.answer for s in held])
+    for f in ("txn_type", "date", "currency"):
+        assert acc[f] >= 0.95, acc
+    assert sum(acc[f] for f in acc if f != "all") / 9 >= 0.8, acc

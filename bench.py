@@ -772,6 +772,7 @@ def main(argv=None) -> int:
                              else ")")),
             "llm_msgs_per_sec": round(llm_value, 1),
             "traffic": args.traffic,
+            "answer_format": args.answer_format,
             "config": {
                 "model": (f"{args.model} extractor LLM (134.5M params, replaces the Gemini call)" if gpu
                           else f"{args.backend} backend (CPU, stubbed LLM = reference config #1)"),
@@ -787,7 +788,11 @@ def main(argv=None) -> int:
                         if args.bus == "busd" else "in-process bus per parser process"),
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
-                "seq_len": "shared prefix 4 (<bos> txn: <sms>) + ~40 prompt + <=155 schema-constrained output tokens (~37 trained)",
+                "seq_len": ("shared prefix 4 (<bos> txn: <sms>) + ~40 prompt + "
+                            + ("<=25 schema-constrained decode steps (txn_type, then a start and an end pointer "
+                               "into the SMS per copied field; ~17 on this traffic)" if args.answer_format == "span"
+                               else "<=155 schema-constrained output tokens (~37 trained)")),
+                "answer_format": args.answer_format,
                 "parallelism": f"dp{world}" if gpu else "cpu",
                 "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
                 "engine_profile": args.profile,

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""GPU time per LLM-routed message from a rocprofv3 ``*_kernel_stats.csv`` of a bench
+run (VERDICT r03 next #2's measure: round 3 = 36.8 us, profiles/PERF.md).
+
+    python scripts/gpu_us_per_msg.py <kernel_stats.csv> <bench JSON line file> [--out f.json]
+
+Messages = (warmup + steps) x msgs_per_step_per_gpu x llm share of the profiled run
+(run it with ``--eval-n 0 --ingest bus``: no quality evaluation, one ingest phase, and
+weights from the cache, so the profile holds the serving kernels only).  Kernel time
+is split into GEMMs, attention, the lm_head arg-max / commit, speculative planning
+and the rest."""
+import argparse
+import csv
+import json
+
+
+def _group(name: str) -> str:
+    n = name.lower()
+    if "gemm" in n or "cijk" in n:
+        return "gemm"
+    if "attn" in n:
+        return "attention"
+    if "argmax" in n or "commit" in n or "fsm_" in n:
+        return "lm_head_argmax_commit"
+    if "spec_" in n:
+        return "spec_plan_verify"
+    return "other"
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser()
+    p.add_argument("stats")
+    p.add_argument("bench")
+    p.add_argument("--out", default="")
+    a = p.parse_args(argv)
+    rows = list(csv.DictReader(open(a.stats)))
+    line = [x for x in open(a.bench).read().splitlines() if x.startswith("{")][-1]
+    b = json.loads(line)
+    per_step = b["config"]["msgs_per_step_per_gpu"]
+    msgs = (b["steps"] + b["warmup"]) * per_step * float(b.get("llm_parsed_share", 1.0))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    groups = {}
+    for r in rows:
+        g = _group(r["Name"])
+        groups[g] = groups.get(g, 0.0) + float(r["TotalDurationNs"])
+    out = {"kernel_s": round(tot / 1e9, 3), "llm_msgs": int(msgs), "gpu_us_per_msg": round(tot / 1e3 / msgs, 2),
+           "by_group_us_per_msg": {k: round(v / 1e3 / msgs, 2) for k, v in sorted(groups.items(), key=lambda x: -x[1])},
+           "bench_value": b["value"], "answer_format": b.get("answer_format"), "traffic": b.get("traffic")}
+    print(json.dumps(out))
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(json.dumps(out, indent=1) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -74,8 +74,8 @@ SPAN_PTR0 = 8192
 
 def span_config(cfg: ExtractorConfig, positions: int = 130) -> ExtractorConfig:
     """``cfg`` for the span-pointer format: the embedding must hold the pointer rows
-    (SmolLM2's 49 152 rows already do; the 8 192-row small models grow by 192)."""
-    vocab = max(cfg.vocab, -(-(SPAN_PTR0 + positions) // 64) * 64)
+    (SmolLM2's 49 152 rows already do; the 8 192-row small models grow by 256)."""
+    vocab = max(cfg.vocab, -(-(SPAN_PTR0 + positions) // 128) * 128)
     return dataclasses.replace(cfg, vocab=vocab, span_positions=positions)
 
 

@@ -459,8 +459,8 @@ def build_span_fsm(tokenizer, vocab_tok: int, n_pos: int,
     States per copied field: start (kind PTR_START | class << 16: a pointer -> end,
     <sep> -> next field) and end (PTR_END | cap << 8 | class << 16: a pointer -> next
     field).  The
-    vocabulary is rounded up to 64 (the GEMM / mask tiles)."""
-    V = -(-(vocab_tok + n_pos) // 64) * 64
+    vocabulary is rounded up to 128 (the lm_head / mask tiles)."""
+    V = -(-(vocab_tok + n_pos) // 128) * 128
     strings = tokenizer.token_strings
     V_tok = len(strings)
     specials = [tokenizer.pad, tokenizer.bos, tokenizer.eos, tokenizer.sep, tokenizer.sms, tokenizer.ans]

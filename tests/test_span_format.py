@@ -25,7 +25,7 @@ def fsms():
 
 def test_shape(fsms):
     tk, f, _ = fsms
-    assert f.span and f.ptr0 == 8192 and f.n_pos == 130 and f.vocab == 8384
+    assert f.span and f.ptr0 == 8192 and f.n_pos == 130 and f.vocab == 8448
     assert f.max_steps() == 8 + 1 + 2 * 8  # enum (+ <sep>) and two pointers per copied field
     assert f.max_answer_tokens() == sum(x.cap for x in f.fields) + len(f.fields)
     kinds = Counter(int(k) & 0xFF for k in f.copy_kind)

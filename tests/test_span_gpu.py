@@ -112,42 +112,58 @@ def _span_engine(w, **kw):
 
 
 def test_span_engine_matches_fp32_reference_decode():
-    """Random-init span model: the engine's answers (HIP path: pointer rows in the
-    prefill input, sparse pointer arg-max, span_commit) == a plain fp32 PyTorch greedy
-    decode under the host rules, except at bf16 near-ties."""
+    """Random-init span model vs a plain fp32 PyTorch greedy decode under the host
+    rules: teacher-forced on the reference's answers, the engine's logits (pointer rows
+    added to the prompt inputs, pointer ids fed back as decode inputs, the lm_head over
+    tokenizer + pointer rows) match at every step, and the greedy answers agree except
+    where bf16 rounding flips a near-tie (one flip changes a whole answer)."""
     from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, reference_forward, span_config
     from smsgate_amd.parse.schema import EXTRACTOR_PROMPT
 
     cfg = span_config(CONFIGS["small"])
     w = ExtractorWeights(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
     eng = _span_engine(w, use_graphs=False)
-    assert eng.span and not eng.spec and eng.Lmax == 160
+    assert eng.span and not eng.spec and eng.Lmax == 160 and eng.V_dec == 8448
     tok, fsm = eng.tok, eng.fsm
     bodies = [normalize_body(s.body) for s in generate(24, seed=8, vocab_name="heldout", families="train") if s.answer]
     bodies += [normalize_body(b) for b in reference_cases()]
-    got = eng.run(bodies)
     msgs = tok.message_ids(bodies, 128)
     prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
     wf = ExtractorWeights(cfg, device=DEV, dtype=torch.float32, seed=None)
     wf.load_state_dict({k: v.float() for k, v in w.state_dict().items()})
+    refs, ref_logits = [], []
+    with torch.no_grad():
+        for m in msgs:
+            seq = prefix + m
+            add = [-1] * len(prefix) + [fsm.ptr0 + j for j in range(len(m))]
+            st, prev, ans, lgs = fsm.start_state, m[-1], [], []
+            while st != fsm.done_state and len(ans) < fsm.max_steps():
+                logits = reference_forward(wf, torch.tensor([seq], device=DEV),
+                                           add_ids=torch.tensor([add], device=DEV))[0, -1, : fsm.vocab]
+                lgs.append(logits)
+                allowed = torch.tensor(fsm.copy_mask_host(st, prev, m), device=DEV)
+                t = int(logits.masked_fill(~allowed, float("-inf")).argmax())
+                ans.append(t)
+                seq.append(t)
+                add.append(-1)
+                st, prev = fsm.step_host(st, t), t
+            refs.append(ans)
+            ref_logits.append(lgs)
+    L = max(len(a) for a in refs)
+    forced = [a + [fsm.sep_token] * (L - len(a)) for a in refs]
+    outs = eng.debug_logits(bodies, [f[:L - 1] for f in forced])
+    for b, lgs in enumerate(ref_logits):
+        for step, ref in enumerate(lgs):
+            got = outs[step][b, : fsm.vocab].float()
+            scale = ref.abs().max().item()
+            err = (got - ref).abs().max().item()
+            assert err <= 0.05 * scale + 0.05, (b, step, err, scale)
+    got = eng.run(bodies)
     same = 0
-    for m, g in zip(msgs, got):
-        seq = prefix + m
-        add = [-1] * len(prefix) + [fsm.ptr0 + j for j in range(len(m))]
-        st, prev, ans = fsm.start_state, m[-1], []
-        while st != fsm.done_state and len(ans) < fsm.max_steps():
-            ids = torch.tensor([seq], device=DEV)
-            logits = reference_forward(wf, ids, add_ids=torch.tensor([add], device=DEV))[0, -1, : fsm.vocab]
-            allowed = torch.tensor(fsm.copy_mask_host(st, prev, m), device=DEV)
-            t = int(logits.masked_fill(~allowed, float("-inf")).argmax())
-            ans.append(t)
-            seq.append(t)
-            add.append(-1)
-            st, prev = fsm.step_host(st, t), t
-        vals = fsm.split_fields(fsm.expand_span_answer(ans, m))
-        ref = {f.name: tok.decode(v).strip() for f, v in zip(fsm.fields, vals)}
-        same += ref == g
-    assert same >= 0.8 * len(bodies), (same, len(bodies))
+    for m, a, g in zip(msgs, refs, got):
+        vals = fsm.split_fields(fsm.expand_span_answer(a, m))
+        same += {f.name: tok.decode(v).strip() for f, v in zip(fsm.fields, vals)} == g
+    assert same >= 0.4 * len(bodies), (same, len(bodies))
 
 
 def test_span_model_learns_extraction():

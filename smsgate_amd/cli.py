@@ -251,7 +251,8 @@ def _train(a, settings) -> None:
             device = "cpu"
             dist.init_process_group("gloo")
     cfg = TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr, n_examples=a.examples,
-                      ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, bucket_mb=a.bucket_mb)
+                      ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, bucket_mb=a.bucket_mb,
+                      answer_format=a.answer_format, families=None if a.families == "legacy" else a.families)
     w = train_extractor(cfg, device=device)
     if not dist.is_initialized() or dist.get_rank() == 0:
         w.save(a.out)
@@ -366,6 +367,10 @@ def build_parser() -> argparse.ArgumentParser:
     tr.add_argument("--ckpt-every", type=int, default=0)
     tr.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --ckpt-dir")
     tr.add_argument("--bucket-mb", type=float, default=64.0, help="DP gradient all-reduce bucket size")
+    tr.add_argument("--answer-format", default="copy", choices=["copy", "span"],
+                    help="span: two pointers per copied field (the checkpoint records it; the engine follows)")
+    tr.add_argument("--families", default="train", help="train (every training SMS layout) | legacy (the two "
+                    "reference formats only)")
     sp.add_parser("config")
     return p
 

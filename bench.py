@@ -257,6 +257,7 @@ def run_replica(args, rank: int, world: int, local: int):
 
         ekw = engine_kwargs(args)
         engine = build_engine(args.model, device=f"cuda:{local}", random_init=weights is None, weights=weights,
+                              answer_format=args.answer_format,
                               fused_gemm=not args.no_fused_gemm, compact=not args.no_compact,
                               split_offset=not args.no_split_offset, split_graphs=args.split_graphs,
                               split_parts=args.split_parts, decode_attn=args.decode_attn,

@@ -127,10 +127,10 @@ class ExtractorWeights(torch.nn.Module):
         from safetensors import safe_open
         from safetensors.torch import load_file
 
-        with safe_open(path, framework="pt") as fh:  # a span-format checkpoint says so in its metadata
+        with safe_open(path, framework="pt") as fh:  # the answer format is the checkpoint's own (metadata)
             meta = fh.metadata() or {}
-        if int(meta.get("span_positions", "0") or 0) > 0:
-            cfg = dataclasses.replace(cfg, vocab=int(meta["vocab"]), span_positions=int(meta["span_positions"]))
+        cfg = dataclasses.replace(cfg, vocab=int(meta.get("vocab", cfg.vocab)),
+                                  span_positions=int(meta.get("span_positions", "0") or 0))
         w = cls(cfg, device="meta" if device is None else device, dtype=dtype, seed=None)
         sd = load_file(path, device=str(device) if device is not None else "cpu")
         w.load_state_dict({k: v.to(dtype) for k, v in sd.items()}, assign=True)

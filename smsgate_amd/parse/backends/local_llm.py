@@ -56,17 +56,20 @@ def resolve_checkpoint(model: str, checkpoint: Optional[str] = None, random_init
 
 
 def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
-                 seed: int = 0, random_init: bool = False, weights=None, **engine_kw: Any):
+                 seed: int = 0, random_init: bool = False, weights=None, answer_format: str = "copy",
+                 **engine_kw: Any):
     """Engine for ``model`` with the weights :func:`resolve_checkpoint` picks;
-    ``random_init=True`` serves random weights (throughput benchmarks only);
-    ``weights`` serves an in-memory :class:`ExtractorWeights` (e.g. just trained)."""
+    ``random_init=True`` serves random weights (throughput benchmarks only; in
+    ``answer_format`` "span" they are a span-pointer model's); ``weights`` serves an
+    in-memory :class:`ExtractorWeights` (e.g. just trained).  A checkpoint's answer
+    format comes from its own metadata."""
     import torch
 
-    from ...models.extractor import CONFIGS, ExtractorWeights
+    from ...models.extractor import CONFIGS, ExtractorWeights, span_config
     from ...models.tokenizer import load_tokenizer
     from ...serving.engine import EngineConfig, ExtractionEngine
 
-    cfg = CONFIGS[model]
+    cfg = span_config(CONFIGS[model]) if answer_format == "span" else CONFIGS[model]
     dev = torch.device(device)
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())

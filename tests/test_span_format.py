@@ -88,3 +88,18 @@ def test_tiny_span_model_trains_on_cpu():
                                     answer_format="span", families=None), device="cpu", log=lambda s: None)
     assert w.cfg.span_positions == 130 and w.embed.shape[0] >= 8192 + 130
     assert torch.isfinite(w.embed.float()).all()
+
+
+def test_checkpoint_carries_its_answer_format(tmp_path):
+    """A span checkpoint loads as a span model whatever config the caller passes, and
+    a copy-format checkpoint (the bundled small extractor) as a copy model."""
+    from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, span_config
+    from smsgate_amd.parse.backends.local_llm import bundled_checkpoint
+
+    w = ExtractorWeights(span_config(CONFIGS["tiny"]), device="cpu", seed=1)
+    p = str(tmp_path / "span.safetensors")
+    w.save(p)
+    got = ExtractorWeights.load(p, CONFIGS["tiny"])
+    assert got.cfg.span_positions == 130 and got.embed.shape[0] == 8448
+    small = ExtractorWeights.load(bundled_checkpoint("small"), span_config(CONFIGS["small"]))
+    assert small.cfg.span_positions == 0 and small.cfg.vocab == 8192

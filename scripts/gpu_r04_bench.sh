@@ -11,11 +11,11 @@ timeout -k 10 840 python3 -u $R/bench.py --answer-format $FMT --steps 20 --warmu
   || { tail -20 $R/gpurun_out/bench_$FMT.err; exit 1; }
 cat $R/gpurun_out/bench_$FMT.json | cut -c1-600
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$FMT -o run -- python3 $R/bench.py \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$FMT -o run -- python3 $R/bench.py \
   --answer-format $FMT --steps 10 --warmup 2 --eval-n 0 --quality-floor 0 --ingest bus \
   > $R/gpurun_out/bench_${FMT}_prof.json 2> $R/gpurun_out/bench_${FMT}_prof.err \
   || { tail -20 $R/gpurun_out/bench_${FMT}_prof.err; exit 1; }
-S=$(find $R/gpurun_out/prof_$FMT -name '*kernel_stats.csv' | head -1)
+S=$(find $R/gpurun_out/prof_$FMT -name '*kernel_stats.csv' -o -name '*.db' | sort | head -1)
 python3 $R/scripts/gpu_us_per_msg.py $S $R/gpurun_out/bench_${FMT}_prof.json --out $R/gpurun_out/gpu_us_$FMT.json
 if [ "$FMT" = "copy" ]; then  # the verify-attention SOL row at the bench's max_q = 7
   cd $R && timeout -k 10 240 python3 -u scripts/sol_table.py > gpurun_out/r04_sol_maxq7.json 2> gpurun_out/r04_sol.log \

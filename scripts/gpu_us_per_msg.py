@@ -2,7 +2,7 @@
 """GPU time per LLM-routed message from a rocprofv3 ``*_kernel_stats.csv`` of a bench
 run (VERDICT r03 next #2's measure: round 3 = 36.8 us, profiles/PERF.md).
 
-    python scripts/gpu_us_per_msg.py <kernel_stats.csv> <bench JSON line file> [--out f.json]
+    python scripts/gpu_us_per_msg.py <kernel_stats.csv | results.db> <bench JSON line file> [--out f.json]
 
 Messages = (warmup + steps) x msgs_per_step_per_gpu x llm share of the profiled run
 (run it with ``--eval-n 0 --ingest bus``: no quality evaluation, one ingest phase, and
@@ -33,7 +33,14 @@ def main(argv=None) -> int:
     p.add_argument("bench")
     p.add_argument("--out", default="")
     a = p.parse_args(argv)
-    rows = list(csv.DictReader(open(a.stats)))
+    if a.stats.endswith(".db"):  # rocprofv3's SQLite output (no --output-format csv): its top_kernels view, us
+        import sqlite3
+
+        db = sqlite3.connect(a.stats)
+        rows = [{"Name": n, "TotalDurationNs": float(t) * 1e3}
+                for n, t in db.execute("SELECT name, total_duration FROM top_kernels")]
+    else:
+        rows = list(csv.DictReader(open(a.stats)))
     line = [x for x in open(a.bench).read().splitlines() if x.startswith("{")][-1]
     b = json.loads(line)
     per_step = b["config"]["msgs_per_step_per_gpu"]

@@ -166,13 +166,23 @@ def test_span_engine_matches_fp32_reference_decode():
     assert same >= 0.4 * len(bodies), (same, len(bodies))
 
 
-def test_span_model_learns_extraction():
-    """A small span model trained 2 500 steps on the legacy mix decodes held-out SMS
-    through the engine as well as the copy-format test model (test_train_gpu.py)."""
-    from smsgate_amd.models.train import TrainConfig, field_accuracy, train_extractor
+@pytest.fixture(scope="module")
+def span_small():
+    """A small span model trained 2 500 steps on the legacy mix (~30 s)."""
+    from smsgate_amd.models.train import TrainConfig, train_extractor
 
     w = train_extractor(TrainConfig(model="small", steps=2500, lr=2e-3, n_examples=30000, log_every=0, families=None,
                                     answer_format="span"), device="cuda")
+    w.requires_grad_(False)
+    return w
+
+
+def test_span_model_learns_extraction(span_small):
+    """The small span model decodes held-out SMS through the engine as well as the
+    copy-format test model (test_train_gpu.py)."""
+    from smsgate_amd.models.train import field_accuracy
+
+    w = span_small
     assert w.cfg.span_positions == 130
     eng = _span_engine(w)
     held = [s for s in generate(300, seed=424242, vocab_name="heldout") if s.answer is not None]
@@ -180,3 +190,25 @@ def test_span_model_learns_extraction():
     for f in ("txn_type", "date", "currency"):
         assert acc[f] >= 0.95, acc
     assert sum(acc[f] for f in acc if f != "all") / 9 >= 0.8, acc
+
+
+def test_span_templates_keep_answers(span_small):
+    """Message-start templates (KV of a common opening computed once, copied into each
+    matching message's slot) leave span answers unchanged: the opening's keys carry
+    the pointer rows of positions 0..k-1 in both cases."""
+    import dataclasses
+
+    from smsgate_amd.utils.synth import generate_traffic
+
+    bodies = [normalize_body(s.body) for s in generate_traffic(1200, seed=17, traffic="formats")]
+    outs, stats = [], []
+    for slots in (0, 16):
+        eng = _span_engine(span_small, template_slots=slots, template_every=128, template_min_count=4)
+        outs.append(eng.run(bodies))
+        stats.append(dataclasses.replace(eng.stats))
+        del eng
+    assert stats[1].templates > 0 and stats[1].template_tokens > len(bodies)
+    bad = [(b, x, y) for b, x, y in zip(bodies, *outs) if x != y]
+    for b, x, y in bad[:5]:
+        print("MISMATCH", repr(b[:120]), {k: (x[k], y[k]) for k in x if x[k] != y[k]})
+    assert len(bad) <= 0.01 * len(bodies), len(bad)

@@ -132,6 +132,7 @@ class EngineConfig:
     template_max_len: int = 12
     template_min_count: int = 16
     template_every: int = 4096
+    span_templates: bool = False  # templates with a span-pointer model (off: see ExtractionEngine.__init__)
     measure_idle: bool = True  # EngineStats.gpu_idle_s from two timing events per step
     # the prefill forward (not graph-captured: its shape changes with every admission)
     # launched by ONE native call (ops.prefill_forward, csrc/runtime.hip) instead of 150
@@ -291,10 +292,16 @@ class ExtractionEngine:
                              "(temperature 0, fused_gemm, lm_head_argmax, sparse_argmax)")
         if ec.spec_k > ops.SPEC_MAX_K:
             raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
+        # message-start templates are not used with span-pointer models: with them the
+        # 135M span bench answered 1.4-18 % of the timed messages card-less (the card
+        # opens many layouts, i.e. lies in the template span), without them 0.03 %, as
+        # with the templates a quality-eval warm-up happened to learn
+        # (profiles/r04_span_template_runs.txt); off until that is understood
+        self.template_slots = 0 if (self.span and not ec.span_templates) else max(0, ec.template_slots)
         # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV
         # there; template KV slots follow it (slot S + 1 + t)
         self.T0 = S + 1
-        S_kv = S + 1 + max(0, ec.template_slots) if (self.spec or ec.template_slots > 0) else S
+        S_kv = S + 1 + self.template_slots if (self.spec or self.template_slots > 0) else S
         self.k_cache = torch.zeros(L, S_kv, nkv, self.Lmax, D, dtype=bf, device=dev)
         self.vt_cache = torch.zeros(L, *ops.vt_shape(S_kv, nkv, D, self.Lmax), dtype=bf, device=dev)
         self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
@@ -637,7 +644,7 @@ class ExtractionEngine:
         admissions promote the most frequent (count x k, >= template_min_count) to
         template slots and compute their keys / values (one small prefill)."""
         ec = self.cfg
-        if ec.template_slots <= 0 or len(self._tpl) >= ec.template_slots:
+        if self.template_slots <= 0 or len(self._tpl) >= self.template_slots:
             return
         cnt = self._tpl_counts
         kmax = ec.template_max_len
@@ -653,7 +660,7 @@ class ExtractionEngine:
         cands = sorted((c * len(key), key) for key, c in cnt.items()
                        if c >= ec.template_min_count and key not in self._tpl)
         new = []
-        while cands and len(self._tpl) + len(new) < ec.template_slots:
+        while cands and len(self._tpl) + len(new) < self.template_slots:
             new.append(cands.pop()[1])
         if new:
             slots = np.arange(len(self._tpl), len(self._tpl) + len(new), dtype=np.int32) + self.T0

@@ -195,7 +195,9 @@ def test_span_model_learns_extraction(span_small):
 def test_span_templates_keep_answers(span_small):
     """Message-start templates (KV of a common opening computed once, copied into each
     matching message's slot) leave span answers unchanged: the opening's keys carry
-    the pointer rows of positions 0..k-1 in both cases."""
+    the pointer rows of positions 0..k-1 in both cases.  (The engine keeps templates
+    off for span models by default -- profiles/r04_span_template_runs.txt -- this is
+    the check that decides when they can come back.)"""
     import dataclasses
 
     from smsgate_amd.utils.synth import generate_traffic
@@ -203,7 +205,8 @@ def test_span_templates_keep_answers(span_small):
     bodies = [normalize_body(s.body) for s in generate_traffic(1200, seed=17, traffic="formats")]
     outs, stats = [], []
     for slots in (0, 16):
-        eng = _span_engine(span_small, template_slots=slots, template_every=128, template_min_count=4)
+        eng = _span_engine(span_small, template_slots=slots, template_every=128, template_min_count=4,
+                           span_templates=True)
         outs.append(eng.run(bodies))
         stats.append(dataclasses.replace(eng.stats))
         del eng

@@ -63,9 +63,10 @@ def _args(argv=None):
     p.add_argument("--train-steps", type=int, default=3000)
     p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
     p.add_argument("--train-lr", type=float, default=1e-3)
-    p.add_argument("--answer-format", default="copy", choices=["copy", "span"],
-                   help="copy: each copied field written with the body's tokens (speculative prompt-lookup "
-                        "decoding); span: two pointers per field (serving/fsm.py build_span_fsm)")
+    # span: the round-4 default (2 decode steps per copied field instead of its tokens; profiles/PERF.md)
+    p.add_argument("--answer-format", default="span", choices=["copy", "span"],
+                   help="span: two pointers per copied field (serving/fsm.py build_span_fsm); copy: each copied "
+                        "field written with the body's tokens (speculative prompt-lookup decoding)")
     p.add_argument("--data-workers", type=int, default=12,
                    help="CPU processes building the training examples (started before the GPU is touched)")
     p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",

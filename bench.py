@@ -186,6 +186,9 @@ def _args(argv=None):
                    help="cProfile the timed region of every parser process and of the rank process into DIR "
                         "(parser-r<rank>-w<k>.pstats, rank<rank>.pstats)")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--eval-after", action="store_true",
+                   help="diagnostics: score held-out formats again after the timed phases and check the served "
+                        "weights did not change")
     return p.parse_args(argv)
 
 
@@ -268,6 +271,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               **ekw,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init
+    w_sum0 = _weights_sum(engine) if (args.eval_after and not echo) else None
     if not echo and args.eval_n and rank == 0:
         quality = evaluate_quality(engine, args)
         (engine.reset_stats() if hasattr(engine, "reset_stats") else engine.stats.__init__())
@@ -329,6 +333,15 @@ def run_replica(args, rank: int, world: int, local: int):
         results[http] = (dt_p, counts_p, cpu_p, estats_p, dict(coord.last_http))
     dt, counts, cpu, estats, _ = results[phases[0]]
     http_res = results.get(True) if phases != [True] else None
+    if args.eval_after and not echo and rank == 0:
+        # diagnostics: the same held-out check AFTER the timed phases, and whether the
+        # weights the engine serves changed while it served
+        from smsgate_amd.models.evaluate import evaluate_engine
+
+        ho2 = evaluate_engine(engine, n=200, seed=4243, vocab_name="heldout", families="heldout")
+        diag_after = {"heldout_formats_exact_after": round(ho2["exact"], 4), "weights_sum_before": w_sum0,
+                      "weights_sum_after": _weights_sum(engine)}
+        print(f"[bench] after the timed phases: {json.dumps(diag_after)}", file=sys.stderr, flush=True)
     bus_members = None
     if broker and coord.bus is not None:  # local rank 0: what each node broker carried
         try:
@@ -381,6 +394,14 @@ def run_replica(args, rank: int, world: int, local: int):
     if args.ingest == "http":  # the only phase is the HTTP one: report its request counts too
         prov["http_ingest_requests"] = results[True][4]
     return dt, counts, init_s, estats, prov, quality, cpu, bus_members, http_res
+
+
+def _weights_sum(engine) -> float:
+    """fp64 sum of |w| over the engine's served tensors (a corruption check)."""
+    ts = [engine.w.embed] + [t for name in ("fw_qkv", "fw_o", "fw_gu", "fw_down") for t in getattr(engine, name, [])]
+    if getattr(engine, "fw_lm", None) is not None:
+        ts.append(engine.fw_lm)
+    return float(sum(t.double().abs().sum().item() for t in ts))
 
 
 def evaluate_quality(engine, args) -> dict:

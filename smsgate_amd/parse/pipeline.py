@@ -25,6 +25,7 @@ the results — the reference did one synchronous HTTPS call per message.
 from __future__ import annotations
 
 import enum
+import os
 import time
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence
@@ -43,6 +44,24 @@ from .text import llm_should_skip, normalize_body
 __all__ = ["Outcome", "ParseResult", "ParsePipeline", "BrokenMessage", "postprocess_answer"]
 
 DEFAULT_TZ = "Asia/Yerevan"  # gemini_parser.py:229, Dockerfile TZ
+
+
+# SMSGATE_DEBUG_ANSWERS=DIR: each process appends the first 200 answers that did not
+# parse (body, backend answer, outcome) to DIR/answers-<pid>.jsonl (diagnostics)
+_DEBUG_DIR = os.environ.get("SMSGATE_DEBUG_ANSWERS", "")
+_DEBUG_LEFT = [200]
+
+
+def _debug_record(body: str, answer: Dict[str, Any], outcome: str) -> None:
+    if _DEBUG_LEFT[0] <= 0:
+        return
+    _DEBUG_LEFT[0] -= 1
+    import json
+
+    os.makedirs(_DEBUG_DIR, exist_ok=True)
+    with open(os.path.join(_DEBUG_DIR, f"answers-{os.getpid()}.jsonl"), "a") as fh:
+        fh.write(json.dumps({"outcome": outcome, "body": body, "answer": answer}, ensure_ascii=False,
+                            default=str) + "\n")
 
 
 class BrokenMessage(Exception):
@@ -190,6 +209,8 @@ class ParsePipeline:
                 r = postprocess_answer(raws[i], bodies[i], ans, self.tz)  # type: ignore[arg-type]
                 r.cached = i in cached
                 results[i] = r
+                if _DEBUG_DIR and r.outcome is not Outcome.PARSED:
+                    _debug_record(bodies[i], ans, r.outcome.value)
         # One observation per message, like the reference's per-message timer around
         # parse_sms_llm (worker.py:130-133, metrics.py:48-53): _count == messages
         # parsed.  The value is the latency each message experienced — the wall time

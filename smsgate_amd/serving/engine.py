@@ -132,7 +132,6 @@ class EngineConfig:
     template_max_len: int = 12
     template_min_count: int = 16
     template_every: int = 4096
-    span_templates: bool = False  # templates with a span-pointer model (off: see ExtractionEngine.__init__)
     measure_idle: bool = True  # EngineStats.gpu_idle_s from two timing events per step
     # the prefill forward (not graph-captured: its shape changes with every admission)
     # launched by ONE native call (ops.prefill_forward, csrc/runtime.hip) instead of 150
@@ -292,12 +291,7 @@ class ExtractionEngine:
                              "(temperature 0, fused_gemm, lm_head_argmax, sparse_argmax)")
         if ec.spec_k > ops.SPEC_MAX_K:
             raise ValueError(f"spec_k <= {ops.SPEC_MAX_K}")
-        # message-start templates are not used with span-pointer models: with them the
-        # 135M span bench answered 1.4-18 % of the timed messages card-less (the card
-        # opens many layouts, i.e. lies in the template span), without them 0.03 %, as
-        # with the templates a quality-eval warm-up happened to learn
-        # (profiles/r04_span_template_runs.txt); off until that is understood
-        self.template_slots = 0 if (self.span and not ec.span_templates) else max(0, ec.template_slots)
+        self.template_slots = max(0, ec.template_slots)
         # speculative mode owns one extra scratch slot: unused pseudo-rows write their KV
         # there; template KV slots follow it (slot S + 1 + t)
         self.T0 = S + 1
@@ -377,7 +371,7 @@ class ExtractionEngine:
         resid = x
         y: Optional[torch.Tensor] = None
         q = torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=x.device)
-        a = torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)
+        a = torch.zeros(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)  # (see _layers_fused)
         for i in range(mc.layers):
             h = ops.rmsnorm_residual(resid, w.ln1[i], mc.eps, x=y)
             qkv = F.linear(h, w.qkv[i])
@@ -400,7 +394,13 @@ class ExtractionEngine:
         mc = self.mc
         T = x.shape[0]
         q = torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=x.device)
-        a = torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)
+        # ZEROED: the decode attention kernels skip finished rows, so their rows of `a`
+        # would keep whatever the allocator's block held -- NaN bit patterns after training
+        # ran in the same process -- and the next layer would write NaN keys / values into
+        # their KV slots at their frozen positions.  A later message in that slot masks the
+        # stale position inside its last key tile, but P = 0 times V = NaN is NaN: its
+        # answer derails (the span bench's card-less answers, profiles/r04_span_template_runs.txt).
+        a = torch.zeros(T, mc.heads * mc.head_dim, dtype=x.dtype, device=x.device)
         ss = self._ss_buffer(T, x.device)
         for i in range(mc.layers):
             # norm prologue + QKV projection + RoPE + KV-cache write: one kernel (layer 0's

@@ -108,7 +108,7 @@ def test_span_commit_expands_like_host(span_data):
 def _span_engine(w, **kw):
     from smsgate_amd.serving.engine import EngineConfig, ExtractionEngine
 
-    return ExtractionEngine(w, load_tokenizer(), EngineConfig(max_slots=512, buckets=(64, 512), **kw))
+    return ExtractionEngine(w, load_tokenizer(), EngineConfig(**{"max_slots": 512, "buckets": (64, 512), **kw}))
 
 
 def test_span_engine_matches_fp32_reference_decode():
@@ -195,9 +195,7 @@ def test_span_model_learns_extraction(span_small):
 def test_span_templates_keep_answers(span_small):
     """Message-start templates (KV of a common opening computed once, copied into each
     matching message's slot) leave span answers unchanged: the opening's keys carry
-    the pointer rows of positions 0..k-1 in both cases.  (The engine keeps templates
-    off for span models by default -- profiles/r04_span_template_runs.txt -- this is
-    the check that decides when they can come back.)"""
+    the pointer rows of positions 0..k-1 in both cases."""
     import dataclasses
 
     from smsgate_amd.utils.synth import generate_traffic
@@ -205,13 +203,35 @@ def test_span_templates_keep_answers(span_small):
     bodies = [normalize_body(s.body) for s in generate_traffic(1200, seed=17, traffic="formats")]
     outs, stats = [], []
     for slots in (0, 16):
-        eng = _span_engine(span_small, template_slots=slots, template_every=128, template_min_count=4,
-                           span_templates=True)
+        eng = _span_engine(span_small, template_slots=slots, template_every=128, template_min_count=4)
         outs.append(eng.run(bodies))
         stats.append(dataclasses.replace(eng.stats))
         del eng
-    assert stats[1].templates > 0 and stats[1].template_tokens > len(bodies)
     bad = [(b, x, y) for b, x, y in zip(bodies, *outs) if x != y]
-    for b, x, y in bad[:5]:
+    print("TEMPLATES", stats[1].templates, stats[1].template_tokens, "mismatches", len(bad), "of", len(bodies))
+    for b, x, y in bad[:8]:
         print("MISMATCH", repr(b[:120]), {k: (x[k], y[k]) for k in x if x[k] != y[k]})
+    assert stats[1].templates > 0 and stats[1].template_tokens > 0.5 * len(bodies)
     assert len(bad) <= 0.01 * len(bodies), len(bad)
+
+
+def test_span_engine_survives_nan_filled_allocator_blocks(span_small):
+    """Regression: finished rows in a decode bucket skip attention, so their rows of the
+    attention output must not carry the allocator block's old contents into the next
+    layer (NaN keys / values in their slots poisoned the slot's next message).  An
+    engine built after NaN-filled memory went back to the caching allocator answers
+    like one built on fresh memory, with rows reused many times."""
+    from smsgate_amd.utils.synth import generate_traffic
+
+    bodies = [normalize_body(s.body) for s in generate_traffic(1500, seed=23, traffic="formats")]
+    kw = dict(max_slots=128, buckets=(64, 128), use_graphs=True)
+    eng = _span_engine(span_small, **kw)
+    clean = eng.run(bodies)
+    del eng
+    torch.cuda.synchronize()
+    junk = torch.full((1 << 30,), float("nan"), dtype=torch.bfloat16, device=DEV)  # 2 GB of NaN
+    del junk  # back to the caching allocator: the next engine's buffers / graph pools reuse it
+    eng = _span_engine(span_small, **kw)
+    dirty = eng.run(bodies)
+    same = sum(a == b for a, b in zip(clean, dirty))
+    assert same >= 0.99 * len(bodies), same

@@ -56,7 +56,8 @@ def test_engine_runs_and_respects_schema(tiny_engine):
     for r in res:
         assert set(r) == {"txn_type", "date", "amount", "currency", "card", "merchant", "city", "address", "balance"}
         assert r["txn_type"] in ("debit", "credit", "otp", "unknown")
-        assert set(r["date"]) <= set("0123456789.:/- ")
+        # the date class (serving/fsm.py): digits, separators and ASCII letters (month names, ISO "T")
+        assert set(r["date"]) <= set("0123456789.:/-, ") | set("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz")
         assert set(r["card"]) <= set("0123456789* ")
     assert eng.stats.completed >= 150
     assert not eng.busy() and len(eng.free_rows) == eng.cfg.max_slots

@@ -317,6 +317,7 @@ def run_replica(args, rank: int, world: int, local: int):
         if hasattr(engine, "spec_stats"):
             engine.spec_stats(reset=True)
         cpu0 = _cpu_snapshot(procs, broker, lprocs)
+        thr0 = _rank_threads()
         rprof = None
         if args.profile_cpu and not http:
             import cProfile
@@ -330,6 +331,7 @@ def run_replica(args, rank: int, world: int, local: int):
             os.makedirs(args.profile_cpu, exist_ok=True)
             rprof.dump_stats(os.path.join(args.profile_cpu, f"rank{rank}.pstats"))
         cpu_p = {k: v1 - cpu0[k] for k, v1 in _cpu_snapshot(procs, broker, lprocs).items()}
+        cpu_p["rank_threads"] = _thread_cores(thr0, _rank_threads(), dt_p)
         estats_p = engine.stats.as_dict()
         if hasattr(engine, "spec_stats"):
             estats_p.update(engine.spec_stats())
@@ -506,12 +508,37 @@ def _cpu_snapshot(procs, brokers, loaders=()) -> dict:
     return out
 
 
+def _rank_threads() -> dict:
+    """CPU seconds per thread of this process: tid -> (thread name, seconds)."""
+    out = {}
+    tick = os.sysconf("SC_CLK_TCK")
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as fh:
+                name = fh.read().strip()
+            with open(f"/proc/self/task/{tid}/stat") as fh:
+                parts = fh.read().rsplit(")", 1)[1].split()
+            out[tid] = (name, (int(parts[11]) + int(parts[12])) / tick)  # utime + stime
+        except (OSError, IndexError, ValueError):
+            pass
+    return out
+
+
+def _thread_cores(t0: dict, t1: dict, dt: float, top: int = 8) -> list:
+    """The busiest threads of this process over dt seconds: [name, cores], grouped by name."""
+    by: dict = {}
+    for tid, (name, sec) in t1.items():
+        by[name] = by.get(name, 0.0) + sec - t0.get(tid, (name, 0.0))[1]
+    return [[n, round(c / dt, 3)] for n, c in sorted(by.items(), key=lambda x: -x[1])[:top]]
+
+
 def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
     """Cores busy per role over the timed region, CPU microseconds per message and the
     cores an 8-GPU node needs at this run's per-GPU rate (weak scaling: per-GPU work is
     fixed, so each role's load scales with the GPU count)."""
     cpu = dict(cpu)
     placement = cpu.pop("placement", None)
+    threads = cpu.pop("rank_threads", None)
     # the HTTP loaders play the phones / webhook senders: client-side CPU, reported
     # apart from the node's server-side budget
     loaders = cpu.pop("loaders", None)
@@ -522,6 +549,7 @@ def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:
             "cpu_us_per_msg": round(sum(cpu.values()) / max(msgs, 1) * 1e6, 1),
             "node_cores_at_8_gpus": round(8 * total, 1),
             "visible_cpus": VISIBLE_CPUS,
+            **({"rank_threads_cores": threads} if threads else {}),
             **({"client_loaders": {"cores_busy_per_gpu": round(loaders / dt / world, 2),
                                    "cpu_us_per_msg": round(loaders / max(msgs, 1) * 1e6, 1)}}
                if loaders is not None and loaders > 0.01 else {}),

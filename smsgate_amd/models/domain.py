@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import datetime as _dt
 import hashlib
-import json
 from decimal import Decimal
 from enum import Enum
 from typing import Literal, Optional
@@ -96,33 +95,16 @@ class ParsedSMS(BaseModel):
         return v.isoformat()
 
 
-_JSON = json.JSONEncoder(ensure_ascii=False, separators=(",", ":")).encode
-
-
 def parsed_wire(p: "ParsedSMS") -> bytes:
-    """``p.model_dump_json().encode()`` without pydantic's per-field Python serializers
-    (~2x faster): the same keys in the same order, ``isoformat`` dates, ``str``
-    decimals, UTF-8 kept and the same escapes (tests/test_parse_helpers.py fuzzes the
-    equality); anything the fast path cannot encode (a lone surrogate) falls back."""
-    try:
-        return _JSON({
-            "msg_id": p.msg_id, "device_id": p.device_id, "sender": p.sender, "date": p.date.isoformat(),
-            "raw_body": p.raw_body, "txn_type": p.txn_type.value if isinstance(p.txn_type, TxnType) else p.txn_type,
-            "amount": None if p.amount is None else str(p.amount), "currency": p.currency, "card": p.card,
-            "merchant": p.merchant, "city": p.city, "address": p.address,
-            "balance": None if p.balance is None else str(p.balance), "parser_version": p.parser_version,
-        }).encode("utf-8")
-    except (UnicodeEncodeError, TypeError, AttributeError, ValueError):
-        return p.model_dump_json().encode("utf-8")
+    """The ``sms.parsed`` payload: ``p.model_dump_json()`` as UTF-8.  (A hand-built
+    dict through ``json.JSONEncoder`` was tried: 12.5 vs 7.9 us per message with
+    pydantic-core's serializer on the mixed-layout traffic, Cyrillic included.)"""
+    return p.model_dump_json().encode("utf-8")
 
 
 def raw_wire(r: "RawSMS") -> bytes:
-    """``r.model_dump_json().encode()``, fast path (see :func:`parsed_wire`)."""
-    try:
-        return _JSON({"msg_id": r.msg_id, "sender": r.sender, "body": r.body, "date": r.date,
-                      "device_id": r.device_id, "source": r.source}).encode("utf-8")
-    except (UnicodeEncodeError, TypeError, ValueError):
-        return r.model_dump_json().encode("utf-8")
+    """The ``sms.raw`` payload: ``r.model_dump_json()`` as UTF-8 (4.4 vs 6.7 us)."""
+    return r.model_dump_json().encode("utf-8")
 
 
 class ParsedSmsCore(BaseModel):

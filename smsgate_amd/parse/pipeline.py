@@ -30,7 +30,7 @@ import time
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence
 
-from ..models.domain import PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
+from ..models.domain import CORE_FIELDS, PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
 from ..obs.errors import sentry_capture
 from ..obs.metrics import GEMINI_LATENCY, observe_many
 from ..runtime.errors import TransientError
@@ -44,6 +44,7 @@ from .text import llm_should_skip, normalize_body
 __all__ = ["Outcome", "ParseResult", "ParsePipeline", "BrokenMessage", "postprocess_answer"]
 
 DEFAULT_TZ = "Asia/Yerevan"  # gemini_parser.py:229, Dockerfile TZ
+_N_CORE = len(CORE_FIELDS)
 
 
 # SMSGATE_DEBUG_ANSWERS=DIR: each process appends the first 200 answers that did not
@@ -96,37 +97,41 @@ def postprocess_answer(raw: RawSMS, fixed_body: str, answer: Dict[str, Any], tz:
         # D8 (kept for parity): a null card raises here, so it lands in the DLQ as
         # "unmatched"; only card *strings* shorter than 4 chars reach BROKEN below.
         card = resp["card"].replace("*", "").replace(" ", "")
-        resp["card"] = card[:4] if len(card) > 4 else card
-        resp["amount"] = parse_ambiguous_decimal(str(resp["amount"]))
+        resp["card"] = card = card[:4] if len(card) > 4 else card
+        amount = resp["amount"] = parse_ambiguous_decimal(str(resp["amount"]))
         resp["balance"] = parse_ambiguous_decimal(str(resp["balance"]))
-        core = ParsedSmsCore.model_validate(resp)
-    except Exception as exc:
-        if resp.get("txn_type") != "otp":
-            sentry_capture(exc, extras={"raw_body": raw.body[:4096]})
-        return ParseResult(Outcome.UNMATCHED, error=exc)
-
-    address = "" if core.address == "null" else core.address
-    if len(str(core.card)) < 4:
-        return ParseResult(Outcome.BROKEN, error=BrokenMessage("no card number in message"))
-    try:
+        if len(card) < 4:
+            # the schema check first (a malformed answer stays UNMATCHED), then BROKEN
+            ParsedSmsCore.model_validate(resp)
+            return ParseResult(Outcome.BROKEN, error=BrokenMessage("no card number in message"))
+        # ONE validation builds the ParsedSMS: it checks every field ParsedSmsCore would
+        # (same types; the schema's required keys and amount >= 0 are checked here), so
+        # the answer is not validated twice (~3.7 us per message)
+        if len(resp) != _N_CORE and any(k not in resp for k in CORE_FIELDS):
+            ParsedSmsCore.model_validate(resp)  # raises its "field required" error
+        if amount is not None and amount < 0:
+            ParsedSmsCore.model_validate(resp)  # raises its "greater than or equal to 0" error
+        address = resp["address"]
         parsed = ParsedSMS(
             msg_id=raw.msg_id,
             device_id=raw.device_id,
             sender=raw.sender,
-            date=core.date,
+            date=resp["date"],
             raw_body=fixed_body,
-            txn_type=core.txn_type,
-            amount=core.amount,
-            currency=core.currency,
-            card=core.card,
-            merchant=core.merchant,
-            city=core.city,
-            address=address,
-            balance=core.balance,
+            txn_type=resp["txn_type"],
+            amount=amount,
+            currency=resp["currency"],
+            card=card[:4] if len(card) > 4 else card,
+            merchant=resp["merchant"],
+            city=resp["city"],
+            address="" if address == "null" else address,
+            balance=resp["balance"],
             parser_version=PARSER_VERSION_LLM,
-        )  # (validation in pydantic-core is ~2.7 us: cheaper than model_construct's ~5.9 us)
-    except Exception as exc:  # e.g. a 5+ char card can't happen, but stay total
-        return ParseResult(Outcome.ERROR, error=exc)
+        )
+    except Exception as exc:
+        if resp.get("txn_type") != "otp":
+            sentry_capture(exc, extras={"raw_body": raw.body[:4096]})
+        return ParseResult(Outcome.UNMATCHED, error=exc)
     return ParseResult(Outcome.PARSED, parsed=parsed)
 
 

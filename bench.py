@@ -354,6 +354,10 @@ def run_replica(args, rank: int, world: int, local: int):
         except Exception as exc:  # noqa: BLE001 - a report, never a failure of the run
             bus_members = [{"error": str(exc)}]
     coord.shutdown(procs + lprocs)
+    # (rank 0's own thread breakdown: a diagnostic, not summed over ranks)
+    threads = cpu.pop("rank_threads", None)
+    if http_res is not None:
+        http_res[2].pop("rank_threads", None)
     if dist is not None:
         dev = "cpu" if echo else "cuda"
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -396,6 +400,8 @@ def run_replica(args, rank: int, world: int, local: int):
         shutil.rmtree(os.path.dirname(broker[0].listens[0].replace("unix://", "")), ignore_errors=True)
     if placement is not None:
         cpu["placement"] = placement
+    if threads:
+        cpu["rank_threads"] = threads
     if args.ingest == "http":  # the only phase is the HTTP one: report its request counts too
         prov["http_ingest_requests"] = results[True][4]
     return dt, counts, init_s, estats, prov, quality, cpu, bus_members, http_res
@@ -525,11 +531,13 @@ def _rank_threads() -> dict:
 
 
 def _thread_cores(t0: dict, t1: dict, dt: float, top: int = 8) -> list:
-    """The busiest threads of this process over dt seconds: [name, cores], grouped by name."""
-    by: dict = {}
+    """The busiest threads of this process over dt seconds: [name #tid, cores]."""
+    main = str(os.getpid())
+    rows = []
     for tid, (name, sec) in t1.items():
-        by[name] = by.get(name, 0.0) + sec - t0.get(tid, (name, 0.0))[1]
-    return [[n, round(c / dt, 3)] for n, c in sorted(by.items(), key=lambda x: -x[1])[:top]]
+        rows.append([f"{name}{' (main)' if tid == main else ''} #{tid}", sec - t0.get(tid, (name, 0.0))[1]])
+    rows.sort(key=lambda x: -x[1])
+    return [[n, round(c / dt, 3)] for n, c in rows[:top]]
 
 
 def cpu_budget(cpu: dict, dt: float, msgs: int, world: int) -> dict:

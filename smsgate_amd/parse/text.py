@@ -114,7 +114,10 @@ def llm_should_skip(body: str) -> bool:
 
 
 def mask_card_number_with_prefix(text: str) -> str:
-    """``'4083***7538'`` → ``'CARD:7538'`` (every occurrence)."""
+    """``'4083***7538'`` → ``'CARD:7538'`` (every occurrence).  (The regex scan costs
+    ~5.8 us per SMS; a body without ``***`` cannot match.)"""
+    if "***" not in text:
+        return text
     return _CARD_RE.sub(r"CARD:\1", text)
 
 

@@ -189,6 +189,7 @@ def _args(argv=None):
                    help="cProfile the timed region of every parser process and of the rank process into DIR "
                         "(parser-r<rank>-w<k>.pstats, rank<rank>.pstats)")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--no-graphs", action="store_true", help="decode steps launched eagerly (no hipGraphs)")
     p.add_argument("--no-measure-idle", action="store_true",
                    help="no GPU-idle timing events per engine step (EngineConfig.measure_idle)")
     p.add_argument("--eval-after", action="store_true",
@@ -273,7 +274,7 @@ def run_replica(args, rank: int, world: int, local: int):
                               prefill_key_split=args.prefill_key_split, spec_policy=args.spec_policy,
                               spec_max_rows=args.spec_max_rows, producer_norm=not args.no_producer_norm,
                               native_prefill=not args.no_native_prefill, sparse_argmax=not args.no_sparse_argmax,
-                              measure_idle=not args.no_measure_idle,
+                              measure_idle=not args.no_measure_idle, use_graphs=not args.no_graphs,
                               **ekw,
                               **({} if args.admit_min_batch is None else {"admit_min_batch": args.admit_min_batch}))
     init_s = time.perf_counter() - t_init

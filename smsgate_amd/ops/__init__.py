@@ -107,6 +107,8 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_prefill_forward.restype = _c_int
     lib.sg_embed_rows.argtypes = [_ip, _vp, _vp, _c_int, _c_int, _c_int, _vp]
     lib.sg_embed_rows.restype = _c_int
+    lib.sg_embed_rows_add.argtypes = [_ip, _ip, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp]
+    lib.sg_embed_rows_add.restype = _c_int
     lib.sg_sparse_argmax.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _vp, _vp, _c_int, _vp, _c_int, _c_float,
                                      _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _c_int, _c_int, _vp, _vp]
     lib.sg_sparse_argmax.restype = _c_int
@@ -842,6 +844,21 @@ def embed_rows(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tenso
     if out.shape != (T, H) or not out.is_contiguous() or out.dtype != torch.bfloat16:
         raise ValueError("embed_rows: bad output")
     _check(load_library().sg_embed_rows(_p(ids), _p(table), _p(out), T, H, V, _stream()), "embed_rows")
+    return out
+
+
+def embed_rows_add(ids: torch.Tensor, pos: torch.Tensor, table: torch.Tensor, base: int) -> torch.Tensor:
+    """``table[ids] + table[base + pos]`` (int32 ids / positions, bf16 rows; the sum
+    rounded like torch's bf16 add) -- the span format's prompt rows, one kernel."""
+    _req(ids, torch.int32, "ids")
+    _req(pos, torch.int32, "pos")
+    V, H = table.shape
+    if table.dtype != torch.bfloat16 or not table.is_contiguous() or H % 8 or pos.numel() != ids.numel():
+        raise ValueError("embed_rows_add: contiguous bf16 table with H % 8 == 0 and one position per id required")
+    T = ids.numel()
+    out = table.new_empty((T, H))
+    _check(load_library().sg_embed_rows_add(_p(ids), _p(pos), _p(table), _p(out), T, H, V, int(base), _stream()),
+           "embed_rows_add")
     return out
 
 

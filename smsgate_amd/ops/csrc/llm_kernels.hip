@@ -2068,6 +2068,30 @@ __global__ void __launch_bounds__(256) embed_rows_kernel(const int* __restrict__
   *reinterpret_cast<uint4*>(out + (size_t)i * H + 8 * c) = v;
 }
 
+// span-format prompt rows: table[ids[i]] + table[base + pos[i]] in one pass (the token's
+// row plus the row of pointer `pos[i]`), the sum rounded to bf16 like torch's bf16 add
+// (fp32 add, RNE).  Replaces a cast, two gathers and an add per prefill.
+__global__ void __launch_bounds__(256) embed_rows_add_kernel(const int* __restrict__ ids, const int* __restrict__ pos,
+                                                             const uint16_t* __restrict__ table,
+                                                             uint16_t* __restrict__ out, int T, int H, int V, int base) {
+  const int cpr = H >> 3;
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long long)T * cpr) return;
+  const int i = (int)(q / cpr), c = (int)(q % cpr);
+  const int t = ids[i], p = base + pos[i];
+  float a[8], b[8];
+  uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+  if (t >= 0 && t < V) va = *reinterpret_cast<const uint4*>(table + (size_t)t * H + 8 * c);
+  if (p >= 0 && p < V) vb = *reinterpret_cast<const uint4*>(table + (size_t)p * H + 8 * c);
+  unpack8(va, a);
+  unpack8(vb, b);
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    w[k] = (uint32_t)f2bf(a[2 * k] + b[2 * k]) | ((uint32_t)f2bf(a[2 * k + 1] + b[2 * k + 1]) << 16);
+  *reinterpret_cast<uint4*>(out + (size_t)i * H + 8 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 __global__ void __launch_bounds__(256) kv_copy_prefix_kernel(uint16_t* __restrict__ k_cache,
                                                              uint16_t* __restrict__ vt_cache,
                                                              const int* __restrict__ items, int n, int S_kv,
@@ -2122,6 +2146,16 @@ int sg_embed_rows(const int* ids, const void* table, void* out, int T, int H, in
   const long long n = (long long)T * (H >> 3);
   hipLaunchKernelGGL(embed_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ids,
                      (const uint16_t*)table, (uint16_t*)out, T, H, V);
+  return (int)hipGetLastError();
+}
+
+int sg_embed_rows_add(const int* ids, const int* pos, const void* table, void* out, int T, int H, int V, int base,
+                      hipStream_t stream) {
+  if (H % 8) return -1;
+  if (T == 0) return 0;
+  const long long n = (long long)T * (H >> 3);
+  hipLaunchKernelGGL(embed_rows_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ids, pos,
+                     (const uint16_t*)table, (uint16_t*)out, T, H, V, base);
   return (int)hipGetLastError();
 }
 

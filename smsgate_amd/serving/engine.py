@@ -526,11 +526,16 @@ class ExtractionEngine:
         qstart = meta_d[o:o + n]
         if kk is not None:
             self._copy_templates(kk, tsl, seq_slots)
-        flat_d = self._stage.to_device(flat, dev)
-        x = F.embedding(flat_d, self.w.embed)
-        if self.span:  # prompt position j also carries pointer j's row
-            x = x + F.embedding(pos_d.long() + self.fsm.ptr0, self.w.embed)
-        x = x.contiguous()
+        if self.span and self.w.embed.dtype == torch.bfloat16 and self.w.embed.is_contiguous():
+            # prompt position j also carries pointer j's row: one fused gather + add
+            flat_d = self._stage.to_device(flat.astype(np.int32), dev)
+            x = ops.embed_rows_add(flat_d, pos_d, self.w.embed, self.fsm.ptr0)
+        else:
+            flat_d = self._stage.to_device(flat, dev)
+            x = F.embedding(flat_d, self.w.embed)
+            if self.span:
+                x = x + F.embedding(pos_d.long() + self.fsm.ptr0, self.w.embed)
+            x = x.contiguous()
         max_q = int(lens.max())
         if self.spec or self.copy:  # the rows' prompts: draft source and copy set
             self.body_buf[slot_d.long(), pos_d.long()] = flat_d.to(torch.int32)

@@ -674,7 +674,14 @@ def _train_plan(args):
     tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
                      n_examples=args.train_steps * args.train_batch, log_every=200, data_parallel=False,
                      families="train", answer_format=args.answer_format)
-    src = open(ASSET, "rb").read() + open(synth.__file__, "rb").read()
+    # every source the trained weights depend on (a cached file from older training code
+    # on the same box was reused once: the key now covers the trainer, the answer FSM,
+    # the model and the tokenizer code too)
+    from smsgate_amd.models import extractor, tokenizer, train
+    from smsgate_amd.serving import fsm
+
+    src = b"".join(open(p, "rb").read() for p in (ASSET, synth.__file__, train.__file__, fsm.__file__,
+                                                    extractor.__file__, tokenizer.__file__))
     h = hashlib.sha256(repr((tc, EXTRACTOR_PROMPT, src)).encode(errors="ignore")).hexdigest()[:16]
     cache = args.weights_cache or os.path.join(tempfile.gettempdir(), f"smsgate-bench-w-{os.getpid()}")
     return tc, os.path.join(cache, f"{args.model}-{h}.safetensors")

@@ -3,7 +3,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
-timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 2 --verbose > gpurun_out/final.json 2> gpurun_out/final.err \
+timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 2 --verbose --weights-cache /tmp/fresh_$$ > gpurun_out/final.json 2> gpurun_out/final.err \
   || { tail -20 gpurun_out/final.err; exit 1; }
 python3 -c "
 import json; d=json.loads([l for l in open('gpurun_out/final.json') if l.startswith('{')][-1])

@@ -9,9 +9,14 @@ its broker stubbed.
 
 Here every message does strictly more work: extraction runs on a *real* LLM —
 the 134.5 M-parameter SmolLM2-135M-architecture extractor on the MI355X through
-the HIP kernels of ``smsgate_amd.ops``, schema-FSM-constrained decoding,
+the HIP kernels of ``smsgate_amd.ops``, schema-FSM-constrained decoding (span-
+pointer answers by default: two pointer tokens per copied field, ``--answer-format``),
 continuous batching and hipGraph-captured decode — and every parsed message
 goes on to the ``pb_writer`` stage and an in-memory sink inside the timed region.
+Traffic (``--traffic formats``): all 32 template families of ``utils/synth.py``,
+6 of them never trained on; the quality gate is the held-out families' exact-answer
+rate.  Ingest (``--ingest bus+http``): a timed phase through the brokers, then one
+through the native HTTP doors (``http_ingest`` in the JSON).
 
 Weights (``--weights``): no pretrained checkpoint exists on the box and a 270 MB
 file is not shipped, so by default the flagship is **trained in the run, before
@@ -21,8 +26,8 @@ other ranks load the file it publishes),
 then the timed traffic uses the *held-out* vocabulary (merchant / city / street
 names the model never saw).  The JSON states the weights' provenance, a held-out
 accuracy check, and the routing split (parsed / keyword-skipped / broken / DLQ).
-``--weights random`` is the old worst case (every message decodes to the
-schema caps, all LLM answers end in the DLQ); ``--weights PATH`` serves a
+``--weights random`` is the worst case (answers are noise and mostly end in the
+DLQ; a span answer is at most 25 decode steps); ``--weights PATH`` serves a
 checkpoint.  ``--backend fake`` reproduces the reference's stubbed-LLM
 configuration on the CPU for a like-for-like comparison.
 

@@ -645,10 +645,12 @@ __global__ void __launch_bounds__(256) sparse_argmax_kernel(
       // span start (serving/fsm.py build_span_fsm): pointer ptr0 + j to a body token at a
       // word boundary and in the field's class; never the closing <ans> (position bl-1)
       const int np = min(bl - 1, n_pos);
+      const bool no_mask = (cls & (4 | 8)) != 0;  // dates / numbers never start right after a card mask
       for (int j = lane; j < np; j += 64) {
         const int t = body[j];
-        const bool glued = j > 0 && (flags(body[j - 1]) & 2) && (flags(t) & 1);
-        if (!glued && (cls == 0 || (flags(t) & cls))) {
+        const int fp = j > 0 ? flags(body[j - 1]) : 0;
+        const bool glued = (fp & 2) && (flags(t) & 1);
+        if (!glued && (cls == 0 || (flags(t) & cls)) && !(no_mask && (fp & 64))) {
           const int c = ptr0 + j;
           if (c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
         }

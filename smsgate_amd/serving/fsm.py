@@ -85,6 +85,11 @@ TOK_STARTS_ALNUM, TOK_ENDS_ALNUM = 1, 2
 # token-class bits (span format: every token of a pointed-to span must be in the
 # field's class, as every copied token must be in copy format's schema mask)
 TOK_CLASS_BITS = {"date": 4, "number": 8, "currency": 16, "card": 32}
+# the token closes a card mask ("****", " *"): the digits after it are the card's, so a
+# date or a number never starts right after it (span format; "**** 7492 17.05.24" is not
+# the date "7492 17.05.24")
+TOK_ENDS_MASK = 64
+_NO_START_AFTER_MASK = TOK_CLASS_BITS["date"] | TOK_CLASS_BITS["number"]
 
 
 def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: int,
@@ -106,7 +111,8 @@ def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: in
         # (and likewise a token that closes with one after a digit, " 1," of "1,234.50")
         starts = t[0].isalnum() or t[0] == "\ufffd" or (len(t) > 1 and t[0] in ".,:" and t[1].isdigit())
         ends = t[-1].isalnum() or t[-1] == "\ufffd" or (len(t) > 1 and t[-1] in ".,:" and t[-2].isdigit())
-        out[i] |= (TOK_STARTS_ALNUM if starts else 0) | (TOK_ENDS_ALNUM if ends else 0)
+        out[i] |= (TOK_STARTS_ALNUM if starts else 0) | (TOK_ENDS_ALNUM if ends else 0) | \
+            (TOK_ENDS_MASK if t.endswith("*") else 0)
     return out
 
 # token classes by the characters of a token's text.  Dates may carry ASCII letters
@@ -279,8 +285,10 @@ class SchemaFSM:
 
         if kind & 0xFF == PTR_START:
             cand[self.sep_token] = True
+            no_mask = bool(cls & _NO_START_AFTER_MASK)
             for j in range(min(n, self.n_pos)):
-                if (j == 0 or self._boundary(body[j - 1], body[j])) and in_cls(body[j]):
+                if (j == 0 or self._boundary(body[j - 1], body[j])) and in_cls(body[j]) and \
+                        not (no_mask and j > 0 and 0 <= body[j - 1] < self.vocab and tf[body[j - 1]] & TOK_ENDS_MASK):
                     cand[self.ptr0 + j] = True
             return cand
         cap = (kind >> 8) & 0xFF

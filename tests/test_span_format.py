@@ -103,3 +103,22 @@ def test_checkpoint_carries_its_answer_format(tmp_path):
     assert got.cfg.span_positions == 130 and got.embed.shape[0] == 8448
     small = ExtractorWeights.load(bundled_checkpoint("small"), span_config(CONFIGS["small"]))
     assert small.cfg.span_positions == 0 and small.cfg.vocab == 8192
+
+
+def test_dates_and_numbers_never_start_inside_a_card_mask(fsms):
+    """'Карта **** 7492 17.05.24 ...': the digits after a mask are the card's -- a date or
+    an amount cannot start there (the held-out ru_karta_first layout's typical miss)."""
+    tk, f, _ = fsms
+    msg = tk.message_ids(["Карта **** 7492 17.05.24 покупка на сумму 41,76 AMD"], 128)[0]
+    strings = [tk.token_strings[t] for t in msg]
+    j_card = next(j for j, t in enumerate(strings) if t.strip() == "****") + 1  # " 7" of " 7" "492"
+    j_date = next(j for j, t in enumerate(strings) if t.strip().startswith("17"))
+    by_field = {x.name: i for i, x in enumerate(f.fields)}
+    for name, allowed in (("date", False), ("amount", False), ("card", True)):
+        st = [s for s in range(f.num_states)
+              if f.field_of_state[s] == by_field[name] and int(f.copy_kind[s]) & 0xFF == PTR_START][0]
+        m = f.copy_mask_host(st, -1, msg)
+        assert bool(m[f.ptr0 + j_card]) is allowed, name
+    date_st = [s for s in range(f.num_states)
+               if f.field_of_state[s] == by_field["date"] and int(f.copy_kind[s]) & 0xFF == PTR_START][0]
+    assert f.copy_mask_host(date_st, -1, msg)[f.ptr0 + j_date]

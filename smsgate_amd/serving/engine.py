@@ -334,10 +334,9 @@ class ExtractionEngine:
         # pinned staging of the prefill / compaction index arrays (a prefill of T tokens
         # and n prompts stages 2T + 4n + 1 int32 + T int64)
         # 6 slots: a slot is reused only after the GPU has run the copy that reads it, so the
-        # next admission waits for the previous one's copies to come up in the stream.  That wait
-        # paces admissions: with 32 slots the host no longer blocked (admission host time 3.9 ->
-        # 1.5 s per phase) but the GPU idled more (0.25-0.68 -> 0.93-1.1 s) and the bench ran
-        # 34.7-35.3 k vs 36.9-39.6 k msgs/s (profiles/r04_bench_final_ring32.json, PERF.md)
+        # next admission may wait for the previous one's copies to come up in the stream; 32
+        # slots removed that wait (admission host time 3.9 -> 1.5 s per phase) without a
+        # throughput change outside the box-to-box spread (profiles/PERF.md, round 4)
         self._stage = _PinnedRing(max(1 << 20, 12 * ec.prefill_max_tokens + 16 * S + 64), slots=6)
         self._pending: Optional[_Snapshot] = None
         self._sides: List[torch.cuda.Stream] = []  # side streams of the split decode / prefill

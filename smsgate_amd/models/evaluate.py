@@ -20,6 +20,7 @@ from decimal import Decimal
 from typing import Any, Dict, List, Optional, Sequence
 
 __all__ = ["score_answers", "evaluate_engine", "regex_answers", "golden_case_results", "golden_case_mismatches",
+           "TorchQAExtractor", "evaluate_negatives",
            "REFERENCE_EXPECTED"]
 
 _FIELDS = ("txn_type", "date", "amount", "currency", "card", "merchant", "city", "address", "balance")
@@ -125,6 +126,89 @@ def evaluate_engine(engine, n: int = 500, seed: int = 987654, vocab_name: str = 
     if with_regex:
         out["regex_exact"] = score_answers(items, regex_answers(items))["exact"]
     return out
+
+
+class TorchQAExtractor:
+    """A qa-format model (serving/qa.py) served by the PyTorch reference forward and
+    the host reference decoder -- the engine interface's ``run`` without the HIP path
+    (quality probes, CPU tests; serving/qa_engine.py is the GPU engine)."""
+
+    def __init__(self, weights, tokenizer=None, max_body: int = 128, batch: int = 256,
+                 compute_dtype=None) -> None:
+        import torch
+
+        from ..serving.qa import qa_layout, qa_token_flags
+        from .extractor import SPAN_PTR0
+        from .tokenizer import load_tokenizer
+
+        self.w = weights
+        self.tok = tokenizer or load_tokenizer()
+        cfg = weights.cfg
+        if cfg.qa_queries <= 0:
+            raise ValueError("TorchQAExtractor: not a qa-format model")
+        self.lay = qa_layout(SPAN_PTR0, cfg.span_positions, cfg.qa_queries)
+        self.flags = qa_token_flags(self.tok, self.lay.vocab)
+        self.max_body = max_body
+        self.batch = batch
+        self.compute_dtype = compute_dtype or torch.float32
+
+    def decode_ids(self, msgs: Sequence[Sequence[int]]):
+        """(class, spans) per message (``body <ans>`` ids)."""
+        import torch
+
+        from ..parse.schema import EXTRACTOR_PROMPT
+        from ..serving.qa import qa_decode_ref, qa_logits
+        from .extractor import reference_forward
+        from .train import qa_batch
+
+        prefix = self.tok.prefix_ids(EXTRACTOR_PROMPT)
+        dev = self.w.embed.device
+        out = []
+        for k in range(0, len(msgs), self.batch):
+            part = [list(m) for m in msgs[k:k + self.batch]]
+            exs = [(m, (0, [(-1, -1)] * self.lay.n_copy)) for m in part]
+            ids, add, qpos, _ = qa_batch(prefix, exs, self.tok.pad, dev, self.lay)
+            with torch.no_grad():
+                h = reference_forward(self.w, ids, compute_dtype=self.compute_dtype, return_hidden=True, add_ids=add)
+                cls, st, nl, en = (t.float().cpu().numpy() for t in qa_logits(h, self.w.embed, qpos, self.lay))
+            out += qa_decode_ref(cls, st, nl, en, part, self.flags, self.lay)
+        return out
+
+    def run(self, bodies: Sequence[str]) -> List[Dict[str, Optional[str]]]:
+        from ..serving.fsm import DEFAULT_FIELDS
+        from ..serving.qa import null_rejection, qa_expand
+
+        msgs = self.tok.message_ids(list(bodies), self.max_body)
+        dec = self.decode_ids(msgs)
+        toks = [qa_expand(self.tok, self.lay, c, sp, m) for (c, sp), m in zip(dec, msgs)]
+        names = [f.name for f in DEFAULT_FIELDS]
+        return [null_rejection(dict(zip(names, vals))) for vals in self.tok.decode_fields(toks, len(names))]
+
+
+def evaluate_negatives(engine, n: int = 500, seed: int = 4244, vocab_name: str = "heldout",
+                       families: Any = "neg_heldout") -> Dict[str, Any]:
+    """Non-transaction SMS (utils/synth.py NEG_FAMILIES) through the extractor and the
+    real post-processing: ``false_parsed_rate`` = the share that would be published on
+    sms.parsed (the reference routes them to the DLQ as unmatched), per family too."""
+    from ..parse.text import normalize_body
+    from ..utils.synth import generate
+
+    items = generate(n, seed=seed, vocab_name=vocab_name, families=families)
+    answers = engine.run([normalize_body(s.body) for s in items])
+    fam_n: Dict[str, int] = {}
+    fam_bad: Dict[str, int] = {}
+    bad = 0
+    txn: Dict[str, int] = {}
+    for it, ans in zip(items, answers):
+        fam_n[it.family] = fam_n.get(it.family, 0) + 1
+        t = str((ans or {}).get("txn_type"))
+        txn[t] = txn.get(t, 0) + 1
+        parsed = _post(it.body, it.timestamp, ans) is not None
+        bad += parsed
+        fam_bad[it.family] = fam_bad.get(it.family, 0) + parsed
+    return {"n": len(items), "false_parsed_rate": bad / max(1, len(items)), "families": families,
+            "by_family": {f: round(fam_bad.get(f, 0) / c, 4) for f, c in sorted(fam_n.items())},
+            "txn_type": dict(sorted(txn.items()))}
 
 
 def golden_case_results(engine) -> List[Optional[Dict[str, Any]]]:

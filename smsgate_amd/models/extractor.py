@@ -25,7 +25,7 @@ import torch
 import torch.nn.functional as F
 
 __all__ = ["ExtractorConfig", "CONFIGS", "ExtractorWeights", "reference_forward", "count_params", "span_config",
-           "SPAN_PTR0"]
+           "SPAN_PTR0", "qa_config"]
 
 
 @dataclass(frozen=True)
@@ -45,6 +45,10 @@ class ExtractorConfig:
     # rows ptr0 .. ptr0 + span_positions - 1 are the pointer tokens, and row ptr0 + j is
     # added to the input of prompt position j
     span_positions: int = 0
+    # > 0: the one-forward span format (serving/qa.py): this many query tokens follow
+    # ``body <ans>``; the span_positions pointer rows are as above, plus the end-pointer,
+    # query, null and class rows of qa_layout
+    qa_queries: int = 0
 
     @property
     def qkv_out(self) -> int:
@@ -77,6 +81,14 @@ def span_config(cfg: ExtractorConfig, positions: int = 130) -> ExtractorConfig:
     (SmolLM2's 49 152 rows already do; the 8 192-row small models grow by 256)."""
     vocab = max(cfg.vocab, -(-(SPAN_PTR0 + positions) // 128) * 128)
     return dataclasses.replace(cfg, vocab=vocab, span_positions=positions)
+
+
+def qa_config(cfg: ExtractorConfig, positions: int = 130, queries: int = 9) -> ExtractorConfig:
+    """``cfg`` for the one-forward span format (serving/qa.py qa_layout)."""
+    from ..serving.qa import qa_layout
+
+    lay = qa_layout(SPAN_PTR0, positions, queries)
+    return dataclasses.replace(cfg, vocab=max(cfg.vocab, lay.vocab), span_positions=positions, qa_queries=queries)
 
 
 def count_params(cfg: ExtractorConfig) -> int:
@@ -130,7 +142,8 @@ class ExtractorWeights(torch.nn.Module):
         with safe_open(path, framework="pt") as fh:  # the answer format is the checkpoint's own (metadata)
             meta = fh.metadata() or {}
         cfg = dataclasses.replace(cfg, vocab=int(meta.get("vocab", cfg.vocab)),
-                                  span_positions=int(meta.get("span_positions", "0") or 0))
+                                  span_positions=int(meta.get("span_positions", "0") or 0),
+                                  qa_queries=int(meta.get("qa_queries", "0") or 0))
         w = cls(cfg, device="meta" if device is None else device, dtype=dtype, seed=None)
         sd = load_file(path, device=str(device) if device is not None else "cpu")
         w.load_state_dict({k: v.to(dtype) for k, v in sd.items()}, assign=True)

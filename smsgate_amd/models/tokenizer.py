@@ -124,6 +124,18 @@ class ExtractorTokenizer:
         ``value`` whose tokens decode back to it (:meth:`value_span_ids`; the span
         format points at these two positions), or None."""
         body, value = model_text(body), model_text(value)  # the offsets index the model text
+        sp = self._value_span(value, body, ids, offsets, strict=True)
+        # a value glued to a word of the other kind ("52.00" in "USD52.00", "1234" in
+        # "x1234"): only when it occurs nowhere at a full word boundary, so a number inside
+        # a merchant name ("AB52") never shadows the real amount
+        return sp if sp is not None else self._value_span(value, body, ids, offsets, strict=False)
+
+    def _value_span(self, value: str, body: str, ids, offsets, strict: bool) -> Optional[Tuple[int, int]]:
+        def glued(x: str, y: str) -> bool:
+            if strict:
+                return x.isalnum() and y.isalnum()
+            return (x.isalpha() and y.isalpha()) or (x.isdigit() and y.isdigit())
+
         start = 0
         while True:
             a = body.find(value, start)
@@ -133,8 +145,7 @@ class ExtractorTokenizer:
             # an occurrence inside a longer word is not the value ("AM" in "AMERIABANK"
             # vs the city ", AM&#10;"): values are copied at word boundaries (the copy
             # constraint, serving/fsm.py, only lets a value start and end there)
-            if (a > 0 and value[0].isalnum() and body[a - 1].isalnum()) or \
-                    (z < len(body) and value[-1].isalnum() and body[z].isalnum()):
+            if (a > 0 and glued(body[a - 1], value[0])) or (z < len(body) and glued(value[-1], body[z])):
                 start = a + 1
                 continue
             k0 = next((k for k, (s, e) in enumerate(offsets) if s <= a < e), None)

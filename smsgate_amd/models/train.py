@@ -47,11 +47,11 @@ import torch.nn.functional as F
 
 from ..parse.schema import EXTRACTOR_PROMPT
 from ..parse.text import normalize_body
-from .extractor import CONFIGS, SPAN_PTR0, ExtractorWeights, reference_forward, span_config
+from .extractor import CONFIGS, SPAN_PTR0, ExtractorWeights, qa_config, reference_forward, span_config
 from .tokenizer import ExtractorTokenizer, load_tokenizer
 
 __all__ = ["TrainConfig", "answer_tokens", "answer_span_tokens", "answer_fsm", "make_examples", "ExamplePool", "train_extractor", "field_accuracy",
-           "latest_checkpoint", "to_serving"]
+           "latest_checkpoint", "to_serving", "qa_batch", "QASpec"]
 
 
 @dataclass
@@ -86,6 +86,9 @@ class TrainConfig:
     # "copy": every copied value written with the body's own tokens; "span": as two
     # pointers to its first and last body token (serving/fsm.py build_span_fsm)
     answer_format: str = "copy"
+    # share of training examples drawn from the non-transaction families (utils/synth.py
+    # NEG_TRAIN_FAMILIES: answer txn_type unknown / otp, every other field null)
+    negatives: float = 0.12
 
 
 def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]],
@@ -141,37 +144,74 @@ def answer_span_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[
     return ids if state == fsm.done_state else None
 
 
+class QASpec:
+    """The one-forward span format's training view (serving/qa.py): the id layout and
+    the token flags its decoder checks gold spans against."""
+    span = False
+    qa = True
+
+    def __init__(self, lay, flags) -> None:
+        self.lay, self.flags = lay, flags
+
+    @property
+    def ptr0(self) -> int:
+        return self.lay.ptr0
+
+    @property
+    def vocab(self) -> int:
+        return self.lay.vocab
+
+    @property
+    def n_pos(self) -> int:
+        return self.lay.n_pos
+
+
 def answer_fsm(tok: ExtractorTokenizer, fmt: str = "copy", max_body: int = 128):
     """The schema FSM the training targets are written for (vocabulary trimmed to the
     tokenizer's ids, plus the pointer ids in span format)."""
     from ..serving.fsm import build_fsm, build_span_fsm, span_positions
 
     v_tok = (tok.vocab_size + 63) // 64 * 64
+    if fmt in ("qa", "qa17"):
+        from ..serving.qa import qa_layout, qa_token_flags
+
+        lay = qa_layout(v_tok, span_positions(max_body), 9 if fmt == "qa" else 17)
+        return QASpec(lay, qa_token_flags(tok, lay.vocab))
     if fmt == "span":
         assert v_tok == SPAN_PTR0, "the span format's pointer ids follow the 8 192-id tokenizer"
         return build_span_fsm(tok, v_tok, span_positions(max_body))
     if fmt != "copy":
-        raise ValueError(f"answer format {fmt!r}: copy | span")
+        raise ValueError(f"answer format {fmt!r}: copy | span | qa | qa17")
     return build_fsm(tok, v_tok)
 
 
 def make_examples(tok: ExtractorTokenizer, fsm, n: int, seed: int,
                   max_body: int = 128, vocab_name: str = "train",
-                  families: Optional[str] = "train") -> List[Tuple[List[int], List[int]]]:
-    """``(message ids, answer ids)`` pairs (prefix excluded: it is shared); span-format
-    answers when ``fsm`` is a span FSM."""
+                  families: Optional[str] = "train", negatives: float = 0.0) -> List[Tuple[List[int], object]]:
+    """``(message ids, answer)`` pairs (prefix excluded: it is shared): answer ids in the
+    copy / span formats, ``(class, spans)`` in the qa format (serving/qa.py qa_targets).
+    ``negatives``: share of non-transaction examples (``families`` must be a split)."""
     from ..utils.synth import HELDOUT_FAMILIES, generate, family_names
 
     if families is not None:
         assert not set(family_names(families)) & set(HELDOUT_FAMILIES), "held-out families are never trained on"
     out: List[Tuple[List[int], List[int]]] = []
-    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name, families=families, training=True)
+    items = [s for s in generate(n, seed=seed, vocab_name=vocab_name, families=families, training=True,
+                                 negatives=negatives if families is not None else 0.0)
              if s.answer is not None]
     bodies = [normalize_body(s.body) for s in items]
     msgs = tok.message_ids(bodies, max_body)
     encs = tok.encode_offsets(bodies)
+    qa = getattr(fsm, "qa", False)
+    if qa:
+        from ..serving.qa import qa_targets
     for m, s, b, e in zip(msgs, items, bodies, encs):
-        a = answer_span_tokens(tok, fsm, s.answer, b, e, len(m)) if fsm.span else answer_tokens(tok, fsm, s.answer, b, e)
+        if qa:
+            a = qa_targets(tok, fsm.lay, fsm.flags, s.answer, b, e, len(m))
+        elif fsm.span:
+            a = answer_span_tokens(tok, fsm, s.answer, b, e, len(m))
+        else:
+            a = answer_tokens(tok, fsm, s.answer, b, e)
         if a is not None:
             out.append((m, a))
     return out
@@ -186,9 +226,9 @@ def _pool_init(tok_path: str, fmt: str = "copy", max_body: int = 128) -> None:
     _POOL_STATE["fsm"] = answer_fsm(tok, fmt, max_body)
 
 
-def _pool_chunk(args) -> List[Tuple[List[int], List[int]]]:
-    n, seed, max_body, vocab_name, families = args
-    return make_examples(_POOL_STATE["tok"], _POOL_STATE["fsm"], n, seed, max_body, vocab_name, families)
+def _pool_chunk(args) -> List[Tuple[List[int], object]]:
+    n, seed, max_body, vocab_name, families, negatives = args
+    return make_examples(_POOL_STATE["tok"], _POOL_STATE["fsm"], n, seed, max_body, vocab_name, families, negatives)
 
 
 class ExamplePool:
@@ -202,12 +242,12 @@ class ExamplePool:
 
     def __init__(self, n: int, seed: int = 0, max_body: int = 128, vocab_name: str = "train",
                  families: Optional[str] = "train", workers: int = 8, chunk: int = 4096,
-                 tok_path: Optional[str] = None, answer_format: str = "copy") -> None:
+                 tok_path: Optional[str] = None, answer_format: str = "copy", negatives: float = 0.0) -> None:
         import multiprocessing as mp
 
         from .tokenizer import ASSET
 
-        jobs = [(min(chunk, n - k * chunk), seed * 7919 + k, max_body, vocab_name, families)
+        jobs = [(min(chunk, n - k * chunk), seed * 7919 + k, max_body, vocab_name, families, negatives)
                 for k in range((n + chunk - 1) // chunk)]
         self.n = n
         self._pool = mp.get_context("spawn").Pool(max(1, min(workers, len(jobs))), initializer=_pool_init,
@@ -240,6 +280,35 @@ def _batch(prefix: List[int], exs: Sequence[Tuple[List[int], List[int]]], pad: i
         if add is not None:
             add[i, P:start] = torch.arange(ptr0, ptr0 + len(m))
     return ids.to(device), labels.to(device), (add.to(device) if add is not None else None)
+
+
+def qa_batch(prefix: List[int], exs, pad: int, device, lay):
+    """qa-format batch: ids ``prefix + message + queries``, the pointer row added to each
+    message position (-1 elsewhere), the query rows' positions and the targets
+    (class, starts, ends, pointable positions) of serving/qa.py qa_loss."""
+    q = lay.query_ids()
+    NQ, NF = len(q), lay.n_copy
+    seqs = [prefix + m + q for m, _ in exs]
+    T = max(len(s) for s in seqs)
+    B = len(exs)
+    ids = torch.full((B, T), pad, dtype=torch.long)
+    add = torch.full((B, T), -1, dtype=torch.long)
+    qpos = torch.zeros((B, NQ), dtype=torch.long)
+    t_cls = torch.zeros(B, dtype=torch.long)
+    t_s = torch.full((B, NF), -1, dtype=torch.long)
+    t_e = torch.full((B, NF), -1, dtype=torch.long)
+    npos = torch.zeros(B, dtype=torch.long)
+    P = len(prefix)
+    for i, ((m, (c, spans)), s) in enumerate(zip(exs, seqs)):
+        ids[i, : len(s)] = torch.tensor(s)
+        add[i, P:P + len(m)] = torch.arange(lay.ptr0, lay.ptr0 + len(m))
+        qpos[i] = torch.arange(P + len(m), P + len(m) + NQ)
+        t_cls[i] = c
+        npos[i] = len(m) - 1
+        for f, (a, z) in enumerate(spans):
+            t_s[i, f], t_e[i, f] = a, z
+    dv = lambda t: t.to(device)  # noqa: E731
+    return dv(ids), dv(add), dv(qpos), (dv(t_cls), dv(t_s), dv(t_e), dv(npos))
 
 
 def latest_checkpoint(ckpt_dir: Optional[str]) -> Optional[Path]:
@@ -298,12 +367,16 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     tok = tok or load_tokenizer()
     mcfg = CONFIGS[cfg.model]
     fsm = answer_fsm(tok, cfg.answer_format, cfg.max_body_tokens)
+    qa = getattr(fsm, "qa", False)
     if fsm.span:
         mcfg = span_config(mcfg, fsm.n_pos)
+    elif qa:
+        mcfg = qa_config(mcfg, fsm.n_pos, fsm.lay.n_queries)
     v_dec = min(mcfg.vocab, fsm.vocab)
     t0 = time.perf_counter()
     if data is None:
-        data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens, cfg.vocab_name, cfg.families)
+        data = make_examples(tok, fsm, cfg.n_examples, cfg.seed, cfg.max_body_tokens, cfg.vocab_name, cfg.families,
+                             cfg.negatives)
     log(f"train: {len(data)} examples ({time.perf_counter() - t0:.1f}s), model {cfg.model}")
     prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
     torch.manual_seed(cfg.seed)
@@ -353,13 +426,21 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     for step in range(start, cfg.steps):
         for g in opt.param_groups:
             g["lr"] = lr_at(step)
-        ids, labels, add = _batch(prefix, rng.sample(data, cfg.batch), tok.pad, device, fsm.ptr0)
+        exs = rng.sample(data, cfg.batch)
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=str(device).startswith("cuda")):
-            h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True, add_ids=add)
-            sel = labels.view(-1) >= 0
-            hs = h.reshape(-1, h.shape[-1])[sel]
-            logits = hs @ w.embed[:v_dec].t()
-            loss = F.cross_entropy(logits.float(), labels.view(-1)[sel])
+            if qa:
+                from ..serving.qa import qa_logits, qa_loss
+
+                ids, add, qpos, targets = qa_batch(prefix, exs, tok.pad, device, fsm.lay)
+                h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True, add_ids=add)
+                loss = qa_loss(qa_logits(h, w.embed, qpos, fsm.lay), targets, fsm.lay)
+            else:
+                ids, labels, add = _batch(prefix, exs, tok.pad, device, fsm.ptr0)
+                h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True, add_ids=add)
+                sel = labels.view(-1) >= 0
+                hs = h.reshape(-1, h.shape[-1])[sel]
+                logits = hs @ w.embed[:v_dec].t()
+                loss = F.cross_entropy(logits.float(), labels.view(-1)[sel])
         if gb is not None:
             gb.zero_grad()
             loss.backward()  # bucket all-reduces start as gradients land

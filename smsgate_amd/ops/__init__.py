@@ -40,6 +40,9 @@ __all__ = [
     "fsm_commit",
     "gemm_argmax",
     "copy_masks",
+    "qa_decode",
+    "qa_params",
+    "embed_rows_add_ids",
     "ref_copy_masks",
     "SPEC_MAX_K",
     "gemm",
@@ -142,6 +145,13 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_copy_masks.argtypes = [_vp, _ip, _c_int, _c_int, _ip, _vp, _ip, _ip, _ip, _ip, _ip, _c_int, _c_int, _vp,
                                   _vp]
     lib.sg_copy_masks.restype = _c_int
+    lib.sg_qa_decode.argtypes = [_vp, _vp, _c_int, _vp, _c_int, _c_float, _ip, _ip, _vp, _c_int, _ip, _ip, _vp, _vp,
+                                 _c_int, _vp]
+    lib.sg_qa_decode.restype = _c_int
+    lib.sg_qa_params_size.argtypes = []
+    lib.sg_qa_params_size.restype = _c_int
+    lib.sg_embed_rows_add_ids.argtypes = [_ip, _ip, _vp, _vp, _c_int, _c_int, _c_int, _vp]
+    lib.sg_embed_rows_add_ids.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version", "sg_kv_copy_prefix"):
         getattr(lib, f).restype = _c_int
@@ -859,6 +869,105 @@ def embed_rows_add(ids: torch.Tensor, pos: torch.Tensor, table: torch.Tensor, ba
     out = table.new_empty((T, H))
     _check(load_library().sg_embed_rows_add(_p(ids), _p(pos), _p(table), _p(out), T, H, V, int(base), _stream()),
            "embed_rows_add")
+    return out
+
+
+QA_MAX_NF, QA_MAX_NQ, QA_MAX_POS, QA_NCLS, QA_MAX_CLS_TOK = 8, 24, 160, 4, 8
+
+
+class QAParams(ctypes.Structure):
+    """``QAParams`` of csrc/qa_kernels.hip (plain ints, same order)."""
+    _fields_ = [("nf", _c_int), ("nq", _c_int), ("n_pos", _c_int),
+                ("start_row", _c_int * QA_MAX_NF), ("end_row", _c_int * QA_MAX_NF),
+                ("cls_bits", _c_int * QA_MAX_NF), ("cap", _c_int * QA_MAX_NF),
+                ("off_end", _c_int), ("off_null", _c_int), ("off_cls", _c_int),
+                ("cls_tok", (_c_int * QA_MAX_CLS_TOK) * QA_NCLS), ("cls_len", _c_int * QA_NCLS),
+                ("reject_mask", _c_int), ("sep", _c_int), ("max_out", _c_int)]
+
+
+def qa_params(lay, tokenizer) -> QAParams:
+    """Kernel parameters of a qa layout (serving/qa.py): query rows, field classes and
+    caps, the W row offsets (W = rows ptr0 .. cls0 + 3 of the final-norm-folded
+    embedding), the class tokens of the copy-format answer."""
+    from ..parse.schema import TXN_TYPES
+    from ..serving.qa import REJECT_TXN, qa_rows
+
+    p = QAParams()
+    nf = lay.n_copy
+    if nf > QA_MAX_NF or lay.n_queries > QA_MAX_NQ or lay.n_pos > QA_MAX_POS:
+        raise ValueError("qa_params: layout exceeds the kernel's limits")
+    p.nf, p.nq, p.n_pos = nf, lay.n_queries, lay.n_pos
+    srows, erows = qa_rows(lay)
+    for f in range(nf):
+        p.start_row[f], p.end_row[f] = srows[f], erows[f]
+        p.cls_bits[f], p.cap[f] = lay.class_bits()[f], lay.caps()[f]
+    p.off_end, p.off_null, p.off_cls = lay.pe0 - lay.ptr0, lay.null_id - lay.ptr0, lay.cls0 - lay.ptr0
+    for c, name in enumerate(TXN_TYPES):
+        toks = tokenizer.encode(name)
+        if not 0 < len(toks) <= QA_MAX_CLS_TOK:
+            raise ValueError(f"qa_params: class {name!r} encodes to {len(toks)} tokens")
+        for k, t in enumerate(toks):
+            p.cls_tok[c][k] = t
+        p.cls_len[c] = len(toks)
+        if name in REJECT_TXN:
+            p.reject_mask |= 1 << c
+    p.sep, p.max_out = tokenizer.sep, lay.max_answer_tokens()
+    if load_library().sg_qa_params_size() != ctypes.sizeof(QAParams):
+        raise RuntimeError("QAParams layout differs from csrc/qa_kernels.hip")
+    return p
+
+
+def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, ids: torch.Tensor,
+              flags: torch.Tensor, params: QAParams, out_buf: torch.Tensor, out_len: torch.Tensor,
+              dbg_scores: Optional[torch.Tensor] = None, dbg_spans: Optional[torch.Tensor] = None) -> None:
+    """The qa format's head (``qa_decode_kernel``): for every sequence ``m`` of a packed
+    prefill batch (rows ``cu[m]:cu[m+1]``, the last ``params.nq`` of them its query
+    rows), scores of the query rows against W (RMSNorm from the un-normed rows ``h``,
+    weight folded into W), the class and every field's joint constrained span decode,
+    and the answer in the copy format into ``out_buf[m]`` / ``out_len[m]``.
+    ``dbg_scores`` [M, 4 + nf (2 n_pos + 1)] fp32 / ``dbg_spans`` [M, 1 + 2 nf] int32:
+    the raw scores and the decoded (class, start, end ...) for tests."""
+    M = cu.numel() - 1
+    T, H = h.shape[0], h.shape[1]
+    if h.dtype != torch.bfloat16 or h.stride(1) != 1 or h.stride(0) % 8 or not h.is_cuda:
+        raise ValueError("qa_decode: bf16 rows with 16-B aligned strides required")
+    R = params.off_cls + QA_NCLS
+    if W.dtype != torch.bfloat16 or not W.is_contiguous() or W.shape[1] != H or W.shape[0] < R:
+        raise ValueError(f"qa_decode: W must be bf16 [>= {R}, {H}]")
+    for t, name in ((cu, "cu"), (ids, "ids"), (out_len, "out_len")):
+        _req(t, torch.int32, name)
+    if ids.numel() < T or out_len.numel() < M or out_buf.dtype != torch.int32 or not out_buf.is_contiguous():
+        raise ValueError("qa_decode: ids / out_len / out_buf too small")
+    if out_buf.dim() != 2 or out_buf.shape[0] < M or out_buf.shape[1] != params.max_out:
+        raise ValueError(f"qa_decode: out_buf must be int32 [>= {M}, {params.max_out}]")
+    if flags.dtype not in (torch.int16, torch.uint16) or not flags.is_contiguous():
+        raise ValueError("qa_decode: flags must be a contiguous 16-bit table")
+    per = QA_NCLS + params.nf * (2 * params.n_pos + 1)
+    if dbg_scores is not None and (dbg_scores.dtype != torch.float32 or dbg_scores.numel() < M * per):
+        raise ValueError(f"qa_decode: dbg_scores must be fp32 [{M}, {per}]")
+    if dbg_spans is not None and (dbg_spans.dtype != torch.int32 or dbg_spans.numel() < M * (1 + 2 * params.nf)):
+        raise ValueError("qa_decode: dbg_spans too small")
+    if M == 0:
+        return
+    _check(load_library().sg_qa_decode(ctypes.byref(params), _p(h), h.stride(0), _p(W), H, float(eps), _p(cu),
+                                       _p(ids), _p(flags), flags.numel(), _p(out_buf), _p(out_len), _p(dbg_scores),
+                                       _p(dbg_spans), M, _stream()), "qa_decode")
+
+
+def embed_rows_add_ids(ids: torch.Tensor, add: torch.Tensor, table: torch.Tensor,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``table[ids] + table[add]`` (no second row where ``add < 0``), bf16 rounded like
+    torch's add -- the qa format's prompt rows (pointer rows on message tokens only)."""
+    _req(ids, torch.int32, "ids")
+    _req(add, torch.int32, "add")
+    V, H = table.shape
+    if table.dtype != torch.bfloat16 or not table.is_contiguous() or H % 8 or add.numel() != ids.numel():
+        raise ValueError("embed_rows_add_ids: contiguous bf16 table with H % 8 == 0 and one add id per id")
+    T = ids.numel()
+    if out is None:
+        out = table.new_empty((T, H))
+    _check(load_library().sg_embed_rows_add_ids(_p(ids), _p(add), _p(table), _p(out), T, H, V, _stream()),
+           "embed_rows_add_ids")
     return out
 
 

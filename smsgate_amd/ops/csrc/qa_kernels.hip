@@ -1,0 +1,354 @@
+// smsgate_amd — one-forward span extraction head (serving/qa.py, gfx950).
+//
+// After the prefill forward of `body <ans> q_0 .. q_{nq-1}` (the native prefill,
+// csrc/runtime.hip), the last nq rows of every sequence are its query rows.  One
+// block per message:
+//
+//   1. stage the nq query rows (bf16, LDS) and their RMSNorm scales (the final norm's
+//      weight is folded into W, ops.fold_norm) and the message's prompt ids / token
+//      flags;
+//   2. scores: every W row the message needs is read ONCE and dotted with every query
+//      row that uses it -- start-pointer row j with the nf start rows, end-pointer row j
+//      with the nf end rows, the null row with the start rows, class row c with query
+//      row 0.  Four lanes per W row (a quarter of H each, 16-B chunks), 16 W rows per
+//      wave pass, fp32 accumulation, fp32 scores in LDS;
+//   3. decode (one wave per field, fields w and w + 4): the class is the arg-max of the
+//      four class scores; per copied field the null decision (null score >= every
+//      valid start's score, or no valid pair) and the joint arg-max of
+//      start[s] + end[e] over valid pairs -- s at a word boundary and in the field's
+//      class (and, for dates / numbers, not right after a card mask), e >= s within
+//      the cap, every token s..e in class, e followed by a word boundary.  Word
+//      boundary: NOT (a ends with a letter and b starts with one, or a ends with a
+//      digit and b starts with one).  One lane per start, its ends scanned in order;
+//      ties go to the lower start, then the lower end (serving/qa.py qa_decode_ref);
+//   4. the answer in the copy format (class tokens, <sep>, each field's body tokens
+//      and <sep>; a rejection class: only its tokens and <sep>) into out_buf.
+//
+// Optional outputs for tests: the raw scores and the decoded (class, spans).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define QA_MAX_NF 8
+#define QA_MAX_NQ 24
+#define QA_MAX_POS 160
+#define QA_NCLS 4
+#define QA_MAX_CLS_TOK 8
+
+#define QF_SL 1
+#define QF_SD 2
+#define QF_EL 4
+#define QF_ED 8
+#define QF_MASK 16
+#define QF_NO_START_AFTER_MASK (32 | 64)  // date | number class bits
+
+struct QAParams {
+  int nf, nq, n_pos;
+  int start_row[QA_MAX_NF];
+  int end_row[QA_MAX_NF];
+  int cls_bits[QA_MAX_NF];
+  int cap[QA_MAX_NF];
+  int off_end, off_null, off_cls;  // W rows relative to start-pointer row 0
+  int cls_tok[QA_NCLS][QA_MAX_CLS_TOK];
+  int cls_len[QA_NCLS];
+  int reject_mask;  // bit c: class c is a non-transaction (no fields)
+  int sep, max_out;
+};
+
+static __device__ __forceinline__ float qa_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+static __device__ __forceinline__ bool qa_glued(int fa, int fb) {
+  return ((fa & QF_EL) && (fb & QF_SL)) || ((fa & QF_ED) && (fb & QF_SD));
+}
+
+__global__ void __launch_bounds__(256) qa_decode_kernel(
+    QAParams p, const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ W, int H, float eps,
+    const int* __restrict__ cu, const int* __restrict__ ids, const uint16_t* __restrict__ flags, int V,
+    int* __restrict__ out_buf, int* __restrict__ out_len, float* __restrict__ dbg_scores,
+    int* __restrict__ dbg_spans) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t hq[];  // [nq][H] bf16
+  __shared__ float rs[QA_MAX_NQ];
+  __shared__ float sc_start[QA_MAX_NF][QA_MAX_POS];
+  __shared__ float sc_end[QA_MAX_NF][QA_MAX_POS];
+  __shared__ float sc_null[QA_MAX_NF];
+  __shared__ float sc_cls[QA_NCLS];
+  __shared__ uint16_t fb[QA_MAX_POS];
+  __shared__ int body[QA_MAX_POS];
+  __shared__ int span_s[QA_MAX_NF], span_e[QA_MAX_NF];
+  __shared__ int cls_sel;
+
+  const int m = blockIdx.x;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int nq = p.nq, nf = p.nf;
+  const int r0 = cu[m], r1 = cu[m + 1];
+  const int qrow0 = r1 - nq;
+  const int n = min(qrow0 - r0 - 1, p.n_pos);  // pointable positions (the body; <ans> excluded)
+  const int nch = H >> 3;                       // 16-B chunks per row
+
+  // ---- 1. stage
+  for (int k = tid; k < nq * nch; k += 256) {
+    const int q = k / nch, c = k - q * nch;
+    *reinterpret_cast<uint4*>(hq + (size_t)q * H + 8 * c) =
+        *reinterpret_cast<const uint4*>(h + (size_t)(qrow0 + q) * ldh + 8 * c);
+  }
+  for (int j = tid; j < n; j += 256) {
+    const int t = ids[r0 + j];
+    body[j] = t;
+    fb[j] = (t >= 0 && t < V) ? flags[t] : (uint16_t)0;
+  }
+  __syncthreads();
+  for (int q = wid; q < nq; q += 4) {
+    float ss = 0.f;
+    const uint32_t* hr = reinterpret_cast<const uint32_t*>(hq + (size_t)q * H);
+    for (int k = lane; k < (H >> 1); k += 64) {
+      const uint32_t u = hr[k];
+      const float lo = qa_bf2f((uint16_t)(u & 0xffffu)), hi = qa_bf2f((uint16_t)(u >> 16));
+      ss = fmaf(lo, lo, fmaf(hi, hi, ss));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    if (lane == 0) rs[q] = rsqrtf(ss / (float)H + eps);
+  }
+  __syncthreads();
+
+  // ---- 2. scores.  Items: [0, n) start rows, [n, 2n) end rows, 2n the null row,
+  // 2n+1 .. 2n+4 the class rows.  16 items per wave pass, four lanes each.
+  const int items = 2 * n + 1 + QA_NCLS;
+  const int ci = lane >> 2, qd = lane & 3, QD = H >> 2, qch = QD >> 3;
+  for (int i0 = wid * 16; i0 < items; i0 += 64) {
+    const int it = i0 + ci;
+    float acc[QA_MAX_NF];
+#pragma unroll
+    for (int f = 0; f < QA_MAX_NF; ++f) acc[f] = 0.f;
+    int wrow = -1, kind = 0;  // kind 0 start, 1 end, 2 null, 3 class
+    if (it < n) { wrow = it; kind = 0; }
+    else if (it < 2 * n) { wrow = p.off_end + (it - n); kind = 1; }
+    else if (it == 2 * n) { wrow = p.off_null; kind = 2; }
+    else if (it < items) { wrow = p.off_cls + (it - 2 * n - 1); kind = 3; }
+    if (wrow >= 0) {
+      const uint16_t* wr = W + (size_t)wrow * H + qd * QD;
+      for (int k = 0; k < qch; ++k) {
+        const uint4 wu = *reinterpret_cast<const uint4*>(wr + 8 * k);
+        const uint32_t a4[4] = {wu.x, wu.y, wu.z, wu.w};
+        float wf[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          wf[2 * e] = qa_bf2f((uint16_t)(a4[e] & 0xffffu));
+          wf[2 * e + 1] = qa_bf2f((uint16_t)(a4[e] >> 16));
+        }
+        if (kind == 3) {
+          const uint4 hu = *reinterpret_cast<const uint4*>(hq + qd * QD + 8 * k);  // query row 0
+          const uint32_t b4[4] = {hu.x, hu.y, hu.z, hu.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            acc[0] = fmaf(wf[2 * e], qa_bf2f((uint16_t)(b4[e] & 0xffffu)), acc[0]);
+            acc[0] = fmaf(wf[2 * e + 1], qa_bf2f((uint16_t)(b4[e] >> 16)), acc[0]);
+          }
+        } else {
+#pragma unroll
+          for (int f = 0; f < QA_MAX_NF; ++f) {
+            if (f < nf) {
+              const int q = kind == 1 ? p.end_row[f] : p.start_row[f];
+              const uint4 hu = *reinterpret_cast<const uint4*>(hq + (size_t)q * H + qd * QD + 8 * k);
+              const uint32_t b4[4] = {hu.x, hu.y, hu.z, hu.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                acc[f] = fmaf(wf[2 * e], qa_bf2f((uint16_t)(b4[e] & 0xffffu)), acc[f]);
+                acc[f] = fmaf(wf[2 * e + 1], qa_bf2f((uint16_t)(b4[e] >> 16)), acc[f]);
+              }
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < QA_MAX_NF; ++f) {
+      acc[f] += __shfl_xor(acc[f], 1, 64);
+      acc[f] += __shfl_xor(acc[f], 2, 64);
+    }
+    if (wrow >= 0 && qd == 0) {
+      if (kind == 3) {
+        sc_cls[it - 2 * n - 1] = acc[0] * rs[0];
+      } else {
+#pragma unroll
+        for (int f = 0; f < QA_MAX_NF; ++f) {
+          if (f < nf) {
+            if (kind == 0) sc_start[f][it] = acc[f] * rs[p.start_row[f]];
+            else if (kind == 1) sc_end[f][it - n] = acc[f] * rs[p.end_row[f]];
+            else sc_null[f] = acc[f] * rs[p.start_row[f]];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. decode
+  if (tid == 0) {
+    int c = 0;
+    for (int k = 1; k < QA_NCLS; ++k)
+      if (sc_cls[k] > sc_cls[c]) c = k;
+    cls_sel = c;
+  }
+  for (int f = wid; f < nf; f += 4) {
+    const int cls = p.cls_bits[f], cap = p.cap[f];
+    float top = -INFINITY;  // best valid start score
+    float best = -INFINITY;
+    int bs = 0x7fffffff, be = -1;
+    for (int s = lane; s < n; s += 64) {
+      const int fs = fb[s];
+      bool ok = (cls == 0) || (fs & cls);
+      if (ok && s > 0) {
+        const int fp = fb[s - 1];
+        ok = !qa_glued(fp, fs) && !((cls & QF_NO_START_AFTER_MASK) && (fp & QF_MASK));
+      }
+      if (!ok) continue;
+      const float ss = sc_start[f][s];
+      top = fmaxf(top, ss);
+      const int emax = min(n, s + cap);
+      for (int e = s; e < emax; ++e) {
+        const int fe = fb[e];
+        if (cls && !(fe & cls)) break;
+        if (e + 1 < n && qa_glued(fe, fb[e + 1])) continue;
+        const float v = ss + sc_end[f][e];
+        if (v > best) { best = v; bs = s; be = e; }  // strict: the lowest end of this start
+      }
+    }
+    // wave: max score, then the lowest start among the lanes that reach it (a lane's
+    // starts ascend with its pass, so its first reaching start is its lowest)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      top = fmaxf(top, __shfl_xor(top, o, 64));
+      const float ob = __shfl_xor(best, o, 64);
+      const int os = __shfl_xor(bs, o, 64), oe = __shfl_xor(be, o, 64);
+      if (ob > best || (ob == best && os < bs)) { best = ob; bs = os; be = oe; }
+    }
+    if (lane == 0) {
+      const bool null = be < 0 || !(top > sc_null[f]);
+      span_s[f] = null ? -1 : bs;
+      span_e[f] = null ? -1 : be;
+    }
+  }
+  __syncthreads();
+
+  // ---- 4. outputs (thread 0 lays out, the block copies)
+  __shared__ int off[QA_MAX_NF + 1];
+  const int c = cls_sel;
+  const bool reject = (p.reject_mask >> c) & 1;
+  if (tid == 0) {
+    int o = p.cls_len[c] + 1;
+    for (int f = 0; f < nf; ++f) {
+      off[f] = o;
+      if (!reject) o += (span_s[f] >= 0 ? span_e[f] - span_s[f] + 1 : 0) + 1;
+    }
+    off[nf] = o;
+    out_len[m] = min(o, p.max_out);
+  }
+  __syncthreads();
+  int* ob = out_buf + (size_t)m * p.max_out;
+  if (tid < p.cls_len[c]) ob[tid] = p.cls_tok[c][tid];
+  if (tid == 0) ob[p.cls_len[c]] = p.sep;
+  if (!reject) {
+    for (int f = 0; f < nf; ++f) {
+      const int len = span_s[f] >= 0 ? span_e[f] - span_s[f] + 1 : 0;
+      for (int j = tid; j <= len; j += 256) {
+        const int o = off[f] + j;
+        if (o < p.max_out) ob[o] = j < len ? body[span_s[f] + j] : p.sep;
+      }
+    }
+  }
+  if (dbg_spans != nullptr && tid <= 2 * nf) {
+    int v = c;
+    if (tid > 0) {
+      const int f = (tid - 1) >> 1;
+      v = reject ? -1 : ((tid - 1) & 1 ? span_e[f] : span_s[f]);
+    }
+    dbg_spans[(size_t)m * (1 + 2 * nf) + tid] = v;
+  }
+  if (dbg_scores != nullptr) {
+    // [4 class][nf][start n_pos][null][end n_pos] (positions past n: -inf)
+    const int per = QA_NCLS + nf * (2 * p.n_pos + 1);
+    float* d = dbg_scores + (size_t)m * per;
+    for (int k = tid; k < per; k += 256) {
+      float v;
+      if (k < QA_NCLS) {
+        v = sc_cls[k];
+      } else {
+        const int r = k - QA_NCLS, f = r / (2 * p.n_pos + 1), j = r % (2 * p.n_pos + 1);
+        if (j < p.n_pos) v = j < n ? sc_start[f][j] : -INFINITY;
+        else if (j == p.n_pos) v = sc_null[f];
+        else v = (j - p.n_pos - 1) < n ? sc_end[f][j - p.n_pos - 1] : -INFINITY;
+      }
+      d[k] = v;
+    }
+  }
+}
+
+// out[t] = table[ids[t]] + (add[t] >= 0 ? table[add[t]] : 0), rounded to bf16 like
+// torch's bf16 add (fp32 sum, round to nearest even).  The qa format's prompt rows: a
+// message token carries its pointer row, a query token does not.
+__global__ void __launch_bounds__(256) embed_rows_add_ids_kernel(const int* __restrict__ ids,
+                                                                 const int* __restrict__ add,
+                                                                 const uint16_t* __restrict__ table,
+                                                                 uint16_t* __restrict__ out, int T, int H, int V) {
+  const int nch = H >> 3;
+  const long total = (long)T * nch;
+  for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (long)gridDim.x * blockDim.x) {
+    const int t = (int)(k / nch), c = (int)(k - (long)t * nch);
+    const int a = ids[t], b = add[t];
+    uint4 u = make_uint4(0u, 0u, 0u, 0u);
+    if (a >= 0 && a < V) u = *reinterpret_cast<const uint4*>(table + (size_t)a * H + 8 * c);
+    if (b >= 0 && b < V) {
+      const uint4 v = *reinterpret_cast<const uint4*>(table + (size_t)b * H + 8 * c);
+      uint32_t x[4] = {u.x, u.y, u.z, u.w};
+      const uint32_t y[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const float s = qa_bf2f((uint16_t)(x[e] >> (16 * half))) + qa_bf2f((uint16_t)(y[e] >> (16 * half)));
+          uint32_t bits = __float_as_uint(s);
+          bits += 0x7fffu + ((bits >> 16) & 1u);  // round to nearest even (no NaN inputs)
+          r |= (bits >> 16) << (16 * half);
+        }
+        x[e] = r;
+      }
+      u = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)t * H + 8 * c) = u;
+  }
+}
+
+extern "C" {
+
+int sg_qa_decode(const void* params, const void* h, int ldh, const void* W, int H, float eps, const int* cu,
+                 const int* ids, const void* flags, int V, int* out_buf, int* out_len, void* dbg_scores,
+                 void* dbg_spans, int M, hipStream_t stream) {
+  const QAParams& p = *reinterpret_cast<const QAParams*>(params);
+  if (H % 64 || H > 1024 || ldh % 8 || p.nf <= 0 || p.nf > QA_MAX_NF || p.nq <= 0 || p.nq > QA_MAX_NQ ||
+      p.n_pos <= 0 || p.n_pos > QA_MAX_POS || p.max_out <= 0)
+    return -1;
+  for (int c = 0; c < QA_NCLS; ++c)
+    if (p.cls_len[c] <= 0 || p.cls_len[c] > QA_MAX_CLS_TOK) return -1;
+  if (M == 0) return 0;
+  const size_t lds = (size_t)p.nq * H * sizeof(uint16_t);
+  hipLaunchKernelGGL(qa_decode_kernel, dim3(M), dim3(256), lds, stream, p, (const uint16_t*)h, ldh,
+                     (const uint16_t*)W, H, eps, cu, ids, (const uint16_t*)flags, V, out_buf, out_len,
+                     (float*)dbg_scores, (int*)dbg_spans);
+  return (int)hipGetLastError();
+}
+
+int sg_qa_params_size() { return (int)sizeof(QAParams); }
+
+int sg_embed_rows_add_ids(const int* ids, const int* add, const void* table, void* out, int T, int H, int V,
+                          hipStream_t stream) {
+  if (H % 8) return -1;
+  if (T == 0) return 0;
+  const long total = (long)T * (H >> 3);
+  const int grid = (int)((total + 255) / 256 < 65536 ? (total + 255) / 256 : 65536);
+  hipLaunchKernelGGL(embed_rows_add_ids_kernel, dim3(grid), dim3(256), 0, stream, ids, add,
+                     (const uint16_t*)table, (uint16_t*)out, T, H, V);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

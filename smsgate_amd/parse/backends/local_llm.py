@@ -65,24 +65,38 @@ def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, d
     format comes from its own metadata."""
     import torch
 
-    from ...models.extractor import CONFIGS, ExtractorWeights, span_config
+    from ...models.extractor import CONFIGS, ExtractorWeights, qa_config, span_config
     from ...models.tokenizer import load_tokenizer
     from ...serving.engine import EngineConfig, ExtractionEngine
+    from ...serving.qa_engine import QAEngine
 
-    cfg = span_config(CONFIGS[model]) if answer_format == "span" else CONFIGS[model]
+    if answer_format == "span":
+        cfg = span_config(CONFIGS[model])
+    elif answer_format in ("qa", "qa17"):
+        cfg = qa_config(CONFIGS[model], queries=9 if answer_format == "qa" else 17)
+    elif answer_format == "copy":
+        cfg = CONFIGS[model]
+    else:
+        raise ValueError(f"answer format {answer_format!r}: copy | span | qa | qa17")
+
+    def make(w):
+        # the weights' own format picks the engine: one forward (qa) or pointer decode
+        cls = QAEngine if w.cfg.qa_queries > 0 else ExtractionEngine
+        return cls(w, load_tokenizer(), EngineConfig(**engine_kw))
+
     dev = torch.device(device)
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
     if weights is not None:
         weights.requires_grad_(False)
-        return ExtractionEngine(weights, load_tokenizer(), EngineConfig(**engine_kw))
+        return make(weights)
     checkpoint = resolve_checkpoint(model, checkpoint, random_init)
     if checkpoint:
         w = ExtractorWeights.load(checkpoint, cfg, device=dev)
     else:
         w = ExtractorWeights(cfg, device=dev, seed=seed)
     w.requires_grad_(False)
-    return ExtractionEngine(w, load_tokenizer(), EngineConfig(**engine_kw))
+    return make(w)
 
 
 class LocalLLMBackend(ParserBackend):

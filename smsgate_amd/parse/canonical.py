@@ -33,6 +33,28 @@ CURRENCY_ALIASES: Dict[str, str] = {
 }
 
 _DAY_FIRST = re.compile(r"(\d{1,2})[/-](\d{1,2})[/-](\d{4}|\d{2})(?![\d])(.*)\Z", re.S)
+# Russian month names (genitive, "6 июня 2025 14:23"; also the nominative / short forms):
+# dateutil knows English month names only, so without this the date would fall back to
+# the message timestamp
+_RU_MONTHS = {"январ": 1, "феврал": 2, "март": 3, "апрел": 4, "ма": 5, "июн": 6, "июл": 7, "август": 8,
+              "сентябр": 9, "октябр": 10, "ноябр": 11, "декабр": 12}
+_RU_DATE = re.compile(r"(\d{1,2})\s+([а-яё]+)\.?\s+(\d{4})(?:\s*г\.?)?(.*)\Z", re.S | re.I)
+_RU_ENDINGS = ("я", "а", "ь", "й", "е", "")
+
+
+def _ru_month(word: str) -> int:
+    w = word.lower()
+    for end in _RU_ENDINGS:
+        if end and not w.endswith(end):
+            continue
+        stem = w[: len(w) - len(end)] if end else w
+        if stem in _RU_MONTHS:
+            return _RU_MONTHS[stem]
+        if len(stem) >= 3:  # "сент", "окт"
+            hits = [m for s, m in _RU_MONTHS.items() if len(s) >= 3 and s.startswith(stem)]
+            if len(hits) == 1:
+                return hits[0]
+    return 0
 
 
 def canonical_currency(value: Any) -> Any:
@@ -47,6 +69,12 @@ def canonical_date_text(value: Any) -> Any:
         return value
     m = _DAY_FIRST.match(value.strip())
     if m is None:
+        r = _RU_DATE.match(value.strip()) if not value.isascii() else None
+        if r is not None:
+            mo = _ru_month(r.group(2))
+            d = int(r.group(1))
+            if mo and 1 <= d <= 31:
+                return f"{r.group(3)}-{mo:02d}-{d:02d}{r.group(4)}"
         return value
     d, mo, y, rest = int(m.group(1)), int(m.group(2)), m.group(3), m.group(4)
     if not (1 <= d <= 31 and 1 <= mo <= 12):

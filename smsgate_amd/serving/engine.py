@@ -41,6 +41,7 @@ from ..models.extractor import ExtractorConfig, ExtractorWeights
 from ..models.tokenizer import ExtractorTokenizer
 from ..parse.schema import EXTRACTOR_PROMPT
 from .fsm import DEFAULT_FIELDS, FieldSpec, SchemaFSM, build_fsm, build_span_fsm
+from .qa import null_rejection
 
 __all__ = ["EngineConfig", "ExtractionEngine", "EngineStats"]
 
@@ -141,6 +142,9 @@ class EngineConfig:
     # (its body tokens / enum tokens, ops.sparse_argmax) instead of the dense 8 192-wide
     # GEMM with the masked arg-max epilogue (fused GEMM path, lm_head_argmax)
     sparse_argmax: bool = True
+    # qa-format models (serving/qa_engine.py): token budget of one packed prefill batch
+    # (messages + their query tokens; max_slots caps the sequences)
+    qa_max_tokens: int = 262144
 
 
 @dataclass
@@ -1118,7 +1122,7 @@ class ExtractionEngine:
                 pieces.extend(vals)
             texts = self.tok.decode_batch(pieces)
             for j, r in enumerate(fin):
-                ans = {f.name: texts[j * nf + i].strip() for i, f in enumerate(self.fsm.fields)}
+                ans = null_rejection({f.name: texts[j * nf + i].strip() for i, f in enumerate(self.fsm.fields)})
                 res.append((self.active.pop(r), ans))
                 heapq.heappush(self.free_rows, r)
         self.stats.completed += len(res)

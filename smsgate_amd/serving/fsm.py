@@ -120,9 +120,13 @@ def token_flags(token_strings: Sequence[str], specials: Sequence[int], vocab: in
 # any script ("USD", "$", "руб") -- parse/canonical.py maps the last two to ISO codes
 _ASCII_LETTERS = set("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz")
 _CURRENCY_SYMBOLS = set("$€£₽₾֏")
+_CYRILLIC = set("абвгдеёжзийклмнопрстуфхцчшщъыьэюяАБВГДЕЁЖЗИЙКЛМНОПРСТУФХЦЧШЩЪЫЬЭЮЯ") | {"�"}
 _CLASS_CHARS = {
-    "date": set("0123456789.:/-, ") | _ASCII_LETTERS,
-    "number": set("0123456789.,- "),
+    # month names in Latin or Cyrillic script ("6 июня 2025"; byte-level pieces of a
+    # Cyrillic letter decode to U+FFFD)
+    "date": set("0123456789.:/-, ") | _ASCII_LETTERS | _CYRILLIC,
+    # apostrophe / right single quote thousands ("1'234.56", Swiss style)
+    "number": set("0123456789.,- '’"),
     "currency": {" "} | _CURRENCY_SYMBOLS,  # plus any alphabetic character (below)
     "card": set("0123456789* "),
 }
@@ -137,7 +141,11 @@ def _token_class_sets(token_strings: Sequence[str], specials: Sequence[int]) -> 
             continue
         out["text"][i] = True
         if not s.strip():
-            continue  # pure-whitespace tokens only count as free text
+            # pure-whitespace tokens only count as free text -- except one blank inside a
+            # date: byte-level BPE leaves the blank before a Cyrillic month name alone
+            # (" 18", " ", "я", "н", ... of "18 января")
+            out["date"][i] = s == " "
+            continue
         cs = set(s)
         for k, allowed in _CLASS_CHARS.items():
             if cs <= allowed or (k == "currency" and all(ch in allowed or ch.isalpha() for ch in cs)):

@@ -1,0 +1,322 @@
+"""One-forward span extraction (the "qa" answer format, VERDICT r04 next #2a).
+
+The span-pointer format (serving/fsm.py build_span_fsm) still decodes
+autoregressively: txn_type, then a start and an end pointer per copied field --
+~17 sequential decode steps per message, each re-reading the row's keys.  Round 4's
+kernel statistics put that decode at 54 % of the GPU time at ~19 rows per message,
+against 41 % for the ~41 prefill rows.
+
+This format asks the whole question in ONE forward.  After ``body <ans>`` the
+engine appends ``n_queries`` query tokens (ids ``q0 + k``) at the next positions;
+the causal model lets every query row attend to the whole body:
+
+* query row 0 classifies the message: its hidden state against the four class
+  rows ``cls0 + c`` (TXN_TYPES order: debit, credit, otp, unknown).  ``otp`` and
+  ``unknown`` are the reference's non-transactions (gemini_parser.py:41): every
+  other field is null, post-processing raises on ``str(None)`` (:235-241) and the
+  worker dead-letters the message as ``{"reason": "unmatched"}`` (worker.py:151-158);
+* per copied field, a start row scores every prompt position ``j`` against the
+  start-pointer row ``ptr0 + j`` (the same row is added to position ``j``'s input,
+  as in the span format, so the model can name a position) and against the
+  ``null_id`` row (an empty value); an end row scores position ``j`` against the
+  end-pointer row ``pe0 + j``.  With ``n_queries == 9`` one row per field does
+  both, with 17 the start and end rows are separate query tokens;
+* decoding is joint and constrained: the field is null when its null score is at
+  least every valid start's score; otherwise the (start, end) pair maximising
+  ``start[s] + end[e]`` over VALID pairs -- ``s <= e < s + cap``, every token in
+  the field's class, ``s`` and ``e + 1`` at word boundaries, a date / number never
+  starting right after a card mask.  Word boundaries split letters from digits
+  ("USD52.00", "x1234" and "1500р" separate), unlike the span format's rule.
+
+The answer is written in the copy format (txn tokens, then each field's body
+tokens, each ended by ``<sep>``), so the tokenizers' field decoders, the remote
+protocol and post-processing are unchanged.  :func:`qa_decode_ref` is the PyTorch
+reference of ``qa_decode_kernel`` (ops/csrc/qa_kernels.hip).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..parse.schema import TXN_TYPES
+from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
+
+__all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
+           "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
+           "QA_MAX_QUERIES"]
+
+# non-transaction classes: every other field of the answer is null
+REJECT_TXN = ("otp", "unknown")
+QA_MAX_QUERIES = 24
+# per-token flags (uint16): starts / ends with a letter / digit, ends a card mask, class bits
+QF_SL, QF_SD, QF_EL, QF_ED, QF_MASK = 1, 2, 4, 8, 16
+QA_CLASS_BITS = {k: v << 3 for k, v in TOK_CLASS_BITS.items()}  # date 32, number 64, currency 128, card 256
+_NO_START_AFTER_MASK = QA_CLASS_BITS["date"] | QA_CLASS_BITS["number"]
+
+
+@dataclass(frozen=True)
+class QALayout:
+    """Ids of the qa format past the tokenizer's vocabulary (``vocab_tok``)."""
+    vocab_tok: int
+    n_pos: int  # pointable prompt positions (max_body_tokens + 2)
+    n_queries: int  # 9 (one row per field) or 17 (txn + a start and an end row per copied field)
+    ptr0: int
+    pe0: int
+    q0: int
+    null_id: int
+    cls0: int
+    vocab: int  # rounded up to 128
+    fields: Tuple[FieldSpec, ...] = DEFAULT_FIELDS
+
+    @property
+    def n_copy(self) -> int:
+        return len(self.fields) - 1
+
+    def start_row(self, f: int) -> int:
+        """Query row scoring copied field ``f``'s start (f = 1 .. n_copy)."""
+        return f if self.n_queries == len(self.fields) else 2 * f - 1
+
+    def end_row(self, f: int) -> int:
+        return f if self.n_queries == len(self.fields) else 2 * f
+
+    def query_ids(self) -> List[int]:
+        return [self.q0 + k for k in range(self.n_queries)]
+
+    def caps(self) -> List[int]:
+        return [f.cap for f in self.fields[1:]]
+
+    def class_bits(self) -> List[int]:
+        return [QA_CLASS_BITS.get(f.kind, 0) for f in self.fields[1:]]
+
+    def max_answer_tokens(self) -> int:
+        return sum(f.cap for f in self.fields) + len(self.fields)
+
+
+def qa_layout(vocab_tok: int = 8192, n_pos: int = 130, n_queries: int = 9,
+              fields: Sequence[FieldSpec] = DEFAULT_FIELDS) -> QALayout:
+    if fields[0].kind != "enum" or any(f.kind == "enum" or not f.copy for f in fields[1:]):
+        raise ValueError("qa format: txn_type enum first, then copied fields")
+    if n_queries not in (len(fields), 2 * len(fields) - 1):
+        raise ValueError(f"qa format: {len(fields)} or {2 * len(fields) - 1} queries, not {n_queries}")
+    ptr0 = vocab_tok
+    pe0 = ptr0 + n_pos
+    q0 = pe0 + n_pos
+    null_id = q0 + QA_MAX_QUERIES
+    cls0 = null_id + 1
+    vocab = -(-(cls0 + len(TXN_TYPES)) // 128) * 128
+    return QALayout(vocab_tok, n_pos, n_queries, ptr0, pe0, q0, null_id, cls0, vocab, tuple(fields))
+
+
+def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
+    """uint16 per id: QF_* letter / digit start / end bits, card-mask end, class bits."""
+    strings = tokenizer.token_strings
+    specials = [tokenizer.pad, tokenizer.bos, tokenizer.eos, tokenizer.sep, tokenizer.sms, tokenizer.ans]
+    classes = _token_class_sets(strings, specials)
+    out = np.zeros(vocab, dtype=np.uint16)
+    n = min(vocab, len(strings))
+    for k, bit in QA_CLASS_BITS.items():
+        out[:n] |= np.where(classes[k][:n], bit, 0).astype(np.uint16)
+    spec = set(specials)
+
+    def letter(ch: str) -> bool:
+        return ch.isalpha() or ch == "�"
+
+    for i, t in enumerate(strings[:vocab]):
+        if i in spec or not t:
+            continue
+        f = 0
+        if letter(t[0]):
+            f |= QF_SL
+        # a number's inner separator before a digit continues the number (".58" of "657.58")
+        if t[0].isdigit() or (len(t) > 1 and t[0] in ".,:'" and t[1].isdigit()):
+            f |= QF_SD
+        if letter(t[-1]):
+            f |= QF_EL
+        if t[-1].isdigit() or (len(t) > 1 and t[-1] in ".,:'" and t[-2].isdigit()):
+            f |= QF_ED
+        if t.endswith("*"):
+            f |= QF_MASK
+        out[i] |= f
+    return out
+
+
+def _glued(fa: int, fb: int) -> bool:
+    return bool(((fa & QF_EL) and (fb & QF_SL)) or ((fa & QF_ED) and (fb & QF_SD)))
+
+
+def valid_starts(flags: np.ndarray, body: Sequence[int], n: int, cls: int) -> np.ndarray:
+    """[n] bool: positions a value of class bits ``cls`` may start at (``n`` pointable)."""
+    ok = np.zeros(n, dtype=bool)
+    for j in range(n):
+        fj = int(flags[body[j]])
+        if cls and not fj & cls:
+            continue
+        if j > 0:
+            fp = int(flags[body[j - 1]])
+            if _glued(fp, fj) or ((cls & _NO_START_AFTER_MASK) and fp & QF_MASK):
+                continue
+        ok[j] = True
+    return ok
+
+
+def valid_ends(flags: np.ndarray, body: Sequence[int], n: int, cls: int, cap: int, s: int) -> List[int]:
+    """End positions of a value starting at ``s``: in class all the way, within the
+    cap, followed by a word boundary (or the end of the pointable body)."""
+    out = []
+    for e in range(s, min(n, s + cap)):
+        fe = int(flags[body[e]])
+        if cls and not fe & cls:
+            break
+        if e + 1 >= n or not _glued(fe, int(flags[body[e + 1]])):
+            out.append(e)
+    return out
+
+
+def qa_targets(tok, lay: QALayout, flags: np.ndarray, answer: Dict[str, Optional[str]], body: str, body_enc,
+               msg_len: int) -> Optional[Tuple[int, List[Tuple[int, int]]]]:
+    """Training target ``(class index, [(start, end) | (-1, -1) per copied field])`` or
+    None when a gold value is not a valid span the decoder could produce (the span
+    format's answer_span_tokens drops such examples too)."""
+    txn = answer.get("txn_type") or "unknown"
+    if txn not in TXN_TYPES:
+        return None
+    cls = TXN_TYPES.index(txn)
+    n = msg_len - 1  # pointable positions (the message ends with <ans>)
+    ids = body_enc[0]
+    spans: List[Tuple[int, int]] = []
+    for f, bits, cap in zip(lay.fields[1:], lay.class_bits(), lay.caps()):
+        v = answer.get(f.name) or ""
+        if not v or txn in REJECT_TXN:
+            spans.append((-1, -1))
+            continue
+        sp = tok.value_span(v, body, ids, body_enc[1])
+        if sp is None or sp[1] >= n:
+            return None
+        s, e = sp
+        if not valid_starts(flags, ids, n, bits)[s] or e not in valid_ends(flags, ids, n, bits, cap, s):
+            return None
+        spans.append((s, e))
+    return cls, spans
+
+
+def qa_rows(lay: QALayout) -> Tuple[List[int], List[int]]:
+    """(start row, end row) per copied field."""
+    return ([lay.start_row(f) for f in range(1, len(lay.fields))],
+            [lay.end_row(f) for f in range(1, len(lay.fields))])
+
+
+def _pair_mask(fb: np.ndarray, n: int, cls: int, cap: int) -> Tuple[np.ndarray, np.ndarray]:
+    """(valid starts [n], valid (start, end) pairs [n, n]) of one field from the body's
+    token flags ``fb`` (vectorised :func:`valid_starts` / :func:`valid_ends`)."""
+    fb = fb[:n].astype(np.int64)
+    prev = np.concatenate([[0], fb[:-1]])
+    glued_prev = (((prev & QF_EL) != 0) & ((fb & QF_SL) != 0)) | (((prev & QF_ED) != 0) & ((fb & QF_SD) != 0))
+    glued_prev[0] = False
+    in_cls = (fb & cls) != 0 if cls else np.ones(n, dtype=bool)
+    after_mask = ((prev & QF_MASK) != 0) & bool(cls & _NO_START_AFTER_MASK)
+    after_mask[0] = False
+    vs = in_cls & ~glued_prev & ~after_mask
+    end_ok = np.ones(n, dtype=bool)
+    end_ok[:-1] = ~glued_prev[1:]
+    bad = np.concatenate([[0], np.cumsum(~in_cls)])  # out-of-class tokens before position k
+    S, E = np.arange(n)[:, None], np.arange(n)[None, :]
+    pairs = (E >= S) & (E - S < cap) & (bad[E + 1] - bad[S] == 0) & end_ok[None, :] & vs[:, None]
+    return vs, pairs
+
+
+def qa_decode_ref(cls_logits, start_logits, null_logits, end_logits, bodies: Sequence[Sequence[int]],
+                  flags: np.ndarray, lay: QALayout) -> List[Tuple[int, List[Tuple[int, int]]]]:
+    """Reference joint decode (host, numpy).  Per message ``m``: ``cls_logits[m]`` [4],
+    ``start_logits[m]`` / ``end_logits[m]`` [n_copy, >= n] over prompt positions,
+    ``null_logits[m]`` [n_copy]; ``bodies[m]`` the prompt ids (``body <ans>``).
+    Returns (class, spans) with (-1, -1) for a null field (every field of a rejection).
+    Ties go to the lower class, then the lower start, then the lower end (the kernel's
+    rule); the field is null when its null score is >= every valid start's score or no
+    valid pair exists."""
+    out = []
+    for m, body in enumerate(bodies):
+        c = int(np.argmax(np.asarray(cls_logits[m], dtype=np.float32)))
+        if TXN_TYPES[c] in REJECT_TXN:
+            out.append((c, [(-1, -1)] * lay.n_copy))
+            continue
+        n = len(body) - 1
+        fb = flags[np.asarray(body[:n], dtype=np.int64)]
+        spans: List[Tuple[int, int]] = []
+        for f, (bits, cap) in enumerate(zip(lay.class_bits(), lay.caps())):
+            st = np.asarray(start_logits[m][f][:n], dtype=np.float32)
+            en = np.asarray(end_logits[m][f][:n], dtype=np.float32)
+            vs, pairs = _pair_mask(fb, n, bits, cap)
+            if not pairs.any() or np.float32(null_logits[m][f]) >= st[vs].max():
+                spans.append((-1, -1))
+                continue
+            sc = np.where(pairs, st[:, None] + en[None, :], -np.inf)
+            k = int(np.argmax(sc))
+            spans.append((k // n, k % n))
+        out.append((c, spans))
+    return out
+
+
+def qa_expand(tok, lay: QALayout, cls: int, spans: Sequence[Tuple[int, int]], body: Sequence[int]) -> List[int]:
+    """The copy-format answer tokens of a decoded (class, spans)."""
+    out = list(tok.encode(TXN_TYPES[cls])) + [tok.sep]
+    if TXN_TYPES[cls] in REJECT_TXN:
+        return out
+    for s, e in spans:
+        if s >= 0:
+            out += list(body[s:e + 1])
+        out.append(tok.sep)
+    return out
+
+
+def qa_logits(h, embed, qpos, lay: QALayout):
+    """Scores of the query rows (PyTorch; training and the reference path).  ``h`` [B, T, H]
+    final-normed hidden states, ``embed`` the (tied) embedding, ``qpos`` [B, n_queries]
+    the query rows' positions.  Returns fp32 ``cls`` [B, 4], ``start`` [B, n_copy, n_pos],
+    ``null`` [B, n_copy], ``end`` [B, n_copy, n_pos]."""
+    import torch
+
+    B = h.shape[0]
+    hq = h[torch.arange(B, device=h.device)[:, None], qpos]  # [B, NQ, H]
+    srows, erows = qa_rows(lay)
+    hs, he = hq[:, srows], hq[:, erows]
+    E = embed if embed.dtype == h.dtype or torch.is_autocast_enabled() else embed.to(h.dtype)
+    cls = (hq[:, 0] @ E[lay.cls0:lay.cls0 + len(TXN_TYPES)].t()).float()
+    start = (hs @ E[lay.ptr0:lay.ptr0 + lay.n_pos].t()).float()
+    null = (hs @ E[lay.null_id]).float()
+    end = (he @ E[lay.pe0:lay.pe0 + lay.n_pos].t()).float()
+    return cls, start, null, end
+
+
+def qa_loss(scores, targets, lay: QALayout):
+    """Mean cross-entropy over the answer's decisions: the class, every copied field's
+    start (null included) and every non-null field's end (positions >= its start).
+    ``targets``: (cls [B], starts [B, n_copy] (-1 = null), ends [B, n_copy], npos [B]
+    pointable positions per message)."""
+    import torch
+    import torch.nn.functional as F
+
+    cls, start, null, end = scores
+    t_cls, t_s, t_e, npos = targets
+    B, NF, NP = start.shape
+    j = torch.arange(NP, device=start.device)
+    out_of_msg = j[None, None, :] >= npos[:, None, None]  # [B, 1, NP]
+    neg = torch.finfo(torch.float32).min / 4
+    st = torch.cat([start.masked_fill(out_of_msg, neg), null[..., None]], -1)  # null = index NP
+    st_t = torch.where(t_s >= 0, t_s, torch.full_like(t_s, NP))
+    l_cls = F.cross_entropy(cls, t_cls, reduction="sum")
+    l_st = F.cross_entropy(st.reshape(-1, NP + 1), st_t.reshape(-1), reduction="sum")
+    has = t_s >= 0
+    en = end.masked_fill(out_of_msg | (j[None, None, :] < t_s[..., None]), neg)
+    l_en = F.cross_entropy(en[has], t_e[has], reduction="sum") if bool(has.any()) else en.sum() * 0
+    return (l_cls + l_st + l_en) / (B + B * NF + int(has.sum()))
+
+
+def null_rejection(answer: Dict[str, Optional[str]]) -> Dict[str, Optional[str]]:
+    """A decoded answer whose txn_type is a non-transaction gets null fields (Gemini's
+    shape for "not a transaction"): post-processing then raises on ``str(None)`` and
+    the message is dead-lettered as unmatched, the reference's path."""
+    if answer.get("txn_type") in REJECT_TXN:
+        return {k: (v if k == "txn_type" else None) for k, v in answer.items()}
+    return answer

@@ -1,0 +1,260 @@
+"""GPU engine of the one-forward span format (serving/qa.py): batched prefill, no decode.
+
+The span-pointer engine (:class:`~smsgate_amd.serving.engine.ExtractionEngine`) keeps a
+KV slot per message for ~17 decode steps, replays decode hipGraphs, compacts rows and
+harvests finished rows step by step.  A qa-format model answers in the forward that
+reads the message, so serving it is a pipeline of packed prefill batches:
+
+    host   take waiting messages (up to ``max_slots`` sequences / ``qa_max_tokens``
+           tokens), append the query tokens, build positions / KV slots / pointer-row
+           ids, stage them in ONE pinned copy
+    GPU    embedding + pointer rows (embed_rows_add_ids) -> the native 30-layer prefill
+           (csrc/runtime.hip, the same fused MFMA GEMM / attention kernels the span
+           engine prefills with) -> qa_decode_kernel (query-row scores, class, joint
+           constrained span decode, copy-format answer) -> async D2H of the answers
+    host   harvest the PREVIOUS batch (its event) while this one runs
+
+A batch of >= ``split_prefill`` tokens runs as two halves on two streams (disjoint KV
+slots and output rows), so one half's attention overlaps the other's GEMMs, as in the
+span engine's prefill.  The KV cache only lives for the batch: slot ``i`` is the
+batch's ``i``-th sequence.
+
+Same interface as the span engine for :class:`~smsgate_amd.serving.remote.EngineServer`
+and :class:`~smsgate_amd.serving.worker.EngineWorker`: ``submit_ids`` / ``submit_many``,
+``step(raw)`` returning ``(key, answer)`` or ``(key, copy-format token array)``,
+``busy``, ``run``, ``stats``.
+"""
+from __future__ import annotations
+
+import time
+from collections import deque
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.extractor import SPAN_PTR0, ExtractorWeights
+from ..models.tokenizer import ExtractorTokenizer
+from ..parse.schema import EXTRACTOR_PROMPT
+from .engine import EngineConfig, EngineStats, ExtractionEngine, _PinnedRing, _round_up
+from .fsm import DEFAULT_FIELDS
+from .qa import null_rejection, qa_layout, qa_token_flags
+
+__all__ = ["QAEngine"]
+
+
+@dataclass
+class _Batch:
+    n: int
+    keys: List[Any]
+    event: Any
+    start_event: Any
+    bufs: Dict[str, torch.Tensor]
+
+
+class QAEngine(ExtractionEngine):
+    """Prefill-only extraction engine of a qa-format model (``cfg.qa_queries > 0``)."""
+
+    def __init__(self, weights: ExtractorWeights, tokenizer: ExtractorTokenizer,
+                 cfg: Optional[EngineConfig] = None, system_prompt: str = EXTRACTOR_PROMPT) -> None:
+        self.cfg = ec = cfg or EngineConfig()
+        self.w = weights
+        self.mc = mc = weights.cfg
+        self.tok = tokenizer
+        self.device = dev = weights.embed.device
+        if dev.type != "cuda":
+            raise RuntimeError("QAEngine needs a GPU (the HIP kernels have no CPU path)")
+        if mc.qa_queries <= 0:
+            raise ValueError("QAEngine serves qa-format models (ExtractorConfig.qa_queries > 0)")
+        if mc.head_dim != 64 or mc.hidden % 64 or mc.inter % 32:
+            raise ValueError("QAEngine: head_dim 64, hidden % 64 == 0, inter % 32 == 0 (fused kernels)")
+        if mc.span_positions < ec.max_body_tokens + 2:
+            raise ValueError("qa model: fewer pointer positions than prompt positions")
+        if weights.embed.dtype != torch.bfloat16 or not weights.embed.is_contiguous():
+            raise ValueError("QAEngine: contiguous bf16 weights")
+        ops.load_library()
+        ops.set_prefill_split(ec.prefill_key_split)
+        ops.set_prefill_impl(ec.prefill_attn)
+        self.lay = lay = qa_layout(SPAN_PTR0, mc.span_positions, mc.qa_queries, DEFAULT_FIELDS)
+        if mc.vocab < lay.vocab:
+            raise ValueError(f"qa model vocab {mc.vocab} < layout {lay.vocab}")
+        self.NQ = lay.n_queries
+        self.qids = np.asarray(lay.query_ids(), dtype=np.int32)
+        # the span engine's state the shared helpers read (_compute_prefix, _layers_fused)
+        self.fused, self.span, self.spec, self.copy, self.sparse, self.argmax = True, False, False, False, False, False
+        self.template_slots = 0
+        w = self.w
+        self.fw_qkv = [ops.fold_norm(w.qkv[i], w.ln1[i]) for i in range(mc.layers)]
+        self.fw_o = [w.o[i].contiguous() for i in range(mc.layers)]
+        self.fw_gu = [ops.interleave_gate_up(ops.fold_norm(w.gate_up[i], w.ln2[i])) for i in range(mc.layers)]
+        self.fw_down = [w.down[i].contiguous() for i in range(mc.layers)]
+        # the head's rows (start pointers .. class rows) with the final norm folded in
+        self.w_qa = ops.fold_norm(w.embed[lay.ptr0:lay.cls0 + 4], w.ln_f)
+        self.flags_t = torch.from_numpy(qa_token_flags(tokenizer, lay.vocab).view(np.int16)).to(dev)
+        self.params = ops.qa_params(lay, tokenizer)
+        self.max_out = lay.max_answer_tokens()
+        self.prefix_ids = tokenizer.prefix_ids(system_prompt)
+        self.P0 = len(self.prefix_ids)
+        self.P0pad = _round_up(self.P0, 32)
+        self.Lmax = _round_up(ec.max_body_tokens + 2 + self.NQ, 32)
+        S, L, nkv, D = ec.max_slots, mc.layers, mc.kv_heads, mc.head_dim
+        bf = torch.bfloat16
+        self.k_cache = torch.zeros(L, S, nkv, self.Lmax, D, dtype=bf, device=dev)
+        self.vt_cache = torch.zeros(L, *ops.vt_shape(S, nkv, D, self.Lmax), dtype=bf, device=dev)
+        self.pk = torch.zeros(L, nkv, self.P0pad, D, dtype=bf, device=dev)
+        self.pvt = torch.zeros(L, *ops.vt_shape(1, nkv, D, self.P0pad)[1:], dtype=bf, device=dev)
+        self.cos_sin = ops.rope_table(self.P0 + self.Lmax + 1, D, mc.rope_theta, dev)
+        self.scale = 1.0 / (D ** 0.5)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.out_buf = torch.zeros(S, self.max_out, **i32)
+        self.out_len = torch.zeros(S, **i32)
+        self._host_bufs = [{"len": torch.zeros(S, dtype=torch.int32).pin_memory(),
+                            "buf": torch.zeros(S, self.max_out, dtype=torch.int32).pin_memory()} for _ in range(2)]
+        self._flip = 0
+        self.max_tokens = max(ec.qa_max_tokens, ec.max_body_tokens + 2 + self.NQ)
+        self._stage = _PinnedRing(max(1 << 20, 4 * (4 * self.max_tokens + 3 * S + 8)), slots=6)
+        self.waiting: deque = deque()
+        self.active: Dict[int, Any] = {}
+        self.stats = EngineStats()
+        self.graphs: Dict[int, Any] = {}
+        self._pending: Optional[_Batch] = None
+        self._sides: List[torch.cuda.Stream] = []
+        self._fwd_ss: Optional[torch.Tensor] = None
+        self._idle_prev = None
+        self._idle_pairs: deque = deque()
+        self._lp = ops.LayerPointers(self.fw_qkv, self.fw_o, self.fw_gu, self.fw_down, self.k_cache, self.vt_cache,
+                                     self.pk, self.pvt)
+        self._compute_prefix()
+
+    # ---------------------------------------------------------------- batches
+    def _forward_part(self, items: List[Any], r0: int) -> int:
+        """Prefill + head of ``items`` into KV slots / output rows ``r0 ..``; returns the
+        tokens computed."""
+        mc, lay, dev = self.mc, self.lay, self.device
+        n = len(items)
+        NQ = self.NQ
+        lens = np.fromiter((len(it.ids) for it in items), dtype=np.int32, count=n)
+        tl = lens + NQ
+        T = int(tl.sum())
+        cu = np.zeros(n + 1, dtype=np.int32)
+        np.cumsum(tl, out=cu[1:])
+        qid = self.qids
+        flat = np.concatenate([np.concatenate([np.asarray(it.ids, dtype=np.int32), qid]) for it in items])
+        starts = np.repeat(cu[:-1], tl)
+        pos = np.arange(T, dtype=np.int32) - starts
+        add = np.where(pos < np.repeat(lens, tl), lay.ptr0 + pos, -1).astype(np.int32)
+        seq_slot = np.arange(r0, r0 + n, dtype=np.int32)
+        slot = np.repeat(seq_slot, tl)
+        qstart = np.zeros(n, dtype=np.int32)
+        meta = self._stage.to_device(np.concatenate([flat, pos, slot, add, cu, qstart, seq_slot]), dev)
+        o = 0
+        flat_d = meta[o:o + T]; o += T
+        pos_d = meta[o:o + T]; o += T
+        slot_d = meta[o:o + T]; o += T
+        add_d = meta[o:o + T]; o += T
+        cu_d = meta[o:o + n + 1]; o += n + 1
+        qstart_d = meta[o:o + n]; o += n
+        seq_slot_d = meta[o:o + n]
+        x = ops.embed_rows_add_ids(flat_d, add_d, self.w.embed)
+        ss = self._ss_buffer(T, dev)
+        ops.prefill_forward(self._lp, x, H=mc.hidden, I=mc.inter, nh=mc.heads, nkv=mc.kv_heads, D=mc.head_dim,
+                            Lmax=self.Lmax, P0=self.P0, P0pad=self.P0pad, pos=pos_d, slot=slot_d,
+                            cos_sin=self.cos_sin, p0=self.P0, cu_q=cu_d, q_start=qstart_d, seq_slot=seq_slot_d,
+                            max_q=int(tl.max()), scale=self.scale,
+                            q=torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=dev),
+                            a=torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=dev),
+                            act=torch.empty(T, mc.inter, dtype=x.dtype, device=dev), ss=ss, eps=mc.eps)
+        ops.qa_decode(x, self.w_qa, mc.eps, cu_d, flat_d, self.flags_t, self.params, self.out_buf[r0:],
+                      self.out_len[r0:])
+        return T
+
+    def _launch(self) -> Optional[_Batch]:
+        ec = self.cfg
+        items: List[Any] = []
+        ntok = 0
+        S = ec.max_slots
+        cap = ec.max_body_tokens + 2
+        while self.waiting and len(items) < S:
+            it = self.waiting[0]
+            if len(it.ids) > cap:  # keep the closing <ans> (submit_ids cuts already)
+                it.ids = list(it.ids[: cap - 1]) + [it.ids[-1]]
+            t = len(it.ids) + self.NQ
+            if items and ntok + t > self.max_tokens:
+                break
+            self.waiting.popleft()
+            items.append(it)
+            ntok += t
+        if not items:
+            return None
+        t0 = time.perf_counter()
+        start_ev = None
+        if ec.measure_idle:
+            start_ev = torch.cuda.Event(enable_timing=True)
+            start_ev.record()
+        n = len(items)
+        split = ec.split_prefill
+        if split and ntok >= split and n >= 2:
+            h = n // 2
+            main = torch.cuda.current_stream(self.device)
+            s2 = self._side_stream()
+            s2.wait_stream(main)
+            T = self._forward_part(items[:h], 0)
+            with torch.cuda.stream(s2):
+                T += self._forward_part(items[h:], h)
+            main.wait_stream(s2)
+        else:
+            T = self._forward_part(items, 0)
+        hb = self._host_bufs[self._flip]
+        self._flip ^= 1
+        hb["len"][:n].copy_(self.out_len[:n], non_blocking=True)
+        hb["buf"][:n].copy_(self.out_buf[:n], non_blocking=True)
+        ev = torch.cuda.Event(enable_timing=ec.measure_idle, blocking=True)
+        ev.record()
+        st = self.stats
+        st.prefill_tokens += T
+        st.prefill_seqs += n
+        st.prefill_s += time.perf_counter() - t0
+        return _Batch(n, [it.key for it in items], ev, start_ev, hb)
+
+    def _harvest_batch(self, b: _Batch, raw: bool) -> List[Tuple[Any, Any]]:
+        t0 = time.perf_counter()
+        b.event.synchronize()
+        self.stats.harvest_wait_s += time.perf_counter() - t0
+        lens = b.bufs["len"][: b.n].numpy().copy()
+        blk = b.bufs["buf"][: b.n].numpy().copy()  # the pinned buffer is reused two batches on
+        if raw:
+            res = [(k, blk[i, : lens[i]]) for i, k in enumerate(b.keys)]
+        else:
+            names = [f.name for f in DEFAULT_FIELDS]
+            rows = self.tok.decode_fields([blk[i, : lens[i]].tolist() for i in range(b.n)], len(names))
+            res = [(k, null_rejection(dict(zip(names, vals)))) for k, vals in zip(b.keys, rows)]
+        self.stats.completed += len(res)
+        self.stats.harvest_s += time.perf_counter() - t0
+        return res
+
+    # -------------------------------------------------------------- scheduler
+    def busy(self) -> bool:
+        return bool(self.waiting or self._pending is not None)
+
+    def step(self, raw: bool = False) -> List[Tuple[Any, Any]]:
+        """Launch a batch of the waiting messages (if any), then harvest the previous
+        batch: the GPU runs batch k while the host stages k and decodes k-1."""
+        t0 = time.perf_counter()
+        new = self._launch() if self.waiting else None
+        if new is not None and self.cfg.measure_idle and self._idle_prev is not None:
+            self._idle_pairs.append((self._idle_prev, new.start_event))
+        if new is not None and self.cfg.measure_idle:
+            self._idle_prev = new.event
+        prev, self._pending = self._pending, new
+        out = self._harvest_batch(prev, raw) if prev is not None else []
+        while self._idle_pairs and self._idle_pairs[0][1].query():
+            a, b = self._idle_pairs.popleft()
+            self.stats.gpu_idle_s += max(0.0, a.elapsed_time(b)) / 1000.0
+        self.stats.steps += 1
+        self.stats.step_s += time.perf_counter() - t0
+        return out
+
+    def debug_logits(self, *a, **k):  # pragma: no cover - the span engine's tool
+        raise NotImplementedError("QAEngine has no decode logits (see ops.qa_decode dbg_scores)")

@@ -28,6 +28,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence
 import numpy as np
 
 from . import protocol as P
+from .qa import null_rejection
 
 __all__ = ["EngineServer", "RemoteEngineClient"]
 
@@ -296,7 +297,7 @@ class RemoteEngineClient:
 
     def decode_answers(self, seqs: List[List[int]]) -> List[Dict[str, str]]:
         fields = self.fields
-        return [dict(zip(fields, vals)) for vals in self.tok.decode_fields(seqs, len(fields))]
+        return [null_rejection(dict(zip(fields, vals))) for vals in self.tok.decode_fields(seqs, len(fields))]
 
     def decode_response(self, buf: bytes) -> List[Dict[str, str]]:
         """Answers of one ``R`` frame (serving/protocol.py)."""
@@ -306,7 +307,8 @@ class RemoteEngineClient:
             rows = self.fast.decode_fields(buf, P.HEADER_SIZE, n, len(fields))
         else:
             rows = self.tok.decode_fields(P.unpack_ids(buf)[2], len(fields))
-        return [dict(zip(fields, vals)) for vals in rows]
+        # a non-transaction (txn_type otp / unknown) comes back with null fields
+        return [null_rejection(dict(zip(fields, vals))) for vals in rows]
 
     def encode_request(self, rid: int, bodies: Sequence[str]) -> bytes:
         """The ``Q`` frame of ``bodies``: ``body <ans>`` ids, each body cut to max_body

@@ -1,0 +1,158 @@
+"""The one-forward span format (serving/qa.py) on the CPU: targets, the reference
+decoder, answer expansion, rejection nulls and the training loss."""
+from __future__ import annotations
+
+from collections import Counter
+
+import numpy as np
+import pytest
+
+from smsgate_amd.models.domain import RawSMS
+from smsgate_amd.models.tokenizer import load_tokenizer
+from smsgate_amd.parse.pipeline import Outcome, postprocess_answer
+from smsgate_amd.parse.text import normalize_body
+from smsgate_amd.serving.fsm import DEFAULT_FIELDS
+from smsgate_amd.serving.qa import (QF_ED, QF_EL, QF_SD, QF_SL, _pair_mask, null_rejection, qa_decode_ref, qa_expand,
+                                    qa_layout, qa_targets, qa_token_flags, valid_ends, valid_starts)
+from smsgate_amd.utils import synth
+
+NAMES = [f.name for f in DEFAULT_FIELDS]
+
+
+@pytest.fixture(scope="module")
+def env():
+    tk = load_tokenizer()
+    lay = qa_layout(8192, 130, 9)
+    return tk, lay, qa_token_flags(tk, lay.vocab)
+
+
+def test_layout_ids_follow_the_tokenizer(env):
+    tk, lay, _ = env
+    assert lay.ptr0 == tk.vocab_size == 8192 and lay.pe0 == lay.ptr0 + 130 and lay.q0 == lay.pe0 + 130
+    assert lay.cls0 == lay.null_id + 1 and lay.vocab % 128 == 0 and lay.vocab >= lay.cls0 + 4
+    assert qa_layout(8192, 130, 17).start_row(1) == 1 and qa_layout(8192, 130, 17).end_row(8) == 16
+    assert lay.start_row(3) == lay.end_row(3) == 3
+    with pytest.raises(ValueError):
+        qa_layout(8192, 130, 10)
+
+
+@pytest.mark.parametrize("which", ["train", "heldout", "heldout_values", "neg_all"])
+def test_gold_answers_are_valid_spans(env, which):
+    """Every gold answer is a span the constrained decoder can produce; decoding one-hot
+    scores of it and expanding gives back exactly the gold values (rejections: nulls)."""
+    tk, lay, fl = env
+    items = synth.generate(800, seed=21, vocab_name="heldout", families=which)
+    bodies = [normalize_body(s.body) for s in items]
+    msgs = tk.message_ids(bodies, 128)
+    encs = tk.encode_offsets(bodies)
+    bad = Counter()
+    for s, b, m, e in zip(items, bodies, msgs, encs):
+        t = qa_targets(tk, lay, fl, s.answer, b, e, len(m))
+        if t is None:
+            bad[s.family] += 1
+            continue
+        cls, spans = t
+        cl = np.full(4, -5.0)
+        cl[cls] = 5.0
+        st = np.full((8, 130), -5.0)
+        en = np.full((8, 130), -5.0)
+        nl = np.zeros(8)
+        for f, (a, z) in enumerate(spans):
+            if a >= 0:
+                st[f, a], en[f, z] = 5.0, 5.0
+        d = qa_decode_ref([cl], [st], [nl], [en], [m], fl, lay)[0]
+        assert d == (cls, spans), (s.family, s.body)
+        ans = null_rejection(dict(zip(NAMES, tk.decode_fields([qa_expand(tk, lay, cls, spans, m)], 9)[0])))
+        raw = RawSMS(msg_id="e", device_id="d", sender="B", date=str(s.timestamp), body=s.body, source="device")
+        r = postprocess_answer(raw, b, ans)
+        if s.kind == "negative":
+            assert r.outcome is Outcome.UNMATCHED, (s.body, ans)
+            assert all(ans[k] is None for k in NAMES[1:])
+        else:
+            assert r.outcome is Outcome.PARSED, (s.body, ans, r.error)
+            for k, v in s.expected.items():
+                got = getattr(r.parsed, k)
+                got = got.value if hasattr(got, "value") else got
+                assert got == v, (s.family, k, got, v, s.body)
+    assert not bad, bad
+
+
+def test_vectorised_pair_mask_equals_the_loop_reference(env):
+    tk, lay, fl = env
+    items = synth.generate(150, seed=8, vocab_name="heldout", families="all", negatives=0.1)
+    for m in tk.message_ids([normalize_body(s.body) for s in items], 128):
+        n = len(m) - 1
+        for bits, cap in zip(lay.class_bits(), lay.caps()):
+            vs, pairs = _pair_mask(fl[np.asarray(m[:n])], n, bits, cap)
+            vs2 = valid_starts(fl, m, n, bits)
+            assert (vs == vs2).all()
+            for s in range(n):
+                ends = valid_ends(fl, m, n, bits, cap, s) if vs2[s] else []
+                assert np.nonzero(pairs[s])[0].tolist() == ends
+
+
+def test_word_boundaries_split_letters_from_digits(env):
+    """"USD52.00", "x1234", "1500р": a value may start / end where a letter meets a digit
+    (the span format's rule glued them); letters / digits on both sides stay glued."""
+    tk, lay, fl = env
+    for text, value in (("Paid USD52.00 at SHOP", "52.00"), ("card x1234 ok", "1234"),
+                        ("Покупка 1500р в МАГАЗИН", "1500"), ("Оплата 1500р", "р")):
+        ids, offs = tk.encode_offsets([text])[0]
+        sp = tk.value_span(value, text, ids, offs)
+        assert sp is not None, (text, value)
+        m = ids + [tk.ans]
+        n = len(m) - 1
+        assert valid_starts(fl, m, n, 0)[sp[0]], (text, value)
+        assert sp[1] in valid_ends(fl, m, n, 0, 48, sp[0]), (text, value)
+    # inside a word: "AM" of "AMERIABANK" is no value
+    ids, offs = tk.encode_offsets(["AMERIABANK API"])[0]
+    assert tk.value_span("AM", "AMERIABANK API", ids, offs) is None
+    f = fl[tk.encode("USD")[0]]
+    assert f & QF_SL and f & QF_EL and not f & (QF_SD | QF_ED)
+
+
+def test_strict_boundaries_win_over_glued_occurrences(env):
+    """The relaxed (letter | digit) rule is a fallback: a number inside a merchant name
+    never shadows the real amount for the training targets."""
+    tk, _, _ = env
+    body = "Paid at AB52 SHOP 52 USD"
+    ids, offs = tk.encode_offsets([body])[0]
+    sp = tk.value_span("52", body, ids, offs)
+    assert tk.decode(ids[sp[0]:sp[1] + 1]).strip() == "52" and sp[0] > 3
+
+
+def test_null_rejection():
+    ans = dict(zip(NAMES, ["unknown", "06.05.25", "1", "USD", "0018", "X", "Y", "", "2"]))
+    out = null_rejection(ans)
+    assert out["txn_type"] == "unknown" and all(out[k] is None for k in NAMES[1:])
+    ok = dict(ans, txn_type="debit")
+    assert null_rejection(ok) == ok
+    assert null_rejection(dict(ans, txn_type="otp"))["amount"] is None
+
+
+def test_reject_class_skips_fields(env):
+    tk, lay, fl = env
+    m = tk.message_ids(["Card *1234 blocked"], 128)[0]
+    cl = np.array([0.0, 0.0, 0.0, 1.0])  # unknown
+    st = np.zeros((8, 130))
+    d = qa_decode_ref([cl], [st], [np.full(8, -1.0)], [st], [m], fl, lay)[0]
+    assert d == (3, [(-1, -1)] * 8)
+    assert tk.decode_fields([qa_expand(tk, lay, *d, m)], 9)[0] == ["unknown"] + [""] * 8
+
+
+def test_qa_training_runs_and_learns_on_cpu():
+    import torch
+
+    from smsgate_amd.models.evaluate import TorchQAExtractor
+    from smsgate_amd.models.train import TrainConfig, train_extractor
+
+    torch.manual_seed(0)
+    losses = []
+    w = train_extractor(TrainConfig(model="tiny", steps=60, batch=16, n_examples=960, log_every=1, warmup=5,
+                                    answer_format="qa", lr=3e-3),
+                        device="cpu", log=lambda s: losses.append(float(s.split("loss")[1].split()[0]))
+                        if "loss" in s else None)
+    assert w.cfg.qa_queries == 9 and w.cfg.vocab == 8576
+    assert np.mean(losses[-10:]) < np.mean(losses[:5]) - 0.3, losses
+    out = TorchQAExtractor(w.float()).run(["APPROVED PURCHASE DB SALE: X, Y,06.05.25 14:23,card ***0018. Amount:5 USD"])
+    assert set(out[0]) == set(NAMES)

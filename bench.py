@@ -71,10 +71,16 @@ def _args(argv=None):
     p.add_argument("--train-steps", type=int, default=4000)
     p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
     p.add_argument("--train-lr", type=float, default=1e-3)
-    # span: the round-4 default (2 decode steps per copied field instead of its tokens; profiles/PERF.md)
-    p.add_argument("--answer-format", default="span", choices=["copy", "span"],
-                   help="span: two pointers per copied field (serving/fsm.py build_span_fsm); copy: each copied "
+    # qa: the round-5 default -- the whole answer from ONE forward (serving/qa.py: query tokens
+    # after the body, joint constrained span decode; no decode steps); span: round 4's
+    # autoregressive pointers (2 decode steps per copied field); copy: each copied field
+    # written with the body's tokens (speculative prompt-lookup decoding)
+    p.add_argument("--answer-format", default="qa", choices=["copy", "span", "qa", "qa17"],
+                   help="qa: one forward, one query row per field (qa17: a start and an end row per field); span: "
+                        "two pointer decode steps per copied field (serving/fsm.py build_span_fsm); copy: each copied "
                         "field written with the body's tokens (speculative prompt-lookup decoding)")
+    p.add_argument("--train-negatives", type=float, default=0.12,
+                   help="share of non-transaction training examples (utils/synth.py NEG_TRAIN_FAMILIES)")
     p.add_argument("--data-workers", type=int, default=12,
                    help="CPU processes building the training examples (started before the GPU is touched)")
     p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",
@@ -94,7 +100,11 @@ def _args(argv=None):
     # reported in quality_heldout.reference_cases (3 / 3 on every round-3 run); 1 = the run fails
     # before the timed region unless all three CASES come out right (the in-run training is not
     # bit-reproducible across boxes, so the default reports rather than gates)
-    p.add_argument("--cases-required", type=int, default=0, choices=[0, 1])
+    p.add_argument("--cases-required", type=int, default=1, choices=[0, 1])
+    # the extractor must also REJECT non-transactions (card blocked, promos, log-in alerts...,
+    # utils/synth.py NEG_FAMILIES): above this share of held-out non-transaction SMS published
+    # on sms.parsed the run fails before the timed region (1 = no gate)
+    p.add_argument("--false-parse-ceiling", type=float, default=0.05)
     p.add_argument("--msgs-per-step", type=int, default=16384)
     p.add_argument("--profile", default="throughput", choices=["throughput", "latency"],
                    help="engine configuration (serving/profiles.py; engine-server --profile serves the same)")
@@ -334,7 +344,8 @@ def run_replica(args, rank: int, world: int, local: int):
             rprof = cProfile.Profile()
             rprof.enable()
         first = args.warmup if not http else 10_001
-        dt_p, counts_p = coord.run_phase(seeds(first, args.steps, http), per[http], sync=sync)
+        dt_p, counts_p = coord.run_phase(seeds(first, args.steps, http), per[http], sync=sync,
+                                         profile=bool(args.profile_cpu) and not http)
         if rprof is not None:
             rprof.disable()
             os.makedirs(args.profile_cpu, exist_ok=True)
@@ -438,7 +449,8 @@ def evaluate_quality(engine, args) -> dict:
 
     Every field is scored after the real post-processing chain against the
     generator's expected value (models/evaluate.py)."""
-    from smsgate_amd.models.evaluate import evaluate_engine, golden_case_mismatches, golden_case_results
+    from smsgate_amd.models.evaluate import (evaluate_engine, evaluate_negatives, golden_case_mismatches,
+                                             golden_case_results)
 
     def short(q):
         out = {"exact": round(q["exact"], 4), "parse_rate": round(q["parse_rate"], 4), "n": q["n"],
@@ -451,13 +463,26 @@ def evaluate_quality(engine, args) -> dict:
     ho = evaluate_engine(engine, n=args.eval_n, seed=4243, vocab_name="heldout", families="heldout", with_regex=True)
     tr = evaluate_engine(engine, n=args.eval_n, seed=4242, vocab_name="heldout", families="train")
     leg = evaluate_engine(engine, n=args.eval_n, seed=4242, vocab_name="heldout")
+    hv = evaluate_engine(engine, n=args.eval_n, seed=4245, vocab_name="heldout", families="heldout_values")
+    neg_h = evaluate_negatives(engine, n=args.eval_n, seed=4246, vocab_name="heldout", families="neg_heldout")
+    neg_t = evaluate_negatives(engine, n=args.eval_n, seed=4247, vocab_name="heldout", families="neg_train")
     quality = {"heldout_formats": short(ho), "train_formats": short(tr), "legacy_mix": short(leg),
+               "heldout_values": short(hv),
+               "negatives": {"false_parsed_rate": round(neg_h["false_parsed_rate"], 4), "n": neg_h["n"],
+                             "by_family": neg_h["by_family"], "txn_type": neg_h["txn_type"],
+                             "families": "held-out non-transaction families (never trained on)",
+                             "train_families": {"false_parsed_rate": round(neg_t["false_parsed_rate"], 4),
+                                                "n": neg_t["n"], "by_family": neg_t["by_family"]},
+                             "ceiling": args.false_parse_ceiling},
                "vocab": "heldout (merchant/city/street names never trained on)", "floor": args.quality_floor,
-               "gate": "heldout_formats.exact"}
+               "gate": "heldout_formats.exact >= floor and negatives.false_parsed_rate <= ceiling"}
     print(f"[bench] quality: {json.dumps(quality)}", file=sys.stderr, flush=True)
     if args.weights != "random" and ho["exact"] < args.quality_floor:
         raise SystemExit(f"bench: held-out-format exact-answer rate {ho['exact']:.4f} is below the quality floor "
                          f"{args.quality_floor} -- no throughput is reported for a broken extractor")
+    if args.weights != "random" and neg_h["false_parsed_rate"] > args.false_parse_ceiling:
+        raise SystemExit(f"bench: {neg_h['false_parsed_rate']:.4f} of held-out non-transactions would be published "
+                         f"on sms.parsed (ceiling {args.false_parse_ceiling}) -- the extractor does not reject them")
     bad = golden_case_mismatches(golden_case_results(engine))
     quality["reference_cases"] = {"passed": 3 - len({b.split(".")[0].split(":")[0] for b in bad}), "of": 3,
                                   "mismatches": bad, "required": bool(args.cases_required)}
@@ -678,7 +703,7 @@ def _train_plan(args):
     # held-out exact 89.6 % vs 87.4 % for 60 k examples reused ~4x (profiles/r03_quality_probe.jsonl)
     tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
                      n_examples=args.train_steps * args.train_batch, log_every=200, data_parallel=False,
-                     families="train", answer_format=args.answer_format)
+                     families="train", answer_format=args.answer_format, negatives=args.train_negatives)
     # every source the trained weights depend on (a cached file from older training code
     # on the same box was reused once: the key now covers the trainer, the answer FSM,
     # the model and the tokenizer code too)
@@ -704,7 +729,7 @@ def start_training_data(args, local: int):
     from smsgate_amd.models.train import ExamplePool
 
     return ExamplePool(tc.n_examples, seed=tc.seed, families=tc.families, workers=args.data_workers,
-                       answer_format=tc.answer_format)
+                       answer_format=tc.answer_format, negatives=tc.negatives)
 
 
 def acquire_weights(args, device: str, rank: int, world: int, pool=None):
@@ -867,9 +892,13 @@ def main(argv=None) -> int:
                 "global_batch": args.msgs_per_step * world,
                 "msgs_per_step_per_gpu": args.msgs_per_step,
                 "seq_len": ("shared prefix 4 (<bos> txn: <sms>) + ~40 prompt + "
-                            + ("<=25 schema-constrained decode steps (txn_type, then a start and an end pointer "
-                               "into the SMS per copied field; ~17 on this traffic)" if args.answer_format == "span"
-                               else "<=155 schema-constrained output tokens (~37 trained)")),
+                            + ({"span": "<=25 schema-constrained decode steps (txn_type, then a start and an end "
+                                        "pointer into the SMS per copied field; ~17 on this traffic)",
+                                "qa": "9 query tokens, ONE forward (class + joint constrained span decode per "
+                                      "field, no decode steps)",
+                                "qa17": "17 query tokens, ONE forward (class + joint constrained span decode per "
+                                        "field, no decode steps)"}.get(args.answer_format,
+                                                                      "<=155 schema-constrained output tokens"))),
                 "answer_format": args.answer_format,
                 "parallelism": f"dp{world}" if gpu else "cpu",
                 "cpu_workers_per_gpu": args.cpu_workers if gpu else 1,
@@ -884,6 +913,8 @@ def main(argv=None) -> int:
         }
         if quality is not None:
             out["quality_heldout_formats"] = quality.pop("heldout_formats")
+            out["quality_heldout_values"] = quality.pop("heldout_values")
+            out["quality_negatives"] = quality.pop("negatives")
             out["quality_train_formats"] = quality.pop("train_formats")
             out["quality_heldout"] = quality
         if cpu is not None:

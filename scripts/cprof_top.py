@@ -35,10 +35,15 @@ def main() -> int:
     p.add_argument("--n", type=int, default=20)
     a = p.parse_args()
     msgs = 0
-    if a.bench:
+    parsers = sorted(glob.glob(os.path.join(a.dir, "parser-*.pstats")))
+    # the messages the parser processes actually parsed while profiling (each dumps its
+    # count next to its stats: only the timed bus phase is profiled)
+    side = [p[: -len(".pstats")] + ".json" for p in parsers]
+    if side and all(os.path.exists(s) for s in side):
+        msgs = sum(json.load(open(s))["msgs"] for s in side)
+    elif a.bench:
         d = json.loads([x for x in open(a.bench) if x.startswith("{")][-1])
         msgs = d["steps"] * d["config"]["msgs_per_step_per_gpu"]  # the profiled (timed) phase
-    parsers = sorted(glob.glob(os.path.join(a.dir, "parser-*.pstats")))
     ranks = sorted(glob.glob(os.path.join(a.dir, "rank*.pstats")))
     print(f"# cProfile of the timed phase ({a.dir}); own time excludes callees; blocking waits (poll / epoll /"
           " event sync) are idle, not CPU")

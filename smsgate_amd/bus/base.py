@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import abc
 import enum
+import re
 import time
 from dataclasses import dataclass
 from typing import AsyncIterator, Dict, List, Optional, Sequence, Tuple
@@ -54,6 +55,7 @@ __all__ = [
     "Subscription",
     "Bus",
     "BusError",
+    "bus_error",
     "subject_matches",
     "default_stream_config",
 ]
@@ -79,8 +81,26 @@ class BusError(RuntimeError):
 
 class BusUnavailable(BusError, ConnectionError):
     """The broker could not be reached (connection closed / reset, no responders,
-    timeout).  Not any message's fault: the consume loop naks the batch whole
-    (runtime/stage.py TRANSIENT) instead of isolating and dead-lettering."""
+    timeout) or refuses EVERY request for now (stream full, resource limits, no
+    leader, no stream for the subject).  Not any message's fault: the consume loop
+    naks the batch whole (runtime/stage.py TRANSIENT) instead of isolating and
+    dead-lettering."""
+
+
+# Refusals that hit every message alike (ADVICE r04): JetStream's publish-ack errors
+# for a full DiscardNew stream, resource limits, a leader election / cluster outage,
+# and a subject no stream captures.  A refusal about ONE message (its payload over
+# the maximum size, a malformed request) stays a plain BusError.
+_BROKER_WIDE = re.compile(
+    r"insufficient (storage |system )?resources|maximum (messages|bytes|consumers|streams)( per subject)? exceeded"
+    r"|resource limits|no (stream|responders)|stream not found|not enabled|leader|cluster|temporarily unavailable"
+    r"|unavailable|jetstream.*(offline|not ready)|503|no space left|storage full|stream (is )?full", re.I)
+
+
+def bus_error(desc: str) -> BusError:
+    """The exception for a broker's refusal ``desc``: :class:`BusUnavailable` when the
+    condition is broker-wide (every message would fail alike), else :class:`BusError`."""
+    return BusUnavailable(desc) if _BROKER_WIDE.search(desc or "") else BusError(desc)
 
 
 class DeliverPolicy(str, enum.Enum):

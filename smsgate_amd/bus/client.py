@@ -11,6 +11,7 @@ from .base import (
     Bus,
     BusError,
     BusUnavailable,
+    bus_error,
     ConsumerInfo,
     Msg,
     MsgMetadata,
@@ -72,7 +73,7 @@ class RemoteBus(Bus, Acker):
                     if ok:
                         fut.set_result(res)
                     else:
-                        fut.set_exception(BusError(res))
+                        fut.set_exception(bus_error(str(res)))
         except (asyncio.IncompleteReadError, ConnectionError, asyncio.CancelledError):
             self._closed = True
             for fut in self._pending.values():

@@ -21,6 +21,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 
 from .base import (
     BusError,
+    BusUnavailable,
     ConsumerConfig,
     ConsumerInfo,
     DeliverPolicy,
@@ -115,8 +116,8 @@ class Engine:
                     st = cand
                     break
             self._route_cache[subject] = st
-        if st is None:
-            raise BusError(f"no stream matches subject {subject!r}")
+        if st is None:  # every message to it would fail alike: not one message's fault
+            raise BusUnavailable(f"no stream matches subject {subject!r}")
         return st
 
     def store(self, subject: str, data: bytes, headers: Optional[Dict[str, str]] = None,

@@ -31,6 +31,7 @@ from .base import (
     Bus,
     BusError,
     BusUnavailable,
+    bus_error,
     ConsumerConfig,
     ConsumerInfo,
     Msg,
@@ -231,6 +232,8 @@ class NatsBus(Bus):
         try:
             await self._pub(subject, payload, inbox)
             return await asyncio.wait_for(fut, timeout or self.timeout)
+        except asyncio.TimeoutError:
+            raise BusUnavailable(f"NATS request on {subject!r} timed out") from None
         finally:
             self._resp.pop(inbox, None)
 
@@ -265,11 +268,11 @@ class NatsBus(Bus):
         f = await self.request(subject, data) if not headers else await self._request_h(subject, data, headers)
         if f.op == "HMSG":
             status, text, _ = P.decode_headers(f.headers)
-            if status == 503:
-                raise BusError(f"no stream captures subject {subject!r}")
+            if status == 503:  # no stream captures it: every publish to it fails alike
+                raise BusUnavailable(f"no stream captures subject {subject!r}")
         d = json.loads(f.payload or b"{}")
         if "error" in d:
-            raise BusError(d["error"].get("description", "publish failed"))
+            raise bus_error(d["error"].get("description", "publish failed"))
         return PubAck(stream=d.get("stream", ""), seq=int(d.get("seq", 0)), duplicate=bool(d.get("duplicate")))
 
     async def _request_h(self, subject: str, data: bytes, headers: Dict[str, str]) -> P.Frame:
@@ -280,6 +283,8 @@ class NatsBus(Bus):
         try:
             await self._pub(subject, data, inbox, P.encode_headers(headers))
             return await asyncio.wait_for(fut, self.timeout)
+        except asyncio.TimeoutError:
+            raise BusUnavailable(f"NATS publish on {subject!r} timed out") from None
         finally:
             self._resp.pop(inbox, None)
 
@@ -292,7 +297,7 @@ class NatsBus(Bus):
         d = await self.api("STREAM.NAMES", {"subject": subject})
         names = d.get("streams") or []
         if not names:
-            raise BusError(f"no stream for subject {subject!r}")
+            raise BusUnavailable(f"no stream for subject {subject!r}")
         self._stream_cache[subject] = names[0]
         return names[0]
 

@@ -643,16 +643,28 @@ __global__ void __launch_bounds__(256) sparse_argmax_kernel(
     const int k8 = kind & 0xff, cls = (kind >> 16) & 0xff;
     if (k8 == 3) {
       // span start (serving/fsm.py build_span_fsm): pointer ptr0 + j to a body token at a
-      // word boundary and in the field's class; never the closing <ans> (position bl-1)
+      // word boundary and in the field's class; never the closing <ans> (position bl-1);
+      // and only a start that HAS an end (the end state has no <sep>, so a
+      // start glued into an out-of-class token -- "1500р" -- would end the answer):
+      // some e in [j, j + cap) with j..e in class and a word boundary after e
       const int np = min(bl - 1, n_pos);
+      const int cap = (kind >> 8) & 0xff;
       const bool no_mask = (cls & (4 | 8)) != 0;  // dates / numbers never start right after a card mask
       for (int j = lane; j < np; j += 64) {
         const int t = body[j];
         const int fp = j > 0 ? flags(body[j - 1]) : 0;
         const bool glued = (fp & 2) && (flags(t) & 1);
         if (!glued && (cls == 0 || (flags(t) & cls)) && !(no_mask && (fp & 64))) {
+          bool has_end = cap == 0;  // (an FSM built without caps in its start states)
+          const int nb = bl - 1;
+          for (int e = j; !has_end && e < min(nb, j + cap); ++e) {
+            const int te = body[e];
+            if (cls && !(flags(te) & cls)) break;
+            const int nx = e + 1 < nb ? body[e + 1] : -1;
+            has_end = nx < 0 || !((flags(te) & 2) && (flags(nx) & 1));
+          }
           const int c = ptr0 + j;
-          if (c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
+          if (has_end && c < fsm.V) atomicOr(&b[c >> 5], 1u << (c & 31));
         }
       }
       if (lane == 0) atomicOr(&b[sep >> 5], 1u << (sep & 31));  // an empty value

@@ -124,8 +124,11 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     await writer.start()
     client.send_control({"event": "ready", "w": widx})
     prepared: List[List[Any]] = []
-    # cProfile of the timed phases only (bench.py --profile-cpu DIR)
+    # cProfile of the phases the coordinator marks as profiled (bench.py --profile-cpu DIR:
+    # the timed bus phase only -- not the warm-up or the HTTP phase); prof_msgs counts the
+    # messages this process parsed while it was on, the per-message denominator
     prof = None
+    prof_msgs = 0
     if cfg.get("profile_dir"):
         import cProfile
 
@@ -140,7 +143,8 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                         for seed in cmd["seeds"]]
             client.send_control({"event": "prepared", "w": widx})
         elif cmd["cmd"] == "go":
-            if prof is not None:
+            profiling = prof is not None and bool(cmd.get("profile"))
+            if profiling:
                 prof.enable()
             c0 = dict(worker.counts)
             w0 = (writer.stage.processed, writer.ok, writer.skipped, writer.fail)
@@ -168,8 +172,9 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                 counts = {k: worker.counts[k] - c0[k] for k in c0}
                 counts.update(sink_stored=writer.ok - w0[1], writer_no_merchant=writer.skipped - w0[2],
                               writer_fail=writer.fail - w0[3])
-                if prof is not None:
+                if profiling:
                     prof.disable()
+                    prof_msgs += worker.stage.processed - base
                 client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
                 continue
             pub_task = asyncio.create_task(publish(0)) if nsteps else None
@@ -191,12 +196,18 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
             counts = {k: worker.counts[k] - c0[k] for k in c0}
             counts.update(sink_stored=writer.ok - w0[1], writer_no_merchant=writer.skipped - w0[2],
                           writer_fail=writer.fail - w0[3])
-            if prof is not None:
+            if profiling:
                 prof.disable()
+                prof_msgs += worker.stage.processed - base
             client.send_control({"event": "done", "w": widx, "s": time.perf_counter() - t0, "counts": counts})
     if prof is not None:
+        import json as _json
+
         os.makedirs(cfg["profile_dir"], exist_ok=True)
-        prof.dump_stats(os.path.join(cfg["profile_dir"], f"parser-r{rank}-w{widx}.pstats"))
+        stem = os.path.join(cfg["profile_dir"], f"parser-r{rank}-w{widx}")
+        prof.dump_stats(stem + ".pstats")
+        with open(stem + ".json", "w") as fh:
+            _json.dump({"msgs": prof_msgs}, fh)
     await writer.stop()
     await worker.stop()
 
@@ -384,8 +395,10 @@ class Coordinator:
             self.server.send_control(i, obj)
 
     def run_phase(self, seeds_per_worker: Sequence[Sequence[int]], n_per_step: int,
-                  sync=None) -> Tuple[float, Dict[str, int]]:
-        """Prepare (untimed), then time ``go`` → all ``done``. Returns (seconds, routing counts)."""
+                  sync=None, profile: bool = False) -> Tuple[float, Dict[str, int]]:
+        """Prepare (untimed), then time ``go`` → all ``done``. Returns (seconds, routing counts).
+        ``profile``: the parser processes cProfile this phase (when they were started with
+        a profile_dir)."""
         self.last_http = {}
         for i in range(self.n):
             self.server.send_control(i, {"cmd": "prepare", "n": n_per_step, "seeds": list(seeds_per_worker[i])})
@@ -397,7 +410,7 @@ class Coordinator:
         if sync is not None:
             sync()
         t0 = time.perf_counter()
-        self.broadcast({"cmd": "go"})
+        self.broadcast({"cmd": "go", "profile": bool(profile)})
         if self.bus is not None:
             self.wait_all("published")
             last = [0.0]

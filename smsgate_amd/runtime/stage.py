@@ -12,12 +12,14 @@ is the one loop, written once:
 * never dies on a handler exception (D1/D2), and bounds poison messages:
 
   - a :class:`~smsgate_amd.runtime.errors.TransientError` (engine restarting,
-    socket closed), a ``BusUnavailable`` / ``ConnectionError`` / timeout (the
-    broker went away mid-batch) naks the whole batch with a delay — not the
+    socket closed, its request timed out), a ``BusUnavailable`` /
+    ``ConnectionError`` (the broker went away mid-batch, timed out, or refuses every
+    request for now: stream full, resource limits, no leader, no stream for the
+    subject -- ``bus.base.bus_error``) naks the whole batch with a delay — not the
     messages' fault, so it never counts toward dead-lettering.  A plain
     ``BusError`` is the broker refusing ONE request (a publish over the maximum
-    payload, no stream for a subject): that is a property of a message and takes
-    the isolate / dead-letter path below, so it cannot pin its batch forever;
+    payload): that is a property of a message and takes the isolate / dead-letter
+    path below, so it cannot pin its batch forever; so does any other timeout;
   - any other exception re-runs the batch one message at a time, so the good
     messages of the batch go through and only the failing one is isolated;
     that one is nak'ed with a delay until it has been delivered
@@ -45,9 +47,14 @@ log = logging.getLogger(__name__)
 
 # not the messages' fault: the batch is nak'ed whole (never split into per-message
 # re-runs, never counted toward dead-lettering) -- a dependency (engine, broker) is
-# down or the connection to the broker broke mid-batch.  (BusUnavailable is a
-# ConnectionError; a plain BusError -- the broker refused one request -- is not here.)
-TRANSIENT = (TransientError, BusUnavailable, ConnectionError, asyncio.TimeoutError, TimeoutError)
+# down, refuses every request for now (stream full, no leader: bus.base.bus_error), or
+# the connection broke mid-batch.  (BusUnavailable is a ConnectionError; a plain
+# BusError -- the broker refused ONE request -- is not here.)  Timeouts are not here
+# either: the bus and engine clients turn THEIR timeouts into
+# BusUnavailable / BackendUnavailable; any other TimeoutError (a handler timing out the
+# same way on one message every time) takes the isolate / dead-letter path, so it
+# cannot pin its batch forever.
+TRANSIENT = (TransientError, BusUnavailable, ConnectionError)
 
 # a dead-letter envelope carries at most this much of the failed payload: the payload
 # may be what the broker refused (over its maximum size), and the envelope must fit

@@ -291,23 +291,33 @@ class SchemaFSM:
         def in_cls(t: int) -> bool:
             return cls == 0 or bool(int(tf[t]) & cls) if 0 <= t < self.vocab else False
 
+        cap = (kind >> 8) & 0xFF
+
+        def ends(s: int) -> List[int]:
+            out = []
+            for e in range(s, min(n, s + cap)):
+                if not in_cls(body[e]):
+                    break
+                if e + 1 >= n or self._boundary(body[e], body[e + 1]):
+                    out.append(e)
+            return out
+
         if kind & 0xFF == PTR_START:
             cand[self.sep_token] = True
             no_mask = bool(cls & _NO_START_AFTER_MASK)
             for j in range(min(n, self.n_pos)):
+                # a start must have an end (the end state has no <sep>); an FSM
+                # whose start states carry no cap (cap 0) skips the check
                 if (j == 0 or self._boundary(body[j - 1], body[j])) and in_cls(body[j]) and \
-                        not (no_mask and j > 0 and 0 <= body[j - 1] < self.vocab and tf[body[j - 1]] & TOK_ENDS_MASK):
+                        not (no_mask and j > 0 and 0 <= body[j - 1] < self.vocab and tf[body[j - 1]] & TOK_ENDS_MASK) \
+                        and (cap == 0 or ends(j)):
                     cand[self.ptr0 + j] = True
             return cand
-        cap = (kind >> 8) & 0xFF
         s = prev - self.ptr0
         if not 0 <= s < n:
             return cand
-        for e in range(s, min(n, s + cap)):
-            if not in_cls(body[e]):
-                break
-            if e + 1 >= n or self._boundary(body[e], body[e + 1]):
-                cand[self.ptr0 + e] = True
+        for e in ends(s):
+            cand[self.ptr0 + e] = True
         return cand
 
     def expand_span_answer(self, toks: Sequence[int], body: Sequence[int]) -> List[int]:
@@ -472,9 +482,9 @@ def build_span_fsm(tokenizer, vocab_tok: int, n_pos: int,
     vocabulary: the model's embedding row of pointer ``j`` is also added to the input
     of prompt position ``j``, so the model can name a position by "reading" it there).
 
-    States per copied field: start (kind PTR_START | class << 16: a pointer -> end,
-    <sep> -> next field) and end (PTR_END | cap << 8 | class << 16: a pointer -> next
-    field).  The
+    States per copied field: start (kind PTR_START | cap << 8 | class << 16: a pointer
+    -> end, <sep> -> next field; only starts with at least one valid end are offered)
+    and end (PTR_END | cap << 8 | class << 16: a pointer -> next field).  The
     vocabulary is rounded up to 128 (the lm_head / mask tiles)."""
     V = -(-(vocab_tok + n_pos) // 128) * 128
     strings = tokenizer.token_strings
@@ -529,7 +539,8 @@ def build_span_fsm(tokenizer, vocab_tok: int, n_pos: int,
             m = ptrs.copy()
             m[sep] = True
             cls = TOK_CLASS_BITS.get(f.kind, 0)
-            a = new_state(m, fi, PTR_START | (cls << 16))
+            # the start state carries the cap too: a start is offered only if it has an end
+            a = new_state(m, fi, PTR_START | (f.cap << 8) | (cls << 16))
             b = new_state(ptrs.copy(), fi, PTR_END | (f.cap << 8) | (cls << 16))
             next_tok[a] = b
             starts.append(a)

@@ -122,3 +122,35 @@ def test_dates_and_numbers_never_start_inside_a_card_mask(fsms):
     date_st = [s for s in range(f.num_states)
                if f.field_of_state[s] == by_field["date"] and int(f.copy_kind[s]) & 0xFF == PTR_START][0]
     assert f.copy_mask_host(date_st, -1, msg)[f.ptr0 + j_date]
+
+
+def test_a_start_is_offered_only_with_an_end(fsms):
+    """the end state has no <sep>, so a start whose word runs on into a glued
+    out-of-class token ("1500р", "17.05.24г") must not be offered -- else the kernel's
+    empty end set decodes <sep> and span_commit ends the whole answer.  Every offered
+    start has at least one end; the glued amount is not offered, the later fields are."""
+    tk, f, _ = fsms
+    body = "Покупка 1500р MARKET, YEREVAN. 17.05.24г Карта *1234. Баланс 200 RUB"
+    msg = tk.message_ids([body], 128)[0]
+    strings = [tk.token_strings[t] for t in msg]
+    fi = {x.name: k for k, x in enumerate(f.fields)}
+    starts = {name: [s for s in range(f.num_states) if f.field_of_state[s] == fi[name]
+                     and f.copy_kind[s] & 0xFF == PTR_START][0] for name in ("amount", "date", "balance", "card")}
+    j1500 = next(j for j, t in enumerate(strings) if t.strip() == "15")  # " 15" "00" "р"
+    m = f.copy_mask_host(starts["amount"], -1, msg)
+    assert not m[f.ptr0 + j1500]  # "1500" + "р": no number end after it
+    for name, st in starts.items():
+        cand = [j for j in range(len(msg)) if f.copy_mask_host(st, -1, msg)[f.ptr0 + j]]
+        for j in cand:
+            e = f.copy_mask_host(int(f.next_tok[st]), f.ptr0 + j, msg)
+            assert e[f.ptr0:f.ptr0 + len(msg)].any(), (name, j, strings[j])
+    # the balance (after the glued tokens) is still reachable
+    jb = next(j for j, t in enumerate(strings) if t.strip() == "200")
+    assert f.copy_mask_host(starts["balance"], -1, msg)[f.ptr0 + jb]
+    # property: over generated bodies (glued currencies included) no start lacks an end
+    items = generate(300, seed=61, vocab_name="heldout", families="all", negatives=0.1)
+    for s in items:
+        m2 = tk.message_ids([normalize_body(s.body)], 128)[0]
+        for st in starts.values():
+            for j in np.nonzero(f.copy_mask_host(st, -1, m2)[f.ptr0:f.ptr0 + len(m2)])[0]:
+                assert f.copy_mask_host(int(f.next_tok[st]), f.ptr0 + int(j), m2)[f.ptr0:f.ptr0 + len(m2)].any()

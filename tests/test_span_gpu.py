@@ -111,25 +111,15 @@ def _span_engine(w, **kw):
     return ExtractionEngine(w, load_tokenizer(), EngineConfig(**{"max_slots": 512, "buckets": (64, 512), **kw}))
 
 
-def test_span_engine_matches_fp32_reference_decode():
-    """Random-init span model vs a plain fp32 PyTorch greedy decode under the host
-    rules: teacher-forced on the reference's answers, the engine's logits (pointer rows
-    added to the prompt inputs, pointer ids fed back as decode inputs, the lm_head over
-    tokenizer + pointer rows) match at every step, and the greedy answers agree except
-    where bf16 rounding flips a near-tie (one flip changes a whole answer)."""
-    from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, reference_forward, span_config
+def _ref_greedy(w, fsm, tok, bodies):
+    """fp32 PyTorch greedy decode of span weights ``w`` under the host rules: the
+    answers and every step's logits."""
+    from smsgate_amd.models.extractor import ExtractorWeights, reference_forward
     from smsgate_amd.parse.schema import EXTRACTOR_PROMPT
 
-    cfg = span_config(CONFIGS["small"])
-    w = ExtractorWeights(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
-    eng = _span_engine(w, use_graphs=False)
-    assert eng.span and not eng.spec and eng.Lmax == 160 and eng.V_dec == 8448
-    tok, fsm = eng.tok, eng.fsm
-    bodies = [normalize_body(s.body) for s in generate(24, seed=8, vocab_name="heldout", families="train") if s.answer]
-    bodies += [normalize_body(b) for b in reference_cases()]
     msgs = tok.message_ids(bodies, 128)
     prefix = tok.prefix_ids(EXTRACTOR_PROMPT)
-    wf = ExtractorWeights(cfg, device=DEV, dtype=torch.float32, seed=None)
+    wf = ExtractorWeights(w.cfg, device=DEV, dtype=torch.float32, seed=None)
     wf.load_state_dict({k: v.float() for k, v in w.state_dict().items()})
     refs, ref_logits = [], []
     with torch.no_grad():
@@ -140,8 +130,8 @@ def test_span_engine_matches_fp32_reference_decode():
             while st != fsm.done_state and len(ans) < fsm.max_steps():
                 logits = reference_forward(wf, torch.tensor([seq], device=DEV),
                                            add_ids=torch.tensor([add], device=DEV))[0, -1, : fsm.vocab]
-                lgs.append(logits)
                 allowed = torch.tensor(fsm.copy_mask_host(st, prev, m), device=DEV)
+                lgs.append((logits, allowed))
                 t = int(logits.masked_fill(~allowed, float("-inf")).argmax())
                 ans.append(t)
                 seq.append(t)
@@ -149,21 +139,70 @@ def test_span_engine_matches_fp32_reference_decode():
                 st, prev = fsm.step_host(st, t), t
             refs.append(ans)
             ref_logits.append(lgs)
+    return msgs, refs, ref_logits
+
+
+def _tol(scale: float) -> float:
+    return 0.05 * scale + 0.05  # bf16 forward vs fp32 (the logits bound asserted below)
+
+
+def test_span_engine_matches_fp32_reference_decode():
+    """Random-init span model vs a plain fp32 PyTorch greedy decode under the host
+    rules: teacher-forced on the reference's answers, the engine's logits (pointer rows
+    added to the prompt inputs, pointer ids fed back as decode inputs, the lm_head over
+    tokenizer + pointer rows) match at every step within bf16 rounding."""
+    from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, span_config
+
+    cfg = span_config(CONFIGS["small"])
+    w = ExtractorWeights(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+    eng = _span_engine(w, use_graphs=False)
+    assert eng.span and not eng.spec and eng.Lmax == 160 and eng.V_dec == 8448
+    tok, fsm = eng.tok, eng.fsm
+    bodies = [normalize_body(s.body) for s in generate(24, seed=8, vocab_name="heldout", families="train") if s.answer]
+    bodies += [normalize_body(b) for b in reference_cases()]
+    msgs, refs, ref_logits = _ref_greedy(w, fsm, tok, bodies)
     L = max(len(a) for a in refs)
     forced = [a + [fsm.sep_token] * (L - len(a)) for a in refs]
     outs = eng.debug_logits(bodies, [f[:L - 1] for f in forced])
     for b, lgs in enumerate(ref_logits):
-        for step, ref in enumerate(lgs):
+        for step, (ref, _) in enumerate(lgs):
             got = outs[step][b, : fsm.vocab].float()
             scale = ref.abs().max().item()
             err = (got - ref).abs().max().item()
-            assert err <= 0.05 * scale + 0.05, (b, step, err, scale)
+            assert err <= _tol(scale), (b, step, err, scale)
+
+
+def test_span_engine_answers_match_fp32_reference(span_small):
+    """The trained span model through the engine vs the fp32 PyTorch greedy decode: at
+    least 90 % of the answers identical, and EVERY disagreement explained -- at the first
+    step where the engine's (teacher-forced) choice differs, the fp32 top-2 margin
+    between the two tokens is within bf16 rounding of the engine's forward."""
+    eng = _span_engine(span_small, use_graphs=False)
+    tok, fsm = eng.tok, eng.fsm
+    items = [s for s in generate(120, seed=9, vocab_name="heldout") if s.answer]  # the mix it was trained on
+    bodies = [normalize_body(s.body) for s in items] + [normalize_body(b) for b in reference_cases()]
+    msgs, refs, ref_logits = _ref_greedy(span_small, fsm, tok, bodies)
     got = eng.run(bodies)
+    L = max(len(a) for a in refs)
+    forced = [a + [fsm.sep_token] * (L - len(a)) for a in refs]
+    outs = eng.debug_logits(bodies, [f[:L - 1] for f in forced])
     same = 0
-    for m, a, g in zip(msgs, refs, got):
+    for b, (m, a, g) in enumerate(zip(msgs, refs, got)):
         vals = fsm.split_fields(fsm.expand_span_answer(a, m))
-        same += {f.name: tok.decode(v).strip() for f, v in zip(fsm.fields, vals)} == g
-    assert same >= 0.4 * len(bodies), (same, len(bodies))
+        if {f.name: tok.decode(v).strip() for f, v in zip(fsm.fields, vals)} == g:
+            same += 1
+            continue
+        explained = False
+        for step, (ref, allowed) in enumerate(ref_logits[b]):
+            e = outs[step][b, : fsm.vocab].float().masked_fill(~allowed, float("-inf"))
+            te = int(e.argmax())
+            if te != a[step]:
+                margin = float(ref[a[step]] - ref[te])
+                assert 0 <= margin <= _tol(float(ref.abs().max())), (b, step, margin)
+                explained = True
+                break
+        assert explained, (b, g, a)
+    assert same >= 0.9 * len(bodies), (same, len(bodies))
 
 
 @pytest.fixture(scope="module")
@@ -212,7 +251,7 @@ def test_span_templates_keep_answers(span_small):
     for b, x, y in bad[:8]:
         print("MISMATCH", repr(b[:120]), {k: (x[k], y[k]) for k in x if x[k] != y[k]})
     assert stats[1].templates > 0 and stats[1].template_tokens > 0.5 * len(bodies)
-    assert len(bad) <= 0.01 * len(bodies), len(bad)
+    assert not bad, len(bad)  # 0 of 1 200 in every logged run (profiles/r04_span_pytest.log)
 
 
 def test_span_engine_survives_nan_filled_allocator_blocks(span_small):
@@ -234,7 +273,7 @@ def test_span_engine_survives_nan_filled_allocator_blocks(span_small):
     eng = _span_engine(span_small, **kw)
     dirty = eng.run(bodies)
     same = sum(a == b for a, b in zip(clean, dirty))
-    assert same >= 0.99 * len(bodies), same
+    assert same == len(bodies), same  # a partial regression of the NaN leak fails too
 
 
 def test_embed_rows_add_matches_torch():
@@ -246,3 +285,41 @@ def test_embed_rows_add_matches_torch():
     got = ops.embed_rows_add(ids, pos, table, 8192)
     ref = table[ids.long()] + table[pos.long() + 8192]
     assert torch.equal(got, ref)
+
+
+def test_sparse_argmax_never_picks_a_start_without_an_end():
+    """ADVICE r04 on the GPU: rows whose hidden state points straight at a start that has
+    no end ("15" of "1500р", glued) get another allowed token from the kernel -- the host
+    rule (serving/fsm.py _span_candidates) and the kernel agree."""
+    tok = load_tokenizer()
+    fsm = answer_fsm(tok, "span").to_device(DEV)
+    bodies = ["Покупка 1500р MARKET, YEREVAN. Карта *1234. Баланс 200 RUB",
+              "Оплата 99р SHOP 17.05.24г карта *4321 остаток 5 RUB"]
+    msgs = tok.message_ids(bodies, 128)
+    fi = next(k for k, x in enumerate(fsm.fields) if x.name == "amount")
+    st = [s for s in range(fsm.num_states) if fsm.field_of_state[s] == fi and fsm.copy_kind[s] & 0xFF == 3][0]
+    H = 576
+    g = torch.Generator().manual_seed(3)
+    w = (torch.randn(fsm.vocab, H, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    rows, glued = [], []
+    for m in msgs:
+        strings = [tok.token_strings[t] for t in m]
+        j = next(j for j, t in enumerate(strings) if t.strip() in ("15", "99"))
+        assert not fsm.copy_mask_host(st, -1, m)[fsm.ptr0 + j]
+        rows.append(w[fsm.ptr0 + j].float() * 20)
+        glued.append(fsm.ptr0 + j)
+    n = len(msgs)
+    h = torch.stack(rows).to(torch.bfloat16)
+    body = torch.zeros(n, 130, **i32)
+    blen = torch.zeros(n, **i32)
+    for r, m in enumerate(msgs):
+        body[r, :len(m)] = torch.tensor(m)
+        blen[r] = len(m)
+    best = torch.zeros(n, dtype=torch.int64, device=DEV)
+    state = torch.full((n,), st, **i32)
+    ops.sparse_argmax(h, ops.fold_norm(w, torch.ones(H, dtype=torch.bfloat16, device=DEV)), state, fsm, best,
+                      torch.tensor([m[-1] for m in msgs], **i32), torch.arange(n, **i32), body, blen, 1e-5)
+    torch.cuda.synchronize()
+    for r, m in enumerate(msgs):
+        t = (0xFFFFFFFF - (int(best[r]) & 0xFFFFFFFF)) if int(best[r]) else fsm.sep_token
+        assert t != glued[r] and fsm.copy_mask_host(st, -1, m)[t], (r, t)

@@ -372,3 +372,76 @@ def test_publish_rejection_is_isolated_and_dead_lettered(arun):
     assert sorted(parsed) == ["ok1", "ok2", "ok3"]  # the good messages went through
     assert info.num_pending == 0 and info.num_ack_pending == 0
     assert issubclass(BusUnavailable, ConnectionError) and not issubclass(BusError, ConnectionError)
+
+
+def test_broker_wide_refusal_naks_the_batch(arun):
+    """a refusal that hits every message alike (a full DiscardNew stream,
+    resource limits, a leader election, no stream for the subject) is BusUnavailable
+    (bus.base.bus_error): the batch is nak'ed whole and retried, nothing is
+    dead-lettered -- during a stream-full episode no message lands in the DLQ."""
+    from smsgate_amd.bus import BusError, BusUnavailable
+    from smsgate_amd.bus.base import bus_error
+
+    for desc in ("maximum messages exceeded", "insufficient resources", "JetStream system temporarily unavailable",
+                 "no stream matches subject 'sms.parsed'", "stream leader not found"):
+        assert isinstance(bus_error(desc), BusUnavailable), desc
+    for desc in ("maximum payload exceeded", "bad request: invalid json"):
+        e = bus_error(desc)
+        assert isinstance(e, BusError) and not isinstance(e, BusUnavailable), desc
+    state = {"full": 3}
+
+    class Full(MemoryBus):
+        async def publish(self, subject, data, headers=None):
+            if subject == SUBJECT_PARSED and state["full"]:
+                state["full"] -= 1
+                raise bus_error("maximum messages exceeded")
+            return await super().publish(subject, data, headers)
+
+    bus = Full()
+
+    async def handler(msgs):
+        for m in msgs:
+            await bus.publish(SUBJECT_PARSED, m.data)
+        for m in msgs:
+            await m.ack()
+
+    async def go():
+        await MemoryBus.publish_many(bus, [(SUBJECT_RAW, b'"a"'), (SUBJECT_RAW, b'"b"'), (SUBJECT_RAW, b'"c"')])
+        st = Stage(bus, SUBJECT_RAW, "g", handler, batch=16, nak_delay=0.0, poison_after=1,
+                   dead_letter=dlq_publisher(bus, SUBJECT_FAILED), stats_interval=0)
+        await _pump(st)
+        info = await bus.consumer_info("SMS", "g")
+        return st, info, await drain(bus, SUBJECT_FAILED)
+
+    st, info, dlq = arun(go())
+    assert st.transient_errors == 3 and st.dead_lettered == 0 and dlq == []
+    assert info.num_pending == 0 and info.num_ack_pending == 0
+
+
+def test_handler_timeout_is_isolated_not_retried_forever(arun):
+    """a TimeoutError raised by a handler on one message (a backend's
+    own wait_for) is not a dependency outage: it takes the isolate / dead-letter path
+    (poison_after), so the consumer is never stuck behind it."""
+    import asyncio
+
+    bus = MemoryBus()
+
+    async def handler(msgs):
+        for m in msgs:
+            if m.data == b"slow":
+                raise asyncio.TimeoutError()
+        for m in msgs:
+            await m.ack()
+
+    async def go():
+        for d in (b"a", b"slow", b"b"):
+            await bus.publish(SUBJECT_RAW, d)
+        st = Stage(bus, SUBJECT_RAW, "g", handler, batch=16, nak_delay=0.0, poison_after=2,
+                   dead_letter=dlq_publisher(bus, SUBJECT_FAILED), stats_interval=0)
+        await _pump(st)
+        info = await bus.consumer_info("SMS", "g")
+        return st, info, await drain(bus, SUBJECT_FAILED)
+
+    st, info, dlq = arun(go())
+    assert st.dead_lettered == 1 and st.transient_errors == 0 and len(dlq) == 1
+    assert info.num_pending == 0 and info.num_ack_pending == 0

@@ -81,6 +81,9 @@ def _args(argv=None):
                         "field written with the body's tokens (speculative prompt-lookup decoding)")
     p.add_argument("--train-negatives", type=float, default=0.12,
                    help="share of non-transaction training examples (utils/synth.py NEG_TRAIN_FAMILIES)")
+    p.add_argument("--train-ddp", type=int, default=1, choices=[0, 1],
+                   help="1: with several ranks, train on all of them (RCCL data parallel over the global batch); "
+                        "0: local rank 0 trains alone and the other ranks load its file")
     p.add_argument("--data-workers", type=int, default=12,
                    help="CPU processes building the training examples (started before the GPU is touched)")
     p.add_argument("--weights-cache", default="/tmp/smsgate_bench_weights",
@@ -717,17 +720,33 @@ def _train_plan(args):
     return tc, os.path.join(cache, f"{args.model}-{h}.safetensors")
 
 
+def _ddp_train(args, world: int) -> bool:
+    """Train with every rank (RCCL data parallel over the global batch) instead of local
+    rank 0 alone while the other ranks wait: whenever the job has
+    several ranks and the global batch splits evenly."""
+    return args.train_ddp and world > 1 and args.train_batch % world == 0
+
+
 def start_training_data(args, local: int):
-    """Local rank 0 of a ``--weights train`` run whose weights are not cached starts
-    building the training examples on CPU worker processes NOW -- before the GPU is
-    touched (spawned, not forked) -- so the work overlaps broker / engine start-up."""
-    if args.weights != "train" or local != 0 or args.cpu_echo_engine or args.backend != "local_llm":
+    """Build the training examples on CPU worker processes NOW -- before the GPU is
+    touched (spawned, not forked) -- so the work overlaps broker / engine start-up.
+    Data-parallel training: every rank builds its own disjoint share (seeded by rank),
+    with the node's data workers split over its ranks; else local rank 0 builds all."""
+    if args.weights != "train" or args.cpu_echo_engine or args.backend != "local_llm":
         return None
     tc, path = _train_plan(args)
     if os.path.exists(path):
         return None
     from smsgate_amd.models.train import ExamplePool
 
+    rank, world, _ = _rank_env()
+    if _ddp_train(args, world):
+        node = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        return ExamplePool(tc.n_examples // world, seed=tc.seed * 1000 + rank, families=tc.families,
+                           workers=max(2, args.data_workers // node), answer_format=tc.answer_format,
+                           negatives=tc.negatives)
+    if local != 0:
+        return None
     return ExamplePool(tc.n_examples, seed=tc.seed, families=tc.families, workers=args.data_workers,
                        answer_format=tc.answer_format, negatives=tc.negatives)
 
@@ -756,6 +775,25 @@ def acquire_weights(args, device: str, rank: int, world: int, pool=None):
     if os.path.exists(path):
         w = ExtractorWeights.load(path, CONFIGS[args.model], device=torch.device(device))
         prov["weights"] += " (reused from an earlier identical run's cache)"
+        return w, prov
+    if _ddp_train(args, world):
+        # every rank trains: the same steps x global batch, split over the ranks, gradients
+        # averaged by bucketed all-reduces overlapped with backward (parallel/ddp.py); the
+        # replicas stay identical, rank 0 publishes the file for later runs
+        import dataclasses
+
+        t0 = time.perf_counter()
+        tcr = dataclasses.replace(tc, batch=tc.batch // world, data_parallel=True, seed=tc.seed)
+        w = train_extractor(tcr, device=device, data=pool.get() if pool is not None else None,
+                            log=(lambda s: print(f"[bench] train {s}", file=sys.stderr, flush=True)) if rank == 0
+                            else (lambda s: None))
+        prov["weights"] = prov["weights"].replace("on local rank 0", f"data parallel over {world} ranks (RCCL)")
+        prov["train_s"] = round(time.perf_counter() - t0, 1)
+        if rank == 0:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            tmp = path + f".{os.getpid()}.tmp"
+            w.save(tmp)
+            os.replace(tmp, path)
         return w, prov
     if local != 0:
         t_end = time.time() + 1800

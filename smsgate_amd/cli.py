@@ -252,7 +252,8 @@ def _train(a, settings) -> None:
             dist.init_process_group("gloo")
     cfg = TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr, n_examples=a.examples,
                       ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, bucket_mb=a.bucket_mb,
-                      answer_format=a.answer_format, families=None if a.families == "legacy" else a.families)
+                      answer_format=a.answer_format, families=None if a.families == "legacy" else a.families,
+                      negatives=a.negatives)
     w = train_extractor(cfg, device=device)
     if not dist.is_initialized() or dist.get_rank() == 0:
         w.save(a.out)
@@ -367,8 +368,11 @@ def build_parser() -> argparse.ArgumentParser:
     tr.add_argument("--ckpt-every", type=int, default=0)
     tr.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --ckpt-dir")
     tr.add_argument("--bucket-mb", type=float, default=64.0, help="DP gradient all-reduce bucket size")
-    tr.add_argument("--answer-format", default="copy", choices=["copy", "span"],
-                    help="span: two pointers per copied field (the checkpoint records it; the engine follows)")
+    tr.add_argument("--answer-format", default="qa", choices=["copy", "span", "qa", "qa17"],
+                    help="qa: the whole answer from one forward (serving/qa.py); span: two pointer decode steps "
+                         "per copied field; copy: the body's tokens (the checkpoint records it; the engine follows)")
+    tr.add_argument("--negatives", type=float, default=0.12,
+                    help="share of non-transaction examples (txn_type unknown / otp, null fields)")
     tr.add_argument("--families", default="train", help="train (every training SMS layout) | legacy (the two "
                     "reference formats only)")
     sp.add_parser("config")

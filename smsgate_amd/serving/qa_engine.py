@@ -140,11 +140,14 @@ class QAEngine(ExtractionEngine):
         T = int(tl.sum())
         cu = np.zeros(n + 1, dtype=np.int32)
         np.cumsum(tl, out=cu[1:])
-        qid = self.qids
-        flat = np.concatenate([np.concatenate([np.asarray(it.ids, dtype=np.int32), qid]) for it in items])
         starts = np.repeat(cu[:-1], tl)
         pos = np.arange(T, dtype=np.int32) - starts
-        add = np.where(pos < np.repeat(lens, tl), lay.ptr0 + pos, -1).astype(np.int32)
+        in_msg = pos < np.repeat(lens, tl)
+        # one concatenation of the messages, the query ids written around them
+        flat = np.empty(T, dtype=np.int32)
+        flat[in_msg] = np.concatenate([np.asarray(it.ids, dtype=np.int32) for it in items])
+        flat[~in_msg] = np.tile(self.qids, n)
+        add = np.where(in_msg, lay.ptr0 + pos, -1).astype(np.int32)
         seq_slot = np.arange(r0, r0 + n, dtype=np.int32)
         slot = np.repeat(seq_slot, tl)
         qstart = np.zeros(n, dtype=np.int32)

@@ -75,10 +75,13 @@ def test_stale_broker_socket_is_not_listening(tmp_path):
 @pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "smsgate_amd/native/_bin/smsgate-busd")),
                     reason="native broker not built")
 def test_eight_ranks_full_node_layout():
-    """VERDICT r03 next #4b: 8 ranks (gloo, CPU echo engines) through the production
-    node layout -- sms.raw over 6 brokers, sms.parsed over 2, one for the rest -- with
-    one parser process each: exact routing totals, traffic on every raw and parsed
-    partition, and a drain that accounts for every message across the 6 partitions."""
+    """VERDICT r03 next #4b / r04 next #3: 8 ranks (gloo, CPU echo engines) through the
+    production node layout (bus/sharded.py NODE_PARTITIONS: sms.raw, sms.parsed and
+    sms.processing partitioned, one broker for the rest) with one parser process each:
+    exact routing totals, traffic on every partition of every partitioned subject, and a
+    drain that accounts for every message across the raw partitions."""
+    from smsgate_amd.bus.sharded import NODE_PARTITIONS
+
     ranks, steps, warm, per = 8, 2, 1, 512
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(ranks),
            "--master-addr", "127.0.0.1", "--master-port", "29683", "bench.py", "--gpus", str(ranks),
@@ -93,17 +96,22 @@ def test_eight_ranks_full_node_layout():
     total = ranks * steps * per
     assert out["n_gpus"] == ranks and rt["parsed"] + rt["keyword_skipped"] + rt["broken"] + rt["dlq"] == total
     assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"]
-    assert "sms.raw over 6" in out["config"]["bus"] and "sms.parsed over 2" in out["config"]["bus"]
+    for subj, n in NODE_PARTITIONS.items():
+        assert f"{subj} over {n}" in out["config"]["bus"], out["config"]["bus"]
     members = out["bus_members"]
-    assert len(members) == 9
-    raw = [m for m in members if m["subjects"] == ["sms.raw"]]
-    parsed = [m for m in members if m["subjects"] == ["sms.parsed"]]
-    assert len(raw) == 6 and len(parsed) == 2
+    assert len(members) == sum(NODE_PARTITIONS.values()) + 1
+    by = {subj: [m for m in members if m["subjects"] == [subj]] for subj in NODE_PARTITIONS}
+    assert {s: len(v) for s, v in by.items()} == NODE_PARTITIONS
+    raw = by["sms.raw"]
     # every raw message of the run stored on exactly one raw partition: the bus-ingest
     # phase (warmup + steps) and the HTTP-ingest phase (1 warmup step + steps) through
-    # the six partitions' native /sms/raw doors
+    # the raw partitions' native /sms/raw doors
     assert sum(m["messages"] for m in raw) == ranks * (steps + warm) * per + ranks * (steps + 1) * per
-    assert all(m["messages"] > 0 for m in raw + parsed)
+    assert all(m["messages"] > 0 for v in by.values() for m in v), members
+    # the parser's two outputs per parsed SMS land on their own partitions, evenly
+    for subj in ("sms.parsed", "sms.processing"):
+        counts = [m["messages"] for m in by[subj]]
+        assert max(counts) <= 1.5 * min(counts) + 64, (subj, counts)
     h = out["http_ingest"]
     assert h["requests"] == total and h["routing"]["parsed"] + h["routing"]["keyword_skipped"] + \
         h["routing"]["broken"] + h["routing"]["dlq"] == total

@@ -108,3 +108,37 @@ def test_torchrun_two_rank_training_cli(tmp_path):
     r = subprocess.run(base + ["--steps", "3", "--resume"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "resumed from" in r.stdout + r.stderr and (ck / "step-0000003.pt").exists()
+
+
+def _bench_worker(rank, world, port, cache, out):
+    import sys
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = bench._args(["--model", "tiny", "--train-steps", "6", "--train-batch", "8", "--weights-cache", cache,
+                        "--data-workers", "2"])
+    pool = bench.start_training_data(args, rank)
+    w, prov = bench.acquire_weights(args, "cpu", rank, world, pool)
+    flat = torch.cat([p.detach().float().reshape(-1) for p in w.parameters()])
+    lst = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(lst, flat)
+    out[rank] = (all(torch.equal(lst[0], x) for x in lst[1:]), prov["weights"], w.cfg.qa_queries)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_trains_data_parallel_on_every_rank(tmp_path):
+    """with several ranks the bench's in-run training runs on ALL of
+    them (the global batch split, gradients all-reduced) instead of local rank 0 while
+    the others wait; the replicas end identical and rank 0 publishes the cache file."""
+    world = 2
+    out = mp.Manager().dict()
+    mp.spawn(_bench_worker, args=(world, _free_port(), str(tmp_path), out), nprocs=world, join=True)
+    assert all(out[r][0] for r in range(world)), dict(out)
+    assert all("data parallel over 2 ranks" in out[r][1] for r in range(world)), dict(out)
+    assert out[0][2] == 9  # the default answer format (qa)
+    assert len(list(tmp_path.glob("tiny-*.safetensors"))) == 1

@@ -130,7 +130,10 @@ class Router:
         self.n = n
         self.pins = dict(pins or {})
         self.default = list(default or range(n))
-        self._rr = itertools.count()
+        # one dealing counter PER subject: a shared one would put every sms.parsed publish
+        # on the even turns and every sms.processing one on the odd turns of a parser
+        # batch that publishes them in pairs -- one partition of each would get nothing
+        self._rr: Dict[str, "itertools.count[int]"] = {}
 
     def members(self, subject: str) -> List[int]:
         if not self.pins:
@@ -141,7 +144,12 @@ class Router:
 
     def publish_target(self, subject: str) -> int:
         ms = self.members(subject)
-        return ms[0] if len(ms) == 1 else ms[next(self._rr) % len(ms)]
+        if len(ms) == 1:
+            return ms[0]
+        rr = self._rr.get(subject)
+        if rr is None:
+            rr = self._rr[subject] = itertools.count()
+        return ms[next(rr) % len(ms)]
 
 
 class _PartitionedSub(Subscription):

@@ -107,7 +107,7 @@ def test_eight_ranks_full_node_layout():
     # phase (warmup + steps) and the HTTP-ingest phase (1 warmup step + steps) through
     # the raw partitions' native /sms/raw doors
     assert sum(m["messages"] for m in raw) == ranks * (steps + warm) * per + ranks * (steps + 1) * per
-    assert all(m["messages"] > 0 for v in by.values() for m in v), members
+    assert all(m["messages"] > 0 for v in by.values() for m in v), str([(m["subjects"][0][4:], m["messages"]) for m in members])
     # the parser's two outputs per parsed SMS land on their own partitions, evenly
     for subj in ("sms.parsed", "sms.processing"):
         counts = [m["messages"] for m in by[subj]]

@@ -148,3 +148,14 @@ def test_partitioned_fetch_low_load_latency(arun):
 
     lat = arun(go())
     assert max(lat) < 0.03, lat
+
+
+def test_publishes_are_dealt_per_subject():
+    """Interleaved publishes of two partitioned subjects (the parser's sms.parsed /
+    sms.processing pairs) reach every partition of each: the dealing turn is per subject."""
+    from smsgate_amd.bus.sharded import Router
+
+    rt = Router(5, {"a": [0, 1], "b": [2, 3]}, [4])
+    got = [rt.publish_target(s) for _ in range(8) for s in ("a", "b")]
+    assert sorted(set(got[0::2])) == [0, 1] and sorted(set(got[1::2])) == [2, 3]
+    assert got[0::2].count(0) == 4 and got[1::2].count(2) == 4

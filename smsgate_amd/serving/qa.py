@@ -291,7 +291,7 @@ def qa_logits(h, embed, qpos, lay: QALayout):
 
 def qa_loss(scores, targets, lay: QALayout):
     """Mean cross-entropy over the answer's decisions: the class, every copied field's
-    start (null included) and every non-null field's end (positions >= its start).
+    start (null included) and every non-null field's end (over all message positions).
     ``targets``: (cls [B], starts [B, n_copy] (-1 = null), ends [B, n_copy], npos [B]
     pointable positions per message)."""
     import torch
@@ -308,7 +308,10 @@ def qa_loss(scores, targets, lay: QALayout):
     l_cls = F.cross_entropy(cls, t_cls, reduction="sum")
     l_st = F.cross_entropy(st.reshape(-1, NP + 1), st_t.reshape(-1), reduction="sum")
     has = t_s >= 0
-    en = end.masked_fill(out_of_msg | (j[None, None, :] < t_s[..., None]), neg)
+    # the end distribution is trained over EVERY position of the message, not only those
+    # at / after the gold start: the decoder scores (start, end) pairs jointly, and end
+    # scores left untrained before the start would let a wrong pair win
+    en = end.masked_fill(out_of_msg, neg)
     l_en = F.cross_entropy(en[has], t_e[has], reduction="sum") if bool(has.any()) else en.sum() * 0
     return (l_cls + l_st + l_en) / (B + B * NF + int(has.sum()))
 

@@ -903,6 +903,87 @@ NEG_FAMILIES: Tuple[Family, ...] = (
         f"Karta {c.CARD()} zablokirovana. Dlya razblokirovki pozvonite {_phone(c)}.",
         f"Karta {c.CARD()} razblokirovana {c.D()}."), heldout=True, split="negative"),
 )
+# Procedural non-transactions (training only): a concept phrase from the language's pool --
+# the same words the held-out negative families use, as the format families share their
+# label words -- with a random subset of transaction-looking values (card, amount, date,
+# merchant, phone, digits) in a random order and separators.  A held-out negative family
+# is a NEW PHRASING of a concept whose words were trained on, never unseen vocabulary.
+_NEG_CONCEPTS = {
+    "en": {
+        "blocked": ("card blocked", "card has been blocked", "card temporarily blocked", "card unblocked",
+                    "card is locked", "BLOCKED", "account blocked"),
+        "login": ("new sign-in", "login to online banking", "password changed", "security alert",
+                  "new device login", "sign-in attempt"),
+        "promo": ("cashback {pct}%", "{pct}% off", "special offer", "double points", "bonus offer", "win a trip"),
+        "limit": ("limit changed", "new daily limit", "spending limit updated", "withdrawal limit"),
+        "balance": ("balance as of", "statement", "balance info", "available balance notice"),
+        "declined": ("declined", "transaction declined", "payment rejected", "not completed", "operation failed"),
+        "p2p": ("money request", "requests money", "transfer request", "awaiting your confirmation"),
+        "tariff": ("service fee", "tariff change", "monthly fee will be charged", "fees change"),
+        "otp": ("verification number", "confirmation number", "one-time number", "security number"),
+    },
+    "ru": {
+        "blocked": ("карта заблокирована", "карта разблокирована", "временно заблокирована", "блокировка карты"),
+        "login": ("вход в мобильный банк", "вход в интернет-банк", "пароль изменен", "новое устройство"),
+        "promo": ("кэшбэк {pct}%", "скидка {pct}%", "акция", "бонусы x2", "специальное предложение"),
+        "limit": ("лимит изменен", "новый лимит", "лимит по карте"),
+        "balance": ("баланс на", "остаток на", "выписка"),
+        "declined": ("отказ", "операция отклонена", "не выполнена", "операция не прошла"),
+        "p2p": ("запрос на перевод", "просит перевести", "ожидает подтверждения"),
+        "tariff": ("плата за обслуживание", "тарифы меняются", "комиссия составит"),
+        "otp": ("пароль для входа", "код подтверждения", "одноразовый пароль"),
+    },
+    "tr": {
+        "blocked": ("karta zablokirovana", "karta razblokirovana", "vremenno zablokirovana", "blokirovka karty"),
+        "login": ("vhod v mobilnyy bank", "parol izmenen", "novoe ustroystvo"),
+        "promo": ("keshbek {pct}%", "skidka {pct}%", "aktsiya", "bonusy x2"),
+        "limit": ("limit izmenen", "novyy limit", "limit po karte"),
+        "balance": ("balans na", "ostatok na", "vypiska"),
+        "declined": ("otkaz", "operatsiya otklonena", "ne vypolnena"),
+        "p2p": ("zapros na perevod", "prosit perevesti"),
+        "tariff": ("plata za obsluzhivanie", "tarify menyayutsya"),
+        "otp": ("parol dlya vhoda", "kod podtverzhdeniya"),
+    },
+}
+_NEG_LABELS = {"en": dict(card=("card", "Card"), amt=("Amount", "Sum"), date=("Date", "on"), phone=("Call", "Tel")),
+               "ru": dict(card=("Карта", "карта"), amt=("Сумма",), date=("Дата",), phone=("Тел", "звоните")),
+               "tr": dict(card=("Karta", "karta"), amt=("Summa",), date=("Data",), phone=("Tel", "zvonite"))}
+
+
+def _neg_proc_render(c: _Ctx) -> str:
+    r, lang = c.r, c.fam.lang
+    concept = r.choice(tuple(_NEG_CONCEPTS[lang]))
+    c.neg_txn = "otp" if concept == "otp" else "unknown"
+    phrase = r.choice(_NEG_CONCEPTS[lang][concept]).format(pct=_pct(c))
+    if r.random() < 0.5:
+        phrase = phrase[0].upper() + phrase[1:]
+    L = _NEG_LABELS[lang]
+    vals = []
+    if r.random() < 0.6:
+        vals.append((r.choice(L["card"]) + " " if r.random() < 0.7 else "") + c.CARD())
+    if r.random() < 0.55 or concept in ("promo", "limit", "balance", "declined", "p2p", "tariff"):
+        v = c.BAL() if concept == "balance" else c.AMT()
+        vals.append((r.choice(L["amt"]) + ": " if r.random() < 0.4 else "") + v)
+    if r.random() < 0.55:
+        vals.append((r.choice(L["date"]) + " " if r.random() < 0.4 else "") + c.D())
+    if r.random() < 0.5 or concept in ("promo", "declined", "p2p"):
+        vals.append(c.M() + (", " + c.C() if r.random() < 0.4 else ""))
+    if concept == "otp" or r.random() < 0.15:
+        vals.append(_digits(c))
+    if concept in ("blocked", "login") and r.random() < 0.5:
+        vals.append(r.choice(L["phone"]) + " " + _phone(c))
+    r.shuffle(vals)
+    k = r.randint(0, len(vals))
+    segs = vals[:k] + [phrase] + vals[k:]
+    sep = r.choice((", ", "; ", ". ", " ", " | ", "\n"))
+    return sep.join(segs) + (c.noise() if sep != "\n" else "")
+
+
+NEG_FAMILIES = NEG_FAMILIES + (
+    Family("neg_proc_en", "en", "unknown", _neg_proc_render, split="negative", cases=("upper", "upper", "title")),
+    Family("neg_proc_ru", "ru", "unknown", _neg_proc_render, split="negative"),
+    Family("neg_proc_tr", "tr", "unknown", _neg_proc_render, split="negative"),
+)
 NEG_TRAIN_FAMILIES: Tuple[str, ...] = tuple(f.name for f in NEG_FAMILIES if not f.heldout)
 NEG_HELDOUT_FAMILIES: Tuple[str, ...] = tuple(f.name for f in NEG_FAMILIES if f.heldout)
 VALUE_HELDOUT_FAMILIES: Tuple[str, ...] = tuple(f.name for f in VALUE_FAMILIES)
@@ -961,7 +1042,7 @@ def _family_one(r: random.Random, v: Vocab, name: str, all_credit_kinds: bool = 
     c = _Ctx(r, v, fam, ts)
     body = fam.render(c)
     if fam.split == "negative":
-        return SynthSMS(body, "negative", rejection_answer(fam.txn), ts, name, None)
+        return SynthSMS(body, "negative", rejection_answer(getattr(c, "neg_txn", fam.txn)), ts, name, None)
     exp = dict(c.exp)
     return SynthSMS(body, "purchase" if fam.txn == "debit" else "credit", dict(c.ans), ts, name, exp)
 
@@ -1010,13 +1091,14 @@ def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "trai
             if not isinstance(families, str) or families not in _NEG_OF:
                 raise ValueError(f"negatives need a split selector ({sorted(_NEG_OF)}), not {families!r}")
             neg_names = family_names(_NEG_OF[families])
+            neg_weights = [_PROC_WEIGHT if f.startswith("neg_proc_") else 1 for f in neg_names]
     out: List[SynthSMS] = []
     seen = set()
     while len(out) < n:
         if not names:
             s = _one(r, v)
         elif neg_names and r.random() < negatives:
-            s = _family_one(r, v, r.choice(neg_names), training)
+            s = _family_one(r, v, r.choices(neg_names, neg_weights)[0], training)
         else:
             s = _family_one(r, v, r.choices(names, weights)[0], training)
         if kinds is not None and s.kind not in kinds:

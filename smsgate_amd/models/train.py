@@ -285,30 +285,29 @@ def _batch(prefix: List[int], exs: Sequence[Tuple[List[int], List[int]]], pad: i
 def qa_batch(prefix: List[int], exs, pad: int, device, lay):
     """qa-format batch: ids ``prefix + message + queries``, the pointer row added to each
     message position (-1 elsewhere), the query rows' positions and the targets
-    (class, starts, ends, pointable positions) of serving/qa.py qa_loss."""
-    q = lay.query_ids()
+    (class, starts, ends, pointable positions) of serving/qa.py qa_loss.  Built with
+    numpy (one pass, no per-element tensor writes: the training step's host time)."""
+    import numpy as np
+
+    q = np.asarray(lay.query_ids(), dtype=np.int64)
     NQ, NF = len(q), lay.n_copy
-    seqs = [prefix + m + q for m, _ in exs]
-    T = max(len(s) for s in seqs)
-    B = len(exs)
-    ids = torch.full((B, T), pad, dtype=torch.long)
-    add = torch.full((B, T), -1, dtype=torch.long)
-    qpos = torch.zeros((B, NQ), dtype=torch.long)
-    t_cls = torch.zeros(B, dtype=torch.long)
-    t_s = torch.full((B, NF), -1, dtype=torch.long)
-    t_e = torch.full((B, NF), -1, dtype=torch.long)
-    npos = torch.zeros(B, dtype=torch.long)
     P = len(prefix)
-    for i, ((m, (c, spans)), s) in enumerate(zip(exs, seqs)):
-        ids[i, : len(s)] = torch.tensor(s)
-        add[i, P:P + len(m)] = torch.arange(lay.ptr0, lay.ptr0 + len(m))
-        qpos[i] = torch.arange(P + len(m), P + len(m) + NQ)
-        t_cls[i] = c
-        npos[i] = len(m) - 1
-        for f, (a, z) in enumerate(spans):
-            t_s[i, f], t_e[i, f] = a, z
-    dv = lambda t: t.to(device)  # noqa: E731
-    return dv(ids), dv(add), dv(qpos), (dv(t_cls), dv(t_s), dv(t_e), dv(npos))
+    B = len(exs)
+    lens = np.fromiter((len(m) for m, _ in exs), dtype=np.int64, count=B)
+    T = P + int(lens.max()) + NQ
+    ids = np.full((B, T), pad, dtype=np.int64)
+    add = np.full((B, T), -1, dtype=np.int64)
+    ids[:, :P] = prefix
+    col = np.arange(T)[None, :]
+    in_msg = (col >= P) & (col < P + lens[:, None])
+    ids[in_msg] = np.concatenate([np.asarray(m, dtype=np.int64) for m, _ in exs])
+    add[in_msg] = np.broadcast_to(lay.ptr0 + col - P, (B, T))[in_msg]
+    qpos = P + lens[:, None] + np.arange(NQ)[None, :]
+    ids[np.arange(B)[:, None], qpos] = q[None, :]
+    t_cls = np.fromiter((c for _, (c, _) in exs), dtype=np.int64, count=B)
+    sp = np.asarray([spans for _, (_, spans) in exs], dtype=np.int64).reshape(B, NF, 2)
+    dv = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    return dv(ids), dv(add), dv(qpos), (dv(t_cls), dv(sp[..., 0]), dv(sp[..., 1]), dv(lens - 1))
 
 
 def latest_checkpoint(ckpt_dir: Optional[str]) -> Optional[Path]:

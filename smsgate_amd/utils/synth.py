@@ -975,6 +975,11 @@ def _neg_proc_render(c: _Ctx) -> str:
     r.shuffle(vals)
     k = r.randint(0, len(vals))
     segs = vals[:k] + [phrase] + vals[k:]
+    # hard negatives: a transaction header word ("Purchase", "Покупка", "Oplata") in front
+    # of a message the concept phrase makes a non-transaction (a declined purchase, a
+    # payment request, a promo) -- the header alone never decides
+    if concept in ("declined", "p2p", "promo", "tariff", "otp", "limit") and r.random() < 0.35:
+        segs.insert(0, r.choice(_PROC_POOLS[lang]["head_debit"] + _PROC_POOLS[lang]["head_credit"]))
     sep = r.choice((", ", "; ", ". ", " ", " | ", "\n"))
     return sep.join(segs) + (c.noise() if sep != "\n" else "")
 

@@ -204,8 +204,11 @@ def _args(argv=None):
                    help="NUMA placement of the rank / parser / broker processes (parallel/placement.py); auto = "
                         "only when this job holds every GPU of the node")
     p.add_argument("--profile-cpu", default=None, metavar="DIR",
-                   help="cProfile the timed region of every parser process and of the rank process into DIR "
-                        "(parser-r<rank>-w<k>.pstats, rank<rank>.pstats)")
+                   help="profile the timed bus phase of every parser process and of the rank process into DIR "
+                        "(parser-r<rank>-w<k>.samples.json / .pstats, rank<rank>.samples.json / .pstats)")
+    p.add_argument("--profile-mode", default="sample", choices=["sample", "cprofile"],
+                   help="sample: CPU-time stack sampling (utils/sampler.py: waits take no samples); "
+                        "cprofile: every call instrumented")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--no-graphs", action="store_true", help="decode steps launched eagerly (no hipGraphs)")
     p.add_argument("--no-measure-idle", action="store_true",
@@ -237,7 +240,7 @@ def run_replica(args, rank: int, world: int, local: int):
 
         sink_dir = tempfile.mkdtemp(prefix=f"smsgate-bench-sink-r{rank}-")
     cfg = {"batch": args.batch, "concurrency": args.concurrency, "max_body_tokens": 128,
-           "profile_dir": args.profile_cpu,
+           "profile_dir": args.profile_cpu, "profile_mode": args.profile_mode,
            "worker_threads": args.worker_threads, "nice": args.worker_nice, "vocab": args.traffic_vocab, "bus": bus_dsn,
            "traffic": args.traffic, "sink": args.sink, "sink_dir": sink_dir}
     # 1) CPU parser processes first: nothing may exec after this process initialises the GPU
@@ -342,17 +345,27 @@ def run_replica(args, rank: int, world: int, local: int):
         thr0 = _rank_threads()
         rprof = None
         if args.profile_cpu and not http:
-            import cProfile
+            if args.profile_mode == "sample":
+                from smsgate_amd.utils.sampler import CpuSampler
 
-            rprof = cProfile.Profile()
-            rprof.enable()
+                rprof = CpuSampler()
+                rprof.start()
+            else:
+                import cProfile
+
+                rprof = cProfile.Profile()
+                rprof.enable()
         first = args.warmup if not http else 10_001
         dt_p, counts_p = coord.run_phase(seeds(first, args.steps, http), per[http], sync=sync,
                                          profile=bool(args.profile_cpu) and not http)
         if rprof is not None:
-            rprof.disable()
             os.makedirs(args.profile_cpu, exist_ok=True)
-            rprof.dump_stats(os.path.join(args.profile_cpu, f"rank{rank}.pstats"))
+            if hasattr(rprof, "dump"):  # CpuSampler (the summary divides by the bench's message count)
+                rprof.stop()
+                rprof.dump(os.path.join(args.profile_cpu, f"rank{rank}.samples.json"))
+            else:
+                rprof.disable()
+                rprof.dump_stats(os.path.join(args.profile_cpu, f"rank{rank}.pstats"))
         cpu_p = {k: v1 - cpu0[k] for k, v1 in _cpu_snapshot(procs, broker, lprocs).items()}
         cpu_p["rank_threads"] = _thread_cores(thr0, _rank_threads(), dt_p)
         estats_p = engine.stats.as_dict()

@@ -37,6 +37,8 @@ def main() -> int:
     p.add_argument("--prefill-m", type=int, default=15104)
     p.add_argument("--prefill-len", type=int, default=37, help="computed prompt tokens per message")
     p.add_argument("--own", type=int, default=60, help="mean own keys per decode row")
+    p.add_argument("--no-spec", action="store_true",
+                   help="skip the speculative verify attention (qa-format shapes: no decode phase)")
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--iters", type=int, default=9)
     p.add_argument("--inner", type=int, default=20)
@@ -118,10 +120,11 @@ def main() -> int:
         turn[0] = (turn[0] + 1) % ROT
         ops.attn_spec(qs, *common, slots[turn[0]], done0, kca, vta, pk, pvt, P0, outs, scale, max_q)
 
-    cases[f"attn_spec_B{B}_T{T}_own{a.own}"] = (
-        spec_fn,
-        2.0 * 2 * D * nh * float((x_pos.float() + 1 + P0).sum()),
-        keys * nkv * D * 2 * 2 + 2 * T * nh * D * 2)
+    if not a.no_spec:
+      cases[f"attn_spec_B{B}_T{T}_own{a.own}"] = (
+          spec_fn,
+          2.0 * 2 * D * nh * float((x_pos.float() + 1 + P0).sum()),
+          keys * nkv * D * 2 * 2 + 2 * T * nh * D * 2)
 
     # prefill attention: the prefill half's sequences, prefill_len tokens each
     L = a.prefill_len

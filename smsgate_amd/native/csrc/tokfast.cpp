@@ -15,7 +15,10 @@
 //     (tables probed against the library itself, models/fasttok.py);
 //   * the added special tokens matched as literals first (AddedVocabulary);
 //   * byte-level BPE with the merge ranks, and a per-pre-token cache (labels,
-//     currency codes and common words repeat across messages);
+//     currency codes and common words repeat across messages): an open-addressing
+//     table over one key arena and one id arena (a lookup hashes the bytes in place:
+//     no std::string per pre-token), emptied whole when it fills, so held-out
+//     traffic's one-off names and amounts cannot freeze it with stale entries;
 //   * truncation to max_body tokens + the <ans> marker, packed as uint16 lengths
 //     and int32 ids;
 //   * answer decoding: <sep>-split fields, byte-table join, UTF-8 "replace"
@@ -29,7 +32,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
-#include <unordered_map>
+#include <algorithm>
 #include <utility>
 #include <vector>
 
@@ -37,14 +40,61 @@ namespace {
 
 enum : uint8_t { C_L = 1, C_N = 2, C_D = 4, C_S = 8 };
 
+// pre-token bytes -> ids.  Slots hold (hash | 1, key offset / length, ids offset /
+// count); keys and ids live in two arenas.  Linear probing at <= 50 % load.
+struct BpeCache {
+    static constexpr size_t SLOTS = 1 << 19, MAX_ENTRIES = SLOTS / 2;
+    std::vector<uint64_t> hk;
+    std::vector<uint32_t> koff, voff;
+    std::vector<uint16_t> klen, vlen;
+    std::string keys;
+    std::vector<int> vals;
+    size_t entries = 0;
+    BpeCache() : hk(SLOTS, 0), koff(SLOTS), voff(SLOTS), klen(SLOTS), vlen(SLOTS) {}
+    static uint64_t hash(const char* s, size_t n) {  // FNV-1a, 64-bit
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)s[i]) * 1099511628211ull;
+        return h | 1;
+    }
+    // ids of the pre-token or nullptr; *slot = where it would go
+    const int* find(const char* s, size_t n, uint64_t h, size_t* cnt, size_t* slot) const {
+        for (size_t i = (h >> 7) & (SLOTS - 1);; i = (i + 1) & (SLOTS - 1)) {
+            if (!hk[i]) { *slot = i; return nullptr; }
+            if (hk[i] == h && klen[i] == n && memcmp(keys.data() + koff[i], s, n) == 0) {
+                *cnt = vlen[i];
+                return vals.data() + voff[i];
+            }
+        }
+    }
+    void put(size_t slot, const char* s, size_t n, uint64_t h, const int* ids, size_t cnt) {
+        if (n > 0xFFFF || cnt > 0xFFFF || keys.size() + n > 0xFFFFFFFFull) return;
+        hk[slot] = h;
+        koff[slot] = (uint32_t)keys.size();
+        klen[slot] = (uint16_t)n;
+        voff[slot] = (uint32_t)vals.size();
+        vlen[slot] = (uint16_t)cnt;
+        keys.append(s, n);
+        vals.insert(vals.end(), ids, ids + cnt);
+        ++entries;
+    }
+    void clear() {
+        std::fill(hk.begin(), hk.end(), 0);
+        keys.clear();
+        vals.clear();
+        entries = 0;
+    }
+};
+
 struct Tok {
     std::vector<std::string> tok_bytes;                       // id -> raw bytes
     void* merge_tab = nullptr;                                 // MergeTable* (defined below)
     int byte_id[256];
     std::vector<uint8_t> cls;                                  // code point -> C_* bits
     std::vector<std::pair<std::string, int>> specials;         // literal -> id
-    std::unordered_map<std::string, std::vector<int>> cache;   // pre-token bytes -> ids
-    size_t cache_max = 1 << 18;
+    BpeCache cache;
+    std::vector<uint32_t> cp, off;                             // scratch of encode_text (GIL held)
+    std::vector<int> sym, rk, mid;                             // scratch of bpe()
+    std::string buf;
 };
 
 inline uint8_t klass(const Tok& t, uint32_t c) { return c < t.cls.size() ? t.cls[c] : 0; }
@@ -185,16 +235,19 @@ struct MergeTable {
 inline const MergeTable& merge_table(const Tok& t) { return *reinterpret_cast<const MergeTable*>(t.merge_tab); }
 
 void bpe(Tok& t, const char* s, size_t len, std::vector<int>& out) {
-    std::string key(s, len);
-    auto it = t.cache.find(key);
-    if (it != t.cache.end()) {
-        out.insert(out.end(), it->second.begin(), it->second.end());
+    const uint64_t h = BpeCache::hash(s, len);
+    size_t cnt = 0, slot = 0;
+    if (const int* hit = t.cache.find(s, len, h, &cnt, &slot)) {
+        out.insert(out.end(), hit, hit + cnt);
         return;
     }
     const MergeTable& mt = merge_table(t);
     // symbols + the rank / merged id of each adjacent pair, updated locally per merge:
     // O(n) table probes per word instead of O(n^2)
-    std::vector<int> sym(len), rk(len), mid(len);
+    if (t.sym.size() < len) { t.sym.resize(len); t.rk.resize(len); t.mid.resize(len); }
+    int* sym = t.sym.data();
+    int* rk = t.rk.data();
+    int* mid = t.mid.data();
     for (size_t i = 0; i < len; ++i) sym[i] = t.byte_id[(unsigned char)s[i]];
     size_t n = len;
     for (size_t i = 0; i + 1 < n; ++i) rk[i] = mt.find(sym[i], sym[i + 1], &mid[i]);
@@ -213,15 +266,19 @@ void bpe(Tok& t, const char* s, size_t len, std::vector<int>& out) {
         else rk[bi] = INT32_MAX;
         if (bi > 0) rk[bi - 1] = mt.find(sym[bi - 1], sym[bi], &mid[bi - 1]);
     }
-    sym.resize(n);
-    if (t.cache.size() < t.cache_max) t.cache.emplace(std::move(key), sym);
-    out.insert(out.end(), sym.begin(), sym.end());
+    if (t.cache.entries >= BpeCache::MAX_ENTRIES) {
+        t.cache.clear();
+        t.cache.find(s, len, h, &cnt, &slot);  // its slot in the emptied table
+    }
+    t.cache.put(slot, s, len, h, sym, n);
+    out.insert(out.end(), sym, sym + n);
 }
 
 void encode_text(Tok& t, const char* s, size_t len, std::vector<int>& out) {
     // model_text: the XML line-break entity reaches the model as one "\n"
-    std::string buf;
+    std::string& buf = t.buf;
     if (len >= 5 && memmem(s, len, "&#10;", 5)) {
+        buf.clear();
         buf.reserve(len);
         for (size_t i = 0; i < len;) {
             if (i + 5 <= len && memcmp(s + i, "&#10;", 5) == 0) {
@@ -234,7 +291,8 @@ void encode_text(Tok& t, const char* s, size_t len, std::vector<int>& out) {
         s = buf.data();
         len = buf.size();
     }
-    std::vector<uint32_t> cp, off;
+    std::vector<uint32_t>& cp = t.cp;
+    std::vector<uint32_t>& off = t.off;
     size_t pos = 0;
     while (pos <= len) {
         // next special-token literal (leftmost; specials never overlap)
@@ -468,7 +526,7 @@ PyObject* py_cache_size(PyObject*, PyObject* args) {
     PyObject* cap;
     if (!PyArg_ParseTuple(args, "O", &cap)) return nullptr;
     Tok* t = get(cap);
-    return t ? PyLong_FromSize_t(t->cache.size()) : nullptr;
+    return t ? PyLong_FromSize_t(t->cache.entries) : nullptr;
 }
 
 PyMethodDef methods[] = {

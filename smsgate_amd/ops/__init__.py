@@ -882,7 +882,8 @@ class QAParams(ctypes.Structure):
                 ("cls_bits", _c_int * QA_MAX_NF), ("cap", _c_int * QA_MAX_NF),
                 ("off_end", _c_int), ("off_null", _c_int), ("off_cls", _c_int),
                 ("cls_tok", (_c_int * QA_MAX_CLS_TOK) * QA_NCLS), ("cls_len", _c_int * QA_NCLS),
-                ("reject_mask", _c_int), ("sep", _c_int), ("max_out", _c_int)]
+                ("reject_mask", _c_int), ("sep", _c_int), ("max_out", _c_int),
+                ("s_need", _c_int * QA_MAX_NF), ("e_need", _c_int * QA_MAX_NF)]
 
 
 def qa_params(lay, tokenizer) -> QAParams:
@@ -900,7 +901,7 @@ def qa_params(lay, tokenizer) -> QAParams:
     srows, erows = qa_rows(lay)
     for f in range(nf):
         p.start_row[f], p.end_row[f] = srows[f], erows[f]
-        p.cls_bits[f], p.cap[f] = lay.class_bits()[f], lay.caps()[f]
+        p.cls_bits[f], p.cap[f], p.s_need[f], p.e_need[f] = lay.rules()[f]
     p.off_end, p.off_null, p.off_cls = lay.pe0 - lay.ptr0, lay.null_id - lay.ptr0, lay.cls0 - lay.ptr0
     for c, name in enumerate(TXN_TYPES):
         toks = tokenizer.encode(name)

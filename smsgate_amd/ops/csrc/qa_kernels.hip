@@ -17,9 +17,12 @@
 //      valid start's score, or no valid pair) and the joint arg-max of
 //      start[s] + end[e] over valid pairs -- s at a word boundary and in the field's
 //      class (and, for dates / numbers, not right after a card mask), e >= s within
-//      the cap, every token s..e in class, e followed by a word boundary.  Word
-//      boundary: NOT (a ends with a letter and b starts with one, or a ends with a
-//      digit and b starts with one).  One lane per start, its ends scanned in order;
+//      the cap, every token s..e in class and none a line break, the first / last
+//      token with the field kind's edge flags (s_need / e_need: a number starts and
+//      ends with a digit ...), e followed by a word boundary.  Word boundary: NOT (a
+//      ends with a letter and b starts with one, or a ends with a digit and b starts
+//      with one), and a lone separator between a digit and a three-digit group joins
+//      them ("218" "," "993").  One lane per start, its ends scanned in order;
 //      ties go to the lower start, then the lower end (serving/qa.py qa_decode_ref);
 //   4. the answer in the copy format (class tokens, <sep>, each field's body tokens
 //      and <sep>; a rejection class: only its tokens and <sep>) into out_buf.
@@ -40,6 +43,10 @@
 #define QF_ED 8
 #define QF_MASK 16
 #define QF_NO_START_AFTER_MASK (32 | 64)  // date | number class bits
+#define QF_NL 512      // contains a line break
+#define QF_LD 8192     // last char a digit
+#define QF_GRP3 16384  // exactly three ASCII digits
+#define QF_SEP 32768   // a lone "," "." "'"
 
 struct QAParams {
   int nf, nq, n_pos;
@@ -52,6 +59,8 @@ struct QAParams {
   int cls_len[QA_NCLS];
   int reject_mask;  // bit c: class c is a non-transaction (no fields)
   int sep, max_out;
+  int s_need[QA_MAX_NF];  // edge flags the first token must all have (serving/qa.py EDGE_RULES)
+  int e_need[QA_MAX_NF];  // ... and the last token
 };
 
 static __device__ __forceinline__ float qa_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
@@ -190,16 +199,17 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
     cls_sel = c;
   }
   for (int f = wid; f < nf; f += 4) {
-    const int cls = p.cls_bits[f], cap = p.cap[f];
+    const int cls = p.cls_bits[f], cap = p.cap[f], sneed = p.s_need[f], eneed = p.e_need[f];
     float top = -INFINITY;  // best valid start score
     float best = -INFINITY;
     int bs = 0x7fffffff, be = -1;
     for (int s = lane; s < n; s += 64) {
       const int fs = fb[s];
-      bool ok = (cls == 0) || (fs & cls);
+      bool ok = ((cls == 0) || (fs & cls)) && !(fs & QF_NL) && (fs & sneed) == sneed;
       if (ok && s > 0) {
         const int fp = fb[s - 1];
-        ok = !qa_glued(fp, fs) && !((cls & QF_NO_START_AFTER_MASK) && (fp & QF_MASK));
+        ok = !qa_glued(fp, fs) && !((cls & QF_NO_START_AFTER_MASK) && (fp & QF_MASK)) &&
+             !(s > 1 && (fp & QF_SEP) && (fs & QF_GRP3) && (fb[s - 2] & QF_LD));
       }
       if (!ok) continue;
       const float ss = sc_start[f][s];
@@ -207,8 +217,14 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
       const int emax = min(n, s + cap);
       for (int e = s; e < emax; ++e) {
         const int fe = fb[e];
-        if (cls && !(fe & cls)) break;
-        if (e + 1 < n && qa_glued(fe, fb[e + 1])) continue;
+        if ((cls && !(fe & cls)) || (fe & QF_NL)) break;
+        if ((fe & eneed) != eneed) continue;
+        if (e + 1 < n) {
+          const int fn = fb[e + 1];
+          if (qa_glued(fe, fn)) continue;
+          if ((fe & QF_SEP) && (fn & QF_GRP3) && e > 0 && (fb[e - 1] & QF_LD)) continue;
+          if ((fe & QF_LD) && (fn & QF_SEP) && e + 2 < n && (fb[e + 2] & QF_GRP3)) continue;
+        }
         const float v = ss + sc_end[f][e];
         if (v > best) { best = v; bs = s; be = e; }  // strict: the lowest end of this start
       }

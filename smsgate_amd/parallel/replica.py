@@ -130,9 +130,15 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     prof = None
     prof_msgs = 0
     if cfg.get("profile_dir"):
-        import cProfile
+        if cfg.get("profile_mode", "sample") == "sample":  # CPU-time sampling (utils/sampler.py)
+            from ..utils.sampler import CpuSampler
 
-        prof = cProfile.Profile()
+            prof = CpuSampler()
+            prof.enable, prof.disable = prof.start, prof.stop
+        else:
+            import cProfile
+
+            prof = cProfile.Profile()
     while True:
         cmd = await asyncio.to_thread(client.control.get)
         if cmd is None or cmd.get("cmd") == "quit":
@@ -205,9 +211,12 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
 
         os.makedirs(cfg["profile_dir"], exist_ok=True)
         stem = os.path.join(cfg["profile_dir"], f"parser-r{rank}-w{widx}")
-        prof.dump_stats(stem + ".pstats")
-        with open(stem + ".json", "w") as fh:
-            _json.dump({"msgs": prof_msgs}, fh)
+        if hasattr(prof, "dump_stats"):
+            prof.dump_stats(stem + ".pstats")
+            with open(stem + ".json", "w") as fh:
+                _json.dump({"msgs": prof_msgs}, fh)
+        else:
+            prof.dump(stem + ".samples.json", msgs=prof_msgs)
     await writer.stop()
     await worker.stop()
 

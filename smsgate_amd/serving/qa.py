@@ -26,7 +26,11 @@ the causal model lets every query row attend to the whole body:
   ``start[s] + end[e]`` over VALID pairs -- ``s <= e < s + cap``, every token in
   the field's class, ``s`` and ``e + 1`` at word boundaries, a date / number never
   starting right after a card mask.  Word boundaries split letters from digits
-  ("USD52.00", "x1234" and "1500р" separate), unlike the span format's rule.
+  ("USD52.00", "x1234" and "1500р" separate), unlike the span format's rule, and
+  join a digit group to a lone separator and a three-digit group ("218" "," "993" is
+  one word).  Value edges by kind (:data:`EDGE_RULES`): a number starts and ends with
+  a digit, a card ends with one, a date or a free-text value starts and ends with a
+  letter or digit; no value crosses a line break.
 
 The answer is written in the copy format (txn tokens, then each field's body
 tokens, each ended by ``<sep>``), so the tokenizers' field decoders, the remote
@@ -45,7 +49,7 @@ from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
            "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
-           "QA_MAX_QUERIES"]
+           "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
@@ -54,6 +58,14 @@ QA_MAX_QUERIES = 24
 QF_SL, QF_SD, QF_EL, QF_ED, QF_MASK = 1, 2, 4, 8, 16
 QA_CLASS_BITS = {k: v << 3 for k, v in TOK_CLASS_BITS.items()}  # date 32, number 64, currency 128, card 256
 _NO_START_AFTER_MASK = QA_CLASS_BITS["date"] | QA_CLASS_BITS["number"]
+# edges: contains a line break; first non-space char a letter-or-digit / a digit; last
+# char a letter-or-digit / a digit; exactly three ASCII digits; a lone "," "." "'"
+QF_NL, QF_FA, QF_FD, QF_LA, QF_LD, QF_GRP3, QF_SEP = 512, 1024, 2048, 4096, 8192, 16384, 32768
+# field kind -> (flags its first token must all have, flags its last token must all have).
+# Every gold value of every training and held-out family obeys them (a free-text value
+# may start with a digit: "7-ELEVEN").
+EDGE_RULES = {"number": (QF_FD, QF_LD), "card": (0, QF_LD), "date": (QF_FA, QF_LA), "text": (QF_FA, QF_LA),
+              "currency": (0, 0)}
 
 
 @dataclass(frozen=True)
@@ -89,6 +101,10 @@ class QALayout:
 
     def class_bits(self) -> List[int]:
         return [QA_CLASS_BITS.get(f.kind, 0) for f in self.fields[1:]]
+
+    def rules(self) -> List[Tuple[int, int, int, int]]:
+        """Per copied field: (class bits, cap, first-token edge flags, last-token edge flags)."""
+        return [(QA_CLASS_BITS.get(f.kind, 0), f.cap) + EDGE_RULES.get(f.kind, (0, 0)) for f in self.fields[1:]]
 
     def max_answer_tokens(self) -> int:
         return sum(f.cap for f in self.fields) + len(self.fields)
@@ -138,6 +154,21 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
             f |= QF_ED
         if t.endswith("*"):
             f |= QF_MASK
+        if "\n" in t:
+            f |= QF_NL
+        h = t.lstrip(" ")
+        if h and (h[0].isalnum() or h[0] == "�"):
+            f |= QF_FA
+        if h[:1].isdigit():
+            f |= QF_FD
+        if t[-1].isalnum() or t[-1] == "�":
+            f |= QF_LA
+        if t[-1].isdigit():
+            f |= QF_LD
+        if len(t) == 3 and t.isascii() and t.isdigit():
+            f |= QF_GRP3
+        if t in (",", ".", "'"):
+            f |= QF_SEP
         out[i] |= f
     return out
 
@@ -146,30 +177,52 @@ def _glued(fa: int, fb: int) -> bool:
     return bool(((fa & QF_EL) and (fb & QF_SL)) or ((fa & QF_ED) and (fb & QF_SD)))
 
 
-def valid_starts(flags: np.ndarray, body: Sequence[int], n: int, cls: int) -> np.ndarray:
-    """[n] bool: positions a value of class bits ``cls`` may start at (``n`` pointable)."""
-    ok = np.zeros(n, dtype=bool)
-    for j in range(n):
-        fj = int(flags[body[j]])
-        if cls and not fj & cls:
-            continue
-        if j > 0:
-            fp = int(flags[body[j - 1]])
-            if _glued(fp, fj) or ((cls & _NO_START_AFTER_MASK) and fp & QF_MASK):
-                continue
-        ok[j] = True
-    return ok
+def _fl(flags: np.ndarray, body: Sequence[int], j: int) -> int:
+    return int(flags[body[j]])
 
 
-def valid_ends(flags: np.ndarray, body: Sequence[int], n: int, cls: int, cap: int, s: int) -> List[int]:
-    """End positions of a value starting at ``s``: in class all the way, within the
-    cap, followed by a word boundary (or the end of the pointable body)."""
+def _start_ok(flags, body, j: int, cls: int, s_need: int) -> bool:
+    fj = _fl(flags, body, j)
+    if (cls and not fj & cls) or fj & QF_NL or (fj & s_need) != s_need:
+        return False
+    if j > 0:
+        fp = _fl(flags, body, j - 1)
+        if _glued(fp, fj) or ((cls & _NO_START_AFTER_MASK) and fp & QF_MASK):
+            return False
+        if j > 1 and fp & QF_SEP and fj & QF_GRP3 and _fl(flags, body, j - 2) & QF_LD:
+            return False  # "993" of "218,993"
+    return True
+
+
+def _end_ok(flags, body, n: int, e: int, e_need: int) -> bool:
+    fe = _fl(flags, body, e)
+    if (fe & e_need) != e_need:
+        return False
+    if e + 1 < n and (_glued(fe, _fl(flags, body, e + 1)) or (
+            e > 0 and fe & QF_SEP and _fl(flags, body, e + 1) & QF_GRP3 and _fl(flags, body, e - 1) & QF_LD)):
+        return False
+    if e + 2 < n and fe & QF_LD and _fl(flags, body, e + 1) & QF_SEP and _fl(flags, body, e + 2) & QF_GRP3:
+        return False  # "218" of "218,993"
+    return True
+
+
+def valid_starts(flags: np.ndarray, body: Sequence[int], n: int, cls: int, s_need: int = 0) -> np.ndarray:
+    """[n] bool: positions a value of class bits ``cls`` may start at (``n`` pointable);
+    ``s_need``: flags the first token must all have (:data:`EDGE_RULES`)."""
+    return np.array([_start_ok(flags, body, j, cls, s_need) for j in range(n)], dtype=bool)
+
+
+def valid_ends(flags: np.ndarray, body: Sequence[int], n: int, cls: int, cap: int, s: int,
+               e_need: int = 0) -> List[int]:
+    """End positions of a value starting at ``s``: in class all the way and never across
+    a line break, within the cap, with the last token's edge flags ``e_need``, followed
+    by a word boundary (or the end of the pointable body)."""
     out = []
     for e in range(s, min(n, s + cap)):
-        fe = int(flags[body[e]])
-        if cls and not fe & cls:
+        fe = _fl(flags, body, e)
+        if (cls and not fe & cls) or fe & QF_NL:
             break
-        if e + 1 >= n or not _glued(fe, int(flags[body[e + 1]])):
+        if _end_ok(flags, body, n, e, e_need):
             out.append(e)
     return out
 
@@ -186,7 +239,7 @@ def qa_targets(tok, lay: QALayout, flags: np.ndarray, answer: Dict[str, Optional
     n = msg_len - 1  # pointable positions (the message ends with <ans>)
     ids = body_enc[0]
     spans: List[Tuple[int, int]] = []
-    for f, bits, cap in zip(lay.fields[1:], lay.class_bits(), lay.caps()):
+    for f, (bits, cap, s_need, e_need) in zip(lay.fields[1:], lay.rules()):
         v = answer.get(f.name) or ""
         if not v or txn in REJECT_TXN:
             spans.append((-1, -1))
@@ -195,7 +248,7 @@ def qa_targets(tok, lay: QALayout, flags: np.ndarray, answer: Dict[str, Optional
         if sp is None or sp[1] >= n:
             return None
         s, e = sp
-        if not valid_starts(flags, ids, n, bits)[s] or e not in valid_ends(flags, ids, n, bits, cap, s):
+        if not _start_ok(flags, ids, s, bits, s_need) or e not in valid_ends(flags, ids, n, bits, cap, s, e_need):
             return None
         spans.append((s, e))
     return cls, spans
@@ -207,19 +260,27 @@ def qa_rows(lay: QALayout) -> Tuple[List[int], List[int]]:
             [lay.end_row(f) for f in range(1, len(lay.fields))])
 
 
-def _pair_mask(fb: np.ndarray, n: int, cls: int, cap: int) -> Tuple[np.ndarray, np.ndarray]:
+def _pair_mask(fb: np.ndarray, n: int, cls: int, cap: int, s_need: int = 0,
+               e_need: int = 0) -> Tuple[np.ndarray, np.ndarray]:
     """(valid starts [n], valid (start, end) pairs [n, n]) of one field from the body's
     token flags ``fb`` (vectorised :func:`valid_starts` / :func:`valid_ends`)."""
     fb = fb[:n].astype(np.int64)
     prev = np.concatenate([[0], fb[:-1]])
+    prev2 = np.concatenate([[0, 0], fb[:-2]])[:n]
     glued_prev = (((prev & QF_EL) != 0) & ((fb & QF_SL) != 0)) | (((prev & QF_ED) != 0) & ((fb & QF_SD) != 0))
+    glued_prev |= ((prev & QF_SEP) != 0) & ((fb & QF_GRP3) != 0) & ((prev2 & QF_LD) != 0)
     glued_prev[0] = False
     in_cls = (fb & cls) != 0 if cls else np.ones(n, dtype=bool)
+    in_cls &= (fb & QF_NL) == 0
     after_mask = ((prev & QF_MASK) != 0) & bool(cls & _NO_START_AFTER_MASK)
     after_mask[0] = False
-    vs = in_cls & ~glued_prev & ~after_mask
-    end_ok = np.ones(n, dtype=bool)
-    end_ok[:-1] = ~glued_prev[1:]
+    vs = in_cls & ~glued_prev & ~after_mask & ((fb & s_need) == s_need)
+    # an end may not be followed by a glued token, nor by a separator glued to a group
+    end_ok = (fb & e_need) == e_need
+    end_ok[:-1] &= ~glued_prev[1:]
+    nxt_sep = np.zeros(n, dtype=bool)
+    nxt_sep[:-2] = ((fb[:-2] & QF_LD) != 0) & ((fb[1:-1] & QF_SEP) != 0) & ((fb[2:] & QF_GRP3) != 0)
+    end_ok &= ~nxt_sep
     bad = np.concatenate([[0], np.cumsum(~in_cls)])  # out-of-class tokens before position k
     S, E = np.arange(n)[:, None], np.arange(n)[None, :]
     pairs = (E >= S) & (E - S < cap) & (bad[E + 1] - bad[S] == 0) & end_ok[None, :] & vs[:, None]
@@ -244,10 +305,10 @@ def qa_decode_ref(cls_logits, start_logits, null_logits, end_logits, bodies: Seq
         n = len(body) - 1
         fb = flags[np.asarray(body[:n], dtype=np.int64)]
         spans: List[Tuple[int, int]] = []
-        for f, (bits, cap) in enumerate(zip(lay.class_bits(), lay.caps())):
+        for f, (bits, cap, s_need, e_need) in enumerate(lay.rules()):
             st = np.asarray(start_logits[m][f][:n], dtype=np.float32)
             en = np.asarray(end_logits[m][f][:n], dtype=np.float32)
-            vs, pairs = _pair_mask(fb, n, bits, cap)
+            vs, pairs = _pair_mask(fb, n, bits, cap, s_need, e_need)
             if not pairs.any() or np.float32(null_logits[m][f]) >= st[vs].max():
                 spans.append((-1, -1))
                 continue

@@ -96,3 +96,22 @@ def test_lone_surrogate_does_not_fail_the_batch(toks):
     ids = np.frombuffer(flat, dtype=np.int32).tolist()
     assert len(ln) == 3 and ids[:ln[0]] == tk.encode("ok body") + [tk.ans]
     assert ids[ln[0] + ln[1]:] == tk.encode("also ok") + [tk.ans]
+
+
+def test_full_cache_is_emptied_and_refilled_exactly(toks):
+    """The pre-token cache empties itself when it reaches its capacity (2^18 entries):
+    held-out traffic's one-off names and amounts must not freeze it.  Encodings before,
+    across and after the reset equal the library's."""
+    tk, ft = toks
+    r = random.Random(9)
+    # letters only: every word is one pre-token (" WORD"), ~300 k distinct ones
+    words = ["".join(r.choice("ABCDEFGHKLMNPRSTUVZ") for _ in range(r.randint(5, 9))) for _ in range(300000)]
+    probe = "Покупка 1 500,00 RUB в SHOP CITY, ул. LENINA 5; баланс 12 345,67 RUB"
+    want = tk.encode(probe)
+    assert ft.encode(probe) == want
+    for i in range(0, len(words), 5000):
+        ft.encode(" ".join(words[i:i + 5000]))
+    assert 0 < ft.cache_size() < len(set(words)) - 2 ** 18 + 1000  # emptied once on the way
+    assert ft.encode(probe) == want
+    sample = " ".join(words[-50:])
+    assert ft.encode(sample) == tk.encode(sample)

@@ -82,12 +82,12 @@ def test_vectorised_pair_mask_equals_the_loop_reference(env):
     items = synth.generate(150, seed=8, vocab_name="heldout", families="all", negatives=0.1)
     for m in tk.message_ids([normalize_body(s.body) for s in items], 128):
         n = len(m) - 1
-        for bits, cap in zip(lay.class_bits(), lay.caps()):
-            vs, pairs = _pair_mask(fl[np.asarray(m[:n])], n, bits, cap)
-            vs2 = valid_starts(fl, m, n, bits)
+        for bits, cap, s_need, e_need in lay.rules():
+            vs, pairs = _pair_mask(fl[np.asarray(m[:n])], n, bits, cap, s_need, e_need)
+            vs2 = valid_starts(fl, m, n, bits, s_need)
             assert (vs == vs2).all()
             for s in range(n):
-                ends = valid_ends(fl, m, n, bits, cap, s) if vs2[s] else []
+                ends = valid_ends(fl, m, n, bits, cap, s, e_need) if vs2[s] else []
                 assert np.nonzero(pairs[s])[0].tolist() == ends
 
 
@@ -109,6 +109,34 @@ def test_word_boundaries_split_letters_from_digits(env):
     assert tk.value_span("AM", "AMERIABANK API", ids, offs) is None
     f = fl[tk.encode("USD")[0]]
     assert f & QF_SL and f & QF_EL and not f & (QF_SD | QF_ED)
+
+
+def _spans_of(tk, fl, text, bits, cap, s_need, e_need):
+    ids = tk.encode_offsets([text])[0][0] + [tk.ans]
+    n = len(ids) - 1
+    vs, pairs = _pair_mask(fl[np.asarray(ids[:n])], n, bits, cap, s_need, e_need)
+    S = tk.token_strings
+    return {"".join(S[t] for t in ids[a:z + 1]).strip() for a, z in zip(*np.nonzero(pairs))}
+
+
+def test_value_edges_follow_the_field_kind(env):
+    """A number starts and ends with a digit and never splits "218,993.63" at its
+    thousands separator; free text starts / ends with a letter or digit; no value crosses
+    a line break (the r05 error analysis: "993.63", "3425.57.", "KENK,", "27\nKEK")."""
+    tk, lay, fl = env
+    rules = dict(zip((f.name for f in lay.fields[1:]), lay.rules()))
+    amounts = _spans_of(tk, fl, "Paid -218,993.63 RUB | SHOP", *rules["amount"])
+    assert "218,993.63" in amounts and not {"993.63", "993", "218", ",993.63"} & amounts, amounts
+    bal = _spans_of(tk, fl, "Bal $3425.57. Bank.", *rules["balance"])
+    assert "3425.57" in bal and "3425.57." not in bal, bal
+    city = _spans_of(tk, fl, "at SHOP, KENK, NTT LANE 118", *rules["city"])
+    assert "KENK" in city and "KENK," not in city and ", KENK" not in city, city
+    addr = _spans_of(tk, fl, "Карта *2928\nпр. BROUN 27\nKEK\nОстаток", *rules["address"])
+    assert "пр. BROUN 27" in addr and not any("\n" in a for a in addr), addr
+    # the reference's legacy layout glues the address to the date with a comma: still two words
+    legacy = "SALE: SHOP, CITY, DUL ST. 108,16.02.23 21:24,card ***3651"
+    assert "16.02.23 21:24" in _spans_of(tk, fl, legacy, *rules["date"])
+    assert "DUL ST. 108" in _spans_of(tk, fl, legacy, *rules["address"])
 
 
 def test_strict_boundaries_win_over_glued_occurrences(env):

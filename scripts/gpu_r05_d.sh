@@ -3,7 +3,7 @@
 # two-stream split A/B (one prefill of the whole batch vs two concurrent halves).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-O=gpurun_out/r05d
+O=${O_D:-gpurun_out/r05d}
 mkdir -p $O
 timeout -k 10 300 python -u scripts/sol_table.py --no-spec --decode-m 221184 --prefill-m 110592 --prefill-len 50 \
   --rounds 2 > $O/sol.json 2> $O/sol.err || { echo "sol rc=$?"; tail -20 $O/sol.err; exit 1; }

@@ -35,8 +35,14 @@ def _group(name: str) -> str:
 
 
 def _busy_ns(db):
-    """(union of the kernel intervals in ns, number of streams) of a results.db."""
-    iv = sorted(db.execute("SELECT start, end FROM kernels"))
+    """(union of the kernel intervals in ns, number of streams) of a results.db, or
+    (None, None) when it has no per-dispatch ``kernels`` view."""
+    try:
+        iv = sorted(db.execute("SELECT start, end FROM kernels"))
+    except Exception:  # noqa: BLE001 -- a stats-only database
+        return None, None
+    if not iv:
+        return None, None
     streams = db.execute("SELECT COUNT(DISTINCT stream_id) FROM kernels").fetchone()[0]
     busy, (cs, ce) = 0, iv[0]
     for s, e in iv[1:]:

@@ -19,6 +19,7 @@ def main() -> int:
     p.add_argument("--format", default="qa")
     p.add_argument("--steps", type=int, default=40)
     p.add_argument("--batch", type=int, default=128)
+    p.add_argument("--fused", default="1,0", help="TrainConfig.fused values to measure (A/B)")
     a = p.parse_args()
     import torch
 
@@ -27,31 +28,33 @@ def main() -> int:
 
     tok = load_tokenizer()
     data = make_examples(tok, answer_fsm(tok, a.format), 8192, seed=1, negatives=0.12)
-    times = []
+    for fused in (bool(int(x)) for x in a.fused.split(",")):
+        times = []
 
-    def log(s):
-        times.append((time.perf_counter(), s))
+        def log(s):
+            times.append((time.perf_counter(), s))
 
-    tc = TrainConfig(steps=a.steps, batch=a.batch, n_examples=len(data), log_every=1, answer_format=a.format,
-                     warmup=5)
-    train_extractor(tc, device="cuda", data=data, log=log)
-    stamps = [t for t, s in times if s.startswith("step")]
-    per = (stamps[-1] - stamps[10]) / (len(stamps) - 11) * 1e3
-    # one profiled step range (kernel count and GPU time)
-    from torch.profiler import ProfilerActivity, profile
+        tc = TrainConfig(steps=a.steps, batch=a.batch, n_examples=len(data), log_every=1, answer_format=a.format,
+                         warmup=5, fused=fused)
+        train_extractor(tc, device="cuda", data=data, log=log)
+        stamps = [t for t, s in times if s.startswith("step")]
+        per = (stamps[-1] - stamps[10]) / (len(stamps) - 11) * 1e3
+        # one profiled step range (kernel count and GPU time)
+        from torch.profiler import ProfilerActivity, profile
 
-    tc2 = TrainConfig(steps=6, batch=a.batch, n_examples=len(data), log_every=0, answer_format=a.format, warmup=2)
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
-        train_extractor(tc2, device="cuda", data=data, log=lambda s: None)
-        torch.cuda.synchronize()
-    ev = [e for e in prof.key_averages() if e.device_type.name == "CUDA" or getattr(e, "self_device_time_total", 0)]
-    kern = sum(e.count for e in prof.key_averages() if getattr(e, "self_device_time_total", 0) > 0)
-    gpu_us = sum(getattr(e, "self_device_time_total", 0) for e in prof.key_averages())
-    top = sorted(prof.key_averages(), key=lambda e: -getattr(e, "self_device_time_total", 0))[:12]
-    print(json.dumps({"format": a.format, "batch": a.batch, "ms_per_step": round(per, 2),
-                      "kernels_per_step": round(kern / 6, 1), "gpu_ms_per_step": round(gpu_us / 6 / 1e3, 2),
-                      "top": [[e.key[:60], round(getattr(e, "self_device_time_total", 0) / 6 / 1e3, 3), e.count // 6]
-                              for e in top]}), flush=True)
+        tc2 = TrainConfig(steps=6, batch=a.batch, n_examples=len(data), log_every=0, answer_format=a.format,
+                          warmup=2, fused=fused)
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            train_extractor(tc2, device="cuda", data=data, log=lambda s: None)
+            torch.cuda.synchronize()
+        kev = [e for e in prof.key_averages() if getattr(e, "self_device_time_total", 0) > 0]
+        kern = sum(e.count for e in kev)
+        gpu_us = sum(e.self_device_time_total for e in kev)
+        top = sorted(kev, key=lambda e: -e.self_device_time_total)[:12]
+        print(json.dumps({"format": a.format, "batch": a.batch, "fused": fused, "ms_per_step": round(per, 2),
+                          "kernels_per_step": round(kern / 6, 1), "gpu_ms_per_step": round(gpu_us / 6 / 1e3, 2),
+                          "top": [[e.key[:60], round(e.self_device_time_total / 6 / 1e3, 3), e.count // 6]
+                                  for e in top]}), flush=True)
     return 0
 
 

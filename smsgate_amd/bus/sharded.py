@@ -52,15 +52,16 @@ __all__ = ["ShardedBus", "shard_of", "parse_members", "Router", "NODE_PARTITIONS
 
 # The 8-GPU node's broker layout (deploy/docker-compose.yml is generated from it by
 # deploy/gen_compose.py; bench.py): every per-SMS subject partitioned -- sms.raw (one
-# publish + delivery + ack per SMS) over sixteen brokers, each also a native HTTP ingest
+# publish + delivery + ack per SMS) over twenty brokers, each also a native HTTP ingest
 # door (smsgate-busd --http-listen: ~56 k single-SMS requests/s each,
-# profiles/r03_ingest_bench.jsonl), sms.parsed (parser -> writer) and sms.processing
-# (one publish per parsed SMS, consumed downstream) over two each -- and the low-rate
-# subjects (sms.failed, sms.categorized) on one more.  tests/test_broker_capacity.py
-# sizes EVERY member and the doors at 2x against the latest measured headline (VERDICT
-# r04 next #3: sms.processing used to share the rest broker at the full node rate).
+# profiles/r03_ingest_bench.jsonl: 20 doors take 2x an 8 x 70 k node), sms.parsed
+# (parser -> writer) and sms.processing (one publish per parsed SMS, consumed
+# downstream) over four each (a member carries ~0.9 / 4 of the node rate: 2x headroom
+# on one ~316 k msgs/s broker up to an 8 x 80 k node) -- and the low-rate subjects
+# (sms.failed, sms.categorized) on one more.  tests/test_broker_capacity.py sizes EVERY
+# member and the doors at 2x against the latest measured headline.
 # Fewer GPUs on a node: node_partitions() scales it down.
-NODE_PARTITIONS = {SUBJECT_RAW: 16, SUBJECT_PARSED: 2, SUBJECT_PROCESSING: 2}
+NODE_PARTITIONS = {SUBJECT_RAW: 20, SUBJECT_PARSED: 4, SUBJECT_PROCESSING: 4}
 NODE_GPUS = 8
 
 

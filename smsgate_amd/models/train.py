@@ -82,6 +82,9 @@ class TrainConfig:
     ema: float = 0.998
     ema_start: int = 0  # first step the average includes (0 = warmup end)
     data_parallel: bool = True  # under torch.distributed: all-reduce gradients (False: train this rank alone)
+    # fused HIP RMSNorm / RoPE / SwiGLU forward+backward (models/train_ops.py) on the GPU;
+    # False: reference_forward (plain PyTorch elementwise chains)
+    fused: bool = True
     eval_every: int = 0  # call on_eval(step, serving weights) every N steps (0 = never)
     # "copy": every copied value written with the body's own tokens; "span": as two
     # pointers to its first and last body token (serving/fsm.py build_span_fsm)
@@ -421,6 +424,13 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
             if rank == 0:
                 rng.setstate(_as_rng_state(state["rng"]))
         log(f"train: resumed from {ck} at step {start}")
+    from . import train_ops
+
+    if cfg.fused and train_ops.available(device):
+        forward = train_ops.fused_forward
+    else:
+        def forward(w_, ids_, add_):
+            return reference_forward(w_, ids_, compute_dtype=torch.float32, return_hidden=True, add_ids=add_)
     t0 = time.perf_counter()
     for step in range(start, cfg.steps):
         for g in opt.param_groups:
@@ -431,11 +441,11 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
                 from ..serving.qa import qa_logits, qa_loss
 
                 ids, add, qpos, targets = qa_batch(prefix, exs, tok.pad, device, fsm.lay)
-                h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True, add_ids=add)
+                h = forward(w, ids, add)
                 loss = qa_loss(qa_logits(h, w.embed, qpos, fsm.lay), targets, fsm.lay)
             else:
                 ids, labels, add = _batch(prefix, exs, tok.pad, device, fsm.ptr0)
-                h = reference_forward(w, ids, compute_dtype=torch.float32, return_hidden=True, add_ids=add)
+                h = forward(w, ids, add)
                 sel = labels.view(-1) >= 0
                 hs = h.reshape(-1, h.shape[-1])[sel]
                 logits = hs @ w.embed[:v_dec].t()

@@ -152,6 +152,14 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_qa_params_size.restype = _c_int
     lib.sg_embed_rows_add_ids.argtypes = [_ip, _ip, _vp, _vp, _c_int, _c_int, _c_int, _vp]
     lib.sg_embed_rows_add_ids.restype = _c_int
+    # training step (csrc/train_kernels.hip, models/train_ops.py)
+    lib.sg_rms_fwd.argtypes = [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_float, _vp]
+    lib.sg_rms_bwd.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp]
+    lib.sg_rope_split.argtypes = [_c_int, _vp, _vp, _vp, _vp, _vp, _vp] + [_c_int] * 5 + [_vp]
+    lib.sg_swiglu_fwd.argtypes = [_vp, _vp, _c_int, _c_int, _vp]
+    lib.sg_swiglu_bwd.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _vp]
+    for fn in (lib.sg_rms_fwd, lib.sg_rms_bwd, lib.sg_rope_split, lib.sg_swiglu_fwd, lib.sg_swiglu_bwd):
+        fn.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version", "sg_kv_copy_prefix"):
         getattr(lib, f).restype = _c_int
@@ -883,7 +891,7 @@ class QAParams(ctypes.Structure):
                 ("off_end", _c_int), ("off_null", _c_int), ("off_cls", _c_int),
                 ("cls_tok", (_c_int * QA_MAX_CLS_TOK) * QA_NCLS), ("cls_len", _c_int * QA_NCLS),
                 ("reject_mask", _c_int), ("sep", _c_int), ("max_out", _c_int),
-                ("s_need", _c_int * QA_MAX_NF), ("e_need", _c_int * QA_MAX_NF)]
+                ("s_need", _c_int * QA_MAX_NF), ("e_need", _c_int * QA_MAX_NF), ("absorb", _c_int * QA_MAX_NF)]
 
 
 def qa_params(lay, tokenizer) -> QAParams:
@@ -902,6 +910,7 @@ def qa_params(lay, tokenizer) -> QAParams:
     for f in range(nf):
         p.start_row[f], p.end_row[f] = srows[f], erows[f]
         p.cls_bits[f], p.cap[f], p.s_need[f], p.e_need[f] = lay.rules()[f]
+        p.absorb[f] = int(lay.absorb_time()[f])
     p.off_end, p.off_null, p.off_cls = lay.pe0 - lay.ptr0, lay.null_id - lay.ptr0, lay.cls0 - lay.ptr0
     for c, name in enumerate(TXN_TYPES):
         toks = tokenizer.encode(name)
@@ -941,8 +950,8 @@ def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, id
         raise ValueError("qa_decode: ids / out_len / out_buf too small")
     if out_buf.dim() != 2 or out_buf.shape[0] < M or out_buf.shape[1] != params.max_out:
         raise ValueError(f"qa_decode: out_buf must be int32 [>= {M}, {params.max_out}]")
-    if flags.dtype not in (torch.int16, torch.uint16) or not flags.is_contiguous():
-        raise ValueError("qa_decode: flags must be a contiguous 16-bit table")
+    if flags.dtype not in (torch.int32, torch.uint32) or not flags.is_contiguous():
+        raise ValueError("qa_decode: flags must be a contiguous 32-bit table (serving/qa.py qa_token_flags)")
     per = QA_NCLS + params.nf * (2 * params.n_pos + 1)
     if dbg_scores is not None and (dbg_scores.dtype != torch.float32 or dbg_scores.numel() < M * per):
         raise ValueError(f"qa_decode: dbg_scores must be fp32 [{M}, {per}]")

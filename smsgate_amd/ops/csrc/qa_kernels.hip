@@ -22,7 +22,9 @@
 //      ends with a digit ...), e followed by a word boundary.  Word boundary: NOT (a
 //      ends with a letter and b starts with one, or a ends with a digit and b starts
 //      with one), and a lone separator between a digit and a three-digit group joins
-//      them ("218" "," "993").  One lane per start, its ends scanned in order;
+//      them ("218" "," "993").  A date span with no time of day then takes the time
+//      token right before (else right after) it when that longer span is valid.
+//      One lane per start, its ends scanned in order;
 //      ties go to the lower start, then the lower end (serving/qa.py qa_decode_ref);
 //   4. the answer in the copy format (class tokens, <sep>, each field's body tokens
 //      and <sep>; a rejection class: only its tokens and <sep>) into out_buf.
@@ -47,6 +49,7 @@
 #define QF_LD 8192     // last char a digit
 #define QF_GRP3 16384  // exactly three ASCII digits
 #define QF_SEP 32768   // a lone "," "." "'"
+#define QF_TIME 65536  // a whole time of day (" 22:09")
 
 struct QAParams {
   int nf, nq, n_pos;
@@ -61,17 +64,48 @@ struct QAParams {
   int sep, max_out;
   int s_need[QA_MAX_NF];  // edge flags the first token must all have (serving/qa.py EDGE_RULES)
   int e_need[QA_MAX_NF];  // ... and the last token
+  int absorb[QA_MAX_NF];  // 1: a span without a time of day takes an adjacent one (dates)
 };
 
 static __device__ __forceinline__ float qa_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-static __device__ __forceinline__ bool qa_glued(int fa, int fb) {
+static __device__ __forceinline__ bool qa_glued(uint32_t fa, uint32_t fb) {
   return ((fa & QF_EL) && (fb & QF_SL)) || ((fa & QF_ED) && (fb & QF_SD));
+}
+
+// s may start a value of class bits `cls` with first-token edge flags `sneed`
+static __device__ __forceinline__ bool qa_start_ok(const uint32_t* fb, int s, int cls, int sneed) {
+  const uint32_t fs = fb[s];
+  bool ok = ((cls == 0) || (fs & cls)) && !(fs & QF_NL) && (fs & sneed) == (uint32_t)sneed;
+  if (ok && s > 0) {
+    const uint32_t fp = fb[s - 1];
+    ok = !qa_glued(fp, fs) && !((cls & QF_NO_START_AFTER_MASK) && (fp & QF_MASK)) &&
+         !(s > 1 && (fp & QF_SEP) && (fs & QF_GRP3) && (fb[s - 2] & QF_LD));
+  }
+  return ok;
+}
+
+// e may end a value (its own token already known in class): last-token edge flags and a
+// word boundary after it
+static __device__ __forceinline__ bool qa_end_ok(const uint32_t* fb, int n, int e, int eneed) {
+  const uint32_t fe = fb[e];
+  if ((fe & eneed) != (uint32_t)eneed) return false;
+  if (e + 1 < n) {
+    const uint32_t fn = fb[e + 1];
+    if (qa_glued(fe, fn)) return false;
+    if ((fe & QF_SEP) && (fn & QF_GRP3) && e > 0 && (fb[e - 1] & QF_LD)) return false;
+    if ((fe & QF_LD) && (fn & QF_SEP) && e + 2 < n && (fb[e + 2] & QF_GRP3)) return false;
+  }
+  return true;
+}
+
+static __device__ __forceinline__ bool qa_in_cls(uint32_t f, int cls) {
+  return ((cls == 0) || (f & cls)) && !(f & QF_NL);
 }
 
 __global__ void __launch_bounds__(256) qa_decode_kernel(
     QAParams p, const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ W, int H, float eps,
-    const int* __restrict__ cu, const int* __restrict__ ids, const uint16_t* __restrict__ flags, int V,
+    const int* __restrict__ cu, const int* __restrict__ ids, const uint32_t* __restrict__ flags, int V,
     int* __restrict__ out_buf, int* __restrict__ out_len, float* __restrict__ dbg_scores,
     int* __restrict__ dbg_spans) {
   extern __shared__ __attribute__((aligned(16))) uint16_t hq[];  // [nq][H] bf16
@@ -80,7 +114,7 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
   __shared__ float sc_end[QA_MAX_NF][QA_MAX_POS];
   __shared__ float sc_null[QA_MAX_NF];
   __shared__ float sc_cls[QA_NCLS];
-  __shared__ uint16_t fb[QA_MAX_POS];
+  __shared__ uint32_t fb[QA_MAX_POS];
   __shared__ int body[QA_MAX_POS];
   __shared__ int span_s[QA_MAX_NF], span_e[QA_MAX_NF];
   __shared__ int cls_sel;
@@ -102,7 +136,7 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
   for (int j = tid; j < n; j += 256) {
     const int t = ids[r0 + j];
     body[j] = t;
-    fb[j] = (t >= 0 && t < V) ? flags[t] : (uint16_t)0;
+    fb[j] = (t >= 0 && t < V) ? flags[t] : 0u;
   }
   __syncthreads();
   for (int q = wid; q < nq; q += 4) {
@@ -204,27 +238,13 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
     float best = -INFINITY;
     int bs = 0x7fffffff, be = -1;
     for (int s = lane; s < n; s += 64) {
-      const int fs = fb[s];
-      bool ok = ((cls == 0) || (fs & cls)) && !(fs & QF_NL) && (fs & sneed) == sneed;
-      if (ok && s > 0) {
-        const int fp = fb[s - 1];
-        ok = !qa_glued(fp, fs) && !((cls & QF_NO_START_AFTER_MASK) && (fp & QF_MASK)) &&
-             !(s > 1 && (fp & QF_SEP) && (fs & QF_GRP3) && (fb[s - 2] & QF_LD));
-      }
-      if (!ok) continue;
+      if (!qa_start_ok(fb, s, cls, sneed)) continue;
       const float ss = sc_start[f][s];
       top = fmaxf(top, ss);
       const int emax = min(n, s + cap);
       for (int e = s; e < emax; ++e) {
-        const int fe = fb[e];
-        if ((cls && !(fe & cls)) || (fe & QF_NL)) break;
-        if ((fe & eneed) != eneed) continue;
-        if (e + 1 < n) {
-          const int fn = fb[e + 1];
-          if (qa_glued(fe, fn)) continue;
-          if ((fe & QF_SEP) && (fn & QF_GRP3) && e > 0 && (fb[e - 1] & QF_LD)) continue;
-          if ((fe & QF_LD) && (fn & QF_SEP) && e + 2 < n && (fb[e + 2] & QF_GRP3)) continue;
-        }
+        if (!qa_in_cls(fb[e], cls)) break;
+        if (!qa_end_ok(fb, n, e, eneed)) continue;
         const float v = ss + sc_end[f][e];
         if (v > best) { best = v; bs = s; be = e; }  // strict: the lowest end of this start
       }
@@ -240,6 +260,17 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
     }
     if (lane == 0) {
       const bool null = be < 0 || !(top > sc_null[f]);
+      if (!null && p.absorb[f]) {
+        bool timed = false;
+        for (int j = bs; j <= be; ++j) timed |= (fb[j] & QF_TIME) != 0;
+        // the longer span must be a valid pair: start / end rules, in class, within the cap
+        if (!timed && bs > 0 && (fb[bs - 1] & QF_TIME) && be - bs + 1 < cap && qa_in_cls(fb[bs - 1], cls) &&
+            qa_start_ok(fb, bs - 1, cls, sneed))
+          bs -= 1;
+        else if (!timed && be + 1 < n && (fb[be + 1] & QF_TIME) && be - bs + 1 < cap && qa_in_cls(fb[be + 1], cls) &&
+                 qa_end_ok(fb, n, be + 1, eneed))
+          be += 1;
+      }
       span_s[f] = null ? -1 : bs;
       span_e[f] = null ? -1 : be;
     }
@@ -349,7 +380,7 @@ int sg_qa_decode(const void* params, const void* h, int ldh, const void* W, int 
   if (M == 0) return 0;
   const size_t lds = (size_t)p.nq * H * sizeof(uint16_t);
   hipLaunchKernelGGL(qa_decode_kernel, dim3(M), dim3(256), lds, stream, p, (const uint16_t*)h, ldh,
-                     (const uint16_t*)W, H, eps, cu, ids, (const uint16_t*)flags, V, out_buf, out_len,
+                     (const uint16_t*)W, H, eps, cu, ids, (const uint32_t*)flags, V, out_buf, out_len,
                      (float*)dbg_scores, (int*)dbg_spans);
   return (int)hipGetLastError();
 }

@@ -1,0 +1,273 @@
+// smsgate_amd — fused elementwise kernels of the extractor's TRAINING step (gfx950).
+//
+// The training forward (models/train_ops.py) is plain PyTorch around hipBLASLt GEMMs
+// and the SDPA flash kernels, but its elementwise glue was ~45 small kernels per layer
+// (RMSNorm as pow / mean / rsqrt / mul / mul / cast, rotate-half RoPE as slices / mul /
+// neg / cat per q and k, SiLU then mul), forward and backward: at the bench recipe
+// (128 x ~60 tokens) over half of a step's GPU time went to re-reading the same
+// activations between launches (scripts/train_step_profile.py).  These kernels do each
+// group in one pass, forward and backward:
+//
+//   rms_fwd     y = bf16(x * rsqrt(mean(x^2) + eps) * w), rstd saved      (fp32 x, w)
+//   rms_bwd     dx = r*(g) - x * r^3/H * sum(g*x) with g = dy*w;  dw partials per block
+//   rope_split  qkv [R, (nh+2nkv)*D] -> q [B,nh,T,D], k, v [B,nkv,T,D] (rotate-half RoPE on
+//               q and k in fp32 from the caller's cos / sin tables), and its adjoint
+//               (rotation by -theta) from dq / dk / dv back to dqkv
+//   swiglu      a = bf16(silu(g) * u) on gu = [gate | up], and dgu from da
+//
+// One wave (64 lanes) per row for the norms (H <= 1024: 4 float4 per lane in
+// registers); 8 bf16 per thread (16-B accesses) for SwiGLU; one lane per output element
+// for RoPE.  fp32 arithmetic throughout, one rounding per stored bf16.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+__device__ __forceinline__ float tk_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ uint16_t tk_f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+constexpr int RMS_MAXC = 4;  // float4 chunks per lane: H <= 64 * 4 * 4 = 1024
+
+__global__ void __launch_bounds__(256) rms_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                      uint16_t* __restrict__ y, float* __restrict__ rstd, int R,
+                                                      int H, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const int nc = H >> 2;
+  const float4* xr = reinterpret_cast<const float4*>(x + (size_t)row * H);
+  float4 v[RMS_MAXC];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < RMS_MAXC; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < nc ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    ss = fmaf(v[i].x, v[i].x, fmaf(v[i].y, v[i].y, fmaf(v[i].z, v[i].z, fmaf(v[i].w, v[i].w, ss))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float r = rsqrtf(ss / (float)H + eps);
+  if (lane == 0) rstd[row] = r;
+  const float4* wr = reinterpret_cast<const float4*>(w);
+  uint2* yr = reinterpret_cast<uint2*>(y + (size_t)row * H);
+#pragma unroll
+  for (int i = 0; i < RMS_MAXC; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nc) {
+      const float4 g = wr[c];
+      yr[c] = make_uint2((uint32_t)tk_f2bf(v[i].x * r * g.x) | ((uint32_t)tk_f2bf(v[i].y * r * g.y) << 16),
+                         (uint32_t)tk_f2bf(v[i].z * r * g.z) | ((uint32_t)tk_f2bf(v[i].w * r * g.w) << 16));
+    }
+  }
+}
+
+// Rows [blockIdx.x * rpb, +rpb) of dx; the block's dw partial (sum over its rows of
+// dy * x * r) into dw_part[blockIdx.x][H].
+__global__ void __launch_bounds__(256) rms_bwd_kernel(const uint16_t* __restrict__ dy, const float* __restrict__ x,
+                                                      const float* __restrict__ w, const float* __restrict__ rstd,
+                                                      float* __restrict__ dx, float* __restrict__ dw_part, int R,
+                                                      int H, int rpb) {
+  __shared__ float4 red[4][64 * RMS_MAXC];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = H >> 2;
+  const float4* wr = reinterpret_cast<const float4*>(w);
+  float4 wv[RMS_MAXC], acc[RMS_MAXC];
+#pragma unroll
+  for (int i = 0; i < RMS_MAXC; ++i) {
+    const int c = lane + 64 * i;
+    wv[i] = c < nc ? wr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int r0 = blockIdx.x * rpb, r1 = min(R, r0 + rpb);
+  for (int row = r0 + wave; row < r1; row += 4) {
+    const float4* xr = reinterpret_cast<const float4*>(x + (size_t)row * H);
+    const uint2* dr = reinterpret_cast<const uint2*>(dy + (size_t)row * H);
+    const float r = rstd[row];
+    float4 xv[RMS_MAXC], gv[RMS_MAXC];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < RMS_MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc) {
+        xv[i] = xr[c];
+        const uint2 u = dr[c];
+        const float d0 = tk_bf2f((uint16_t)(u.x & 0xffffu)), d1 = tk_bf2f((uint16_t)(u.x >> 16));
+        const float d2 = tk_bf2f((uint16_t)(u.y & 0xffffu)), d3 = tk_bf2f((uint16_t)(u.y >> 16));
+        gv[i] = make_float4(d0 * wv[i].x, d1 * wv[i].y, d2 * wv[i].z, d3 * wv[i].w);
+        dot = fmaf(gv[i].x, xv[i].x, fmaf(gv[i].y, xv[i].y, fmaf(gv[i].z, xv[i].z, fmaf(gv[i].w, xv[i].w, dot))));
+        acc[i].x = fmaf(d0 * r, xv[i].x, acc[i].x);
+        acc[i].y = fmaf(d1 * r, xv[i].y, acc[i].y);
+        acc[i].z = fmaf(d2 * r, xv[i].z, acc[i].z);
+        acc[i].w = fmaf(d3 * r, xv[i].w, acc[i].w);
+      } else {
+        xv[i] = gv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 64);
+    const float k = r * r * r * dot / (float)H;
+    float4* dxr = reinterpret_cast<float4*>(dx + (size_t)row * H);
+#pragma unroll
+    for (int i = 0; i < RMS_MAXC; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nc)
+        dxr[c] = make_float4(r * gv[i].x - k * xv[i].x, r * gv[i].y - k * xv[i].y, r * gv[i].z - k * xv[i].z,
+                             r * gv[i].w - k * xv[i].w);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RMS_MAXC; ++i) red[wave][lane + 64 * i] = acc[i];
+  __syncthreads();
+  float4* dp = reinterpret_cast<float4*>(dw_part + (size_t)blockIdx.x * H);
+  for (int c = threadIdx.x; c < nc; c += 256) {
+    const float4 a = red[0][c], b = red[1][c], e = red[2][c], f = red[3][c];
+    dp[c] = make_float4((a.x + b.x) + (e.x + f.x), (a.y + b.y) + (e.y + f.y), (a.z + b.z) + (e.z + f.z),
+                        (a.w + b.w) + (e.w + f.w));
+  }
+}
+
+// One block of 64 x 4 threads per (row, 4 heads): lane j of a wave is output element j
+// of head (blockIdx.y * 4 + wave) of row blockIdx.x.  dir = +1 forward (qkv -> q/k/v),
+// -1 the adjoint (dq/dk/dv -> dqkv).
+template <int DIR>
+__global__ void __launch_bounds__(256) rope_split_kernel(uint16_t* __restrict__ qkv, uint16_t* __restrict__ q,
+                                                         uint16_t* __restrict__ k, uint16_t* __restrict__ v,
+                                                         const float* __restrict__ cos_t,
+                                                         const float* __restrict__ sin_t, int T, int nh, int nkv) {
+  constexpr int D = 64, HD = 32;
+  const int row = blockIdx.x, wave = threadIdx.x >> 6, j = threadIdx.x & 63;
+  const int hh = blockIdx.y * 4 + wave;
+  const int NH = nh + 2 * nkv;
+  if (hh >= NH) return;
+  const int b = row / T, t = row - b * T;
+  uint16_t* src = qkv + (size_t)row * NH * D + hh * D;
+  uint16_t* dst;
+  bool rot = true;
+  if (hh < nh) {
+    dst = q + (((size_t)b * nh + hh) * T + t) * D;
+  } else if (hh < nh + nkv) {
+    dst = k + (((size_t)b * nkv + (hh - nh)) * T + t) * D;
+  } else {
+    dst = v + (((size_t)b * nkv + (hh - nh - nkv)) * T + t) * D;
+    rot = false;
+  }
+  if (!rot) {
+    if (DIR > 0) dst[j] = src[j];
+    else src[j] = dst[j];
+    return;
+  }
+  const int jj = j & (HD - 1);
+  const float c = cos_t[t * HD + jj], s = sin_t[t * HD + jj];
+  if (DIR > 0) {
+    const float x1 = tk_bf2f(src[jj]), x2 = tk_bf2f(src[jj + HD]);
+    dst[j] = tk_f2bf(j < HD ? x1 * c - x2 * s : x2 * c + x1 * s);
+  } else {  // adjoint: rotation by -theta
+    const float d1 = tk_bf2f(dst[jj]), d2 = tk_bf2f(dst[jj + HD]);
+    src[j] = tk_f2bf(j < HD ? d1 * c + d2 * s : d2 * c - d1 * s);
+  }
+}
+
+__device__ __forceinline__ float tk_sigmoid(float g) { return __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
+
+// gu [R, 2I] = [gate | up]; 8 elements per thread
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ a,
+                                                         int R, int I) {
+  const int per_row = I >> 3;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)R * per_row) return;
+  const int row = (int)(idx / per_row), c = (int)(idx - (long)row * per_row);
+  const uint4 g4 = *reinterpret_cast<const uint4*>(gu + (size_t)row * 2 * I + 8 * c);
+  const uint4 u4 = *reinterpret_cast<const uint4*>(gu + (size_t)row * 2 * I + I + 8 * c);
+  const uint32_t gw[4] = {g4.x, g4.y, g4.z, g4.w}, uw[4] = {u4.x, u4.y, u4.z, u4.w};
+  uint32_t ow[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float g0 = tk_bf2f((uint16_t)(gw[e] & 0xffffu)), g1 = tk_bf2f((uint16_t)(gw[e] >> 16));
+    const float u0 = tk_bf2f((uint16_t)(uw[e] & 0xffffu)), u1 = tk_bf2f((uint16_t)(uw[e] >> 16));
+    ow[e] = (uint32_t)tk_f2bf(g0 * tk_sigmoid(g0) * u0) | ((uint32_t)tk_f2bf(g1 * tk_sigmoid(g1) * u1) << 16);
+  }
+  *reinterpret_cast<uint4*>(a + (size_t)row * I + 8 * c) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+}
+
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restrict__ da,
+                                                         const uint16_t* __restrict__ gu,
+                                                         uint16_t* __restrict__ dgu, int R, int I) {
+  const int per_row = I >> 3;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)R * per_row) return;
+  const int row = (int)(idx / per_row), c = (int)(idx - (long)row * per_row);
+  const uint4 g4 = *reinterpret_cast<const uint4*>(gu + (size_t)row * 2 * I + 8 * c);
+  const uint4 u4 = *reinterpret_cast<const uint4*>(gu + (size_t)row * 2 * I + I + 8 * c);
+  const uint4 d4 = *reinterpret_cast<const uint4*>(da + (size_t)row * I + 8 * c);
+  const uint32_t gw[4] = {g4.x, g4.y, g4.z, g4.w}, uw[4] = {u4.x, u4.y, u4.z, u4.w}, dw[4] = {d4.x, d4.y, d4.z, d4.w};
+  uint32_t og[4], ou[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float gg[2], uu[2], dd[2], rg[2], ru[2];
+    gg[0] = tk_bf2f((uint16_t)(gw[e] & 0xffffu)); gg[1] = tk_bf2f((uint16_t)(gw[e] >> 16));
+    uu[0] = tk_bf2f((uint16_t)(uw[e] & 0xffffu)); uu[1] = tk_bf2f((uint16_t)(uw[e] >> 16));
+    dd[0] = tk_bf2f((uint16_t)(dw[e] & 0xffffu)); dd[1] = tk_bf2f((uint16_t)(dw[e] >> 16));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float s = tk_sigmoid(gg[h]);
+      rg[h] = dd[h] * uu[h] * s * (1.f + gg[h] * (1.f - s));
+      ru[h] = dd[h] * gg[h] * s;
+    }
+    og[e] = (uint32_t)tk_f2bf(rg[0]) | ((uint32_t)tk_f2bf(rg[1]) << 16);
+    ou[e] = (uint32_t)tk_f2bf(ru[0]) | ((uint32_t)tk_f2bf(ru[1]) << 16);
+  }
+  *reinterpret_cast<uint4*>(dgu + (size_t)row * 2 * I + 8 * c) = make_uint4(og[0], og[1], og[2], og[3]);
+  *reinterpret_cast<uint4*>(dgu + (size_t)row * 2 * I + I + 8 * c) = make_uint4(ou[0], ou[1], ou[2], ou[3]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int sg_rms_fwd(const void* x, const void* w, void* y, void* rstd, int R, int H, float eps, hipStream_t st) {
+  if (H % 4 || H > 64 * 4 * RMS_MAXC || R <= 0) return 1;
+  rms_fwd_kernel<<<dim3((R + 3) / 4), dim3(256), 0, st>>>((const float*)x, (const float*)w, (uint16_t*)y,
+                                                          (float*)rstd, R, H, eps);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int sg_rms_bwd(const void* dy, const void* x, const void* w, const void* rstd, void* dx, void* dw_part, int R,
+               int H, int rpb, hipStream_t st) {
+  if (H % 4 || H > 64 * 4 * RMS_MAXC || R <= 0 || rpb <= 0) return 1;
+  rms_bwd_kernel<<<dim3((R + rpb - 1) / rpb), dim3(256), 0, st>>>(
+      (const uint16_t*)dy, (const float*)x, (const float*)w, (const float*)rstd, (float*)dx, (float*)dw_part, R, H,
+      rpb);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int sg_rope_split(int dir, void* qkv, void* q, void* k, void* v, const void* cos_t, const void* sin_t, int B, int T,
+                  int nh, int nkv, int D, hipStream_t st) {
+  if (D != 64 || B <= 0 || T <= 0) return 1;
+  const dim3 grid(B * T, (nh + 2 * nkv + 3) / 4);
+  if (dir > 0)
+    rope_split_kernel<1><<<grid, dim3(256), 0, st>>>((uint16_t*)qkv, (uint16_t*)q, (uint16_t*)k, (uint16_t*)v,
+                                                     (const float*)cos_t, (const float*)sin_t, T, nh, nkv);
+  else
+    rope_split_kernel<-1><<<grid, dim3(256), 0, st>>>((uint16_t*)qkv, (uint16_t*)q, (uint16_t*)k, (uint16_t*)v,
+                                                      (const float*)cos_t, (const float*)sin_t, T, nh, nkv);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int sg_swiglu_fwd(const void* gu, void* a, int R, int I, hipStream_t st) {
+  if (I % 8 || R <= 0) return 1;
+  const long n = (long)R * (I / 8);
+  swiglu_fwd_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>((const uint16_t*)gu, (uint16_t*)a, R, I);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int sg_swiglu_bwd(const void* da, const void* gu, void* dgu, int R, int I, hipStream_t st) {
+  if (I % 8 || R <= 0) return 1;
+  const long n = (long)R * (I / 8);
+  swiglu_bwd_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>((const uint16_t*)da,
+                                                                             (const uint16_t*)gu, (uint16_t*)dgu, R, I);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // extern "C"

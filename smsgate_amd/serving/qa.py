@@ -30,7 +30,8 @@ the causal model lets every query row attend to the whole body:
   join a digit group to a lone separator and a three-digit group ("218" "," "993" is
   one word).  Value edges by kind (:data:`EDGE_RULES`): a number starts and ends with
   a digit, a card ends with one, a date or a free-text value starts and ends with a
-  letter or digit; no value crosses a line break.
+  letter or digit; no value crosses a line break.  A date span without a time of day
+  takes the time token right next to it ("22:09 13.02.2023": the value is a datetime).
 
 The answer is written in the copy format (txn tokens, then each field's body
 tokens, each ended by ``<sep>``), so the tokenizers' field decoders, the remote
@@ -39,6 +40,7 @@ reference of ``qa_decode_kernel`` (ops/csrc/qa_kernels.hip).
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -49,18 +51,21 @@ from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
            "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
-           "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP"]
+           "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP",
+           "QF_TIME"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
 QA_MAX_QUERIES = 24
-# per-token flags (uint16): starts / ends with a letter / digit, ends a card mask, class bits
+# per-token flags (uint32): starts / ends with a letter / digit, ends a card mask, class bits
 QF_SL, QF_SD, QF_EL, QF_ED, QF_MASK = 1, 2, 4, 8, 16
 QA_CLASS_BITS = {k: v << 3 for k, v in TOK_CLASS_BITS.items()}  # date 32, number 64, currency 128, card 256
 _NO_START_AFTER_MASK = QA_CLASS_BITS["date"] | QA_CLASS_BITS["number"]
 # edges: contains a line break; first non-space char a letter-or-digit / a digit; last
 # char a letter-or-digit / a digit; exactly three ASCII digits; a lone "," "." "'"
 QF_NL, QF_FA, QF_FD, QF_LA, QF_LD, QF_GRP3, QF_SEP = 512, 1024, 2048, 4096, 8192, 16384, 32768
+QF_TIME = 1 << 16  # a whole time of day: " 22:09", "05:27:11"
+_TIME_RE = re.compile(r" ?\d{1,2}:\d{2}(?::\d{2})?\Z")
 # field kind -> (flags its first token must all have, flags its last token must all have).
 # Every gold value of every training and held-out family obeys them (a free-text value
 # may start with a digit: "7-ELEVEN").
@@ -106,6 +111,10 @@ class QALayout:
         """Per copied field: (class bits, cap, first-token edge flags, last-token edge flags)."""
         return [(QA_CLASS_BITS.get(f.kind, 0), f.cap) + EDGE_RULES.get(f.kind, (0, 0)) for f in self.fields[1:]]
 
+    def absorb_time(self) -> List[bool]:
+        """Per copied field: a span without a time of day takes an adjacent one (dates)."""
+        return [f.kind == "date" for f in self.fields[1:]]
+
     def max_answer_tokens(self) -> int:
         return sum(f.cap for f in self.fields) + len(self.fields)
 
@@ -126,14 +135,14 @@ def qa_layout(vocab_tok: int = 8192, n_pos: int = 130, n_queries: int = 9,
 
 
 def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
-    """uint16 per id: QF_* letter / digit start / end bits, card-mask end, class bits."""
+    """uint32 per id: QF_* letter / digit start / end bits, card-mask end, class bits."""
     strings = tokenizer.token_strings
     specials = [tokenizer.pad, tokenizer.bos, tokenizer.eos, tokenizer.sep, tokenizer.sms, tokenizer.ans]
     classes = _token_class_sets(strings, specials)
-    out = np.zeros(vocab, dtype=np.uint16)
+    out = np.zeros(vocab, dtype=np.uint32)
     n = min(vocab, len(strings))
     for k, bit in QA_CLASS_BITS.items():
-        out[:n] |= np.where(classes[k][:n], bit, 0).astype(np.uint16)
+        out[:n] |= np.where(classes[k][:n], bit, 0).astype(np.uint32)
     spec = set(specials)
 
     def letter(ch: str) -> bool:
@@ -169,6 +178,8 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
             f |= QF_GRP3
         if t in (",", ".", "'"):
             f |= QF_SEP
+        if _TIME_RE.match(t):
+            f |= QF_TIME
         out[i] |= f
     return out
 
@@ -287,6 +298,18 @@ def _pair_mask(fb: np.ndarray, n: int, cls: int, cap: int, s_need: int = 0,
     return vs, pairs
 
 
+def _absorb_time(fb: np.ndarray, pairs: np.ndarray, a: int, z: int, n: int) -> Tuple[int, int]:
+    """A date span (a, z) with no time-of-day token takes the one right before it, else
+    the one right after it, when the longer span is itself a valid pair."""
+    if (fb[a:z + 1] & QF_TIME).any():
+        return a, z
+    if a > 0 and fb[a - 1] & QF_TIME and pairs[a - 1, z]:
+        return a - 1, z
+    if z + 1 < n and fb[z + 1] & QF_TIME and pairs[a, z + 1]:
+        return a, z + 1
+    return a, z
+
+
 def qa_decode_ref(cls_logits, start_logits, null_logits, end_logits, bodies: Sequence[Sequence[int]],
                   flags: np.ndarray, lay: QALayout) -> List[Tuple[int, List[Tuple[int, int]]]]:
     """Reference joint decode (host, numpy).  Per message ``m``: ``cls_logits[m]`` [4],
@@ -306,6 +329,7 @@ def qa_decode_ref(cls_logits, start_logits, null_logits, end_logits, bodies: Seq
         fb = flags[np.asarray(body[:n], dtype=np.int64)]
         spans: List[Tuple[int, int]] = []
         for f, (bits, cap, s_need, e_need) in enumerate(lay.rules()):
+            absorb = lay.absorb_time()
             st = np.asarray(start_logits[m][f][:n], dtype=np.float32)
             en = np.asarray(end_logits[m][f][:n], dtype=np.float32)
             vs, pairs = _pair_mask(fb, n, bits, cap, s_need, e_need)
@@ -314,7 +338,10 @@ def qa_decode_ref(cls_logits, start_logits, null_logits, end_logits, bodies: Seq
                 continue
             sc = np.where(pairs, st[:, None] + en[None, :], -np.inf)
             k = int(np.argmax(sc))
-            spans.append((k // n, k % n))
+            a, z = k // n, k % n
+            if absorb[f]:
+                a, z = _absorb_time(fb, pairs, a, z, n)
+            spans.append((a, z))
         out.append((c, spans))
     return out
 

@@ -92,7 +92,7 @@ class QAEngine(ExtractionEngine):
         self.fw_down = [w.down[i].contiguous() for i in range(mc.layers)]
         # the head's rows (start pointers .. class rows) with the final norm folded in
         self.w_qa = ops.fold_norm(w.embed[lay.ptr0:lay.cls0 + 4], w.ln_f)
-        self.flags_t = torch.from_numpy(qa_token_flags(tokenizer, lay.vocab).view(np.int16)).to(dev)
+        self.flags_t = torch.from_numpy(qa_token_flags(tokenizer, lay.vocab).view(np.int32)).to(dev)
         self.params = ops.qa_params(lay, tokenizer)
         self.max_out = lay.max_answer_tokens()
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)

@@ -139,6 +139,28 @@ def test_value_edges_follow_the_field_kind(env):
     assert "DUL ST. 108" in _spans_of(tk, fl, legacy, *rules["address"])
 
 
+@pytest.mark.parametrize("body,picked,want", [
+    ("Карта **3001 22:09 13.02.2023 покупка на сумму 186379.01 RUB", "13.02.2023", "22:09 13.02.2023"),
+    ("Оплата 13.02.2023 22:09 на сумму 5.00 RUB", "13.02.2023", "13.02.2023 22:09"),
+    ("Оплата 13.02.2023 22:09 на сумму 5.00 RUB", "13.02.2023 22:09", "13.02.2023 22:09"),
+    ("Оплата 13.02.2023 на сумму 5.00 RUB", "13.02.2023", "13.02.2023"),
+])
+def test_date_span_takes_the_adjacent_time(env, body, picked, want):
+    """A date span without a time of day takes the time token next to it (the r05 error
+    analysis: ru_karta_first's "22:09 13.02.2023" decoded as the date alone)."""
+    tk, lay, fl = env
+    ids, offs = tk.encode_offsets([body])[0]
+    m = ids + [tk.ans]
+    a, z = tk.value_span(picked, body, ids, offs)
+    cl = np.array([5.0, -5, -5, -5])
+    st, en, nl = np.full((8, 130), -5.0), np.full((8, 130), -5.0), np.full(8, 10.0)
+    nl[0] = -10.0  # only the date is non-null
+    st[0, a], en[0, z] = 5.0, 5.0
+    (c, spans), = qa_decode_ref([cl], [st], [nl], [en], [m], fl, lay)
+    s0, e0 = spans[0]
+    assert "".join(tk.token_strings[t] for t in m[s0:e0 + 1]).strip() == want
+
+
 def test_strict_boundaries_win_over_glued_occurrences(env):
     """The relaxed (letter | digit) rule is a fallback: a number inside a merchant name
     never shadows the real amount for the training targets."""

@@ -95,7 +95,7 @@ def test_qa_decode_kernel_matches_reference(tk, nq):
     per = 4 + lay.n_copy * (2 * lay.n_pos + 1)
     dbg = torch.zeros(M, per, dtype=torch.float32, device="cuda")
     spans = torch.zeros(M, 1 + 2 * lay.n_copy, dtype=torch.int32, device="cuda")
-    ops.qa_decode(h, W, eps, cu, ids, torch.from_numpy(flags.view(np.int16)).cuda(), p, out, olen, dbg, spans)
+    ops.qa_decode(h, W, eps, cu, ids, torch.from_numpy(flags.view(np.int32)).cuda(), p, out, olen, dbg, spans)
     torch.cuda.synchronize()
     ref = _ref_scores(h, W, eps, cu, nq, lay)
     fin = torch.isfinite(ref)

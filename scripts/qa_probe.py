@@ -38,7 +38,13 @@ def main() -> int:
     p.add_argument("--model", default="smollm-135m")
     p.add_argument("--out", default="gpurun_out/qa_probe.jsonl")
     p.add_argument("--save-dir", default="")
+    p.add_argument("--variants", default="",
+                   help="';'-separated training variants of the FIRST format, each 'key=value,...' over steps, "
+                        "negatives, lr, fused, proc (procedural family weight, SMSGATE_PROC_WEIGHT); e.g. "
+                        "'steps=4000;steps=6000;proc=6'")
     a = p.parse_args()
+    if a.variants:
+        return _variants(a)
 
     from smsgate_amd.models.train import ExamplePool, TrainConfig
 
@@ -91,6 +97,49 @@ def main() -> int:
         with open(a.out, "a") as fh:
             fh.write(line + "\n")
         del eng, w
+        torch.cuda.empty_cache()
+    return 0
+
+
+def _variants(a) -> int:
+    """One format, several training recipes, each trained and scored like main()."""
+    import torch
+
+    from smsgate_amd.models.evaluate import TorchQAExtractor, evaluate_engine, evaluate_negatives
+    from smsgate_amd.models.train import ExamplePool, TrainConfig, train_extractor
+
+    fmt = a.formats.split(",")[0]
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    for spec in a.variants.split(";"):
+        kv = dict(x.split("=") for x in spec.split(",") if x)
+        steps = int(kv.get("steps", a.steps))
+        neg = float(kv.get("negatives", a.negatives))
+        if "proc" in kv:
+            os.environ["SMSGATE_PROC_WEIGHT"] = kv["proc"]
+        else:
+            os.environ.pop("SMSGATE_PROC_WEIGHT", None)
+        t0 = time.time()
+        data = ExamplePool(steps * a.batch, seed=0, families="train", workers=12, answer_format=fmt,
+                           negatives=neg).get()
+        tc = TrainConfig(model=a.model, steps=steps, batch=a.batch, lr=float(kv.get("lr", a.lr)),
+                         n_examples=steps * a.batch, log_every=1000, data_parallel=False, families="train",
+                         answer_format=fmt, negatives=neg, fused=bool(int(kv.get("fused", 1))))
+        t1 = time.time()
+        w = train_extractor(tc, device="cuda", data=data, log=lambda s: print(f"[{spec}] {s}", flush=True))
+        res = {"format": fmt, "variant": spec, "steps": steps, "negatives": neg, "data_s": round(t1 - t0, 1),
+               "train_s": round(time.time() - t1, 1)}
+        eng = TorchQAExtractor(w, batch=256)
+        for name, fam in (("heldout_formats", "heldout"), ("train_formats", "train"),
+                          ("heldout_values", "heldout_values")):
+            q = evaluate_engine(eng, n=a.eval_n, seed=4243, vocab_name="heldout", families=fam)
+            res[name] = {"exact": round(q["exact"], 4), "parse_rate": round(q["parse_rate"], 4),
+                         "by_family": q.get("by_family")}
+        res["negatives_heldout"] = evaluate_negatives(eng, n=a.eval_n, families="neg_heldout")
+        line = json.dumps(res)
+        print(line, flush=True)
+        with open(a.out, "a") as fh:
+            fh.write(line + "\n")
+        del eng, w, data
         torch.cuda.empty_cache()
     return 0
 

@@ -86,8 +86,8 @@ def main() -> int:
             lambda h=h, r=resid, s=sso, c=c_dn: ops.gemm(h, w_down, epi="resid", resid=r, cfg=c, ss_out=s),
             2.0 * M * H * I, 2 * (M * I + H * I + 2 * M * H))
         cases[f"qkv_rope_{tag}_M{M}_cfg{c_q}"] = (
-            lambda x=x, pos=pos, slot=slot, q=q_out, c=c_q: ops.gemm_qkv_rope(
-                x, w_qkv, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, P0, cfg=c, ss_in=ss),
+            lambda x=x, pos=pos, slot=slot, q=q_out, c=c_q, s=ss: ops.gemm_qkv_rope(
+                x, w_qkv, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, P0, cfg=c, ss_in=s),
             2.0 * M * NQKV * H, 2 * (M * H + NQKV * H + M * NQKV))
 
     # speculative verify attention: B rows, nd pseudo-rows each (mean decode_m / B), own keys ~ own

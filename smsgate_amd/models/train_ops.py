@@ -22,7 +22,9 @@ losses and gradients).  CPU / no-library: reference_forward.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 from typing import Optional
 
 import torch
@@ -169,11 +171,30 @@ def fused_forward(w: ExtractorWeights, ids: torch.Tensor, add_ids: Optional[torc
     cos, sin = _rope_tables(T, D, cfg.rope_theta, ids.device)
     cos, sin = cos.reshape(T, D // 2).contiguous(), sin.reshape(T, D // 2).contiguous()
     scale = 1.0 / math.sqrt(D)
-    for i in range(cfg.layers):
-        h = rms_norm(x, w.ln1[i], cfg.eps)
-        q, k, v = rope_split(h @ w.qkv[i].t(), cos, sin, nh, nkv)
-        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale, enable_gqa=nh != nkv)
-        x = x + a.transpose(1, 2).reshape(B, T, nh * D) @ w.o[i].t()
-        h = rms_norm(x, w.ln2[i], cfg.eps)
-        x = x + swiglu(h @ w.gate_up[i].t()) @ w.down[i].t()
+    with _sdpa_backend():
+        for i in range(cfg.layers):
+            x = _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D)
     return rms_norm(x, w.ln_f, cfg.eps)
+
+
+def _sdpa_backend():
+    """SMSGATE_TRAIN_SDPA = flash | efficient | math pins SDPA's backend (A/B of the
+    training step, scripts/train_step_profile.py); default: PyTorch's choice."""
+    name = os.environ.get("SMSGATE_TRAIN_SDPA", "")
+    if not name:
+        return contextlib.nullcontext()
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+
+    return sdpa_kernel({"flash": SDPBackend.FLASH_ATTENTION, "efficient": SDPBackend.EFFICIENT_ATTENTION,
+                        "math": SDPBackend.MATH}[name])
+
+
+def _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D):
+    """One decoder layer of the residual stream ``x`` (fp32)."""
+    eps = w.cfg.eps
+    h = rms_norm(x, w.ln1[i], eps)
+    q, k, v = rope_split(h @ w.qkv[i].t(), cos, sin, nh, nkv)
+    a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale, enable_gqa=nh != nkv)
+    x = x + a.transpose(1, 2).reshape(B, T, nh * D) @ w.o[i].t()
+    h = rms_norm(x, w.ln2[i], eps)
+    return x + swiglu(h @ w.gate_up[i].t()) @ w.down[i].t()

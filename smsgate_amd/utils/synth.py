@@ -34,6 +34,7 @@ pipeline under test.  :func:`generate` is deterministic for a seed.
 """
 from __future__ import annotations
 
+import os
 import random
 import zlib
 from dataclasses import dataclass, field
@@ -1090,7 +1091,9 @@ def generate(n: int, seed: int = 0, unique: bool = True, vocab_name: str = "trai
     neg_names: Tuple[str, ...] = ()
     if families is not None:
         names = family_names(families)
-        weights = [(_LEGACY_WEIGHT if f in LEGACY_FAMILIES else _PROC_WEIGHT if f.startswith("proc_") else 1)
+        # SMSGATE_PROC_WEIGHT: training-mix experiments (scripts/qa_probe.py --variants)
+        pw = int(os.environ.get("SMSGATE_PROC_WEIGHT", _PROC_WEIGHT))
+        weights = [(_LEGACY_WEIGHT if f in LEGACY_FAMILIES else pw if f.startswith("proc_") else 1)
                    if len(names) > 3 else 1 for f in names]
         if negatives > 0:
             if not isinstance(families, str) or families not in _NEG_OF:

@@ -25,6 +25,8 @@ def main() -> int:
     p.add_argument("--qa-max-tokens", type=int, default=262144)
     p.add_argument("--split-prefill", type=int, default=8192)
     p.add_argument("--request", type=int, default=512)
+    p.add_argument("--packed", type=int, default=1, choices=[0, 1],
+                   help="1: each request one engine unit (submit_packed, the engine server's path)")
     a = p.parse_args()
 
     import numpy as np
@@ -46,6 +48,7 @@ def main() -> int:
     bodies = [normalize_body(s.body) for s in generate_traffic(a.n, seed=1, traffic="formats")]
     ids = [np.asarray(x, dtype=np.int32) for x in tok.message_ids(bodies, 128)]
     tokens = sum(len(x) for x in ids) / len(ids)
+    lens = np.asarray([len(x) for x in ids], dtype=np.int32)
 
     def run_once() -> float:
         torch.cuda.synchronize()
@@ -54,10 +57,15 @@ def main() -> int:
         k = 0
         while done < len(ids):
             # keep ~8 requests waiting, like 8 parser processes with one request in flight each
-            while k < len(ids) and len(eng.waiting) < 8 * a.request:
-                eng.submit_ids([(i, ids[i]) for i in range(k, min(k + a.request, len(ids)))])
+            while k < len(ids) and len(eng.waiting) < (8 if a.packed else 8 * a.request):
+                part = range(k, min(k + a.request, len(ids)))
+                if a.packed:
+                    eng.submit_packed(k, lens[part.start:part.stop], np.concatenate([ids[i] for i in part]))
+                else:
+                    eng.submit_ids([(i, ids[i]) for i in part])
                 k += a.request
-            done += len(eng.step(raw=True))
+            out = eng.step(raw=True)
+            done += sum(len(v.lens) for _, v in out) if a.packed else len(out)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
@@ -71,7 +79,7 @@ def main() -> int:
            "batches": st.steps, "msgs_per_batch": round(st.prefill_seqs / max(1, st.steps), 1),
            "gpu_idle_s": round(st.gpu_idle_s, 4), "host_prefill_s": round(st.prefill_s, 3),
            "harvest_wait_s": round(st.harvest_wait_s, 3),
-           "config": {"max_slots": a.max_slots, "qa_max_tokens": a.qa_max_tokens, "split_prefill": a.split_prefill}}
+           "config": {"packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": a.qa_max_tokens, "split_prefill": a.split_prefill}}
     print(json.dumps(out), flush=True)
     return 0
 

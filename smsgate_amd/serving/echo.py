@@ -1,7 +1,9 @@
 """CPU stand-in for :class:`~smsgate_amd.serving.engine.ExtractionEngine` with the
 same serving surface (``submit_ids`` / ``step(raw=True)`` / ``busy`` / ``stats``).
 
-Answers every prompt with the token ids of the fake backend's canned answer.
+Answers every prompt with the token ids of the fake backend's canned answer.  With
+``packed`` (default) it also takes whole wire requests (``submit_packed``) and answers
+them as one :class:`~smsgate_amd.serving.protocol.PackedAnswer`, like the qa engine.
 Used to exercise the replica / distributed harness end to end without a GPU
 (``bench.py --cpu-echo-engine`` under ``torch.distributed.run`` with gloo, and
 the multi-process tests); it is never a fallback for the GPU engine.
@@ -24,7 +26,7 @@ class _Stats:
 
 
 class EchoEngine:
-    def __init__(self, per_step: int = 300) -> None:
+    def __init__(self, per_step: int = 300, packed: bool = True) -> None:
         from ..models.tokenizer import load_tokenizer
         from ..parse.backends.fake import DEFAULT_ANSWER
         from .fsm import DEFAULT_FIELDS
@@ -34,8 +36,10 @@ class EchoEngine:
         for f in DEFAULT_FIELDS:
             toks += tk.encode(DEFAULT_ANSWER[f.name]) + [tk.sep]
         self.answer = np.asarray(toks, dtype=np.int32)
-        self.waiting: List[Tuple[Any, Sequence[int]]] = []
+        self.waiting: List[Tuple[Any, Any]] = []
         self.per_step = per_step
+        if not packed:
+            self.submit_packed = None  # shadows the method: the engine server's per-message path
         self.seen = 0
         self.stats = _Stats()
 
@@ -45,9 +49,22 @@ class EchoEngine:
     def busy(self) -> bool:
         return bool(self.waiting)
 
+    def submit_packed(self, key: Any, lens, ids) -> None:
+        self.waiting.append((key, ("packed", len(lens))))
+
     def step(self, raw: bool = True):
-        out = [(k, self.answer) for k, _ in self.waiting[: self.per_step]]
+        from .protocol import PackedAnswer
+
+        out = []
+        for k, v in self.waiting[: self.per_step]:
+            if isinstance(v, tuple) and v and v[0] == "packed":
+                n = v[1]
+                out.append((k, PackedAnswer(np.full(n, len(self.answer), dtype=np.uint16), np.tile(self.answer, n))))
+                self.seen += n
+                self.stats.completed += n
+            else:
+                out.append((k, self.answer))
+                self.seen += 1
+                self.stats.completed += 1
         del self.waiting[: self.per_step]
-        self.seen += len(out)
-        self.stats.completed += len(out)
         return out

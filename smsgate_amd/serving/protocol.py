@@ -15,11 +15,12 @@ from __future__ import annotations
 import itertools
 import json
 import struct
+from dataclasses import dataclass
 from typing import Any, List, Sequence, Tuple
 
 import numpy as np
 
-__all__ = ["pack_ids", "pack_raw", "unpack_ids", "unpack_id_arrays", "pack_error", "pack_control", "kind", "req_id",
+__all__ = ["pack_ids", "pack_raw", "unpack_ids", "unpack_id_arrays", "unpack_arrays", "PackedAnswer", "pack_error", "pack_control", "kind", "req_id",
            "count", "HEADER_SIZE"]
 
 _HDR = struct.Struct("<cQI")
@@ -78,6 +79,25 @@ def unpack_id_arrays(buf: bytes) -> Tuple[bytes, int, List[np.ndarray]]:
     # swapaxes per sub-array) on the GPU feeder's loop
     ends = np.cumsum(lens, dtype=np.int64).tolist()
     return tag, req_id, [flat[a:b] for a, b in zip([0] + ends[:-1], ends)]
+
+
+@dataclass
+class PackedAnswer:
+    """Answers of a whole request (an engine's ``submit_packed`` unit): copy-format token
+    lengths (uint16 [n]) and the ids back to back (int32) -- a response frame's arrays."""
+    lens: np.ndarray
+    flat: np.ndarray
+
+
+def unpack_arrays(buf: bytes) -> Tuple[bytes, int, np.ndarray, np.ndarray]:
+    """``(tag, req_id, lens int32 [n], ids int32 [sum(lens)])``: a frame as two arrays
+    (a copy of the ids; the engine's packed-request path)."""
+    tag, req_id, n = _HDR.unpack_from(buf, 0)
+    off = _HDR.size
+    lens = np.frombuffer(buf, dtype=np.uint16, count=n, offset=off).astype(np.int32)
+    off += 2 * n
+    flat = np.frombuffer(buf, dtype=np.int32, count=int(lens.sum()), offset=off).copy()
+    return tag, req_id, lens, flat
 
 
 def pack_error(req_id: int, msg: str) -> bytes:

@@ -22,7 +22,10 @@ batch's ``i``-th sequence.
 Same interface as the span engine for :class:`~smsgate_amd.serving.remote.EngineServer`
 and :class:`~smsgate_amd.serving.worker.EngineWorker`: ``submit_ids`` / ``submit_many``,
 ``step(raw)`` returning ``(key, answer)`` or ``(key, copy-format token array)``,
-``busy``, ``run``, ``stats``.
+``busy``, ``run``, ``stats``.  Plus :meth:`submit_packed`: a whole wire request (uint16
+lengths + int32 ids) queued as ONE unit and answered as one :class:`PackedAnswer`, so
+the engine server's Python work per request is a handful of numpy calls, not a few
+objects and slices per message.
 """
 from __future__ import annotations
 
@@ -40,15 +43,25 @@ from ..models.tokenizer import ExtractorTokenizer
 from ..parse.schema import EXTRACTOR_PROMPT
 from .engine import EngineConfig, EngineStats, ExtractionEngine, _PinnedRing, _round_up
 from .fsm import DEFAULT_FIELDS
+from .protocol import PackedAnswer
 from .qa import null_rejection, qa_layout, qa_token_flags
 
-__all__ = ["QAEngine"]
+__all__ = ["QAEngine", "PackedAnswer"]
+
+
+@dataclass
+class _Unit:
+    """Queued work: one message (``packed`` False: ``submit_ids``) or a whole request."""
+    key: Any
+    lens: np.ndarray  # int32 [n] prompt lengths (capped)
+    flat: np.ndarray  # int32 [sum(lens)] prompt ids
+    packed: bool
 
 
 @dataclass
 class _Batch:
     n: int
-    keys: List[Any]
+    units: List[_Unit]
     event: Any
     start_event: Any
     bufs: Dict[str, torch.Tensor]
@@ -129,13 +142,12 @@ class QAEngine(ExtractionEngine):
         self._compute_prefix()
 
     # ---------------------------------------------------------------- batches
-    def _forward_part(self, items: List[Any], r0: int) -> int:
-        """Prefill + head of ``items`` into KV slots / output rows ``r0 ..``; returns the
-        tokens computed."""
+    def _forward_part(self, lens: np.ndarray, ids: np.ndarray, r0: int) -> int:
+        """Prefill + head of the messages ``lens`` / ``ids`` (int32, back to back) into KV
+        slots / output rows ``r0 ..``; returns the tokens computed."""
         mc, lay, dev = self.mc, self.lay, self.device
-        n = len(items)
+        n = len(lens)
         NQ = self.NQ
-        lens = np.fromiter((len(it.ids) for it in items), dtype=np.int32, count=n)
         tl = lens + NQ
         T = int(tl.sum())
         cu = np.zeros(n + 1, dtype=np.int32)
@@ -145,7 +157,7 @@ class QAEngine(ExtractionEngine):
         in_msg = pos < np.repeat(lens, tl)
         # one concatenation of the messages, the query ids written around them
         flat = np.empty(T, dtype=np.int32)
-        flat[in_msg] = np.concatenate([np.asarray(it.ids, dtype=np.int32) for it in items])
+        flat[in_msg] = ids
         flat[~in_msg] = np.tile(self.qids, n)
         add = np.where(in_msg, lay.ptr0 + pos, -1).astype(np.int32)
         seq_slot = np.arange(r0, r0 + n, dtype=np.int32)
@@ -173,42 +185,70 @@ class QAEngine(ExtractionEngine):
                       self.out_len[r0:])
         return T
 
+    def submit_ids(self, items) -> None:
+        """Queue pre-tokenised prompts (``body <ans>`` ids), one unit per message."""
+        cap = self.cfg.max_body_tokens + 2
+        for k, ids in items:
+            a = np.asarray(ids, dtype=np.int32)
+            if len(a) > cap:  # keep the closing <ans>
+                a = np.concatenate([a[: cap - 1], a[-1:]])
+            self.waiting.append(_Unit(k, np.asarray([len(a)], dtype=np.int32), a, False))
+
+    def submit_packed(self, key: Any, lens: np.ndarray, ids: np.ndarray) -> None:
+        """Queue a whole request (wire lengths / ids); answered by :meth:`step` as
+        ``(key, PackedAnswer)``.  Prompts over ``max_body_tokens + 2`` keep their first
+        ``max_body_tokens + 1`` ids and their closing ``<ans>``."""
+        lens = np.asarray(lens, dtype=np.int32)
+        ids = np.asarray(ids, dtype=np.int32)
+        cap = self.cfg.max_body_tokens + 2
+        if len(lens) and int(lens.max()) > cap:
+            ends = np.cumsum(lens)
+            keep = np.ones(len(ids), dtype=bool)
+            for i in np.nonzero(lens > cap)[0].tolist():
+                a, b = int(ends[i] - lens[i]), int(ends[i])
+                keep[a + cap - 1:b - 1] = False
+            ids, lens = ids[keep], np.minimum(lens, cap)
+        self.waiting.append(_Unit(key, lens, ids, True))
+
     def _launch(self) -> Optional[_Batch]:
         ec = self.cfg
-        items: List[Any] = []
-        ntok = 0
+        units: List[_Unit] = []
+        n = ntok = 0
         S = ec.max_slots
-        cap = ec.max_body_tokens + 2
-        while self.waiting and len(items) < S:
-            it = self.waiting[0]
-            if len(it.ids) > cap:  # keep the closing <ans> (submit_ids cuts already)
-                it.ids = list(it.ids[: cap - 1]) + [it.ids[-1]]
-            t = len(it.ids) + self.NQ
-            if items and ntok + t > self.max_tokens:
+        while self.waiting:
+            u = self.waiting[0]
+            m, t = len(u.lens), int(u.lens.sum()) + self.NQ * len(u.lens)
+            if units and (n + m > S or ntok + t > self.max_tokens):
                 break
+            if m > S or t > self.max_tokens:
+                raise ValueError(f"a request of {m} prompts / {t} tokens exceeds the engine's batch "
+                                 f"({S} slots, {self.max_tokens} tokens)")
             self.waiting.popleft()
-            items.append(it)
+            units.append(u)
+            n += m
             ntok += t
-        if not items:
+        if not units:
             return None
         t0 = time.perf_counter()
         start_ev = None
         if ec.measure_idle:
             start_ev = torch.cuda.Event(enable_timing=True)
             start_ev.record()
-        n = len(items)
+        lens = np.concatenate([u.lens for u in units]) if len(units) > 1 else units[0].lens
+        ids = np.concatenate([u.flat for u in units]) if len(units) > 1 else units[0].flat
         split = ec.split_prefill
         if split and ntok >= split and n >= 2:
             h = n // 2
+            o = int(lens[:h].sum())
             main = torch.cuda.current_stream(self.device)
             s2 = self._side_stream()
             s2.wait_stream(main)
-            T = self._forward_part(items[:h], 0)
+            T = self._forward_part(lens[:h], ids[:o], 0)
             with torch.cuda.stream(s2):
-                T += self._forward_part(items[h:], h)
+                T += self._forward_part(lens[h:], ids[o:], h)
             main.wait_stream(s2)
         else:
-            T = self._forward_part(items, 0)
+            T = self._forward_part(lens, ids, 0)
         hb = self._host_bufs[self._flip]
         self._flip ^= 1
         hb["len"][:n].copy_(self.out_len[:n], non_blocking=True)
@@ -219,7 +259,7 @@ class QAEngine(ExtractionEngine):
         st.prefill_tokens += T
         st.prefill_seqs += n
         st.prefill_s += time.perf_counter() - t0
-        return _Batch(n, [it.key for it in items], ev, start_ev, hb)
+        return _Batch(n, units, ev, start_ev, hb)
 
     def _harvest_batch(self, b: _Batch, raw: bool) -> List[Tuple[Any, Any]]:
         t0 = time.perf_counter()
@@ -227,13 +267,25 @@ class QAEngine(ExtractionEngine):
         self.stats.harvest_wait_s += time.perf_counter() - t0
         lens = b.bufs["len"][: b.n].numpy().copy()
         blk = b.bufs["buf"][: b.n].numpy().copy()  # the pinned buffer is reused two batches on
-        if raw:
-            res = [(k, blk[i, : lens[i]]) for i, k in enumerate(b.keys)]
-        else:
-            names = [f.name for f in DEFAULT_FIELDS]
-            rows = self.tok.decode_fields([blk[i, : lens[i]].tolist() for i in range(b.n)], len(names))
-            res = [(k, null_rejection(dict(zip(names, vals)))) for k, vals in zip(b.keys, rows)]
-        self.stats.completed += len(res)
+        res: List[Tuple[Any, Any]] = []
+        names = [f.name for f in DEFAULT_FIELDS]
+        single: List[Tuple[Any, int]] = []
+        r = 0
+        for u in b.units:
+            m = len(u.lens)
+            if u.packed:
+                ln = lens[r:r + m]
+                keep = np.arange(blk.shape[1])[None, :] < ln[:, None]
+                res.append((u.key, PackedAnswer(ln.astype(np.uint16), blk[r:r + m][keep])))
+            elif raw:
+                res.append((u.key, blk[r, : lens[r]]))
+            else:
+                single.append((u.key, r))
+            r += m
+        if single:
+            rows = self.tok.decode_fields([blk[i, : lens[i]].tolist() for _, i in single], len(names))
+            res += [(k, null_rejection(dict(zip(names, vals)))) for (k, _), vals in zip(single, rows)]
+        self.stats.completed += b.n
         self.stats.harvest_s += time.perf_counter() - t0
         return res
 

@@ -19,15 +19,17 @@ from __future__ import annotations
 import asyncio
 import itertools
 import queue
+import selectors
 import threading
 import time
 from dataclasses import dataclass, field
-from multiprocessing.connection import Connection, wait
+from multiprocessing.connection import Connection
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import numpy as np
 
 from . import protocol as P
+from .protocol import PackedAnswer
 from .qa import null_rejection
 
 __all__ = ["EngineServer", "RemoteEngineClient"]
@@ -49,10 +51,26 @@ class EngineServer:
         self.on_control = on_control
         self.reqs: Dict[tuple, _Req] = {}
         self.served = 0
+        self._packed = callable(getattr(engine, "submit_packed", None))
+        # one persistent selector over the live connections (multiprocessing's wait()
+        # builds and tears down a selector per call: ~3 us per message of the poll loop)
+        self._sel = selectors.DefaultSelector()
+        for i, c in enumerate(self.conns):
+            self._sel.register(c, selectors.EVENT_READ, i)
 
     def add_connection(self, conn: Connection) -> int:
         self.conns.append(conn)
+        self._sel.register(conn, selectors.EVENT_READ, len(self.conns) - 1)
         return len(self.conns) - 1
+
+    def _drop(self, idx: int) -> None:
+        c = self.conns[idx]
+        self.conns[idx] = None
+        if c is not None:
+            try:
+                self._sel.unregister(c)
+            except (KeyError, ValueError, OSError):
+                pass
 
     def send_control(self, idx: int, obj: Any) -> None:
         c = self.conns[idx]
@@ -72,21 +90,29 @@ class EngineServer:
                 st.server_poll_s += time.perf_counter() - t0
 
     def _poll(self, timeout: Optional[float]) -> None:
-        live = self._live()
-        if not live:
+        if not self._sel.get_map():
             if timeout:
                 time.sleep(min(timeout, 0.01))
             return
-        for c in wait(live, timeout):
-            idx = self.conns.index(c)
+        for key, _ in self._sel.select(timeout):
+            idx, c = key.data, key.fileobj
             while True:
                 try:
                     buf = c.recv_bytes()
                 except (EOFError, OSError):
-                    self.conns[idx] = None
+                    self._drop(idx)
                     break
                 k = P.kind(buf)
                 if k == b"Q":
+                    if self._packed:  # the whole request is one engine unit (QAEngine.submit_packed)
+                        _, rid, lens, flat = P.unpack_arrays(buf)
+                        if not len(lens):
+                            c.send_bytes(P.pack_ids(b"R", rid, []))
+                        else:
+                            self.engine.submit_packed((idx, rid), lens, flat)
+                        if not c.poll():
+                            break
+                        continue
                     _, rid, seqs = P.unpack_id_arrays(buf)
                     if not seqs:
                         c.send_bytes(P.pack_ids(b"R", rid, []))
@@ -102,7 +128,12 @@ class EngineServer:
         try:
             finished = self.engine.step(raw=True)
         except Exception as exc:  # fail every waiting request loudly
-            for (idx, rid), _ in list(self.reqs.items()):
+            keys = list(self.reqs)
+            if self._packed:  # whole requests queued / in flight in the engine
+                pend = getattr(self.engine, "_pending", None)
+                units = list(self.engine.waiting) + list(getattr(pend, "units", None) or [])
+                keys += [u.key for u in units if getattr(u, "packed", False)]
+            for idx, rid in keys:
                 c = self.conns[idx]
                 if c is not None:
                     c.send_bytes(P.pack_error(rid, repr(exc)))
@@ -112,7 +143,15 @@ class EngineServer:
             self.engine._pending = None
             raise
         t0 = time.perf_counter()
-        for (idx, rid, i), toks in finished:
+        for key, toks in finished:
+            if isinstance(toks, PackedAnswer):  # a whole request: its response frame as is
+                idx, rid = key
+                c = self.conns[idx]
+                if c is not None:
+                    c.send_bytes(P.pack_arrays(b"R", rid, toks.lens, toks.flat))
+                self.served += len(toks.lens)
+                continue
+            idx, rid, i = key
             r = self.reqs.get((idx, rid))
             if r is None:
                 continue
@@ -165,12 +204,14 @@ class EngineServer:
             self.serve_until(pred)
         finally:
             listener.close()
-            for c in self._live():  # clients see EOF (and reconnect to the next server)
+            for i, c in enumerate(self.conns):  # clients see EOF (and reconnect to the next server)
+                if c is None:
+                    continue
+                self._drop(i)
                 try:
                     c.close()
                 except OSError:
                     pass
-            self.conns = [None] * len(self.conns)
 
 
 class RemoteEngineClient:

@@ -161,6 +161,41 @@ def test_qa_engine_batches_split_and_pipelined(tk, small_qa):
     assert a == b == c
 
 
+def test_qa_engine_packed_requests_match_per_message_answers(tk, small_qa):
+    """submit_packed (the engine server's path: a whole wire request as one unit) gives
+    the per-message path's answers, request by request, including an over-long prompt."""
+    from smsgate_amd.serving.engine import EngineConfig
+    from smsgate_amd.serving.protocol import PackedAnswer
+    from smsgate_amd.serving.qa_engine import QAEngine
+
+    bodies = [normalize_body(s.body) for s in synth.generate(900, seed=13, vocab_name="heldout", families="all",
+                                                             negatives=0.1)]
+    bodies[5] = bodies[5] + " ПОДРОБНЕЕ" * 80  # > max_body_tokens: cut, <ans> kept
+    ids = tk.message_ids(bodies, 10_000)
+    cfg = EngineConfig(max_slots=1024, qa_max_tokens=40000, split_prefill=2048)
+    e1 = QAEngine(small_qa, tk, cfg)
+    e1.submit_ids(list(enumerate(ids)))
+    per = {}
+    while e1.busy():
+        per.update((k, v.tolist()) for k, v in e1.step(raw=True))
+    e2 = QAEngine(small_qa, tk, cfg)
+    reqs = [(r, list(range(a, min(a + 256, len(ids))))) for r, a in enumerate(range(0, len(ids), 256))]
+    for r, idx in reqs:
+        e2.submit_packed(r, np.asarray([len(ids[i]) for i in idx], dtype=np.int32),
+                         np.concatenate([np.asarray(ids[i], dtype=np.int32) for i in idx]))
+    got = {}
+    while e2.busy():
+        for k, v in e2.step(raw=True):
+            assert isinstance(v, PackedAnswer)
+            got[k] = v
+    for r, idx in reqs:
+        v = got[r]
+        ends = np.cumsum(v.lens.astype(np.int64))
+        for j, i in enumerate(idx):
+            assert v.flat[ends[j] - v.lens[j]:ends[j]].tolist() == per[i], i
+    assert e2.stats.completed == len(ids)
+
+
 def test_qa_negatives_reach_the_dlq(tk, small_qa, arun):
     """Non-transactions through local_llm (the qa engine behind the backend interface)
     and the parser stage land in sms.failed as {"reason": "unmatched"}, not in

@@ -445,3 +445,38 @@ def test_handler_timeout_is_isolated_not_retried_forever(arun):
     st, info, dlq = arun(go())
     assert st.dead_lettered == 1 and st.transient_errors == 0 and len(dlq) == 1
     assert info.num_pending == 0 and info.num_ack_pending == 0
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_engine_server_packed_and_per_message_paths(tmp_path, packed, arun):
+    """The engine server answers a wire request either as ONE engine unit (engines with
+    ``submit_packed``: QAEngine) or message by message; the client sees the same answers."""
+    import threading
+    from multiprocessing.connection import Client
+
+    from smsgate_amd.serving.echo import EchoEngine
+    from smsgate_amd.serving.remote import EngineServer, RemoteEngineClient
+
+    path = str(tmp_path / "engine.sock")
+    stop = threading.Event()
+    srv = EngineServer(EchoEngine(packed=packed))
+    assert srv._packed is packed
+    th = threading.Thread(target=srv.serve_listener, args=(path, stop), daemon=True)
+    th.start()
+    for _ in range(200):
+        if (tmp_path / "engine.sock").exists():
+            break
+        threading.Event().wait(0.01)
+
+    async def go():
+        client = RemoteEngineClient(connector=lambda: Client(path, family="AF_UNIX"))
+        try:
+            return await client.extract([f"Paid {i}.00 USD at SHOP {i}" for i in range(37)]), await client.extract([])
+        finally:
+            stop.set()
+
+    got, empty = arun(go())
+    th.join(5)
+    assert empty == [] and len(got) == 37
+    assert all(g == got[0] for g in got) and got[0]["merchant"]
+    assert srv.served == 37

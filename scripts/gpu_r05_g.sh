@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 5: GEMM tile sweep at the qa engine's prefill-half shapes, then one bench with
+# the CPU sampling profile of every process (parser workers + rank).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r05g
+mkdir -p $O
+timeout -k 10 300 python -u scripts/gemm_tune.py --rows 110592,55296 --rounds 2 --inner 8 > $O/gemm_tune.json \
+  2> $O/gemm_tune.err || { echo "gemm_tune rc=$?"; tail -20 $O/gemm_tune.err; exit 1; }
+cat $O/gemm_tune.json
+timeout -k 10 900 python -u bench.py --steps 10 --warmup 2 --profile-cpu $O/sprof ${BENCH_ARGS} \
+  > $O/bench.json 2> $O/bench.err || { echo "bench failed rc=$?"; tail -40 $O/bench.err; exit 1; }
+python scripts/samples_top.py $O/sprof --bench $O/bench.json -n 40 > $O/samples_top.txt
+tail -c 1500 $O/bench.json

@@ -21,7 +21,12 @@ from decimal import Decimal
 from enum import Enum
 from typing import Literal, Optional
 
-from pydantic import BaseModel, Field, field_serializer, field_validator
+from pydantic import BaseModel, Field, StringConstraints, field_serializer
+from typing_extensions import Annotated
+
+# upper-cased by pydantic-core itself (the reference's validator, `v.upper() if v else v`,
+# as a Python callback cost a GIL round trip inside every Rust validation)
+_UpperStr = Annotated[str, StringConstraints(to_upper=True)]
 
 __all__ = [
     "TxnType",
@@ -70,7 +75,7 @@ class ParsedSMS(BaseModel):
 
     txn_type: TxnType
     amount: Optional[Decimal] = None
-    currency: Optional[str] = None
+    currency: Optional[_UpperStr] = None
     card: Optional[str] = Field(None, min_length=4, max_length=4)
 
     merchant: Optional[str] = None
@@ -81,15 +86,8 @@ class ParsedSMS(BaseModel):
 
     parser_version: str = "0.1.0"
 
-    @field_validator("currency")
-    @classmethod
-    def _currency_upper(cls, v: Optional[str]) -> Optional[str]:
-        return v.upper() if v else v
-
-    @field_serializer("amount", "balance", when_used="json")
-    def _dec_str(self, v: Optional[Decimal]) -> Optional[str]:
-        return None if v is None else str(v)
-
+    # amount / balance: pydantic-core's JSON form of a Decimal is str(v), the reference's
+    # serializer (libs/models.py), so no Python callback per field
     @field_serializer("date", when_used="json")
     def _iso(self, v: _dt.datetime) -> str:
         return v.isoformat()

@@ -88,25 +88,25 @@ class _RMSNorm(torch.autograd.Function):
 
 class _RopeSplit(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nh: int, nkv: int):
+    def forward(ctx, qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nh: int, nkv: int, rep: int):
         B, T, N = qkv.shape
         D = N // (nh + 2 * nkv)
         if qkv.dtype != torch.bfloat16 or D != 64 or N != (nh + 2 * nkv) * D:
             raise ValueError("rope_split: bf16 [B, T, (nh + 2 nkv) * 64]")
         qkv = qkv.contiguous()
         q = torch.empty(B, nh, T, D, dtype=qkv.dtype, device=qkv.device)
-        k = torch.empty(B, nkv, T, D, dtype=qkv.dtype, device=qkv.device)
-        v = torch.empty(B, nkv, T, D, dtype=qkv.dtype, device=qkv.device)
+        k = torch.empty(B, nkv * rep, T, D, dtype=qkv.dtype, device=qkv.device)
+        v = torch.empty(B, nkv * rep, T, D, dtype=qkv.dtype, device=qkv.device)
         _ok(_lib().sg_rope_split(1, qkv.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), cos.data_ptr(),
-                                 sin.data_ptr(), B, T, nh, nkv, D, _st()), "rope_split")
+                                 sin.data_ptr(), B, T, nh, nkv, D, rep, _st()), "rope_split")
         ctx.save_for_backward(cos, sin)
-        ctx.dims = (B, T, nh, nkv, D)
+        ctx.dims = (B, T, nh, nkv, D, rep)
         return q, k, v
 
     @staticmethod
     def backward(ctx, dq, dk, dv):
         cos, sin = ctx.saved_tensors
-        B, T, nh, nkv, D = ctx.dims
+        B, T, nh, nkv, D, rep = ctx.dims
         dev = cos.device
 
         def _g(t, h):
@@ -114,11 +114,11 @@ class _RopeSplit(torch.autograd.Function):
                 return torch.zeros(B, h, T, D, dtype=torch.bfloat16, device=dev)
             return t.to(torch.bfloat16).contiguous()
 
-        dq, dk, dv = _g(dq, nh), _g(dk, nkv), _g(dv, nkv)
+        dq, dk, dv = _g(dq, nh), _g(dk, nkv * rep), _g(dv, nkv * rep)
         dqkv = torch.empty(B, T, (nh + 2 * nkv) * D, dtype=torch.bfloat16, device=dev)
         _ok(_lib().sg_rope_split(-1, dqkv.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), cos.data_ptr(),
-                                 sin.data_ptr(), B, T, nh, nkv, D, _st()), "rope_split_bwd")
-        return dqkv, None, None, None, None
+                                 sin.data_ptr(), B, T, nh, nkv, D, rep, _st()), "rope_split_bwd")
+        return dqkv, None, None, None, None, None
 
 
 class _SwiGLU(torch.autograd.Function):
@@ -149,8 +149,9 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     return _RMSNorm.apply(x, w, eps)
 
 
-def rope_split(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nh: int, nkv: int):
-    return _RopeSplit.apply(qkv, cos, sin, nh, nkv)
+def rope_split(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, nh: int, nkv: int, rep: int = 1):
+    """q [B, nh, T, D], k / v [B, nkv * rep, T, D] (``rep`` copies of each kv head)."""
+    return _RopeSplit.apply(qkv, cos, sin, nh, nkv, rep)
 
 
 def swiglu(gu: torch.Tensor) -> torch.Tensor:
@@ -171,9 +172,12 @@ def fused_forward(w: ExtractorWeights, ids: torch.Tensor, add_ids: Optional[torc
     cos, sin = _rope_tables(T, D, cfg.rope_theta, ids.device)
     cos, sin = cos.reshape(T, D // 2).contiguous(), sin.reshape(T, D // 2).contiguous()
     scale = 1.0 / math.sqrt(D)
+    # grouped-query attention inside SDPA (flash); the efficient backend has no GQA
+    # support, so it gets k / v expanded to nh heads by rope_split (its adjoint sums them)
+    rep = nh // nkv if os.environ.get("SMSGATE_TRAIN_SDPA", "") == "efficient" else 1
     with _sdpa_backend():
         for i in range(cfg.layers):
-            x = _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D)
+            x = _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep)
     return rms_norm(x, w.ln_f, cfg.eps)
 
 
@@ -189,12 +193,12 @@ def _sdpa_backend():
                         "math": SDPBackend.MATH}[name])
 
 
-def _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D):
+def _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep=1):
     """One decoder layer of the residual stream ``x`` (fp32)."""
     eps = w.cfg.eps
     h = rms_norm(x, w.ln1[i], eps)
-    q, k, v = rope_split(h @ w.qkv[i].t(), cos, sin, nh, nkv)
-    a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale, enable_gqa=nh != nkv)
+    q, k, v = rope_split(h @ w.qkv[i].t(), cos, sin, nh, nkv, rep)
+    a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale, enable_gqa=nh != nkv * rep)
     x = x + a.transpose(1, 2).reshape(B, T, nh * D) @ w.o[i].t()
     h = rms_norm(x, w.ln2[i], eps)
     return x + swiglu(h @ w.gate_up[i].t()) @ w.down[i].t()

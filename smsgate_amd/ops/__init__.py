@@ -155,7 +155,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     # training step (csrc/train_kernels.hip, models/train_ops.py)
     lib.sg_rms_fwd.argtypes = [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_float, _vp]
     lib.sg_rms_bwd.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp]
-    lib.sg_rope_split.argtypes = [_c_int, _vp, _vp, _vp, _vp, _vp, _vp] + [_c_int] * 5 + [_vp]
+    lib.sg_rope_split.argtypes = [_c_int, _vp, _vp, _vp, _vp, _vp, _vp] + [_c_int] * 6 + [_vp]
     lib.sg_swiglu_fwd.argtypes = [_vp, _vp, _c_int, _c_int, _vp]
     lib.sg_swiglu_bwd.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _vp]
     for fn in (lib.sg_rms_fwd, lib.sg_rms_bwd, lib.sg_rope_split, lib.sg_swiglu_fwd, lib.sg_swiglu_bwd):

@@ -11,8 +11,9 @@
 //   rms_fwd     y = bf16(x * rsqrt(mean(x^2) + eps) * w), rstd saved      (fp32 x, w)
 //   rms_bwd     dx = r*(g) - x * r^3/H * sum(g*x) with g = dy*w;  dw partials per block
 //   rope_split  qkv [R, (nh+2nkv)*D] -> q [B,nh,T,D], k, v [B,nkv,T,D] (rotate-half RoPE on
-//               q and k in fp32 from the caller's cos / sin tables), and its adjoint
-//               (rotation by -theta) from dq / dk / dv back to dqkv
+//               q and k in fp32 from the caller's cos / sin tables; optionally k / v
+//               expanded to nh heads), and its adjoint (rotation by -theta, expanded
+//               copies summed) from dq / dk / dv back to dqkv
 //   swiglu      a = bf16(silu(g) * u) on gu = [gate | up], and dgu from da
 //
 // One wave (64 lanes) per row for the norms (H <= 1024: 4 float4 per lane in
@@ -130,12 +131,15 @@ __global__ void __launch_bounds__(256) rms_bwd_kernel(const uint16_t* __restrict
 
 // One block of 64 x 4 threads per (row, 4 heads): lane j of a wave is output element j
 // of head (blockIdx.y * 4 + wave) of row blockIdx.x.  dir = +1 forward (qkv -> q/k/v),
-// -1 the adjoint (dq/dk/dv -> dqkv).
+// -1 the adjoint (dq/dk/dv -> dqkv).  rep > 1 writes k / v expanded to nh heads (each kv
+// head `rep` times: SDPA backends without grouped-query support), whose adjoint sums
+// the rep copies' gradients.
 template <int DIR>
 __global__ void __launch_bounds__(256) rope_split_kernel(uint16_t* __restrict__ qkv, uint16_t* __restrict__ q,
                                                          uint16_t* __restrict__ k, uint16_t* __restrict__ v,
                                                          const float* __restrict__ cos_t,
-                                                         const float* __restrict__ sin_t, int T, int nh, int nkv) {
+                                                         const float* __restrict__ sin_t, int T, int nh, int nkv,
+                                                         int rep) {
   constexpr int D = 64, HD = 32;
   const int row = blockIdx.x, wave = threadIdx.x >> 6, j = threadIdx.x & 63;
   const int hh = blockIdx.y * 4 + wave;
@@ -143,29 +147,47 @@ __global__ void __launch_bounds__(256) rope_split_kernel(uint16_t* __restrict__ 
   if (hh >= NH) return;
   const int b = row / T, t = row - b * T;
   uint16_t* src = qkv + (size_t)row * NH * D + hh * D;
+  const int kvh = nkv * rep;  // heads of the k / v outputs
   uint16_t* dst;
+  size_t hstride = (size_t)T * D;  // between consecutive heads of one batch row
+  int copies = 1;
   bool rot = true;
   if (hh < nh) {
     dst = q + (((size_t)b * nh + hh) * T + t) * D;
   } else if (hh < nh + nkv) {
-    dst = k + (((size_t)b * nkv + (hh - nh)) * T + t) * D;
+    dst = k + (((size_t)b * kvh + (hh - nh) * rep) * T + t) * D;
+    copies = rep;
   } else {
-    dst = v + (((size_t)b * nkv + (hh - nh - nkv)) * T + t) * D;
+    dst = v + (((size_t)b * kvh + (hh - nh - nkv) * rep) * T + t) * D;
+    copies = rep;
     rot = false;
   }
-  if (!rot) {
-    if (DIR > 0) dst[j] = src[j];
-    else src[j] = dst[j];
-    return;
-  }
   const int jj = j & (HD - 1);
-  const float c = cos_t[t * HD + jj], s = sin_t[t * HD + jj];
   if (DIR > 0) {
-    const float x1 = tk_bf2f(src[jj]), x2 = tk_bf2f(src[jj + HD]);
-    dst[j] = tk_f2bf(j < HD ? x1 * c - x2 * s : x2 * c + x1 * s);
-  } else {  // adjoint: rotation by -theta
-    const float d1 = tk_bf2f(dst[jj]), d2 = tk_bf2f(dst[jj + HD]);
-    src[j] = tk_f2bf(j < HD ? d1 * c + d2 * s : d2 * c - d1 * s);
+    float o;
+    if (rot) {
+      const float c = cos_t[t * HD + jj], s = sin_t[t * HD + jj];
+      const float x1 = tk_bf2f(src[jj]), x2 = tk_bf2f(src[jj + HD]);
+      o = j < HD ? x1 * c - x2 * s : x2 * c + x1 * s;
+    } else {
+      o = tk_bf2f(src[j]);
+    }
+    const uint16_t ob = tk_f2bf(o);
+    for (int r = 0; r < copies; ++r) dst[r * hstride + j] = ob;
+  } else {  // adjoint: sum of the copies' gradients, then rotation by -theta
+    if (rot) {
+      const float c = cos_t[t * HD + jj], s = sin_t[t * HD + jj];
+      float d1 = 0.f, d2 = 0.f;
+      for (int r = 0; r < copies; ++r) {
+        d1 += tk_bf2f(dst[r * hstride + jj]);
+        d2 += tk_bf2f(dst[r * hstride + jj + HD]);
+      }
+      src[j] = tk_f2bf(j < HD ? d1 * c + d2 * s : d2 * c - d1 * s);
+    } else {
+      float d = 0.f;
+      for (int r = 0; r < copies; ++r) d += tk_bf2f(dst[r * hstride + j]);
+      src[j] = tk_f2bf(d);
+    }
   }
 }
 
@@ -243,15 +265,15 @@ int sg_rms_bwd(const void* dy, const void* x, const void* w, const void* rstd, v
 }
 
 int sg_rope_split(int dir, void* qkv, void* q, void* k, void* v, const void* cos_t, const void* sin_t, int B, int T,
-                  int nh, int nkv, int D, hipStream_t st) {
-  if (D != 64 || B <= 0 || T <= 0) return 1;
+                  int nh, int nkv, int D, int rep, hipStream_t st) {
+  if (D != 64 || B <= 0 || T <= 0 || rep < 1) return 1;
   const dim3 grid(B * T, (nh + 2 * nkv + 3) / 4);
   if (dir > 0)
     rope_split_kernel<1><<<grid, dim3(256), 0, st>>>((uint16_t*)qkv, (uint16_t*)q, (uint16_t*)k, (uint16_t*)v,
-                                                     (const float*)cos_t, (const float*)sin_t, T, nh, nkv);
+                                                     (const float*)cos_t, (const float*)sin_t, T, nh, nkv, rep);
   else
     rope_split_kernel<-1><<<grid, dim3(256), 0, st>>>((uint16_t*)qkv, (uint16_t*)q, (uint16_t*)k, (uint16_t*)v,
-                                                      (const float*)cos_t, (const float*)sin_t, T, nh, nkv);
+                                                      (const float*)cos_t, (const float*)sin_t, T, nh, nkv, rep);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

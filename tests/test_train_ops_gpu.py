@@ -36,7 +36,10 @@ def test_rms_norm_forward_backward():
     assert _rel(wa.grad, wr.grad) < 1e-4
 
 
-def test_rope_split_forward_backward():
+@pytest.mark.parametrize("rep", [1, 3])
+def test_rope_split_forward_backward(rep):
+    """rep = 3: k / v expanded to the 9 query heads (repeat_interleave order), the
+    adjoint summing the copies' gradients."""
     from smsgate_amd.models import train_ops
     from smsgate_amd.models.extractor import _rope, _rope_tables
 
@@ -46,7 +49,7 @@ def test_rope_split_forward_backward():
     cos, sin = _rope_tables(T, D, 100000.0, dev)
     c2, s2 = cos.reshape(T, D // 2).contiguous(), sin.reshape(T, D // 2).contiguous()
     qa = qkv.clone().requires_grad_()
-    q, k, v = train_ops.rope_split(qa, c2, s2, nh, nkv)
+    q, k, v = train_ops.rope_split(qa, c2, s2, nh, nkv, rep)
     gq, gk, gv = (torch.randn_like(t) for t in (q, k, v))
     (q.float() * gq.float()).sum().add((k.float() * gk.float()).sum()).add((v.float() * gv.float()).sum()).backward()
     qr_in = qkv.float().clone().requires_grad_()
@@ -54,6 +57,7 @@ def test_rope_split_forward_backward():
     qr = _rope(a.reshape(B, T, nh, D), cos, sin).transpose(1, 2)
     kr = _rope(b.reshape(B, T, nkv, D), cos, sin).transpose(1, 2)
     vr = c.reshape(B, T, nkv, D).transpose(1, 2)
+    kr, vr = kr.repeat_interleave(rep, dim=1), vr.repeat_interleave(rep, dim=1)
     (qr * gq.float()).sum().add((kr * gk.float()).sum()).add((vr * gv.float()).sum()).backward()
     for got, want in ((q, qr), (k, kr), (v, vr)):
         assert got.shape == want.shape and _rel(got, want) < 5e-3
@@ -78,9 +82,12 @@ def test_swiglu_forward_backward():
     assert _rel(ga.grad, gr.grad) < 5e-3
 
 
-def test_fused_forward_matches_reference_forward():
+@pytest.mark.parametrize("sdpa", ["", "efficient"])
+def test_fused_forward_matches_reference_forward(sdpa, monkeypatch):
     """Loss and every gradient of the fused training forward agree with
-    reference_forward's (both bf16 autocast over fp32 master weights)."""
+    reference_forward's (both bf16 autocast over fp32 master weights); also with the
+    efficient SDPA backend on expanded k / v."""
+    monkeypatch.setenv("SMSGATE_TRAIN_SDPA", sdpa)
     from smsgate_amd.models import train_ops
     from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, reference_forward
 

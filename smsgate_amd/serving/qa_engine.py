@@ -185,6 +185,12 @@ class QAEngine(ExtractionEngine):
                       self.out_len[r0:])
         return T
 
+    def submit_many(self, items) -> None:
+        """Queue ``(key, body)`` pairs (tokenised here), one unit per message."""
+        if items:
+            self.submit_ids(list(zip((k for k, _ in items),
+                                     self.tok.message_ids([b for _, b in items], self.cfg.max_body_tokens))))
+
     def submit_ids(self, items) -> None:
         """Queue pre-tokenised prompts (``body <ans>`` ids), one unit per message."""
         cap = self.cfg.max_body_tokens + 2

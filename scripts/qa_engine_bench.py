@@ -23,7 +23,7 @@ def main() -> int:
     p.add_argument("--queries", type=int, default=9)
     p.add_argument("--max-slots", type=int, default=8192)
     p.add_argument("--qa-max-tokens", type=int, default=262144)
-    p.add_argument("--split-prefill", type=int, default=8192)
+    p.add_argument("--split-prefill", type=int, default=0, help="EngineConfig.qa_split_prefill")
     p.add_argument("--request", type=int, default=512)
     p.add_argument("--packed", type=int, default=1, choices=[0, 1],
                    help="1: each request one engine unit (submit_packed, the engine server's path)")
@@ -44,7 +44,7 @@ def main() -> int:
     w = ExtractorWeights(cfg, device="cuda", seed=0)
     w.requires_grad_(False)
     eng = QAEngine(w, tok, EngineConfig(max_slots=a.max_slots, qa_max_tokens=a.qa_max_tokens,
-                                        split_prefill=a.split_prefill))
+                                        qa_split_prefill=a.split_prefill))
     bodies = [normalize_body(s.body) for s in generate_traffic(a.n, seed=1, traffic="formats")]
     ids = [np.asarray(x, dtype=np.int32) for x in tok.message_ids(bodies, 128)]
     tokens = sum(len(x) for x in ids) / len(ids)
@@ -79,7 +79,7 @@ def main() -> int:
            "batches": st.steps, "msgs_per_batch": round(st.prefill_seqs / max(1, st.steps), 1),
            "gpu_idle_s": round(st.gpu_idle_s, 4), "host_prefill_s": round(st.prefill_s, 3),
            "harvest_wait_s": round(st.harvest_wait_s, 3),
-           "config": {"packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": a.qa_max_tokens, "split_prefill": a.split_prefill}}
+           "config": {"packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": a.qa_max_tokens, "qa_split_prefill": a.split_prefill}}
     print(json.dumps(out), flush=True)
     return 0
 

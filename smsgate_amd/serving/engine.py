@@ -145,6 +145,10 @@ class EngineConfig:
     # qa-format models (serving/qa_engine.py): token budget of one packed prefill batch
     # (messages + their query tokens; max_slots caps the sequences)
     qa_max_tokens: int = 262144
+    # qa engine: a batch of >= this many tokens runs as two halves on two streams; 0 =
+    # one prefill (profiles/r05_qa_split_ab.jsonl: 64.5 k msgs/s either way at the
+    # ~220 k-row batches, so one stream, whose kernel times are not inflated by sharing)
+    qa_split_prefill: int = 0
 
 
 @dataclass

@@ -14,9 +14,10 @@ reads the message, so serving it is a pipeline of packed prefill batches:
            constrained span decode, copy-format answer) -> async D2H of the answers
     host   harvest the PREVIOUS batch (its event) while this one runs
 
-A batch of >= ``split_prefill`` tokens runs as two halves on two streams (disjoint KV
-slots and output rows), so one half's attention overlaps the other's GEMMs, as in the
-span engine's prefill.  The KV cache only lives for the batch: slot ``i`` is the
+With ``qa_split_prefill`` > 0 a batch of that many tokens or more runs as two halves on
+two streams (disjoint KV slots and output rows), one half's attention overlapping the
+other's GEMMs as in the span engine's prefill; off by default (the ~220 k-row batches
+fill the GPU alone: profiles/r05_qa_split_ab.jsonl).  The KV cache only lives for the batch: slot ``i`` is the
 batch's ``i``-th sequence.
 
 Same interface as the span engine for :class:`~smsgate_amd.serving.remote.EngineServer`
@@ -242,7 +243,7 @@ class QAEngine(ExtractionEngine):
             start_ev.record()
         lens = np.concatenate([u.lens for u in units]) if len(units) > 1 else units[0].lens
         ids = np.concatenate([u.flat for u in units]) if len(units) > 1 else units[0].flat
-        split = ec.split_prefill
+        split = ec.qa_split_prefill
         if split and ntok >= split and n >= 2:
             h = n // 2
             o = int(lens[:h].sum())

@@ -136,7 +136,7 @@ def test_qa_engine_matches_torch_reference(tk, small_qa):
     from smsgate_amd.serving.engine import EngineConfig
     from smsgate_amd.serving.qa_engine import QAEngine
 
-    eng = QAEngine(small_qa, tk, EngineConfig(max_slots=512, qa_max_tokens=8192, split_prefill=4096))
+    eng = QAEngine(small_qa, tk, EngineConfig(max_slots=512, qa_max_tokens=8192, qa_split_prefill=4096))
     items = synth.generate(600, seed=11, vocab_name="heldout", families="all", negatives=0.1)
     bodies = [normalize_body(s.body) for s in items]
     got = eng.run(bodies)
@@ -155,9 +155,9 @@ def test_qa_engine_batches_split_and_pipelined(tk, small_qa):
 
     bodies = [normalize_body(s.body) for s in synth.generate(700, seed=12, vocab_name="heldout", families="all",
                                                              negatives=0.1)]
-    a = QAEngine(small_qa, tk, EngineConfig(max_slots=1024, qa_max_tokens=1 << 18, split_prefill=0)).run(bodies)
-    b = QAEngine(small_qa, tk, EngineConfig(max_slots=1024, qa_max_tokens=1 << 18, split_prefill=2048)).run(bodies)
-    c = QAEngine(small_qa, tk, EngineConfig(max_slots=64, qa_max_tokens=3000, split_prefill=1024)).run(bodies)
+    a = QAEngine(small_qa, tk, EngineConfig(max_slots=1024, qa_max_tokens=1 << 18, qa_split_prefill=0)).run(bodies)
+    b = QAEngine(small_qa, tk, EngineConfig(max_slots=1024, qa_max_tokens=1 << 18, qa_split_prefill=2048)).run(bodies)
+    c = QAEngine(small_qa, tk, EngineConfig(max_slots=64, qa_max_tokens=3000, qa_split_prefill=1024)).run(bodies)
     assert a == b == c
 
 
@@ -172,7 +172,7 @@ def test_qa_engine_packed_requests_match_per_message_answers(tk, small_qa):
                                                              negatives=0.1)]
     bodies[5] = bodies[5] + " ПОДРОБНЕЕ" * 80  # > max_body_tokens: cut, <ans> kept
     ids = tk.message_ids(bodies, 10_000)
-    cfg = EngineConfig(max_slots=1024, qa_max_tokens=40000, split_prefill=2048)
+    cfg = EngineConfig(max_slots=1024, qa_max_tokens=40000, qa_split_prefill=2048)
     e1 = QAEngine(small_qa, tk, cfg)
     e1.submit_ids(list(enumerate(ids)))
     per = {}

@@ -149,6 +149,11 @@ class EngineConfig:
     # one prefill (profiles/r05_qa_split_ab.jsonl: 64.5 k msgs/s either way at the
     # ~220 k-row batches, so one stream, whose kernel times are not inflated by sharing)
     qa_split_prefill: int = 0
+    # qa engine: how long one step() waits for the oldest in-flight batch before it
+    # returns (the engine server then polls its connections), and the sleep between
+    # event queries while it waits (no busy-wait on the host)
+    qa_wait_s: float = 0.002
+    qa_poll_s: float = 0.0002
 
 
 @dataclass

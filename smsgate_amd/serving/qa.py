@@ -52,7 +52,7 @@ from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
            "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
            "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP",
-           "QF_TIME"]
+           "QF_TIME", "QF_DEND"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
@@ -65,11 +65,14 @@ _NO_START_AFTER_MASK = QA_CLASS_BITS["date"] | QA_CLASS_BITS["number"]
 # char a letter-or-digit / a digit; exactly three ASCII digits; a lone "," "." "'"
 QF_NL, QF_FA, QF_FD, QF_LA, QF_LD, QF_GRP3, QF_SEP = 512, 1024, 2048, 4096, 8192, 16384, 32768
 QF_TIME = 1 << 16  # a whole time of day: " 22:09", "05:27:11"
+QF_DEND = 1 << 17  # may end a date: last char a digit, or AM / PM
 _TIME_RE = re.compile(r" ?\d{1,2}:\d{2}(?::\d{2})?\Z")
 # field kind -> (flags its first token must all have, flags its last token must all have).
+# A date ends with a digit or AM / PM (a span into the next word -- "12.05.25 покупка",
+# month names make letters part of the date class -- is no date).
 # Every gold value of every training and held-out family obeys them (a free-text value
 # may start with a digit: "7-ELEVEN").
-EDGE_RULES = {"number": (QF_FD, QF_LD), "card": (0, QF_LD), "date": (QF_FA, QF_LA), "text": (QF_FA, QF_LA),
+EDGE_RULES = {"number": (QF_FD, QF_LD), "card": (0, QF_LD), "date": (QF_FA, QF_DEND), "text": (QF_FA, QF_LA),
               "currency": (0, 0)}
 
 
@@ -180,6 +183,8 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
             f |= QF_SEP
         if _TIME_RE.match(t):
             f |= QF_TIME
+        if t[-1].isdigit() or t.strip().upper() in ("AM", "PM", "M"):  # "PM" is " P" + "M"
+            f |= QF_DEND
         out[i] |= f
     return out
 

@@ -133,7 +133,7 @@ class QAEngine(ExtractionEngine):
         self.active: Dict[int, Any] = {}
         self.stats = EngineStats()
         self.graphs: Dict[int, Any] = {}
-        self._pending: Optional[_Batch] = None
+        self._inflight: deque = deque()  # launched, not yet harvested (oldest first; at most 2)
         self._sides: List[torch.cuda.Stream] = []
         self._fwd_ss: Optional[torch.Tensor] = None
         self._idle_prev = None
@@ -270,8 +270,8 @@ class QAEngine(ExtractionEngine):
 
     def _harvest_batch(self, b: _Batch, raw: bool) -> List[Tuple[Any, Any]]:
         t0 = time.perf_counter()
-        b.event.synchronize()
-        self.stats.harvest_wait_s += time.perf_counter() - t0
+        if not b.event.query():
+            self._wait(b.event, float("inf"))
         lens = b.bufs["len"][: b.n].numpy().copy()
         blk = b.bufs["buf"][: b.n].numpy().copy()  # the pinned buffer is reused two batches on
         res: List[Tuple[Any, Any]] = []
@@ -298,19 +298,42 @@ class QAEngine(ExtractionEngine):
 
     # -------------------------------------------------------------- scheduler
     def busy(self) -> bool:
-        return bool(self.waiting or self._pending is not None)
+        return bool(self.waiting or self._inflight)
+
+    def _wait(self, ev, budget_s: float) -> bool:
+        """Wait up to ``budget_s`` for ``ev`` without spinning a core: hipEventSynchronize
+        (even on a blocking-sync event) kept the rank process busy-waiting, 12.7 of its
+        17.9 us of CPU per message (profiles/r05_samples_top_bench.txt)."""
+        t0 = time.perf_counter()
+        done = ev.query()
+        while not done and time.perf_counter() - t0 < budget_s:
+            time.sleep(self.cfg.qa_poll_s)
+            done = ev.query()
+        self.stats.harvest_wait_s += time.perf_counter() - t0
+        return done
 
     def step(self, raw: bool = False) -> List[Tuple[Any, Any]]:
-        """Launch a batch of the waiting messages (if any), then harvest the previous
-        batch: the GPU runs batch k while the host stages k and decodes k-1."""
+        """Harvest every batch the GPU has finished, keep two batches in flight (the GPU
+        runs batch k while the host stages k + 1 and decodes k - 1), and when neither is
+        possible wait up to ``qa_wait_s`` for the oldest batch (then the caller -- the
+        engine server -- polls its connections again).  Returns ``(key, answer)`` /
+        ``(key, tokens)`` / ``(key, PackedAnswer)`` of the harvested work."""
         t0 = time.perf_counter()
-        new = self._launch() if self.waiting else None
-        if new is not None and self.cfg.measure_idle and self._idle_prev is not None:
-            self._idle_pairs.append((self._idle_prev, new.start_event))
-        if new is not None and self.cfg.measure_idle:
-            self._idle_prev = new.event
-        prev, self._pending = self._pending, new
-        out = self._harvest_batch(prev, raw) if prev is not None else []
+        out: List[Tuple[Any, Any]] = []
+        while self._inflight and self._inflight[0].event.query():
+            out += self._harvest_batch(self._inflight.popleft(), raw)
+        while self.waiting and len(self._inflight) < 2:
+            new = self._launch()
+            if new is None:
+                break
+            if self.cfg.measure_idle:
+                if self._idle_prev is not None:
+                    self._idle_pairs.append((self._idle_prev, new.start_event))
+                self._idle_prev = new.event
+            self._inflight.append(new)
+        if not out and self._inflight and (len(self._inflight) >= 2 or not self.waiting):
+            if self._wait(self._inflight[0].event, self.cfg.qa_wait_s):
+                out = self._harvest_batch(self._inflight.popleft(), raw)
         while self._idle_pairs and self._idle_pairs[0][1].query():
             a, b = self._idle_pairs.popleft()
             self.stats.gpu_idle_s += max(0.0, a.elapsed_time(b)) / 1000.0

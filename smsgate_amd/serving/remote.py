@@ -130,8 +130,9 @@ class EngineServer:
         except Exception as exc:  # fail every waiting request loudly
             keys = list(self.reqs)
             if self._packed:  # whole requests queued / in flight in the engine
-                pend = getattr(self.engine, "_pending", None)
-                units = list(self.engine.waiting) + list(getattr(pend, "units", None) or [])
+                units = list(self.engine.waiting)
+                for b in getattr(self.engine, "_inflight", ()):
+                    units += list(getattr(b, "units", None) or [])
                 keys += [u.key for u in units if getattr(u, "packed", False)]
             for idx, rid in keys:
                 c = self.conns[idx]
@@ -141,6 +142,8 @@ class EngineServer:
             self.engine.waiting.clear()
             self.engine.active.clear()
             self.engine._pending = None
+            if hasattr(self.engine, "_inflight"):
+                self.engine._inflight.clear()
             raise
         t0 = time.perf_counter()
         for key, toks in finished:

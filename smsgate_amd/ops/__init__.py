@@ -289,10 +289,17 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #   256 rows, 9.7 vs 8.4 at 1024; profiles/r03_resid_small_m_tune.json) -- small decode
 #   buckets only, i.e. serving latency at low load, not the throughput bench's 9216-row
 #   halves.
+#   Round 5 (the qa engine's one-forward batches: 110 k / 220 k prefill rows), interleaved
+#   at 55 296 / 110 592 rows (profiles/r05_gemm_tune_qa.json): 128x192 with 4 waves
+#   (64x96 wave tiles, cfg 28) beats the 96-wide tiles for both residual GEMMs -- down-proj
+#   116.0 / 233.4 us vs 121.6 / 270.0 (cfg 21), o-proj 59.4 / 105.2 vs 59.6 / 117.8 (cfg
+#   22) -- and the QKV+RoPE GEMM (qkv_cfg).  Its x² parts stay 96 columns wide (two per
+#   tile, each summed like a 96-wide tile's), so results do not depend on the config.
 GEMM_MEASURED = {
     ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 6143, 19), (6144, 1 << 30, 20)],
-    ("resid", 576, 576): [(1, 2047, 27), (2048, 6143, 22), (6144, 12287, 21), (12288, 1 << 30, 22)],
-    ("resid", 576, 1536): [(1, 2047, 27), (2048, 6143, 22), (6144, 1 << 30, 21)],
+    ("resid", 576, 576): [(1, 2047, 27), (2048, 6143, 22), (6144, 12287, 21), (12288, 32767, 22),
+                          (32768, 1 << 30, 28)],
+    ("resid", 576, 1536): [(1, 2047, 27), (2048, 6143, 22), (6144, 32767, 21), (32768, 1 << 30, 28)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
 
@@ -408,14 +415,19 @@ def qkv_cfg(M: int, nh: int = 9, nkv: int = 3) -> int:
     us at 512 / 1024 / 2048, profiles/r01c_kbench_small_buckets.json); 128x192 with 4
     waves (64x96 wave tiles) at the 9 216-row decode halves (24.45 vs 25.10 us,
     profiles/r03s2_tiles_tune.json); 128x64 from 12 288 rows (prefill halves: 39.0 vs 40.7
-    us at 16 384, r02s3_gemm_tune.json).  Every config accumulates each output in the
+    us at 16 384, r02s3_gemm_tune.json); 128x192 again from 32 768 rows (the qa engine's
+    batches: 113.8-114.5 / 222.1 vs 133.7 / 264.4 us at 55 296 / 110 592 rows,
+    profiles/r05_gemm_tune_qa.json).  Every config accumulates each output in the
     same K order, so the choice never changes a result.  192-wide tiles hold three
     heads: only for head counts divisible by 3."""
+    three = nh % 3 == 0 and nkv % 3 == 0
     if M <= 2 * GEMM_SMALL_M:
         return 17
+    if M >= 32768 and three:  # the qa engine's batches: 222 vs 264 us at 110 592 rows (r05_gemm_tune_qa.json)
+        return 28
     if M >= 12288:
         return 1
-    return 28 if M >= 6144 and nh % 3 == 0 and nkv % 3 == 0 else 3
+    return 28 if M >= 6144 and three else 3
 
 
 def gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, eps: float, pos: torch.Tensor, slot: torch.Tensor,

@@ -80,13 +80,14 @@ def test_measured_tile_exceptions():
     assert ops.gemm_cfg(16384, 3072, epi="swiglu", K=576) == 20
     assert ops.gemm_cfg(2304, 3072, epi="swiglu", K=576) == 13
     assert ops.gemm_cfg(4608, 3072, epi="swiglu", K=576) == 19
-    # o-proj and down-proj of one forward tile N alike at every row count (the
-    # producer-norm partials image holds one part per N tile)
-    for M in range(1, 40000, 97):
+    # o-proj and down-proj of one forward tile N alike at every row count, in multiples
+    # of 96 columns (the producer-norm partials are 96-column parts whatever the tile)
+    for M in list(range(1, 40000, 97)) + [65536, 110592, 221184]:
         bn = {ops.GEMM_TILES[ops.gemm_cfg(M, 576, epi="resid", K=k)][1] for k in (576, 1536)}
-        assert len(bn) == 1, (M, bn)
+        assert len(bn) == 1 and bn.pop() % 96 == 0, (M, bn)
     assert ops.gemm_cfg(9216, 576, epi="resid", K=1536) == 21
-    assert {ops.GEMM_TILES[ops.gemm_cfg(M, 576, epi="resid", K=576)][1] for M in range(1, 40000, 97)} == {96}
+    # the qa engine's batches: 128x192 (profiles/r05_gemm_tune_qa.json)
+    assert ops.gemm_cfg(110592, 576, epi="resid", K=1536) == ops.gemm_cfg(110592, 576, epi="resid", K=576) == 28
     assert ops.GEMM_TILES[20] == (256, 256) and 20 in ops.GEMM_SWIGLU_ONLY
     assert all(576 % ops.GEMM_TILES[c][1] == 0 for c in ops.GEMM_NO_SWIGLU)  # the N = 576 residual GEMMs
 
@@ -99,5 +100,6 @@ def test_qkv_tile_rule():
     assert ops.qkv_cfg(9216, 9, 3) == 28
     assert ops.qkv_cfg(9216, 4, 2) == 3 and ops.qkv_cfg(9216, 9, 2) == 3
     assert ops.qkv_cfg(1000) == 17 and ops.qkv_cfg(4608) == 3 and ops.qkv_cfg(15104) == 1
+    assert ops.qkv_cfg(110592) == 28 and ops.qkv_cfg(110592, 4, 2) == 1
     bm, bn = ops.GEMM_TILES[28]
     assert (bm, bn) == (128, 192) and 28 in ops.GEMM_NO_SWIGLU

@@ -14,9 +14,13 @@ autograd Function with a hand-written backward:
 * ``RopeSplit``: the QKV GEMM's bf16 output -> q / k / v in SDPA's [B, heads, T, D]
   layout with rotate-half RoPE on q and k (fp32 math, the caller's cos / sin tables);
   backward is the adjoint rotation straight into dqkv;
-* ``SwiGLU``: silu(gate) * up from the fused gate/up GEMM output, and its backward.
+* ``SwiGLU``: silu(gate) * up from the fused gate/up GEMM output, and its backward;
+* ``Attention``: causal grouped-query attention over the batch (<= 192 rows) straight
+  into the o-proj's [B, T, heads * 64] input, log-sum-exp saved, and its backward (two
+  kernels recomputing the probabilities).  SDPA made one synchronous host-to-device
+  copy per call, so the host could never run ahead of the GPU (63 per step).
 
-GEMMs stay hipBLASLt (autocast bf16) and attention stays SDPA (flash), so the math is
+GEMMs stay hipBLASLt (autocast bf16), so the math is
 reference_forward's up to bf16 rounding order (tests/test_train_ops_gpu.py compares
 losses and gradients).  CPU / no-library: reference_forward.
 """
@@ -33,7 +37,7 @@ import torch.nn.functional as F
 from .. import ops
 from .extractor import ExtractorWeights, _rope_tables
 
-__all__ = ["fused_forward", "rms_norm", "rope_split", "swiglu", "available"]
+__all__ = ["fused_forward", "rms_norm", "rope_split", "swiglu", "attention", "available", "ATTN_MAX_T"]
 
 
 def available(device) -> bool:
@@ -145,6 +149,46 @@ class _SwiGLU(torch.autograd.Function):
         return dgu.view(ctx.shape)
 
 
+ATTN_MAX_T = 192  # csrc/train_kernels.hip AT_MAXT
+
+
+class _Attention(torch.autograd.Function):
+    """Causal grouped-query attention of one training batch (attn_train_* kernels):
+    q [B, nh, T, 64], k / v [B, nkv, T, 64] -> out [B, T, nh * 64] (the o-proj input)."""
+
+    @staticmethod
+    def forward(ctx, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:
+        B, nh, T, D = q.shape
+        nkv = k.shape[1]
+        if D != 64 or T > ATTN_MAX_T or nh % nkv or q.dtype != torch.bfloat16:
+            raise ValueError("attention: bf16, head_dim 64, T <= 192, nh % nkv == 0")
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out = torch.empty(B, T, nh * D, dtype=q.dtype, device=q.device)
+        lse = torch.empty(B, nh, T, dtype=torch.float32, device=q.device)
+        _ok(_lib().sg_attn_train_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(), B, T,
+                                     nh, nkv, float(scale), _st()), "attn_train_fwd")
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout: torch.Tensor):
+        q, k, v, out, lse = ctx.saved_tensors
+        B, nh, T, D = q.shape
+        nkv = k.shape[1]
+        dout = dout.to(torch.bfloat16).contiguous()
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        dsum = torch.empty(B, nh, T, dtype=torch.float32, device=q.device)
+        _ok(_lib().sg_attn_train_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), lse.data_ptr(),
+                                     dout.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dsum.data_ptr(), B,
+                                     T, nh, nkv, float(ctx.scale), _st()), "attn_train_bwd")
+        return dq, dk, dv, None
+
+
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:
+    return _Attention.apply(q, k, v, scale)
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
     return _RMSNorm.apply(x, w, eps)
 
@@ -172,12 +216,15 @@ def fused_forward(w: ExtractorWeights, ids: torch.Tensor, add_ids: Optional[torc
     cos, sin = _rope_tables(T, D, cfg.rope_theta, ids.device)
     cos, sin = cos.reshape(T, D // 2).contiguous(), sin.reshape(T, D // 2).contiguous()
     scale = 1.0 / math.sqrt(D)
-    # grouped-query attention inside SDPA (flash); the efficient backend has no GQA
-    # support, so it gets k / v expanded to nh heads by rope_split (its adjoint sums them)
-    rep = nh // nkv if os.environ.get("SMSGATE_TRAIN_SDPA", "") == "efficient" else 1
+    # attention: the training kernels (attn_train_*) up to 192 rows, else SDPA (flash); the
+    # efficient SDPA backend has no GQA support, so it gets k / v expanded to nh heads by
+    # rope_split (its adjoint sums them)
+    sdpa = os.environ.get("SMSGATE_TRAIN_SDPA", "")
+    rep = nh // nkv if sdpa == "efficient" else 1
+    own = not sdpa and T <= ATTN_MAX_T
     with _sdpa_backend():
         for i in range(cfg.layers):
-            x = _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep)
+            x = _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep, own)
     return rms_norm(x, w.ln_f, cfg.eps)
 
 
@@ -193,12 +240,16 @@ def _sdpa_backend():
                         "math": SDPBackend.MATH}[name])
 
 
-def _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep=1):
+def _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep=1, own=False):
     """One decoder layer of the residual stream ``x`` (fp32)."""
     eps = w.cfg.eps
     h = rms_norm(x, w.ln1[i], eps)
     q, k, v = rope_split(h @ w.qkv[i].t(), cos, sin, nh, nkv, rep)
-    a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale, enable_gqa=nh != nkv * rep)
-    x = x + a.transpose(1, 2).reshape(B, T, nh * D) @ w.o[i].t()
+    if own:
+        a = attention(q, k, v, scale)
+    else:
+        a = F.scaled_dot_product_attention(q, k, v, is_causal=True, scale=scale,
+                                           enable_gqa=nh != nkv * rep).transpose(1, 2).reshape(B, T, nh * D)
+    x = x + a @ w.o[i].t()
     h = rms_norm(x, w.ln2[i], eps)
     return x + swiglu(h @ w.gate_up[i].t()) @ w.down[i].t()

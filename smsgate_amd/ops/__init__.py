@@ -158,7 +158,10 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.sg_rope_split.argtypes = [_c_int, _vp, _vp, _vp, _vp, _vp, _vp] + [_c_int] * 6 + [_vp]
     lib.sg_swiglu_fwd.argtypes = [_vp, _vp, _c_int, _c_int, _vp]
     lib.sg_swiglu_bwd.argtypes = [_vp, _vp, _vp, _c_int, _c_int, _vp]
-    for fn in (lib.sg_rms_fwd, lib.sg_rms_bwd, lib.sg_rope_split, lib.sg_swiglu_fwd, lib.sg_swiglu_bwd):
+    lib.sg_attn_train_fwd.argtypes = [_vp] * 5 + [_c_int] * 4 + [_c_float, _vp]
+    lib.sg_attn_train_bwd.argtypes = [_vp] * 10 + [_c_int] * 4 + [_c_float, _vp]
+    for fn in (lib.sg_rms_fwd, lib.sg_rms_bwd, lib.sg_rope_split, lib.sg_swiglu_fwd, lib.sg_swiglu_bwd,
+               lib.sg_attn_train_fwd, lib.sg_attn_train_bwd):
         fn.restype = _c_int
     for f in ("sg_gemm", "sg_gemm_qkv_rope", "sg_rmsnorm_residual", "sg_silu_mul", "sg_rope_qkv_cache", "sg_attn_prefill", "sg_attn_decode",
               "sg_fsm_sample", "sg_version", "sg_kv_copy_prefix"):

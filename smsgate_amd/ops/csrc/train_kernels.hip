@@ -15,6 +15,12 @@
 //               expanded to nh heads), and its adjoint (rotation by -theta, expanded
 //               copies summed) from dq / dk / dv back to dqkv
 //   swiglu      a = bf16(silu(g) * u) on gu = [gate | up], and dgu from da
+//   attn_train  causal grouped-query attention over one training batch (T <= 192 rows,
+//               D = 64): forward with the per-row log-sum-exp saved, backward in two
+//               passes that recompute the probabilities (query rows -> dQ; key rows ->
+//               dK / dV summed over the group's query heads).  SDPA's kernels made one
+//               synchronous host-to-device copy per call (63 per step, the host could not
+//               run ahead of the GPU: scripts/train_step_profile.py); these make none.
 //
 // One wave (64 lanes) per row for the norms (H <= 1024: 4 float4 per lane in
 // registers); 8 bf16 per thread (16-B accesses) for SwiGLU; one lane per output element
@@ -244,6 +250,235 @@ __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const uint16_t* __restr
   *reinterpret_cast<uint4*>(dgu + (size_t)row * 2 * I + I + 8 * c) = make_uint4(ou[0], ou[1], ou[2], ou[3]);
 }
 
+// ---- training attention ------------------------------------------------------
+// q [B, nh, T, 64], k / v [B, nkv, T, 64] (bf16, rope_split's layout), o [B, T, nh*64]
+// (the o-proj GEMM's input layout: no transpose copy), lse [B, nh, T] fp32.  Query head h
+// reads kv head h / (nh / nkv).  One thread per row (T <= 256 = the block), the group's
+// K and V staged in LDS as bf16 and read by every lane of a wave at the same address
+// (LDS broadcast).  fp32 math; the causal mask is the loop bound.
+constexpr int AT_D = 64;
+constexpr int AT_MAXT = 192;
+
+__device__ __forceinline__ void at_row_f32(const uint16_t* p, float* out) {
+#pragma unroll
+  for (int c = 0; c < AT_D / 8; ++c) {
+    const uint4 u = reinterpret_cast<const uint4*>(p)[c];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      out[8 * c + 2 * e] = tk_bf2f((uint16_t)(w[e] & 0xffffu));
+      out[8 * c + 2 * e + 1] = tk_bf2f((uint16_t)(w[e] >> 16));
+    }
+  }
+}
+
+__device__ __forceinline__ float at_dot(const float* a, const uint16_t* b_lds) {
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < AT_D / 8; ++c) {
+    const uint4 u = reinterpret_cast<const uint4*>(b_lds)[c];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s = fmaf(a[8 * c + 2 * e], tk_bf2f((uint16_t)(w[e] & 0xffffu)), s);
+      s = fmaf(a[8 * c + 2 * e + 1], tk_bf2f((uint16_t)(w[e] >> 16)), s);
+    }
+  }
+  return s;
+}
+
+__device__ __forceinline__ void at_axpy(float* y, float a, const uint16_t* x_lds) {
+#pragma unroll
+  for (int c = 0; c < AT_D / 8; ++c) {
+    const uint4 u = reinterpret_cast<const uint4*>(x_lds)[c];
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      y[8 * c + 2 * e] = fmaf(a, tk_bf2f((uint16_t)(w[e] & 0xffffu)), y[8 * c + 2 * e]);
+      y[8 * c + 2 * e + 1] = fmaf(a, tk_bf2f((uint16_t)(w[e] >> 16)), y[8 * c + 2 * e + 1]);
+    }
+  }
+}
+
+__device__ __forceinline__ void at_store_bf16(uint16_t* p, const float* v, float scale) {
+#pragma unroll
+  for (int c = 0; c < AT_D / 8; ++c) {
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] = (uint32_t)tk_f2bf(v[8 * c + 2 * e] * scale) | ((uint32_t)tk_f2bf(v[8 * c + 2 * e + 1] * scale) << 16);
+    reinterpret_cast<uint4*>(p)[c] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// stage `rows` rows of 64 bf16 (row stride `ld` elements) into LDS
+__device__ __forceinline__ void at_stage(uint16_t* dst, const uint16_t* src, int rows, size_t ld) {
+  for (int i = threadIdx.x; i < rows * (AT_D / 8); i += blockDim.x) {
+    const int r = i / (AT_D / 8), c = i % (AT_D / 8);
+    reinterpret_cast<uint4*>(dst + r * AT_D)[c] = reinterpret_cast<const uint4*>(src + (size_t)r * ld)[c];
+  }
+}
+
+__global__ void __launch_bounds__(256) attn_train_fwd_kernel(const uint16_t* __restrict__ q,
+                                                             const uint16_t* __restrict__ k,
+                                                             const uint16_t* __restrict__ v, uint16_t* __restrict__ o,
+                                                             float* __restrict__ lse, int T, int nh, int nkv,
+                                                             float scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t ks[AT_MAXT * AT_D];
+  __shared__ __attribute__((aligned(16))) uint16_t vs[AT_MAXT * AT_D];
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh, g = h / (nh / nkv);
+  const size_t kvo = ((size_t)b * nkv + g) * T * AT_D;
+  at_stage(ks, k + kvo, T, AT_D);
+  at_stage(vs, v + kvo, T, AT_D);
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= T) return;
+  float qr[AT_D], acc[AT_D];
+  at_row_f32(q + (((size_t)b * nh + h) * T + t) * AT_D, qr);
+#pragma unroll
+  for (int d = 0; d < AT_D; ++d) {
+    qr[d] *= scale;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j <= t; ++j) {
+    const float sc = at_dot(qr, ks + j * AT_D);
+    if (sc > m) {
+      const float corr = __expf(m - sc);
+      l *= corr;
+#pragma unroll
+      for (int d = 0; d < AT_D; ++d) acc[d] *= corr;
+      m = sc;
+    }
+    const float p = __expf(sc - m);
+    l += p;
+    at_axpy(acc, p, vs + j * AT_D);
+  }
+  at_store_bf16(o + ((size_t)b * T + t) * nh * AT_D + h * AT_D, acc, 1.f / l);
+  lse[((size_t)b * nh + h) * T + t] = m + __logf(l);
+}
+
+// Backward, two kernels (one thread per row each; splitting them keeps every thread's
+// live set under the VGPR file: a fused pass spilled).  ds_tj = p_tj (do_t . v_j - D_t),
+// D_t = do_t . o_t, p_tj = exp(scale q_t . k_j - lse_t).
+// A (block = batch x query head, thread = query row t): dq_t = scale sum_j ds_tj k_j, and
+//   D_t into dsum [B, nh, T] for B.
+__global__ void __launch_bounds__(256) attn_train_bwd_q_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    const uint16_t* __restrict__ o, const float* __restrict__ lse, const uint16_t* __restrict__ dout,
+    uint16_t* __restrict__ dq, float* __restrict__ dsum, int T, int nh, int nkv, float scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t ks[AT_MAXT * AT_D];
+  __shared__ __attribute__((aligned(16))) uint16_t vs[AT_MAXT * AT_D];
+  const int b = blockIdx.x / nh, h = blockIdx.x % nh, g = h / (nh / nkv);
+  const size_t kvo = ((size_t)b * nkv + g) * T * AT_D;
+  at_stage(ks, k + kvo, T, AT_D);
+  at_stage(vs, v + kvo, T, AT_D);
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= T) return;
+  const size_t row = ((size_t)b * nh + h) * T + t;  // [B, nh, T] index
+  const size_t orow = ((size_t)b * T + t) * nh * AT_D + h * AT_D;
+  float qt[AT_D], dt[AT_D], acc[AT_D];
+  at_row_f32(o + orow, acc);  // o_t (scratch for D_t)
+  at_row_f32(dout + orow, dt);
+  float D = 0.f;
+#pragma unroll
+  for (int d = 0; d < AT_D; ++d) D = fmaf(dt[d], acc[d], D);
+  dsum[row] = D;
+  at_row_f32(q + row * AT_D, qt);
+#pragma unroll
+  for (int d = 0; d < AT_D; ++d) {
+    qt[d] *= scale;
+    acc[d] = 0.f;
+  }
+  const float L = lse[row];
+  for (int j = 0; j <= t; ++j) {
+    const float p = __expf(at_dot(qt, ks + j * AT_D) - L);
+    const float ds = p * (at_dot(dt, vs + j * AT_D) - D);
+    at_axpy(acc, ds, ks + j * AT_D);
+  }
+  at_store_bf16(dq + row * AT_D, acc, scale);
+}
+
+// B (block = batch x kv head, thread = key row j): over the group's query heads,
+// dv_j += sum_{t>=j} p_tj do_t and dk_j += scale sum_{t>=j} ds_tj q_t.  k_j / v_j stay
+// packed bf16 in registers, q / dO / lse / D of the current head in LDS (broadcast reads).
+__global__ void __launch_bounds__(256) attn_train_bwd_kv_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ k, const uint16_t* __restrict__ v,
+    const float* __restrict__ lse, const float* __restrict__ dsum, const uint16_t* __restrict__ dout,
+    uint16_t* __restrict__ dk, uint16_t* __restrict__ dv, int T, int nh, int nkv, float scale) {
+  __shared__ __attribute__((aligned(16))) uint16_t qs[AT_MAXT * AT_D];
+  __shared__ __attribute__((aligned(16))) uint16_t dos[AT_MAXT * AT_D];
+  __shared__ float ls[AT_MAXT], Ds[AT_MAXT];
+  const int b = blockIdx.x / nkv, g = blockIdx.x % nkv, rep = nh / nkv;
+  const size_t kvo = ((size_t)b * nkv + g) * T * AT_D;
+  const int j = threadIdx.x;
+  uint32_t kp[AT_D / 2], vp[AT_D / 2];
+  float dkj[AT_D], dvj[AT_D];
+  if (j < T) {
+#pragma unroll
+    for (int c = 0; c < AT_D / 8; ++c) {
+      const uint4 ku = reinterpret_cast<const uint4*>(k + kvo + (size_t)j * AT_D)[c];
+      const uint4 vu = reinterpret_cast<const uint4*>(v + kvo + (size_t)j * AT_D)[c];
+      kp[4 * c] = ku.x; kp[4 * c + 1] = ku.y; kp[4 * c + 2] = ku.z; kp[4 * c + 3] = ku.w;
+      vp[4 * c] = vu.x; vp[4 * c + 1] = vu.y; vp[4 * c + 2] = vu.z; vp[4 * c + 3] = vu.w;
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < AT_D; ++d) dkj[d] = dvj[d] = 0.f;
+  for (int r = 0; r < rep; ++r) {
+    const int h = g * rep + r;
+    const size_t qo = ((size_t)b * nh + h) * T;
+    __syncthreads();  // the previous head's rows are no longer read
+    at_stage(qs, q + qo * AT_D, T, AT_D);
+    at_stage(dos, dout + (size_t)b * T * nh * AT_D + h * AT_D, T, (size_t)nh * AT_D);
+    for (int i = threadIdx.x; i < T; i += blockDim.x) {
+      ls[i] = lse[qo + i];
+      Ds[i] = dsum[qo + i];
+    }
+    __syncthreads();
+    if (j >= T) continue;
+    for (int t = j; t < T; ++t) {
+      const uint16_t* qr = qs + t * AT_D;
+      const uint16_t* dr = dos + t * AT_D;
+      float s = 0.f, dpv = 0.f;
+#pragma unroll
+      for (int c = 0; c < AT_D / 8; ++c) {
+        const uint4 qu = reinterpret_cast<const uint4*>(qr)[c];
+        const uint4 du = reinterpret_cast<const uint4*>(dr)[c];
+        const uint32_t qw[4] = {qu.x, qu.y, qu.z, qu.w}, dw[4] = {du.x, du.y, du.z, du.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t kk = kp[4 * c + e], vv = vp[4 * c + e];
+          s = fmaf(tk_bf2f((uint16_t)(qw[e] & 0xffffu)), tk_bf2f((uint16_t)(kk & 0xffffu)), s);
+          s = fmaf(tk_bf2f((uint16_t)(qw[e] >> 16)), tk_bf2f((uint16_t)(kk >> 16)), s);
+          dpv = fmaf(tk_bf2f((uint16_t)(dw[e] & 0xffffu)), tk_bf2f((uint16_t)(vv & 0xffffu)), dpv);
+          dpv = fmaf(tk_bf2f((uint16_t)(dw[e] >> 16)), tk_bf2f((uint16_t)(vv >> 16)), dpv);
+        }
+      }
+      const float p = __expf(scale * s - ls[t]);
+      const float ds = p * (dpv - Ds[t]) * scale;
+#pragma unroll
+      for (int c = 0; c < AT_D / 8; ++c) {
+        const uint4 qu = reinterpret_cast<const uint4*>(qr)[c];
+        const uint4 du = reinterpret_cast<const uint4*>(dr)[c];
+        const uint32_t qw[4] = {qu.x, qu.y, qu.z, qu.w}, dw[4] = {du.x, du.y, du.z, du.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          dvj[8 * c + 2 * e] = fmaf(p, tk_bf2f((uint16_t)(dw[e] & 0xffffu)), dvj[8 * c + 2 * e]);
+          dvj[8 * c + 2 * e + 1] = fmaf(p, tk_bf2f((uint16_t)(dw[e] >> 16)), dvj[8 * c + 2 * e + 1]);
+          dkj[8 * c + 2 * e] = fmaf(ds, tk_bf2f((uint16_t)(qw[e] & 0xffffu)), dkj[8 * c + 2 * e]);
+          dkj[8 * c + 2 * e + 1] = fmaf(ds, tk_bf2f((uint16_t)(qw[e] >> 16)), dkj[8 * c + 2 * e + 1]);
+        }
+      }
+    }
+  }
+  if (j < T) {
+    at_store_bf16(dk + kvo + (size_t)j * AT_D, dkj, 1.f);
+    at_store_bf16(dv + kvo + (size_t)j * AT_D, dvj, 1.f);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -289,6 +524,29 @@ int sg_swiglu_bwd(const void* da, const void* gu, void* dgu, int R, int I, hipSt
   const long n = (long)R * (I / 8);
   swiglu_bwd_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st>>>((const uint16_t*)da,
                                                                              (const uint16_t*)gu, (uint16_t*)dgu, R, I);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int sg_attn_train_fwd(const void* q, const void* k, const void* v, void* o, void* lse, int B, int T, int nh, int nkv,
+                      float scale, hipStream_t st) {
+  if (T <= 0 || T > AT_MAXT || B <= 0 || nkv <= 0 || nh % nkv) return 1;
+  attn_train_fwd_kernel<<<dim3(B * nh), dim3(256), 0, st>>>((const uint16_t*)q, (const uint16_t*)k,
+                                                            (const uint16_t*)v, (uint16_t*)o, (float*)lse, T, nh, nkv,
+                                                            scale);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+int sg_attn_train_bwd(const void* q, const void* k, const void* v, const void* o, const void* lse, const void* dout,
+                      void* dq, void* dk, void* dv, void* dsum, int B, int T, int nh, int nkv, float scale,
+                      hipStream_t st) {
+  if (T <= 0 || T > AT_MAXT || B <= 0 || nkv <= 0 || nh % nkv) return 1;
+  attn_train_bwd_q_kernel<<<dim3(B * nh), dim3(256), 0, st>>>(
+      (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const float*)lse,
+      (const uint16_t*)dout, (uint16_t*)dq, (float*)dsum, T, nh, nkv, scale);
+  if (hipGetLastError() != hipSuccess) return 2;
+  attn_train_bwd_kv_kernel<<<dim3(B * nkv), dim3(256), 0, st>>>(
+      (const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const float*)lse, (const float*)dsum,
+      (const uint16_t*)dout, (uint16_t*)dk, (uint16_t*)dv, T, nh, nkv, scale);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

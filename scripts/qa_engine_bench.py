@@ -22,7 +22,7 @@ def main() -> int:
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--queries", type=int, default=9)
     p.add_argument("--max-slots", type=int, default=8192)
-    p.add_argument("--qa-max-tokens", type=int, default=262144)
+    p.add_argument("--qa-max-tokens", default="262144", help="comma list: one JSON line per value (a sweep)")
     p.add_argument("--split-prefill", type=int, default=0, help="EngineConfig.qa_split_prefill")
     p.add_argument("--request", type=int, default=512)
     p.add_argument("--packed", type=int, default=1, choices=[0, 1],
@@ -43,21 +43,19 @@ def main() -> int:
     cfg = qa_config(CONFIGS["smollm-135m"], queries=a.queries)
     w = ExtractorWeights(cfg, device="cuda", seed=0)
     w.requires_grad_(False)
-    eng = QAEngine(w, tok, EngineConfig(max_slots=a.max_slots, qa_max_tokens=a.qa_max_tokens,
-                                        qa_split_prefill=a.split_prefill))
     bodies = [normalize_body(s.body) for s in generate_traffic(a.n, seed=1, traffic="formats")]
     ids = [np.asarray(x, dtype=np.int32) for x in tok.message_ids(bodies, 128)]
     tokens = sum(len(x) for x in ids) / len(ids)
     lens = np.asarray([len(x) for x in ids], dtype=np.int32)
 
-    def run_once() -> float:
+    def run_once(eng) -> float:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         done = 0
         k = 0
         while done < len(ids):
             # keep ~8 requests waiting, like 8 parser processes with one request in flight each
-            while k < len(ids) and len(eng.waiting) < (8 if a.packed else 8 * a.request):
+            while k < len(ids) and len(eng.waiting) * (a.request if a.packed else 1) < 8 * a.request:
                 part = range(k, min(k + a.request, len(ids)))
                 if a.packed:
                     eng.submit_packed(k, lens[part.start:part.stop], np.concatenate([ids[i] for i in part]))
@@ -69,18 +67,23 @@ def main() -> int:
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    run_once()  # warm-up (allocator, first launches)
-    eng.reset_stats()
-    times = [run_once() for _ in range(a.reps)]
-    st = eng.stats
-    out = {"metric": "qa_engine_msgs_per_s", "value": round(a.n / min(times), 1),
-           "runs_s": [round(t, 3) for t in times], "n": a.n, "queries": a.queries,
-           "prompt_tokens_per_msg": round(tokens, 2), "rows_per_msg": round(tokens + a.queries, 2),
-           "batches": st.steps, "msgs_per_batch": round(st.prefill_seqs / max(1, st.steps), 1),
-           "gpu_idle_s": round(st.gpu_idle_s, 4), "host_prefill_s": round(st.prefill_s, 3),
-           "harvest_wait_s": round(st.harvest_wait_s, 3),
-           "config": {"packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": a.qa_max_tokens, "qa_split_prefill": a.split_prefill}}
-    print(json.dumps(out), flush=True)
+    for mt in (int(x) for x in str(a.qa_max_tokens).split(",")):
+        eng = QAEngine(w, tok, EngineConfig(max_slots=a.max_slots, qa_max_tokens=mt, qa_split_prefill=a.split_prefill))
+        run_once(eng)  # warm-up (allocator, first launches)
+        eng.reset_stats()
+        times = [run_once(eng) for _ in range(a.reps)]
+        st = eng.stats
+        out = {"metric": "qa_engine_msgs_per_s", "value": round(a.n / min(times), 1),
+               "runs_s": [round(t, 3) for t in times], "n": a.n, "queries": a.queries,
+               "prompt_tokens_per_msg": round(tokens, 2), "rows_per_msg": round(tokens + a.queries, 2),
+               "batches": st.prefill_batches, "msgs_per_batch": round(st.prefill_seqs / max(1, st.prefill_batches), 1),
+               "gpu_idle_s": round(st.gpu_idle_s, 4), "host_prefill_s": round(st.prefill_s, 3),
+               "harvest_wait_s": round(st.harvest_wait_s, 3),
+               "config": {"packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": mt,
+                          "qa_split_prefill": a.split_prefill}}
+        print(json.dumps(out), flush=True)
+        del eng
+        torch.cuda.empty_cache()
     return 0
 
 

@@ -160,6 +160,7 @@ class EngineConfig:
 class EngineStats:
     prefill_tokens: int = 0
     prefill_seqs: int = 0
+    prefill_batches: int = 0  # qa engine: packed prefill launches
     prefill_s: float = 0.0
     template_tokens: int = 0  # prompt tokens NOT computed: copied from a message-start template
     templates: int = 0

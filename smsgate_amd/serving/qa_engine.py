@@ -265,6 +265,7 @@ class QAEngine(ExtractionEngine):
         st = self.stats
         st.prefill_tokens += T
         st.prefill_seqs += n
+        st.prefill_batches += 1
         st.prefill_s += time.perf_counter() - t0
         return _Batch(n, units, ev, start_ev, hb)
 

@@ -57,6 +57,10 @@ def _is_future(dt: datetime) -> bool:
     return dt > datetime.now(timezone.utc)
 
 
+def _text(data: bytes) -> str:
+    return data.decode(errors="ignore")
+
+
 def _dump(obj: Dict[str, Any]) -> bytes:
     return json.dumps(obj).encode()
 
@@ -67,31 +71,34 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
     # ok / fail / skip are the reference's metric semantics (a keyword skip counts as
     # ok, D11); parsed and keyword_skipped split "ok" into what actually happened
     counts = {"ok": 0, "fail": 0, "skip": 0, "parsed": 0, "keyword_skipped": 0}
-    texts: List[str] = []
+    texts: List[bytes] = []
     raws: List[RawSMS] = []
     raw_idx: List[int] = []
 
     with start_span("validate"):
         for i, m in enumerate(msgs):
             data = m.data
-            text = data.decode(errors="ignore") if isinstance(data, (bytes, bytearray)) else str(data)
-            texts.append(text)
+            if not isinstance(data, (bytes, bytearray)):
+                data = str(data).encode()
+            texts.append(data)  # decoded only for a failure envelope (_text)
             try:
-                if '"raw"' not in text:
-                    # fast path: pydantic-core parses + validates the JSON in one pass
-                    # (falls back below on any error, so failure routing is unchanged)
+                if b'"raw"' not in data:
+                    # fast path: pydantic-core parses + validates the JSON bytes in one
+                    # pass (falls back below on any error, so failure routing is unchanged)
                     try:
-                        raw = RawSMS.model_validate_json(text)
+                        raw = RawSMS.model_validate_json(data)
                     except Exception:
                         raw = None
                 else:
                     raw = None
                 if raw is None:
+                    text = _text(data)
                     payload = json.loads(text)
                     if isinstance(payload, dict) and "raw" in payload:
                         payload = payload["raw"]
                     raw = RawSMS(**payload)
             except Exception as err:
+                text = _text(data)
                 out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))
                 counts["fail"] += 1
                 sentry_capture(err, extras={"raw_data": text})
@@ -114,7 +121,7 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
 
         with start_span("validate_parsed"):
             for raw, i, res in zip(raws, raw_idx, results):
-                text = texts[i]
+                data = texts[i]
                 if res.outcome is Outcome.BROKEN:
                     counts["skip"] += 1
                     continue
@@ -131,6 +138,7 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                 # only the serialisation keeps the shape-(d) failure route.
                 parsed = res.parsed
                 if _is_future(parsed.date):
+                    text = _text(data)
                     sentry_capture(ValueError(FUTURE_DATE_ERR), extras={"raw_data": text})
                     out.append((SUBJECT_FAILED, _dump({"err": FUTURE_DATE_ERR, "entry": text})))
                     counts["fail"] += 1
@@ -138,6 +146,7 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                 try:
                     payload = parsed_wire(parsed)
                 except Exception as err:
+                    text = _text(data)
                     sentry_capture(err, extras={"raw_data": text})
                     out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))
                     counts["fail"] += 1

@@ -67,18 +67,19 @@ class WriterService:
             dlq.append((SUBJECT_FAILED, json.dumps({"err": str(err), "entry": text}).encode()))
 
         for m in msgs:
-            text = m.data.decode(errors="ignore")
+            data = m.data
             try:
-                # one Rust pass parses and validates (the reference: json + model_validate)
-                p = ParsedSMS.model_validate_json(text)
+                # one Rust pass parses and validates the bytes (the reference: json +
+                # model_validate); the text is decoded only for a failure envelope
+                p = ParsedSMS.model_validate_json(data)
                 if not p.merchant:
                     self.skipped += 1
                     continue
                 if _future(p.date):
                     raise ValueError("Bad date")
-                to_store.append((p, text))
+                to_store.append((p, data))
             except Exception as err:  # noqa: BLE001
-                fail(err, text)
+                fail(err, data.decode(errors="ignore") if isinstance(data, (bytes, bytearray)) else str(data))
 
         if to_store:
             try:
@@ -91,7 +92,8 @@ class WriterService:
                         await self._upsert([p])
                         stored += 1
                     except Exception as err:  # noqa: BLE001
-                        fail(err.__cause__ or err, text)
+                        fail(err.__cause__ or err, text.decode(errors="ignore")
+                             if isinstance(text, (bytes, bytearray)) else str(text))
             self.ok += stored
             if stored:
                 M.WRITER_OK.inc(stored)

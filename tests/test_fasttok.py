@@ -111,7 +111,9 @@ def test_full_cache_is_emptied_and_refilled_exactly(toks):
     assert ft.encode(probe) == want
     for i in range(0, len(words), 5000):
         ft.encode(" ".join(words[i:i + 5000]))
-    assert 0 < ft.cache_size() < len(set(words)) - 2 ** 18 + 1000  # emptied once on the way
+    # more distinct pre-tokens than the capacity went in: a cache that stopped inserting
+    # when full would sit at exactly 2^18 entries
+    assert 0 < ft.cache_size() < 2 ** 18
     assert ft.encode(probe) == want
     sample = " ".join(words[-50:])
     assert ft.encode(sample) == tk.encode(sample)

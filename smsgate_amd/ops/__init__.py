@@ -146,7 +146,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   _vp]
     lib.sg_copy_masks.restype = _c_int
     lib.sg_qa_decode.argtypes = [_vp, _vp, _c_int, _vp, _c_int, _c_float, _ip, _ip, _vp, _c_int, _ip, _ip, _vp, _vp,
-                                 _c_int, _vp]
+                                 _c_int, _c_int, _vp]
     lib.sg_qa_decode.restype = _c_int
     lib.sg_qa_params_size.argtypes = []
     lib.sg_qa_params_size.restype = _c_int
@@ -481,8 +481,9 @@ class LayerPointers:
 def prefill_forward(lp: LayerPointers, x: torch.Tensor, *, H: int, I: int, nh: int, nkv: int, D: int, Lmax: int,
                     P0: int, P0pad: int, pos: torch.Tensor, slot: torch.Tensor, cos_sin: torch.Tensor, p0: int,
                     cu_q: torch.Tensor, q_start: torch.Tensor, seq_slot: torch.Tensor, max_q: int, scale: float,
-                    q: torch.Tensor, a: torch.Tensor, act: torch.Tensor, ss: Optional[torch.Tensor], eps: float) -> None:
-    """The fused prefill forward (every layer: QKV+RoPE+KV write, varlen prefill
+                    q: torch.Tensor, a: torch.Tensor, act: torch.Tensor, ss: Optional[torch.Tensor], eps: float,
+                    layers: Optional[int] = None) -> None:
+    """The fused prefill forward (every layer -- or the first ``layers`` -- : QKV+RoPE+KV write, varlen prefill
     attention, o-proj + residual, SwiGLU gate/up, down-proj + residual) as ONE native
     call (``sg_prefill_forward``) — the kernels and tile configs of ``gemm_qkv_rope`` /
     ``attn_prefill`` / ``gemm`` launched from C instead of ~150 Python wrapper calls.
@@ -498,8 +499,11 @@ def prefill_forward(lp: LayerPointers, x: torch.Tensor, *, H: int, I: int, nh: i
     cfg_gu = gemm_cfg(T, 2 * I, epi="swiglu", K=H)
     cfg_down = gemm_cfg(T, H, epi="resid", K=I)
     ld = _ss_check(ss, T, "prefill_forward ss")
+    L = lp.L if layers is None else int(layers)
+    if not 0 <= L <= lp.L:
+        raise ValueError(f"prefill_forward: {L} layers of {lp.L}")
     rc = load_library().sg_prefill_forward(
-        lp.L, *lp.ptrs, _p(x), T, H, I, nh, nkv, D, Lmax, P0, P0pad, _p(pos), _p(slot), _p(cos_sin), p0, _p(cu_q),
+        L, *lp.ptrs, _p(x), T, H, I, nh, nkv, D, Lmax, P0, P0pad, _p(pos), _p(slot), _p(cos_sin), p0, _p(cu_q),
         _p(q_start), _p(seq_slot), nseq, max_q, float(scale), _p(q), _p(a), _p(act), _p(ss), ld, float(eps),
         cfg_qkv, cfg_o, cfg_gu, cfg_down, _stream())
     _check(rc, "prefill_forward")
@@ -944,10 +948,11 @@ def qa_params(lay, tokenizer) -> QAParams:
 
 def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, ids: torch.Tensor,
               flags: torch.Tensor, params: QAParams, out_buf: torch.Tensor, out_len: torch.Tensor,
-              dbg_scores: Optional[torch.Tensor] = None, dbg_spans: Optional[torch.Tensor] = None) -> None:
+              dbg_scores: Optional[torch.Tensor] = None, dbg_spans: Optional[torch.Tensor] = None,
+              compact: bool = False) -> None:
     """The qa format's head (``qa_decode_kernel``): for every sequence ``m`` of a packed
     prefill batch (rows ``cu[m]:cu[m+1]``, the last ``params.nq`` of them its query
-    rows), scores of the query rows against W (RMSNorm from the un-normed rows ``h``,
+    rows; ``compact``: ``h`` holds only the query rows, ``m * nq ..``), scores of the query rows against W (RMSNorm from the un-normed rows ``h``,
     weight folded into W), the class and every field's joint constrained span decode,
     and the answer in the copy format into ``out_buf[m]`` / ``out_len[m]``.
     ``dbg_scores`` [M, 4 + nf (2 n_pos + 1)] fp32 / ``dbg_spans`` [M, 1 + 2 nf] int32:
@@ -961,7 +966,10 @@ def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, id
         raise ValueError(f"qa_decode: W must be bf16 [>= {R}, {H}]")
     for t, name in ((cu, "cu"), (ids, "ids"), (out_len, "out_len")):
         _req(t, torch.int32, name)
-    if ids.numel() < T or out_len.numel() < M or out_buf.dtype != torch.int32 or not out_buf.is_contiguous():
+    if compact and T < M * params.nq:
+        raise ValueError("qa_decode: compact h needs nq rows per sequence")
+    if out_len.numel() < M or out_buf.dtype != torch.int32 or not out_buf.is_contiguous() or (
+            not compact and ids.numel() < T):
         raise ValueError("qa_decode: ids / out_len / out_buf too small")
     if out_buf.dim() != 2 or out_buf.shape[0] < M or out_buf.shape[1] != params.max_out:
         raise ValueError(f"qa_decode: out_buf must be int32 [>= {M}, {params.max_out}]")
@@ -976,7 +984,7 @@ def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, id
         return
     _check(load_library().sg_qa_decode(ctypes.byref(params), _p(h), h.stride(0), _p(W), H, float(eps), _p(cu),
                                        _p(ids), _p(flags), flags.numel(), _p(out_buf), _p(out_len), _p(dbg_scores),
-                                       _p(dbg_spans), M, _stream()), "qa_decode")
+                                       _p(dbg_spans), M, int(bool(compact)), _stream()), "qa_decode")
 
 
 def embed_rows_add_ids(ids: torch.Tensor, add: torch.Tensor, table: torch.Tensor,

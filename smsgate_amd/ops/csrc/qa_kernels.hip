@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
     QAParams p, const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ W, int H, float eps,
     const int* __restrict__ cu, const int* __restrict__ ids, const uint32_t* __restrict__ flags, int V,
     int* __restrict__ out_buf, int* __restrict__ out_len, float* __restrict__ dbg_scores,
-    int* __restrict__ dbg_spans) {
+    int* __restrict__ dbg_spans, int compact) {
   extern __shared__ __attribute__((aligned(16))) uint16_t hq[];  // [nq][H] bf16
   __shared__ float rs[QA_MAX_NQ];
   __shared__ float sc_start[QA_MAX_NF][QA_MAX_POS];
@@ -123,8 +123,10 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int nq = p.nq, nf = p.nf;
   const int r0 = cu[m], r1 = cu[m + 1];
-  const int qrow0 = r1 - nq;
-  const int n = min(qrow0 - r0 - 1, p.n_pos);  // pointable positions (the body; <ans> excluded)
+  // query rows: the last nq rows of the sequence, or (compact: the engine ran the last
+  // layer on the query rows only) rows m * nq .. of a query-rows-only h
+  const int qrow0 = compact ? m * nq : r1 - nq;
+  const int n = min(r1 - nq - r0 - 1, p.n_pos);  // pointable positions (the body; <ans> excluded)
   const int nch = H >> 3;                       // 16-B chunks per row
 
   // ---- 1. stage
@@ -370,7 +372,7 @@ extern "C" {
 
 int sg_qa_decode(const void* params, const void* h, int ldh, const void* W, int H, float eps, const int* cu,
                  const int* ids, const void* flags, int V, int* out_buf, int* out_len, void* dbg_scores,
-                 void* dbg_spans, int M, hipStream_t stream) {
+                 void* dbg_spans, int M, int compact, hipStream_t stream) {
   const QAParams& p = *reinterpret_cast<const QAParams*>(params);
   if (H % 64 || H > 1024 || ldh % 8 || p.nf <= 0 || p.nf > QA_MAX_NF || p.nq <= 0 || p.nq > QA_MAX_NQ ||
       p.n_pos <= 0 || p.n_pos > QA_MAX_POS || p.max_out <= 0)
@@ -381,7 +383,7 @@ int sg_qa_decode(const void* params, const void* h, int ldh, const void* W, int 
   const size_t lds = (size_t)p.nq * H * sizeof(uint16_t);
   hipLaunchKernelGGL(qa_decode_kernel, dim3(M), dim3(256), lds, stream, p, (const uint16_t*)h, ldh,
                      (const uint16_t*)W, H, eps, cu, ids, (const uint32_t*)flags, V, out_buf, out_len,
-                     (float*)dbg_scores, (int*)dbg_spans);
+                     (float*)dbg_scores, (int*)dbg_spans, compact);
   return (int)hipGetLastError();
 }
 

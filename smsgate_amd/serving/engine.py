@@ -152,6 +152,9 @@ class EngineConfig:
     # qa engine: how long one step() waits for the oldest in-flight batch before it
     # returns (the engine server then polls its connections), and the sleep between
     # event queries while it waits (no busy-wait on the host)
+    # qa engine: the last layer only for the query rows (K / V of every row): the body
+    # rows' last hidden states are never read
+    qa_trim_last: bool = True
     qa_wait_s: float = 0.002
     qa_poll_s: float = 0.0002
 

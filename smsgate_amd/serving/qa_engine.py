@@ -164,7 +164,13 @@ class QAEngine(ExtractionEngine):
         seq_slot = np.arange(r0, r0 + n, dtype=np.int32)
         slot = np.repeat(seq_slot, tl)
         qstart = np.zeros(n, dtype=np.int32)
-        meta = self._stage.to_device(np.concatenate([flat, pos, slot, add, cu, qstart, seq_slot]), dev)
+        trim = self.cfg.qa_trim_last and mc.layers > 1
+        # the last layer on the query rows only: their indices, per-sequence row offsets
+        # and key offsets (the body's length)
+        qidx = (cu[1:, None] - NQ + np.arange(NQ, dtype=np.int32)[None, :]).reshape(-1)
+        cuq = (NQ * np.arange(n + 1)).astype(np.int32)
+        extra = [qidx, cuq, lens.astype(np.int32)] if trim else []
+        meta = self._stage.to_device(np.concatenate([flat, pos, slot, add, cu, qstart, seq_slot] + extra), dev)
         o = 0
         flat_d = meta[o:o + T]; o += T
         pos_d = meta[o:o + T]; o += T
@@ -172,18 +178,46 @@ class QAEngine(ExtractionEngine):
         add_d = meta[o:o + T]; o += T
         cu_d = meta[o:o + n + 1]; o += n + 1
         qstart_d = meta[o:o + n]; o += n
-        seq_slot_d = meta[o:o + n]
+        seq_slot_d = meta[o:o + n]; o += n
         x = ops.embed_rows_add_ids(flat_d, add_d, self.w.embed)
         ss = self._ss_buffer(T, dev)
-        ops.prefill_forward(self._lp, x, H=mc.hidden, I=mc.inter, nh=mc.heads, nkv=mc.kv_heads, D=mc.head_dim,
+        H, I, nh, nkv, D = mc.hidden, mc.inter, mc.heads, mc.kv_heads, mc.head_dim
+        q = torch.empty(T, nh, D, dtype=x.dtype, device=dev)
+        ops.prefill_forward(self._lp, x, H=H, I=I, nh=nh, nkv=nkv, D=D,
                             Lmax=self.Lmax, P0=self.P0, P0pad=self.P0pad, pos=pos_d, slot=slot_d,
                             cos_sin=self.cos_sin, p0=self.P0, cu_q=cu_d, q_start=qstart_d, seq_slot=seq_slot_d,
-                            max_q=int(tl.max()), scale=self.scale,
-                            q=torch.empty(T, mc.heads, mc.head_dim, dtype=x.dtype, device=dev),
-                            a=torch.empty(T, mc.heads * mc.head_dim, dtype=x.dtype, device=dev),
-                            act=torch.empty(T, mc.inter, dtype=x.dtype, device=dev), ss=ss, eps=mc.eps)
-        ops.qa_decode(x, self.w_qa, mc.eps, cu_d, flat_d, self.flags_t, self.params, self.out_buf[r0:],
-                      self.out_len[r0:])
+                            max_q=int(tl.max()), scale=self.scale, q=q,
+                            a=torch.empty(T, nh * D, dtype=x.dtype, device=dev),
+                            act=torch.empty(T, I, dtype=x.dtype, device=dev), ss=ss, eps=mc.eps,
+                            layers=mc.layers - 1 if trim else None)
+        if not trim:
+            ops.qa_decode(x, self.w_qa, mc.eps, cu_d, flat_d, self.flags_t, self.params, self.out_buf[r0:],
+                          self.out_len[r0:])
+            return T
+        Tq = n * NQ
+        qidx_d = meta[o:o + Tq]; o += Tq
+        cuq_d = meta[o:o + n + 1]; o += n + 1
+        lens_d = meta[o:o + n]
+        # last layer: K / V of every row (the query rows attend to the body), everything
+        # else -- attention, o-proj, MLP -- for the query rows only (the body rows' last
+        # hidden states are never read).  Same kernels and reduction orders per row as
+        # the full layer, so the answers are the untrimmed ones (tests/test_qa_gpu.py).
+        i = mc.layers - 1
+        ops.gemm_qkv_rope(x, self.fw_qkv[i], mc.eps, pos_d, slot_d, self.cos_sin, q, self.k_cache[i],
+                          self.vt_cache[i], nh, nkv, self.P0, cfg=ops.qkv_cfg(T, nh, nkv), ss_in=ss)
+        a = torch.empty(Tq, nh * D, dtype=x.dtype, device=dev)
+        ops.attn_prefill(q.index_select(0, qidx_d), cuq_d, lens_d, seq_slot_d, NQ, self.k_cache[i],
+                         self.vt_cache[i], self.pk[i], self.pvt[i], self.P0, a, self.scale)
+        xq = x.index_select(0, qidx_d)
+        ssq = self._ss_buffer(Tq, dev)
+        ops.gemm(a, self.fw_o[i], epi="resid", resid=xq, cfg=ops.gemm_cfg(Tq, H, epi="resid", K=nh * D),
+                 ss_out=ssq)
+        act = ops.gemm(xq, self.fw_gu[i], epi="swiglu", norm_eps=mc.eps,
+                       out=torch.empty(Tq, I, dtype=x.dtype, device=dev),
+                       cfg=ops.gemm_cfg(Tq, 2 * I, epi="swiglu", K=H), ss_in=ssq)
+        ops.gemm(act, self.fw_down[i], epi="resid", resid=xq, cfg=ops.gemm_cfg(Tq, H, epi="resid", K=I))
+        ops.qa_decode(xq, self.w_qa, mc.eps, cu_d, flat_d, self.flags_t, self.params, self.out_buf[r0:],
+                      self.out_len[r0:], compact=True)
         return T
 
     def submit_many(self, items) -> None:

@@ -196,6 +196,20 @@ def test_qa_engine_packed_requests_match_per_message_answers(tk, small_qa):
     assert e2.stats.completed == len(ids)
 
 
+def test_qa_engine_trimmed_last_layer_matches_full(tk, small_qa):
+    """The last layer run on the query rows only (EngineConfig.qa_trim_last, default)
+    answers like the full last layer: the same kernels and per-row reduction orders."""
+    from smsgate_amd.serving.engine import EngineConfig
+    from smsgate_amd.serving.qa_engine import QAEngine
+
+    bodies = [normalize_body(s.body) for s in synth.generate(800, seed=14, vocab_name="heldout", families="all",
+                                                             negatives=0.1)]
+    full = QAEngine(small_qa, tk, EngineConfig(max_slots=1024, qa_max_tokens=1 << 16, qa_trim_last=False)).run(bodies)
+    trim = QAEngine(small_qa, tk, EngineConfig(max_slots=1024, qa_max_tokens=1 << 16)).run(bodies)
+    same = sum(a == b for a, b in zip(full, trim))
+    assert same >= 0.995 * len(bodies), (same, len(bodies))
+
+
 def test_qa_negatives_reach_the_dlq(tk, small_qa, arun):
     """Non-transactions through local_llm (the qa engine behind the backend interface)
     and the parser stage land in sms.failed as {"reason": "unmatched"}, not in

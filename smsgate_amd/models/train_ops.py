@@ -15,10 +15,11 @@ autograd Function with a hand-written backward:
   layout with rotate-half RoPE on q and k (fp32 math, the caller's cos / sin tables);
   backward is the adjoint rotation straight into dqkv;
 * ``SwiGLU``: silu(gate) * up from the fused gate/up GEMM output, and its backward;
-* ``Attention``: causal grouped-query attention over the batch (<= 192 rows) straight
-  into the o-proj's [B, T, heads * 64] input, log-sum-exp saved, and its backward (two
-  kernels recomputing the probabilities).  SDPA made one synchronous host-to-device
-  copy per call, so the host could never run ahead of the GPU (63 per step).
+* ``Attention`` (opt-in, ``SMSGATE_TRAIN_SDPA=own``): causal grouped-query attention over
+  the batch (<= 192 rows) straight into the o-proj's [B, T, heads * 64] input and its
+  backward -- correct (fp32-reference tests) but one thread per row is latency-bound:
+  56 ms of a step against SDPA's ~6 (``r05_train_step_sdpa_ab.jsonl``), so SDPA (flash)
+  stays the default.
 
 GEMMs stay hipBLASLt (autocast bf16), so the math is
 reference_forward's up to bf16 rounding order (tests/test_train_ops_gpu.py compares
@@ -216,12 +217,13 @@ def fused_forward(w: ExtractorWeights, ids: torch.Tensor, add_ids: Optional[torc
     cos, sin = _rope_tables(T, D, cfg.rope_theta, ids.device)
     cos, sin = cos.reshape(T, D // 2).contiguous(), sin.reshape(T, D // 2).contiguous()
     scale = 1.0 / math.sqrt(D)
-    # attention: the training kernels (attn_train_*) up to 192 rows, else SDPA (flash); the
-    # efficient SDPA backend has no GQA support, so it gets k / v expanded to nh heads by
-    # rope_split (its adjoint sums them)
+    # attention: SDPA (flash) by default; SMSGATE_TRAIN_SDPA=own runs the attn_train_*
+    # kernels (<= 192 rows; correct, but 56 vs ~6 ms per step: one thread per row is
+    # latency-bound, r05_train_step_sdpa_ab.jsonl); the efficient backend has no GQA
+    # support, so it gets k / v expanded to nh heads by rope_split (its adjoint sums them)
     sdpa = os.environ.get("SMSGATE_TRAIN_SDPA", "")
     rep = nh // nkv if sdpa == "efficient" else 1
-    own = not sdpa and T <= ATTN_MAX_T
+    own = sdpa == "own" and T <= ATTN_MAX_T
     with _sdpa_backend():
         for i in range(cfg.layers):
             x = _layer(w, i, x, cos, sin, scale, B, T, nh, nkv, D, rep, own)
@@ -232,7 +234,7 @@ def _sdpa_backend():
     """SMSGATE_TRAIN_SDPA = flash | efficient | math pins SDPA's backend (A/B of the
     training step, scripts/train_step_profile.py); default: PyTorch's choice."""
     name = os.environ.get("SMSGATE_TRAIN_SDPA", "")
-    if not name:
+    if name in ("", "own"):
         return contextlib.nullcontext()
     from torch.nn.attention import SDPBackend, sdpa_kernel
 

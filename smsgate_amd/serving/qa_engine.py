@@ -261,9 +261,8 @@ class QAEngine(ExtractionEngine):
             m, t = len(u.lens), int(u.lens.sum()) + self.NQ * len(u.lens)
             if units and (n + m > S or ntok + t > self.max_tokens):
                 break
-            if m > S or t > self.max_tokens:
-                raise ValueError(f"a request of {m} prompts / {t} tokens exceeds the engine's batch "
-                                 f"({S} slots, {self.max_tokens} tokens)")
+            if m > S:  # the token budget is soft (a request larger than it runs alone); slots are not
+                raise ValueError(f"a request of {m} prompts exceeds the engine's {S} slots")
             self.waiting.popleft()
             units.append(u)
             n += m

@@ -109,7 +109,7 @@ def test_attention_forward_backward(T):
         assert _rel(got, want) < 2e-2
 
 
-@pytest.mark.parametrize("sdpa", ["", "efficient"])
+@pytest.mark.parametrize("sdpa", ["", "efficient", "own"])
 def test_fused_forward_matches_reference_forward(sdpa, monkeypatch):
     """Loss and every gradient of the fused training forward agree with
     reference_forward's (both bf16 autocast over fp32 master weights); also with the

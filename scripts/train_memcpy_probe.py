@@ -22,17 +22,26 @@ def main() -> int:
     data = make_examples(tok, answer_fsm(tok, "qa"), 2048, seed=1, negatives=0.12)
     tc = TrainConfig(steps=4, batch=128, n_examples=len(data), log_every=0, answer_format="qa", warmup=2)
     train_extractor(tc, device="cuda", data=data, log=lambda s: None)
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=True) as prof:
         train_extractor(tc, device="cuda", data=data, log=lambda s: None)
         torch.cuda.synchronize()
     by_op, stacks = collections.Counter(), {}
+    parents = collections.Counter()
     for e in prof.events():
         for k in getattr(e, "kernels", []) or []:
-            if "Memcpy HtoD" in k.name or "HtoD" in k.name:
-                by_op[e.name] += 1
-                if e.name not in stacks:
-                    stacks[e.name] = [str(f) for f in (e.stack or [])][:12]
-    print(json.dumps({"htod_by_cpu_op": by_op.most_common(20), "stacks": stacks}, indent=1))
+            if "HtoD" in k.name:
+                key = f"{e.name} {e.input_shapes}"
+                by_op[key] += 1
+                chain, p = [], e.cpu_parent
+                while p is not None and len(chain) < 8:
+                    chain.append(p.name)
+                    p = p.cpu_parent
+                parents[" <- ".join(chain)] += 1
+                if key not in stacks:
+                    stacks[key] = [str(f) for f in (e.stack or [])][:12]
+    print(json.dumps({"htod_by_cpu_op": by_op.most_common(20), "parents": parents.most_common(20), "stacks": stacks},
+                     indent=1))
     return 0
 
 

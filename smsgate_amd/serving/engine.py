@@ -155,6 +155,9 @@ class EngineConfig:
     # qa engine: the last layer only for the query rows (K / V of every row): the body
     # rows' last hidden states are never read
     qa_trim_last: bool = True
+    # qa engine: rows that must be waiting before a SECOND batch is launched behind the
+    # one in flight (the first always launches at once)
+    qa_min_tokens: int = 65536
     qa_wait_s: float = 0.002
     qa_poll_s: float = 0.0002
 

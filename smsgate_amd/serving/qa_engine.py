@@ -57,6 +57,7 @@ class _Unit:
     lens: np.ndarray  # int32 [n] prompt lengths (capped)
     flat: np.ndarray  # int32 [sum(lens)] prompt ids
     packed: bool
+    ntok: int = 0  # rows it adds to a batch (prompts + query tokens)
 
 
 @dataclass
@@ -233,7 +234,7 @@ class QAEngine(ExtractionEngine):
             a = np.asarray(ids, dtype=np.int32)
             if len(a) > cap:  # keep the closing <ans>
                 a = np.concatenate([a[: cap - 1], a[-1:]])
-            self.waiting.append(_Unit(k, np.asarray([len(a)], dtype=np.int32), a, False))
+            self.waiting.append(_Unit(k, np.asarray([len(a)], dtype=np.int32), a, False, len(a) + self.NQ))
 
     def submit_packed(self, key: Any, lens: np.ndarray, ids: np.ndarray) -> None:
         """Queue a whole request (wire lengths / ids); answered by :meth:`step` as
@@ -249,7 +250,7 @@ class QAEngine(ExtractionEngine):
                 a, b = int(ends[i] - lens[i]), int(ends[i])
                 keep[a + cap - 1:b - 1] = False
             ids, lens = ids[keep], np.minimum(lens, cap)
-        self.waiting.append(_Unit(key, lens, ids, True))
+        self.waiting.append(_Unit(key, lens, ids, True, int(lens.sum()) + self.NQ * len(lens)))
 
     def _launch(self) -> Optional[_Batch]:
         ec = self.cfg
@@ -258,7 +259,7 @@ class QAEngine(ExtractionEngine):
         S = ec.max_slots
         while self.waiting:
             u = self.waiting[0]
-            m, t = len(u.lens), int(u.lens.sum()) + self.NQ * len(u.lens)
+            m, t = len(u.lens), u.ntok
             if units and (n + m > S or ntok + t > self.max_tokens):
                 break
             if m > S:  # the token budget is soft (a request larger than it runs alone); slots are not
@@ -357,6 +358,11 @@ class QAEngine(ExtractionEngine):
         while self._inflight and self._inflight[0].event.query():
             out += self._harvest_batch(self._inflight.popleft(), raw)
         while self.waiting and len(self._inflight) < 2:
+            # a second batch only once enough has queued: launching every trickle at once
+            # (HTTP ingest) made batches of a few hundred rows, at a fraction of the
+            # GPU's large-batch rate (profiles/r05_qa_engine_budget_sweep.jsonl)
+            if self._inflight and sum(u.ntok for u in self.waiting) < self.cfg.qa_min_tokens:
+                break
             new = self._launch()
             if new is None:
                 break
@@ -365,7 +371,8 @@ class QAEngine(ExtractionEngine):
                     self._idle_pairs.append((self._idle_prev, new.start_event))
                 self._idle_prev = new.event
             self._inflight.append(new)
-        if not out and self._inflight and (len(self._inflight) >= 2 or not self.waiting):
+        if not out and self._inflight and (len(self._inflight) >= 2 or not self.waiting
+                                           or sum(u.ntok for u in self.waiting) < self.cfg.qa_min_tokens):
             if self._wait(self._inflight[0].event, self.cfg.qa_wait_s):
                 out = self._harvest_batch(self._inflight.popleft(), raw)
         while self._idle_pairs and self._idle_pairs[0][1].query():

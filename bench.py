@@ -971,7 +971,7 @@ def main(argv=None) -> int:
         if cpu is not None:
             out["cpu"] = cpu_budget(cpu, dt, total, world)
         if http_res is not None:
-            hdt, hcounts, hcpu, _, hhttp = http_res
+            hdt, hcounts, hcpu, hest, hhttp = http_res
             hrouted = hcounts.get("ok", 0) + hcounts.get("fail", 0) + hcounts.get("skip", 0)
             if hrouted != total or hhttp["accepted"] != total or hhttp["rejected"]:
                 raise SystemExit(f"bench: HTTP ingest phase routed {hrouted} / accepted {hhttp['accepted']} "
@@ -985,6 +985,8 @@ def main(argv=None) -> int:
                 "routing": {"parsed": hcounts.get("parsed", 0), "keyword_skipped": hcounts.get("keyword_skipped", 0),
                             "broken": hcounts.get("skip", 0), "dlq": hcounts.get("fail", 0)},
                 "cpu": cpu_budget(hcpu, hdt, total, world)}
+            if args.verbose and hest:
+                out["http_ingest"]["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in hest.items()}
         if bus_members is not None:
             # messages held per node broker over the whole run (warmup included): every
             # partition of sms.raw / sms.parsed must carry traffic

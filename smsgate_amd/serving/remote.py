@@ -57,6 +57,40 @@ class EngineServer:
         self._sel = selectors.DefaultSelector()
         for i, c in enumerate(self.conns):
             self._sel.register(c, selectors.EVENT_READ, i)
+        # responses leave through a sender thread: a parser process that is slow to read
+        # (its reader thread waits for the GIL) filled its socket and blocked the engine
+        # loop inside send_bytes -- 1.7 s of a 3.2 s phase with the GPU idle behind it
+        self._outq: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._sender: Optional[threading.Thread] = None
+
+    def _send(self, c: Connection, frame: bytes) -> None:
+        """Queue ``frame`` for ``c`` (per-connection order kept: one FIFO, one thread)."""
+        if self._sender is None:
+            self._sender = threading.Thread(target=self._send_loop, name="engine-send", daemon=True)
+            self._sender.start()
+        self._outq.put((c, frame))
+
+    def _send_loop(self) -> None:
+        while True:
+            item = self._outq.get()
+            if item is None:
+                return
+            c, frame = item
+            if c is None:  # a flush marker
+                frame.set()
+                continue
+            try:
+                c.send_bytes(frame)
+            except (OSError, EOFError, ValueError):  # the client went away: its reads fail too
+                pass
+
+    def flush(self, timeout: float = 30.0) -> None:
+        """Wait until every queued frame has been handed to the sockets."""
+        if self._sender is None:
+            return
+        done = threading.Event()
+        self._outq.put((None, done))
+        done.wait(timeout)
 
     def add_connection(self, conn: Connection) -> int:
         self.conns.append(conn)
@@ -75,7 +109,8 @@ class EngineServer:
     def send_control(self, idx: int, obj: Any) -> None:
         c = self.conns[idx]
         if c is not None:
-            c.send_bytes(P.pack_control(obj))
+            self._send(c, P.pack_control(obj))
+            self.flush()  # control frames (harness commands) leave before the caller goes on
 
     def _live(self) -> List[Connection]:
         return [c for c in self.conns if c is not None]
@@ -107,7 +142,7 @@ class EngineServer:
                     if self._packed:  # the whole request is one engine unit (QAEngine.submit_packed)
                         _, rid, lens, flat = P.unpack_arrays(buf)
                         if not len(lens):
-                            c.send_bytes(P.pack_ids(b"R", rid, []))
+                            self._send(c, P.pack_ids(b"R", rid, []))
                         else:
                             self.engine.submit_packed((idx, rid), lens, flat)
                         if not c.poll():
@@ -115,7 +150,7 @@ class EngineServer:
                         continue
                     _, rid, seqs = P.unpack_id_arrays(buf)
                     if not seqs:
-                        c.send_bytes(P.pack_ids(b"R", rid, []))
+                        self._send(c, P.pack_ids(b"R", rid, []))
                     else:
                         self.reqs[(idx, rid)] = _Req(idx, rid, [None] * len(seqs), len(seqs))
                         self.engine.submit_ids([((idx, rid, i), s) for i, s in enumerate(seqs)])
@@ -137,7 +172,7 @@ class EngineServer:
             for idx, rid in keys:
                 c = self.conns[idx]
                 if c is not None:
-                    c.send_bytes(P.pack_error(rid, repr(exc)))
+                    self._send(c, P.pack_error(rid, repr(exc)))
             self.reqs.clear()
             self.engine.waiting.clear()
             self.engine.active.clear()
@@ -151,7 +186,7 @@ class EngineServer:
                 idx, rid = key
                 c = self.conns[idx]
                 if c is not None:
-                    c.send_bytes(P.pack_arrays(b"R", rid, toks.lens, toks.flat))
+                    self._send(c, P.pack_arrays(b"R", rid, toks.lens, toks.flat))
                 self.served += len(toks.lens)
                 continue
             idx, rid, i = key
@@ -166,7 +201,7 @@ class EngineServer:
                 if c is not None:
                     lens = np.fromiter((len(t) for t in r.out), dtype=np.uint16, count=len(r.out))
                     flat = np.concatenate(r.out) if r.out else np.zeros(0, np.int32)
-                    c.send_bytes(P.pack_arrays(b"R", rid, lens, flat))
+                    self._send(c, P.pack_arrays(b"R", rid, lens, flat))
                 self.served += len(r.out)
         st = getattr(self.engine, "stats", None)
         if st is not None and hasattr(st, "server_send_s"):
@@ -207,6 +242,7 @@ class EngineServer:
             self.serve_until(pred)
         finally:
             listener.close()
+            self.flush(5.0)  # answers already produced reach their clients
             for i, c in enumerate(self.conns):  # clients see EOF (and reconnect to the next server)
                 if c is None:
                     continue

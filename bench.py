@@ -171,6 +171,8 @@ def _args(argv=None):
                    help="A/B: attention walks the shared-prefix tiles, then the own-key tiles (ops.set_attn_merge)")
     p.add_argument("--prefill-key-split", type=int, default=1, choices=[1, 2],
                    help="waves sharing each prefill attention tile's keys")
+    p.add_argument("--qa-min-tokens", type=int, default=None,
+                   help="EngineConfig.qa_min_tokens: rows queued before a second in-flight qa batch")
     p.add_argument("--split-prefill", type=int, default=None,
                    help="prefill batches of >= N tokens run as two halves on two streams (0 = off)")
     p.add_argument("--spec-policy", type=int, default=0, help="draft policy (EngineConfig.spec_policy)")
@@ -623,7 +625,7 @@ def engine_kwargs(args) -> dict:
                         admit_min_fraction=args.admit_frac, spec_k=args.spec_k, spec_draft_frac=args.spec_frac,
                         split_decode=args.split_decode, split_prefill=args.split_prefill,
                         copy_constrain=False if args.no_copy else None, prefill_attn=args.prefill_attn,
-                        template_slots=args.template_slots)
+                        template_slots=args.template_slots, qa_min_tokens=args.qa_min_tokens)
     if args.bucket_step:
         kw["buckets"] = tuple(range(args.bucket_step, kw["max_slots"] + 1, args.bucket_step))
     return kw

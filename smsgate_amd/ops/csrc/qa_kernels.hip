@@ -23,7 +23,8 @@
 //      ends with a letter and b starts with one, or a ends with a digit and b starts
 //      with one), and a lone separator between a digit and a three-digit group joins
 //      them ("218" "," "993").  A date span with no time of day then takes the time
-//      token right before (else right after) it when that longer span is valid.
+//      token right before (else right after) it when that longer span is valid, and a
+//      span ending in a digit a following AM / PM.
 //      One lane per start, its ends scanned in order;
 //      ties go to the lower start, then the lower end (serving/qa.py qa_decode_ref);
 //   4. the answer in the copy format (class tokens, <sep>, each field's body tokens
@@ -50,6 +51,9 @@
 #define QF_GRP3 16384  // exactly three ASCII digits
 #define QF_SEP 32768   // a lone "," "." "'"
 #define QF_TIME 65536  // a whole time of day (" 22:09")
+#define QF_AMPM (1 << 18)  // " AM" / " PM"
+#define QF_AP (1 << 19)    // " A" / " P" (a split " AM" / " PM")
+#define QF_M (1 << 20)     // "M"
 
 struct QAParams {
   int nf, nq, n_pos;
@@ -272,6 +276,15 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
         else if (!timed && be + 1 < n && (fb[be + 1] & QF_TIME) && be - bs + 1 < cap && qa_in_cls(fb[be + 1], cls) &&
                  qa_end_ok(fb, n, be + 1, eneed))
           be += 1;
+        // then a span ending in a digit takes a following AM / PM
+        if (fb[be] & QF_LD) {
+          if (be + 1 < n && (fb[be + 1] & QF_AMPM) && be - bs + 1 < cap && qa_in_cls(fb[be + 1], cls) &&
+              qa_end_ok(fb, n, be + 1, eneed))
+            be += 1;
+          else if (be + 2 < n && (fb[be + 1] & QF_AP) && (fb[be + 2] & QF_M) && be - bs + 2 < cap &&
+                   qa_in_cls(fb[be + 1], cls) && qa_in_cls(fb[be + 2], cls) && qa_end_ok(fb, n, be + 2, eneed))
+            be += 2;
+        }
       }
       span_s[f] = null ? -1 : bs;
       span_e[f] = null ? -1 : be;

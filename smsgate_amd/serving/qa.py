@@ -31,7 +31,8 @@ the causal model lets every query row attend to the whole body:
   one word).  Value edges by kind (:data:`EDGE_RULES`): a number starts and ends with
   a digit, a card ends with one, a date or a free-text value starts and ends with a
   letter or digit; no value crosses a line break.  A date span without a time of day
-  takes the time token right next to it ("22:09 13.02.2023": the value is a datetime).
+  takes the time token right next to it ("22:09 13.02.2023": the value is a datetime),
+  and one ending in digits takes a following AM / PM ("2:23 PM").
 
 The answer is written in the copy format (txn tokens, then each field's body
 tokens, each ended by ``<sep>``), so the tokenizers' field decoders, the remote
@@ -52,7 +53,7 @@ from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
            "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
            "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP",
-           "QF_TIME", "QF_DEND"]
+           "QF_TIME", "QF_DEND", "QF_AMPM", "QF_AP", "QF_M"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
@@ -66,6 +67,9 @@ _NO_START_AFTER_MASK = QA_CLASS_BITS["date"] | QA_CLASS_BITS["number"]
 QF_NL, QF_FA, QF_FD, QF_LA, QF_LD, QF_GRP3, QF_SEP = 512, 1024, 2048, 4096, 8192, 16384, 32768
 QF_TIME = 1 << 16  # a whole time of day: " 22:09", "05:27:11"
 QF_DEND = 1 << 17  # may end a date: last char a digit, or AM / PM
+QF_AMPM = 1 << 18  # " AM" / " PM" as one token
+QF_AP = 1 << 19  # " A" / " P": the first piece of a split " AM" / " PM"
+QF_M = 1 << 20  # "M": its second piece
 _TIME_RE = re.compile(r" ?\d{1,2}:\d{2}(?::\d{2})?\Z")
 # field kind -> (flags its first token must all have, flags its last token must all have).
 # A date ends with a digit or AM / PM (a span into the next word -- "12.05.25 покупка",
@@ -185,6 +189,12 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
             f |= QF_TIME
         if t[-1].isdigit() or t.strip().upper() in ("AM", "PM", "M"):  # "PM" is " P" + "M"
             f |= QF_DEND
+        if t.upper() in (" AM", " PM"):
+            f |= QF_AMPM
+        if t.upper() in (" A", " P"):
+            f |= QF_AP
+        if t.upper() == "M":
+            f |= QF_M
         out[i] |= f
     return out
 
@@ -305,13 +315,18 @@ def _pair_mask(fb: np.ndarray, n: int, cls: int, cap: int, s_need: int = 0,
 
 def _absorb_time(fb: np.ndarray, pairs: np.ndarray, a: int, z: int, n: int) -> Tuple[int, int]:
     """A date span (a, z) with no time-of-day token takes the one right before it, else
-    the one right after it, when the longer span is itself a valid pair."""
-    if (fb[a:z + 1] & QF_TIME).any():
-        return a, z
-    if a > 0 and fb[a - 1] & QF_TIME and pairs[a - 1, z]:
-        return a - 1, z
-    if z + 1 < n and fb[z + 1] & QF_TIME and pairs[a, z + 1]:
-        return a, z + 1
+    the one right after it, when the longer span is itself a valid pair; then a span
+    ending in a digit takes a following " AM" / " PM" (one token or " A" / " P" + "M")."""
+    if not (fb[a:z + 1] & QF_TIME).any():
+        if a > 0 and fb[a - 1] & QF_TIME and pairs[a - 1, z]:
+            a -= 1
+        elif z + 1 < n and fb[z + 1] & QF_TIME and pairs[a, z + 1]:
+            z += 1
+    if fb[z] & QF_LD:
+        if z + 1 < n and fb[z + 1] & QF_AMPM and pairs[a, z + 1]:
+            z += 1
+        elif z + 2 < n and fb[z + 1] & QF_AP and fb[z + 2] & QF_M and pairs[a, z + 2]:
+            z += 2
     return a, z
 
 

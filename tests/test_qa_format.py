@@ -149,6 +149,8 @@ def test_value_edges_follow_the_field_kind(env):
     ("Оплата 13.02.2023 22:09 на сумму 5.00 RUB", "13.02.2023", "13.02.2023 22:09"),
     ("Оплата 13.02.2023 22:09 на сумму 5.00 RUB", "13.02.2023 22:09", "13.02.2023 22:09"),
     ("Оплата 13.02.2023 на сумму 5.00 RUB", "13.02.2023", "13.02.2023"),
+    ("card 0849: Purchase 5.00 USD. Jan 14, 2025 11:49 PM. Available", "Jan 14, 2025 11:49", "Jan 14, 2025 11:49 PM"),
+    ("card 0849: Purchase 5.00 USD. Nov 26, 2023 9:48 AM. Avl", "Nov 26, 2023 9:48", "Nov 26, 2023 9:48 AM"),
 ])
 def test_date_span_takes_the_adjacent_time(env, body, picked, want):
     """A date span without a time of day takes the time token next to it (the r05 error

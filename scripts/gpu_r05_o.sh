@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 5: parser processes per GPU A/B (the parsers ran at 7.0 of 8 cores at 65 k msgs/s).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+O=gpurun_out/r05o
+mkdir -p $O
+for w in 10 8 10; do
+  timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 2 --verbose --cpu-workers $w \
+    >> $O/workers_ab.jsonl 2>> $O/workers_ab.err || { echo "bench w=$w rc=$?"; tail -40 $O/workers_ab.err; exit 1; }
+  tail -1 $O/workers_ab.jsonl | cut -c1-120
+done

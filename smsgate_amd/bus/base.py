@@ -132,7 +132,7 @@ class ConsumerConfig:
         self.deliver_policy = DeliverPolicy(self.deliver_policy)
 
 
-@dataclass
+@dataclass(slots=True)  # one per published message
 class PubAck:
     stream: str
     seq: int
@@ -182,7 +182,7 @@ def default_stream_config(max_age: float = 3 * 24 * 3600.0) -> StreamConfig:
     return StreamConfig(name=STREAM_NAME, subjects=list(ALL_SUBJECTS), max_age=max_age)
 
 
-@dataclass
+@dataclass(slots=True)  # one per delivered message: no per-instance dict
 class MsgMetadata:
     sequence: int
     num_delivered: int

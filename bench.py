@@ -204,7 +204,7 @@ def _args(argv=None):
                         "POST /sms/raw/batch")
     p.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
                    help="NUMA placement of the rank / parser / broker processes (parallel/placement.py); auto = "
-                        "only when this job holds every GPU of the node")
+                        "when this job holds every GPU it can see")
     p.add_argument("--profile-cpu", default=None, metavar="DIR",
                    help="profile the timed bus phase of every parser process and of the rank process into DIR "
                         "(parser-r<rank>-w<k>.samples.json / .pstats, rank<rank>.samples.json / .pstats)")
@@ -513,9 +513,11 @@ def evaluate_quality(engine, args) -> dict:
 def pin_replica(args, local: int, procs, brokers):
     """NUMA placement (parallel/placement.py): this rank and its parser processes on
     the cores of its GPU's NUMA node, the node's brokers (local rank 0) on a reserved
-    pair.  ``--pin auto`` pins only when the job holds every GPU of the node (a
-    shared single-GPU box keeps the scheduler's placement).  Returns the plan for
-    the JSON line (None: nothing pinned / no topology)."""
+    pair.  ``--pin auto`` pins when the job holds every GPU it can see -- the whole
+    8-GPU node, or a one-GPU box (+4 % through the brokers, +5 % through the HTTP doors
+    there, interleaved: profiles/r05_pin_ab.jsonl); a job holding some of a node's GPUs
+    keeps the scheduler's placement.  Returns the plan for the JSON line (None: nothing
+    pinned / no topology)."""
     if args.pin == "off" or args.cpu_echo_engine:
         return None
     from smsgate_amd.parallel.placement import gpu_topology, plan
@@ -526,9 +528,9 @@ def pin_replica(args, local: int, procs, brokers):
     if p is None:
         return {"pinned": False, "why": "no GPU topology in sysfs"}
     n_topo = len(gpu_topology())
-    if args.pin == "auto" and (node_gpus < 2 or node_gpus != n_topo):
-        # a single-GPU job shares its machine (the other GPUs' jobs, cgroup CPU quotas):
-        # the scheduler places it; a job holding every GPU of the node owns the placement
+    if args.pin == "auto" and node_gpus != n_topo:
+        # a job holding part of a node shares the machine with the other GPUs' jobs: the
+        # scheduler places it; a job holding every visible GPU owns the placement
         return {"pinned": False, "why": f"auto: the job holds {node_gpus} GPU(s) of the {n_topo} visible",
                 **p.describe()}
     p.apply(rank_pid=0, worker_pids=[q.pid for q in procs], broker_pids=[b.pid for b in (brokers or [])])

@@ -48,6 +48,15 @@ def test_prefill_and_decode_logits_match_reference(tiny_engine):
                 assert int(lg[b].argmax()) == int(ref.argmax())
 
 
+def _date_chars():
+    from smsgate_amd.serving.fsm import _CLASS_CHARS
+
+    return set(_CLASS_CHARS["date"])
+
+
+_DATE_CHARS = _date_chars()
+
+
 def test_engine_runs_and_respects_schema(tiny_engine):
     eng = tiny_engine
     bodies = generate_bodies(150, seed=9)  # > max_slots: exercises continuous refill
@@ -56,8 +65,11 @@ def test_engine_runs_and_respects_schema(tiny_engine):
     for r in res:
         assert set(r) == {"txn_type", "date", "amount", "currency", "card", "merchant", "city", "address", "balance"}
         assert r["txn_type"] in ("debit", "credit", "otp", "unknown")
-        # the date class (serving/fsm.py): digits, separators and ASCII letters (month names, ISO "T")
-        assert set(r["date"]) <= set("0123456789.:/-, ") | set("ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz")
+        if r["txn_type"] in ("otp", "unknown"):  # a rejection: null fields (serving/qa.py null_rejection)
+            assert all(r[k] is None for k in r if k != "txn_type"), r
+            continue
+        # the date class (serving/fsm.py): digits, separators, month-name letters, ISO "T"
+        assert set(r["date"]) <= _DATE_CHARS, r["date"]
         assert set(r["card"]) <= set("0123456789* ")
     assert eng.stats.completed >= 150
     assert not eng.busy() and len(eng.free_rows) == eng.cfg.max_slots

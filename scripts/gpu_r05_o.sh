@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/r05o
 mkdir -p $O
 for w in 10 8 10 8; do
-  timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 2 --verbose --cpu-workers $w \
+  timeout -k 10 900 python -u bench.py --gpus 1 --steps 20 --warmup 2 --verbose --cpu-workers $w --msgs-per-step 16000 \
     >> $O/workers_ab.jsonl 2>> $O/workers_ab.err || { echo "bench w=$w rc=$?"; tail -40 $O/workers_ab.err; exit 1; }
   tail -1 $O/workers_ab.jsonl | cut -c1-120
 done

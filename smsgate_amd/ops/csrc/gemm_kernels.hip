@@ -445,16 +445,38 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       // V^T address is a scalar base + 16 B x lane
       static_assert(BM <= 128, "V^T scatter: rows per lane register");
       const int kh0 = h0 - ra.nh - ra.nkv, nb = ra.Lmax >> 3;
+      // (position, slot) of tile row r (wave-uniform r): broadcast from the lane registers
+      auto pos_of = [&](int r) {
+        return __builtin_amdgcn_readlane((BM > 64 && (r >> 6)) ? epos[VU - 1] : epos[0], r & 63);
+      };
+      auto slot_of = [&](int r) {
+        return __builtin_amdgcn_readlane((BM > 64 && (r >> 6)) ? eslot[VU - 1] : eslot[0], r & 63);
+      };
       for (int row = __builtin_amdgcn_readfirstlane(wave); row < BM; row += NW) {
         const int gr = m0 + row;
         if (gr >= M) break;
-        const int u = BM > 64 ? (row >> 6) : 0;
-        const int p = __builtin_amdgcn_readlane(u ? epos[VU - 1] : epos[0], row & 63);
-        const int sl = __builtin_amdgcn_readlane(u ? eslot[VU - 1] : eslot[0], row & 63);
+        const int p = pos_of(row), sl = slot_of(row);
+        // V^T blocks hold 8 consecutive positions per dim: when the tile has all 8 rows of
+        // this row's block (one sequence, positions 8k .. 8k+7), its first row writes them
+        // as one 16-B chunk per dim and the others skip; partial blocks (sequence / tile
+        // edges) are written element by element
+        const int g = row - (p & 7);
+        const bool full = g >= 0 && g + 7 < BM && m0 + g + 7 < M && slot_of(g) == sl && pos_of(g) == p - (p & 7) &&
+                          slot_of(g + 7) == sl && pos_of(g + 7) == p - (p & 7) + 7;
+        if (full && g != row) continue;
 #pragma unroll
         for (int j = 0; j < HT; ++j) {
-          const size_t base = (((size_t)sl * ra.nkv + kh0 + j) * nb + (p >> 3)) * 512 + (p & 7);
-          ra.vt_cache[base + (size_t)lane * 8] = Cs[row * CST + j * 64 + lane];
+          const size_t base = (((size_t)sl * ra.nkv + kh0 + j) * nb + (p >> 3)) * 512;
+          if (full) {
+            uint32_t w[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              w[e] = (uint32_t)Cs[(row + 2 * e) * CST + j * 64 + lane] |
+                     ((uint32_t)Cs[(row + 2 * e + 1) * CST + j * 64 + lane] << 16);
+            *reinterpret_cast<uint4*>(ra.vt_cache + base + (size_t)lane * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+          } else {
+            ra.vt_cache[base + (p & 7) + (size_t)lane * 8] = Cs[row * CST + j * 64 + lane];
+          }
         }
       }
     }

@@ -280,6 +280,38 @@ def test_gemm_qkv_rope_matches_unfused(cfg, M):
         torch.testing.assert_close(a.float(), b.float(), atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("cfg", [1, 3, 17, 23, 28])
+def test_gemm_qkv_rope_packed_sequences(cfg):
+    """Packed prefill rows (sequences of 1..70 tokens at positions 0.., one slot each):
+    the epilogue writes whole 8-position V^T blocks as 16-B chunks when a tile holds all
+    8 rows of one, element by element at sequence and tile edges -- the caches equal the
+    unfused path's exactly."""
+    nh, nkv, D, S, Lmax, K, p0 = 9, 3, 64, 512, 192, 576, 6
+    g = torch.Generator(device="cpu").manual_seed(61)
+    lens = torch.randint(1, 71, (300,), generator=g)
+    M = int(lens.sum())
+    pos = torch.cat([torch.arange(int(n)) for n in lens]).to(torch.int32).to(DEV)
+    slot = torch.repeat_interleave(torch.randperm(S, generator=g)[:300], lens).to(torch.int32).to(DEV)
+    x = _bf(M, K, seed=62)
+    w = _bf((nh + 2 * nkv) * D, K, scale=K ** -0.5, seed=63)
+    cs = ops.rope_table(p0 + Lmax + 1, D, 100000.0, DEV)
+    caches = []
+    for fused in (True, False):
+        kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
+        vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=DEV)
+        q = torch.zeros(M, nh, D, dtype=torch.bfloat16, device=DEV)
+        if fused:
+            ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, p0, cfg=cfg)
+        else:
+            qkv = ops.gemm(x, w, norm_eps=1e-5, cfg=cfg)
+            ops.rope_qkv_cache(qkv, pos, slot, cs, q, kc, vt, nh, nkv, D, p0)
+        caches.append((q, kc, vt))
+    (qa, ka, va), (qb, kb, vb) = caches
+    assert torch.equal(va, vb)  # V^T: copied values, exact
+    torch.testing.assert_close(qa.float(), qb.float(), atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(ka.float(), kb.float(), atol=1e-2, rtol=1e-2)
+
+
 @pytest.mark.parametrize("cfg", [0, 3, 17])
 @pytest.mark.parametrize("M", [1, 77, 700])
 def test_gemm_argmax_matches_logits_path(cfg, M):

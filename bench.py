@@ -523,8 +523,10 @@ def pin_replica(args, local: int, procs, brokers):
     from smsgate_amd.parallel.placement import gpu_topology, plan
 
     node_gpus = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
-    # one core per node broker (single-threaded event loops: 9 on an 8-GPU node)
-    p = plan(local, node_gpus, broker_cores=len(brokers) if brokers else 0)
+    # the node's brokers share 2 + one core per GPU (they are single-threaded event loops,
+    # but 29 of them carry ~0.3 - 0.8 cores per GPU together: a core each would take 29
+    # cores from GPU 0's NUMA node)
+    p = plan(local, node_gpus, broker_cores=min(len(brokers), 2 + node_gpus) if brokers else 0)
     if p is None:
         return {"pinned": False, "why": "no GPU topology in sysfs"}
     n_topo = len(gpu_topology())

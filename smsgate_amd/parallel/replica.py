@@ -403,18 +403,20 @@ class Coordinator:
         for i in range(self.n):
             self.server.send_control(i, obj)
 
-    def run_phase(self, seeds_per_worker: Sequence[Sequence[int]], n_per_step: int,
+    def run_phase(self, seeds_per_worker: Sequence[Sequence[int]], n_per_step,
                   sync=None, profile: bool = False) -> Tuple[float, Dict[str, int]]:
         """Prepare (untimed), then time ``go`` → all ``done``. Returns (seconds, routing counts).
-        ``profile``: the parser processes cProfile this phase (when they were started with
+        ``n_per_step``: messages per step and connection (an int, or one per connection).
+        ``profile``: the parser processes profile this phase (when they were started with
         a profile_dir)."""
         self.last_http = {}
+        per = [n_per_step] * self.n if isinstance(n_per_step, int) else list(n_per_step)
         for i in range(self.n):
-            self.server.send_control(i, {"cmd": "prepare", "n": n_per_step, "seeds": list(seeds_per_worker[i])})
+            self.server.send_control(i, {"cmd": "prepare", "n": per[i], "seeds": list(seeds_per_worker[i])})
         self.wait_all("prepared")
         target = 0
         if self.bus is not None:
-            n_raw = sum(len(s) for s in seeds_per_worker) * n_per_step * self.node_ranks
+            n_raw = sum(len(s) * k for s, k in zip(seeds_per_worker, per)) * self.node_ranks
             target = self.bus.consumer_info("SMS", self.COUNTER)["num_pending"] + n_raw
         if sync is not None:
             sync()

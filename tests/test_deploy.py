@@ -18,7 +18,14 @@ def test_compose_is_an_8_gpu_node():
         assert v["environment"]["LLM_CHECKPOINT"] and "--random-init" not in v["command"]
         assert "/dev/kfd" in v["devices"]
     parsers = [v for k, v in svc.items() if k.startswith("parser")]
-    assert len(parsers) == 8 and all(p["deploy"]["replicas"] == 8 for p in parsers)
+    # one parser service per GPU, as many replicas as the bench runs parser processes per GPU
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    workers = bench._args([]).cpu_workers
+    assert len(parsers) == 8 and all(p["deploy"]["replicas"] == workers for p in parsers)
     assert {p["command"][p["command"].index("--group") + 1] for p in parsers} == {"parser_worker"}
     assert {p["command"][p["command"].index("--engine") + 1] for p in parsers} == socks
     dsn = parsers[0]["environment"]["NATS_DSN"]

@@ -40,7 +40,7 @@ def main() -> int:
     p.add_argument("--save-dir", default="")
     p.add_argument("--variants", default="",
                    help="';'-separated training variants of the FIRST format, each 'key=value,...' over steps, "
-                        "negatives, lr, fused, proc (procedural family weight, SMSGATE_PROC_WEIGHT); e.g. "
+                        "negatives, lr, fused, proc (procedural family weight, SMSGATE_PROC_WEIGHT), labels (pseudo-word label share, SMSGATE_SYNTH_LABELS); e.g. "
                         "'steps=4000;steps=6000;proc=6'")
     a = p.parse_args()
     if a.variants:
@@ -114,10 +114,11 @@ def _variants(a) -> int:
         kv = dict(x.split("=") for x in spec.split(",") if x)
         steps = int(kv.get("steps", a.steps))
         neg = float(kv.get("negatives", a.negatives))
-        if "proc" in kv:
-            os.environ["SMSGATE_PROC_WEIGHT"] = kv["proc"]
-        else:
-            os.environ.pop("SMSGATE_PROC_WEIGHT", None)
+        for key, env in (("proc", "SMSGATE_PROC_WEIGHT"), ("labels", "SMSGATE_SYNTH_LABELS")):
+            if key in kv:
+                os.environ[env] = kv[key]
+            else:
+                os.environ.pop(env, None)
         t0 = time.time()
         data = ExamplePool(steps * a.batch, seed=0, families="train", workers=12, answer_format=fmt,
                            negatives=neg).get()

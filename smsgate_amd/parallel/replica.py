@@ -147,15 +147,19 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
             n = int(cmd["n"])
             prepared = [_payload_bytes(n, seed, cfg.get("vocab", "heldout"), cfg.get("traffic", "mixed"))
                         for seed in cmd["seeds"]]
+            # the phase's counters start HERE, before any process is told to go: with a
+            # shared broker the parser and writer groups span every process, so a process
+            # that reads its "go" late has already parsed / written messages other
+            # processes published, and a snapshot taken at "go" would drop them
+            c0 = dict(worker.counts)
+            w0 = (writer.stage.processed, writer.ok, writer.skipped, writer.fail)
+            base = worker.stage.processed
             client.send_control({"event": "prepared", "w": widx})
         elif cmd["cmd"] == "go":
             profiling = prof is not None and bool(cmd.get("profile"))
             if profiling:
                 prof.enable()
-            c0 = dict(worker.counts)
-            w0 = (writer.stage.processed, writer.ok, writer.skipped, writer.fail)
             t0 = time.perf_counter()
-            base = worker.stage.processed
 
             async def publish(i: int) -> None:
                 # gateway ingestion in chunks that yield to the parser stage, so parsing

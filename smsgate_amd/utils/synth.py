@@ -372,6 +372,11 @@ class _Ctx:
         self.num_style = r.choice(fam.numbers or pools["numbers"])
         self.date_style = r.choice(fam.dates or pools["dates"])
         self.card_style = r.choice(fam.cards or pools["cards"])
+        if fam.name.startswith("proc_") and r.random() < _label_noise() * 0.5:
+            # a "#1234" mask: one more mask shape than the fixed families use, so an unseen
+            # one reads as a card, not as merchant text ("№1234" is no valid span: the
+            # tokenizer glues the sign's bytes to the first digit)
+            self.card_style = "hash"
         cyr = fam.lang == "ru" and r.random() < 0.5
         self.cyr = cyr
         self.case = r.choice(fam.cases)
@@ -477,6 +482,8 @@ class _Ctx:
             s, a = f"**** {c}", c
         elif st == "ending":
             s, a = f"ending {c}", c
+        elif st == "hash":
+            s, a = f"#{c}", c
         elif st == "x_mask":  # held-out value style
             s, a = f"x{c}", c
         elif st == "dots_mask":  # held-out value style
@@ -654,6 +661,17 @@ _HELDOUT_SIGNATURES = frozenset({
 })
 
 
+def _label_noise() -> float:
+    """Share of procedural labels drawn as an unseen pseudo-word ("Vokta: ..."), so that
+    the extractor learns that any "Word:" before a value is a label, not part of it (a
+    held-out "Sender: NAME" otherwise leaks into the merchant).  SMSGATE_SYNTH_LABELS
+    overrides it for training-mix experiments (scripts/qa_probe.py --variants)."""
+    return float(os.environ.get("SMSGATE_SYNTH_LABELS", _LABEL_NOISE))
+
+
+_LABEL_NOISE = 0.0
+
+
 def _proc_layout(r: random.Random, lang: str) -> Tuple[Tuple[str, ...], bool]:
     while True:
         order = list(_SEGMENTS)
@@ -694,8 +712,13 @@ def _proc_render(c: "_Ctx") -> str:
     def want_fill(p: float) -> bool:
         return fills[0] > 0 and r.random() < p
 
-    def lab(pool: Sequence[str]) -> str:
-        return r.choice(pool) + colon + (filler() + " " if want_fill(0.3) else "")
+    noise = _label_noise()
+
+    def lab(pool: Sequence[str], unseen_ok: bool = True) -> str:
+        # never for the balance: an amount and a balance are told apart by their label
+        word = _filler(r, lang).split(" ")[0].title() if unseen_ok and noise and r.random() < noise \
+            else r.choice(pool)
+        return word + colon + (filler() + " " if want_fill(0.3) else "")
 
     segs: List[str] = []
     head = ""
@@ -726,7 +749,7 @@ def _proc_render(c: "_Ctx") -> str:
                 segs.append(v)
         elif seg == "BAL":
             v = c.BAL()
-            segs.append(lab(P["bal"]) + v)
+            segs.append(lab(P["bal"], False) + v)
         else:  # PLACE
             m = c.M()
             city = c.C() if r.random() < 0.85 else ""

@@ -95,7 +95,7 @@ def test_eight_ranks_full_node_layout():
     rt = out["routing"]
     total = ranks * steps * per
     assert out["n_gpus"] == ranks and rt["parsed"] + rt["keyword_skipped"] + rt["broken"] + rt["dlq"] == total
-    assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"]
+    assert rt["sink_stored"] + rt["writer_no_merchant"] == rt["parsed"], json.dumps(rt)
     for subj, n in NODE_PARTITIONS.items():
         assert f"{subj} over {n}" in out["config"]["bus"], out["config"]["bus"]
     members = out["bus_members"]

@@ -100,9 +100,9 @@ def _args(argv=None):
     # fails before the timed region (0 = no floor)
     p.add_argument("--quality-floor", type=float, default=0.85)
     # the reference's acceptance test (tests/test_parsers.py:11-86) on the flagship being timed,
-    # reported in quality_heldout.reference_cases (3 / 3 on every round-3 run); 1 = the run fails
-    # before the timed region unless all three CASES come out right (the in-run training is not
-    # bit-reproducible across boxes, so the default reports rather than gates)
+    # reported in quality_heldout.reference_cases (3 / 3 on every run since round 3); 1 (the
+    # default) = the run fails before the timed region unless all three CASES
+    # come out right; 0 = report only
     p.add_argument("--cases-required", type=int, default=1, choices=[0, 1])
     # the extractor must also REJECT non-transactions (card blocked, promos, log-in alerts...,
     # utils/synth.py NEG_FAMILIES): above this share of held-out non-transaction SMS published

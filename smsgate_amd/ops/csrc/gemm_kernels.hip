@@ -228,22 +228,25 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       for (int e = 0; e < 4; ++e) ssv[i][e] = sp[(size_t)e * na.ld];
     }
   }
-  // EPI 1: this thread's residual chunks, loaded before the K loop (their latency hides
-  // behind it instead of stalling the epilogue; R may alias C, but every element is
-  // read and written by the same thread)
+  // EPI 1: this thread's residual chunks (R may alias C, but every element is read and
+  // written by the same thread).  RPRE_EARLY: loaded before the K loop, their latency
+  // hidden behind it but their registers live through it; else issued right after the
+  // K loop, in flight while the accumulators are staged through LDS
   constexpr int RIT = EPI == 1 ? (BM * (BN / 8) + NT - 1) / NT : 1;  // (32x96: 1.5 chunks per thread)
+  constexpr bool RPRE_EARLY = RIT <= 6;
   uint4 rpre[RIT];
-  if constexpr (EPI == 1) {
+  auto load_rpre = [&]() {
 #pragma unroll
     for (int it = 0; it < RIT; ++it) {
       const int q = min(tid + it * NT, BM * (BN / 8) - 1), row = q / (BN / 8), c = q % (BN / 8);
       const int gr = min(m0 + row, M - 1);
       rpre[it] = *reinterpret_cast<const uint4*>(R + (size_t)gr * ldr + n0 + c * 8);
     }
-  }
+  };
+  if constexpr (EPI == 1 && RPRE_EARLY) load_rpre();
   // EPI 3: the tile's token positions / KV slots, likewise loaded before the K loop —
-  // q/k heads: the rows of this thread's (row, head, quarter) items; v heads: row = lane (+64)
-  constexpr int QIT = (BM * 4 * HT + NT - 1) / NT, VU = BM > 64 ? 2 : 1;
+  // q/k heads: the rows of this thread's (row, quarter) items; v heads: row = lane (+64)
+  constexpr int QIT = (BM * 4 + NT - 1) / NT, VU = BM > 64 ? 2 : 1;
   constexpr int EPN = EPI == 3 ? (QIT > VU ? QIT : VU) : 1;
   int epos[EPN], eslot[EPN];
   if constexpr (EPI == 3) {
@@ -251,7 +254,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     if (h < ra.nh + ra.nkv) {
 #pragma unroll
       for (int it = 0; it < QIT; ++it) {
-        const int gr = min(m0 + (tid + it * NT) / (4 * HT), M - 1);
+        const int gr = min(m0 + ((tid + it * NT) >> 2), M - 1);
         epos[it] = ra.pos[gr];
         eslot[it] = h >= ra.nh ? ra.slot[gr] : 0;
       }
@@ -342,6 +345,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail re-loads ...
   __syncthreads();  // ... of EVERY wave have landed before the C tile reuses the buffers
+  if constexpr (EPI == 1 && !RPRE_EARLY) {
+    load_rpre();
+    asm volatile("" ::: "memory");  // issued here, not sunk to their first use
+  }
   if constexpr (PROBE == 4) {
     float keep = 0.f;  // every accumulator stays live (no dead MFMAs)
 #pragma unroll
@@ -410,33 +417,41 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   if constexpr (EPI == 3) {
     const int h0 = n0 >> 6;
     if (h0 < ra.nh + ra.nkv) {
+      // one (row, quarter) item per thread and trip: its (cos, sin) chunk is loaded once
+      // and rotates that quarter of all HT heads of the tile (the heads share the row's
+      // position)
 #pragma unroll
       for (int it = 0; it < QIT; ++it) {
         const int q = tid + it * NT;
-        if (q >= BM * 4 * HT) break;
-        const int row = q / (4 * HT), j = (q >> 2) % HT, c = q & 3;
-        const int h = h0 + j;
+        if (q >= BM * 4) break;
+        const int row = q >> 2, c = q & 3;
         const int gr = m0 + row;
         if (gr >= M) continue;
         const int p = epos[it];
-        const uint4 v1 = *reinterpret_cast<const uint4*>(Cs + row * CST + j * 64 + c * 8);
-        const uint4 v2 = *reinterpret_cast<const uint4*>(Cs + row * CST + j * 64 + 32 + c * 8);
         const float4* csp = reinterpret_cast<const float4*>(ra.cs + (size_t)(ra.p0 + p) * 32 + c * 8);
-        const uint32_t a1[4] = {v1.x, v1.y, v1.z, v1.w}, a2[4] = {v2.x, v2.y, v2.z, v2.w};
-        uint32_t o1[4], o2[4];
+        float4 t[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float4 t = csp[e];  // (cos, sin) of dims 2e, 2e+1 of this chunk
-          const float x1l = bf2f(a1[e] & 0xffffu), x1h = bf2f(a1[e] >> 16);
-          const float x2l = bf2f(a2[e] & 0xffffu), x2h = bf2f(a2[e] >> 16);
-          o1[e] = (uint32_t)f2bf(x1l * t.x - x2l * t.y) | ((uint32_t)f2bf(x1h * t.z - x2h * t.w) << 16);
-          o2[e] = (uint32_t)f2bf(x2l * t.x + x1l * t.y) | ((uint32_t)f2bf(x2h * t.z + x1h * t.w) << 16);
+        for (int e = 0; e < 4; ++e) t[e] = csp[e];  // (cos, sin) of dims 2e, 2e+1 of this chunk
+#pragma unroll
+        for (int j = 0; j < HT; ++j) {
+          const int h = h0 + j;
+          const uint4 v1 = *reinterpret_cast<const uint4*>(Cs + row * CST + j * 64 + c * 8);
+          const uint4 v2 = *reinterpret_cast<const uint4*>(Cs + row * CST + j * 64 + 32 + c * 8);
+          const uint32_t a1[4] = {v1.x, v1.y, v1.z, v1.w}, a2[4] = {v2.x, v2.y, v2.z, v2.w};
+          uint32_t o1[4], o2[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x1l = bf2f(a1[e] & 0xffffu), x1h = bf2f(a1[e] >> 16);
+            const float x2l = bf2f(a2[e] & 0xffffu), x2h = bf2f(a2[e] >> 16);
+            o1[e] = (uint32_t)f2bf(x1l * t[e].x - x2l * t[e].y) | ((uint32_t)f2bf(x1h * t[e].z - x2h * t[e].w) << 16);
+            o2[e] = (uint32_t)f2bf(x2l * t[e].x + x1l * t[e].y) | ((uint32_t)f2bf(x2h * t[e].z + x1h * t[e].w) << 16);
+          }
+          uint16_t* dst;
+          if (h < ra.nh) dst = ra.q_out + ((size_t)gr * ra.nh + h) * 64;
+          else dst = ra.k_cache + (((size_t)eslot[it] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
+          *reinterpret_cast<uint4*>(dst + c * 8) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
+          *reinterpret_cast<uint4*>(dst + 32 + c * 8) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
         }
-        uint16_t* dst;
-        if (h < ra.nh) dst = ra.q_out + ((size_t)gr * ra.nh + h) * 64;
-        else dst = ra.k_cache + (((size_t)eslot[it] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
-        *reinterpret_cast<uint4*>(dst + c * 8) = make_uint4(o1[0], o1[1], o1[2], o1[3]);
-        *reinterpret_cast<uint4*>(dst + 32 + c * 8) = make_uint4(o2[0], o2[1], o2[2], o2[3]);
       }
     } else {
       // one token per wave-instruction (lane = d).  The tile's positions / slots sit one

@@ -1,0 +1,71 @@
+"""Register budgets of the serving hot path's GEMMs (CPU: hipcc's resource remarks).
+
+A 4-wave 128x192 tile holds 24 MFMA accumulators per lane, so it sits near the
+256-register line.  Over that line a SIMD runs one wave of the kernel instead of two,
+and the kernel still produces the same results, only slower.  Round 5 measured this
+case.  The residual chunks prefetched before the K loop (48 registers live through
+it) put the residual GEMM at 332.  The QKV+RoPE epilogue's per-head (cos, sin) loads put
+that GEMM at 260.  Both ran at 1 wave per SIMD until the prefetch moved behind the K
+loop and the heads of a tile shared one (cos, sin) load
+(ops/csrc/gemm_kernels.hip).  This pins both, and pins no scratch spills, for the
+kernels the default engine runs.
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def gemm_resources(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    out = tmp_path_factory.mktemp("kr") / "gemm.o"
+    src = os.path.join(ROOT, "smsgate_amd/ops/csrc/gemm_kernels.hip")
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", src, "-o", str(out),
+                        "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res, cur = {}, None
+    for line in r.stderr.splitlines():
+        m = re.search(r"remark:\s+(.*?) \[-Rpass", line)
+        if not m:
+            continue
+        txt = m.group(1)
+        if txt.startswith("Function Name:"):
+            cur = res.setdefault(txt.split(":", 1)[1].strip(), {})
+        elif cur is not None and ":" in txt:
+            k, v = txt.split(":", 1)
+            cur[k.strip()] = v.strip()
+    return res
+
+
+def _find(res, pattern):
+    hits = {k: v for k, v in res.items() if re.search(pattern, k)}
+    assert hits, pattern
+    return hits
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("epi_norm", ["1ELi0", "3ELi1", "3ELi2"])
+def test_big_tile_gemms_run_two_waves_per_simd(gemm_resources, epi_norm):
+    """cfg 28 (128x192, 2x2 waves): the residual (EPI 1) and QKV+RoPE (EPI 3) forms the
+    engine runs from 32 768 rows fit 256 registers (2 waves per SIMD) without spills."""
+    for name, r in _find(gemm_resources, rf"gemm_fused_kernelILi128ELi192ELi2ELi2ELi{epi_norm}ELi2ELi0E").items():
+        assert int(r["Occupancy [waves/SIMD]"]) >= 2, (name, r)
+        assert int(r["ScratchSize [bytes/lane]"]) == 0, (name, r)
+
+
+@pytest.mark.slow
+def test_default_gemms_do_not_spill(gemm_resources):
+    """The persistent SwiGLU GEMM (cfg 20) and the residual / QKV tiles of the qa engine."""
+    pats = [r"gemm256p_swiglu_kernelILi[012]E", r"gemm_fused_kernelILi128ELi96ELi2ELi2ELi1ELi0ELi2ELi0E",
+            r"gemm_fused_kernelILi64ELi96ELi2ELi2ELi1ELi0ELi2ELi0E", r"gemm_fused_kernelILi128ELi64ELi2ELi2ELi3E"]
+    for p in pats:
+        for name, r in _find(gemm_resources, p).items():
+            assert int(r["ScratchSize [bytes/lane]"]) == 0, (name, r)

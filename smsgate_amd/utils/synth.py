@@ -372,7 +372,8 @@ class _Ctx:
         self.num_style = r.choice(fam.numbers or pools["numbers"])
         self.date_style = r.choice(fam.dates or pools["dates"])
         self.card_style = r.choice(fam.cards or pools["cards"])
-        if fam.name.startswith("proc_") and r.random() < _label_noise() * 0.5:
+        noise = _label_noise() if fam.name.startswith("proc_") else 0.0
+        if noise > 0 and r.random() < noise * 0.5:  # (off: no draw, the default stream is unchanged)
             # a "#1234" mask: one more mask shape than the fixed families use, so an unseen
             # one reads as a card, not as merchant text ("№1234" is no valid span: the
             # tokenizer glues the sign's bytes to the first digit)

@@ -250,3 +250,21 @@ def test_russian_month_dates_canonicalise():
     assert canonical_date_text("1 мая 2024 г. 09:05") == "2024-05-01 09:05"
     assert canonical_date_text("06.05.25 14:23") == "06.05.25 14:23"  # dotted: the reference chain's
     assert canonical_date_text("6 foo 2025") == "6 foo 2025"
+
+
+def test_training_stream_is_pinned(monkeypatch):
+    """The in-run training data is a fixed function of the seed: the bench's quality
+    numbers reproduce from run to run (training on the box is deterministic too).  A
+    default-off experiment knob must not draw from the generator's RNG.  Round 5 hit
+    this: an unconditional draw for SMSGATE_SYNTH_LABELS changed every later example and
+    moved held-out formats from 99.0 to 95.2 %.  Update the fingerprint only on a
+    deliberate change to the training distribution."""
+    import hashlib
+
+    monkeypatch.delenv("SMSGATE_SYNTH_LABELS", raising=False)
+    monkeypatch.delenv("SMSGATE_PROC_WEIGHT", raising=False)
+    h = hashlib.sha256()
+    for s in generate(400, seed=5, families="train"):
+        h.update(s.body.encode())
+        h.update(repr(sorted((s.answer or {}).items())).encode())
+    assert h.hexdigest()[:16] == "8b88708782371b05"

@@ -196,9 +196,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   constexpr int NI = (BM / 8 + NW - 1) / NW + (BN / 8 + NW - 1) / NW;  // glds instructions per stage per wave
   static_assert(ST >= 2 && ST <= 4, "pipeline stages");
   static_assert(BM * CST <= ST * TILE, "C staging fits in the K-loop buffers");
+  // EPI 1 with a non-power-of-two chunk count per row (96 / 192-wide tiles) sums the
+  // rows' x² partials through a [BM][CPR] fp32 image beside the staged C tile; a 256-row
+  // tile needs more than its K-loop buffers for the two (the array grows past them)
+  constexpr int CPR1 = BNO / 8;
+  constexpr int EPI1_LDS = EPI == 1 && (CPR1 & (CPR1 - 1)) != 0 ? BM * CST + 2 * BM * CPR1 : 0;
+  constexpr int SMEM = ST * TILE > EPI1_LDS ? ST * TILE : EPI1_LDS;
+  static_assert(SMEM * 2 <= 160 * 1024, "LDS");
 
   // ONE __shared__ array (a second one makes hipcc wait vmcnt(0) before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint16_t smem[ST * TILE];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
   // ---- XCD-aware, bijective tile assignment: the blocks of one XCD (orig % 8)
   // get a contiguous range of tiles, so tiles that share A rows share an L2
@@ -549,7 +556,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
     constexpr bool POW2 = (CPR & (CPR - 1)) == 0;
     // the shuffle reduction needs every lane on the same trip count
     static_assert(CPR <= 64 && (!POW2 || (BM * CPR) % NT == 0), "uniform epilogue trips");
-    static_assert(POW2 || BM * CST + 2 * BM * CPR <= ST * TILE, "x² image fits beside the C tile");
+    static_assert(POW2 || BM * CST + 2 * BM * CPR <= SMEM, "x² image fits beside the C tile");
     float* ssl = reinterpret_cast<float*>(smem + BM * CST);
     const bool want_ss = na.ssout != nullptr;
 #pragma unroll
@@ -1095,6 +1102,7 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //      (21..27: epi 0 / 1 only — 48-wide wave tiles for the N = 576 residual GEMMs)
 //  28: 128x192 (2x2) 2st   29: 256x96 (4x1) 2st — 64x96 wave tiles
 //  30: 128x96 (4x2) 2st, 8 waves   31: 64x96 (4x2) 2st, 8 waves
+//  32: 256x192 (4x2) 2st, 8 waves — 64x96 wave tiles (epi 0 / 1 only)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1123,9 +1131,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[32] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96};
-  if (cfg < 0 || cfg > 31) return -1;
+  static const int BNs[33] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96, 192};
+  if (cfg < 0 || cfg > 32) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1194,6 +1202,9 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     // hide the one-tile-per-block latency of the short K loops (K = 576 / 1536)
     case 30: return dispatch_resid<128, 96, 4, 2, 2>(SG_ARGS);
     case 31: return dispatch_resid<64, 96, 4, 2, 2>(SG_ARGS);
+    // 256x192, 8 waves, the 64x96 wave tiles of 28: 1.4x its MFMA work per staged byte
+    // (the big-M residual loop is L2-bound at 77 FLOP/B; this tile is 110)
+    case 32: return dispatch_resid<256, 192, 4, 2, 2>(SG_ARGS);
     default: return dispatch_resid<32, 96, 2, 2, 2>(SG_ARGS);
   }
 #undef SG_ARGS

@@ -299,11 +299,14 @@ GEMM_SMALL_M = int(os.environ.get("SMSGATE_GEMM_SMALL_M", "1024"))
 #   116.0 / 233.4 us vs 121.6 / 270.0 (cfg 21), o-proj 59.4 / 105.2 vs 59.6 / 117.8 (cfg
 #   22) -- and the QKV+RoPE GEMM (qkv_cfg).  Its x² parts stay 96 columns wide (two per
 #   tile, each summed like a 96-wide tile's), so results do not depend on the config.
+#   With both fitting 256 registers (r05_gemm_tune_resid_u.json, 3 interleaved rounds):
+#   down-proj at 27 648 rows 59.7 us on 28 vs 67.6 on 21, so 28 from 16 384 rows; the
+#   256x192 8-wave tile (cfg 32) trails 28 at every size (257.8 vs 223.5 us at 110 592).
 GEMM_MEASURED = {
     ("swiglu", 3072, 576): [(2048, 4095, 13), (4096, 6143, 19), (6144, 1 << 30, 20)],
     ("resid", 576, 576): [(1, 2047, 27), (2048, 6143, 22), (6144, 12287, 21), (12288, 32767, 22),
                           (32768, 1 << 30, 28)],
-    ("resid", 576, 1536): [(1, 2047, 27), (2048, 6143, 22), (6144, 32767, 21), (32768, 1 << 30, 28)],
+    ("resid", 576, 1536): [(1, 2047, 27), (2048, 6143, 22), (6144, 16383, 21), (16384, 1 << 30, 28)],
 } if os.environ.get("SMSGATE_GEMM_MEASURED", "1") != "0" else {}
 
 

@@ -38,13 +38,22 @@ def main() -> int:
         ss[:6] = torch.rand(6, M, device=dev)
         pos = torch.randint(0, 120, (M,), generator=g, dtype=torch.int32).to(dev)
         slot = torch.randint(0, S, (M,), generator=g, dtype=torch.int32).to(dev)
+        # the engine's layout: packed sequences of ~50 rows, positions 0.. within each, one
+        # KV slot per sequence (whole 8-position V^T blocks)
+        r = torch.arange(M, dtype=torch.int32)
+        ppos, pslot = (r % 50).to(dev), ((r // 50) % S).to(dev)
         q = torch.empty(M, nh, D, dtype=bf16, device=dev)
         c = torch.empty(M, N, dtype=bf16, device=dev)
         cases = {
-            "store_cfg28": lambda: ops.gemm(x, w, norm_eps=1e-5, out=c, cfg=28, ss_in=ss),
-            "store_cfg1": lambda: ops.gemm(x, w, norm_eps=1e-5, out=c, cfg=1, ss_in=ss),
-            "rope_cfg28": lambda: ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, 20, cfg=28, ss_in=ss),
-            "rope_cfg1": lambda: ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, 20, cfg=1, ss_in=ss),
+            # NORM 1 (x² in the K loop) on both sides: plain store vs the fused epilogue
+            "store_n1_cfg28": lambda: ops.gemm(x, w, norm_eps=1e-5, out=c, cfg=28),
+            "rope_n1_cfg28_packed": lambda: ops.gemm_qkv_rope(x, w, 1e-5, ppos, pslot, cs, q, kc, vt, nh, nkv, 20,
+                                                              cfg=28),
+            "rope_n1_cfg28_random": lambda: ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, 20,
+                                                              cfg=28),
+            # the engine's flavour (producer partials)
+            "rope_n2_cfg28_packed": lambda: ops.gemm_qkv_rope(x, w, 1e-5, ppos, pslot, cs, q, kc, vt, nh, nkv, 20,
+                                                              cfg=28, ss_in=ss),
         }
         best = {}
         for k, fn in list(cases.items()):

@@ -753,8 +753,10 @@ def _ddp_train(args, world: int) -> bool:
 def start_training_data(args, local: int):
     """Build the training examples on CPU worker processes NOW -- before the GPU is
     touched (spawned, not forked) -- so the work overlaps broker / engine start-up.
-    Data-parallel training: every rank builds its own disjoint share (seeded by rank),
-    with the node's data workers split over its ranks; else local rank 0 builds all."""
+    Data-parallel training: every rank builds the single-GPU run's whole example list
+    (the same seed: the list depends only on it, not on the worker count) and trains on
+    its slice of the same global batches, so an N-rank job trains the model a one-GPU job
+    does (up to the all-reduce's summation order); else local rank 0 builds it."""
     if args.weights != "train" or args.cpu_echo_engine or args.backend != "local_llm":
         return None
     tc, path = _train_plan(args)
@@ -765,8 +767,8 @@ def start_training_data(args, local: int):
     rank, world, _ = _rank_env()
     if _ddp_train(args, world):
         node = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-        return ExamplePool(tc.n_examples // world, seed=tc.seed * 1000 + rank, families=tc.families,
-                           workers=max(2, args.data_workers // node), answer_format=tc.answer_format,
+        return ExamplePool(tc.n_examples, seed=tc.seed, families=tc.families,
+                           workers=max(4, args.data_workers // node), answer_format=tc.answer_format,
                            negatives=tc.negatives)
     if local != 0:
         return None
@@ -800,13 +802,14 @@ def acquire_weights(args, device: str, rank: int, world: int, pool=None):
         prov["weights"] += " (reused from an earlier identical run's cache)"
         return w, prov
     if _ddp_train(args, world):
-        # every rank trains: the same steps x global batch, split over the ranks, gradients
-        # averaged by bucketed all-reduces overlapped with backward (parallel/ddp.py); the
-        # replicas stay identical, rank 0 publishes the file for later runs
+        # every rank trains: the same steps x global batch -- the one-GPU run's batches,
+        # split over the ranks -- gradients averaged by bucketed all-reduces overlapped with
+        # backward (parallel/ddp.py); the replicas stay identical, rank 0 publishes the file
         import dataclasses
 
         t0 = time.perf_counter()
-        tcr = dataclasses.replace(tc, batch=tc.batch // world, data_parallel=True, seed=tc.seed)
+        tcr = dataclasses.replace(tc, batch=tc.batch // world, global_batch=tc.batch, data_parallel=True,
+                                  seed=tc.seed)
         w = train_extractor(tcr, device=device, data=pool.get() if pool is not None else None,
                             log=(lambda s: print(f"[bench] train {s}", file=sys.stderr, flush=True)) if rank == 0
                             else (lambda s: None))

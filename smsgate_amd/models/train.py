@@ -82,6 +82,11 @@ class TrainConfig:
     ema: float = 0.998
     ema_start: int = 0  # first step the average includes (0 = warmup end)
     data_parallel: bool = True  # under torch.distributed: all-reduce gradients (False: train this rank alone)
+    # data parallel with global_batch = batch x world: every rank holds the same example
+    # list and draws the same global batch each step (the single-GPU run's stream), then
+    # trains on its slice -- N ranks see exactly the examples one GPU would (0: each rank
+    # draws its own batch from its own list)
+    global_batch: int = 0
     # fused HIP RMSNorm / RoPE / SwiGLU forward+backward (models/train_ops.py) on the GPU;
     # False: reference_forward (plain PyTorch elementwise chains)
     fused: bool = True
@@ -412,7 +417,11 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
         p = (step - cfg.warmup) / max(1, cfg.steps - cfg.warmup)
         return cfg.lr * (cfg.min_lr_frac + (1 - cfg.min_lr_frac) * 0.5 * (1 + math.cos(math.pi * p)))
 
-    rng = random.Random(cfg.seed * 1000003 + rank)  # each rank draws its own examples
+    shared = ddp and cfg.global_batch > 0
+    if shared and cfg.global_batch != cfg.batch * world:
+        raise ValueError(f"global_batch {cfg.global_batch} != batch {cfg.batch} x world {world}")
+    # each rank draws its own examples, or (shared) every rank the single-GPU stream
+    rng = random.Random(cfg.seed * 1000003 + (0 if shared else rank))
     start = 0
     ck = latest_checkpoint(cfg.ckpt_dir) if cfg.resume else None
     if ck is not None:
@@ -424,7 +433,7 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
         start = int(state["step"])
         if "ema" in state:
             ema_params = [e.to(p.device) for e, p in zip(state["ema"], params)]
-        if world == 1:
+        if world == 1 or shared:
             rng.setstate(_as_rng_state(state["rng"]))
         else:  # rank 0's stream was saved; the others re-derive theirs deterministically
             rng = random.Random((cfg.seed * 1000003 + rank) ^ (start * 7919))
@@ -442,14 +451,22 @@ def train_extractor(cfg: TrainConfig, device="cuda", log: Callable[[str], None] 
     for step in range(start, cfg.steps):
         for g in opt.param_groups:
             g["lr"] = lr_at(step)
-        exs = rng.sample(data, cfg.batch)
+        if shared:
+            exs_g = rng.sample(data, cfg.global_batch)
+            exs = exs_g[rank * cfg.batch:(rank + 1) * cfg.batch]
+        else:
+            exs_g = exs = rng.sample(data, cfg.batch)
         with torch.autocast(device_type="cuda", dtype=torch.bfloat16, enabled=str(device).startswith("cuda")):
             if qa:
                 from ..serving.qa import qa_logits, qa_loss
 
                 ids, add, qpos, targets = qa_batch(prefix, exs, tok.pad, device, fsm.lay)
                 h = forward(w, ids, add)
-                loss = qa_loss(qa_logits(h, w.embed, qpos, fsm.lay), targets, fsm.lay)
+                # decisions of the (global) batch: class + a start per field + an end per
+                # non-null field -- counted on the host, divided over the ranks
+                n_dec = sum(1 + len(sp) + sum(1 for s_, _ in sp if s_ >= 0) for _, (_, sp) in exs_g)
+                loss = qa_loss(qa_logits(h, w.embed, qpos, fsm.lay), targets, fsm.lay,
+                               denom=n_dec / (world if shared else 1))
             else:
                 ids, labels, add = _batch(prefix, exs, tok.pad, device, fsm.ptr0)
                 h = forward(w, ids, add)

@@ -397,11 +397,13 @@ def qa_logits(h, embed, qpos, lay: QALayout):
     return cls, start, null, end
 
 
-def qa_loss(scores, targets, lay: QALayout):
+def qa_loss(scores, targets, lay: QALayout, denom: Optional[float] = None):
     """Mean cross-entropy over the answer's decisions: the class, every copied field's
     start (null included) and every non-null field's end (over all message positions).
     ``targets``: (cls [B], starts [B, n_copy] (-1 = null), ends [B, n_copy], npos [B]
-    pointable positions per message)."""
+    pointable positions per message).  ``denom``: the decision count to divide by, from
+    the host (no device sync; data parallel: the GLOBAL batch's count / world, so the
+    averaged gradient is the one-GPU batch's); default this batch's own count."""
     import torch
     import torch.nn.functional as F
 
@@ -421,7 +423,7 @@ def qa_loss(scores, targets, lay: QALayout):
     # scores left untrained before the start would let a wrong pair win
     en = end.masked_fill(out_of_msg, neg)
     l_en = F.cross_entropy(en[has], t_e[has], reduction="sum") if bool(has.any()) else en.sum() * 0
-    return (l_cls + l_st + l_en) / (B + B * NF + int(has.sum()))
+    return (l_cls + l_st + l_en) / (denom if denom is not None else (B + B * NF + int(has.sum())))
 
 
 def null_rejection(answer: Dict[str, Optional[str]]) -> Dict[str, Optional[str]]:

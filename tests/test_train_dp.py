@@ -142,3 +142,56 @@ def test_bench_trains_data_parallel_on_every_rank(tmp_path):
     assert all("data parallel over 2 ranks" in out[r][1] for r in range(world)), dict(out)
     assert out[0][2] == 9  # the default answer format (qa)
     assert len(list(tmp_path.glob("tiny-*.safetensors"))) == 1
+
+
+def _single_worker(cache, out):
+    import sys
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(k, None)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    args = bench._args(["--model", "tiny", "--train-steps", "6", "--train-batch", "8", "--weights-cache", cache,
+                        "--data-workers", "2"])
+    pool = bench.start_training_data(args, 0)
+    w, _ = bench.acquire_weights(args, "cpu", 0, 1, pool)
+    out[0] = torch.cat([p.detach().float().reshape(-1) for p in w.parameters()])
+
+
+def _bench_flat_worker(rank, world, port, cache, out):
+    import sys
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = bench._args(["--model", "tiny", "--train-steps", "6", "--train-batch", "8", "--weights-cache", cache,
+                        "--data-workers", "2"])
+    pool = bench.start_training_data(args, rank)
+    w, _ = bench.acquire_weights(args, "cpu", rank, world, pool)
+    if rank == 0:
+        out[0] = torch.cat([p.detach().float().reshape(-1) for p in w.parameters()])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_data_parallel_trains_the_one_gpu_model(tmp_path):
+    """The N-rank job trains on the one-GPU job's global batches (every rank draws the
+    same batch from the same example list and takes its slice).  Quality depends on the
+    training sample (profiles/PERF.md, "Training determinism"), so the scaling runs must
+    not train a different model at every N.  The weights match the single-process run up
+    to the all-reduce's summation order."""
+    single, multi = mp.Manager().dict(), mp.Manager().dict()
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_single_worker, args=(str(tmp_path / "one"), single))
+    p.start()
+    p.join(600)
+    assert p.exitcode == 0
+    mp.spawn(_bench_flat_worker, args=(2, _free_port(), str(tmp_path / "two"), multi), nprocs=2, join=True)
+    a, b = single[0], multi[0]
+    rel = float((a - b).norm() / a.norm())
+    print("relative weight difference, 2 ranks vs 1:", rel)
+    assert rel < 1e-6, rel

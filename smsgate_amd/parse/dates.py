@@ -123,7 +123,13 @@ def parse_custom_datetime(text: str) -> datetime:
     try:
         return datetime.strptime(text, "%d.%m.%y %H:%M")
     except Exception:
-        return _du_parse(text)
+        dt = _du_parse(text)
+    if dt.tzinfo is not None:
+        # a numeric zone of a day or more ("10:00 +2500") builds an aware datetime whose
+        # every later use -- printing, comparing, converting -- raises; raise here, where
+        # a parse error is a parse failure (the message is dead-lettered, not its batch)
+        dt.utcoffset()
+    return dt
 
 
 def parse_unix_timestamp(ts: Union[int, float, str], tz: str = "UTC", aware: bool = True) -> datetime:

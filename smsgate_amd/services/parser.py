@@ -137,7 +137,15 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                 # worker.py:161-170) — a no-op for an already-validated model, so
                 # only the serialisation keeps the shape-(d) failure route.
                 parsed = res.parsed
-                if _is_future(parsed.date):
+                try:
+                    future = _is_future(parsed.date)
+                except (ValueError, OverflowError) as err:  # an unusable date: this message's failure
+                    text = _text(data)
+                    sentry_capture(err, extras={"raw_data": text})
+                    out.append((SUBJECT_FAILED, _dump({"err": str(err), "entry": text})))
+                    counts["fail"] += 1
+                    continue
+                if future:
                     text = _text(data)
                     sentry_capture(ValueError(FUTURE_DATE_ERR), extras={"raw_data": text})
                     out.append((SUBJECT_FAILED, _dump({"err": FUTURE_DATE_ERR, "entry": text})))

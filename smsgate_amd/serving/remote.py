@@ -57,40 +57,55 @@ class EngineServer:
         self._sel = selectors.DefaultSelector()
         for i, c in enumerate(self.conns):
             self._sel.register(c, selectors.EVENT_READ, i)
-        # responses leave through a sender thread: a parser process that is slow to read
-        # (its reader thread waits for the GIL) filled its socket and blocked the engine
-        # loop inside send_bytes -- 1.7 s of a 3.2 s phase with the GPU idle behind it
-        self._outq: "queue.SimpleQueue" = queue.SimpleQueue()
-        self._sender: Optional[threading.Thread] = None
+        # responses leave through sender threads, one per connection: a parser process
+        # that is slow to read (its reader thread waits for the GIL) filled its socket and
+        # blocked the engine loop inside send_bytes -- 1.7 s of a 3.2 s phase with the GPU
+        # idle behind it -- and with one shared sender it would hold back every other
+        # connection's responses the same way
+        self._senders: Dict[int, "queue.SimpleQueue"] = {}  # id(connection) -> its FIFO
+        self._senders_lock = threading.Lock()
 
     def _send(self, c: Connection, frame: bytes) -> None:
-        """Queue ``frame`` for ``c`` (per-connection order kept: one FIFO, one thread)."""
-        if self._sender is None:
-            self._sender = threading.Thread(target=self._send_loop, name="engine-send", daemon=True)
-            self._sender.start()
-        self._outq.put((c, frame))
+        """Queue ``frame`` for ``c`` (its frames leave in order, on its own thread)."""
+        q = self._senders.get(id(c))
+        if q is None:
+            with self._senders_lock:
+                q = self._senders.get(id(c))
+                if q is None:
+                    q = self._senders[id(c)] = queue.SimpleQueue()
+                    threading.Thread(target=self._send_loop, args=(c, q), name="engine-send",
+                                     daemon=True).start()
+        q.put(frame)
 
-    def _send_loop(self) -> None:
+    @staticmethod
+    def _send_loop(c: Connection, q: "queue.SimpleQueue") -> None:
+        dead = False
         while True:
-            item = self._outq.get()
-            if item is None:
+            frame = q.get()
+            if frame is None:
                 return
-            c, frame = item
-            if c is None:  # a flush marker
+            if isinstance(frame, threading.Event):  # a flush marker
                 frame.set()
+                continue
+            if dead:
                 continue
             try:
                 c.send_bytes(frame)
-            except (OSError, EOFError, ValueError):  # the client went away: its reads fail too
-                pass
+            except (OSError, EOFError, ValueError):  # the client went away: drop what follows
+                dead = True
 
     def flush(self, timeout: float = 30.0) -> None:
         """Wait until every queued frame has been handed to the sockets."""
-        if self._sender is None:
-            return
-        done = threading.Event()
-        self._outq.put((None, done))
-        done.wait(timeout)
+        with self._senders_lock:
+            queues = list(self._senders.values())
+        marks = []
+        for q in queues:
+            ev = threading.Event()
+            q.put(ev)
+            marks.append(ev)
+        t_end = time.monotonic() + timeout
+        for ev in marks:
+            ev.wait(max(0.0, t_end - time.monotonic()))
 
     def add_connection(self, conn: Connection) -> int:
         self.conns.append(conn)
@@ -105,6 +120,10 @@ class EngineServer:
                 self._sel.unregister(c)
             except (KeyError, ValueError, OSError):
                 pass
+            with self._senders_lock:
+                q = self._senders.pop(id(c), None)
+            if q is not None:  # its sender ends after the frames already queued
+                q.put(None)
 
     def send_control(self, idx: int, obj: Any) -> None:
         c = self.conns[idx]

@@ -314,3 +314,25 @@ def test_fast_wire_json_equals_pydantic():
         raw = RawSMS(msg_id=t, sender=t or "s", body=t or "b", date=t, device_id=r.choice([None, t]),
                      source=r.choice(["device", "xml"]))
         assert raw_wire(raw) == raw.model_dump_json().encode()
+
+
+@pytest.mark.parametrize("date", ["2024-01-01 10:00 +2500", "10:00 -9999"])
+def test_day_sized_zone_offset_is_a_parse_failure(date):
+    """A model that writes a numeric zone of a day or more ("+2500") got dateutil to build
+    an aware datetime whose every later use raises.  The round-5 bench with random weights
+    met one: the parser's future-date check raised on it, and its whole batch was
+    re-run message by message.  The one message was then dead-lettered only after five
+    deliveries, and the routing count came up one short.  The error now happens at parse
+    time, so the message takes the normal failure path."""
+    from smsgate_amd.models.domain import RawSMS
+    from smsgate_amd.parse.dates import parse_custom_datetime
+    from smsgate_amd.parse.pipeline import Outcome, postprocess_answer
+
+    with pytest.raises(ValueError):
+        parse_custom_datetime(date)
+    ans = {"txn_type": "debit", "date": date, "amount": "5.00", "currency": "USD", "card": "1234",
+           "merchant": "SHOP", "city": "", "address": "", "balance": "1.00"}
+    for body in ("PURCHASE 5.00 USD SHOP card *1234", "PURCHASE 5.00 USD SHOP 01.02.24 card *1234"):
+        raw = RawSMS(msg_id="e", device_id="d", sender="B", date="1700000000", body=body, source="device")
+        r = postprocess_answer(raw, body, dict(ans))
+        assert r.outcome is not Outcome.PARSED or r.parsed.date.utcoffset() is None, r

@@ -480,3 +480,39 @@ def test_engine_server_packed_and_per_message_paths(tmp_path, packed, arun):
     assert empty == [] and len(got) == 37
     assert all(g == got[0] for g in got) and got[0]["merchant"]
     assert srv.served == 37
+
+
+def test_engine_server_slow_reader_does_not_hold_back_others():
+    """Responses leave on one sender thread per connection: a client that stops reading
+    (its socket buffer full) stalls only its own responses.  The engine loop and every
+    other client's responses go on, and ``flush`` is bounded."""
+    import threading
+    import time
+    from multiprocessing import Pipe
+
+    from smsgate_amd.serving import protocol as P
+    from smsgate_amd.serving.remote import EngineServer
+
+    (ca, sa), (cb, sb) = Pipe(), Pipe()
+    srv = EngineServer(engine=None, conns=[sa, sb])
+    big = P.pack_control({"pad": "x" * (1 << 20)})  # ~1 MiB: a few fill the socket buffer
+    for _ in range(8):
+        srv._send(sa, big)  # client A never reads
+    t0 = time.perf_counter()
+    for i in range(50):
+        srv._send(sb, P.pack_control({"i": i}))
+    got = [P.unpack_control(cb.recv_bytes())["i"] for _ in range(50)]
+    assert got == list(range(50)) and time.perf_counter() - t0 < 5.0
+    t1 = time.perf_counter()
+    srv.flush(timeout=0.5)  # A's queue cannot drain: flush returns at its timeout
+    assert time.perf_counter() - t1 < 2.0
+    ca.close()  # A goes away: its sender drops what is left and the thread ends
+    srv._drop(0)
+
+    def senders() -> int:
+        return sum(t.name == "engine-send" for t in threading.enumerate())
+
+    deadline = time.time() + 5
+    while senders() > 1 and time.time() < deadline:
+        time.sleep(0.05)
+    assert senders() == 1  # B's

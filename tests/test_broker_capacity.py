@@ -57,6 +57,8 @@ def measured_shares():
             rec = json.loads([x for x in open(p) if x.startswith("{")][-1])
         except (ValueError, IndexError):
             continue
+        if str(rec.get("weights", "")).startswith("random"):
+            continue  # random weights dead-letter every message: not the traffic mix
         if rec.get("bus_members") and all("messages" in m for m in rec["bus_members"]):
             key = (os.path.basename(p)[:3], os.path.getmtime(p))
             if best is None or key > best[0]:

@@ -110,22 +110,44 @@ __device__ __forceinline__ float silu(float g) { return g * __builtin_amdgcn_rcp
 // registers — nothing for the compiler to sink or spill (cdna_hip_programming.md §5).
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int ROWS, int NW>
+// BKT 32 (64-B rows, 4 chunks): one instruction writes 16 rows (lane l -> row l>>2,
+// physical chunk l&3) and physical chunk p of row r holds logical chunk
+// p ^ ((r >> 1) & 2) -- the XOR that keeps every ds_read_b128 lane group of the
+// fragment reads on distinct bank slots with 64-B rows (rows r, r+4, r+8, r+12 share
+// banks; they differ in bit 2 or 3 of r)
+__device__ __forceinline__ int sw32(int row) { return (row >> 1) & 2; }
+
+template <int ROWS, int NW, int BKT = BK>
 __device__ __forceinline__ void issue_tile(const uint16_t* __restrict__ src, int ld, int r0, int rmax, int k0,
                                            uint16_t* dst, int wave, int lane) {
-  static_assert(ROWS % 8 == 0, "8-row pieces");
-  constexpr int PIECES = ROWS / 8;
-  const int rr = lane >> 3, p = lane & 7;
-  // every wave issues the same count (the K loop's counted vmcnt): when the pieces do
-  // not divide evenly (96 rows over 8 waves), the spare issues re-load the last piece
-  // into its own place (same bytes, same LDS address)
+  if constexpr (BKT == 32) {
+    static_assert(ROWS % 16 == 0, "16-row pieces");
+    constexpr int PIECES = ROWS / 16;
+    const int rr = lane >> 2, p = lane & 3;
 #pragma unroll
-  for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
-    const int g = PIECES % NW == 0 ? wave + NW * i : min(wave + NW * i, PIECES - 1);  // 8-row piece
-    const int row = 8 * g + rr;
-    const int gr = min(r0 + row, rmax);  // rows past the end re-read the last row (never stored)
-    const uint16_t* gp = src + (size_t)gr * ld + k0 + ((p ^ (row & 7)) << 3);
-    __builtin_amdgcn_global_load_lds((const void*)gp, (lds_ptr_t)(dst + g * 8 * BK), 16, 0, 0);
+    for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
+      const int g = PIECES % NW == 0 ? wave + NW * i : min(wave + NW * i, PIECES - 1);
+      const int row = 16 * g + rr;
+      const int gr = min(r0 + row, rmax);
+      const uint16_t* gp = src + (size_t)gr * ld + k0 + ((p ^ sw32(row)) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)gp, (lds_ptr_t)(dst + g * 16 * BKT), 16, 0, 0);
+    }
+  } else {
+    static_assert(BKT == 64, "BK 64 or 32");
+    static_assert(ROWS % 8 == 0, "8-row pieces");
+    constexpr int PIECES = ROWS / 8;
+    const int rr = lane >> 3, p = lane & 7;
+    // every wave issues the same count (the K loop's counted vmcnt): when the pieces do
+    // not divide evenly (96 rows over 8 waves), the spare issues re-load the last piece
+    // into its own place (same bytes, same LDS address)
+#pragma unroll
+    for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
+      const int g = PIECES % NW == 0 ? wave + NW * i : min(wave + NW * i, PIECES - 1);  // 8-row piece
+      const int row = 8 * g + rr;
+      const int gr = min(r0 + row, rmax);  // rows past the end re-read the last row (never stored)
+      const uint16_t* gp = src + (size_t)gr * ld + k0 + ((p ^ (row & 7)) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)gp, (lds_ptr_t)(dst + g * 8 * BK), 16, 0, 0);
+    }
   }
 }
 
@@ -139,22 +161,23 @@ __device__ __forceinline__ float sumsq_frag(const bf16x8& v, float acc) {
   return acc;
 }
 
-template <int FM, int FN, int NORM>
+template <int FM, int FN, int NORM, int BKT = BK>
 __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], const uint16_t* as,
                                          const uint16_t* bs, int wm0, int wn0, int lane) {
+  auto at = [](int row, int ch) { return row * BKT + ((BKT == 64 ? ch ^ (row & 7) : ch ^ sw32(row)) << 3); };
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < BKT / 32; ++s) {
     const int ch = s * 4 + (lane >> 4);
     bf16x8 af[FM], bfr[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int row = wn0 + j * 16 + (lane & 15);
-      bfr[j] = *reinterpret_cast<const bf16x8*>(bs + row * BK + ((ch ^ (row & 7)) << 3));
+      bfr[j] = *reinterpret_cast<const bf16x8*>(bs + at(row, ch));
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int row = wm0 + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const bf16x8*>(as + row * BK + ((ch ^ (row & 7)) << 3));
+      af[i] = *reinterpret_cast<const bf16x8*>(as + at(row, ch));
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
@@ -175,7 +198,7 @@ __device__ __forceinline__ void mma_tile(f32x4 (&acc)[FM][FN], float (&ss)[FM], 
 // prologue loads either, 4 = as 3 and no epilogue (nothing stored).
 // NORM: 0 none, 1 row scale from x² accumulated beside the MFMAs, 2 row scale from
 // the producer's partial sums (NormArgs).
-template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST, int PROBE = 0>
+template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST, int PROBE = 0, int BKT = BK>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t* __restrict__ A, int lda,
                                                          const uint16_t* __restrict__ W,
                                                          uint16_t* C, int ldc, const uint16_t* R, int ldr,
@@ -192,8 +215,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   static_assert(EPI != 2 || FN % 2 == 0, "SwiGLU pairs gate/up 16-col groups inside a wave tile");
   constexpr int BNO = EPI == 2 ? BN / 2 : BN;  // output columns of the block
   constexpr int CST = BNO + 8;                // staged C row stride (elements), +16 B pad
-  constexpr int TILE = (BM + BN) * BK;        // one stage (A + B) in elements
-  constexpr int NI = (BM / 8 + NW - 1) / NW + (BN / 8 + NW - 1) / NW;  // glds instructions per stage per wave
+  constexpr int TILE = (BM + BN) * BKT;       // one stage (A + B) in elements
+  constexpr int RPI = BKT == 64 ? 8 : 16;     // rows per LDS-DMA instruction (1 KiB)
+  constexpr int NI = (BM / RPI + NW - 1) / NW + (BN / RPI + NW - 1) / NW;  // glds instructions per stage per wave
   static_assert(ST >= 2 && ST <= 4, "pipeline stages");
   static_assert(BM * CST <= ST * TILE, "C staging fits in the K-loop buffers");
   // EPI 1 with a non-power-of-two chunk count per row (96 / 192-wide tiles) sums the
@@ -307,30 +331,30 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   // wave's newest NI·(ST-1) resp. NI·(ST-2) DMAs may stay outstanding): past the last tile the
   // issue slot re-loads tile KT-1 into the idle buffer (never read) so the count
   // stays exact.  Raw s_barrier: a __syncthreads() would drain the DMA queue.
-  const int KT = K / BK;
+  const int KT = K / BKT;
   if constexpr (PROBE >= 3) {  // no loads at all: deterministic (zero) LDS operands
     for (int i = tid * 8; i < ST * TILE; i += NT * 8) *reinterpret_cast<uint4*>(smem + i) = make_uint4(0, 0, 0, 0);
     __syncthreads();
   }
 #pragma unroll
   for (int s0 = 0; s0 < (PROBE >= 3 ? 0 : ST - 1); ++s0) {
-    const int kk = min(s0, KT - 1) * BK;
-    issue_tile<BM, NW>(A, lda, m0, M - 1, kk, smem + s0 * TILE, wave, lane);
-    issue_tile<BN, NW>(W, K, n0, N - 1, kk, smem + s0 * TILE + BM * BK, wave, lane);
+    const int kk = min(s0, KT - 1) * BKT;
+    issue_tile<BM, NW, BKT>(A, lda, m0, M - 1, kk, smem + s0 * TILE, wave, lane);
+    issue_tile<BN, NW, BKT>(W, K, n0, N - 1, kk, smem + s0 * TILE + BM * BKT, wave, lane);
   }
   int cur = 0;
   if constexpr (ST == 2) {
     for (int kt = 0; kt < KT; ++kt) {
       const int nb = cur ^ 1;  // buffer of tile kt + 1 == (kt - 1) % 2
-      const int kk = min(kt + 1, KT - 1) * BK;
+      const int kk = min(kt + 1, KT - 1) * BKT;
       if constexpr (PROBE != 2) {
-        issue_tile<BM, NW>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
-        issue_tile<BN, NW>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
+        issue_tile<BM, NW, BKT>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+        issue_tile<BN, NW, BKT>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BKT, wave, lane);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // tile kt landed (this wave's part)
       }
       __builtin_amdgcn_s_barrier();  // ... and every wave's part
       if constexpr (PROBE != 1)
-        mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+        mma_tile<FM, FN, NORM, BKT>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BKT, wm0, wn0, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // WAR: buffer `cur` is re-filled by the next issue
       cur ^= 1;
@@ -342,10 +366,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI * (ST - 2)) : "memory");  // tile kt landed (this wave)
       __builtin_amdgcn_s_barrier();                                          // ... every wave; kt-1 read
       const int nb = cur == 0 ? ST - 1 : cur - 1;  // buffer of tile kt + ST - 1 == (kt - 1) % ST
-      const int kk = min(kt + ST - 1, KT - 1) * BK;
-      issue_tile<BM, NW>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
-      issue_tile<BN, NW>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BK, wave, lane);
-      mma_tile<FM, FN, NORM>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BK, wm0, wn0, lane);
+      const int kk = min(kt + ST - 1, KT - 1) * BKT;
+      issue_tile<BM, NW, BKT>(A, lda, m0, M - 1, kk, smem + nb * TILE, wave, lane);
+      issue_tile<BN, NW, BKT>(W, K, n0, N - 1, kk, smem + nb * TILE + BM * BKT, wave, lane);
+      mma_tile<FM, FN, NORM, BKT>(acc, ss, smem + cur * TILE, smem + cur * TILE + BM * BKT, wm0, wn0, lane);
       cur = cur + 1 == ST ? 0 : cur + 1;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1039,17 +1063,18 @@ __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __
 
 int g_group_m = 8;  // M-tiles per rasterisation group (sg_gemm_set_group_m)
 
-template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST>
+template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST, int BKT = BK>
 int launch(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
            float eps, hipStream_t stream, const RopeArgs& ra = RopeArgs{}, const ArgmaxArgs& xa = ArgmaxArgs{},
            const NormArgs& na = NormArgs{}) {
   // the staged C tile must fit in the K-loop buffers (not so for 256-wide plain outputs)
   constexpr int BNO = EPI == 2 ? BN / 2 : BN;
-  if constexpr (BM * (BNO + 8) > ST * (BM + BN) * BK) {
+  if constexpr (BM * (BNO + 8) > ST * (BM + BN) * BKT) {
     return -3;
   } else {
+    if (K % BKT) return -2;
     const int tm = (M + BM - 1) / BM, tn = N / BN;
-    hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST>), dim3(tm * tn), dim3(WM * WN * 64), 0,
+    hipLaunchKernelGGL((gemm_fused_kernel<BM, BN, WM, WN, EPI, NORM, ST, 0, BKT>), dim3(tm * tn), dim3(WM * WN * 64), 0,
                        stream, (const uint16_t*)A, lda, (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R,
                        ldr, M, N, K, eps, tm, tn, g_group_m > 0 ? g_group_m : 1, ra, xa, na);
     return 0;
@@ -1074,14 +1099,17 @@ int dispatch_epi(int epi, int norm, const void* A, int lda, const void* W, void*
 
 // 96 / 192-wide tiles (3 MFMA columns per wave: no SwiGLU pairing) — the N = 576
 // residual GEMMs (o-proj, down-proj) and plain stores only
-template <int BM, int BN, int WM, int WN, int ST>
+template <int BM, int BN, int WM, int WN, int ST, int BKT = BK>
 int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr,
                    int M, int N, int K, float eps, hipStream_t s, const NormArgs& na) {
   const RopeArgs ra{};
   const ArgmaxArgs xa{};
-  if (epi == 1 && norm == 0) return launch<BM, BN, WM, WN, 1, 0, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
-  if (epi == 0 && norm == 0) return launch<BM, BN, WM, WN, 0, 0, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
-  if (epi == 0 && norm == 1) return launch<BM, BN, WM, WN, 0, 1, ST>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
+  if (epi == 1 && norm == 0)
+    return launch<BM, BN, WM, WN, 1, 0, ST, BKT>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
+  if (epi == 0 && norm == 0)
+    return launch<BM, BN, WM, WN, 0, 0, ST, BKT>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
+  if (epi == 0 && norm == 1)
+    return launch<BM, BN, WM, WN, 0, 1, ST, BKT>(A, lda, W, C, ldc, R, ldr, M, N, K, eps, s, ra, xa, na);
   return -3;
 }
 
@@ -1103,6 +1131,7 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  28: 128x192 (2x2) 2st   29: 256x96 (4x1) 2st — 64x96 wave tiles
 //  30: 128x96 (4x2) 2st, 8 waves   31: 64x96 (4x2) 2st, 8 waves
 //  32: 256x192 (4x2) 2st, 8 waves — 64x96 wave tiles (epi 0 / 1 only)
+//  33: 128x192 (2x2) BK 32, 4st   34: 256x192 (4x2) BK 32, 4st, 8 waves (epi 0 / 1 only)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1131,9 +1160,9 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[33] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96, 192};
-  if (cfg < 0 || cfg > 32) return -1;
+  static const int BNs[35] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96, 192, 192, 192};
+  if (cfg < 0 || cfg > 34) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1205,6 +1234,10 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     // 256x192, 8 waves, the 64x96 wave tiles of 28: 1.4x its MFMA work per staged byte
     // (the big-M residual loop is L2-bound at 77 FLOP/B; this tile is 110)
     case 32: return dispatch_resid<256, 192, 4, 2, 2>(SG_ARGS);
+    // BK 32 with 4 stages in the same LDS: three K-steps of loads in flight instead of one
+    // (the residual loop waits on loads: bytes in flight per CU set its rate)
+    case 33: return dispatch_resid<128, 192, 2, 2, 4, 32>(SG_ARGS);
+    case 34: return dispatch_resid<256, 192, 4, 2, 4, 32>(SG_ARGS);
     default: return dispatch_resid<32, 96, 2, 2, 2>(SG_ARGS);
   }
 #undef SG_ARGS

@@ -352,7 +352,7 @@ def test_gemm_argmax_matches_logits_path(cfg, M):
             assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 17, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32])
+@pytest.mark.parametrize("cfg", [1, 3, 17, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34])
 @pytest.mark.parametrize("M", [5, 333, 2048])
 def test_gemm_producer_norm(cfg, M):
     """Residual GEMM with ``ss_out`` writes per-N-tile x² partials of the rows it

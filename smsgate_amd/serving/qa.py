@@ -53,14 +53,18 @@ from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
            "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
            "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP",
-           "QF_TIME", "QF_DEND", "QF_AMPM", "QF_AP", "QF_M"]
+           "QF_TIME", "QF_DEND", "QF_AMPM", "QF_AP", "QF_M", "QF_TEXT"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
 QA_MAX_QUERIES = 24
 # per-token flags (uint32): starts / ends with a letter / digit, ends a card mask, class bits
 QF_SL, QF_SD, QF_EL, QF_ED, QF_MASK = 1, 2, 4, 8, 16
-QA_CLASS_BITS = {k: v << 3 for k, v in TOK_CLASS_BITS.items()}  # date 32, number 64, currency 128, card 256
+QF_TEXT = 1 << 21  # may be inside a free-text value (merchant / city / address): no ':' in it
+# date 32, number 64, currency 128, card 256; text: a label's colon ("Sender: NAME") is never
+# part of a name (no gold merchant / city / address of any family has one), so a text value
+# never runs across one
+QA_CLASS_BITS = {**{k: v << 3 for k, v in TOK_CLASS_BITS.items()}, "text": QF_TEXT}
 _NO_START_AFTER_MASK = QA_CLASS_BITS["date"] | QA_CLASS_BITS["number"]
 # edges: contains a line break; first non-space char a letter-or-digit / a digit; last
 # char a letter-or-digit / a digit; exactly three ASCII digits; a lone "," "." "'"
@@ -149,7 +153,8 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
     out = np.zeros(vocab, dtype=np.uint32)
     n = min(vocab, len(strings))
     for k, bit in QA_CLASS_BITS.items():
-        out[:n] |= np.where(classes[k][:n], bit, 0).astype(np.uint32)
+        out[:n] |= np.where(classes[k][:n], bit, 0).astype(np.uint32)  # text: every non-special token
+    no_text = np.uint32(~QF_TEXT & 0xFFFFFFFF)
     spec = set(specials)
 
     def letter(ch: str) -> bool:
@@ -196,6 +201,8 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
         if t.upper() == "M":
             f |= QF_M
         out[i] |= f
+        if ":" in t:
+            out[i] &= no_text
     return out
 
 

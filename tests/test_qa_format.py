@@ -144,6 +144,33 @@ def test_value_edges_follow_the_field_kind(env):
     assert "DUL ST. 108" in _spans_of(tk, fl, legacy, *rules["address"])
 
 
+def test_text_values_never_cross_a_colon(env):
+    """A free-text value never contains a label's colon: "Sender: TEAM" offers "TEAM" and
+    not "Sender: TEAM".  This was the held-out credit family's main error in round 5.
+    No gold merchant / city / address of any family contains ':'."""
+    tk, lay, fl = env
+    rules = dict(zip((f.name for f in lay.fields[1:]), lay.rules()))
+    body = "Incoming payment 943.47 GBP credited to card ****9788. Sender: TEAM, QNK4M. 2025-10-17 19:00"
+    merch = _spans_of(tk, fl, body, *rules["merchant"])
+    assert "TEAM" in merch and not any(":" in m for m in merch), merch
+    # the date keeps its colon (date class, not text)
+    assert "2025-10-17 19:00" in _spans_of(tk, fl, body, *rules["date"])
+    # decoding scores that prefer the labelled span yields the name alone
+    ids, offs = tk.encode_offsets([body])[0]
+    m = ids + [tk.ans]
+    a, _ = tk.value_span("Sender", body, ids, offs)
+    _, z = tk.value_span("TEAM", body, ids, offs)
+    a2, _ = tk.value_span("TEAM", body, ids, offs)
+    cl = np.array([5.0, -5, -5, -5])
+    st, en, nl = np.full((8, 130), -5.0), np.full((8, 130), -5.0), np.full(8, 10.0)
+    f = NAMES[1:].index("merchant")
+    nl[f] = -10.0
+    st[f, a], st[f, a2], en[f, z] = 5.0, 3.0, 5.0
+    (_, spans), = qa_decode_ref([cl], [st], [nl], [en], [m], fl, lay)
+    s0, e0 = spans[f]
+    assert "".join(tk.token_strings[t] for t in m[s0:e0 + 1]).strip() == "TEAM"
+
+
 @pytest.mark.parametrize("body,picked,want", [
     ("Карта **3001 22:09 13.02.2023 покупка на сумму 186379.01 RUB", "13.02.2023", "22:09 13.02.2023"),
     ("Оплата 13.02.2023 22:09 на сумму 5.00 RUB", "13.02.2023", "13.02.2023 22:09"),

@@ -2198,7 +2198,10 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   if ((g_prefill_impl == 2 || g_prefill_impl >= 4) && G <= 16) {
     // st64 (impl 6): 64 columns, half the waves re-read a sequence's keys; st32pf (impl 7):
     // st32 with the one-tile register prefetch; stpf (impl 8): st with it
-    const int ncb = (g_prefill_impl == 4 || g_prefill_impl == 8) ? 1 : g_prefill_impl == 6 ? 4 : 2, qpw = 16 * ncb / G;
+    // auto from 1 024 sequences (the qa engine's packed batches: 2 211 / 4 422 sequences of
+    // ~50 rows): st64, 103.4 / 198.7 us vs 110.0 / 210.0 for st32 (profiles/r05_prefill_qa.jsonl)
+    const bool wide = g_prefill_impl == 6 || (g_prefill_impl == 2 && nseq >= 1024);
+    const int ncb = (g_prefill_impl == 4 || g_prefill_impl == 8) ? 1 : wide ? 4 : 2, qpw = 16 * ncb / G;
     dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
 #define SG_PST(NC, PFV)                                                                                             \
   hipLaunchKernelGGL((attn_prefill_st_kernel<NC, PFV>), grid, dim3(64), 0, stream, (const uint16_t*)q, cu_q, q_start, \

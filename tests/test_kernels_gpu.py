@@ -130,6 +130,36 @@ def test_attn_prefill(P0, heads, impl):
         o += n
 
 
+def test_attn_prefill_auto_width_is_bitwise_stable():
+    """auto switches the transposed kernel from 32 to 64 columns per wave at 1 024
+    sequences (the qa engine's batches).  A column's arithmetic does not depend on the
+    width, so outputs are bit for bit the same.  A message's answer then cannot depend
+    on the batch it was packed into."""
+    nh, nkv, D, Lmax, P0 = 9, 3, 64, 192, 4
+    g = torch.Generator(device="cpu").manual_seed(3)
+    lens = torch.randint(45, 56, (1100,), generator=g).tolist()
+    S, T = len(lens), sum(lens)
+    q = _bf(T, nh, D, seed=31)
+    kc = _bf(S, nkv, Lmax, D, seed=32)
+    vt = ops.rows_to_vt(_bf(S, nkv, Lmax, D, seed=33))
+    pk = torch.zeros(nkv, 32, D, dtype=torch.bfloat16, device=DEV)
+    pk[:, :P0] = _bf(nkv, P0, D, seed=34)
+    pvt = ops.rows_to_vt(pk.clone())
+    cu = torch.tensor([0] + torch.cumsum(torch.tensor(lens), 0).tolist(), dtype=torch.int32, device=DEV)
+    qs = torch.zeros(S, dtype=torch.int32, device=DEV)
+    sl = torch.arange(S, dtype=torch.int32, device=DEV)
+    outs = {}
+    try:
+        for impl in ("st32", "st64", "auto"):
+            ops.set_prefill_impl(impl)
+            out = torch.empty(T, nh * D, dtype=torch.bfloat16, device=DEV)
+            ops.attn_prefill(q, cu, qs, sl, max(lens), kc, vt, pk, pvt, P0, out, 1 / math.sqrt(D))
+            outs[impl] = out
+    finally:
+        ops.set_prefill_impl("auto")
+    assert torch.equal(outs["st32"], outs["st64"]) and torch.equal(outs["auto"], outs["st64"])
+
+
 @pytest.mark.parametrize("impl", ["grouped", "grouped_h", "grouped6", "grouped_pf", "cascade", "mfma", "mfma_v1", "valu", "split2", "split4",
                                   "split8"])
 @pytest.mark.parametrize("P0", [0, 20, 75])

@@ -40,7 +40,7 @@ def main() -> int:
     p.add_argument("--save-dir", default="")
     p.add_argument("--variants", default="",
                    help="';'-separated training variants of the FIRST format, each 'key=value,...' over steps, "
-                        "negatives, lr, fused, proc (procedural family weight, SMSGATE_PROC_WEIGHT), labels (pseudo-word label share, SMSGATE_SYNTH_LABELS); e.g. "
+                        "negatives, lr, fused, proc (procedural family weight, SMSGATE_PROC_WEIGHT), labels (pseudo-word label share, SMSGATE_SYNTH_LABELS), seed (training sample); e.g. "
                         "'steps=4000;steps=6000;proc=6'")
     a = p.parse_args()
     if a.variants:
@@ -120,11 +120,12 @@ def _variants(a) -> int:
             else:
                 os.environ.pop(env, None)
         t0 = time.time()
-        data = ExamplePool(steps * a.batch, seed=0, families="train", workers=12, answer_format=fmt,
+        seed = int(kv.get("seed", 0))  # the training sample (data and init); the bench trains seed 0
+        data = ExamplePool(steps * a.batch, seed=seed, families="train", workers=12, answer_format=fmt,
                            negatives=neg).get()
         tc = TrainConfig(model=a.model, steps=steps, batch=a.batch, lr=float(kv.get("lr", a.lr)),
                          n_examples=steps * a.batch, log_every=1000, data_parallel=False, families="train",
-                         answer_format=fmt, negatives=neg, fused=bool(int(kv.get("fused", 1))))
+                         answer_format=fmt, negatives=neg, fused=bool(int(kv.get("fused", 1))), seed=seed)
         t1 = time.time()
         w = train_extractor(tc, device="cuda", data=data, log=lambda s: print(f"[{spec}] {s}", flush=True))
         res = {"format": fmt, "variant": spec, "steps": steps, "negatives": neg, "data_s": round(t1 - t0, 1),

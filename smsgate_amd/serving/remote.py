@@ -64,12 +64,15 @@ class EngineServer:
         # connection's responses the same way
         self._senders: Dict[int, "queue.SimpleQueue"] = {}  # id(connection) -> its FIFO
         self._senders_lock = threading.Lock()
+        self._dropped: set = set()  # connections gone: late frames for them are discarded
 
     def _send(self, c: Connection, frame: bytes) -> None:
         """Queue ``frame`` for ``c`` (its frames leave in order, on its own thread)."""
         q = self._senders.get(id(c))
         if q is None:
             with self._senders_lock:
+                if c in self._dropped:  # (no new sender thread for a connection that is gone)
+                    return
                 q = self._senders.get(id(c))
                 if q is None:
                     q = self._senders[id(c)] = queue.SimpleQueue()
@@ -122,6 +125,7 @@ class EngineServer:
                 pass
             with self._senders_lock:
                 q = self._senders.pop(id(c), None)
+                self._dropped.add(c)
             if q is not None:  # its sender ends after the frames already queued
                 q.put(None)
 

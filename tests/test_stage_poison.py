@@ -516,3 +516,5 @@ def test_engine_server_slow_reader_does_not_hold_back_others():
     while senders() > base + 1 and time.time() < deadline:
         time.sleep(0.05)
     assert senders() == base + 1  # B's
+    srv._send(sa, big)  # a late frame for the dropped connection starts no new sender
+    assert senders() == base + 1

@@ -68,18 +68,22 @@ def _args(argv=None):
     # span answers: held-out formats exact 0.973 / 0.980 / 0.992 / 0.993 at 2 / 3 / 4 / 5 k steps
     # (profiles/r04_family_probe_span5k.jsonl, one 5 k-step cosine run); 4 k keeps the whole
     # bench inside ~7 minutes
-    p.add_argument("--train-steps", type=int, default=4000)
-    p.add_argument("--train-batch", type=int, default=128, help="global training batch (split over ranks)")
-    p.add_argument("--train-lr", type=float, default=1e-3)
+    # the training defaults ARE the flagship recipe (models/train.py FLAGSHIP_RECIPE), the one
+    # `train-extractor` and the compose `train` service use: the deployed model is the benchmarked one
+    from smsgate_amd.models.train import FLAGSHIP_RECIPE as R
+
+    p.add_argument("--train-steps", type=int, default=R.steps)
+    p.add_argument("--train-batch", type=int, default=R.batch, help="global training batch (split over ranks)")
+    p.add_argument("--train-lr", type=float, default=R.lr)
     # qa: the round-5 default -- the whole answer from ONE forward (serving/qa.py: query tokens
     # after the body, joint constrained span decode; no decode steps); span: round 4's
     # autoregressive pointers (2 decode steps per copied field); copy: each copied field
     # written with the body's tokens (speculative prompt-lookup decoding)
-    p.add_argument("--answer-format", default="qa", choices=["copy", "span", "qa", "qa17"],
+    p.add_argument("--answer-format", default=R.answer_format, choices=["copy", "span", "qa", "qa17"],
                    help="qa: one forward, one query row per field (qa17: a start and an end row per field); span: "
                         "two pointer decode steps per copied field (serving/fsm.py build_span_fsm); copy: each copied "
                         "field written with the body's tokens (speculative prompt-lookup decoding)")
-    p.add_argument("--train-negatives", type=float, default=0.12,
+    p.add_argument("--train-negatives", type=float, default=R.negatives,
                    help="share of non-transaction training examples (utils/synth.py NEG_TRAIN_FAMILIES)")
     p.add_argument("--train-ddp", type=int, default=1, choices=[0, 1],
                    help="1: with several ranks, train on all of them (RCCL data parallel over the global batch); "
@@ -719,7 +723,7 @@ def _train_plan(args):
     import tempfile
 
     from smsgate_amd.models.tokenizer import ASSET
-    from smsgate_amd.models.train import TrainConfig
+    from smsgate_amd.models.train import recipe
     from smsgate_amd.parse.schema import EXTRACTOR_PROMPT
     from smsgate_amd.utils import synth
 
@@ -727,9 +731,8 @@ def _train_plan(args):
     # serves identical weights) and publishes the file; the other ranks load it.
     # Fresh examples for every step (steps x batch unique synthetic SMS, none repeated):
     # held-out exact 89.6 % vs 87.4 % for 60 k examples reused ~4x (profiles/r03_quality_probe.jsonl)
-    tc = TrainConfig(model=args.model, steps=args.train_steps, batch=args.train_batch, lr=args.train_lr,
-                     n_examples=args.train_steps * args.train_batch, log_every=200, data_parallel=False,
-                     families="train", answer_format=args.answer_format, negatives=args.train_negatives)
+    tc = recipe(args.model, args.train_steps, args.train_batch, lr=args.train_lr, log_every=200,
+                data_parallel=False, answer_format=args.answer_format, negatives=args.train_negatives)
     # every source the trained weights depend on (a cached file from older training code
     # on the same box was reused once: the key now covers the trainer, the answer FSM,
     # the model and the tokenizer code too)

@@ -231,13 +231,25 @@ def _engine_server(a) -> None:
         exporter.stop()
 
 
+def train_config(a, world: int = 1):
+    """The :class:`TrainConfig` of ``train-extractor`` arguments: the flagship recipe
+    (models/train.py FLAGSHIP_RECIPE -- what bench.py trains and measures) with the
+    given overrides; ``--batch`` is the global batch, split over ``world`` ranks."""
+    from .models.train import recipe
+
+    return recipe(a.model, a.steps, a.batch, world=world, lr=a.lr, n_examples=a.examples, seed=a.seed,
+                  ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, bucket_mb=a.bucket_mb,
+                  answer_format=a.answer_format, families=None if a.families == "legacy" else a.families,
+                  negatives=a.negatives)
+
+
 def _train(a, settings) -> None:
     """``train-extractor``; under ``torchrun --nproc-per-node N`` one rank per GPU
     (RCCL data parallel, :mod:`smsgate_amd.parallel.ddp`)."""
     import torch
     import torch.distributed as dist
 
-    from .models.train import TrainConfig, train_extractor
+    from .models.train import train_extractor
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     device = settings.llm_device
@@ -250,10 +262,7 @@ def _train(a, settings) -> None:
         else:
             device = "cpu"
             dist.init_process_group("gloo")
-    cfg = TrainConfig(model=a.model, steps=a.steps, batch=a.batch, lr=a.lr, n_examples=a.examples,
-                      ckpt_dir=a.ckpt_dir, ckpt_every=a.ckpt_every, resume=a.resume, bucket_mb=a.bucket_mb,
-                      answer_format=a.answer_format, families=None if a.families == "legacy" else a.families,
-                      negatives=a.negatives)
+    cfg = train_config(a, world)
     w = train_extractor(cfg, device=device)
     if not dist.is_initialized() or dist.get_rank() == 0:
         w.save(a.out)
@@ -357,21 +366,25 @@ def build_parser() -> argparse.ArgumentParser:
     lg.add_argument("--cache", default="sms_cache.sqlite")
     lg.add_argument("--purchases", default="parsed_sms_cache.sqlite")
     lg.add_argument("--credits", default="credit_sms_cache.sqlite")
-    tr = sp.add_parser("train-extractor", help="train the local extractor LM on synthetic SMS (GPU)")
-    tr.add_argument("--model", default="smollm-135m")
-    tr.add_argument("--steps", type=int, default=1500)
-    tr.add_argument("--batch", type=int, default=64)
-    tr.add_argument("--lr", type=float, default=1e-3)
-    tr.add_argument("--examples", type=int, default=60000)
+    from .models.train import FLAGSHIP_RECIPE as R
+
+    tr = sp.add_parser("train-extractor", help="train the local extractor LM on synthetic SMS (GPU); the defaults "
+                       "are the flagship recipe bench.py trains and measures (models/train.py FLAGSHIP_RECIPE)")
+    tr.add_argument("--model", default=R.model)
+    tr.add_argument("--steps", type=int, default=R.steps)
+    tr.add_argument("--batch", type=int, default=R.batch, help="GLOBAL batch (split over torchrun ranks)")
+    tr.add_argument("--lr", type=float, default=R.lr)
+    tr.add_argument("--examples", type=int, default=0, help="training examples (0 = steps x batch, all fresh)")
+    tr.add_argument("--seed", type=int, default=R.seed)
     tr.add_argument("--out", required=True, help="safetensors path (LLM_CHECKPOINT for the local_llm backend)")
     tr.add_argument("--ckpt-dir", default=None, help="training checkpoints (weights + optimizer + step)")
     tr.add_argument("--ckpt-every", type=int, default=0)
     tr.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --ckpt-dir")
     tr.add_argument("--bucket-mb", type=float, default=64.0, help="DP gradient all-reduce bucket size")
-    tr.add_argument("--answer-format", default="qa", choices=["copy", "span", "qa", "qa17"],
+    tr.add_argument("--answer-format", default=R.answer_format, choices=["copy", "span", "qa", "qa17"],
                     help="qa: the whole answer from one forward (serving/qa.py); span: two pointer decode steps "
                          "per copied field; copy: the body's tokens (the checkpoint records it; the engine follows)")
-    tr.add_argument("--negatives", type=float, default=0.12,
+    tr.add_argument("--negatives", type=float, default=R.negatives,
                     help="share of non-transaction examples (txn_type unknown / otp, null fields)")
     tr.add_argument("--families", default="train", help="train (every training SMS layout) | legacy (the two "
                     "reference formats only)")

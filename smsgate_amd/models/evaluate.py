@@ -17,7 +17,7 @@ Two numbers matter and they are different things:
 from __future__ import annotations
 
 from decimal import Decimal
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 __all__ = ["score_answers", "evaluate_engine", "regex_answers", "golden_case_results", "golden_case_mismatches",
            "TorchQAExtractor", "evaluate_negatives",
@@ -63,24 +63,35 @@ def _same(field: str, got: Any, want: Any) -> bool:
 
 
 def score_answers(items: Sequence[Any], answers: Sequence[Optional[Dict[str, Any]]],
-                  by_family: bool = False) -> Dict[str, Any]:
+                  by_family: bool = False, per_item: bool = False) -> Dict[str, Any]:
     """``items``: :class:`~smsgate_amd.utils.synth.SynthSMS` with answers;
     ``answers``: the raw extractor answers in the same order.  Every field is
     compared AFTER the real post-processing chain (the stored ``ParsedSMS``
     value: datetime, Decimal, ISO currency, 4-digit card) with the generator's
-    expected value; ``exact`` = all nine fields right.  ``by_family``: also the
-    exact rate per template family."""
+    expected value; ``exact`` = all nine fields right.  ``published_wrong_rate``: the
+    share that would be published on sms.parsed with a wrong field (parsed, not
+    exact) -- the cost a wrong answer has and a declined one (``declined_rate``:
+    answered as a non-transaction, dead-lettered) does not.  ``by_family``: also the
+    exact rate per template family (and ``wrong_by_family``); ``per_item``: also the
+    (published, exact) flags of every item (calibration)."""
+    from ..serving.qa import REJECT_TXN
+
     n = len(items)
     parsed = 0
+    declined = 0
     hits = {f: 0 for f in _FIELDS}
     whole = 0
     fam_n: Dict[str, int] = {}
     fam_ok: Dict[str, int] = {}
+    fam_wrong: Dict[str, int] = {}
+    flags: List[Tuple[bool, bool]] = []
     for it, ans in zip(items, answers):
         fam = getattr(it, "family", "legacy")
         fam_n[fam] = fam_n.get(fam, 0) + 1
+        declined += bool(ans) and ans.get("txn_type") in REJECT_TXN
         p = _post(it.body, it.timestamp, ans)
         if p is None:
+            flags.append((False, False))
             continue
         parsed += 1
         want = _expected(it)
@@ -94,10 +105,16 @@ def score_answers(items: Sequence[Any], answers: Sequence[Optional[Dict[str, Any
             ok &= same
         whole += ok
         fam_ok[fam] = fam_ok.get(fam, 0) + ok
+        fam_wrong[fam] = fam_wrong.get(fam, 0) + (not ok)
+        flags.append((True, ok))
     d = max(1, n)
-    out = {"n": n, "parse_rate": parsed / d, "field_acc": {f: hits[f] / d for f in _FIELDS}, "exact": whole / d}
+    out = {"n": n, "parse_rate": parsed / d, "field_acc": {f: hits[f] / d for f in _FIELDS}, "exact": whole / d,
+           "published_wrong_rate": (parsed - whole) / d, "declined_rate": declined / d}
     if by_family:
         out["by_family"] = {f: round(fam_ok.get(f, 0) / c, 4) for f, c in sorted(fam_n.items())}
+        out["wrong_by_family"] = {f: round(fam_wrong.get(f, 0) / c, 4) for f, c in sorted(fam_n.items())}
+    if per_item:
+        out["items"] = flags
     return out
 
 
@@ -109,7 +126,7 @@ def regex_answers(items: Sequence[Any]) -> List[Dict[str, Any]]:
 
 
 def evaluate_engine(engine, n: int = 500, seed: int = 987654, vocab_name: str = "heldout",
-                    families: Any = None, with_regex: bool = False) -> Dict[str, Any]:
+                    families: Any = None, with_regex: bool = False, per_item: bool = False) -> Dict[str, Any]:
     """Decode ``n`` generated SMS (LLM-routed kinds only) and score them.
     ``families``: None = the legacy mix, else template families (``"heldout"`` = the
     layouts never trained on); ``with_regex`` adds the regex backend's score on the
@@ -119,7 +136,9 @@ def evaluate_engine(engine, n: int = 500, seed: int = 987654, vocab_name: str = 
 
     items = [s for s in generate(n, seed=seed, vocab_name=vocab_name, families=families) if s.answer is not None]
     answers = engine.run([normalize_body(s.body) for s in items])
-    out = score_answers(items, answers, by_family=families is not None)
+    out = score_answers(items, answers, by_family=families is not None, per_item=per_item)
+    if per_item and getattr(engine, "last_conf", None) is not None and len(engine.last_conf) == len(items):
+        out["conf"] = [round(float(c), 5) for c in engine.last_conf]
     out["vocab"] = vocab_name
     if families is not None:
         out["families"] = families if isinstance(families, str) else list(families)
@@ -134,8 +153,10 @@ class TorchQAExtractor:
     (quality probes, CPU tests; serving/qa_engine.py is the GPU engine)."""
 
     def __init__(self, weights, tokenizer=None, max_body: int = 128, batch: int = 256,
-                 compute_dtype=None) -> None:
+                 compute_dtype=None, min_conf: Optional[float] = None) -> None:
         import torch
+
+        from ..serving.engine import QA_MIN_CONF
 
         from ..serving.qa import qa_layout, qa_token_flags
         from .extractor import SPAN_PTR0
@@ -151,27 +172,44 @@ class TorchQAExtractor:
         self.max_body = max_body
         self.batch = batch
         self.compute_dtype = compute_dtype or torch.float32
+        # abstention threshold (serving/qa.py qa_decode_ref); the confidence of every
+        # answer of the last run() is kept in ``last_conf`` (calibration)
+        self.min_conf = QA_MIN_CONF if min_conf is None else float(min_conf)
+        self.last_conf: List[float] = []
 
-    def decode_ids(self, msgs: Sequence[Sequence[int]]):
-        """(class, spans) per message (``body <ans>`` ids)."""
+    def scores(self, msgs: Sequence[Sequence[int]]):
+        """The head's fp32 scores of ``msgs`` (``body <ans>`` ids): (cls [M, 4],
+        start [M, nf, n_pos], null [M, nf], end [M, nf, n_pos]) numpy arrays."""
+        import numpy as np
         import torch
 
         from ..parse.schema import EXTRACTOR_PROMPT
-        from ..serving.qa import qa_decode_ref, qa_logits
+        from ..serving.qa import qa_logits
         from .extractor import reference_forward
         from .train import qa_batch
 
         prefix = self.tok.prefix_ids(EXTRACTOR_PROMPT)
         dev = self.w.embed.device
-        out = []
+        parts = []
         for k in range(0, len(msgs), self.batch):
             part = [list(m) for m in msgs[k:k + self.batch]]
             exs = [(m, (0, [(-1, -1)] * self.lay.n_copy)) for m in part]
             ids, add, qpos, _ = qa_batch(prefix, exs, self.tok.pad, dev, self.lay)
             with torch.no_grad():
                 h = reference_forward(self.w, ids, compute_dtype=self.compute_dtype, return_hidden=True, add_ids=add)
-                cls, st, nl, en = (t.float().cpu().numpy() for t in qa_logits(h, self.w.embed, qpos, self.lay))
-            out += qa_decode_ref(cls, st, nl, en, part, self.flags, self.lay)
+                parts.append([t.float().cpu().numpy() for t in qa_logits(h, self.w.embed, qpos, self.lay)])
+        return tuple(np.concatenate([p[i] for p in parts]) for i in range(4))
+
+    def decode_ids(self, msgs: Sequence[Sequence[int]]):
+        """(class, spans) per message (``body <ans>`` ids)."""
+        from ..serving.qa import qa_decode_ref
+
+        out = []
+        self.last_conf = []
+        for k in range(0, len(msgs), self.batch):
+            part = [list(m) for m in msgs[k:k + self.batch]]
+            cls, st, nl, en = self.scores(part)
+            out += qa_decode_ref(cls, st, nl, en, part, self.flags, self.lay, self.min_conf, self.last_conf)
         return out
 
     def run(self, bodies: Sequence[str]) -> List[Dict[str, Optional[str]]]:

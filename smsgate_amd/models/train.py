@@ -50,7 +50,7 @@ from ..parse.text import normalize_body
 from .extractor import CONFIGS, SPAN_PTR0, ExtractorWeights, qa_config, reference_forward, span_config
 from .tokenizer import ExtractorTokenizer, load_tokenizer
 
-__all__ = ["TrainConfig", "answer_tokens", "answer_span_tokens", "answer_fsm", "make_examples", "ExamplePool", "train_extractor", "field_accuracy",
+__all__ = ["TrainConfig", "FLAGSHIP_RECIPE", "recipe", "answer_tokens", "answer_span_tokens", "answer_fsm", "make_examples", "ExamplePool", "train_extractor", "field_accuracy",
            "latest_checkpoint", "to_serving", "qa_batch", "QASpec"]
 
 
@@ -97,6 +97,36 @@ class TrainConfig:
     # share of training examples drawn from the non-transaction families (utils/synth.py
     # NEG_TRAIN_FAMILIES: answer txn_type unknown / otp, every other field null)
     negatives: float = 0.12
+
+
+# The ONE training recipe of the served extractor: bench.py's in-run
+# training, ``python -m smsgate_amd train-extractor``'s defaults and the compose ``train``
+# service all resolve to it (tests/test_deploy.py pins that), so the deployed model is
+# the benchmarked one.  Fresh examples every step (n_examples = steps x global batch: a
+# reused 60 k pool scored 87.4 vs 89.6 % held-out exact, profiles/r03_quality_probe.jsonl),
+# 4 000 steps (6 000 did not help held-out formats, 96.5 vs 98.6 %,
+# profiles/r05_qa_probe4_steps.jsonl), the one-forward qa answers, 12 % non-transactions.
+# ``batch`` is the GLOBAL batch: data-parallel runs split it over the ranks
+# (``global_batch``), so N GPUs train on the one-GPU run's batches.
+FLAGSHIP_RECIPE = TrainConfig(model="smollm-135m", steps=4000, batch=128, lr=1e-3, n_examples=4000 * 128,
+                              families="train", answer_format="qa", negatives=0.12, seed=0)
+
+
+def recipe(model: Optional[str] = None, steps: Optional[int] = None, batch: Optional[int] = None,
+           world: int = 1, **overrides) -> TrainConfig:
+    """:data:`FLAGSHIP_RECIPE` with ``model`` / ``steps`` / global ``batch`` overridden
+    (``n_examples`` follows: steps x batch fresh examples) and, for ``world`` > 1
+    data-parallel ranks, the per-rank batch with ``global_batch`` set."""
+    r = FLAGSHIP_RECIPE
+    steps = r.steps if steps is None else steps
+    batch = r.batch if batch is None else batch
+    cfg = dataclasses.replace(r, model=model or r.model, steps=steps, batch=batch,
+                              n_examples=overrides.pop("n_examples", 0) or steps * batch, **overrides)
+    if world > 1:
+        if batch % world:
+            raise ValueError(f"global batch {batch} does not split over {world} ranks")
+        cfg = dataclasses.replace(cfg, batch=batch // world, global_batch=batch, data_parallel=True)
+    return cfg
 
 
 def answer_tokens(tok: ExtractorTokenizer, fsm, answer: Dict[str, Optional[str]],
@@ -183,6 +213,9 @@ def answer_fsm(tok: ExtractorTokenizer, fmt: str = "copy", max_body: int = 128):
     if fmt in ("qa", "qa17"):
         from ..serving.qa import qa_layout, qa_token_flags
 
+        # the engines (QAEngine, TorchQAExtractor) lay the pointer / query / class rows out
+        # from SPAN_PTR0: a tokenizer of another size would train other rows than they serve
+        assert v_tok == SPAN_PTR0, "the qa format's pointer ids follow the 8 192-id tokenizer"
         lay = qa_layout(v_tok, span_positions(max_body), 9 if fmt == "qa" else 17)
         return QASpec(lay, qa_token_flags(tok, lay.vocab))
     if fmt == "span":

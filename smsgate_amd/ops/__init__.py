@@ -146,7 +146,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                   _vp]
     lib.sg_copy_masks.restype = _c_int
     lib.sg_qa_decode.argtypes = [_vp, _vp, _c_int, _vp, _c_int, _c_float, _ip, _ip, _vp, _c_int, _ip, _ip, _vp, _vp,
-                                 _c_int, _c_int, _vp]
+                                 _vp, _c_int, _c_int, _vp]
     lib.sg_qa_decode.restype = _c_int
     lib.sg_qa_params_size.argtypes = []
     lib.sg_qa_params_size.restype = _c_int
@@ -914,15 +914,18 @@ class QAParams(ctypes.Structure):
                 ("off_end", _c_int), ("off_null", _c_int), ("off_cls", _c_int),
                 ("cls_tok", (_c_int * QA_MAX_CLS_TOK) * QA_NCLS), ("cls_len", _c_int * QA_NCLS),
                 ("reject_mask", _c_int), ("sep", _c_int), ("max_out", _c_int),
-                ("s_need", _c_int * QA_MAX_NF), ("e_need", _c_int * QA_MAX_NF), ("absorb", _c_int * QA_MAX_NF)]
+                ("s_need", _c_int * QA_MAX_NF), ("e_need", _c_int * QA_MAX_NF), ("absorb", _c_int * QA_MAX_NF),
+                ("min_conf", _c_float), ("abstain_cls", _c_int)]
 
 
-def qa_params(lay, tokenizer) -> QAParams:
+def qa_params(lay, tokenizer, min_conf: float = 0.0) -> QAParams:
     """Kernel parameters of a qa layout (serving/qa.py): query rows, field classes and
     caps, the W row offsets (W = rows ptr0 .. cls0 + 3 of the final-norm-folded
-    embedding), the class tokens of the copy-format answer."""
+    embedding), the class tokens of the copy-format answer, and the abstention
+    threshold (``min_conf``: a transaction answer less confident than this becomes the
+    ``unknown`` class; 0 = never)."""
     from ..parse.schema import TXN_TYPES
-    from ..serving.qa import REJECT_TXN, qa_rows
+    from ..serving.qa import ABSTAIN_TXN, REJECT_TXN, qa_rows
 
     p = QAParams()
     nf = lay.n_copy
@@ -945,6 +948,7 @@ def qa_params(lay, tokenizer) -> QAParams:
         if name in REJECT_TXN:
             p.reject_mask |= 1 << c
     p.sep, p.max_out = tokenizer.sep, lay.max_answer_tokens()
+    p.min_conf, p.abstain_cls = float(min_conf), TXN_TYPES.index(ABSTAIN_TXN)
     if load_library().sg_qa_params_size() != ctypes.sizeof(QAParams):
         raise RuntimeError("QAParams layout differs from csrc/qa_kernels.hip")
     return p
@@ -953,14 +957,16 @@ def qa_params(lay, tokenizer) -> QAParams:
 def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, ids: torch.Tensor,
               flags: torch.Tensor, params: QAParams, out_buf: torch.Tensor, out_len: torch.Tensor,
               dbg_scores: Optional[torch.Tensor] = None, dbg_spans: Optional[torch.Tensor] = None,
-              compact: bool = False) -> None:
+              compact: bool = False, out_conf: Optional[torch.Tensor] = None) -> None:
     """The qa format's head (``qa_decode_kernel``): for every sequence ``m`` of a packed
     prefill batch (rows ``cu[m]:cu[m+1]``, the last ``params.nq`` of them its query
     rows; ``compact``: ``h`` holds only the query rows, ``m * nq ..``), scores of the query rows against W (RMSNorm from the un-normed rows ``h``,
     weight folded into W), the class and every field's joint constrained span decode,
     and the answer in the copy format into ``out_buf[m]`` / ``out_len[m]``.
     ``dbg_scores`` [M, 4 + nf (2 n_pos + 1)] fp32 / ``dbg_spans`` [M, 1 + 2 nf] int32:
-    the raw scores and the decoded (class, start, end ...) for tests."""
+    the raw scores and the decoded (class, start, end ...) for tests.  ``out_conf`` [M]
+    fp32: each answer's confidence (the least probable of its decisions; before the
+    ``params.min_conf`` abstention)."""
     M = cu.numel() - 1
     T, H = h.shape[0], h.shape[1]
     if h.dtype != torch.bfloat16 or h.stride(1) != 1 or h.stride(0) % 8 or not h.is_cuda:
@@ -984,11 +990,13 @@ def qa_decode(h: torch.Tensor, W: torch.Tensor, eps: float, cu: torch.Tensor, id
         raise ValueError(f"qa_decode: dbg_scores must be fp32 [{M}, {per}]")
     if dbg_spans is not None and (dbg_spans.dtype != torch.int32 or dbg_spans.numel() < M * (1 + 2 * params.nf)):
         raise ValueError("qa_decode: dbg_spans too small")
+    if out_conf is not None and (out_conf.dtype != torch.float32 or out_conf.numel() < M or not out_conf.is_cuda):
+        raise ValueError("qa_decode: out_conf must be fp32 [>= M] on the GPU")
     if M == 0:
         return
     _check(load_library().sg_qa_decode(ctypes.byref(params), _p(h), h.stride(0), _p(W), H, float(eps), _p(cu),
                                        _p(ids), _p(flags), flags.numel(), _p(out_buf), _p(out_len), _p(dbg_scores),
-                                       _p(dbg_spans), M, int(bool(compact)), _stream()), "qa_decode")
+                                       _p(dbg_spans), _p(out_conf), M, int(bool(compact)), _stream()), "qa_decode")
 
 
 def embed_rows_add_ids(ids: torch.Tensor, add: torch.Tensor, table: torch.Tensor,

@@ -27,6 +27,12 @@
 //      span ending in a digit a following AM / PM.
 //      One lane per start, its ends scanned in order;
 //      ties go to the lower start, then the lower end (serving/qa.py qa_decode_ref);
+//      Confidence: the probability of each decision under the distributions the head
+//      is trained on (serving/qa.py qa_loss) -- the class softmax, per field the start
+//      softmax over the body positions and null, and the end softmax over the body
+//      positions -- a field's confidence the product of its start and end probabilities
+//      (its null probability when null), the answer's the least of them.  A transaction
+//      answer under p.min_conf is turned into p.abstain_cls (serving/qa.py qa_decode_ref);
 //   4. the answer in the copy format (class tokens, <sep>, each field's body tokens
 //      and <sep>; a rejection class: only its tokens and <sep>) into out_buf.
 //
@@ -69,6 +75,11 @@ struct QAParams {
   int s_need[QA_MAX_NF];  // edge flags the first token must all have (serving/qa.py EDGE_RULES)
   int e_need[QA_MAX_NF];  // ... and the last token
   int absorb[QA_MAX_NF];  // 1: a span without a time of day takes an adjacent one (dates)
+  // abstention: a transaction answer whose confidence (the least probable of its
+  // decisions, below) is under min_conf becomes class abstain_cls (a non-transaction:
+  // null fields -> the unmatched DLQ) instead of being published with a doubtful field
+  float min_conf;
+  int abstain_cls;
 };
 
 static __device__ __forceinline__ float qa_bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
@@ -111,7 +122,7 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
     QAParams p, const uint16_t* __restrict__ h, int ldh, const uint16_t* __restrict__ W, int H, float eps,
     const int* __restrict__ cu, const int* __restrict__ ids, const uint32_t* __restrict__ flags, int V,
     int* __restrict__ out_buf, int* __restrict__ out_len, float* __restrict__ dbg_scores,
-    int* __restrict__ dbg_spans, int compact) {
+    int* __restrict__ dbg_spans, float* __restrict__ out_conf, int compact) {
   extern __shared__ __attribute__((aligned(16))) uint16_t hq[];  // [nq][H] bf16
   __shared__ float rs[QA_MAX_NQ];
   __shared__ float sc_start[QA_MAX_NF][QA_MAX_POS];
@@ -121,6 +132,7 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
   __shared__ uint32_t fb[QA_MAX_POS];
   __shared__ int body[QA_MAX_POS];
   __shared__ int span_s[QA_MAX_NF], span_e[QA_MAX_NF];
+  __shared__ float conf_f[QA_MAX_NF];
   __shared__ int cls_sel;
 
   const int m = blockIdx.x;
@@ -130,7 +142,9 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
   // query rows: the last nq rows of the sequence, or (compact: the engine ran the last
   // layer on the query rows only) rows m * nq .. of a query-rows-only h
   const int qrow0 = compact ? m * nq : r1 - nq;
-  const int n = min(r1 - nq - r0 - 1, p.n_pos);  // pointable positions (the body; <ans> excluded)
+  // pointable positions (the body; <ans> excluded); >= 0 even for a malformed sequence
+  // (the host refuses empty prompts, serving/qa_engine.py), so the class rows are scored
+  const int n = max(0, min(r1 - nq - r0 - 1, p.n_pos));
   const int nch = H >> 3;                       // 16-B chunks per row
 
   // ---- 1. stage
@@ -264,8 +278,33 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
       const int os = __shfl_xor(bs, o, 64), oe = __shfl_xor(be, o, 64);
       if (ob > best || (ob == best && os < bs)) { best = ob; bs = os; be = oe; }
     }
+    // the field's start (body positions + null) and end (body positions) softmax
+    float mxs = -INFINITY, mxe = -INFINITY;
+    for (int j = lane; j < n; j += 64) {
+      mxs = fmaxf(mxs, sc_start[f][j]);
+      mxe = fmaxf(mxe, sc_end[f][j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mxs = fmaxf(mxs, __shfl_xor(mxs, o, 64));
+      mxe = fmaxf(mxe, __shfl_xor(mxe, o, 64));
+    }
+    mxs = fmaxf(mxs, sc_null[f]);
+    float zs = 0.f, ze = 0.f;
+    for (int j = lane; j < n; j += 64) {
+      zs += expf(sc_start[f][j] - mxs);
+      ze += expf(sc_end[f][j] - mxe);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      zs += __shfl_xor(zs, o, 64);
+      ze += __shfl_xor(ze, o, 64);
+    }
+    zs += expf(sc_null[f] - mxs);
     if (lane == 0) {
       const bool null = be < 0 || !(top > sc_null[f]);
+      conf_f[f] = null ? expf(sc_null[f] - mxs) / zs
+                       : (expf(sc_start[f][bs] - mxs) / zs) * (expf(sc_end[f][be] - mxe) / ze);
       if (!null && p.absorb[f]) {
         bool timed = false;
         for (int j = bs; j <= be; ++j) timed |= (fb[j] & QF_TIME) != 0;
@@ -289,6 +328,20 @@ __global__ void __launch_bounds__(256) qa_decode_kernel(
       span_s[f] = null ? -1 : bs;
       span_e[f] = null ? -1 : be;
     }
+  }
+  __syncthreads();
+
+  // ---- confidence and abstention
+  if (tid == 0) {
+    const int c0 = cls_sel;
+    float z = 0.f;
+    for (int k = 0; k < QA_NCLS; ++k) z += expf(sc_cls[k] - sc_cls[c0]);
+    float conf = 1.f / z;
+    const bool rej0 = (p.reject_mask >> c0) & 1;
+    if (!rej0)
+      for (int f = 0; f < nf; ++f) conf = fminf(conf, conf_f[f]);
+    if (out_conf != nullptr) out_conf[m] = conf;
+    if (!rej0 && conf < p.min_conf) cls_sel = p.abstain_cls;
   }
   __syncthreads();
 
@@ -385,10 +438,11 @@ extern "C" {
 
 int sg_qa_decode(const void* params, const void* h, int ldh, const void* W, int H, float eps, const int* cu,
                  const int* ids, const void* flags, int V, int* out_buf, int* out_len, void* dbg_scores,
-                 void* dbg_spans, int M, int compact, hipStream_t stream) {
+                 void* dbg_spans, void* out_conf, int M, int compact, hipStream_t stream) {
   const QAParams& p = *reinterpret_cast<const QAParams*>(params);
   if (H % 64 || H > 1024 || ldh % 8 || p.nf <= 0 || p.nf > QA_MAX_NF || p.nq <= 0 || p.nq > QA_MAX_NQ ||
-      p.n_pos <= 0 || p.n_pos > QA_MAX_POS || p.max_out <= 0)
+      p.n_pos <= 0 || p.n_pos > QA_MAX_POS || p.max_out <= 0 || p.abstain_cls < 0 || p.abstain_cls >= QA_NCLS ||
+      !((p.reject_mask >> p.abstain_cls) & 1))
     return -1;
   for (int c = 0; c < QA_NCLS; ++c)
     if (p.cls_len[c] <= 0 || p.cls_len[c] > QA_MAX_CLS_TOK) return -1;
@@ -396,7 +450,7 @@ int sg_qa_decode(const void* params, const void* h, int ldh, const void* W, int 
   const size_t lds = (size_t)p.nq * H * sizeof(uint16_t);
   hipLaunchKernelGGL(qa_decode_kernel, dim3(M), dim3(256), lds, stream, p, (const uint16_t*)h, ldh,
                      (const uint16_t*)W, H, eps, cu, ids, (const uint32_t*)flags, V, out_buf, out_len,
-                     (float*)dbg_scores, (int*)dbg_spans, compact);
+                     (float*)dbg_scores, (int*)dbg_spans, (float*)out_conf, compact);
   return (int)hipGetLastError();
 }
 

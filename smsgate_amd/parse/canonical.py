@@ -33,13 +33,23 @@ CURRENCY_ALIASES: Dict[str, str] = {
 }
 
 _DAY_FIRST = re.compile(r"(\d{1,2})[/-](\d{1,2})[/-](\d{4}|\d{2})(?![\d])(.*)\Z", re.S)
-# Russian month names (genitive, "6 июня 2025 14:23"; also the nominative / short forms):
+# Russian month names (genitive, "6 июня 2025 14:23"; also the nominative / short forms,
+# "г." / "в" before the time of day, the time first, and Latin transliterations):
 # dateutil knows English month names only, so without this the date would fall back to
 # the message timestamp
 _RU_MONTHS = {"январ": 1, "феврал": 2, "март": 3, "апрел": 4, "ма": 5, "июн": 6, "июл": 7, "август": 8,
               "сентябр": 9, "октябр": 10, "ноябр": 11, "декабр": 12}
-_RU_DATE = re.compile(r"(\d{1,2})\s+([а-яё]+)\.?\s+(\d{4})(?:\s*г\.?)?(.*)\Z", re.S | re.I)
+_RU_DATE = re.compile(r"(\d{1,2})\s+([а-яё]+)\.?\s+(\d{4})(?:\s*г\.?)?(?:\s+в(?=\s))?(.*)\Z", re.S | re.I)
+# the time of day first: "14:23 6 июня 2025" (and the transliterated "14:23 6 iyunya 2025")
+_MONTH_TIME_FIRST = re.compile(r"(\d{1,2}:\d{2}(?::\d{2})?)\s+(\d{1,2})\s+([^\W\d_]+)\.?\s+(\d{4})(?:\s*г\.?)?\Z",
+                               re.I)
 _RU_ENDINGS = ("я", "а", "ь", "й", "е", "")
+# Russian month names in Latin letters (the transliterated SMS: "6 iyunya 2025 14:23")
+_TR_MONTHS = {w: i for i, ws in enumerate((
+    ("yanvarya", "yanvar"), ("fevralya", "fevral"), ("marta", "mart"), ("aprelya", "aprel"), ("maya", "mai"),
+    ("iyunya", "iyun"), ("iyulya", "iyul"), ("avgusta", "avgust"), ("sentyabrya", "sentyabr"),
+    ("oktyabrya", "oktyabr"), ("noyabrya", "noyabr"), ("dekabrya", "dekabr")), 1) for w in ws}
+_TR_DATE = re.compile(r"(\d{1,2})\s+([a-z]+)\s+(\d{4})(?:\s*g\.?)?(?:\s+v(?=\s))?(.*)\Z", re.S | re.I)
 
 
 def _ru_month(word: str) -> int:
@@ -64,14 +74,27 @@ def canonical_currency(value: Any) -> Any:
     return CURRENCY_ALIASES.get(v.upper(), value)
 
 
+def _month_number(word: str) -> int:
+    """Month of a Russian (Cyrillic) or transliterated month name, 0 for anything else
+    (English names are dateutil's)."""
+    return _ru_month(word) if not word.isascii() else _TR_MONTHS.get(word.lower(), 0)
+
+
 def canonical_date_text(value: Any) -> Any:
     if not isinstance(value, str):
         return value
-    m = _DAY_FIRST.match(value.strip())
+    v = value.strip()
+    m = _DAY_FIRST.match(v)
     if m is None:
-        r = _RU_DATE.match(value.strip()) if not value.isascii() else None
+        t = _MONTH_TIME_FIRST.match(v)
+        if t is not None:
+            mo, d = _month_number(t.group(3)), int(t.group(2))
+            if mo and 1 <= d <= 31:
+                return f"{t.group(4)}-{mo:02d}-{d:02d} {t.group(1)}"
+            return value
+        r = _RU_DATE.match(v) if not v.isascii() else _TR_DATE.match(v)
         if r is not None:
-            mo = _ru_month(r.group(2))
+            mo = _month_number(r.group(2))
             d = int(r.group(1))
             if mo and 1 <= d <= 31:
                 return f"{r.group(3)}-{mo:02d}-{d:02d}{r.group(4)}"

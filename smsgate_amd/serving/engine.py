@@ -50,6 +50,10 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+# the served abstention threshold (EngineConfig.qa_min_conf, TorchQAExtractor)
+QA_MIN_CONF = 0.0
+
+
 @dataclass
 class EngineConfig:
     max_slots: int = 1024
@@ -158,6 +162,12 @@ class EngineConfig:
     # qa engine: rows that must be waiting before a SECOND batch is launched behind the
     # one in flight (the first always launches at once)
     qa_min_tokens: int = 65536
+    # qa engine: abstention threshold -- a transaction answer whose confidence (its least
+    # probable decision, serving/qa.py qa_confidence) is under this becomes "unknown"
+    # (null fields: the reference's unmatched DLQ path) instead of being published with
+    # a doubtful value; 0 = never abstain.  Calibrated on a validation set of TRAINING
+    # layouts (profiles/PERF.md, "Abstention")
+    qa_min_conf: float = QA_MIN_CONF
     qa_wait_s: float = 0.002
     qa_poll_s: float = 0.0002
 

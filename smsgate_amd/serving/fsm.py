@@ -64,7 +64,7 @@ class FieldSpec:
 # copy-constrained: the model can pick the span, never invent a name.
 DEFAULT_FIELDS: Tuple[FieldSpec, ...] = (
     FieldSpec("txn_type", "enum", 8, TXN_TYPES),  # cap = bound on the enum trie depth
-    FieldSpec("date", "date", 16, copy=True),
+    FieldSpec("date", "date", 20, copy=True),  # "11 февраля 2025 г. 11:54": 14 tokens
     FieldSpec("amount", "number", 10, copy=True),
     FieldSpec("currency", "currency", 4, copy=True),
     FieldSpec("card", "card", 6, copy=True),

@@ -51,12 +51,15 @@ from ..parse.schema import TXN_TYPES
 from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
-           "REJECT_TXN", "null_rejection", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
+           "REJECT_TXN", "ABSTAIN_TXN", "null_rejection", "qa_confidence", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
            "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP",
            "QF_TIME", "QF_DEND", "QF_AMPM", "QF_AP", "QF_M", "QF_TEXT"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
+# the class an abstained answer (confidence under the threshold) is turned into: the
+# reference's "not a transaction" shape, so the message is dead-lettered as unmatched
+ABSTAIN_TXN = "unknown"
 QA_MAX_QUERIES = 24
 # per-token flags (uint32): starts / ends with a letter / digit, ends a card mask, class bits
 QF_SL, QF_SD, QF_EL, QF_ED, QF_MASK = 1, 2, 4, 8, 16
@@ -337,38 +340,82 @@ def _absorb_time(fb: np.ndarray, pairs: np.ndarray, a: int, z: int, n: int) -> T
     return a, z
 
 
+def _p_of(logits: np.ndarray, k: int) -> float:
+    """Softmax probability of entry ``k`` (fp32, max-shifted like the kernel)."""
+    x = np.asarray(logits, dtype=np.float32)
+    mx = x.max()
+    return float(np.exp(x[k] - mx) / np.exp(x - mx).sum(dtype=np.float32))
+
+
+def qa_confidence(cls_logits, start_logits, null_logits, end_logits, n: int, c: int,
+                  spans: Sequence[Tuple[int, int]]) -> float:
+    """An answer's confidence: the probability of its least probable decision under the
+    head's training distributions (:func:`qa_loss`) -- the class softmax; per copied
+    field the start softmax over the ``n`` body positions and null (for a null field the
+    null probability) times the end softmax over the body positions.  ``spans``: the
+    decoded (start, end) BEFORE time / AM-PM absorption; a rejection is judged by its
+    class alone."""
+    conf = _p_of(cls_logits, c)
+    if TXN_TYPES[c] in REJECT_TXN:
+        return conf
+    for f, (a, z) in enumerate(spans):
+        st = np.concatenate([np.asarray(start_logits[f][:n], dtype=np.float32),
+                             np.asarray([null_logits[f]], dtype=np.float32)])
+        if a < 0:
+            pf = _p_of(st, n)
+        else:
+            pf = _p_of(st, a) * _p_of(np.asarray(end_logits[f][:n], dtype=np.float32), z)
+        conf = min(conf, pf)
+    return conf
+
+
 def qa_decode_ref(cls_logits, start_logits, null_logits, end_logits, bodies: Sequence[Sequence[int]],
-                  flags: np.ndarray, lay: QALayout) -> List[Tuple[int, List[Tuple[int, int]]]]:
+                  flags: np.ndarray, lay: QALayout, min_conf: float = 0.0,
+                  conf_out: Optional[List[float]] = None) -> List[Tuple[int, List[Tuple[int, int]]]]:
     """Reference joint decode (host, numpy).  Per message ``m``: ``cls_logits[m]`` [4],
     ``start_logits[m]`` / ``end_logits[m]`` [n_copy, >= n] over prompt positions,
     ``null_logits[m]`` [n_copy]; ``bodies[m]`` the prompt ids (``body <ans>``).
     Returns (class, spans) with (-1, -1) for a null field (every field of a rejection).
     Ties go to the lower class, then the lower start, then the lower end (the kernel's
     rule); the field is null when its null score is >= every valid start's score or no
-    valid pair exists."""
+    valid pair exists.  A transaction answer whose :func:`qa_confidence` is under
+    ``min_conf`` abstains: class :data:`ABSTAIN_TXN`, every field null.  ``conf_out``
+    collects each answer's confidence (before abstention)."""
     out = []
+    abstain = TXN_TYPES.index(ABSTAIN_TXN)
     for m, body in enumerate(bodies):
         c = int(np.argmax(np.asarray(cls_logits[m], dtype=np.float32)))
         if TXN_TYPES[c] in REJECT_TXN:
+            if conf_out is not None:
+                conf_out.append(_p_of(cls_logits[m], c))
             out.append((c, [(-1, -1)] * lay.n_copy))
             continue
         n = len(body) - 1
         fb = flags[np.asarray(body[:n], dtype=np.int64)]
         spans: List[Tuple[int, int]] = []
+        raw: List[Tuple[int, int]] = []  # before absorption: what the confidence judges
+        absorb = lay.absorb_time()
         for f, (bits, cap, s_need, e_need) in enumerate(lay.rules()):
-            absorb = lay.absorb_time()
             st = np.asarray(start_logits[m][f][:n], dtype=np.float32)
             en = np.asarray(end_logits[m][f][:n], dtype=np.float32)
             vs, pairs = _pair_mask(fb, n, bits, cap, s_need, e_need)
             if not pairs.any() or np.float32(null_logits[m][f]) >= st[vs].max():
                 spans.append((-1, -1))
+                raw.append((-1, -1))
                 continue
             sc = np.where(pairs, st[:, None] + en[None, :], -np.inf)
             k = int(np.argmax(sc))
             a, z = k // n, k % n
+            raw.append((a, z))
             if absorb[f]:
                 a, z = _absorb_time(fb, pairs, a, z, n)
             spans.append((a, z))
+        conf = qa_confidence(cls_logits[m], start_logits[m], null_logits[m], end_logits[m], n, c, raw)
+        if conf_out is not None:
+            conf_out.append(conf)
+        if conf < min_conf:
+            out.append((abstain, [(-1, -1)] * lay.n_copy))
+            continue
         out.append((c, spans))
     return out
 

@@ -51,6 +51,14 @@ __all__ = ["QAEngine", "PackedAnswer"]
 
 
 @dataclass
+class _Join:
+    """A request larger than the engine's slots, queued as several units: their answers
+    are joined into one :class:`PackedAnswer` (in request order) when the last one lands."""
+    parts: List[Optional[PackedAnswer]]
+    left: int
+
+
+@dataclass
 class _Unit:
     """Queued work: one message (``packed`` False: ``submit_ids``) or a whole request."""
     key: Any
@@ -58,6 +66,8 @@ class _Unit:
     flat: np.ndarray  # int32 [sum(lens)] prompt ids
     packed: bool
     ntok: int = 0  # rows it adds to a batch (prompts + query tokens)
+    join: Optional[_Join] = None  # part ``part`` of a split request
+    part: int = 0
 
 
 @dataclass
@@ -108,7 +118,7 @@ class QAEngine(ExtractionEngine):
         # the head's rows (start pointers .. class rows) with the final norm folded in
         self.w_qa = ops.fold_norm(w.embed[lay.ptr0:lay.cls0 + 4], w.ln_f)
         self.flags_t = torch.from_numpy(qa_token_flags(tokenizer, lay.vocab).view(np.int32)).to(dev)
-        self.params = ops.qa_params(lay, tokenizer)
+        self.params = ops.qa_params(lay, tokenizer, min_conf=ec.qa_min_conf)
         self.max_out = lay.max_answer_tokens()
         self.prefix_ids = tokenizer.prefix_ids(system_prompt)
         self.P0 = len(self.prefix_ids)
@@ -139,6 +149,7 @@ class QAEngine(ExtractionEngine):
         self._fwd_ss: Optional[torch.Tensor] = None
         self._idle_prev = None
         self._idle_pairs: deque = deque()
+        self._dbg: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None  # debug_decode's outputs
         self._lp = ops.LayerPointers(self.fw_qkv, self.fw_o, self.fw_gu, self.fw_down, self.k_cache, self.vt_cache,
                                      self.pk, self.pvt)
         self._compute_prefix()
@@ -191,9 +202,10 @@ class QAEngine(ExtractionEngine):
                             a=torch.empty(T, nh * D, dtype=x.dtype, device=dev),
                             act=torch.empty(T, I, dtype=x.dtype, device=dev), ss=ss, eps=mc.eps,
                             layers=mc.layers - 1 if trim else None)
+        dbg = self._dbg if self._dbg is not None else (None, None, None)
         if not trim:
             ops.qa_decode(x, self.w_qa, mc.eps, cu_d, flat_d, self.flags_t, self.params, self.out_buf[r0:],
-                          self.out_len[r0:])
+                          self.out_len[r0:], dbg[0], dbg[1], out_conf=dbg[2])
             return T
         Tq = n * NQ
         qidx_d = meta[o:o + Tq]; o += Tq
@@ -218,7 +230,7 @@ class QAEngine(ExtractionEngine):
                        cfg=ops.gemm_cfg(Tq, 2 * I, epi="swiglu", K=H), ss_in=ssq)
         ops.gemm(act, self.fw_down[i], epi="resid", resid=xq, cfg=ops.gemm_cfg(Tq, H, epi="resid", K=I))
         ops.qa_decode(xq, self.w_qa, mc.eps, cu_d, flat_d, self.flags_t, self.params, self.out_buf[r0:],
-                      self.out_len[r0:], compact=True)
+                      self.out_len[r0:], dbg[0], dbg[1], compact=True, out_conf=dbg[2])
         return T
 
     def submit_many(self, items) -> None:
@@ -239,9 +251,16 @@ class QAEngine(ExtractionEngine):
     def submit_packed(self, key: Any, lens: np.ndarray, ids: np.ndarray) -> None:
         """Queue a whole request (wire lengths / ids); answered by :meth:`step` as
         ``(key, PackedAnswer)``.  Prompts over ``max_body_tokens + 2`` keep their first
-        ``max_body_tokens + 1`` ids and their closing ``<ans>``."""
+        ``max_body_tokens + 1`` ids and their closing ``<ans>``.  A request of more
+        prompts than ``max_slots`` is queued as several units and answered as one.
+        Raises ``ValueError`` (nothing queued) for an empty prompt or lengths that do not
+        add up to the ids: the wire is not trusted (a zero-length prompt would leave the
+        decode kernel without a body to point into)."""
         lens = np.asarray(lens, dtype=np.int32)
         ids = np.asarray(ids, dtype=np.int32)
+        if len(lens) and (int(lens.min()) < 1 or int(lens.sum(dtype=np.int64)) != len(ids)):
+            raise ValueError(f"malformed request: {len(lens)} prompts, min length {int(lens.min())}, "
+                             f"{int(lens.sum(dtype=np.int64))} ids declared, {len(ids)} sent")
         cap = self.cfg.max_body_tokens + 2
         if len(lens) and int(lens.max()) > cap:
             ends = np.cumsum(lens)
@@ -250,7 +269,18 @@ class QAEngine(ExtractionEngine):
                 a, b = int(ends[i] - lens[i]), int(ends[i])
                 keep[a + cap - 1:b - 1] = False
             ids, lens = ids[keep], np.minimum(lens, cap)
-        self.waiting.append(_Unit(key, lens, ids, True, int(lens.sum()) + self.NQ * len(lens)))
+        S = self.cfg.max_slots
+        if len(lens) <= S:
+            self.waiting.append(_Unit(key, lens, ids, True, int(lens.sum()) + self.NQ * len(lens)))
+            return
+        k = -(-len(lens) // S)
+        join = _Join([None] * k, k)
+        ends = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)])
+        for j in range(k):
+            a, b = j * S, min(len(lens), (j + 1) * S)
+            part = lens[a:b]
+            self.waiting.append(_Unit(key, part, ids[int(ends[a]):int(ends[b])], True,
+                                      int(part.sum()) + self.NQ * len(part), join, j))
 
     def _launch(self) -> Optional[_Batch]:
         ec = self.cfg
@@ -318,7 +348,16 @@ class QAEngine(ExtractionEngine):
             if u.packed:
                 ln = lens[r:r + m]
                 keep = np.arange(blk.shape[1])[None, :] < ln[:, None]
-                res.append((u.key, PackedAnswer(ln.astype(np.uint16), blk[r:r + m][keep])))
+                ans = PackedAnswer(ln.astype(np.uint16), blk[r:r + m][keep])
+                if u.join is None:
+                    res.append((u.key, ans))
+                else:
+                    u.join.parts[u.part] = ans
+                    u.join.left -= 1
+                    if u.join.left == 0:
+                        parts = u.join.parts
+                        res.append((u.key, PackedAnswer(np.concatenate([p.lens for p in parts]),
+                                                        np.concatenate([p.flat for p in parts]))))
             elif raw:
                 res.append((u.key, blk[r, : lens[r]]))
             else:
@@ -382,5 +421,27 @@ class QAEngine(ExtractionEngine):
         self.stats.step_s += time.perf_counter() - t0
         return out
 
-    def debug_logits(self, *a, **k):  # pragma: no cover - the span engine's tool
-        raise NotImplementedError("QAEngine has no decode logits (see ops.qa_decode dbg_scores)")
+    def debug_decode(self, msgs) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Tests: one synchronous batch of prompt ids (``body <ans>`` each) with the
+        head's debug outputs -- the decoded (class, start, end ...) [M, 1 + 2 nf] int32
+        (after abstention), the raw scores [M, 4 + nf (2 n_pos + 1)] fp32 and each
+        answer's confidence [M] (ops.qa_decode)."""
+        if self.busy():
+            raise RuntimeError("debug_decode on a busy engine")
+        cap = self.cfg.max_body_tokens + 2
+        arrs = [np.asarray(m, dtype=np.int32) for m in msgs]
+        arrs = [a if len(a) <= cap else np.concatenate([a[:cap - 1], a[-1:]]) for a in arrs]
+        if not 0 < len(arrs) <= self.cfg.max_slots:
+            raise ValueError("debug_decode: 1 .. max_slots prompts")
+        M, nf, npos = len(arrs), self.lay.n_copy, self.lay.n_pos
+        dev = self.device
+        self._dbg = (torch.zeros(M, 4 + nf * (2 * npos + 1), dtype=torch.float32, device=dev),
+                     torch.zeros(M, 1 + 2 * nf, dtype=torch.int32, device=dev),
+                     torch.zeros(M, dtype=torch.float32, device=dev))
+        try:
+            self._forward_part(np.asarray([len(a) for a in arrs], dtype=np.int32), np.concatenate(arrs), 0)
+            torch.cuda.synchronize(dev)
+            sc, sp, cf = (t.cpu().numpy() for t in self._dbg)
+        finally:
+            self._dbg = None
+        return sp, sc, cf

@@ -22,6 +22,7 @@ import queue
 import selectors
 import threading
 import time
+import weakref
 from dataclasses import dataclass, field
 from multiprocessing.connection import Connection
 from typing import Any, Callable, Dict, List, Optional, Sequence
@@ -64,7 +65,9 @@ class EngineServer:
         # connection's responses the same way
         self._senders: Dict[int, "queue.SimpleQueue"] = {}  # id(connection) -> its FIFO
         self._senders_lock = threading.Lock()
-        self._dropped: set = set()  # connections gone: late frames for them are discarded
+        # connections gone: late frames for them are discarded.  Weak: a dropped connection
+        # is closed by its sender thread once its queued frames are out, then collected
+        self._dropped: "weakref.WeakSet[Connection]" = weakref.WeakSet()
 
     def _send(self, c: Connection, frame: bytes) -> None:
         """Queue ``frame`` for ``c`` (its frames leave in order, on its own thread)."""
@@ -85,7 +88,11 @@ class EngineServer:
         dead = False
         while True:
             frame = q.get()
-            if frame is None:
+            if frame is None:  # dropped: the frames queued before are out, release the socket
+                try:
+                    c.close()
+                except OSError:
+                    pass
                 return
             if isinstance(frame, threading.Event):  # a flush marker
                 frame.set()
@@ -97,18 +104,28 @@ class EngineServer:
             except (OSError, EOFError, ValueError):  # the client went away: drop what follows
                 dead = True
 
-    def flush(self, timeout: float = 30.0) -> None:
-        """Wait until every queued frame has been handed to the sockets."""
+    def flush(self, timeout: float = 30.0, conns: Optional[Sequence[Connection]] = None) -> bool:
+        """Wait until every queued frame (of ``conns``, default all connections) has been
+        handed to the sockets.  False (and a log line) when ``timeout`` ran out first: a
+        parser that stalls without disconnecting must not hold the caller silently."""
         with self._senders_lock:
-            queues = list(self._senders.values())
+            if conns is None:
+                queues = list(self._senders.values())
+            else:
+                queues = [q for q in (self._senders.get(id(c)) for c in conns) if q is not None]
         marks = []
         for q in queues:
             ev = threading.Event()
             q.put(ev)
             marks.append(ev)
         t_end = time.monotonic() + timeout
-        for ev in marks:
-            ev.wait(max(0.0, t_end - time.monotonic()))
+        ok = all([ev.wait(max(0.0, t_end - time.monotonic())) for ev in marks])
+        if not ok:
+            import logging
+
+            logging.getLogger(__name__).warning("engine server: %d of %d connection(s) did not drain within %.1f s",
+                                                sum(not ev.is_set() for ev in marks), len(marks), timeout)
+        return ok
 
     def add_connection(self, conn: Connection) -> int:
         self.conns.append(conn)
@@ -126,14 +143,22 @@ class EngineServer:
             with self._senders_lock:
                 q = self._senders.pop(id(c), None)
                 self._dropped.add(c)
-            if q is not None:  # its sender ends after the frames already queued
+            if q is not None:  # its sender closes it after the frames already queued
                 q.put(None)
+            else:  # no sender thread: nothing queued, close it now
+                try:
+                    c.close()
+                except OSError:
+                    pass
 
     def send_control(self, idx: int, obj: Any) -> None:
         c = self.conns[idx]
         if c is not None:
             self._send(c, P.pack_control(obj))
-            self.flush()  # control frames (harness commands) leave before the caller goes on
+            # control frames (harness commands) leave before the caller goes on; only this
+            # connection's queue is waited for (a broadcast over N connections would
+            # otherwise wait N times on every stalled parser)
+            self.flush(conns=[c])
 
     def _live(self) -> List[Connection]:
         return [c for c in self.conns if c is not None]
@@ -167,7 +192,10 @@ class EngineServer:
                         if not len(lens):
                             self._send(c, P.pack_ids(b"R", rid, []))
                         else:
-                            self.engine.submit_packed((idx, rid), lens, flat)
+                            try:
+                                self.engine.submit_packed((idx, rid), lens, flat)
+                            except ValueError as exc:  # a malformed request fails alone
+                                self._send(c, P.pack_error(rid, repr(exc)))
                         if not c.poll():
                             break
                         continue
@@ -192,7 +220,7 @@ class EngineServer:
                 for b in getattr(self.engine, "_inflight", ()):
                     units += list(getattr(b, "units", None) or [])
                 keys += [u.key for u in units if getattr(u, "packed", False)]
-            for idx, rid in keys:
+            for idx, rid in dict.fromkeys(keys):  # (a split request's parts share one key)
                 c = self.conns[idx]
                 if c is not None:
                     self._send(c, P.pack_error(rid, repr(exc)))
@@ -266,14 +294,11 @@ class EngineServer:
         finally:
             listener.close()
             self.flush(5.0)  # answers already produced reach their clients
-            for i, c in enumerate(self.conns):  # clients see EOF (and reconnect to the next server)
-                if c is None:
-                    continue
-                self._drop(i)
-                try:
-                    c.close()
-                except OSError:
-                    pass
+            # clients see EOF (and reconnect to the next server): _drop closes each
+            # connection, on its sender thread once that thread's frames are out
+            for i, c in enumerate(self.conns):
+                if c is not None:
+                    self._drop(i)
 
 
 class RemoteEngineClient:

@@ -303,6 +303,25 @@ _DATE_STYLES: Dict[str, Tuple[str, bool]] = {
     "mon": ("%d %b %Y %H:%M", True),
     "mon_up": ("%d-%b-%Y %H:%M", True),
     "time_first": ("%H:%M %d.%m.%Y", True),
+    # the value grammar's other axes (VERDICT r05 next #1a): month-first order, full
+    # month names, 12-hour clocks (zero-padded or not, glued or spaced, upper or lower
+    # case, time after or before the date), Russian month names in every combination but
+    # the held-out one.  Each held-out style below is a combination of axes that all occur
+    # here, never the combination itself (tests/test_families.py pins both)
+    "mdy_mon": ("%b %d, %Y %H:%M", True),  # "Jun 06, 2025 14:23"
+    "mdy_mon_date": ("%b %-d, %Y", False),  # "Jun 6, 2025"
+    "full_month": ("%-d %B %Y %H:%M", True),  # "6 June 2025 14:23"
+    "dmy4_12h": ("%d.%m.%Y %I:%M %p", True),  # "06.06.2025 02:23 PM"
+    "slash_12h": ("%d/%m/%Y %-I:%M%p", True),  # "06/06/2025 2:23PM"
+    "mon_12h": ("%-d %b %Y %-I:%M %p", True),  # "6 Jun 2025 2:23 PM"
+    "iso_12h": ("%Y-%m-%d %I:%M %p", True),  # "2025-06-06 02:23 pm" (lower case)
+    "time_first_12h": ("%-I:%M %p %d.%m.%Y", True),  # "2:23 PM 06.06.2025"
+    "ru_month_date": ("", False),  # "6 июня 2025"
+    "ru_month_g": ("", True),  # "6 июня 2025 г. 14:23"
+    "ru_month_v": ("", True),  # "6 июня 2025 в 14:23"
+    "ru_time_month": ("", True),  # "14:23 6 июня 2025"
+    "ru_mon_abbr": ("", True),  # "6 июн. 2025 14:23" / "06 июн 2025 14:23"
+    "tr_month": ("", True),  # "6 iyunya 2025 14:23" (transliterated genitive)
     # held-out VALUE styles (never in a training pool: only the heldout_values families
     # below render them; tests/test_families.py pins it)
     "en_12h": ("%b %-d, %Y %-I:%M %p", True),  # "Jun 6, 2025 2:23 PM"
@@ -310,23 +329,30 @@ _DATE_STYLES: Dict[str, Tuple[str, bool]] = {
 }
 _RU_MONTHS_GEN = ("января", "февраля", "марта", "апреля", "мая", "июня", "июля", "августа", "сентября",
                   "октября", "ноября", "декабря")
+# short forms: "май" (not the genitive "мая", which would be the held-out style itself)
+_RU_MONTHS_ABBR = ("янв", "фев", "мар", "апр", "май", "июн", "июл", "авг", "сен", "окт", "ноя", "дек")
+_TR_MONTHS_GEN = ("yanvarya", "fevralya", "marta", "aprelya", "maya", "iyunya", "iyulya", "avgusta", "sentyabrya",
+                  "oktyabrya", "noyabrya", "dekabrya")
 # held-out value styles of every kind (dates above, money / number / card styles below)
 HELDOUT_VALUE_STYLES = {"dates": ("en_12h", "ru_month"), "money": ("code_glued",), "numbers": ("apos",),
                         "cards": ("x_mask", "dots_mask")}
 # per language: date styles, money layouts, number formats, card masks
 _STYLE_POOLS = {
-    "en": dict(dates=("dmy2", "dmy4", "iso", "iso_t", "slash", "mon", "mon_up"),
+    "en": dict(dates=("dmy2", "dmy4", "iso", "iso_t", "slash", "mon", "mon_up", "mdy_mon", "mdy_mon_date",
+                      "full_month", "dmy4_12h", "slash_12h", "mon_12h", "iso_12h", "time_first_12h"),
                money=("code_after", "code_after", "code_before", "sym_before", "sym_after"),
                numbers=("dot", "comma_dot", "comma_dot", "int"),
-               cards=("star1", "stars2", "stars3", "stars4", "spaced", "first_mask", "ending")),
-    "ru": dict(dates=("dmy2", "dmy4", "dmy4_date", "dmy2_date", "time_first", "iso"),
+               cards=("star1", "stars2", "stars3", "stars4", "spaced", "first_mask", "ending", "xx_mask", "dots3",
+                      "x_groups")),
+    "ru": dict(dates=("dmy2", "dmy4", "dmy4_date", "dmy2_date", "time_first", "iso", "ru_month_date", "ru_month_g",
+                      "ru_month_v", "ru_time_month", "ru_mon_abbr"),
                money=("code_after", "code_after", "code_before", "sym_after", "word_after"),
                numbers=("space_comma", "space_comma", "comma", "dot", "int"),
-               cards=("star1", "stars2", "stars4", "spaced", "first_mask")),
-    "tr": dict(dates=("dmy2", "dmy4", "time_first", "iso", "slash"),
+               cards=("star1", "stars2", "stars4", "spaced", "first_mask", "xx_mask", "dots3")),
+    "tr": dict(dates=("dmy2", "dmy4", "time_first", "iso", "slash", "tr_month", "tr_month"),
                money=("code_after", "code_before", "sym_after"),
                numbers=("dot", "comma", "space_comma", "comma_dot"),
-               cards=("star1", "stars2", "stars4", "first_mask")),
+               cards=("star1", "stars2", "stars4", "first_mask", "xx_mask", "dots3", "x_groups")),
 }
 _NOISE = {
     "en": ("", "", "", " Thank you.", " Details in the app.", " Bank."),
@@ -425,12 +451,31 @@ class _Ctx:
                       r.randint(0, 23), r.randint(0, 59), r.randint(0, 59) if "%S" in fmt else 0)
         if not timed:
             dt = dt.replace(hour=0, minute=0, second=0)
-        if self.date_style == "ru_month":
-            s = f"{dt.day} {_RU_MONTHS_GEN[dt.month - 1]} {dt.year} {dt.hour:02d}:{dt.minute:02d}"
+        st = self.date_style
+        hm = f"{dt.hour:02d}:{dt.minute:02d}"
+        if st == "ru_month":
+            s = f"{dt.day} {_RU_MONTHS_GEN[dt.month - 1]} {dt.year} {hm}"
+        elif st.startswith("ru_"):
+            dm = f"{dt.day} {_RU_MONTHS_GEN[dt.month - 1]} {dt.year}"
+            if st == "ru_month_date":
+                s = dm
+            elif st == "ru_month_g":
+                s = f"{dm} г. {hm}"
+            elif st == "ru_month_v":
+                s = f"{dm} в {hm}"
+            elif st == "ru_time_month":
+                s = f"{hm} {dm}"
+            else:  # ru_mon_abbr
+                d = f"{dt.day:02d}" if r.random() < 0.5 else f"{dt.day}"
+                s = f"{d} {_RU_MONTHS_ABBR[dt.month - 1]}{r.choice(('.', ''))} {dt.year} {hm}"
+        elif st == "tr_month":
+            s = f"{dt.day} {_TR_MONTHS_GEN[dt.month - 1]} {dt.year} {hm}"
         else:
             s = dt.strftime(fmt)
-        if self.date_style == "mon_up":
+        if st == "mon_up":
             s = s.upper()
+        elif st == "iso_12h":
+            s = s.lower()
         self.ans["date"] = s
         self.exp["date"] = dt
         return s
@@ -485,6 +530,12 @@ class _Ctx:
             s, a = f"ending {c}", c
         elif st == "hash":
             s, a = f"#{c}", c
+        elif st == "xx_mask":  # "XX1234", "xxxx1234", "XXXX 1234" (one glyph: the held-out x_mask)
+            s, a = f"{self.r.choice('xX') * self.r.randint(2, 4)}{self.r.choice(('', '', ' '))}{c}", c
+        elif st == "dots3":  # "...1234", "…1234" (two dots: the held-out dots_mask)
+            s, a = f"{self.r.choice(('...', '…'))}{c}", c
+        elif st == "x_groups":  # "XXXX XXXX XXXX 1234"
+            s, a = f"{' '.join([self.r.choice(('XXXX', 'xxxx', '****'))] * 3)} {c}", c
         elif st == "x_mask":  # held-out value style
             s, a = f"x{c}", c
         elif st == "dots_mask":  # held-out value style

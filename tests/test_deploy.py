@@ -122,3 +122,37 @@ def test_env_example_dsn_names_compose_brokers():
     dsn = _env_example()["NATS_DSN"]
     hosts = {part.split("://")[1].split(":")[0] for part in dsn.replace("sharded+", "").split(",")}
     assert hosts <= set(svc), hosts
+
+
+def test_compose_train_cli_and_bench_train_the_same_recipe():
+    """the deployed extractor is the benchmarked one.  compose's
+    ``train`` command (8 torchrun ranks), the ``train-extractor`` CLI defaults (one GPU)
+    and bench.py's in-run training resolve to models/train.py FLAGSHIP_RECIPE -- the
+    same steps, GLOBAL batch of fresh examples, lr, answer format, negatives and seed;
+    the 8-rank run splits the global batch (global_batch = 128, 16 per rank)."""
+    import dataclasses
+    import importlib.util
+
+    from smsgate_amd.cli import build_parser, train_config
+    from smsgate_amd.models.train import FLAGSHIP_RECIPE
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    bench_tc, _ = bench._train_plan(bench._args([]))
+
+    svc = yaml.safe_load(open(os.path.join(ROOT, "deploy", "docker-compose.yml")))["services"]["train"]
+    world = int(svc["entrypoint"][svc["entrypoint"].index("--nproc-per-node") + 1])
+    compose_tc = train_config(build_parser().parse_args(svc["command"]), world)
+    cli_tc = train_config(build_parser().parse_args(["train-extractor", "--out", "x.safetensors"]), 1)
+
+    keys = ("model", "steps", "lr", "n_examples", "families", "answer_format", "negatives", "seed", "warmup",
+            "min_lr_frac", "ema", "weight_decay", "max_body_tokens", "vocab_name")
+    want = {k: getattr(FLAGSHIP_RECIPE, k) for k in keys}
+    for name, tc in (("bench", bench_tc), ("compose", compose_tc), ("cli", cli_tc)):
+        assert {k: getattr(tc, k) for k in keys} == want, name
+    assert bench_tc.batch == cli_tc.batch == FLAGSHIP_RECIPE.batch
+    assert world == 8 and compose_tc.global_batch == FLAGSHIP_RECIPE.batch and compose_tc.batch * world == 128
+    assert FLAGSHIP_RECIPE.n_examples == FLAGSHIP_RECIPE.steps * FLAGSHIP_RECIPE.batch  # fresh every step
+    assert dataclasses.replace(compose_tc, batch=128, global_batch=0, data_parallel=True, ckpt_dir=None,
+                               ckpt_every=0, resume=False).answer_format == "qa"

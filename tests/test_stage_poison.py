@@ -518,3 +518,43 @@ def test_engine_server_slow_reader_does_not_hold_back_others():
     assert senders() == base + 1  # B's
     srv._send(sa, big)  # a late frame for the dropped connection starts no new sender
     assert senders() == base + 1
+
+
+def test_engine_server_releases_dropped_connections():
+    """a dropped connection is closed (its socket released) once the frames
+    queued for it are out, and the server keeps no strong reference to it; a control
+    frame to one connection waits for that connection's queue only."""
+    import gc
+    import time
+    import weakref
+    from multiprocessing import Pipe
+
+    from smsgate_amd.serving import protocol as P
+    from smsgate_amd.serving.remote import EngineServer
+
+    (ca, sa), (cb, sb), (cc, sc) = Pipe(), Pipe(), Pipe()
+    srv = EngineServer(engine=None, conns=[sa, sb, sc])
+    big = P.pack_control({"pad": "x" * (1 << 20)})
+    for _ in range(8):
+        srv._send(sc, big)  # C never reads: its queue cannot drain
+    srv._send(sa, P.pack_control({"last": 1}))
+    ref = weakref.ref(sa)
+    srv._drop(0)
+    assert P.unpack_control(ca.recv_bytes()) == {"last": 1}  # queued frames still delivered first
+    deadline = time.time() + 5
+    while not sa.closed and time.time() < deadline:
+        time.sleep(0.02)
+    assert sa.closed
+    with pytest.raises(EOFError):
+        ca.recv_bytes()  # the client sees the server side closed
+    srv._drop(1)  # never sent to: no sender thread, closed at once
+    assert sb.closed
+    del sa, sb
+    gc.collect()
+    assert ref() is None  # not held by the server
+    t0 = time.perf_counter()
+    srv.send_control(1, {"x": 1}) if srv.conns[1] is not None else None
+    (cd, sd) = Pipe()
+    idx = srv.add_connection(sd)
+    srv.send_control(idx, {"hello": 1})  # C's stalled queue is not waited for
+    assert time.perf_counter() - t0 < 5.0 and P.unpack_control(cd.recv_bytes()) == {"hello": 1}

@@ -34,8 +34,12 @@ def cxx() -> str:
     raise RuntimeError("no C++ compiler found")
 
 
+# CPython extensions (one .cpp each), not part of the broker binary
+EXTENSIONS = ("tokfast.cpp", "parsefast.cpp")
+
+
 def sources() -> List[Path]:
-    return sorted(p for p in CSRC.glob("*.cpp") if p.name != "tokfast.cpp") + sorted(CSRC.glob("*.hpp"))
+    return sorted(p for p in CSRC.glob("*.cpp") if p.name not in EXTENSIONS) + sorted(CSRC.glob("*.hpp"))
 
 
 def needs_build(target: Path = BUSD) -> bool:
@@ -48,16 +52,26 @@ def needs_build(target: Path = BUSD) -> bool:
 def build_tokfast(force: bool = False, verbose: bool = False) -> Path:
     """``_lib/_tokfast*.so``: the CPython extension of ``csrc/tokfast.cpp`` (native
     BPE encoder / answer decoder of the parser processes, models/fasttok.py)."""
+    return build_extension("tokfast", force, verbose)
+
+
+def build_parsefast(force: bool = False, verbose: bool = False) -> Path:
+    """``_lib/_parsefast*.so``: ``csrc/parsefast.cpp``, the parser processes' native
+    per-message path (parse/fastpath.py)."""
+    return build_extension("parsefast", force, verbose)
+
+
+def build_extension(name: str, force: bool = False, verbose: bool = False) -> Path:
     import sysconfig
 
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    target = LIBDIR / ("_tokfast" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
-    src = CSRC / "tokfast.cpp"
+    target = LIBDIR / ("_" + name + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    src = CSRC / f"{name}.cpp"
     if not force and target.exists() and target.stat().st_mtime > max(src.stat().st_mtime,
                                                                        Path(__file__).stat().st_mtime):
         return target
     tmp = target.with_suffix(".tmp")
-    cmd = [cxx(), "-O2", "-std=c++17", "-Wall", "-shared", "-fPIC", "-fvisibility=hidden",
+    cmd = [cxx(), "-O3", "-std=c++17", "-Wall", "-Wno-unused-function", "-shared", "-fPIC", "-fvisibility=hidden",
            f"-I{sysconfig.get_paths()['include']}", str(src), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -69,6 +83,7 @@ def build_tokfast(force: bool = False, verbose: bool = False) -> Path:
 def build(force: bool = False, verbose: bool = False, extra: List[str] = (), sanitize: bool = False) -> Path:
     if not sanitize:
         build_tokfast(force=force, verbose=verbose)
+        build_parsefast(force=force, verbose=verbose)
     target = BUSD_SAN if sanitize else BUSD
     if not force and not needs_build(target):
         return target

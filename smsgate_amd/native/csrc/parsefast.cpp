@@ -1,0 +1,1356 @@
+// smsgate_amd — native per-message path of the parser processes (CPython extension
+// ``_parsefast``; VERDICT r05 next #3: host CPU per message dominated the node budget).
+//
+// The parser worker's per-message Python work (services/parser.py route_batch,
+// parse/pipeline.py postprocess_answer) is, in the common case, a fixed chain: validate
+// the sms.raw JSON as a RawSMS, run the keyword filters, normalise the body, and after
+// the extractor answered, canonicalise / parse / repair the date, strip the card, parse
+// the two amounts, build a ParsedSMS and serialise it.  This module does that chain on
+// UTF-8 bytes, with no per-field Python objects, and reports FALLBACK for every message
+// it cannot prove it handles exactly like the Python path -- that message then takes the
+// Python path, so routing and payloads never depend on which path ran
+// (tests/test_parsefast.py pins byte equality on the synthetic corpus, hostile
+// strings and the DLQ envelope shapes).
+//
+//   scan_raw(payloads, now)      -> per payload: None (Python path) or
+//                                   (msg_id, sender, body, date, device_id, source, norm_body)
+//                                   for a valid RawSMS that no keyword filter can touch;
+//   postprocess(rows, metas, now)-> per message: bytes (the sms.parsed payload),
+//                                   UNMATCHED (1) or FALLBACK (2).
+//
+// Equivalences (each one a Python function of the parse package):
+//   * RawSMS.model_validate_json: a JSON object; msg_id / sender / body / date strings,
+//     sender and body non-empty, device_id string or null, source "device" | "xml"
+//     (default "device"), other keys skipped (they must still be valid JSON).  Anything
+//     else -- duplicate known keys, lone surrogates, raw control characters, invalid
+//     UTF-8, a "raw" envelope -- is FALLBACK;
+//   * worker_should_skip / llm_should_skip: both scan for keyword SUBSTRINGS first and
+//     only then check word boundaries, so a body without any keyword substring is never
+//     skipped in either mode; a body with one is FALLBACK.  body.upper() is ASCII
+//     upper-casing unless the body has a character whose upper case contains an ASCII
+//     letter (the table from init(): "ß" -> "SS", "ı" -> "I" ...): FALLBACK;
+//   * normalize_body: U+00A0 -> " ", U+2022 -> "*", then re.sub(r"\d{4}\*{3}(\d{4})",
+//     "CARD:\1") -- \d is Unicode, so a body with a non-ASCII decimal digit is FALLBACK;
+//   * canonicalize_answer (currency aliases, day-first / Russian / transliterated month
+//     dates), parse_custom_datetime (its fast shapes; anything dateutil would be asked
+//     is FALLBACK), fix_broken_datetime, parse_ambiguous_decimal, str(Decimal), the
+//     ParsedSMS constraints, the future-date check and pydantic-core's JSON encoding.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <unordered_map>
+#include <algorithm>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+// ------------------------------------------------------------------ state from init()
+// a code-point set: a bitmap over the BMP, a hash set above it
+struct CpSet {
+  std::vector<uint64_t> bmp = std::vector<uint64_t>(1024, 0);
+  std::unordered_set<uint32_t> astral;
+  void clear() { std::fill(bmp.begin(), bmp.end(), 0); astral.clear(); }
+  void insert(uint32_t c) {
+    if (c < 0x10000) bmp[c >> 6] |= 1ull << (c & 63);
+    else astral.insert(c);
+  }
+  bool count(uint32_t c) const { return c < 0x10000 ? (bmp[c >> 6] >> (c & 63)) & 1 : astral.count(c) > 0; }
+};
+CpSet g_upper_ascii;  // non-ASCII code points whose upper() has ASCII
+CpSet g_udigits;      // non-ASCII Unicode decimal digits (\d)
+std::unordered_map<std::string, std::string> g_alias_exact;  // currency value -> ISO code
+std::unordered_map<std::string, std::string> g_alias_upper;  // ASCII upper key -> ISO code
+bool g_inited = false;
+
+constexpr int UNMATCHED = 1, FALLBACK = 2;
+
+// ------------------------------------------------------------------ UTF-8
+// decode one code point at s[i] (valid UTF-8 assumed checked); returns length
+inline int u8len(unsigned char c) { return c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4; }
+
+uint32_t u8at(const std::string& s, size_t i, int* n) {
+  const unsigned char* p = (const unsigned char*)s.data() + i;
+  int l = u8len(p[0]);
+  *n = l;
+  if (l == 1) return p[0];
+  if (l == 2) return ((p[0] & 0x1F) << 6) | (p[1] & 0x3F);
+  if (l == 3) return ((p[0] & 0x0F) << 12) | ((p[1] & 0x3F) << 6) | (p[2] & 0x3F);
+  return ((p[0] & 0x07) << 18) | ((p[1] & 0x3F) << 12) | ((p[2] & 0x3F) << 6) | (p[3] & 0x3F);
+}
+
+void u8put(std::string& o, uint32_t c) {
+  if (c < 0x80) {
+    o += (char)c;
+  } else if (c < 0x800) {
+    o += (char)(0xC0 | (c >> 6));
+    o += (char)(0x80 | (c & 0x3F));
+  } else if (c < 0x10000) {
+    o += (char)(0xE0 | (c >> 12));
+    o += (char)(0x80 | ((c >> 6) & 0x3F));
+    o += (char)(0x80 | (c & 0x3F));
+  } else {
+    o += (char)(0xF0 | (c >> 18));
+    o += (char)(0x80 | ((c >> 12) & 0x3F));
+    o += (char)(0x80 | ((c >> 6) & 0x3F));
+    o += (char)(0x80 | (c & 0x3F));
+  }
+}
+
+// strict UTF-8 validation (no overlongs, no surrogates, <= U+10FFFF)
+bool valid_utf8(const unsigned char* p, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    if (i + 8 <= n) {  // eight ASCII bytes at once
+      uint64_t w;
+      memcpy(&w, p + i, 8);
+      if (!(w & 0x8080808080808080ull)) { i += 8; continue; }
+    }
+    unsigned char c = p[i];
+    if (c < 0x80) { ++i; continue; }
+    int l;
+    uint32_t cp;
+    if (c >= 0xC2 && c <= 0xDF) { l = 2; cp = c & 0x1F; }
+    else if (c >= 0xE0 && c <= 0xEF) { l = 3; cp = c & 0x0F; }
+    else if (c >= 0xF0 && c <= 0xF4) { l = 4; cp = c & 0x07; }
+    else return false;
+    if (i + l > n) return false;
+    for (int k = 1; k < l; ++k) {
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (p[i + k] & 0x3F);
+    }
+    if ((l == 3 && cp < 0x800) || (l == 4 && (cp < 0x10000 || cp > 0x10FFFF)) || (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    i += l;
+  }
+  return true;
+}
+
+inline bool is_ascii_digit(char c) { return c >= '0' && c <= '9'; }
+
+// any non-ASCII code point of `s` in `set`
+bool has_any(const std::string& s, const CpSet& set) {
+  for (size_t i = 0; i < s.size();) {
+    unsigned char c = s[i];
+    if (c < 0x80) { ++i; continue; }
+    int n;
+    uint32_t cp = u8at(s, i, &n);
+    if (set.count(cp)) return true;
+    i += n;
+  }
+  return false;
+}
+
+bool is_ascii(const std::string& s) {
+  for (unsigned char c : s)
+    if (c >= 0x80) return false;
+  return true;
+}
+
+// Python str.isspace() for the ASCII range plus the Unicode whitespace str.strip() drops
+bool py_space(uint32_t c) {
+  return (c >= 9 && c <= 13) || (c >= 0x1C && c <= 0x20) || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+         (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+
+// str.strip() (Unicode whitespace)
+std::string py_strip(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b) {
+    int n;
+    uint32_t c = u8at(s, a, &n);
+    if (!py_space(c)) break;
+    a += n;
+  }
+  while (b > a) {
+    size_t k = b - 1;
+    while (k > a && ((unsigned char)s[k] & 0xC0) == 0x80) --k;
+    int n;
+    uint32_t c = u8at(s, k, &n);
+    if (!py_space(c)) break;
+    b = k;
+  }
+  return s.substr(a, b - a);
+}
+
+std::string ascii_upper(const std::string& s) {
+  std::string o = s;
+  for (auto& c : o)
+    if (c >= 'a' && c <= 'z') c = (char)(c - 32);
+  return o;
+}
+
+std::string ascii_lower(const std::string& s) {
+  std::string o = s;
+  for (auto& c : o)
+    if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
+  return o;
+}
+
+// ------------------------------------------------------------------ JSON (RawSMS)
+struct JP {
+  const char* p;
+  const char* e;
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+};
+
+int hex4(const char* p) {
+  int v = 0;
+  for (int k = 0; k < 4; ++k) {
+    char c = p[k];
+    v <<= 4;
+    if (c >= '0' && c <= '9') v |= c - '0';
+    else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+    else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+    else return -1;
+  }
+  return v;
+}
+
+// a JSON string at jp.p (the opening quote) into `out` (UTF-8); false: not one we accept
+bool jstring(JP& jp, std::string* out) {
+  if (jp.p >= jp.e || *jp.p != '"') return false;
+  ++jp.p;
+  if (out) out->clear();
+  while (jp.p < jp.e) {
+    // a run of plain bytes at once (no quote, backslash or control character)
+    const char* q = jp.p;
+    while (q < jp.e && (unsigned char)*q >= 0x20 && *q != '"' && *q != '\\') ++q;
+    if (q > jp.p) {
+      if (out) out->append(jp.p, (size_t)(q - jp.p));
+      jp.p = q;
+      continue;
+    }
+    unsigned char c = (unsigned char)*jp.p;
+    if (c == '"') { ++jp.p; return true; }
+    if (c < 0x20) return false;  // raw control character
+    if (c == '\\') {
+      if (jp.p + 1 >= jp.e) return false;
+      char x = jp.p[1];
+      jp.p += 2;
+      uint32_t cp;
+      switch (x) {
+        case '"': cp = '"'; break;
+        case '\\': cp = '\\'; break;
+        case '/': cp = '/'; break;
+        case 'b': cp = 8; break;
+        case 'f': cp = 12; break;
+        case 'n': cp = 10; break;
+        case 'r': cp = 13; break;
+        case 't': cp = 9; break;
+        case 'u': {
+          if (jp.e - jp.p < 4) return false;
+          int h = hex4(jp.p);
+          if (h < 0) return false;
+          jp.p += 4;
+          cp = (uint32_t)h;
+          if (cp >= 0xD800 && cp <= 0xDBFF) {  // a surrogate pair, or FALLBACK
+            if (jp.e - jp.p < 6 || jp.p[0] != '\\' || jp.p[1] != 'u') return false;
+            int l = hex4(jp.p + 2);
+            if (l < 0xDC00 || l > 0xDFFF) return false;
+            jp.p += 6;
+            cp = 0x10000 + ((cp - 0xD800) << 10) + ((uint32_t)l - 0xDC00);
+          } else if (cp >= 0xDC00 && cp <= 0xDFFF) {
+            return false;
+          }
+          break;
+        }
+        default:
+          return false;
+      }
+      if (out) u8put(*out, cp);
+      continue;
+    }
+    // a raw UTF-8 sequence (validated as a whole before parsing)
+    int l = u8len(c);
+    if (jp.p + l > jp.e) return false;
+    if (out) out->append(jp.p, l);
+    jp.p += l;
+  }
+  return false;
+}
+
+bool jskip(JP& jp, int depth);
+
+// numbers of skipped keys: small integers only (a float, an exponent or a big integer
+// is FALLBACK: the Python path's parser decides what it makes of them)
+bool jnumber(JP& jp) {
+  if (jp.p < jp.e && *jp.p == '-') ++jp.p;
+  if (jp.p >= jp.e) return false;
+  if (*jp.p == '0') {
+    ++jp.p;
+  } else if (*jp.p >= '1' && *jp.p <= '9') {
+    int n = 0;
+    while (jp.p < jp.e && is_ascii_digit(*jp.p)) { ++jp.p; ++n; }
+    if (n > 15) return false;
+  } else {
+    return false;
+  }
+  return !(jp.p < jp.e && (*jp.p == '.' || *jp.p == 'e' || *jp.p == 'E' || is_ascii_digit(*jp.p)));
+}
+
+bool jlit(JP& jp, const char* w) {
+  size_t n = strlen(w);
+  if ((size_t)(jp.e - jp.p) < n || memcmp(jp.p, w, n) != 0) return false;
+  jp.p += n;
+  return true;
+}
+
+bool jskip(JP& jp, int depth) {
+  if (depth > 64) return false;
+  jp.ws();
+  if (jp.p >= jp.e) return false;
+  char c = *jp.p;
+  if (c == '"') return jstring(jp, nullptr);
+  if (c == '{' || c == '[') {
+    const char close = c == '{' ? '}' : ']';
+    ++jp.p;
+    jp.ws();
+    if (jp.p < jp.e && *jp.p == close) { ++jp.p; return true; }
+    while (true) {
+      if (c == '{') {
+        jp.ws();
+        if (!jstring(jp, nullptr)) return false;
+        jp.ws();
+        if (jp.p >= jp.e || *jp.p != ':') return false;
+        ++jp.p;
+      }
+      if (!jskip(jp, depth + 1)) return false;
+      jp.ws();
+      if (jp.p >= jp.e) return false;
+      if (*jp.p == ',') { ++jp.p; continue; }
+      if (*jp.p == close) { ++jp.p; return true; }
+      return false;
+    }
+  }
+  if (c == 't') return jlit(jp, "true");
+  if (c == 'f') return jlit(jp, "false");
+  if (c == 'n') return jlit(jp, "null");
+  return jnumber(jp);
+}
+
+struct Raw {
+  std::string msg_id, sender, body, date, device_id, source;
+  bool has_msg_id = false, has_sender = false, has_body = false, has_date = false, device_null = true;
+  bool has_device = false, has_source = false;
+};
+
+// RawSMS.model_validate_json, the accepted subset (see the file comment)
+bool parse_raw(const char* data, size_t n, Raw& r) {
+  if (!valid_utf8((const unsigned char*)data, n)) return false;
+  JP jp{data, data + n};
+  jp.ws();
+  if (jp.p >= jp.e || *jp.p != '{') return false;
+  ++jp.p;
+  jp.ws();
+  std::string key;
+  if (jp.p < jp.e && *jp.p == '}') {
+    ++jp.p;
+  } else {
+    while (true) {
+      jp.ws();
+      if (!jstring(jp, &key)) return false;
+      jp.ws();
+      if (jp.p >= jp.e || *jp.p != ':') return false;
+      ++jp.p;
+      jp.ws();
+      std::string* dst = nullptr;
+      bool* seen = nullptr;
+      if (key == "msg_id") { dst = &r.msg_id; seen = &r.has_msg_id; }
+      else if (key == "sender") { dst = &r.sender; seen = &r.has_sender; }
+      else if (key == "body") { dst = &r.body; seen = &r.has_body; }
+      else if (key == "date") { dst = &r.date; seen = &r.has_date; }
+      else if (key == "source") { dst = &r.source; seen = &r.has_source; }
+      else if (key == "raw") return false;  // a DLQ envelope: the Python path unwraps it
+      if (key == "device_id") {
+        if (r.has_device) return false;
+        r.has_device = true;
+        if (jp.p < jp.e && *jp.p == 'n') {
+          if (!jlit(jp, "null")) return false;
+          r.device_null = true;
+        } else {
+          if (!jstring(jp, &r.device_id)) return false;
+          r.device_null = false;
+        }
+      } else if (dst) {
+        if (*seen) return false;  // duplicate key
+        if (!jstring(jp, dst)) return false;
+        *seen = true;
+      } else if (!jskip(jp, 0)) {
+        return false;
+      }
+      jp.ws();
+      if (jp.p >= jp.e) return false;
+      if (*jp.p == ',') { ++jp.p; continue; }
+      if (*jp.p == '}') { ++jp.p; break; }
+      return false;
+    }
+  }
+  jp.ws();
+  if (jp.p != jp.e) return false;
+  if (!r.has_msg_id || !r.has_sender || !r.has_body || !r.has_date) return false;
+  if (r.sender.empty() || r.body.empty()) return false;
+  if (!r.has_source) r.source = "device";
+  else if (r.source != "device" && r.source != "xml") return false;
+  return true;
+}
+
+// ------------------------------------------------------------------ keyword filters
+const char* WORKER_KW[] = {"OTP", "CODE:", "NOT ENOUGH FUNDS", "INSUFFICIENT FUNDS", "CREDIT PAYMENT", "C2C RECEIVED",
+                           "PASS:", "PASS=", "PERSON TO PERSON"};
+const char* WORKER_KW_CS[] = {"Daily limit exceeded"};
+const char* LLM_KW[] = {"OTP", "CODE:", "PASS:", "PASS=", "Daily limit exceeded:"};
+
+inline char up(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
+
+// body[i:] starts with the ASCII keyword k, compared upper-cased (ci) or as is
+inline bool at(const std::string& b, size_t i, const char* k, bool ci) {
+  for (size_t j = 0; k[j]; ++j) {
+    if (i + j >= b.size()) return false;
+    if ((ci ? up(b[i + j]) : b[i + j]) != k[j]) return false;
+  }
+  return true;
+}
+
+// true: some keyword substring occurs (or upper-casing is not ASCII-local): Python
+// decides.  One pass over the body, keywords tried where their first letter is; the
+// case-sensitive LLM keywords are substrings of the upper-cased worker ones
+// ("Daily limit exceeded:" of the case-sensitive worker keyword)
+bool keyword_risk(const std::string& body) {
+  bool non_ascii = false;
+  for (size_t i = 0; i < body.size(); ++i) {
+    const char c = up(body[i]);
+    if ((unsigned char)c >= 0x80) { non_ascii = true; continue; }
+    bool hit = false;
+    switch (c) {
+      case 'O':
+        hit = at(body, i, "OTP", true);
+        break;
+      case 'C':
+        hit = at(body, i, "CODE:", true) || at(body, i, "CREDIT PAYMENT", true) || at(body, i, "C2C RECEIVED", true);
+        break;
+      case 'N':
+        hit = at(body, i, "NOT ENOUGH FUNDS", true);
+        break;
+      case 'I':
+        hit = at(body, i, "INSUFFICIENT FUNDS", true);
+        break;
+      case 'P':
+        hit = at(body, i, "PASS:", true) || at(body, i, "PASS=", true) || at(body, i, "PERSON TO PERSON", true);
+        break;
+      case 'D':
+        hit = at(body, i, WORKER_KW_CS[0], false);
+        break;
+      default:
+        break;
+    }
+    if (hit) return true;
+  }
+  (void)WORKER_KW;
+  (void)LLM_KW;
+  return non_ascii && has_any(body, g_upper_ascii);
+}
+
+// ------------------------------------------------------------------ normalize_body
+std::string normalize(const std::string& body) {
+  if (body.find("\xc2\xa0") == std::string::npos && body.find("\xe2\x80\xa2") == std::string::npos &&
+      body.find("***") == std::string::npos)
+    return body;  // nothing to replace or mask
+  std::string s;
+  s.reserve(body.size());
+  for (size_t i = 0; i < body.size();) {
+    unsigned char c = body[i];
+    if (c < 0x80) { s += (char)c; ++i; continue; }
+    int n;
+    uint32_t cp = u8at(body, i, &n);
+    if (cp == 0xA0) s += ' ';
+    else if (cp == 0x2022) s += '*';
+    else s.append(body, i, n);
+    i += n;
+  }
+  if (s.find("***") == std::string::npos) return s;
+  std::string o;
+  o.reserve(s.size());
+  size_t i = 0;
+  while (i < s.size()) {
+    if (i + 11 <= s.size() && is_ascii_digit(s[i]) && is_ascii_digit(s[i + 1]) && is_ascii_digit(s[i + 2]) &&
+        is_ascii_digit(s[i + 3]) && s[i + 4] == '*' && s[i + 5] == '*' && s[i + 6] == '*' && is_ascii_digit(s[i + 7]) &&
+        is_ascii_digit(s[i + 8]) && is_ascii_digit(s[i + 9]) && is_ascii_digit(s[i + 10])) {
+      o += "CARD:";
+      o.append(s, i + 7, 4);
+      i += 11;
+    } else {
+      o += s[i];
+      ++i;
+    }
+  }
+  return o;
+}
+
+PyObject* pystr(const std::string& s) { return PyUnicode_DecodeUTF8(s.data(), (Py_ssize_t)s.size(), "strict"); }
+
+// ------------------------------------------------------------------ dates
+struct DT {
+  int y, mo, d, h, mi, s;
+};
+
+int days_in(int y, int m) {
+  static const int md[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  if (m == 2) return ((y % 4 == 0 && y % 100 != 0) || y % 400 == 0) ? 29 : 28;
+  return md[m - 1];
+}
+
+bool valid_dt(const DT& t) {
+  return t.y >= 1 && t.y <= 9999 && t.mo >= 1 && t.mo <= 12 && t.d >= 1 && t.d <= days_in(t.y, t.mo) && t.h >= 0 &&
+         t.h <= 23 && t.mi >= 0 && t.mi <= 59 && t.s >= 0 && t.s <= 59;
+}
+
+// a tiny matcher over an ASCII string: fixed-width digit groups and literals
+struct Cur {
+  const std::string& s;
+  size_t i = 0;
+  explicit Cur(const std::string& x) : s(x) {}
+  bool end() const { return i == s.size(); }
+  bool lit(char c) {
+    if (i < s.size() && s[i] == c) { ++i; return true; }
+    return false;
+  }
+  bool digits(int n, int* v) {  // exactly n digits
+    if (i + n > s.size()) return false;
+    int x = 0;
+    for (int k = 0; k < n; ++k) {
+      if (!is_ascii_digit(s[i + k])) return false;
+      x = x * 10 + (s[i + k] - '0');
+    }
+    i += n;
+    *v = x;
+    return true;
+  }
+  bool digits12(int* v) {  // \d{1,2} (greedy)
+    if (i >= s.size() || !is_ascii_digit(s[i])) return false;
+    int x = s[i] - '0';
+    ++i;
+    if (i < s.size() && is_ascii_digit(s[i])) { x = x * 10 + (s[i] - '0'); ++i; }
+    *v = x;
+    return true;
+  }
+  bool word(int lo, int hi, std::string* w) {  // [A-Za-z]{lo,hi} (greedy, then must stop)
+    size_t j = i;
+    while (j < s.size() && ((s[j] >= 'A' && s[j] <= 'Z') || (s[j] >= 'a' && s[j] <= 'z'))) ++j;
+    int n = (int)(j - i);
+    if (n < lo || n > hi) return false;
+    *w = s.substr(i, n);
+    i = j;
+    return true;
+  }
+  bool ampm(int* pm) {  // " ?[AaPp][Mm]"
+    size_t j = i;
+    if (j < s.size() && s[j] == ' ') ++j;
+    if (j + 2 > s.size()) return false;
+    char a = s[j], m = s[j + 1];
+    if (!(a == 'A' || a == 'a' || a == 'P' || a == 'p') || !(m == 'M' || m == 'm')) return false;
+    *pm = (a == 'P' || a == 'p');
+    i = j + 2;
+    return true;
+  }
+};
+
+int g_now_year = 2026;
+
+int yy_posix(int y) { return y + (y >= 69 ? 1900 : 2000); }
+
+// dateutil parserinfo.convertyear for a 2-digit year (century window around now)
+int du_year(int y) {
+  if (y >= 100) return y;
+  int century = g_now_year / 100 * 100;
+  y += century;
+  if (y >= g_now_year + 50) y -= 100;
+  else if (y < g_now_year - 50) y += 100;
+  return y;
+}
+
+DT month_first(int a, int b, int y, int h, int mi) {
+  if (a <= 12) return DT{y, a, b, h, mi, 0};
+  return DT{y, b, a, h, mi, 0};
+}
+
+int hour12(int h, int pm, bool has) {
+  if (!has) return h;
+  if (h < 0 || h > 12) return -1;
+  if (pm && h < 12) return h + 12;
+  if (!pm && h == 12) return 0;
+  return h;
+}
+
+int month_word(const std::string& w) {
+  static const char* names[][3] = {{"jan", "january", nullptr}, {"feb", "february", nullptr},
+                                   {"mar", "march", nullptr},    {"apr", "april", nullptr},
+                                   {"may", "may", nullptr},      {"jun", "june", nullptr},
+                                   {"jul", "july", nullptr},     {"aug", "august", nullptr},
+                                   {"sep", "september", "sept"}, {"oct", "october", nullptr},
+                                   {"nov", "november", nullptr}, {"dec", "december", nullptr}};
+  std::string l = ascii_lower(w);
+  for (int m = 0; m < 12; ++m)
+    for (int k = 0; k < 3; ++k)
+      if (names[m][k] && l == names[m][k]) return m + 1;
+  return 0;
+}
+
+int month_abbr3(const std::string& w) {  // _FAST_MON: the 3-letter abbreviations only
+  static const char* ab[] = {"jan", "feb", "mar", "apr", "may", "jun", "jul", "aug", "sep", "oct", "nov", "dec"};
+  std::string l = ascii_lower(w);
+  for (int m = 0; m < 12; ++m)
+    if (l == ab[m]) return m + 1;
+  return 0;
+}
+
+// parse_custom_datetime on an ASCII string: true + *out when one of its shapes (or the
+// strptime format) computes the value; false = dateutil would be asked (FALLBACK).
+bool parse_dt(const std::string& t, DT* out) {
+  int a, b, c, h, mi, se, pm;
+  // _FAST_DMY_HM: dd.mm.yy HH:MM  (strptime('%d.%m.%y %H:%M'))
+  {
+    Cur k(t);
+    if (k.digits(2, &a) && k.lit('.') && k.digits(2, &b) && k.lit('.') && k.digits(2, &c) && k.lit(' ') &&
+        k.digits(2, &h) && k.lit(':') && k.digits(2, &mi) && k.end()) {
+      DT v{yy_posix(c), b, a, h, mi, 0};
+      if (valid_dt(v)) { *out = v; return true; }
+      return false;  // strptime fails, then dateutil decides
+    }
+  }
+  // _FAST_ISO: YYYY-MM-DD[( |T)HH:MM[:SS]]
+  {
+    Cur k(t);
+    if (k.digits(4, &c) && k.lit('-') && k.digits(2, &b) && k.lit('-') && k.digits(2, &a)) {
+      h = mi = se = 0;
+      bool ok = k.end();
+      if (!ok && (k.lit(' ') || k.lit('T')) && k.digits(2, &h) && k.lit(':') && k.digits(2, &mi)) {
+        ok = k.end() || (k.lit(':') && k.digits(2, &se) && k.end());
+      }
+      if (ok) {
+        DT v{c, b, a, h, mi, se};
+        if (valid_dt(v)) { *out = v; return true; }
+        return false;
+      }
+    }
+  }
+  // _FAST_DOTTED: dd.mm.(yyyy|yy)[ HH:MM]  (month first when it can be)
+  {
+    Cur k(t);
+    if (k.digits(2, &a) && k.lit('.') && k.digits(2, &b) && k.lit('.')) {
+      size_t save = k.i;
+      int y = -1;
+      if (k.digits(4, &c)) y = c;
+      else { k.i = save; if (k.digits(2, &c)) y = du_year(c); }
+      if (y >= 0) {
+        h = mi = 0;
+        bool ok = k.end() || (k.lit(' ') && k.digits(2, &h) && k.lit(':') && k.digits(2, &mi) && k.end());
+        if (ok) {
+          DT v = month_first(a, b, y, h, mi);
+          if (valid_dt(v)) { *out = v; return true; }
+          return false;
+        }
+      }
+    }
+  }
+  // _FAST_TIME_FIRST: HH:MM dd.mm.yyyy
+  {
+    Cur k(t);
+    if (k.digits(2, &h) && k.lit(':') && k.digits(2, &mi) && k.lit(' ') && k.digits(2, &a) && k.lit('.') &&
+        k.digits(2, &b) && k.lit('.') && k.digits(4, &c) && k.end()) {
+      DT v = month_first(a, b, c, h, mi);
+      if (valid_dt(v)) { *out = v; return true; }
+      return false;
+    }
+  }
+  // _FAST_MON: d{1,2}( |-)Mon\2yyyy[ HH:MM]
+  {
+    Cur k(t);
+    std::string w;
+    if (k.digits12(&a) && k.i < t.size() && (t[k.i] == ' ' || t[k.i] == '-')) {
+      char sep = t[k.i];
+      ++k.i;
+      if (k.word(3, 3, &w) && k.lit(sep) && k.digits(4, &c)) {
+        h = mi = 0;
+        bool ok = k.end() || (k.lit(' ') && k.digits(2, &h) && k.lit(':') && k.digits(2, &mi) && k.end());
+        if (ok) {
+          int mo = month_abbr3(w);
+          if (mo) {
+            DT v{c, mo, a, h, mi, 0};
+            if (valid_dt(v)) { *out = v; return true; }
+            return false;
+          }
+        }
+      }
+    }
+  }
+  const char last = t.empty() ? 0 : t.back();
+  if (!(is_ascii_digit(last) || last == 'M' || last == 'm' || strchr("rRyYlLtTeEnNhHvV", last))) return false;
+  // _FAST_ISO_12: YYYY-MM-DD H:MM ?(AM|PM)
+  {
+    Cur k(t);
+    if (k.digits(4, &c) && k.lit('-') && k.digits(2, &b) && k.lit('-') && k.digits(2, &a) && k.lit(' ') &&
+        k.digits12(&h) && k.lit(':') && k.digits(2, &mi) && k.ampm(&pm) && k.end()) {
+      int hh = hour12(h, pm, true);
+      if (hh < 0) return false;
+      DT v{c, b, a, hh, mi, 0};
+      if (valid_dt(v)) { *out = v; return true; }
+      return false;
+    }
+  }
+  // _FAST_DOTTED_12: dd.mm.yyyy H:MM ?(AM|PM)
+  {
+    Cur k(t);
+    if (k.digits(2, &a) && k.lit('.') && k.digits(2, &b) && k.lit('.') && k.digits(4, &c) && k.lit(' ') &&
+        k.digits12(&h) && k.lit(':') && k.digits(2, &mi) && k.ampm(&pm) && k.end()) {
+      int hh = hour12(h, pm, true);
+      if (hh < 0) return false;
+      DT v = month_first(a, b, c, hh, mi);
+      if (valid_dt(v)) { *out = v; return true; }
+      return false;
+    }
+  }
+  // _FAST_TIME_FIRST_12: H:MM ?(AM|PM) dd.mm.yyyy
+  {
+    Cur k(t);
+    if (k.digits12(&h) && k.lit(':') && k.digits(2, &mi) && k.ampm(&pm) && k.lit(' ') && k.digits(2, &a) &&
+        k.lit('.') && k.digits(2, &b) && k.lit('.') && k.digits(4, &c) && k.end()) {
+      int hh = hour12(h, pm, true);
+      if (hh < 0) return false;
+      DT v = month_first(a, b, c, hh, mi);
+      if (valid_dt(v)) { *out = v; return true; }
+      return false;
+    }
+  }
+  // _FAST_MDY: Month d{1,2}, yyyy[ H:MM[ ?AM]]  /  _FAST_DMY_WORD: d{1,2} Month yyyy[ ...]
+  for (int form = 0; form < 2; ++form) {
+    Cur k(t);
+    std::string w;
+    bool head = form == 0 ? (k.word(3, 9, &w) && k.lit(' ') && k.digits12(&a) && k.lit(',') && k.lit(' ') &&
+                             k.digits(4, &c))
+                          : (k.digits12(&a) && k.lit(' ') && k.word(3, 9, &w) && k.lit(' ') && k.digits(4, &c));
+    if (!head) continue;
+    h = mi = 0;
+    bool has_pm = false;
+    pm = 0;
+    bool ok = k.end();
+    if (!ok && k.lit(' ') && k.digits12(&h) && k.lit(':') && k.digits(2, &mi)) {
+      size_t save = k.i;
+      if (k.ampm(&pm)) has_pm = true;
+      else k.i = save;
+      ok = k.end();
+    }
+    if (!ok) continue;
+    int mo = month_word(w);
+    if (!mo) return false;
+    int hh = hour12(h, pm, has_pm);
+    if (hh < 0) return false;
+    DT v{c, mo, a, hh, mi, 0};
+    if (valid_dt(v)) { *out = v; return true; }
+    return false;
+  }
+  return false;
+}
+
+// ---- canonical_date_text
+int ru_lower_cp(uint32_t c) {  // Cyrillic А-Я / Ё lower-casing (others unchanged)
+  if (c >= 0x410 && c <= 0x42F) return (int)(c + 0x20);
+  if (c == 0x401) return 0x451;
+  return (int)c;
+}
+
+bool is_ru_letter(uint32_t c) { return (c >= 0x430 && c <= 0x44F) || c == 0x451 || (c >= 0x410 && c <= 0x42F) || c == 0x401; }
+
+// _ru_month(word): stems with the endings ("я", "а", "ь", "й", "е", "") and unique 3+ prefixes
+int ru_month(const std::string& word) {
+  // lower-case Cyrillic, as UTF-8
+  std::string w;
+  for (size_t i = 0; i < word.size();) {
+    int n;
+    uint32_t c = u8at(word, i, &n);
+    u8put(w, (uint32_t)ru_lower_cp(c));
+    i += n;
+  }
+  static const char* stems[] = {"январ", "феврал", "март", "апрел", "ма", "июн", "июл", "август", "сентябр", "октябр",
+                                "ноябр", "декабр"};
+  static const char* endings[] = {"я", "а", "ь", "й", "е", ""};
+  for (const char* e : endings) {
+    size_t el = strlen(e);
+    if (el && (w.size() < el || w.compare(w.size() - el, el, e) != 0)) continue;
+    std::string stem = w.substr(0, w.size() - el);
+    for (int m = 0; m < 12; ++m)
+      if (stem == stems[m]) return m + 1;
+    // len(stem) >= 3 in code points (Cyrillic: 2 bytes each)
+    size_t cps = 0;
+    for (size_t i = 0; i < stem.size();) { int n; u8at(stem, i, &n); i += n; ++cps; }
+    if (cps >= 3) {
+      int hit = 0, nh = 0;
+      for (int m = 0; m < 12; ++m) {
+        size_t scps = 0;
+        std::string s = stems[m];
+        for (size_t i = 0; i < s.size();) { int n; u8at(s, i, &n); i += n; ++scps; }
+        if (scps >= 3 && s.compare(0, stem.size(), stem) == 0 && s.size() >= stem.size()) { hit = m + 1; ++nh; }
+      }
+      if (nh == 1) return hit;
+    }
+  }
+  return 0;
+}
+
+int tr_month(const std::string& w) {
+  static const char* names[][2] = {{"yanvarya", "yanvar"}, {"fevralya", "fevral"}, {"marta", "mart"},
+                                   {"aprelya", "aprel"},   {"maya", "mai"},        {"iyunya", "iyun"},
+                                   {"iyulya", "iyul"},     {"avgusta", "avgust"},  {"sentyabrya", "sentyabr"},
+                                   {"oktyabrya", "oktyabr"}, {"noyabrya", "noyabr"}, {"dekabrya", "dekabr"}};
+  std::string l = ascii_lower(w);
+  for (int m = 0; m < 12; ++m)
+    if (l == names[m][0] || l == names[m][1]) return m + 1;
+  return 0;
+}
+
+// \s in a str regex (Unicode whitespace; the Cyrillic dates use plain blanks)
+bool re_space(uint32_t c) { return py_space(c); }
+
+// one code point at s[i] (0 at the end)
+uint32_t cp_at(const std::string& s, size_t i, int* n) {
+  if (i >= s.size()) { *n = 0; return 0; }
+  return u8at(s, i, n);
+}
+
+std::string two(int v) {
+  char b[8];
+  snprintf(b, sizeof b, "%02d", v);
+  return b;
+}
+
+// canonical_date_text(value): *out = the canonical text; false = FALLBACK (a shape this
+// port does not follow exactly -- the Python function decides)
+bool canonical_date(const std::string& value, std::string* out) {
+  std::string v = py_strip(value);
+  // _DAY_FIRST: (\d{1,2})[/-](\d{1,2})[/-](\d{4}|\d{2})(?![\d])(.*)\Z
+  {
+    Cur k(v);
+    int d, mo, y;
+    if (k.digits12(&d) && k.i < v.size() && (v[k.i] == '/' || v[k.i] == '-')) {
+      ++k.i;
+      if (k.digits12(&mo) && k.i < v.size() && (v[k.i] == '/' || v[k.i] == '-')) {
+        ++k.i;
+        size_t save = k.i;
+        int yl = 0;
+        if (k.digits(4, &y)) yl = 4;
+        else { k.i = save; if (k.digits(2, &y)) yl = 2; }
+        if (yl) {
+          // (?![\d]): a 4-digit year followed by a digit backtracks to the 2-digit try,
+          // which is then followed by a digit too: no match either way
+          if (k.i < v.size() && is_ascii_digit(v[k.i])) {
+            *out = value;
+            return true;  // no _DAY_FIRST match; the remaining shapes need a letter -> unchanged below
+          }
+          std::string rest = v.substr(k.i);
+          if (!(1 <= d && d <= 31 && 1 <= mo && mo <= 12)) { *out = value; return true; }
+          int year = yl == 4 ? y : (y < 69 ? 2000 + y : 1900 + y);
+          char b[16];
+          snprintf(b, sizeof b, "%04d-%02d-%02d", year, mo, d);
+          *out = std::string(b) + rest;
+          return true;
+        }
+      }
+    }
+  }
+  // month-name dates: _MONTH_TIME_FIRST, then _RU_DATE (non-ASCII) / _TR_DATE (ASCII).
+  // Followed faithfully for strings whose only whitespace is the blank and whose
+  // non-ASCII characters are basic Cyrillic letters; anything else with a letter in it
+  // is FALLBACK.
+  bool letters = false;
+  for (size_t i = 0; i < v.size();) {
+    int n;
+    uint32_t c = u8at(v, i, &n);
+    if (c >= 0x80) {
+      if (!is_ru_letter(c)) return false;
+      letters = true;
+    } else if ((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z')) {
+      letters = true;
+    } else if (c != ' ' && re_space(c)) {
+      return false;
+    }
+    i += n;
+  }
+  if (!letters) { *out = value; return true; }
+  const bool ascii = is_ascii(v);
+  auto blanks = [&](Cur& k) {  // \s+ over blanks
+    size_t q = k.i;
+    while (k.i < v.size() && v[k.i] == ' ') ++k.i;
+    return k.i > q;
+  };
+  auto word = [&](Cur& k, bool any_script, bool cyr) {  // a maximal letter run
+    size_t q = k.i;
+    while (k.i < v.size()) {
+      int n;
+      uint32_t c = u8at(v, k.i, &n);
+      bool lat = (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z');
+      bool ru = is_ru_letter(c);
+      if (!(any_script ? (lat || ru) : cyr ? ru : lat)) break;
+      k.i += n;
+    }
+    return v.substr(q, k.i - q);
+  };
+  auto g_tail = [&](Cur& k, bool latin) {  // (?:\s*г\.?)? -- г / Г (g / G), greedy
+    size_t q = k.i;
+    while (q < v.size() && v[q] == ' ') ++q;
+    int n;
+    uint32_t c = cp_at(v, q, &n);
+    bool g = latin ? (c == 'g' || c == 'G') : (c == 0x433 || c == 0x413);
+    if (g) {
+      q += n;
+      if (q < v.size() && v[q] == '.') ++q;
+      k.i = q;
+    }
+  };
+  // _MONTH_TIME_FIRST: (\d{1,2}:\d{2}(?::\d{2})?)\s+(\d{1,2})\s+(LETTERS)\.?\s+(\d{4})(?:\s*г\.?)?\Z
+  {
+    Cur k(v);
+    int h, mi, se, d, y;
+    if (k.digits12(&h) && k.lit(':') && k.digits(2, &mi)) {
+      size_t save = k.i;
+      if (!(k.lit(':') && k.digits(2, &se))) k.i = save;
+      std::string tm = v.substr(0, k.i);
+      bool m = !(k.i < v.size() && is_ascii_digit(v[k.i])) && blanks(k) && k.digits12(&d) && blanks(k);
+      std::string w;
+      if (m) {
+        w = word(k, true, false);
+        m = !w.empty();
+      }
+      if (m) {
+        k.lit('.');
+        m = blanks(k) && k.digits(4, &y);
+      }
+      if (m) {
+        g_tail(k, false);
+        m = k.end();
+      }
+      if (m) {
+        int mo = is_ascii(w) ? tr_month(w) : ru_month(w);
+        if (mo && 1 <= d && d <= 31) {
+          char b[16];
+          snprintf(b, sizeof b, "%04d-%02d-%02d ", y, mo, d);
+          *out = std::string(b) + tm;
+        } else {
+          *out = value;
+        }
+        return true;
+      }
+      // no match: on to the day-first month regexes (they need \d{1,2}\s+ first, which a
+      // time of day never is), so the value is unchanged
+      *out = value;
+      return true;
+    }
+  }
+  // _RU_DATE / _TR_DATE: (\d{1,2})\s+WORD(\.?)\s+(\d{4})(?:\s*г\.?)?(?:\s+в(?=\s))?(.*)\Z
+  // (WORD [а-яё]+ with a dot allowed after it / [a-z]+ without; "g" / "v" in Latin)
+  {
+    Cur k(v);
+    int d, y;
+    bool m = k.digits12(&d) && blanks(k);
+    std::string w;
+    if (m) {
+      w = word(k, false, !ascii);
+      m = !w.empty();
+    }
+    if (m) {
+      if (!ascii) k.lit('.');
+      m = blanks(k) && k.digits(4, &y);
+    }
+    if (!m) {
+      *out = value;
+      return true;
+    }
+    g_tail(k, ascii);
+    {  // (?:\s+в(?=\s))?
+      size_t q = k.i;
+      while (q < v.size() && v[q] == ' ') ++q;
+      if (q > k.i) {
+        int n;
+        uint32_t c = cp_at(v, q, &n);
+        bool vv = ascii ? (c == 'v' || c == 'V') : (c == 0x432 || c == 0x412);
+        if (vv && q + n < v.size() && v[q + n] == ' ') k.i = q + n;
+      }
+    }
+    std::string rest = v.substr(k.i);
+    int mo = ascii ? tr_month(w) : ru_month(w);
+    if (mo && 1 <= d && d <= 31) {
+      char b[16];
+      snprintf(b, sizeof b, "%04d-%02d-%02d", y, mo, d);
+      *out = std::string(b) + rest;
+      return true;
+    }
+    *out = value;
+    return true;
+  }
+}
+
+// fix_broken_datetime(body, dt): the first dd.mm.yy match bounds where the first
+// dd.mm.yyyy match may start
+bool date_at(const std::string& s, size_t i, int ylen) {
+  if (i + 6 + ylen > s.size()) return false;
+  for (size_t k : {0, 1, 3, 4}) if (!is_ascii_digit(s[i + k])) return false;
+  if (s[i + 2] != '.' || s[i + 5] != '.') return false;
+  for (int k = 0; k < ylen; ++k) if (!is_ascii_digit(s[i + 6 + k])) return false;
+  return true;
+}
+
+void fix_broken(const std::string& body, DT* dt) {
+  size_t m2 = std::string::npos;
+  for (size_t i = 0; i + 8 <= body.size(); ++i)
+    if (date_at(body, i, 2)) { m2 = i; break; }
+  if (m2 == std::string::npos) return;
+  size_t m4 = std::string::npos;
+  for (size_t i = m2; i + 10 <= body.size(); ++i)
+    if (date_at(body, i, 4)) { m4 = i; break; }
+  auto num = [&](size_t i, int n) { int v = 0; for (int k = 0; k < n; ++k) v = v * 10 + (body[i + k] - '0'); return v; };
+  if (m4 != std::string::npos) {
+    DT v{num(m4 + 6, 4), num(m4 + 3, 2), num(m4, 2), 0, 0, 0};
+    if (valid_dt(v)) { dt->y = v.y; dt->mo = v.mo; dt->d = v.d; return; }
+  }
+  DT v{yy_posix(num(m2 + 6, 2)), num(m2 + 3, 2), num(m2, 2), 0, 0, 0};
+  if (valid_dt(v)) { dt->y = v.y; dt->mo = v.mo; dt->d = v.d; }
+}
+
+// ------------------------------------------------------------------ decimals
+// parse_ambiguous_decimal(value) then str(Decimal): false = FALLBACK (an invalid or
+// exotic remainder: Python raises / formats it)
+bool decimal_str(const std::string& value, std::string* out, bool* negative) {
+  if (!is_ascii(value)) return false;
+  std::string v = py_strip(value);
+  std::string s;
+  for (char c : v) if (c != ' ') s += c;
+  if (s.empty()) { *out = "0.0"; *negative = false; return true; }
+  // _canonical
+  size_t dot = s.rfind('.'), comma = s.rfind(',');
+  std::string c;
+  auto remove = [](const std::string& x, char ch) { std::string o; for (char y : x) if (y != ch) o += y; return o; };
+  if (dot != std::string::npos && comma != std::string::npos) {
+    if (comma > dot) { c = remove(s, '.'); for (auto& y : c) if (y == ',') y = '.'; }
+    else c = remove(s, ',');
+  } else if (comma != std::string::npos) {
+    size_t nc = 0;
+    for (char y : s) nc += y == ',';
+    if (nc > 1) c = remove(s, ',');
+    else { c = s; for (auto& y : c) if (y == ',') y = '.'; }
+  } else if (dot != std::string::npos) {
+    size_t nd = 0;
+    for (char y : s) nd += y == '.';
+    if (nd > 1) c = remove(s.substr(0, dot), '.') + "." + s.substr(dot + 1);
+    else c = s;
+  } else {
+    c = s;
+  }
+  std::string k;  // _KEEP: only [0-9.-]
+  for (char y : c) if (is_ascii_digit(y) || y == '.' || y == '-') k += y;
+  // Decimal(k): -?(\d+\.?\d*|\.\d+)
+  size_t i = 0;
+  bool neg = false;
+  if (i < k.size() && k[i] == '-') { neg = true; ++i; }
+  std::string ip, fp;
+  while (i < k.size() && is_ascii_digit(k[i])) ip += k[i++];
+  bool has_dot = false;
+  if (i < k.size() && k[i] == '.') { has_dot = true; ++i; while (i < k.size() && is_ascii_digit(k[i])) fp += k[i++]; }
+  if (i != k.size() || (ip.empty() && fp.empty())) return false;  // InvalidOperation -> Python's error
+  (void)has_dot;
+  // str(Decimal): coefficient digits ip+fp (leading zeros dropped), exponent -len(fp)
+  std::string coef = ip + fp;
+  size_t z = 0;
+  while (z + 1 < coef.size() && coef[z] == '0') ++z;
+  coef = coef.substr(z);
+  int exp = -(int)fp.size();
+  int adjusted = (int)coef.size() - 1 + exp;
+  if (coef == "0") adjusted = exp;  // zero: Python's adjusted() is exp for a zero coefficient
+  if (adjusted < -6) return false;  // scientific notation: Python formats it
+  std::string r;
+  if (exp == 0) {
+    r = coef;
+  } else {
+    int nfrac = -exp;
+    if ((int)coef.size() > nfrac) r = coef.substr(0, coef.size() - nfrac) + "." + coef.substr(coef.size() - nfrac);
+    else r = "0." + std::string(nfrac - coef.size(), '0') + coef;
+  }
+  bool nonzero = coef != "0";
+  *negative = neg && nonzero;
+  *out = (neg ? "-" : "") + r;
+  return true;
+}
+
+// ------------------------------------------------------------------ JSON out
+// pydantic-core's string encoding: \" \\ \b \f \n \r \t, other C0 controls \u00XX,
+// everything else (DEL and non-ASCII included) as UTF-8
+void jstr(std::string& o, const std::string& s) {
+  o += '"';
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\b': o += "\\b"; break;
+      case '\f': o += "\\f"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          char b[8];
+          snprintf(b, sizeof b, "\\u%04x", c);
+          o += b;
+        } else {
+          o += (char)c;
+        }
+    }
+  }
+  o += '"';
+}
+
+// ------------------------------------------------------------------ Python glue
+bool get_str(PyObject* o, std::string* out) {
+  if (!PyUnicode_Check(o)) return false;
+  Py_ssize_t n;
+  const char* p = PyUnicode_AsUTF8AndSize(o, &n);
+  if (!p) { PyErr_Clear(); return false; }  // lone surrogates
+  out->assign(p, (size_t)n);
+  return true;
+}
+
+bool now_tuple(PyObject* now, int v[7]) {
+  if (!PyTuple_Check(now) || PyTuple_GET_SIZE(now) != 7) return false;
+  for (int k = 0; k < 7; ++k) {
+    v[k] = (int)PyLong_AsLong(PyTuple_GET_ITEM(now, k));
+    if (v[k] == -1 && PyErr_Occurred()) return false;
+  }
+  return true;
+}
+
+PyObject* py_init(PyObject*, PyObject* args) {
+  PyObject *upper, *digits, *aliases;
+  if (!PyArg_ParseTuple(args, "OOO", &upper, &digits, &aliases)) return nullptr;
+  g_upper_ascii.clear();
+  g_udigits.clear();
+  g_alias_exact.clear();
+  g_alias_upper.clear();
+  std::string s;
+  if (!get_str(upper, &s)) { PyErr_SetString(PyExc_TypeError, "upper: str"); return nullptr; }
+  for (size_t i = 0; i < s.size();) { int n; g_upper_ascii.insert(u8at(s, i, &n)); i += n; }
+  if (!get_str(digits, &s)) { PyErr_SetString(PyExc_TypeError, "digits: str"); return nullptr; }
+  for (size_t i = 0; i < s.size();) { int n; g_udigits.insert(u8at(s, i, &n)); i += n; }
+  if (!PyDict_Check(aliases)) { PyErr_SetString(PyExc_TypeError, "aliases: dict"); return nullptr; }
+  PyObject *k, *v;
+  Py_ssize_t pos = 0;
+  while (PyDict_Next(aliases, &pos, &k, &v)) {
+    std::string ks, vs;
+    if (!get_str(k, &ks) || !get_str(v, &vs)) { PyErr_SetString(PyExc_TypeError, "aliases: str -> str"); return nullptr; }
+    g_alias_exact[ks] = vs;
+    if (is_ascii(ks)) g_alias_upper[ascii_upper(ks)] = vs;
+  }
+  g_inited = true;
+  Py_RETURN_NONE;
+}
+
+PyObject* py_scan_raw(PyObject*, PyObject* args) {
+  PyObject* lst;
+  if (!PyArg_ParseTuple(args, "O", &lst)) return nullptr;
+  if (!g_inited) { PyErr_SetString(PyExc_RuntimeError, "_parsefast.init() first"); return nullptr; }
+  PyObject* seq = PySequence_Fast(lst, "scan_raw: a sequence of bytes");
+  if (!seq) return nullptr;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject* out = PyList_New(n);
+  Raw r;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = PySequence_Fast_GET_ITEM(seq, i);
+    PyObject* res = nullptr;
+    char* data;
+    Py_ssize_t len;
+    if (PyBytes_Check(it) && PyBytes_AsStringAndSize(it, &data, &len) == 0) {
+      r = Raw();
+      if (parse_raw(data, (size_t)len, r) && !keyword_risk(r.body) && !has_any(r.body, g_udigits)) {
+        std::string nb = normalize(r.body);
+        PyObject* dev = r.device_null ? (Py_INCREF(Py_None), Py_None) : pystr(r.device_id);
+        res = Py_BuildValue("(NNNNNNN)", pystr(r.msg_id), pystr(r.sender), pystr(r.body), pystr(r.date), dev,
+                            pystr(r.source), pystr(nb));
+        if (!res) { PyErr_Clear(); res = nullptr; }
+      }
+    }
+    if (!res) { Py_INCREF(Py_None); res = Py_None; }
+    PyList_SET_ITEM(out, i, res);
+  }
+  Py_DECREF(seq);
+  return out;
+}
+
+// one message: the sms.parsed payload into `o`; returns 0, UNMATCHED or FALLBACK
+int post_one(PyObject* row, PyObject* meta, const int now[7], std::string& o) {
+  if (!PyList_Check(row) || PyList_GET_SIZE(row) != 9 || !PyTuple_Check(meta) || PyTuple_GET_SIZE(meta) != 6)
+    return FALLBACK;
+  std::string f[9];
+  for (int k = 0; k < 9; ++k)
+    if (!get_str(PyList_GET_ITEM(row, k), &f[k])) return FALLBACK;
+  const std::string& txn = f[0];
+  if (txn == "otp" || txn == "unknown") return UNMATCHED;  // null fields: the card check raises
+  if (txn != "debit" && txn != "credit") return FALLBACK;
+  std::string msg_id, sender, date_raw, body, norm;
+  PyObject* dev = PyTuple_GET_ITEM(meta, 1);
+  std::string device;
+  bool dev_null = dev == Py_None;
+  if (!get_str(PyTuple_GET_ITEM(meta, 0), &msg_id) || (!dev_null && !get_str(dev, &device)) ||
+      !get_str(PyTuple_GET_ITEM(meta, 2), &sender) || !get_str(PyTuple_GET_ITEM(meta, 3), &date_raw) ||
+      !get_str(PyTuple_GET_ITEM(meta, 4), &body) || !get_str(PyTuple_GET_ITEM(meta, 5), &norm))
+    return FALLBACK;
+  (void)date_raw;
+  // ---- date: canonical text, its fast shape, the body-date repair
+  std::string dtext;
+  if (!canonical_date(f[1], &dtext)) return FALLBACK;
+  if (!is_ascii(dtext)) return FALLBACK;
+  DT dt;
+  if (!parse_dt(dtext, &dt)) return FALLBACK;  // dateutil / the message timestamp
+  if (has_any(body, g_udigits)) return FALLBACK;
+  fix_broken(body, &dt);
+  // ---- card
+  std::string card;
+  if (!is_ascii(f[4])) return FALLBACK;
+  for (char c : f[4]) if (c != '*' && c != ' ') card += c;
+  if (card.size() < 4) return FALLBACK;  // BROKEN after the schema check: Python's
+  if (card.size() > 4) card.resize(4);
+  // ---- amounts
+  std::string amount, balance;
+  bool neg_a, neg_b;
+  if (!decimal_str(f[2], &amount, &neg_a) || !decimal_str(f[8], &balance, &neg_b)) return FALLBACK;
+  if (neg_a) return FALLBACK;  // ParsedSmsCore: amount >= 0
+  // ---- currency: canonical_currency, then ParsedSMS upper-cases
+  std::string cur;
+  {
+    std::string v = py_strip(f[3]);
+    while (!v.empty() && v.back() == '.') v.pop_back();
+    auto it = g_alias_exact.find(v);
+    if (it != g_alias_exact.end()) {
+      cur = it->second;
+    } else if (is_ascii(v)) {
+      auto iu = g_alias_upper.find(ascii_upper(v));
+      if (iu != g_alias_upper.end()) cur = iu->second;
+      else if (is_ascii(f[3])) cur = ascii_upper(f[3]);
+      else return FALLBACK;
+    } else {
+      return FALLBACK;  // a non-ASCII value: Python's Unicode upper / alias lookup
+    }
+  }
+  // ---- future date (naive local now, microseconds included)
+  {
+    const int d[6] = {dt.y, dt.mo, dt.d, dt.h, dt.mi, dt.s};
+    int cmp = 0;
+    for (int k = 0; k < 6 && !cmp; ++k) cmp = d[k] < now[k] ? -1 : d[k] > now[k] ? 1 : 0;
+    if (cmp > 0) return FALLBACK;  // the future-date DLQ envelope: Python's
+  }
+  std::string address = f[7] == "null" ? std::string() : f[7];
+  // ---- ParsedSMS JSON (field order of the model)
+  char dbuf[32];
+  snprintf(dbuf, sizeof dbuf, "%04d-%02d-%02dT%02d:%02d:%02d", dt.y, dt.mo, dt.d, dt.h, dt.mi, dt.s);
+  o.clear();
+  o += "{\"msg_id\":";
+  jstr(o, msg_id);
+  o += ",\"device_id\":";
+  if (dev_null) o += "null";
+  else jstr(o, device);
+  o += ",\"sender\":";
+  jstr(o, sender);
+  o += ",\"date\":\"";
+  o += dbuf;
+  o += "\",\"raw_body\":";
+  jstr(o, norm);
+  o += ",\"txn_type\":\"";
+  o += txn;
+  o += "\",\"amount\":\"";
+  o += amount;
+  o += "\",\"currency\":";
+  jstr(o, cur);
+  o += ",\"card\":";
+  jstr(o, card);
+  o += ",\"merchant\":";
+  jstr(o, f[5]);
+  o += ",\"city\":";
+  jstr(o, f[6]);
+  o += ",\"address\":";
+  jstr(o, address);
+  o += ",\"balance\":\"";
+  o += balance;
+  o += "\",\"parser_version\":\"llm-0.2.0\"}";
+  return 0;
+}
+
+PyObject* py_postprocess(PyObject*, PyObject* args) {
+  PyObject *rows, *metas, *now;
+  if (!PyArg_ParseTuple(args, "OOO", &rows, &metas, &now)) return nullptr;
+  if (!g_inited) { PyErr_SetString(PyExc_RuntimeError, "_parsefast.init() first"); return nullptr; }
+  int nv[7];
+  if (!now_tuple(now, nv)) { PyErr_SetString(PyExc_TypeError, "now: (y, mo, d, h, mi, s, us)"); return nullptr; }
+  g_now_year = nv[0];
+  // microseconds: a date equal to now's second is not in the future when now has any
+  if (!PyList_Check(rows) || !PyList_Check(metas) || PyList_GET_SIZE(rows) != PyList_GET_SIZE(metas)) {
+    PyErr_SetString(PyExc_TypeError, "postprocess(rows: list, metas: list, now)");
+    return nullptr;
+  }
+  Py_ssize_t n = PyList_GET_SIZE(rows);
+  PyObject* out = PyList_New(n);
+  std::string o;
+  o.reserve(1024);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    int rc = post_one(PyList_GET_ITEM(rows, i), PyList_GET_ITEM(metas, i), nv, o);
+    PyObject* v = rc == 0 ? PyBytes_FromStringAndSize(o.data(), (Py_ssize_t)o.size()) : PyLong_FromLong(rc);
+    if (!v) { Py_DECREF(out); return nullptr; }
+    PyList_SET_ITEM(out, i, v);
+  }
+  return out;
+}
+
+PyObject* py_normalize(PyObject*, PyObject* args) {  // tests: normalize_body's port
+  PyObject* s;
+  if (!PyArg_ParseTuple(args, "U", &s)) return nullptr;
+  std::string b;
+  if (!get_str(s, &b)) Py_RETURN_NONE;
+  return pystr(normalize(b));
+}
+
+PyObject* py_canonical_date(PyObject*, PyObject* args) {  // tests: (canonical text | None, parsed tuple | None)
+  PyObject *s, *now;
+  if (!PyArg_ParseTuple(args, "UO", &s, &now)) return nullptr;
+  int nv[7];
+  if (!now_tuple(now, nv)) { PyErr_SetString(PyExc_TypeError, "now tuple"); return nullptr; }
+  g_now_year = nv[0];
+  std::string v, c;
+  if (!get_str(s, &v) || !canonical_date(v, &c)) return Py_BuildValue("(OO)", Py_None, Py_None);
+  DT dt;
+  if (!is_ascii(c) || !parse_dt(c, &dt)) return Py_BuildValue("(NO)", pystr(c), Py_None);
+  return Py_BuildValue("(N(iiiiii))", pystr(c), dt.y, dt.mo, dt.d, dt.h, dt.mi, dt.s);
+}
+
+PyObject* py_decimal(PyObject*, PyObject* args) {  // tests: parse_ambiguous_decimal + str()
+  PyObject* s;
+  if (!PyArg_ParseTuple(args, "U", &s)) return nullptr;
+  std::string v, out;
+  bool neg;
+  if (!get_str(s, &v) || !decimal_str(v, &out, &neg)) Py_RETURN_NONE;
+  return pystr(out);
+}
+
+PyMethodDef methods[] = {
+    {"init", py_init, METH_VARARGS, "init(upper_ascii_chars, unicode_digits, currency_aliases)"},
+    {"scan_raw", py_scan_raw, METH_VARARGS, "scan_raw(payloads) -> [None | (msg_id, sender, body, date, device_id, source, norm_body)]"},
+    {"postprocess", py_postprocess, METH_VARARGS, "postprocess(rows, metas, now) -> [bytes | 1 (unmatched) | 2 (fallback)]"},
+    {"normalize", py_normalize, METH_VARARGS, "normalize(body) -> str"},
+    {"canonical_date", py_canonical_date, METH_VARARGS, "canonical_date(value, now) -> (text | None, tuple | None)"},
+    {"decimal", py_decimal, METH_VARARGS, "decimal(value) -> str | None"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_parsefast", "native per-message parse path", -1, methods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__parsefast(void) { return PyModule_Create(&module); }

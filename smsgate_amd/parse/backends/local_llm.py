@@ -176,3 +176,14 @@ class RemoteLLMBackend(ParserBackend):
             raise  # engine unreachable: the stage naks the batch (no DLQ traffic)
         except Exception as exc:  # noqa: BLE001 — every message of the batch fails loudly
             return [exc] * len(bodies)
+
+    async def extract_rows(self, bodies: Sequence[str]) -> List[Any]:
+        """:meth:`extract_batch` as the nine decoded field strings per answer (no dicts:
+        the pipeline's native post-processing reads them, parse/fastpath.py); the same
+        failure semantics."""
+        try:
+            return list(await self.client.extract_rows(bodies))
+        except TransientError:
+            raise
+        except Exception as exc:  # noqa: BLE001
+            return [exc] * len(bodies)

@@ -62,6 +62,19 @@ _FAST_TIME_FIRST = re.compile(r"(\d{2}):(\d{2}) (\d{2})\.(\d{2})\.(\d{4})\Z")
 _FAST_MON = re.compile(r"(\d{1,2})([ -])([A-Za-z]{3})\2(\d{4})(?: (\d{2}):(\d{2}))?\Z")
 _MONTHS = {m: i for i, m in enumerate(("jan", "feb", "mar", "apr", "may", "jun", "jul", "aug", "sep", "oct", "nov",
                                        "dec"), 1)}
+# dateutil's month words (parserinfo.MONTHS: abbreviation, "Sept", full name; any case)
+_MONTH_WORDS = {**_MONTHS, **{w: i for i, w in enumerate(("january", "february", "march", "april", "may", "june",
+                                                          "july", "august", "september", "october", "november",
+                                                          "december"), 1)}, "sept": 9}
+# the value grammar's other shapes (12-hour clocks, month names; round 6): each computed
+# with dateutil's rules -- a dotted d.m.y month first when it can be, "12 AM" = 0 h,
+# "h PM" = h + 12, an hour over 12 with AM / PM is dateutil's error (falls through)
+_AMPM = r"(?: ?([AaPp][Mm]))"
+_FAST_ISO_12 = re.compile(r"(\d{4})-(\d{2})-(\d{2}) (\d{1,2}):(\d{2})" + _AMPM + r"\Z")
+_FAST_DOTTED_12 = re.compile(r"(\d{2})\.(\d{2})\.(\d{4}) (\d{1,2}):(\d{2})" + _AMPM + r"\Z")
+_FAST_TIME_FIRST_12 = re.compile(r"(\d{1,2}):(\d{2})" + _AMPM + r" (\d{2})\.(\d{2})\.(\d{4})\Z")
+_FAST_MDY = re.compile(r"([A-Za-z]{3,9}) (\d{1,2}), (\d{4})(?: (\d{1,2}):(\d{2})" + _AMPM + r"?)?\Z")
+_FAST_DMY_WORD = re.compile(r"(\d{1,2}) ([A-Za-z]{3,9}) (\d{4})(?: (\d{1,2}):(\d{2})" + _AMPM + r"?)?\Z")
 _DU_INFO = None
 
 
@@ -79,6 +92,46 @@ def _month_first(a: int, b: int, y: int, hh: int = 0, mm: int = 0) -> datetime:
     if a <= 12:
         return datetime(y, a, b, hh, mm)
     return datetime(y, b, a, hh, mm)
+
+
+def _hour12(h: int, ampm) -> int:
+    """dateutil's AM / PM rule (None: a 24-hour time); -1 for an hour it refuses."""
+    if ampm is None:
+        return h
+    if not 0 <= h <= 12:
+        return -1
+    pm = ampm[0] in "Pp"
+    return h + 12 if (pm and h < 12) else 0 if (not pm and h == 12) else h
+
+
+def _fast_dateutil_12(text: str):
+    m = _FAST_ISO_12.match(text)
+    if m is not None:
+        y, mo, d, hh, mi, ap = m.groups()
+        h = _hour12(int(hh), ap)
+        return None if h < 0 else datetime(int(y), int(mo), int(d), h, int(mi))
+    m = _FAST_DOTTED_12.match(text)
+    if m is not None:
+        a, b, y, hh, mi, ap = m.groups()
+        h = _hour12(int(hh), ap)
+        return None if h < 0 else _month_first(int(a), int(b), int(y), h, int(mi))
+    m = _FAST_TIME_FIRST_12.match(text)
+    if m is not None:
+        hh, mi, ap, a, b, y = m.groups()
+        h = _hour12(int(hh), ap)
+        return None if h < 0 else _month_first(int(a), int(b), int(y), h, int(mi))
+    m = _FAST_MDY.match(text) or _FAST_DMY_WORD.match(text)
+    if m is not None:
+        if m.re is _FAST_MDY:
+            word, d, y, hh, mi, ap = m.groups()
+        else:
+            d, word, y, hh, mi, ap = m.groups()
+        mo = _MONTH_WORDS.get(word.lower())
+        if mo is None:
+            return None
+        h = _hour12(int(hh), ap) if hh is not None else 0
+        return None if h < 0 else datetime(int(y), mo, int(d), h, int(mi or 0))
+    return None
 
 
 def _fast_dateutil(text: str):
@@ -102,6 +155,8 @@ def _fast_dateutil(text: str):
             mo = _MONTHS.get(mon.lower())
             if mo is not None:
                 return datetime(int(y), mo, int(d), int(hh or 0), int(mi or 0))
+        if text[-1:] in "MmrRyYlLtTeEnNhHvV0123456789":  # (cheap pre-check: AM / PM or a month word / digit last)
+            return _fast_dateutil_12(text)
     except ValueError:
         return None  # impossible date: dateutil decides (and raises its own error)
     return None

@@ -1,0 +1,115 @@
+"""The parser processes' native per-message path (``native/csrc/parsefast.cpp``).
+
+VERDICT r05 next #3: host CPU per message dominated the node budget (113.6 us, 8.4x the
+GPU's), most of it per-message Python -- RawSMS validation, keyword filters, answer
+post-processing, ParsedSMS construction and serialisation.  The extension does that
+chain on UTF-8 bytes for the common case and hands every message it cannot prove
+equivalent back to the Python path (``None`` from :func:`scan`, :data:`FALLBACK` from
+:func:`postprocess`), so the routing and every payload are the Python path's, byte for
+byte (tests/test_parsefast.py: the synthetic corpus, hostile strings, the DLQ envelope
+shapes).
+
+* :func:`scan` -- sms.raw payloads -> :class:`FastRaw` (a validated RawSMS that no
+  keyword filter can touch, with its normalised body) or ``None``;
+* :func:`postprocess` -- extractor answer rows (the nine decoded field strings) ->
+  the sms.parsed payload bytes, :data:`UNMATCHED` or :data:`FALLBACK`.
+
+``SMSGATE_NATIVE_PARSE=0`` turns it off (the Python path only); :func:`available` is
+False when the extension is not built.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import unicodedata
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, List, Optional, Sequence, Union
+
+__all__ = ["FastRaw", "available", "scan", "postprocess", "UNMATCHED", "FALLBACK"]
+
+UNMATCHED, FALLBACK = 1, 2
+_LIB = Path(__file__).resolve().parent.parent / "native" / "_lib"
+_EXT: Any = None
+_TRIED = False
+
+
+class FastRaw:
+    """A RawSMS the native scan validated (the attributes post-processing and the DLQ
+    envelopes read; ``model_dump`` is RawSMS's), plus its normalised body."""
+    __slots__ = ("msg_id", "sender", "body", "date", "device_id", "source", "norm")
+
+    def __init__(self, t) -> None:
+        self.msg_id, self.sender, self.body, self.date, self.device_id, self.source, self.norm = t
+
+    def model_dump(self) -> Dict[str, Any]:
+        return {"msg_id": self.msg_id, "sender": self.sender, "body": self.body, "date": self.date,
+                "device_id": self.device_id, "source": self.source}
+
+
+def _tables():
+    """(chars whose upper case contains an ASCII letter, non-ASCII \\d digits, currency
+    alias variants whose .upper() is the alias key)."""
+    from .canonical import CURRENCY_ALIASES
+
+    upper, digits = [], []
+    for c in range(0x80, 0x110000):
+        if 0xD800 <= c <= 0xDFFF:
+            continue
+        ch = chr(c)
+        if any(ord(x) < 0x80 for x in ch.upper()):
+            upper.append(ch)
+        if unicodedata.category(ch) == "Nd":
+            digits.append(ch)
+    aliases: Dict[str, str] = {}
+    for key, code in CURRENCY_ALIASES.items():
+        for v in {key, key.lower(), key.title(), key.capitalize(), key.casefold()}:
+            if v.upper() == key:
+                aliases[v] = code
+    return "".join(upper), "".join(digits), aliases
+
+
+def _ext():
+    global _EXT, _TRIED
+    if _TRIED:
+        return _EXT
+    _TRIED = True
+    if os.environ.get("SMSGATE_NATIVE_PARSE", "1") == "0":
+        return None
+    p = str(_LIB)
+    if p not in sys.path:
+        sys.path.insert(0, p)
+    try:
+        import _parsefast  # type: ignore
+    except ImportError:
+        return None
+    _parsefast.init(*_tables())
+    _EXT = _parsefast
+    return _EXT
+
+
+def available() -> bool:
+    return _ext() is not None
+
+
+def _now():
+    n = datetime.now()
+    return (n.year, n.month, n.day, n.hour, n.minute, n.second, n.microsecond)
+
+
+def scan(payloads: Sequence[bytes]) -> List[Optional[FastRaw]]:
+    """Per sms.raw payload: a :class:`FastRaw`, or None (the Python path decides)."""
+    ext = _ext()
+    if ext is None:
+        return [None] * len(payloads)
+    return [None if t is None else FastRaw(t) for t in ext.scan_raw(payloads)]
+
+
+def postprocess(rows: List[List[str]], raws: Sequence[FastRaw]) -> List[Union[bytes, int]]:
+    """Per answer row (txn_type, date, amount, currency, card, merchant, city, address,
+    balance -- decoded strings): the sms.parsed payload, UNMATCHED or FALLBACK."""
+    ext = _ext()
+    if ext is None:
+        return [FALLBACK] * len(rows)
+    metas = [(r.msg_id, r.device_id, r.sender, r.date, r.body, r.norm) for r in raws]
+    return ext.postprocess(rows, metas, _now())

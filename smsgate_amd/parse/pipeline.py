@@ -30,12 +30,14 @@ import time
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence
 
+from ..serving.qa import null_rejection
 from ..models.domain import CORE_FIELDS, PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
 from ..obs.errors import sentry_capture
 from ..obs.metrics import GEMINI_LATENCY, observe_many
 from ..runtime.errors import TransientError
 from .backends.base import BackendError, ParserBackend
 from .cache import MemoryKV, ResponseCache, cache_key
+from . import fastpath
 from .canonical import canonicalize_answer
 from .dates import fix_broken_datetime, parse_custom_datetime, parse_unix_timestamp
 from .numeric import parse_ambiguous_decimal
@@ -82,6 +84,9 @@ class ParseResult:
     parsed: Optional[ParsedSMS] = None
     error: Optional[BaseException] = None
     cached: bool = False
+    # the native path's PARSED result: the sms.parsed payload itself (parse/fastpath.py;
+    # byte-identical to parsed_wire(parsed), future dates already excluded), no ParsedSMS
+    wire: Optional[bytes] = None
 
 
 def postprocess_answer(raw: RawSMS, fixed_body: str, answer: Dict[str, Any], tz: str = DEFAULT_TZ) -> ParseResult:
@@ -157,13 +162,18 @@ class ParsePipeline:
         keys: List[Optional[str]] = [None] * n
         todo: List[int] = []
         for i, raw in enumerate(raws):
-            if llm_should_skip(raw.body):
-                results[i] = ParseResult(Outcome.UNMATCHED)
-                continue
-            fb = normalize_body(raw.body)
+            fb = getattr(raw, "norm", None)  # a FastRaw: no keyword can match, body normalised natively
+            if fb is None:
+                if llm_should_skip(raw.body):
+                    results[i] = ParseResult(Outcome.UNMATCHED)
+                    continue
+                fb = normalize_body(raw.body)
             bodies[i] = fb
             keys[i] = cache_key(fb)
             todo.append(i)
+        # the native post-processing needs the answers as rows: backends that give them
+        rows_api = getattr(self.backend, "extract_rows", None) if fastpath.available() else None
+        rows: Dict[int, List[str]] = {}
 
         answers: Dict[int, Any] = {}
         cached: set = set()
@@ -184,7 +194,7 @@ class ParsePipeline:
                 ubodies = list(uniq)
                 t0 = time.perf_counter()
                 try:
-                    got = await self.backend.extract_batch(ubodies)
+                    got = await (rows_api or self.backend.extract_batch)(ubodies)
                 except TransientError:
                     raise  # backend unreachable: the stage naks the batch and retries it
                 except Exception as exc:  # whole-batch failure
@@ -196,6 +206,11 @@ class ParsePipeline:
                 self.backend_seconds += time.perf_counter() - t0
                 to_cache = []
                 for b, r in zip(ubodies, got):
+                    if rows_api is not None and isinstance(r, list):
+                        for i in uniq[b]:
+                            rows[i] = r
+                        # the answer as the backend interface gives it (cached raw, D7)
+                        r = null_rejection(dict(zip(CORE_FIELDS, r)))
                     if not isinstance(r, BaseException) and not isinstance(r, dict):
                         r = BackendError(f"backend returned {type(r).__name__}, not a JSON object")
                     for i in uniq[b]:
@@ -205,7 +220,23 @@ class ParsePipeline:
                 if to_cache:
                     self.cache.put_many(to_cache)
 
+        # native post-processing of the fresh answers of natively scanned messages:
+        # the sms.parsed payload, an unmatched verdict, or (FALLBACK) the Python path below
+        if rows:
+            nat = [i for i in todo if i in rows and isinstance(raws[i], fastpath.FastRaw)]
+            if nat:
+                for i, res in zip(nat, fastpath.postprocess([rows[i] for i in nat], [raws[i] for i in nat])):
+                    if isinstance(res, bytes):
+                        results[i] = ParseResult(Outcome.PARSED, wire=res)
+                    elif res == fastpath.UNMATCHED:  # a non-transaction class: null fields
+                        err = AttributeError("'NoneType' object has no attribute 'replace'")
+                        if rows[i][0] != "otp":  # (the Python path's capture rule)
+                            sentry_capture(err, extras={"raw_body": raws[i].body[:4096]})
+                        results[i] = ParseResult(Outcome.UNMATCHED, error=err)
+
         for i in todo:
+            if results[i] is not None:
+                continue
             ans = answers[i]
             if isinstance(ans, BaseException):
                 sentry_capture(ans, extras={"raw_body": raws[i].body[:4096]})

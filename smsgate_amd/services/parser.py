@@ -40,6 +40,7 @@ from ..models.domain import RawSMS, parsed_wire
 from ..obs import metrics as M
 from ..obs.errors import sentry_capture
 from ..obs.tracing import start_span, start_transaction
+from ..parse import fastpath
 from ..parse.pipeline import Outcome, ParsePipeline
 from ..parse.text import worker_should_skip
 from ..runtime.stage import Stage, dlq_publisher
@@ -76,11 +77,16 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
     raw_idx: List[int] = []
 
     with start_span("validate"):
-        for i, m in enumerate(msgs):
-            data = m.data
-            if not isinstance(data, (bytes, bytearray)):
-                data = str(data).encode()
+        datas = [m.data if isinstance(m.data, (bytes, bytearray)) else str(m.data).encode() for m in msgs]
+        # the native scan (parse/fastpath.py): a valid RawSMS no keyword filter can touch,
+        # body normalised -- or None, and the Python path below decides
+        fast = fastpath.scan(datas)
+        for i, data in enumerate(datas):
             texts.append(data)  # decoded only for a failure envelope (_text)
+            if fast[i] is not None:
+                raws.append(fast[i])
+                raw_idx.append(i)
+                continue
             try:
                 if b'"raw"' not in data:
                     # fast path: pydantic-core parses + validates the JSON bytes in one
@@ -129,13 +135,19 @@ async def route_batch(pipeline: ParsePipeline, msgs: Sequence[Msg]) -> Tuple[Lis
                     out.append((SUBJECT_FAILED, _dump({"err": str(res.error), "entry": raw.model_dump()})))
                     counts["fail"] += 1
                     continue
-                if res.outcome is Outcome.UNMATCHED or res.parsed is None:
+                if res.outcome is Outcome.UNMATCHED or (res.parsed is None and res.wire is None):
                     out.append((SUBJECT_FAILED, _dump({"reason": "unmatched", "raw": raw.model_dump()})))
                     counts["fail"] += 1
                     continue
                 # The reference re-validated here (ParsedSMS(**parsed.model_dump()),
                 # worker.py:161-170) — a no-op for an already-validated model, so
                 # only the serialisation keeps the shape-(d) failure route.
+                if res.wire is not None:  # the native path's payload (future dates excluded there)
+                    out.append((SUBJECT_PARSED, res.wire))
+                    out.append((SUBJECT_PROCESSING, res.wire))
+                    counts["ok"] += 1
+                    counts["parsed"] += 1
+                    continue
                 parsed = res.parsed
                 try:
                     future = _is_future(parsed.date)

@@ -438,6 +438,15 @@ class RemoteEngineClient:
         # a non-transaction (txn_type otp / unknown) comes back with null fields
         return [null_rejection(dict(zip(fields, vals))) for vals in rows]
 
+    def decode_rows(self, buf: bytes) -> List[List[str]]:
+        """The nine decoded field strings of every answer of one ``R`` frame, with no
+        per-answer dict: the parser's native post-processing (parse/fastpath.py) reads
+        them as they are (a non-transaction class is judged there)."""
+        fields = self.fields
+        if self.fast is not None:
+            return self.fast.decode_fields(buf, P.HEADER_SIZE, P.count(buf), len(fields))
+        return self.tok.decode_fields(P.unpack_ids(buf)[2], len(fields))
+
     def encode_request(self, rid: int, bodies: Sequence[str]) -> bytes:
         """The ``Q`` frame of ``bodies``: ``body <ans>`` ids, each body cut to max_body
         tokens (counted like ExtractorTokenizer.message_ids)."""
@@ -452,6 +461,13 @@ class RemoteEngineClient:
         return P.pack_raw(b"Q", rid, len(bodies), lens, flat)
 
     async def extract(self, bodies: Sequence[str]) -> List[Dict[str, str]]:
+        return self.decode_response(await self._roundtrip(bodies))
+
+    async def extract_rows(self, bodies: Sequence[str]) -> List[List[str]]:
+        """:meth:`extract` as answer rows (:meth:`decode_rows`)."""
+        return self.decode_rows(await self._roundtrip(bodies))
+
+    async def _roundtrip(self, bodies: Sequence[str]) -> bytes:
         rid = next(self._ids)
         msg = self.encode_request(rid, bodies)
         conn = self._connection()  # may raise BackendUnavailable: nothing registered yet
@@ -481,4 +497,4 @@ class RemoteEngineClient:
             with self._plock:
                 self._pending.pop(rid, None)
             raise self._unavailable(f"engine server did not answer within {self.request_timeout:.0f} s") from None
-        return self.decode_response(buf)
+        return buf

@@ -284,6 +284,42 @@ def test_date_fast_paths_equal_dateutil():
     assert fast > 4000
 
 
+def test_date_fast_paths_12h_and_month_words_equal_dateutil():
+    """The value grammar's other shapes (round 6: 12-hour clocks glued or spaced, any
+    case, time first; month-first "Jun 6, 2025"; full / "Sept" month names) are computed
+    without dateutil and fuzzed against it -- impossible dates, hours over 12 with AM /
+    PM and non-month words included (they fall through to dateutil and its error)."""
+    import random
+
+    from dateutil.parser import parse as du
+
+    from smsgate_amd.parse.dates import _fast_dateutil
+
+    r = random.Random(3)
+    mons = ["Jan", "Feb", "Mar", "Apr", "May", "Jun", "Jul", "Aug", "Sep", "Sept", "Oct", "Nov", "Dec", "June",
+            "September", "may", "JUNE", "Foo", "Mars"]
+    fast = 0
+    for _ in range(12000):
+        y, a, b = r.randint(1990, 2030), r.randint(0, 32), r.randint(0, 32)
+        hh, mi = r.randint(0, 24), r.randint(0, 59)
+        ap, sp, mon = r.choice(["AM", "PM", "am", "pm", "Pm"]), r.choice([" ", ""]), r.choice(mons)
+        s = r.choice([f"{y}-{a % 13:02d}-{b:02d} {hh}:{mi:02d}{sp}{ap}", f"{a:02d}.{b:02d}.{y} {hh:02d}:{mi:02d} {ap}",
+                      f"{hh}:{mi:02d} {ap} {a:02d}.{b:02d}.{y}", f"{mon} {a}, {y}", f"{mon} {a:02d}, {y} {hh:02d}:{mi:02d}",
+                      f"{mon} {a}, {y} {hh}:{mi:02d} {ap}", f"{a} {mon} {y} {hh}:{mi:02d} {ap}",
+                      f"{a} {mon} {y} {hh:02d}:{mi:02d}", f"{a:02d} {mon} {y}"])
+        try:
+            want = du(s)
+        except Exception:
+            want = None
+        try:
+            got = parse_custom_datetime(s)
+        except Exception:
+            got = None
+        assert got == want, s
+        fast += _fast_dateutil(s) is not None
+    assert fast > 6000
+
+
 def test_fast_wire_json_equals_pydantic():
     """parsed_wire / raw_wire are byte-for-byte model_dump_json (the sms.parsed and
     sms.raw contracts), on every template family and on hostile strings."""

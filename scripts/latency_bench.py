@@ -6,8 +6,9 @@ arrival time has passed before every engine step, and records submit → answer
 latency per message.  Reports achieved throughput and p50/p95/p99 latency —
 the serving-side view of the headline throughput number (the reference's
 ``sms_parser_processing_seconds`` histogram measured one Gemini round trip per
-message).  Random-init 135M weights, so every answer decodes the schema's
-maximum 59 tokens (the worst case for latency).
+message).  The qa engine (default) answers in one forward whatever the weights; the
+span / copy engines' random-init answers decode the schema's maximum tokens (their
+worst case).
 
     python scripts/latency_bench.py --rates 2000,8000,14000 --seconds 6
 """
@@ -71,6 +72,12 @@ def main() -> None:
     p.add_argument("--weights", default="random",
                    help="random | train (bench.py's in-run training, reusing its weights cache) | checkpoint path")
     p.add_argument("--spec-k", type=int, default=0, help="speculative decoding drafts per row (0 = off)")
+    p.add_argument("--answer-format", default="qa", choices=["qa", "span", "copy"],
+                   help="qa: the one-forward engine (serving/qa_engine.py, the default extractor); span / copy: the "
+                        "autoregressive engine of rounds 3-4")
+    p.add_argument("--traffic", default="formats", help="utils/synth.py TRAFFIC preset of the offered SMS")
+    p.add_argument("--qa-max-tokens", type=int, default=None)
+    p.add_argument("--qa-min-tokens", type=int, default=None)
     p.add_argument("--profile", default=None, choices=["throughput", "latency", "latency_r2"],
                    help="engine configuration of serving/profiles.py (what engine-server --profile serves); "
                         "--max-slots / --spec-k are then ignored")
@@ -80,8 +87,7 @@ def main() -> None:
     from smsgate_amd import ops
     from smsgate_amd.parse.backends.local_llm import build_engine
     from smsgate_amd.parse.text import normalize_body
-    from smsgate_amd.utils.synth import generate_bodies
-
+    
     if a.gemm_small_m is not None:
         ops.GEMM_SMALL_M = a.gemm_small_m
     kw = {} if a.attn_small_rows is None else dict(decode_attn_small_rows=a.attn_small_rows,
@@ -92,11 +98,15 @@ def main() -> None:
         kw["prefill_key_split"] = a.prefill_key_split
     if a.admit_max_wait_ms is not None:
         kw["admit_max_wait_s"] = a.admit_max_wait_ms / 1000.0
+    if a.qa_max_tokens is not None:
+        kw["qa_max_tokens"] = a.qa_max_tokens
+    if a.qa_min_tokens is not None:
+        kw["qa_min_tokens"] = a.qa_min_tokens
     weights = None
     if a.weights != "random":
         import bench
 
-        bargs = bench._args(["--weights", a.weights])
+        bargs = bench._args(["--weights", a.weights, "--answer-format", a.answer_format])
         weights, _ = bench.acquire_weights(bargs, "cuda:0", 0, 1)
     if a.profile:
         from smsgate_amd.serving.profiles import profile_kwargs
@@ -105,13 +115,21 @@ def main() -> None:
     else:
         ekw = dict(max_slots=a.max_slots, steps_per_graph=2, buckets=(64, 128, 256, 512, 1024, 2048, 4096, 8192),
                    spec_k=a.spec_k, **kw)
-    eng = build_engine("smollm-135m", device="cuda", random_init=weights is None, weights=weights, **ekw)
+    eng = build_engine("smollm-135m", device="cuda", random_init=weights is None, weights=weights,
+                       answer_format=a.answer_format, **ekw)
     a.spec_k = eng.cfg.spec_k
-    arm = {"profile": a.profile, "attn_small_rows": eng.cfg.decode_attn_small_rows, "attn_small": eng.cfg.decode_attn_small,
-           "gemm_small_m": ops.GEMM_SMALL_M, "admit_min_batch": eng.cfg.admit_min_batch,
-           "admit_max_wait_ms": eng.cfg.admit_max_wait_s * 1000.0, "prefill_key_split": eng.cfg.prefill_key_split,
-           "weights": a.weights, "spec_k": a.spec_k}
-    bodies = [normalize_body(b) for b in generate_bodies(20000, seed=5, vocab_name="heldout")]
+    arm = {"profile": a.profile, "answer_format": a.answer_format, "traffic": a.traffic,
+           "weights": a.weights, "engine": type(eng).__name__}
+    if a.answer_format == "qa":
+        arm.update(qa_max_tokens=eng.cfg.qa_max_tokens, qa_min_tokens=eng.cfg.qa_min_tokens, max_slots=eng.cfg.max_slots)
+    else:
+        arm.update(attn_small_rows=eng.cfg.decode_attn_small_rows, attn_small=eng.cfg.decode_attn_small,
+                   gemm_small_m=ops.GEMM_SMALL_M, admit_min_batch=eng.cfg.admit_min_batch,
+                   admit_max_wait_ms=eng.cfg.admit_max_wait_s * 1000.0, prefill_key_split=eng.cfg.prefill_key_split,
+                   spec_k=a.spec_k)
+    from smsgate_amd.utils.synth import generate_traffic
+
+    bodies = [normalize_body(s.body) for s in generate_traffic(20000, seed=5, traffic=a.traffic)]
     ids = eng.tok.message_ids(bodies, eng.cfg.max_body_tokens)
     run_rate(eng, ids, 2000.0, 1.0, seed=0)  # warm-up
     torch.cuda.synchronize()

@@ -39,6 +39,8 @@ __all__ = [
     "CORE_FIELDS",
     "parsed_wire",
     "raw_wire",
+    "LazyParsedSMS",
+    "as_parsed",
 ]
 
 PARSER_VERSION_LLM = "llm-0.2.0"  # gemini_parser.py:267
@@ -98,6 +100,37 @@ def parsed_wire(p: "ParsedSMS") -> bytes:
     dict through ``json.JSONEncoder`` was tried: 12.5 vs 7.9 us per message with
     pydantic-core's serializer on the mixed-layout traffic, Cyrillic included.)"""
     return p.model_dump_json().encode("utf-8")
+
+
+class LazyParsedSMS:
+    """An sms.parsed payload the writer validated natively (parse/fastpath.py
+    ``peek_parsed``: the canonical form of a valid ParsedSMS, every field checked); the
+    :class:`ParsedSMS` object is built from the same bytes on first use (a sink that
+    reads fields, :meth:`model`).  Its attributes are the model's."""
+    __slots__ = ("msg_id", "_data", "_model")
+
+    def __init__(self, msg_id: str, data: bytes) -> None:
+        self.msg_id = msg_id
+        self._data = data
+        self._model: Optional[ParsedSMS] = None
+
+    def model(self) -> ParsedSMS:
+        if self._model is None:
+            self._model = ParsedSMS.model_validate_json(self._data)
+        return self._model
+
+    def __getattr__(self, name: str):
+        return getattr(self.model(), name)
+
+    def __eq__(self, other) -> bool:
+        return self.model() == (other.model() if isinstance(other, LazyParsedSMS) else other)
+
+    __hash__ = None  # type: ignore[assignment]
+
+
+def as_parsed(r) -> "ParsedSMS":
+    """The ParsedSMS of a sink record (a :class:`LazyParsedSMS` or the model itself)."""
+    return r.model() if isinstance(r, LazyParsedSMS) else r
 
 
 def raw_wire(r: "RawSMS") -> bytes:

@@ -67,8 +67,8 @@ def build_extension(name: str, force: bool = False, verbose: bool = False) -> Pa
     LIBDIR.mkdir(parents=True, exist_ok=True)
     target = LIBDIR / ("_" + name + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
     src = CSRC / f"{name}.cpp"
-    if not force and target.exists() and target.stat().st_mtime > max(src.stat().st_mtime,
-                                                                       Path(__file__).stat().st_mtime):
+    deps = [src, Path(__file__)] + sorted(CSRC.glob("*.hpp"))
+    if not force and target.exists() and target.stat().st_mtime > max(d.stat().st_mtime for d in deps):
         return target
     tmp = target.with_suffix(".tmp")
     cmd = [cxx(), "-O3", "-std=c++17", "-Wall", "-Wno-unused-function", "-shared", "-fPIC", "-fvisibility=hidden",

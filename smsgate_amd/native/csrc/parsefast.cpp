@@ -47,6 +47,8 @@
 #include <unordered_set>
 #include <vector>
 
+#include "http_ingest.hpp"  // Md5, the RawSMS encoding of the native HTTP doors
+
 namespace {
 
 // ------------------------------------------------------------------ state from init()
@@ -1340,7 +1342,152 @@ PyObject* py_decimal(PyObject*, PyObject* args) {  // tests: parse_ambiguous_dec
   return pystr(out);
 }
 
+// ---- the writer's check of an sms.parsed payload (services/writer.py): the canonical
+// form only -- ParsedSMS.model_dump_json()'s key order, no blanks, every value of the
+// type and shape ParsedSMS accepts (the date as isoformat() writes it, the amounts as
+// plain decimal strings, a 4-character card).  Anything else is None: pydantic decides.
+bool canon_str_or_null(JP& jp, std::string* out, bool* null) {
+  if (jp.p < jp.e && *jp.p == 'n') {
+    if (!jlit(jp, "null")) return false;
+    *null = true;
+    return true;
+  }
+  *null = false;
+  return jstring(jp, out);
+}
+
+bool canon_key(JP& jp, const char* k, bool first) {
+  if (!first) {
+    if (jp.p >= jp.e || *jp.p != ',') return false;
+    ++jp.p;
+  }
+  std::string key;
+  if (!jstring(jp, &key) || key != k) return false;
+  if (jp.p >= jp.e || *jp.p != ':') return false;
+  ++jp.p;
+  return true;
+}
+
+bool plain_decimal(const std::string& s) {  // -?\d+(\.\d+)?
+  size_t i = 0;
+  if (i < s.size() && s[i] == '-') ++i;
+  size_t a = i;
+  while (i < s.size() && is_ascii_digit(s[i])) ++i;
+  if (i == a) return false;
+  if (i < s.size() && s[i] == '.') {
+    size_t b = ++i;
+    while (i < s.size() && is_ascii_digit(s[i])) ++i;
+    if (i == b) return false;
+  }
+  return i == s.size();
+}
+
+size_t cp_count(const std::string& s) {
+  size_t n = 0;
+  for (unsigned char c : s) n += (c & 0xC0) != 0x80;
+  return n;
+}
+
+// (msg_id, merchant is truthy, (y, mo, d, h, mi, s)) or None
+PyObject* peek_one(const char* data, size_t n) {
+  if (!valid_utf8((const unsigned char*)data, n)) return nullptr;
+  JP jp{data, data + n};
+  if (jp.p >= jp.e || *jp.p != '{') return nullptr;
+  ++jp.p;
+  std::string msg_id, v, merchant;
+  bool null;
+  if (!canon_key(jp, "msg_id", true) || !jstring(jp, &msg_id)) return nullptr;
+  if (!canon_key(jp, "device_id", false) || !canon_str_or_null(jp, &v, &null)) return nullptr;
+  if (!canon_key(jp, "sender", false) || !jstring(jp, &v)) return nullptr;
+  if (!canon_key(jp, "date", false) || !jstring(jp, &v)) return nullptr;
+  DT dt;
+  {
+    Cur k(v);
+    if (!(k.digits(4, &dt.y) && k.lit('-') && k.digits(2, &dt.mo) && k.lit('-') && k.digits(2, &dt.d) && k.lit('T') &&
+          k.digits(2, &dt.h) && k.lit(':') && k.digits(2, &dt.mi) && k.lit(':') && k.digits(2, &dt.s) && k.end()))
+      return nullptr;
+    if (!valid_dt(dt)) return nullptr;
+  }
+  if (!canon_key(jp, "raw_body", false) || !jstring(jp, &v)) return nullptr;
+  if (!canon_key(jp, "txn_type", false) || !jstring(jp, &v)) return nullptr;
+  if (v != "debit" && v != "credit" && v != "otp" && v != "unknown") return nullptr;
+  if (!canon_key(jp, "amount", false) || !canon_str_or_null(jp, &v, &null) || (!null && !plain_decimal(v))) return nullptr;
+  if (!canon_key(jp, "currency", false) || !canon_str_or_null(jp, &v, &null)) return nullptr;
+  if (!canon_key(jp, "card", false) || !canon_str_or_null(jp, &v, &null) || (!null && cp_count(v) != 4)) return nullptr;
+  bool mnull;
+  if (!canon_key(jp, "merchant", false) || !canon_str_or_null(jp, &merchant, &mnull)) return nullptr;
+  if (!canon_key(jp, "city", false) || !canon_str_or_null(jp, &v, &null)) return nullptr;
+  if (!canon_key(jp, "address", false) || !canon_str_or_null(jp, &v, &null)) return nullptr;
+  if (!canon_key(jp, "balance", false) || !canon_str_or_null(jp, &v, &null) || (!null && !plain_decimal(v))) return nullptr;
+  if (!canon_key(jp, "parser_version", false) || !jstring(jp, &v)) return nullptr;
+  if (jp.p >= jp.e || *jp.p != '}' || jp.p + 1 != jp.e) return nullptr;
+  PyObject* id = pystr(msg_id);
+  if (!id) { PyErr_Clear(); return nullptr; }
+  return Py_BuildValue("(NO(iiiiii))", id, (!mnull && !merchant.empty()) ? Py_True : Py_False, dt.y, dt.mo, dt.d,
+                       dt.h, dt.mi, dt.s);
+}
+
+PyObject* py_peek_parsed(PyObject*, PyObject* args) {
+  PyObject* lst;
+  if (!PyArg_ParseTuple(args, "O", &lst)) return nullptr;
+  PyObject* seq = PySequence_Fast(lst, "peek_parsed: a sequence of bytes");
+  if (!seq) return nullptr;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject* out = PyList_New(n);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = PySequence_Fast_GET_ITEM(seq, i);
+    PyObject* res = nullptr;
+    char* data;
+    Py_ssize_t len;
+    if (PyBytes_Check(it) && PyBytes_AsStringAndSize(it, &data, &len) == 0) res = peek_one(data, (size_t)len);
+    if (!res) { Py_INCREF(Py_None); res = Py_None; }
+    PyList_SET_ITEM(out, i, res);
+  }
+  Py_DECREF(seq);
+  return out;
+}
+
+// payload_to_raw(p) + raw_wire(): the gateway role's sms.raw payload of RawSMSPayload
+// fields (device_id, message, sender, timestamp, source); None where RawSMS validation
+// would refuse it (empty sender / message, a source other than device / xml) -- the
+// Python path raises its error there
+PyObject* py_raw_wires(PyObject*, PyObject* args) {
+  PyObject* lst;
+  if (!PyArg_ParseTuple(args, "O", &lst)) return nullptr;
+  PyObject* seq = PySequence_Fast(lst, "raw_wires: a sequence of tuples");
+  if (!seq) return nullptr;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  PyObject* out = PyList_New(n);
+  ingest::Payload p;
+  std::string o;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* t = PySequence_Fast_GET_ITEM(seq, i);
+    PyObject* res = nullptr;
+    if (PyTuple_Check(t) && PyTuple_GET_SIZE(t) == 5) {
+      PyObject* src = PyTuple_GET_ITEM(t, 4);
+      PyObject* ts = PyTuple_GET_ITEM(t, 3);
+      p.has_source = src != Py_None;
+      bool ok = get_str(PyTuple_GET_ITEM(t, 0), &p.device_id) && get_str(PyTuple_GET_ITEM(t, 1), &p.message) &&
+                get_str(PyTuple_GET_ITEM(t, 2), &p.sender) && PyLong_CheckExact(ts) &&
+                (!p.has_source || get_str(src, &p.source));
+      if (ok) {
+        int overflow = 0;
+        long long v = PyLong_AsLongLongAndOverflow(ts, &overflow);
+        if (overflow || (v == -1 && PyErr_Occurred())) { PyErr_Clear(); ok = false; }
+        p.timestamp = v;
+      }
+      if (ok && ingest::to_raw_json(p, o)) res = PyBytes_FromStringAndSize(o.data(), (Py_ssize_t)o.size());
+    }
+    if (!res) { Py_INCREF(Py_None); res = Py_None; }
+    PyList_SET_ITEM(out, i, res);
+  }
+  Py_DECREF(seq);
+  return out;
+}
+
 PyMethodDef methods[] = {
+    {"peek_parsed", py_peek_parsed, METH_VARARGS, "peek_parsed([bytes]) -> [None | (msg_id, merchant?, date tuple)]"},
+    {"raw_wires", py_raw_wires, METH_VARARGS, "raw_wires([(device_id, message, sender, timestamp, source)]) -> [bytes | None]"},
     {"init", py_init, METH_VARARGS, "init(upper_ascii_chars, unicode_digits, currency_aliases)"},
     {"scan_raw", py_scan_raw, METH_VARARGS, "scan_raw(payloads) -> [None | (msg_id, sender, body, date, device_id, source, norm_body)]"},
     {"postprocess", py_postprocess, METH_VARARGS, "postprocess(rows, metas, now) -> [bytes | 1 (unmatched) | 2 (fallback)]"},

@@ -90,8 +90,7 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
     from ..parse.backends.local_llm import RemoteLLMBackend
     from ..parse.pipeline import ParsePipeline
     from ..serving.remote import RemoteEngineClient
-    from ..models.domain import raw_wire
-    from ..services.gateway import payload_to_raw
+    from ..parse.fastpath import raw_wires  # the gateway role's payload -> sms.raw bytes (native)
     from ..services.parser import ParserWorker
     from ..services.writer import WriterService
     from ..sinks.memory import MemorySink
@@ -167,7 +166,7 @@ async def _worker_async(conn: Connection, rank: int, widx: int, cfg: Dict[str, A
                 chunk = 256
                 msgs = prepared[i]
                 for c in range(0, len(msgs), chunk):
-                    items = [(SUBJECT_RAW, raw_wire(payload_to_raw(p))) for p in msgs[c:c + chunk]]
+                    items = [(SUBJECT_RAW, w) for w in raw_wires(msgs[c:c + chunk])]
                     await bus.publish_many(items)
                     await asyncio.sleep(0)
 

@@ -26,7 +26,7 @@ from datetime import datetime
 from pathlib import Path
 from typing import Any, Dict, List, Optional, Sequence, Union
 
-__all__ = ["FastRaw", "available", "scan", "postprocess", "UNMATCHED", "FALLBACK"]
+__all__ = ["FastRaw", "available", "scan", "postprocess", "raw_wires", "peek_parsed", "UNMATCHED", "FALLBACK"]
 
 UNMATCHED, FALLBACK = 1, 2
 _LIB = Path(__file__).resolve().parent.parent / "native" / "_lib"
@@ -113,3 +113,26 @@ def postprocess(rows: List[List[str]], raws: Sequence[FastRaw]) -> List[Union[by
         return [FALLBACK] * len(rows)
     metas = [(r.msg_id, r.device_id, r.sender, r.date, r.body, r.norm) for r in raws]
     return ext.postprocess(rows, metas, _now())
+
+
+def raw_wires(payloads) -> List[bytes]:
+    """``raw_wire(payload_to_raw(p))`` of gateway payloads (services/gateway.py
+    RawSMSPayload): the md5 message id and RawSMS's JSON natively, the Python path for
+    any payload RawSMS validation would refuse (it raises there)."""
+    from ..models.domain import raw_wire
+    from ..services.gateway import payload_to_raw
+
+    ext = _ext()
+    got = ext.raw_wires([(p.device_id, p.message, p.sender, p.timestamp, p.source) for p in payloads]) \
+        if ext is not None else [None] * len(payloads)
+    return [g if g is not None else raw_wire(payload_to_raw(p)) for g, p in zip(got, payloads)]
+
+
+def peek_parsed(payloads: Sequence[bytes]) -> List[Optional[tuple]]:
+    """The writer's check of sms.parsed payloads: per payload ``(msg_id, merchant is
+    truthy, (y, mo, d, h, mi, s))`` when it is the canonical form of a valid ParsedSMS
+    (every field checked natively), else None (pydantic decides)."""
+    ext = _ext()
+    if ext is None:
+        return [None] * len(payloads)
+    return ext.peek_parsed(payloads)

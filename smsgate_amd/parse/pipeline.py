@@ -30,7 +30,6 @@ import time
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence
 
-from ..serving.qa import null_rejection
 from ..models.domain import CORE_FIELDS, PARSER_VERSION_LLM, ParsedSMS, ParsedSmsCore, RawSMS
 from ..obs.errors import sentry_capture
 from ..obs.metrics import GEMINI_LATENCY, observe_many
@@ -65,6 +64,16 @@ def _debug_record(body: str, answer: Dict[str, Any], outcome: str) -> None:
     with open(os.path.join(_DEBUG_DIR, f"answers-{os.getpid()}.jsonl"), "a") as fh:
         fh.write(json.dumps({"outcome": outcome, "body": body, "answer": answer}, ensure_ascii=False,
                             default=str) + "\n")
+
+
+_REJECT_TXN = ("otp", "unknown")  # serving/qa.py REJECT_TXN (not imported: parse must not import serving)
+
+
+def _null_rejection(answer: Dict[str, Any]) -> Dict[str, Any]:
+    """serving/qa.py null_rejection: a non-transaction class nulls every other field."""
+    if answer.get("txn_type") in _REJECT_TXN:
+        return {k: (v if k == "txn_type" else None) for k, v in answer.items()}
+    return answer
 
 
 class BrokenMessage(Exception):
@@ -210,7 +219,7 @@ class ParsePipeline:
                         for i in uniq[b]:
                             rows[i] = r
                         # the answer as the backend interface gives it (cached raw, D7)
-                        r = null_rejection(dict(zip(CORE_FIELDS, r)))
+                        r = _null_rejection(dict(zip(CORE_FIELDS, r)))
                     if not isinstance(r, BaseException) and not isinstance(r, dict):
                         r = BackendError(f"backend returned {type(r).__name__}, not a JSON object")
                     for i in uniq[b]:

@@ -22,7 +22,8 @@ from datetime import datetime, timezone
 from typing import List, Optional, Sequence, Tuple
 
 from ..bus.base import SUBJECT_FAILED, SUBJECT_PARSED, Bus, Msg, ack_all
-from ..models.domain import ParsedSMS
+from ..models.domain import LazyParsedSMS, ParsedSMS
+from ..parse import fastpath
 from ..obs import metrics as M
 from ..obs.errors import sentry_capture
 from ..runtime.retry import retry
@@ -66,8 +67,25 @@ class WriterService:
             sentry_capture(err, extras={"raw_msg": text})
             dlq.append((SUBJECT_FAILED, json.dumps({"err": str(err), "entry": text}).encode()))
 
-        for m in msgs:
-            data = m.data
+        datas = [m.data for m in msgs]
+        # the canonical payloads (what the parser writes) are checked natively and stored
+        # as LazyParsedSMS records: no second pydantic pass over bytes just produced
+        peek = fastpath.peek_parsed([d if isinstance(d, bytes) else b"" for d in datas])
+        now = None
+        for data, pk in zip(datas, peek):
+            if pk is not None:
+                msg_id, has_merchant, dt = pk
+                if not has_merchant:
+                    self.skipped += 1
+                    continue
+                if now is None:
+                    n = datetime.now()
+                    now = (n.year, n.month, n.day, n.hour, n.minute, n.second, n.microsecond)
+                if dt > now[:6]:  # naive date in the future (equal seconds: not after now)
+                    fail(ValueError("Bad date"), data.decode(errors="ignore"))
+                    continue
+                to_store.append((LazyParsedSMS(msg_id, data), data))
+                continue
             try:
                 # one Rust pass parses and validates the bytes (the reference: json +
                 # model_validate); the text is decoded only for a failure envelope

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from typing import Dict, List, Sequence
 
-from ..models.domain import ParsedSMS
+from ..models.domain import ParsedSMS, as_parsed
 from .base import Sink
 
 __all__ = ["MemorySink"]
@@ -22,4 +22,4 @@ class MemorySink(Sink):
         self.writes += len(records)
 
     def all(self) -> List[ParsedSMS]:
-        return list(self.records.values())
+        return [as_parsed(r) for r in self.records.values()]

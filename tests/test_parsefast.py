@@ -300,3 +300,84 @@ def test_route_batch_is_byte_identical_with_and_without_the_native_path(arun, mo
         else:
             assert a == b
     assert native_counts["parsed"] > 300 and native_counts["fail"] > 50, native_counts
+
+
+def test_raw_wires_equal_the_gateway_mapping():
+    """The gateway role's sms.raw payloads (bench ingestion): native md5 id + RawSMS
+    JSON == raw_wire(payload_to_raw(p)); payloads RawSMS refuses raise as before."""
+    from smsgate_amd.models.domain import raw_wire
+    from smsgate_amd.services.gateway import RawSMSPayload, payload_to_raw
+
+    r = random.Random(31)
+    ps = [RawSMSPayload(device_id=r.choice(["bench", "dev \"x\"\n", "Д"]), message=s.body, sender=r.choice(["BANK", "Банк"]),
+                        timestamp=r.choice([s.timestamp, -5, 0, 10 ** 15]), source=r.choice(["device", "xml"]))
+          for s in _corpus(600, seed=32)]
+    ps += [RawSMSPayload(device_id="d", message="x\x00\x1f\x7f😀 ", sender="s", timestamp=1, source="device")]
+    assert fastpath.raw_wires(ps) == [raw_wire(payload_to_raw(p)) for p in ps]
+    for bad in (RawSMSPayload(device_id="d", message="", sender="s", timestamp=1, source="device"),
+                RawSMSPayload(device_id="d", message="m", sender="s", timestamp=1, source=None),
+                RawSMSPayload(device_id="d", message="m", sender="s", timestamp=1, source="web")):
+        with pytest.raises(Exception):
+            fastpath.raw_wires([bad])
+
+
+def test_writer_peek_accepts_only_valid_parsed_payloads():
+    """The writer's native check: whenever it accepts a payload, pydantic validates it to
+    the same msg_id, merchant truthiness and date; payloads off the canonical form, or
+    invalid, are left to pydantic.  And the writer's output (sink records, skips, DLQ)
+    is the pydantic path's."""
+    from decimal import Decimal
+
+    from smsgate_amd.models.domain import ParsedSMS
+
+    r = random.Random(41)
+    good = []
+    for s in _corpus(600, seed=42):
+        if not s.answer or s.kind == "negative":
+            continue
+        raw = RawSMS(msg_id=f"m{len(good)}", sender="B", body=s.body, date=str(s.timestamp), device_id=r.choice(["d", None]))
+        p = postprocess_answer(raw, normalize_body(s.body), s.answer).parsed
+        if p is not None:
+            good.append(parsed_wire(p))
+    good.append(parsed_wire(ParsedSMS(msg_id="x", device_id=None, sender="s", date=datetime(2024, 2, 29, 1, 2, 3),
+                                      raw_body="b", txn_type="otp", amount=None, currency=None, card=None,
+                                      merchant="", city=None, address=None, balance=Decimal("-0.0"))))
+    bad = []
+    for g in good[:150]:
+        for a, b in ((b'"date":"', b'"date":"2025-02-30T'), (b'"card":"', b'"card":"12345'), (b'"amount":"', b'"amount":"1E'),
+                     (b'"txn_type":"', b'"txn_type":"x'), (b',"city"', b', "city"'), (b'"amount":"', b'"amount":'),
+                     (b'{"msg_id"', b'{"msg_id":"y","msg_id"')):
+            bad.append(g.replace(a, b, 1))
+        k = r.randrange(len(g))
+        bad.append(g[:k] + bytes([r.randrange(256)]) + g[k + 1:])
+    allp = good + bad
+    got = fastpath.peek_parsed(allp)
+    assert all(g is not None for g in got[:len(good)])
+    for data, pk in zip(allp, got):
+        if pk is None:
+            continue
+        p = ParsedSMS.model_validate_json(data)
+        assert pk[0] == p.msg_id and pk[1] == bool(p.merchant) and datetime(*pk[2]) == p.date, data
+
+
+def test_pipeline_null_rejection_matches_the_engine_rule():
+    from smsgate_amd.parse.pipeline import _REJECT_TXN, _null_rejection
+    from smsgate_amd.serving.qa import REJECT_TXN
+
+    assert tuple(_REJECT_TXN) == tuple(REJECT_TXN)
+    for t in ("debit", "credit", "otp", "unknown"):
+        a = dict(zip(FIELDS, [t] + ["x"] * 8))
+        assert _null_rejection(a) == null_rejection(a)
+
+
+@pytest.mark.parametrize("first", ["smsgate_amd.serving", "smsgate_amd.parse", "smsgate_amd.serving.qa",
+                                   "smsgate_amd.parallel.replica", "smsgate_amd.services.parser"])
+def test_package_imports_in_any_order(first):
+    """A fresh interpreter imports every package whichever comes first (a parse ->
+    serving import made serving-first imports circular)."""
+    import subprocess
+    import sys
+
+    code = f"import {first}; import smsgate_amd.parse.pipeline, smsgate_amd.serving.remote, smsgate_amd.services.writer"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]

@@ -247,7 +247,8 @@ GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 6
               13: (128, 128), 14: (256, 128), 15: (128, 256), 16: (256, 64), 17: (32, 64), 18: (32, 64),
               19: (256, 256), 20: (256, 256), 21: (128, 96), 22: (64, 96), 23: (128, 192), 24: (256, 96),
               25: (128, 96), 26: (64, 192), 27: (32, 96), 28: (128, 192), 29: (256, 96),
-              30: (128, 96), 31: (64, 96), 32: (256, 192), 33: (128, 192), 34: (256, 192)}
+              30: (128, 96), 31: (64, 96), 32: (256, 192), 33: (128, 192), 34: (256, 192),
+              35: (256, 192), 36: (256, 192), 37: (256, 192), 38: (256, 192)}
 # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 # a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
@@ -256,7 +257,10 @@ GEMM_SWIGLU_ONLY = {10, 19, 20}
 # 21..26: 48-wide wave tiles (96 / 192-wide blocks) for the N = 576 residual GEMMs: no SwiGLU
 # 28 / 29: 128x192 / 256x96 with 4 waves (64x96 wave tiles); 30 / 31: 128x96 / 64x96 with 8 waves
 # 32: 256x192 with 8 waves (64x96 wave tiles); 33 / 34: 128x192 / 256x192 with BK 32 and 4 stages
-GEMM_NO_SWIGLU = {21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34}
+GEMM_NO_SWIGLU = {21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38}
+# 35..38: the persistent, staggered 256x192 residual GEMM (gemm256p_resid_kernel: 4 / 5
+# ring buffers, 16x16x32 / 32x32x16 MFMAs) -- epi "resid" only
+GEMM_RESID_ONLY = {35, 36, 37, 38}
 _EPI = {"store": 0, "resid": 1, "swiglu": 2}
 
 

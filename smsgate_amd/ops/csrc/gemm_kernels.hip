@@ -35,6 +35,7 @@
 // so each XCD is given a contiguous range of tiles (tiles sharing A rows share
 // that XCD's L2).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 namespace {
@@ -1061,6 +1062,213 @@ __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail DMAs
 }
 
+// ---------------------------------------------------------------------------
+// Persistent, STAGGERED 256x192 residual GEMM (cfg 35): C = R + A·Wᵀ for the N = 576
+// residual GEMMs (o-proj, down-proj), the residual counterpart of the gate/up kernel's
+// schedule (the one-group read-then-multiply loop of cfg 28 kept
+// both at 24-29 % of the dense peak).
+//
+//  * 8 waves in two groups; group wr owns tile rows wr·128 + [0,128) and runs ONE
+//    barrier behind the other, so on every SIMD one wave's MFMA cluster overlaps the
+//    other wave's LDS reads (2 waves per SIMD);
+//  * wave (wr, wi, wj) computes rows wr·128 + wi·64 + [0,64) x columns wj·96 + [0,96):
+//    64x96 wave tiles (cfg 28's), 4 x 6 fragments of 16x16x32 MFMAs;
+//  * BK 32 K-steps (64-B LDS rows, the sw32 swizzle) in NB ring buffers of 28 KB
+//    (A 256 rows + W 192 rows); a step's 4 LDS-DMAs per wave are issued NB-1 steps
+//    ahead, right AFTER the barrier that ends a read section (the lagging group's reads
+//    of the buffer being refilled have retired: it waits lgkmcnt(0) before its next
+//    barrier), and retired by a counted vmcnt one step before the step is read (every
+//    wave's wait precedes a barrier that precedes any read of that step);
+//  * persistent: one block per CU walks its tiles through the same XCD-aware grouped map,
+//    the step sequence runs on across tiles (the next tile's first K-steps are in flight
+//    during this tile's last), and the epilogue works from the accumulators: residual add
+//    with the unfused path's rounding (bf16 product, fp32 add, bf16), 8-byte stores, and
+//    the output rows' x² partials per 96-column part in the EXACT order of the 96-wide
+//    tiles (pairs (2e, 2e+1) of an 8-column chunk by fmaf chains, chunks summed left to
+//    right), so every consumer sees the same partials whichever tile produced them.
+// MF 32: the same tile with v_mfma_f32_32x32x16_bf16 (2 x 3 fragments of 32x32 per wave;
+// VERDICT r05 next #2's A/B): the same 10 fragment reads per K-step (the wave tile, not
+// the MFMA shape, sets the LDS traffic) for 12 instead of 24 MFMAs.
+template <int NB, int MF>
+__global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __restrict__ A, int lda,
+                                                            const uint16_t* __restrict__ W, uint16_t* C, int ldc,
+                                                            const uint16_t* R, int ldr, int M, int N, int K,
+                                                            int tiles_m, int tiles_n, int gm, NormArgs na) {
+  constexpr int BM = 256, BN = 192, BKT = 32, BUF = (BM + BN) * BKT;
+  static_assert(NB >= 4 && NB * BUF * 2 <= 160 * 1024, "ring buffers");
+  static_assert(MF == 16 || MF == 32, "MFMA shape");
+  constexpr int FI = 64 / MF, FJ = 96 / MF;  // fragments per wave tile
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  typedef typename std::conditional<MF == 16, f32x4, f32x16>::type accv;
+  constexpr int AV = MF == 16 ? 4 : 16;  // accumulator values per lane per fragment
+  constexpr int KS = MF == 16 ? 1 : 2;   // MFMA k-substeps per BK 32 step
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NB * BUF];
+
+  const int T = tiles_m * tiles_n;
+  auto tile_mn = [&](int v, int& m0, int& n0) {
+    const int xcd = v & 7, q8 = T >> 3, r8 = T & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+    const int gsz = gm * tiles_n, g = t / gsz, gl = t - g * gsz;
+    const int grows = min(gm, tiles_m - g * gm);
+    m0 = (g * gm + gl % grows) * BM;
+    n0 = (gl / grows) * BN;
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wi = (wave >> 1) & 1, wj = wave & 1;
+  const int rbase = wr * 128 + wi * 64, cbase = wj * 96;
+  const int KT = K / BKT;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= T) return;  // (the launcher sizes the grid <= T: never taken)
+  const int my_tiles = (T - (int)blockIdx.x + G - 1) / G;
+  const int S = my_tiles * KT;  // K-steps of this block, over all its tiles
+
+  // step t's DMAs (4 per wave) into buffer t % NB; steps past the end re-load the last
+  // one (same bytes, an idle buffer, never read) so every wave's vmcnt stays exact
+  auto stage = [&](int t) {
+    const int tt = min(t, S - 1);
+    int mm, nn;
+    tile_mn((int)blockIdx.x + (tt / KT) * G, mm, nn);
+    const int kk = (tt % KT) * BKT;
+    uint16_t* dst = smem + (t % NB) * BUF;
+    issue_tile<BM, 8, BKT>(A, lda, mm, M - 1, kk, dst, wave, lane);
+    issue_tile<BN, 8, BKT>(W, K, nn, N - 1, kk, dst + BM * BKT, wave, lane);
+  };
+  accv acc[FI][FJ];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int q = 0; q < AV; ++q) acc[i][j][q] = 0.f;
+  };
+  zero_acc();
+  bf16x8 af[KS][FI], bq[KS][FJ];
+  // MF 16: lane reads 16-B chunk (lane >> 4) of row (lane & 15); MF 32: chunk
+  // 2·ks + (lane >> 5) of row (lane & 31)
+  auto read_frags = [&](const uint16_t* buf) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int ch = MF == 16 ? (lane >> 4) : 2 * ks + (lane >> 5);
+      const int rl = lane & (MF - 1);
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int row = rbase + i * MF + rl;
+        af[ks][i] = *reinterpret_cast<const bf16x8*>(buf + row * BKT + ((ch ^ sw32(row)) << 3));
+      }
+      const uint16_t* bb = buf + BM * BKT;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int row = cbase + j * MF + rl;
+        bq[ks][j] = *reinterpret_cast<const bf16x8*>(bb + row * BKT + ((ch ^ sw32(row)) << 3));
+      }
+    }
+  };
+
+  // prologue: steps 0 .. NB-2 in flight; step 0 retired by every wave before a common
+  // barrier, then group 1 falls one barrier behind (its extra barrier pairs with group
+  // 0's first mid barrier; group 0 re-aligns after the loop)
+#pragma unroll
+  for (int t = 0; t < NB - 1; ++t) stage(t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NB - 2)) : "memory");
+  __builtin_amdgcn_s_barrier();
+  if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
+
+  int v = blockIdx.x, m0, n0;
+  tile_mn(v, m0, n0);
+  int kt = 0;
+  for (int s = 0; s < S; ++s) {
+    // ---- read section of step s (its data landed: retired one step ago, or above)
+    read_frags(smem + (s % NB) * BUF);
+    // step s+1 retired before the barrier that precedes its reads (NB-3 younger steps
+    // of this wave may stay in flight)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NB - 3)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // ---- MFMA section: refill the buffer of step s-1 (read before the previous barrier
+    // by both groups) with step s+NB-1
+    stage(s + NB - 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          if constexpr (MF == 16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bq[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    if (++kt < KT) continue;
+    // ---- tile done: epilogue from the accumulators (no barriers), then the next tile.
+    // MF 16: lane holds rows rbase + 16i + (lane & 15), columns cbase + 16j + 4·(lane >> 4)
+    // + q; MF 32: rows rbase + 32i + (lane & 31), columns cbase + 32j + 8g + 4·(lane >> 5)
+    // + q (value 4g + q).  An 8-column x² chunk: its first 4 columns in one lane, its last
+    // 4 in the partner lane (xor 16 / xor 32), the fmaf chain run through both in order.
+    kt = 0;
+    const bool want_ss = na.ssout != nullptr;
+#pragma unroll
+    for (int i = 0; i < FI; ++i) {
+      const int gr = m0 + rbase + i * MF + (lane & (MF - 1));
+      const bool ok = gr < M;
+      constexpr int NCH = FJ * (AV / 4);  // this lane's 4-column groups
+      float own[NCH];
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int g = 0; g < AV / 4; ++g) {
+          const int col = n0 + cbase + (MF == 16 ? j * 16 + 4 * (lane >> 4) : j * 32 + 8 * g + 4 * (lane >> 5));
+          uint2 rv = make_uint2(0u, 0u);
+          if (ok) rv = *reinterpret_cast<const uint2*>(R + (size_t)gr * ldr + col);
+          float o[4];
+          const uint32_t rw[2] = {rv.x, rv.y};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float prod = bf2f(f2bf(acc[i][j][4 * g + q]));  // the staged bf16 product (cfg 28's C tile)
+            const float res = bf2f((rw[q >> 1] >> ((q & 1) * 16)) & 0xffffu);
+            o[q] = bf2f(f2bf(prod + res));
+          }
+          if (ok)
+            *reinterpret_cast<uint2*>(C + (size_t)gr * ldc + col) =
+                make_uint2((uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16),
+                           (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16));
+          const float first = fmaf(o[2], o[2], fmaf(o[3], o[3], fmaf(o[0], o[0], fmaf(o[1], o[1], 0.f))));
+          const float recv = __shfl_xor(first, MF == 16 ? 16 : 32, 64);
+          own[j * (AV / 4) + g] = fmaf(o[2], o[2], fmaf(o[3], o[3], fmaf(o[0], o[0], fmaf(o[1], o[1], recv))));
+        }
+      if (want_ss) {
+        float sum = 0.f;
+        if constexpr (MF == 16) {
+          // lane group 1 holds chunks 0, 2 .. 10 of the row's 96-column part, group 3
+          // chunks 1, 3 .. 11: summed left to right in group 1
+          float other[NCH];
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) other[c] = __shfl_xor(own[c], 32, 64);
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            sum += own[c];
+            sum += other[c];
+          }
+          if ((lane >> 4) == 1 && ok) na.ssout[(size_t)(n0 / 96 + wj) * na.ld + gr] = sum;
+        } else {
+          // the upper half-wave holds all 12 chunks of its row, in order
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) sum += own[c];
+          if ((lane >> 5) == 1 && ok) na.ssout[(size_t)(n0 / 96 + wj) * na.ld + gr] = sum;
+        }
+      }
+    }
+    zero_acc();
+    v += G;
+    if (s + 1 < S) tile_mn(v, m0, n0);
+  }
+  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's dummy DMAs
+}
+
 int g_group_m = 8;  // M-tiles per rasterisation group (sg_gemm_set_group_m)
 
 template <int BM, int BN, int WM, int WN, int EPI, int NORM, int ST, int BKT = BK>
@@ -1132,6 +1340,8 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  30: 128x96 (4x2) 2st, 8 waves   31: 64x96 (4x2) 2st, 8 waves
 //  32: 256x192 (4x2) 2st, 8 waves — 64x96 wave tiles (epi 0 / 1 only)
 //  33: 128x192 (2x2) BK 32, 4st   34: 256x192 (4x2) BK 32, 4st, 8 waves (epi 0 / 1 only)
+//  35: 256x192 persistent staggered residual GEMM (gemm256p_resid_kernel, 4 ring buffers,
+//      16x16x32 MFMAs; epi 1 only)   36: 5 ring buffers   37 / 38: 35 / 36 with 32x32x16 MFMAs
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1160,9 +1370,10 @@ int sg_gemm_probe(const void* A, const void* W, void* C, int M, int N, int K, in
 // zero-padded); ssout (EPI 1 only, may be null): this GEMM's output-row partials.
 int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void* R, int ldr, int M, int N, int K,
             int epi, int norm, float eps, int cfg, const float* ssin, float* ssout, int ss_ld, hipStream_t stream) {
-  static const int BNs[35] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
-                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96, 192, 192, 192};
-  if (cfg < 0 || cfg > 34) return -1;
+  static const int BNs[39] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
+                             256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96, 192, 192, 192, 192, 192,
+                             192, 192};
+  if (cfg < 0 || cfg > 38) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
   if ((norm == 2 && (!ssin || ss_ld < M)) || (ssout && (epi != 1 || N / BNs[cfg] > SS_PARTS || ss_ld < M)))
@@ -1194,6 +1405,22 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     else if (norm == 1) SG_256P(1);
     else SG_256P(0);
 #undef SG_256P
+    return 0;
+  }
+  if (cfg >= 35 && cfg <= 38) {  // persistent staggered residual GEMM: one block per CU
+    if (epi != 1 || norm != 0 || K % 32 != 0) return -3;
+    if (ssout && N / 96 > SS_PARTS) return -2;
+    const int tm = (M + 255) / 256, tn = N / 192, T = tm * tn;
+    const int grid = T < 256 ? T : 256;
+    const int gmv = g_group_m > 0 ? g_group_m : 1;
+#define SG_RP(NB_, MF_)                                                                                       \
+  hipLaunchKernelGGL((gemm256p_resid_kernel<NB_, MF_>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda, \
+                     (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R, ldr, M, N, K, tm, tn, gmv, na)
+    if (cfg == 35) SG_RP(4, 16);
+    else if (cfg == 36) SG_RP(5, 16);
+    else if (cfg == 37) SG_RP(4, 32);
+    else SG_RP(5, 32);
+#undef SG_RP
     return 0;
   }
 #define SG_ARGS epi, norm, A, lda, W, C, ldc, R, ldr, M, N, K, eps, stream, na

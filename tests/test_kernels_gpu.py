@@ -236,7 +236,7 @@ def test_fsm_sample_greedy_and_transitions():
 def _tile_cases(shapes):
     """(cfg, *shape) for every tile config whose BN divides N (others cannot run it)."""
     return [(cfg, *s) for cfg in sorted(ops.GEMM_TILES) for s in shapes
-            if cfg not in ops.GEMM_SWIGLU_ONLY and s[1] % ops.GEMM_TILES[cfg][1] == 0]
+            if cfg not in ops.GEMM_SWIGLU_ONLY | ops.GEMM_RESID_ONLY and s[1] % ops.GEMM_TILES[cfg][1] == 0]
 
 
 @pytest.mark.parametrize("cfg,M,N,K", _tile_cases([(1, 128, 64), (100, 576, 576), (777, 960, 576),
@@ -251,7 +251,9 @@ def test_gemm_store_and_norm(cfg, M, N, K):
     torch.testing.assert_close(out_n.float(), ops.ref_gemm(a, w, norm_eps=1e-5, norm_w=nw), atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("cfg,M,N,K", _tile_cases([(1, 576, 1536), (333, 576, 1536), (2048, 576, 1536)]))
+@pytest.mark.parametrize("cfg,M,N,K", _tile_cases([(1, 576, 1536), (333, 576, 1536), (2048, 576, 1536)])
+                         + [(c, M, 576, K) for c in sorted(ops.GEMM_RESID_ONLY)
+                            for M, K in ((1, 1536), (333, 1536), (2048, 576), (70000, 1536))])
 def test_gemm_residual_inplace(cfg, M, N, K):
     a = _bf(M, K, seed=21)
     w = _bf(N, K, scale=K ** -0.5, seed=22)
@@ -382,7 +384,7 @@ def test_gemm_argmax_matches_logits_path(cfg, M):
             assert int(tok_b[b]) == int(lf[b].masked_fill(~allowed[s], float("-inf")).argmax())
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 17, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34])
+@pytest.mark.parametrize("cfg", [1, 3, 17, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36])
 @pytest.mark.parametrize("M", [5, 333, 2048])
 def test_gemm_producer_norm(cfg, M):
     """Residual GEMM with ``ss_out`` writes per-N-tile x² partials of the rows it
@@ -675,3 +677,26 @@ def test_embed_rows_matches_f_embedding():
     bad = torch.tensor([-1, 8192, 5], dtype=torch.int32, device=DEV)
     out = ops.embed_rows(bad, table)
     assert torch.count_nonzero(out[:2]) == 0 and torch.equal(out[2], table[5])
+
+
+@pytest.mark.parametrize("cfg", sorted(ops.GEMM_RESID_ONLY))
+@pytest.mark.parametrize("M,K", [(110592, 1536), (55296, 576), (4099, 576)])
+def test_gemm_resid_persistent_matches_cfg28(cfg, M, K):
+    """The persistent staggered residual GEMM at the qa engine's operating points (many
+    tiles per block: the step ring runs across tile boundaries): 16x16x32 (35 / 36)
+    bit-identical to cfg 28, outputs and x² partials (the consumer's row scales do not
+    depend on the config); 32x32x16 (37 / 38: other fp32 accumulation chunks) within
+    rounding of it, partials within fp32 rounding."""
+    H = 576
+    a = _bf(M, K, seed=81)
+    w = _bf(H, K, scale=K ** -0.5, seed=82)
+    x = _bf(M, H, seed=83)
+    x28, ss28 = x.clone(), ops.ss_buffer(M, DEV)
+    ops.gemm(a, w, epi="resid", resid=x28, cfg=28, ss_out=ss28)
+    xn, ssn = x.clone(), ops.ss_buffer(M, DEV)
+    ops.gemm(a, w, epi="resid", resid=xn, cfg=cfg, ss_out=ssn)
+    if cfg in (35, 36):
+        assert torch.equal(xn, x28) and torch.equal(ssn, ss28)
+    else:
+        torch.testing.assert_close(xn.float(), x28.float(), atol=2e-2, rtol=1e-2)
+        torch.testing.assert_close(ssn, ss28, rtol=2e-2, atol=1e-2)

@@ -5,6 +5,7 @@ CPU checks: every gold answer of every template family is expressible and walks 
 FSM under the copy rules; expanding a span answer gives exactly the copy-format
 answer (what ops.span_commit writes on the GPU); the host masks' start / end rules;
 a tiny span model trains."""
+import re
 from collections import Counter
 
 import numpy as np
@@ -32,13 +33,27 @@ def test_shape(fsms):
     assert kinds[PTR_START] == 8 and kinds[PTR_END] == 8
 
 
+# round 6's glued card masks ("XX1234", "...1234", "XXXX XXXX XXXX 1234"): the span / copy
+# formats' word boundaries do not split letters or dots from digits, so these values are
+# not expressible there; the served qa format's are (tests/test_families.py
+# test_gold_answers_reachable_by_qa_decoder).  The autoregressive formats are kept for the
+# reference's own formats and the layouts of rounds 3-5.
+_GLUED_MASK = re.compile(r"(?:[xX]{2,4} ?|\.\.\.|…|(?:(?:XXXX|xxxx|\*\*\*\*) ){3})(\d{4})\b")
+
+
 @pytest.mark.parametrize("families", ["train", "heldout", None])
 def test_gold_answers_expressible_and_expand_to_copy_format(fsms, families):
     tk, f, fc = fsms
     bad = Counter()
     lens = []
+    skipped = 0
+    n = 0
     for s in generate(1200, seed=31, vocab_name="heldout", families=families):
         if s.answer is None:
+            continue
+        n += 1
+        if _GLUED_MASK.search(s.body):
+            skipped += 1
             continue
         b = normalize_body(s.body)
         enc = tk.encode_offsets([b])[0]
@@ -50,6 +65,7 @@ def test_gold_answers_expressible_and_expand_to_copy_format(fsms, families):
         lens.append(len(sp))
         assert f.expand_span_answer(sp, msg) == answer_tokens(tk, fc, s.answer, b, enc), s.body
     assert not bad, bad
+    assert skipped < 0.4 * n and (families is not None or skipped == 0), (skipped, n)
     assert np.mean(lens) <= 19  # vs ~36 answer tokens in copy format (scripts/span_sim.py)
 
 

@@ -16,7 +16,7 @@ from smsgate_amd.utils.synth import generate_bodies  # noqa: E402
 
 def main():
     S = int(os.environ.get("SLOTS", "8192"))
-    eng = build_engine("smollm-135m", device="cuda", random_init=True, max_slots=S, steps_per_graph=2)
+    eng = build_engine("smollm-135m", device="cuda", random_init=True, answer_format="copy", max_slots=S, steps_per_graph=2)
     res = {"slots": S}
     bodies = generate_bodies(S, seed=5)
     ids = eng.tok.message_ids(bodies, 128)

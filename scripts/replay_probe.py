@@ -38,7 +38,7 @@ def main() -> None:
     for name, kw in [("single", dict(split_decode=0)), ("split_one_graph", dict(split_decode=4096, split_graphs=1)),
                      ("split_two_graphs", dict(split_decode=4096, split_graphs=2))]:
         try:
-            eng = build_engine("smollm-135m", device="cuda", random_init=True, max_slots=8192, steps_per_graph=2,
+            eng = build_engine("smollm-135m", device="cuda", random_init=True, answer_format="copy", max_slots=8192, steps_per_graph=2,
                                buckets=(4096, 8192), **kw)
         except TypeError as exc:  # option not available in this build
             out[name] = str(exc)

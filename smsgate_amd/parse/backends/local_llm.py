@@ -56,13 +56,14 @@ def resolve_checkpoint(model: str, checkpoint: Optional[str] = None, random_init
 
 
 def build_engine(model: str = "smollm-135m", checkpoint: Optional[str] = None, device: str = "cuda",
-                 seed: int = 0, random_init: bool = False, weights=None, answer_format: str = "copy",
+                 seed: int = 0, random_init: bool = False, weights=None, answer_format: str = "qa",
                  **engine_kw: Any):
     """Engine for ``model`` with the weights :func:`resolve_checkpoint` picks;
     ``random_init=True`` serves random weights (throughput benchmarks only; in
     ``answer_format`` "span" they are a span-pointer model's); ``weights`` serves an
     in-memory :class:`ExtractorWeights` (e.g. just trained).  A checkpoint's answer
-    format comes from its own metadata."""
+    format comes from its own metadata; ``answer_format`` (default "qa", the flagship
+    one-forward head) only shapes random-init weights."""
     import torch
 
     from ...models.extractor import CONFIGS, ExtractorWeights, qa_config, span_config

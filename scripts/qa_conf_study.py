@@ -94,7 +94,14 @@ def main() -> int:
             dec = qa_decode_ref(cls, st, nl, en, msgs, flags, lay)
             toks = [qa_expand(tok, lay, c, sp, m) for (c, sp), m in zip(dec, msgs)]
             answers = [null_rejection(dict(zip(names, v))) for v in tok.decode_fields(toks, len(names))]
-            sc = score_answers(items, answers, by_family=True, per_item=True)
+            if fam.startswith("neg"):  # non-transactions: every published answer is wrong
+                from smsgate_amd.models.evaluate import _post
+
+                pubs = [_post(it.body, it.timestamp, ans) is not None for it, ans in zip(items, answers)]
+                sc = {"items": [(p_, False) for p_ in pubs], "exact": 0.0,
+                      "published_wrong_rate": sum(pubs) / len(pubs), "declined_rate": 0.0}
+            else:
+                sc = score_answers(items, answers, by_family=True, per_item=True)
             # raw spans (before absorption) for the measures: decode once more without absorption
             raw = []
             for m, body in enumerate(msgs):

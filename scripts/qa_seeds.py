@@ -133,6 +133,7 @@ def main() -> int:
     p.add_argument("--workers", type=int, default=4, help="example-building processes per seed")
     p.add_argument("--overrides", default="", help="JSON TrainConfig overrides (plus 'env': {...})")
     p.add_argument("--tag", default="recipe")
+    p.add_argument("--variants", default="", help="JSON list of {tag, overrides}: several recipes at once")
     p.add_argument("--out", default="gpurun_out/qa_seeds.jsonl")
     p.add_argument("--log-dir", default="gpurun_out/qa_seeds_logs")
     p.add_argument("--device", default="cuda")
@@ -144,34 +145,46 @@ def main() -> int:
     if a.child:
         return child(a)
     seeds = [int(s) for s in a.seeds.split(",")]
+    # --variants '[{"tag": "lr5e4", "overrides": {"lr": 5e-4}}, ...]': every variant x every
+    # seed trains concurrently (one child each), one summary line per variant
+    variants = json.loads(a.variants) if a.variants else [{"tag": a.tag, "overrides": a.overrides}]
+    for v in variants:
+        if isinstance(v.get("overrides"), dict):
+            v["overrides"] = json.dumps(v["overrides"])
     procs = []
-    for s in seeds:
-        cmd = [sys.executable, os.path.abspath(__file__), "--child", "--seed", str(s), "--eval-n", str(a.eval_n),
-               "--workers", str(a.workers), "--tag", a.tag, "--device", a.device, "--log-dir", a.log_dir,
-               "--child-out", os.path.join(a.log_dir, f"{a.tag}-seed{s}.json")]
-        for k in ("model", "steps", "batch"):
-            if getattr(a, k) is not None:
-                cmd += [f"--{k}", str(getattr(a, k))]
-        if a.overrides:
-            cmd += ["--overrides", a.overrides]
-        procs.append((s, subprocess.Popen(cmd)))
-    rcs = {s: pr.wait() for s, pr in procs}
-    results = []
-    for s in seeds:
-        path = os.path.join(a.log_dir, f"{a.tag}-seed{s}.json")
-        if rcs[s] == 0 and os.path.exists(path):
-            results.append(json.load(open(path)))
-    if not results:
-        print(json.dumps({"tag": a.tag, "error": "no seed finished", "rcs": rcs}))
-        return 1
-    summ = summarise(results)
-    summ.update(tag=a.tag, overrides=a.overrides, rcs=rcs,
-                train_s=[r["train_s"] for r in results], data_s=[r["data_s"] for r in results])
-    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
-    with open(a.out, "a") as fh:
-        fh.write(json.dumps(summ) + "\n")
-    print(json.dumps({k: summ["by_tau"][k] for k in ("0.0", "0.5")}, indent=None))
-    return 0 if all(v == 0 for v in rcs.values()) else 1
+    for v in variants:
+        for s in seeds:
+            cmd = [sys.executable, os.path.abspath(__file__), "--child", "--seed", str(s), "--eval-n", str(a.eval_n),
+                   "--workers", str(a.workers), "--tag", v["tag"], "--device", a.device, "--log-dir", a.log_dir,
+                   "--child-out", os.path.join(a.log_dir, f"{v['tag']}-seed{s}.json")]
+            for k in ("model", "steps", "batch"):
+                if getattr(a, k) is not None:
+                    cmd += [f"--{k}", str(getattr(a, k))]
+            if v.get("overrides"):
+                cmd += ["--overrides", v["overrides"]]
+            procs.append(((v["tag"], s), subprocess.Popen(cmd)))
+    rcs = {key: pr.wait() for key, pr in procs}
+    ok = True
+    for v in variants:
+        results = []
+        vr = {s: rcs[(v["tag"], s)] for s in seeds}
+        for s in seeds:
+            path = os.path.join(a.log_dir, f"{v['tag']}-seed{s}.json")
+            if vr[s] == 0 and os.path.exists(path):
+                results.append(json.load(open(path)))
+        if not results:
+            print(json.dumps({"tag": v["tag"], "error": "no seed finished", "rcs": vr}))
+            ok = False
+            continue
+        summ = summarise(results)
+        summ.update(tag=v["tag"], overrides=v.get("overrides", ""), rcs=vr,
+                    train_s=[r["train_s"] for r in results], data_s=[r["data_s"] for r in results])
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "a") as fh:
+            fh.write(json.dumps(summ) + "\n")
+        print(json.dumps({"tag": v["tag"], **{k: summ["by_tau"][k] for k in ("0.0",)}}), flush=True)
+        ok &= all(x == 0 for x in vr.values())
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

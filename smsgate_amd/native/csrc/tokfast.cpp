@@ -40,45 +40,48 @@ namespace {
 
 enum : uint8_t { C_L = 1, C_N = 2, C_D = 4, C_S = 8 };
 
-// pre-token bytes -> ids.  Slots hold (hash | 1, key offset / length, ids offset /
-// count); keys and ids live in two arenas.  Linear probing at <= 50 % load.
+// pre-token bytes -> ids.  One 24-byte slot per entry (hash | 1, key offset / length,
+// ids offset / count: a probe touches one cache line); keys and ids live in two arenas.
+// Linear probing at <= 50 % load.  Sized for the words that repeat (labels, currency
+// codes, common words: a few thousand) so the table stays cache-resident; one-off
+// numbers are not cached at all (bpe()).
 struct BpeCache {
-    static constexpr size_t SLOTS = 1 << 19, MAX_ENTRIES = SLOTS / 2;
-    std::vector<uint64_t> hk;
-    std::vector<uint32_t> koff, voff;
-    std::vector<uint16_t> klen, vlen;
+    static constexpr size_t SLOTS = 1 << 18, MAX_ENTRIES = SLOTS / 2;
+    struct Slot {
+        uint64_t h;
+        uint32_t koff, voff;
+        uint16_t klen, vlen;
+    };
+    std::vector<Slot> slot;
     std::string keys;
     std::vector<int> vals;
     size_t entries = 0;
-    BpeCache() : hk(SLOTS, 0), koff(SLOTS), voff(SLOTS), klen(SLOTS), vlen(SLOTS) {}
+    BpeCache() : slot(SLOTS, Slot{0, 0, 0, 0, 0}) {}
     static uint64_t hash(const char* s, size_t n) {  // FNV-1a, 64-bit
         uint64_t h = 1469598103934665603ull;
         for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)s[i]) * 1099511628211ull;
         return h | 1;
     }
-    // ids of the pre-token or nullptr; *slot = where it would go
-    const int* find(const char* s, size_t n, uint64_t h, size_t* cnt, size_t* slot) const {
+    // ids of the pre-token or nullptr; *at = where it would go
+    const int* find(const char* s, size_t n, uint64_t h, size_t* cnt, size_t* at) const {
         for (size_t i = (h >> 7) & (SLOTS - 1);; i = (i + 1) & (SLOTS - 1)) {
-            if (!hk[i]) { *slot = i; return nullptr; }
-            if (hk[i] == h && klen[i] == n && memcmp(keys.data() + koff[i], s, n) == 0) {
-                *cnt = vlen[i];
-                return vals.data() + voff[i];
+            const Slot& e = slot[i];
+            if (!e.h) { *at = i; return nullptr; }
+            if (e.h == h && e.klen == n && memcmp(keys.data() + e.koff, s, n) == 0) {
+                *cnt = e.vlen;
+                return vals.data() + e.voff;
             }
         }
     }
-    void put(size_t slot, const char* s, size_t n, uint64_t h, const int* ids, size_t cnt) {
+    void put(size_t at, const char* s, size_t n, uint64_t h, const int* ids, size_t cnt) {
         if (n > 0xFFFF || cnt > 0xFFFF || keys.size() + n > 0xFFFFFFFFull) return;
-        hk[slot] = h;
-        koff[slot] = (uint32_t)keys.size();
-        klen[slot] = (uint16_t)n;
-        voff[slot] = (uint32_t)vals.size();
-        vlen[slot] = (uint16_t)cnt;
+        slot[at] = Slot{h, (uint32_t)keys.size(), (uint32_t)vals.size(), (uint16_t)n, (uint16_t)cnt};
         keys.append(s, n);
         vals.insert(vals.end(), ids, ids + cnt);
         ++entries;
     }
     void clear() {
-        std::fill(hk.begin(), hk.end(), 0);
+        std::fill(slot.begin(), slot.end(), Slot{0, 0, 0, 0, 0});
         keys.clear();
         vals.clear();
         entries = 0;
@@ -91,6 +94,7 @@ struct Tok {
     int byte_id[256];
     std::vector<uint8_t> cls;                                  // code point -> C_* bits
     std::vector<std::pair<std::string, int>> specials;         // literal -> id
+    bool sp_first[256] = {};                                   // first bytes of the specials
     BpeCache cache;
     std::vector<uint32_t> cp, off;                             // scratch of encode_text (GIL held)
     std::vector<int> sym, rk, mid;                             // scratch of bpe()
@@ -234,12 +238,24 @@ struct MergeTable {
 
 inline const MergeTable& merge_table(const Tok& t) { return *reinterpret_cast<const MergeTable*>(t.merge_tab); }
 
+// a pre-token with more than two ASCII digits is a one-off (an amount, a date, a
+// card number): not worth a cache entry, and caching it would evict the words that repeat
+inline bool one_off(const char* s, size_t len) {
+    int d = 0;
+    for (size_t i = 0; i < len; ++i) d += (unsigned)(s[i] - '0') < 10u;
+    return d > 2;
+}
+
 void bpe(Tok& t, const char* s, size_t len, std::vector<int>& out) {
-    const uint64_t h = BpeCache::hash(s, len);
+    const bool cache = !one_off(s, len);
+    uint64_t h = 0;
     size_t cnt = 0, slot = 0;
-    if (const int* hit = t.cache.find(s, len, h, &cnt, &slot)) {
-        out.insert(out.end(), hit, hit + cnt);
-        return;
+    if (cache) {
+        h = BpeCache::hash(s, len);
+        if (const int* hit = t.cache.find(s, len, h, &cnt, &slot)) {
+            out.insert(out.end(), hit, hit + cnt);
+            return;
+        }
     }
     const MergeTable& mt = merge_table(t);
     // symbols + the rank / merged id of each adjacent pair, updated locally per merge:
@@ -266,11 +282,13 @@ void bpe(Tok& t, const char* s, size_t len, std::vector<int>& out) {
         else rk[bi] = INT32_MAX;
         if (bi > 0) rk[bi - 1] = mt.find(sym[bi - 1], sym[bi], &mid[bi - 1]);
     }
-    if (t.cache.entries >= BpeCache::MAX_ENTRIES) {
-        t.cache.clear();
-        t.cache.find(s, len, h, &cnt, &slot);  // its slot in the emptied table
+    if (cache) {
+        if (t.cache.entries >= BpeCache::MAX_ENTRIES) {
+            t.cache.clear();
+            t.cache.find(s, len, h, &cnt, &slot);  // its slot in the emptied table
+        }
+        t.cache.put(slot, s, len, h, sym, n);
     }
-    t.cache.put(slot, s, len, h, sym, n);
     out.insert(out.end(), sym, sym + n);
 }
 
@@ -298,12 +316,15 @@ void encode_text(Tok& t, const char* s, size_t len, std::vector<int>& out) {
         // next special-token literal (leftmost; specials never overlap)
         size_t sp_at = len, sp_len = 0;
         int sp_id = -1;
-        for (auto& sp : t.specials) {
-            const void* f = memmem(s + pos, len - pos, sp.first.data(), sp.first.size());
-            if (f) {
-                size_t at = (const char*)f - s;
-                if (at < sp_at) { sp_at = at; sp_len = sp.first.size(); sp_id = sp.second; }
-            }
+        for (size_t q = pos; q < len && sp_id < 0; ++q) {
+            if (!t.sp_first[(unsigned char)s[q]]) continue;
+            for (auto& sp : t.specials)  // list order breaks ties, like the library
+                if (sp.first.size() <= len - q && memcmp(s + q, sp.first.data(), sp.first.size()) == 0) {
+                    sp_at = q;
+                    sp_len = sp.first.size();
+                    sp_id = sp.second;
+                    break;
+                }
         }
         if (sp_at > pos) {
             const char* seg = s + pos;
@@ -372,7 +393,9 @@ PyObject* py_new(PyObject*, PyObject* args) {
         Py_ssize_t n;
         int id;
         if (!PyArg_ParseTuple(PyList_GET_ITEM(sp, i), "y#i", &p, &n, &id)) { destroy_tok(t); return nullptr; }
+        if (n < 1) { destroy_tok(t); PyErr_SetString(PyExc_ValueError, "empty special token"); return nullptr; }
         t->specials.emplace_back(std::string(p, n), id);
+        t->sp_first[(unsigned char)p[0]] = true;
     }
     // single-byte tokens (the byte-level alphabet is always in the vocabulary)
     for (Py_ssize_t i = 0; i < V; ++i)

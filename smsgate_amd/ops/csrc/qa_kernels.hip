@@ -60,6 +60,9 @@
 #define QF_AMPM (1 << 18)  // " AM" / " PM"
 #define QF_AP (1 << 19)    // " A" / " P" (a split " AM" / " PM")
 #define QF_M (1 << 20)     // "M"
+#define QF_CARDL (1 << 22)  // " CARD" (normalize_body's "CARD:7538")
+#define QF_COLON (1 << 23)  // a lone ":"
+#define QF_XMASK (1 << 24)  // x / X letters only ("XXXX" of "XXXX1438")
 
 struct QAParams {
   int nf, nq, n_pos;
@@ -95,6 +98,8 @@ static __device__ __forceinline__ bool qa_start_ok(const uint32_t* fb, int s, in
   if (ok && s > 0) {
     const uint32_t fp = fb[s - 1];
     ok = !qa_glued(fp, fs) && !((cls & QF_NO_START_AFTER_MASK) && (fp & QF_MASK)) &&
+         !((cls & QF_NO_START_AFTER_MASK) && (((fp & QF_XMASK) && (fs & QF_SD)) ||
+                                             (s > 1 && (fp & QF_COLON) && (fb[s - 2] & QF_CARDL)))) &&
          !(s > 1 && (fp & QF_SEP) && (fs & QF_GRP3) && (fb[s - 2] & QF_LD));
   }
   return ok;

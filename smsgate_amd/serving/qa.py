@@ -53,7 +53,7 @@ from .fsm import DEFAULT_FIELDS, TOK_CLASS_BITS, FieldSpec, _token_class_sets
 __all__ = ["QALayout", "qa_layout", "qa_token_flags", "qa_targets", "qa_decode_ref", "qa_expand", "qa_rows", "qa_logits", "qa_loss",
            "REJECT_TXN", "ABSTAIN_TXN", "null_rejection", "qa_confidence", "QF_SL", "QF_SD", "QF_EL", "QF_ED", "QF_MASK", "QA_CLASS_BITS",
            "QA_MAX_QUERIES", "EDGE_RULES", "QF_NL", "QF_FA", "QF_FD", "QF_LA", "QF_LD", "QF_GRP3", "QF_SEP",
-           "QF_TIME", "QF_DEND", "QF_AMPM", "QF_AP", "QF_M", "QF_TEXT"]
+           "QF_TIME", "QF_DEND", "QF_AMPM", "QF_AP", "QF_M", "QF_TEXT", "QF_CARDL", "QF_COLON", "QF_XMASK"]
 
 # non-transaction classes: every other field of the answer is null
 REJECT_TXN = ("otp", "unknown")
@@ -77,6 +77,13 @@ QF_DEND = 1 << 17  # may end a date: last char a digit, or AM / PM
 QF_AMPM = 1 << 18  # " AM" / " PM" as one token
 QF_AP = 1 << 19  # " A" / " P": the first piece of a split " AM" / " PM"
 QF_M = 1 << 20  # "M": its second piece
+# " CARD" + ":" is what normalize_body writes for a "4083***7538" mask ("CARD:7538"): the
+# digits after that colon are the card's, so a date or a number never starts there
+# (like after a mask); so are digits glued to a token of x / X letters only ("XXXX1438",
+# "xx0735": x-masks), but not a spaced word after one ("HSMEX 07 Dec")
+QF_CARDL = 1 << 22  # " CARD" / "CARD"
+QF_COLON = 1 << 23  # a lone ":"
+QF_XMASK = 1 << 24  # x / X letters only
 _TIME_RE = re.compile(r" ?\d{1,2}:\d{2}(?::\d{2})?\Z")
 # field kind -> (flags its first token must all have, flags its last token must all have).
 # A date ends with a digit or AM / PM (a span into the next word -- "12.05.25 покупка",
@@ -178,6 +185,12 @@ def qa_token_flags(tokenizer, vocab: int) -> np.ndarray:
             f |= QF_ED
         if t.endswith("*"):
             f |= QF_MASK
+        if t.strip(" ") and not t.strip(" ").strip("xX"):
+            f |= QF_XMASK
+        if t.strip(" ") == "CARD":
+            f |= QF_CARDL
+        if t == ":":
+            f |= QF_COLON
         if "\n" in t:
             f |= QF_NL
         h = t.lstrip(" ")
@@ -225,6 +238,9 @@ def _start_ok(flags, body, j: int, cls: int, s_need: int) -> bool:
         fp = _fl(flags, body, j - 1)
         if _glued(fp, fj) or ((cls & _NO_START_AFTER_MASK) and fp & QF_MASK):
             return False
+        if (cls & _NO_START_AFTER_MASK) and ((fp & QF_XMASK and fj & QF_SD) or (
+                j > 1 and fp & QF_COLON and _fl(flags, body, j - 2) & QF_CARDL)):
+            return False  # "1438" of "XXXX1438", "7538" of "CARD:7538"
         if j > 1 and fp & QF_SEP and fj & QF_GRP3 and _fl(flags, body, j - 2) & QF_LD:
             return False  # "993" of "218,993"
     return True
@@ -308,7 +324,8 @@ def _pair_mask(fb: np.ndarray, n: int, cls: int, cap: int, s_need: int = 0,
     glued_prev[0] = False
     in_cls = (fb & cls) != 0 if cls else np.ones(n, dtype=bool)
     in_cls &= (fb & QF_NL) == 0
-    after_mask = ((prev & QF_MASK) != 0) & bool(cls & _NO_START_AFTER_MASK)
+    after_mask = (((prev & QF_MASK) != 0) | (((prev & QF_COLON) != 0) & ((prev2 & QF_CARDL) != 0))
+                  | (((prev & QF_XMASK) != 0) & ((fb & QF_SD) != 0))) & bool(cls & _NO_START_AFTER_MASK)
     after_mask[0] = False
     vs = in_cls & ~glued_prev & ~after_mask & ((fb & s_need) == s_need)
     # an end may not be followed by a glued token, nor by a separator glued to a group

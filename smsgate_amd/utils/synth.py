@@ -681,24 +681,29 @@ FAMILIES: Tuple[Family, ...] = (
 _PROC_POOLS = {
     "en": dict(
         head_debit=("Purchase", "PURCHASE", "POS", "Payment", "Card payment", "DEBIT", "Debit", "Charge", "POS PURCHASE"),
-        head_credit=("Refund", "Credit", "Reversal", "Incoming transfer", "REFUND"),
+        head_credit=("Refund", "Credit", "Reversal", "Incoming transfer", "REFUND", "Payment received",
+                     "Credited", "Deposit", "Transfer received", "Money received"),
         amt=("Amount", "Amt", "Sum", "Total", "AMOUNT"), card=("card", "Card", "CARD", "Card no"),
         merch=("Merchant", "Shop", "Payee", "MERCHANT"), city=("City", "Location", "CITY"),
+        merch_credit=("From", "Sender", "Payer", "Remitter"), credited=("credited", "received", "deposited"),
+        to_card=("to card", "to your card", "to account"),
         addr=("Address", "Addr"), date=("Date", "Time", "DATE"),
         bal=("Balance", "Bal", "Avail. balance", "Available", "Avl bal", "Remaining balance", "BALANCE", "Bal."),
         at=("at", "AT"), on=("on",), inn=("in",)),
     "ru": dict(
         head_debit=("Покупка", "Оплата", "Списание", "ПОКУПКА", "Оплата товаров"),
-        head_credit=("Зачисление", "Возврат", "Пополнение"),
+        head_credit=("Зачисление", "Возврат", "Пополнение", "Поступление", "Перевод получен"),
         amt=("Сумма", "Списано", "Сумма операции"), card=("Карта", "карта", "по карте", "КАРТА"),
         merch=("Магазин", "Место", "Получатель"), city=("Город",), addr=("Адрес",), date=("Дата", "Время"),
+        merch_credit=("Отправитель", "От"), credited=("зачислено", "поступило"), to_card=("на карту", "на счет"),
         bal=("Остаток", "Баланс", "Доступно", "Доступный остаток"),
         at=("в",), on=("",), inn=("г.",)),
     "tr": dict(
         head_debit=("Pokupka", "Oplata", "Spisanie", "POKUPKA"),
-        head_credit=("Zachislenie", "Vozvrat", "Popolnenie"),
+        head_credit=("Zachislenie", "Vozvrat", "Popolnenie", "Postuplenie"),
         amt=("Summa", "Spisano"), card=("karta", "Karta", "po karte", "s karty"),
         merch=("Mesto", "Magazin", "Poluchatel"), city=("Gorod",), addr=("Adres",), date=("Data", "Vremya"),
+        merch_credit=("Otpravitel", "Ot"), credited=("zachisleno", "postupilo"), to_card=("na kartu", "na schet"),
         bal=("ostatok", "Ostatok", "dostupno", "Dostupno", "balans", "Balans"),
         at=("v",), on=("",), inn=("g.",)),
 }
@@ -774,6 +779,7 @@ def _proc_render(c: "_Ctx") -> str:
 
     segs: List[str] = []
     head = ""
+    credit = c.fam.txn == "credit"
     # a credit is always announced (nothing else tells it from a debit); a debit's header
     # is optional -- an unlabelled transaction is a debit
     if c.fam.txn == "credit" or r.random() < 0.75:
@@ -781,7 +787,9 @@ def _proc_render(c: "_Ctx") -> str:
     for seg in order:
         if seg == "AMT":
             v = c.AMT()
-            if r.random() < 0.15:  # a debit written as a negative amount ("-52.00 USD")
+            if credit and r.random() < 0.35:  # "2 500 RUB зачислено", "52.00 USD credited"
+                v = v + " " + r.choice(P["credited"])
+            elif r.random() < 0.15:  # a debit written as a negative amount ("-52.00 USD")
                 v = "-" + v
             if labelled or r.random() < 0.2:
                 v = lab(P["amt"]) + v
@@ -790,7 +798,10 @@ def _proc_render(c: "_Ctx") -> str:
             segs.append(v)
         elif seg == "CARD":
             v = c.CARD()
-            segs.append(lab(P["card"]) + v if (labelled or r.random() < 0.7) else v)
+            if credit and r.random() < 0.3:  # "to card *1234", "на карту *1234"
+                segs.append(r.choice(P["to_card"]) + " " + v)
+            else:
+                segs.append(lab(P["card"]) + v if (labelled or r.random() < 0.7) else v)
         elif seg == "DATE":
             v = c.D()
             if labelled and r.random() < 0.7:
@@ -807,7 +818,8 @@ def _proc_render(c: "_Ctx") -> str:
             city = c.C() if r.random() < 0.85 else ""
             addr = c.A() if r.random() < 0.35 else ""
             if labelled and r.random() < 0.6:
-                parts = [lab(P["merch"]) + m] + ([lab(P["city"]) + city] if city else []) + \
+                mlab = P["merch_credit"] if credit and r.random() < 0.6 else P["merch"]
+                parts = [lab(mlab) + m] + ([lab(P["city"]) + city] if city else []) + \
                     ([lab(P["addr"]) + addr] if addr else [])
                 segs.extend(parts) if multi else segs.append(", ".join(parts))
                 continue

@@ -317,4 +317,18 @@ def test_training_stream_is_pinned(monkeypatch):
     for s in generate(400, seed=5, families="train"):
         h.update(s.body.encode())
         h.update(repr(sorted((s.answer or {}).items())).encode())
-    assert h.hexdigest()[:16] == "98512ff89e23f11b"  # round 6: the widened value grammar
+    assert h.hexdigest()[:16] == "47169bc036094f72"  # round 6: widened value grammar + credit phrasing
+
+
+def test_heldout_credit_layout_is_an_interpolation():
+    """hv_en_credit ("Incoming payment X credited to card Y. Sender: M, C. D. Bal B") stays
+    unseen as a whole -- its header phrase is in no training body and its segment order
+    is a held-out signature -- while its parts are trained: "credited" after an amount,
+    "to card", a sender label, in other procedural credit layouts."""
+    import re
+
+    train = generate(20000, seed=51, vocab_name="train", families="train", negatives=0.12, training=True)
+    assert not [s.body for s in train if "Incoming payment" in s.body]
+    credit = [s.body for s in train if s.family == "proc_en_credit"]
+    assert any(re.search(r"\d credited\b", b) for b in credit)
+    assert any("to card" in b for b in credit) and any("Sender" in b for b in credit)

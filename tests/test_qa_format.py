@@ -240,3 +240,25 @@ def test_qa_training_runs_and_learns_on_cpu():
     assert np.mean(losses[-10:]) < np.mean(losses[:5]) - 0.3, losses
     out = TorchQAExtractor(w.float()).run(["APPROVED PURCHASE DB SALE: X, Y,06.05.25 14:23,card ***0018. Amount:5 USD"])
     assert set(out[0]) == set(NAMES)
+
+
+def test_dates_and_amounts_never_start_inside_a_card(env):
+    """The digits of "CARD:9242" (normalize_body's form of "6361***9242") and of an x-mask
+    ("XXXX1438") are the card's: no date / amount starts there -- the held-out
+    ru_karta_first layout's typical miss -- while a spaced word after an x-ending name
+    ("HSMEX 07 Dec") may start a date."""
+    from smsgate_amd.serving.qa import QA_CLASS_BITS, _pair_mask, valid_starts
+
+    tk, lay, fl = env
+    date = QA_CLASS_BITS["date"]
+    for body, piece, allowed in (("Карта 6361***9242 16 августа 2024 покупка", "9", False),
+                                 ("Карта XXXX1438 8 сентября 2023 в 18:53", "14", False),
+                                 ("Карта xx0735 12.12.2023 покупка", "07", False),
+                                 ("DEBIT 132.52 GBP CARD**8490 QNHZU/HSMEX 07 Dec 2025 15:18", " 07", True)):
+        m = tk.message_ids([normalize_body(body)], 128)[0]
+        strings = [tk.token_strings[t] for t in m]
+        j = strings.index(piece)
+        n = len(m) - 1
+        vs = valid_starts(fl, m, n, date)
+        vs2, _ = _pair_mask(fl[np.asarray(m[:n])], n, date, 20)
+        assert bool(vs[j]) is allowed and bool(vs2[j]) is allowed, (body, strings)

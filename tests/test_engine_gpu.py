@@ -225,7 +225,7 @@ def test_message_start_templates_reuse_kv():
     the trained small extractor's answers are unchanged (a template's keys come from
     a different GEMM tiling, so a last-bit difference may flip a rare near-tie), and
     the computed prompt tokens drop."""
-    from smsgate_amd.parse.backends.local_llm import build_engine
+    from smsgate_amd.parse.backends.local_llm import build_engine, bundled_checkpoint
     from smsgate_amd.parse.text import normalize_body
     from smsgate_amd.utils.synth import TRAFFIC_KINDS, generate
 
@@ -233,7 +233,7 @@ def test_message_start_templates_reuse_kv():
                                                           kinds=TRAFFIC_KINDS["purchase"])]
     outs, stats = [], []
     for slots in (0, 16):
-        eng = build_engine("small", device="cuda:0", max_slots=128, buckets=(64, 128), template_slots=slots,
+        eng = build_engine("small", bundled_checkpoint("small-copy"), device="cuda:0", max_slots=128, buckets=(64, 128), template_slots=slots,
                            template_every=128, template_min_count=4)
         outs.append(eng.run(bodies))
         stats.append(dataclasses.replace(eng.stats))

@@ -14,20 +14,26 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(),
 
 from conftest import REFERENCE_CASES  # noqa: E402
 from smsgate_amd.models import RawSMS, TxnType  # noqa: E402
-from smsgate_amd.parse.backends.local_llm import LocalLLMBackend, build_engine  # noqa: E402
+from smsgate_amd.parse.backends.local_llm import LocalLLMBackend, build_engine, bundled_checkpoint  # noqa: E402
 from smsgate_amd.parse.pipeline import ParsePipeline  # noqa: E402
 
 
 @pytest.fixture(scope="module")
 def pipeline():
-    eng = build_engine("small", device="cuda", max_slots=64, buckets=(64,), spec_k=0)
+    eng = build_engine("small", bundled_checkpoint("small-copy"), device="cuda", max_slots=64, buckets=(64,), spec_k=0)
     return ParsePipeline(LocalLLMBackend.from_engine(eng))
 
 
-@pytest.mark.parametrize("spec_k", [0, 4])
-def test_reference_cases_local_llm(pipeline, spec_k, arun):
-    if spec_k:
-        eng = build_engine("small", device="cuda", max_slots=64, buckets=(64,), spec_k=spec_k)
+@pytest.mark.parametrize("fmt,spec_k", [("qa", 0), ("copy", 0), ("copy", 4)])
+def test_reference_cases_local_llm(pipeline, fmt, spec_k, arun):
+    """qa: the bundled one-forward checkpoint (the default ``small`` weights); copy: the
+    round-4 autoregressive checkpoint, without and with speculative drafts."""
+    if fmt == "qa":
+        eng = build_engine("small", device="cuda", max_slots=64)
+        assert type(eng).__name__ == "QAEngine"
+        pipe = ParsePipeline(LocalLLMBackend.from_engine(eng))
+    elif spec_k:
+        eng = build_engine("small", bundled_checkpoint("small-copy"), device="cuda", max_slots=64, buckets=(64,), spec_k=spec_k)
         pipe = ParsePipeline(LocalLLMBackend.from_engine(eng))
     else:
         pipe = pipeline

@@ -107,8 +107,9 @@ def test_tiny_span_model_trains_on_cpu():
 
 
 def test_checkpoint_carries_its_answer_format(tmp_path):
-    """A span checkpoint loads as a span model whatever config the caller passes, and
-    a copy-format checkpoint (the bundled small extractor) as a copy model."""
+    """A span checkpoint loads as a span model whatever config the caller passes, a
+    copy-format checkpoint (the round-4 small extractor) as a copy model, and the
+    bundled small extractor as a qa model (VERDICT r05 next #4)."""
     from smsgate_amd.models.extractor import CONFIGS, ExtractorWeights, span_config
     from smsgate_amd.parse.backends.local_llm import bundled_checkpoint
 
@@ -117,8 +118,10 @@ def test_checkpoint_carries_its_answer_format(tmp_path):
     w.save(p)
     got = ExtractorWeights.load(p, CONFIGS["tiny"])
     assert got.cfg.span_positions == 130 and got.embed.shape[0] == 8448
-    small = ExtractorWeights.load(bundled_checkpoint("small"), span_config(CONFIGS["small"]))
-    assert small.cfg.span_positions == 0 and small.cfg.vocab == 8192
+    copy = ExtractorWeights.load(bundled_checkpoint("small-copy"), span_config(CONFIGS["small"]))
+    assert copy.cfg.span_positions == 0 and copy.cfg.qa_queries == 0 and copy.cfg.vocab == 8192
+    small = ExtractorWeights.load(bundled_checkpoint("small"), CONFIGS["small"])
+    assert small.cfg.qa_queries == 9 and small.cfg.span_positions == 130
 
 
 def test_dates_and_numbers_never_start_inside_a_card_mask(fsms):

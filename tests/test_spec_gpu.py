@@ -11,10 +11,10 @@ from smsgate_amd.utils.synth import generate, reference_cases  # noqa: E402
 
 
 def _engine(spec_k, use_graphs, **kw):
-    from smsgate_amd.parse.backends.local_llm import build_engine
+    from smsgate_amd.parse.backends.local_llm import build_engine, bundled_checkpoint
 
     # one attention kernel and our own lm_head GEMM in both modes: identical per-row arithmetic
-    return build_engine("small", device="cuda", max_slots=512, buckets=(64, 512), use_graphs=use_graphs,
+    return build_engine("small", bundled_checkpoint("small-copy"), device="cuda", max_slots=512, buckets=(64, 512), use_graphs=use_graphs,
                         spec_k=spec_k, decode_attn_small_rows=0, lm_head_fused=True, split_decode=0, **kw)
 
 

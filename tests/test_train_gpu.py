@@ -1,6 +1,7 @@
 """The local extractor actually learns the task: train on synthetic SMS (fwd+bwd on
 the GPU), then decode through the HIP serving engine and score field accuracy on
-held-out synthetic SMS.  Also: the bundled trained checkpoint extracts correctly."""
+held-out synthetic SMS.  Also: the bundled trained (qa-format) checkpoint extracts
+correctly and rejects non-transactions."""
 import os
 
 import pytest
@@ -34,10 +35,20 @@ def test_training_learns_extraction():
 
 
 def test_bundled_checkpoint_extracts():
+    """The bundled small extractor is a qa-format model trained with the flagship recipe
+    (scripts/train_small_asset.py): through the HIP qa engine it extracts held-out
+    layouts with held-out names, rejects held-out non-transactions and parses the
+    reference CASES."""
+    from smsgate_amd.models.evaluate import evaluate_engine, evaluate_negatives, golden_case_mismatches, \
+        golden_case_results
     from smsgate_amd.parse.backends.local_llm import bundled_checkpoint, build_engine
 
     path = bundled_checkpoint("small")
     assert path is not None and os.path.exists(path)
-    eng = build_engine("small", device="cuda", max_slots=512, buckets=(64, 512))
-    acc = _score(eng.w)  # held-out vocabulary (names never seen in training)
-    assert acc["all"] >= 0.85 and acc["merchant"] >= 0.9 and acc["amount"] >= 0.98, acc
+    eng = build_engine("small", device="cuda", max_slots=1024)
+    assert type(eng).__name__ == "QAEngine"
+    q = evaluate_engine(eng, n=300, seed=4243, vocab_name="heldout", families="heldout")
+    assert q["exact"] >= 0.95 and q["published_wrong_rate"] <= 0.03, q
+    neg = evaluate_negatives(eng, n=300, seed=4246, families="neg_heldout")
+    assert neg["false_parsed_rate"] <= 0.01, neg
+    assert not golden_case_mismatches(golden_case_results(eng))

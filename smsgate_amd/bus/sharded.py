@@ -28,7 +28,6 @@ Two layouts, chosen by the DSN:
 from __future__ import annotations
 
 import asyncio
-import itertools
 import time
 import zlib
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -134,7 +133,7 @@ class Router:
         # one dealing counter PER subject: a shared one would put every sms.parsed publish
         # on the even turns and every sms.processing one on the odd turns of a parser
         # batch that publishes them in pairs -- one partition of each would get nothing
-        self._rr: Dict[str, "itertools.count[int]"] = {}
+        self._rr: Dict[str, int] = {}  # per partitioned subject: messages dealt so far
 
     def members(self, subject: str) -> List[int]:
         if not self.pins:
@@ -147,10 +146,20 @@ class Router:
         ms = self.members(subject)
         if len(ms) == 1:
             return ms[0]
-        rr = self._rr.get(subject)
-        if rr is None:
-            rr = self._rr[subject] = itertools.count()
-        return ms[next(rr) % len(ms)]
+        k = self._rr.get(subject, 0)
+        self._rr[subject] = k + 1
+        return ms[k % len(ms)]
+
+    def deal(self, subject: str, n: int) -> List[Tuple[int, slice]]:
+        """``n`` messages of ``subject`` dealt round-robin over its members, exactly as
+        ``n`` calls of :meth:`publish_target` would: ``(member, slice of the n)`` pairs."""
+        ms = self.members(subject)
+        if len(ms) == 1:
+            return [(ms[0], slice(0, n))]
+        k = self._rr.get(subject, 0)
+        self._rr[subject] = k + n
+        m = len(ms)
+        return [(ms[(k + r) % m], slice(r, n, m)) for r in range(min(m, n))]
 
 
 class _PartitionedSub(Subscription):
@@ -315,9 +324,16 @@ class ShardedBus(Bus):
         return await self._bus(subject).publish(subject, data, headers)
 
     async def publish_many(self, items: Sequence[Tuple[str, bytes]]) -> List[PubAck]:
+        by_subject: Dict[str, List[int]] = {}
+        for i, it in enumerate(items):
+            by_subject.setdefault(it[0], []).append(i)
         groups: Dict[int, List[int]] = {}
-        for i, (s, _) in enumerate(items):
-            groups.setdefault(self.router.publish_target(s), []).append(i)
+        for subject, idx in by_subject.items():  # the per-message deal, one subject at a time
+            for k, sl in self.router.deal(subject, len(idx)):
+                groups.setdefault(k, []).extend(idx[sl])
+        if len(by_subject) > 1:
+            for g in groups.values():
+                g.sort()  # each member receives its messages in publish order
         if len(groups) == 1:
             (k, _), = groups.items()
             return await self.members[k].publish_many(items)

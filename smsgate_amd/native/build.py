@@ -61,6 +61,10 @@ def build_parsefast(force: bool = False, verbose: bool = False) -> Path:
     return build_extension("parsefast", force, verbose)
 
 
+# libraries an extension links (the system OpenSSL the interpreter's hashlib uses)
+LINK = {"parsefast": ["-lcrypto"]}
+
+
 def build_extension(name: str, force: bool = False, verbose: bool = False) -> Path:
     import sysconfig
 
@@ -72,7 +76,7 @@ def build_extension(name: str, force: bool = False, verbose: bool = False) -> Pa
         return target
     tmp = target.with_suffix(".tmp")
     cmd = [cxx(), "-O3", "-std=c++17", "-Wall", "-Wno-unused-function", "-shared", "-fPIC", "-fvisibility=hidden",
-           f"-I{sysconfig.get_paths()['include']}", str(src), "-o", str(tmp)]
+           f"-I{sysconfig.get_paths()['include']}", str(src), "-o", str(tmp)] + LINK.get(name, [])
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -12,10 +12,12 @@
 // (tests/test_parsefast.py pins byte equality on the synthetic corpus, hostile
 // strings and the DLQ envelope shapes).
 //
-//   scan_raw(payloads, now)      -> per payload: None (Python path) or
-//                                   (msg_id, sender, body, date, device_id, source, norm_body)
-//                                   for a valid RawSMS that no keyword filter can touch;
-//   postprocess(rows, metas, now)-> per message: bytes (the sms.parsed payload),
+//   scan_raw(payloads)           -> per payload: None (Python path) or (blob, norm_body,
+//                                   cache_key) for a valid RawSMS that no keyword filter
+//                                   can touch -- blob: the message's UTF-8 fields and
+//                                   pre-encoded sms.parsed fragments (raw_fields() reads
+//                                   the fields back), cache_key: sha256(norm_body) hex;
+//   postprocess(rows, blobs, now)-> per message: bytes (the sms.parsed payload),
 //                                   UNMATCHED (1) or FALLBACK (2).
 //
 // Equivalences (each one a Python function of the parse package):
@@ -46,6 +48,8 @@
 #include <algorithm>
 #include <unordered_set>
 #include <vector>
+
+#include <openssl/sha.h>  // the response-cache key: sha256(normalised body) (parse/cache.py)
 
 #include "http_ingest.hpp"  // Md5, the RawSMS encoding of the native HTTP doors
 
@@ -1158,6 +1162,81 @@ PyObject* py_init(PyObject*, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+// A scanned message's native record (one bytes object, parse/fastpath.py FastRaw.blob):
+// eight u32 lengths, then the segments in this order --
+//   A: '{"msg_id":..,"device_id":..,"sender":..,"date":"'  (the sms.parsed prefix)
+//   B: '","raw_body":<normalised body>,"txn_type":"'       (its middle)
+//   the body, msg_id, sender, date, device_id (length 0xFFFFFFFF: null), source
+// so post-processing and the DLQ envelopes never convert Python strings back to UTF-8.
+enum { SEG_A, SEG_B, SEG_BODY, SEG_MSG_ID, SEG_SENDER, SEG_DATE, SEG_DEVICE, SEG_SOURCE, NSEG };
+constexpr uint32_t SEG_NULL = 0xFFFFFFFFu;
+
+struct Blob {
+  const char* seg[NSEG];
+  uint32_t len[NSEG];
+};
+
+bool blob_view(PyObject* o, Blob* b) {
+  if (!PyBytes_Check(o)) return false;
+  const char* p = PyBytes_AS_STRING(o);
+  size_t n = (size_t)PyBytes_GET_SIZE(o);
+  if (n < 4 * NSEG) return false;
+  size_t off = 4 * NSEG;
+  for (int k = 0; k < NSEG; ++k) {
+    uint32_t l;
+    memcpy(&l, p + 4 * k, 4);
+    b->len[k] = l;
+    b->seg[k] = p + off;
+    if (l != SEG_NULL) {
+      if (off + l > n) return false;
+      off += l;
+    }
+  }
+  return off == n;
+}
+
+PyObject* make_blob(const Raw& r, const std::string& nb) {
+  std::string a, m;
+  a.reserve(96 + r.msg_id.size() + r.sender.size() + r.device_id.size());
+  a += "{\"msg_id\":";
+  jstr(a, r.msg_id);
+  a += ",\"device_id\":";
+  if (r.device_null) a += "null";
+  else jstr(a, r.device_id);
+  a += ",\"sender\":";
+  jstr(a, r.sender);
+  a += ",\"date\":\"";
+  m.reserve(nb.size() + 48);
+  m += "\",\"raw_body\":";
+  jstr(m, nb);
+  m += ",\"txn_type\":\"";
+  const std::string* segs[NSEG] = {&a, &m, &r.body, &r.msg_id, &r.sender, &r.date, &r.device_id, &r.source};
+  uint32_t len[NSEG];
+  size_t total = 4 * NSEG;
+  for (int k = 0; k < NSEG; ++k) {
+    len[k] = (k == SEG_DEVICE && r.device_null) ? SEG_NULL : (uint32_t)segs[k]->size();
+    if (len[k] != SEG_NULL) total += len[k];
+  }
+  PyObject* out = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)total);
+  if (!out) return nullptr;
+  char* p = PyBytes_AS_STRING(out);
+  memcpy(p, len, sizeof len);
+  p += sizeof len;
+  for (int k = 0; k < NSEG; ++k)
+    if (len[k] != SEG_NULL) { memcpy(p, segs[k]->data(), len[k]); p += len[k]; }
+  return out;
+}
+
+PyObject* sha256_hex(const std::string& s) {
+  unsigned char h[SHA256_DIGEST_LENGTH];
+  SHA256((const unsigned char*)s.data(), s.size(), h);
+  static const char* X = "0123456789abcdef";
+  char hex[2 * SHA256_DIGEST_LENGTH];
+  for (int k = 0; k < SHA256_DIGEST_LENGTH; ++k) { hex[2 * k] = X[h[k] >> 4]; hex[2 * k + 1] = X[h[k] & 15]; }
+  return PyUnicode_FromStringAndSize(hex, sizeof hex);
+}
+
+// scan_raw(payloads) -> per payload (blob, normalised body, cache key) or None
 PyObject* py_scan_raw(PyObject*, PyObject* args) {
   PyObject* lst;
   if (!PyArg_ParseTuple(args, "O", &lst)) return nullptr;
@@ -1176,9 +1255,7 @@ PyObject* py_scan_raw(PyObject*, PyObject* args) {
       r = Raw();
       if (parse_raw(data, (size_t)len, r) && !keyword_risk(r.body) && !has_any(r.body, g_udigits)) {
         std::string nb = normalize(r.body);
-        PyObject* dev = r.device_null ? (Py_INCREF(Py_None), Py_None) : pystr(r.device_id);
-        res = Py_BuildValue("(NNNNNNN)", pystr(r.msg_id), pystr(r.sender), pystr(r.body), pystr(r.date), dev,
-                            pystr(r.source), pystr(nb));
+        res = Py_BuildValue("(NNN)", make_blob(r, nb), pystr(nb), sha256_hex(nb));
         if (!res) { PyErr_Clear(); res = nullptr; }
       }
     }
@@ -1189,25 +1266,28 @@ PyObject* py_scan_raw(PyObject*, PyObject* args) {
   return out;
 }
 
+// raw_fields(blob) -> (msg_id, sender, body, date, device_id | None, source)
+PyObject* py_raw_fields(PyObject*, PyObject* args) {
+  PyObject* o;
+  if (!PyArg_ParseTuple(args, "O", &o)) return nullptr;
+  Blob b;
+  if (!blob_view(o, &b)) { PyErr_SetString(PyExc_ValueError, "raw_fields: not a scan_raw blob"); return nullptr; }
+  auto S = [&](int k) { return PyUnicode_DecodeUTF8(b.seg[k], (Py_ssize_t)b.len[k], "strict"); };
+  PyObject* dev = b.len[SEG_DEVICE] == SEG_NULL ? (Py_INCREF(Py_None), Py_None) : S(SEG_DEVICE);
+  return Py_BuildValue("(NNNNNN)", S(SEG_MSG_ID), S(SEG_SENDER), S(SEG_BODY), S(SEG_DATE), dev, S(SEG_SOURCE));
+}
+
 // one message: the sms.parsed payload into `o`; returns 0, UNMATCHED or FALLBACK
 int post_one(PyObject* row, PyObject* meta, const int now[7], std::string& o) {
-  if (!PyList_Check(row) || PyList_GET_SIZE(row) != 9 || !PyTuple_Check(meta) || PyTuple_GET_SIZE(meta) != 6)
-    return FALLBACK;
+  Blob b;
+  if (!PyList_Check(row) || PyList_GET_SIZE(row) != 9 || !blob_view(meta, &b)) return FALLBACK;
   std::string f[9];
   for (int k = 0; k < 9; ++k)
     if (!get_str(PyList_GET_ITEM(row, k), &f[k])) return FALLBACK;
   const std::string& txn = f[0];
   if (txn == "otp" || txn == "unknown") return UNMATCHED;  // null fields: the card check raises
   if (txn != "debit" && txn != "credit") return FALLBACK;
-  std::string msg_id, sender, date_raw, body, norm;
-  PyObject* dev = PyTuple_GET_ITEM(meta, 1);
-  std::string device;
-  bool dev_null = dev == Py_None;
-  if (!get_str(PyTuple_GET_ITEM(meta, 0), &msg_id) || (!dev_null && !get_str(dev, &device)) ||
-      !get_str(PyTuple_GET_ITEM(meta, 2), &sender) || !get_str(PyTuple_GET_ITEM(meta, 3), &date_raw) ||
-      !get_str(PyTuple_GET_ITEM(meta, 4), &body) || !get_str(PyTuple_GET_ITEM(meta, 5), &norm))
-    return FALLBACK;
-  (void)date_raw;
+  const std::string body(b.seg[SEG_BODY], b.len[SEG_BODY]);
   // ---- date: canonical text, its fast shape, the body-date repair
   std::string dtext;
   if (!canonical_date(f[1], &dtext)) return FALLBACK;
@@ -1256,18 +1336,9 @@ int post_one(PyObject* row, PyObject* meta, const int now[7], std::string& o) {
   char dbuf[32];
   snprintf(dbuf, sizeof dbuf, "%04d-%02d-%02dT%02d:%02d:%02d", dt.y, dt.mo, dt.d, dt.h, dt.mi, dt.s);
   o.clear();
-  o += "{\"msg_id\":";
-  jstr(o, msg_id);
-  o += ",\"device_id\":";
-  if (dev_null) o += "null";
-  else jstr(o, device);
-  o += ",\"sender\":";
-  jstr(o, sender);
-  o += ",\"date\":\"";
+  o.append(b.seg[SEG_A], b.len[SEG_A]);  // {"msg_id":..,"device_id":..,"sender":..,"date":"
   o += dbuf;
-  o += "\",\"raw_body\":";
-  jstr(o, norm);
-  o += ",\"txn_type\":\"";
+  o.append(b.seg[SEG_B], b.len[SEG_B]);  // ","raw_body":..,"txn_type":"
   o += txn;
   o += "\",\"amount\":\"";
   o += amount;
@@ -1296,7 +1367,7 @@ PyObject* py_postprocess(PyObject*, PyObject* args) {
   g_now_year = nv[0];
   // microseconds: a date equal to now's second is not in the future when now has any
   if (!PyList_Check(rows) || !PyList_Check(metas) || PyList_GET_SIZE(rows) != PyList_GET_SIZE(metas)) {
-    PyErr_SetString(PyExc_TypeError, "postprocess(rows: list, metas: list, now)");
+    PyErr_SetString(PyExc_TypeError, "postprocess(rows: list, blobs: list, now)");
     return nullptr;
   }
   Py_ssize_t n = PyList_GET_SIZE(rows);
@@ -1489,8 +1560,9 @@ PyMethodDef methods[] = {
     {"peek_parsed", py_peek_parsed, METH_VARARGS, "peek_parsed([bytes]) -> [None | (msg_id, merchant?, date tuple)]"},
     {"raw_wires", py_raw_wires, METH_VARARGS, "raw_wires([(device_id, message, sender, timestamp, source)]) -> [bytes | None]"},
     {"init", py_init, METH_VARARGS, "init(upper_ascii_chars, unicode_digits, currency_aliases)"},
-    {"scan_raw", py_scan_raw, METH_VARARGS, "scan_raw(payloads) -> [None | (msg_id, sender, body, date, device_id, source, norm_body)]"},
-    {"postprocess", py_postprocess, METH_VARARGS, "postprocess(rows, metas, now) -> [bytes | 1 (unmatched) | 2 (fallback)]"},
+    {"scan_raw", py_scan_raw, METH_VARARGS, "scan_raw(payloads) -> [None | (blob, norm_body, cache_key)]"},
+    {"raw_fields", py_raw_fields, METH_VARARGS, "raw_fields(blob) -> (msg_id, sender, body, date, device_id, source)"},
+    {"postprocess", py_postprocess, METH_VARARGS, "postprocess(rows, blobs, now) -> [bytes | 1 (unmatched) | 2 (fallback)]"},
     {"normalize", py_normalize, METH_VARARGS, "normalize(body) -> str"},
     {"canonical_date", py_canonical_date, METH_VARARGS, "canonical_date(value, now) -> (text | None, tuple | None)"},
     {"decimal", py_decimal, METH_VARARGS, "decimal(value) -> str | None"},

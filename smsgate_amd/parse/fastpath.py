@@ -10,7 +10,7 @@ byte (tests/test_parsefast.py: the synthetic corpus, hostile strings, the DLQ en
 shapes).
 
 * :func:`scan` -- sms.raw payloads -> :class:`FastRaw` (a validated RawSMS that no
-  keyword filter can touch, with its normalised body) or ``None``;
+  keyword filter can touch, with its normalised body and response-cache key) or ``None``;
 * :func:`postprocess` -- extractor answer rows (the nine decoded field strings) ->
   the sms.parsed payload bytes, :data:`UNMATCHED` or :data:`FALLBACK`.
 
@@ -35,16 +35,32 @@ _TRIED = False
 
 
 class FastRaw:
-    """A RawSMS the native scan validated (the attributes post-processing and the DLQ
-    envelopes read; ``model_dump`` is RawSMS's), plus its normalised body."""
-    __slots__ = ("msg_id", "sender", "body", "date", "device_id", "source", "norm")
+    """A RawSMS the native scan validated: its native record (``blob``: the UTF-8 fields
+    and the pre-encoded sms.parsed fragments), its normalised body (``norm``) and the
+    response-cache key of that body (``key`` = parse/cache.py cache_key(norm)).  The
+    RawSMS attributes the DLQ envelopes and error reports read (``model_dump`` is
+    RawSMS's) are decoded from the record only when asked for."""
+    __slots__ = ("blob", "norm", "key", "_f")
 
     def __init__(self, t) -> None:
-        self.msg_id, self.sender, self.body, self.date, self.device_id, self.source, self.norm = t
+        self.blob, self.norm, self.key = t
+        self._f = None
+
+    def _fields(self):
+        if self._f is None:
+            self._f = _EXT.raw_fields(self.blob)
+        return self._f
+
+    msg_id = property(lambda self: self._fields()[0])
+    sender = property(lambda self: self._fields()[1])
+    body = property(lambda self: self._fields()[2])
+    date = property(lambda self: self._fields()[3])
+    device_id = property(lambda self: self._fields()[4])
+    source = property(lambda self: self._fields()[5])
 
     def model_dump(self) -> Dict[str, Any]:
-        return {"msg_id": self.msg_id, "sender": self.sender, "body": self.body, "date": self.date,
-                "device_id": self.device_id, "source": self.source}
+        f = self._fields()
+        return {"msg_id": f[0], "sender": f[1], "body": f[2], "date": f[3], "device_id": f[4], "source": f[5]}
 
 
 def _tables():
@@ -111,8 +127,7 @@ def postprocess(rows: List[List[str]], raws: Sequence[FastRaw]) -> List[Union[by
     ext = _ext()
     if ext is None:
         return [FALLBACK] * len(rows)
-    metas = [(r.msg_id, r.device_id, r.sender, r.date, r.body, r.norm) for r in raws]
-    return ext.postprocess(rows, metas, _now())
+    return ext.postprocess(rows, [r.blob for r in raws], _now())
 
 
 def raw_wires(payloads) -> List[bytes]:

@@ -171,14 +171,16 @@ class ParsePipeline:
         keys: List[Optional[str]] = [None] * n
         todo: List[int] = []
         for i, raw in enumerate(raws):
-            fb = getattr(raw, "norm", None)  # a FastRaw: no keyword can match, body normalised natively
-            if fb is None:
+            if type(raw) is fastpath.FastRaw:  # no keyword can match; body normalised and keyed natively
+                bodies[i] = raw.norm
+                keys[i] = raw.key
+            else:
                 if llm_should_skip(raw.body):
                     results[i] = ParseResult(Outcome.UNMATCHED)
                     continue
                 fb = normalize_body(raw.body)
-            bodies[i] = fb
-            keys[i] = cache_key(fb)
+                bodies[i] = fb
+                keys[i] = cache_key(fb)
             todo.append(i)
         # the native post-processing needs the answers as rows: backends that give them
         rows_api = getattr(self.backend, "extract_rows", None) if fastpath.available() else None

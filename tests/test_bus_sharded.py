@@ -159,3 +159,21 @@ def test_publishes_are_dealt_per_subject():
     got = [rt.publish_target(s) for _ in range(8) for s in ("a", "b")]
     assert sorted(set(got[0::2])) == [0, 1] and sorted(set(got[1::2])) == [2, 3]
     assert got[0::2].count(0) == 4 and got[1::2].count(2) == 4
+
+
+def test_bulk_deal_equals_the_per_message_deal():
+    """publish_many deals a batch over a subject's partitions in one step per subject
+    (Router.deal) -- the same member for every message as one publish_target call per
+    message would pick, batch after batch."""
+    from smsgate_amd.bus.sharded import Router
+
+    pins = {SUBJECT_RAW: [0, 1, 2], SUBJECT_PARSED: [3, 4]}
+    a, b = Router(6, pins, [5]), Router(6, pins, [5])
+    for n in (1, 2, 7, 3, 12, 5):
+        for subj in (SUBJECT_RAW, SUBJECT_PARSED, SUBJECT_PROCESSING):
+            one = [a.publish_target(subj) for _ in range(n)]
+            bulk = [None] * n
+            for k, sl in b.deal(subj, n):
+                for i in range(n)[sl]:
+                    bulk[i] = k
+            assert bulk == one, (subj, n)

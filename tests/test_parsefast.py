@@ -381,3 +381,24 @@ def test_package_imports_in_any_order(first):
     code = f"import {first}; import smsgate_amd.parse.pipeline, smsgate_amd.serving.remote, smsgate_amd.services.writer"
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_scan_record_carries_the_cache_key_and_fields():
+    """A FastRaw's cache key is parse/cache.py cache_key of its normalised body, and the
+    RawSMS fields read back from its native record are pydantic's."""
+    from smsgate_amd.models.domain import RawSMS
+    from smsgate_amd.parse.cache import cache_key
+
+    r = random.Random(7)
+    items = synth.generate(300, seed=61, vocab_name="heldout", families="all", negatives=0.1)
+    payloads = [_payload(i, s, r) for i, s in enumerate(items)]
+    got = fastpath.scan(payloads)
+    assert sum(g is not None for g in got) > 250
+    for p, g in zip(payloads, got):
+        if g is None:
+            continue
+        ref = RawSMS.model_validate_json(p)
+        assert g.key == cache_key(normalize_body(ref.body)) and g.norm == normalize_body(ref.body)
+        assert g.model_dump() == ref.model_dump()
+        assert (g.msg_id, g.sender, g.body, g.date, g.device_id, g.source) == (
+            ref.msg_id, ref.sender, ref.body, ref.date, ref.device_id, ref.source)

@@ -153,7 +153,8 @@ def main() -> int:
             v["overrides"] = json.dumps(v["overrides"])
     procs = []
     for v in variants:
-        for s in seeds:
+        v["seeds"] = [int(x) for x in v.get("seeds", seeds)]  # a variant may name its own seeds
+        for s in v["seeds"]:
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--seed", str(s), "--eval-n", str(a.eval_n),
                    "--workers", str(a.workers), "--tag", v["tag"], "--device", a.device, "--log-dir", a.log_dir,
                    "--child-out", os.path.join(a.log_dir, f"{v['tag']}-seed{s}.json")]
@@ -167,8 +168,8 @@ def main() -> int:
     ok = True
     for v in variants:
         results = []
-        vr = {s: rcs[(v["tag"], s)] for s in seeds}
-        for s in seeds:
+        vr = {s: rcs[(v["tag"], s)] for s in v["seeds"]}
+        for s in v["seeds"]:
             path = os.path.join(a.log_dir, f"{v['tag']}-seed{s}.json")
             if vr[s] == 0 and os.path.exists(path):
                 results.append(json.load(open(path)))

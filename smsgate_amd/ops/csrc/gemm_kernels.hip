@@ -1089,7 +1089,7 @@ __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __
 // MF 32: the same tile with v_mfma_f32_32x32x16_bf16 (2 x 3 fragments of 32x32 per wave;
 // VERDICT r05 next #2's A/B): the same 10 fragment reads per K-step (the wave tile, not
 // the MFMA shape, sets the LDS traffic) for 12 instead of 24 MFMAs.
-template <int NB, int MF>
+template <int NB, int MF, bool STAG = true>
 __global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __restrict__ A, int lda,
                                                             const uint16_t* __restrict__ W, uint16_t* C, int ldc,
                                                             const uint16_t* R, int ldr, int M, int N, int K,
@@ -1144,6 +1144,7 @@ __global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __r
   };
   zero_acc();
   bf16x8 af[KS][FI], bq[KS][FJ];
+  uint2 rres[FI][FJ * (AV / 4)];  // the tile's residual chunks (requested on its last K-step)
   // MF 16: lane reads 16-B chunk (lane >> 4) of row (lane & 15); MF 32: chunk
   // 2·ks + (lane >> 5) of row (lane & 31)
   auto read_frags = [&](const uint16_t* buf) {
@@ -1172,22 +1173,21 @@ __global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __r
   for (int t = 0; t < NB - 1; ++t) stage(t);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NB - 2)) : "memory");
   __builtin_amdgcn_s_barrier();
-  if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
+  if (STAG && __builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
 
-  int v = blockIdx.x, m0, n0;
-  tile_mn(v, m0, n0);
-  int kt = 0;
-  for (int s = 0; s < S; ++s) {
-    // ---- read section of step s (its data landed: retired one step ago, or above)
+  // one K-step (step s of this block): the read section, the mid barrier, the MFMA
+  // section (refill first, or -- on a tile's last step, LAST -- after the MFMAs and the
+  // tile's residual requests, in the fragment registers the MFMAs free: the epilogue
+  // then waits for them and for the two older steps, one round trip per tile and never
+  // for the refill, as vmcnt retires in order), the end barrier
+  auto kstep = [&](int s, bool LAST, int m0, int n0) {
     read_frags(smem + (s % NB) * BUF);
     // step s+1 retired before the barrier that precedes its reads (NB-3 younger steps
     // of this wave may stay in flight)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NB - 3)) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // ---- MFMA section: refill the buffer of step s-1 (read before the previous barrier
-    // by both groups) with step s+NB-1
-    stage(s + NB - 1);
+    if (!LAST) stage(s + NB - 1);  // refill the buffer of step s-1 (read by both groups)
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
@@ -1201,14 +1201,37 @@ __global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __r
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bq[ks][j], af[ks][i], acc[i][j], 0, 0, 0);
         }
     __builtin_amdgcn_s_setprio(0);
+    if (LAST) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i) {
+        const int gr = m0 + rbase + i * MF + (lane & (MF - 1));
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+          for (int g = 0; g < AV / 4; ++g) {
+            const int col = n0 + cbase + (MF == 16 ? j * 16 + 4 * (lane >> 4) : j * 32 + 8 * g + 4 * (lane >> 5));
+            rres[i][j * (AV / 4) + g] =
+                gr < M ? *reinterpret_cast<const uint2*>(R + (size_t)gr * ldr + col) : make_uint2(0u, 0u);
+          }
+      }
+      stage(s + NB - 1);
+    }
     __builtin_amdgcn_s_barrier();
-    if (++kt < KT) continue;
+  };
+
+  int s = 0;
+  for (int tile = 0; tile < my_tiles; ++tile) {
+    int m0, n0;
+    tile_mn((int)blockIdx.x + tile * G, m0, n0);
+    zero_acc();
+    for (int kt = 0; kt < KT - 1; ++kt, ++s) kstep(s, false, m0, n0);
+    kstep(s, true, m0, n0);
+    ++s;
     // ---- tile done: epilogue from the accumulators (no barriers), then the next tile.
     // MF 16: lane holds rows rbase + 16i + (lane & 15), columns cbase + 16j + 4·(lane >> 4)
     // + q; MF 32: rows rbase + 32i + (lane & 31), columns cbase + 32j + 8g + 4·(lane >> 5)
     // + q (value 4g + q).  An 8-column x² chunk: its first 4 columns in one lane, its last
     // 4 in the partner lane (xor 16 / xor 32), the fmaf chain run through both in order.
-    kt = 0;
     const bool want_ss = na.ssout != nullptr;
 #pragma unroll
     for (int i = 0; i < FI; ++i) {
@@ -1221,8 +1244,7 @@ __global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __r
 #pragma unroll
         for (int g = 0; g < AV / 4; ++g) {
           const int col = n0 + cbase + (MF == 16 ? j * 16 + 4 * (lane >> 4) : j * 32 + 8 * g + 4 * (lane >> 5));
-          uint2 rv = make_uint2(0u, 0u);
-          if (ok) rv = *reinterpret_cast<const uint2*>(R + (size_t)gr * ldr + col);
+          const uint2 rv = rres[i][j * (AV / 4) + g];
           float o[4];
           const uint32_t rw[2] = {rv.x, rv.y};
 #pragma unroll
@@ -1261,11 +1283,8 @@ __global__ void __launch_bounds__(512) gemm256p_resid_kernel(const uint16_t* __r
         }
       }
     }
-    zero_acc();
-    v += G;
-    if (s + 1 < S) tile_mn(v, m0, n0);
   }
-  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  if (STAG && __builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's dummy DMAs
 }
 
@@ -1341,7 +1360,8 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  32: 256x192 (4x2) 2st, 8 waves — 64x96 wave tiles (epi 0 / 1 only)
 //  33: 128x192 (2x2) BK 32, 4st   34: 256x192 (4x2) BK 32, 4st, 8 waves (epi 0 / 1 only)
 //  35: 256x192 persistent staggered residual GEMM (gemm256p_resid_kernel, 4 ring buffers,
-//      16x16x32 MFMAs; epi 1 only)   36: 5 ring buffers   37 / 38: 35 / 36 with 32x32x16 MFMAs
+//      16x16x32 MFMAs; epi 1 only)   36: 35 without the group stagger (A/B)   37: 35 with
+//      32x32x16 MFMAs   38: 37 with 5 ring buffers
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1413,11 +1433,11 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
     const int tm = (M + 255) / 256, tn = N / 192, T = tm * tn;
     const int grid = T < 256 ? T : 256;
     const int gmv = g_group_m > 0 ? g_group_m : 1;
-#define SG_RP(NB_, MF_)                                                                                       \
-  hipLaunchKernelGGL((gemm256p_resid_kernel<NB_, MF_>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda, \
+#define SG_RP(NB_, MF_, ...)                                                                                  \
+  hipLaunchKernelGGL((gemm256p_resid_kernel<NB_, MF_, ##__VA_ARGS__>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda, \
                      (const uint16_t*)W, (uint16_t*)C, ldc, (const uint16_t*)R, ldr, M, N, K, tm, tn, gmv, na)
     if (cfg == 35) SG_RP(4, 16);
-    else if (cfg == 36) SG_RP(5, 16);
+    else if (cfg == 36) SG_RP(4, 16, false);  // A/B: the same loop without the group stagger
     else if (cfg == 37) SG_RP(4, 32);
     else SG_RP(5, 32);
 #undef SG_RP

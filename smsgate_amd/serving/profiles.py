@@ -20,11 +20,14 @@ the headline bench measured).
 The one-forward qa engine (serving/qa_engine.py, the default extractor since round 5)
 reads only its ``qa_*`` knobs and ``max_slots``:
 
-* ``throughput`` -- packed batches of up to 262 144 rows (~5 000 messages), a second
-  batch in flight once 65 536 rows wait (profiles/r05_qa_min_tokens_ab.jsonl);
-* ``latency`` -- batches of up to 16 384 rows (~330 messages), a second in flight once
-  2 048 rows wait, so a message waits for at most about one small batch
-  (profiles/r06_latency_qa*.json).
+* both profiles: packed batches of up to 262 144 rows (~5 000 messages), a second batch
+  in flight once 65 536 rows wait (profiles/r05_qa_min_tokens_ab.jsonl).  Under Poisson
+  arrivals that gives p50 / p99 of 1.4 / 1.7 ms at 1 k msgs/s, 1.7 / 2.0 ms at 10 k and
+  5.4 / 6.5 ms at 40 k (profiles/r06_latency_qa_throughput.json): a batch is launched as
+  soon as the GPU is free, so at these loads it holds what arrived during one forward.
+  Smaller batches (16 384 rows, a second in flight from 2 048) were slower at every
+  load -- 3.9 ms p99 at 10 k, 13.0 ms at 40 k (profiles/r06_latency_qa_latency.json) --
+  so the latency profile serves the throughput profile's qa knobs.
 
 Everything not listed keeps the :class:`~smsgate_amd.serving.engine.EngineConfig`
 default.
@@ -43,7 +46,7 @@ PROFILES: Dict[str, Dict[str, Any]] = {
                        template_slots=32, qa_max_tokens=262144, qa_min_tokens=65536),
     "latency": dict(max_slots=4096, steps_per_graph=2, admit_min_fraction=0.125, spec_k=6, spec_draft_frac=1.25,
                     buckets=BUCKETS[:-1], split_decode=4096, split_prefill=8192, copy_constrain=True,
-                    template_slots=32, qa_max_tokens=16384, qa_min_tokens=2048),
+                    template_slots=32, qa_max_tokens=262144, qa_min_tokens=65536),
     # the round-2 latency profile (4 steps per graph, 25 % admission, 4 drafts): with the
     # round-3 kernels it was behind the throughput profile at every load
     # (profiles/r03s2_latency_{latency,throughput}.json, r03s2b_latency_latency_r2.json)

@@ -192,22 +192,38 @@ class MsgMetadata:
 
 
 class Msg:
-    """One delivered message.  ``data`` is bytes; ack/nak/term are idempotent."""
+    """One delivered message.  ``data`` is bytes; ack/nak/term are idempotent.  The
+    delivery metadata is kept as plain slots (one object per delivered message, not
+    two); ``metadata`` builds the :class:`MsgMetadata` view when asked."""
 
-    __slots__ = ("subject", "data", "headers", "metadata", "_acker", "_done")
+    __slots__ = ("subject", "data", "headers", "_acker", "_done", "_seq", "_nd", "_ts", "_stream", "_consumer")
 
     def __init__(self, subject: str, data: bytes, metadata: MsgMetadata, acker: "Acker",
                  headers: Optional[Dict[str, str]] = None) -> None:
         self.subject = subject
         self.data = data
         self.headers = headers or {}
-        self.metadata = metadata
         self._acker = acker
         self._done = False
+        self._seq, self._nd, self._ts = metadata.sequence, metadata.num_delivered, metadata.timestamp
+        self._stream, self._consumer = metadata.stream, metadata.consumer
+
+    @classmethod
+    def delivered(cls, subject: str, data: bytes, seq: int, num_delivered: int, timestamp: float, stream: str,
+                  consumer: str, acker: "Acker", headers: Optional[Dict[str, str]] = None) -> "Msg":
+        """A message straight from a fetch reply's fields (no MsgMetadata built)."""
+        m = cls.__new__(cls)
+        m.subject, m.data, m.headers, m._acker, m._done = subject, data, headers or {}, acker, False
+        m._seq, m._nd, m._ts, m._stream, m._consumer = seq, num_delivered, timestamp, stream, consumer
+        return m
+
+    @property
+    def metadata(self) -> MsgMetadata:
+        return MsgMetadata(self._seq, self._nd, self._ts, self._stream, self._consumer)
 
     @property
     def seq(self) -> int:
-        return self.metadata.sequence
+        return self._seq
 
     @property
     def settled(self) -> bool:
@@ -217,21 +233,21 @@ class Msg:
     async def ack(self) -> None:
         if not self._done:
             self._done = True
-            await self._acker.ack(self.metadata.stream, self.metadata.consumer, self.metadata.sequence)
+            await self._acker.ack(self._stream, self._consumer, self._seq)
 
     async def nak(self, delay: float = 0.0) -> None:
         if not self._done:
             self._done = True
-            await self._acker.nak(self.metadata.stream, self.metadata.consumer, self.metadata.sequence, delay)
+            await self._acker.nak(self._stream, self._consumer, self._seq, delay)
 
     async def term(self) -> None:
         if not self._done:
             self._done = True
-            await self._acker.term(self.metadata.stream, self.metadata.consumer, self.metadata.sequence)
+            await self._acker.term(self._stream, self._consumer, self._seq)
 
     async def in_progress(self) -> None:
         if not self._done:
-            await self._acker.touch(self.metadata.stream, self.metadata.consumer, self.metadata.sequence)
+            await self._acker.touch(self._stream, self._consumer, self._seq)
 
     def json(self):
         import json
@@ -250,12 +266,11 @@ async def ack_all(msgs: Sequence["Msg"]) -> None:
         if m._done:
             continue
         m._done = True
-        md = m.metadata
-        key = (id(m._acker), md.stream, md.consumer)
+        key = (id(m._acker), m._stream, m._consumer)
         g = groups.get(key)
         if g is None:
             g = groups[key] = (m._acker, [])
-        g[1].append(md.sequence)
+        g[1].append(m._seq)
     for (_, stream, consumer), (acker, seqs) in groups.items():
         fn = getattr(acker, "ack_seqs", None)
         if fn is not None:

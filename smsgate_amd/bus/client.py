@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import asyncio
 import itertools
+from collections.abc import Sequence as SequenceABC
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import urlparse
 
@@ -14,7 +15,6 @@ from .base import (
     bus_error,
     ConsumerInfo,
     Msg,
-    MsgMetadata,
     PubAck,
     StreamConfig,
     StreamInfo,
@@ -36,11 +36,33 @@ class _RemoteSub(Subscription):
         if self._closed:
             return []
         rows = await self.bus._call("fetch", self.stream, self.consumer, batch, timeout)
-        return [Msg(subj, data, MsgMetadata(seq, nd, ts, self.stream, self.consumer), self.bus, hdr)
-                for subj, data, seq, nd, ts, hdr in rows]
+        mk, st, co, bus = Msg.delivered, self.stream, self.consumer, self.bus
+        return [mk(subj, data, seq, nd, ts, st, co, bus, hdr) for subj, data, seq, nd, ts, hdr in rows]
 
     async def unsubscribe(self) -> None:
         self._closed = True
+
+
+class _PubAcks(SequenceABC):
+    """The acks of one publish_many, built only when read (the hot publishers -- the
+    parser stage, the ingest path -- never read them)."""
+
+    __slots__ = ("_r",)
+
+    def __init__(self, rows) -> None:
+        self._r = rows
+
+    def __len__(self) -> int:
+        return len(self._r)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [PubAck(s, q) for s, q in self._r[i]]
+        s, q = self._r[i]
+        return PubAck(s, q)
+
+    def __eq__(self, other) -> bool:
+        return list(self) == list(other)
 
 
 class RemoteBus(Bus, Acker):
@@ -119,8 +141,8 @@ class RemoteBus(Bus, Acker):
         return PubAck(s, q)
 
     async def publish_many(self, items: Sequence[Tuple[str, bytes]]) -> List[PubAck]:
-        res = await self._call("publish_many", [[s, bytes(d)] for s, d in items])
-        return [PubAck(s, q) for s, q in res]
+        res = await self._call("publish_many", [[s, d if type(d) is bytes else bytes(d)] for s, d in items])
+        return _PubAcks(res)
 
     async def subscribe(self, subject: str, durable: str, **opts: Any) -> Subscription:
         opts = {k: (v.value if hasattr(v, "value") else v) for k, v in opts.items()}

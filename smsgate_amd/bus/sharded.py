@@ -28,6 +28,7 @@ Two layouts, chosen by the DSN:
 from __future__ import annotations
 
 import asyncio
+from collections.abc import Sequence as SequenceABC
 import time
 import zlib
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -160,6 +161,31 @@ class Router:
         self._rr[subject] = k + n
         m = len(ms)
         return [(ms[(k + r) % m], slice(r, n, m)) for r in range(min(m, n))]
+
+
+class _MergedAcks(SequenceABC):
+    """publish_many's acks in publish order, gathered from the members' replies only
+    when read (the hot publishers never read them)."""
+
+    __slots__ = ("_n", "_parts", "_flat")
+
+    def __init__(self, n: int, parts) -> None:
+        self._n, self._parts, self._flat = n, parts, None
+
+    def __len__(self) -> int:
+        return self._n
+
+    def __getitem__(self, i):
+        if self._flat is None:
+            flat: List[Optional[PubAck]] = [None] * self._n
+            for idx, acks in self._parts:
+                for k, a in zip(idx, acks):
+                    flat[k] = a
+            self._flat = flat
+        return self._flat[i]
+
+    def __eq__(self, other) -> bool:
+        return list(self) == list(other)
 
 
 class _PartitionedSub(Subscription):
@@ -339,11 +365,7 @@ class ShardedBus(Bus):
             return await self.members[k].publish_many(items)
         res = await asyncio.gather(*(self.members[k].publish_many([items[i] for i in idx])
                                      for k, idx in groups.items()))
-        out: List[Optional[PubAck]] = [None] * len(items)
-        for (k, idx), acks in zip(groups.items(), res):
-            for i, a in zip(idx, acks):
-                out[i] = a
-        return out  # type: ignore[return-value]
+        return _MergedAcks(len(items), list(zip(groups.values(), res)))
 
     async def subscribe(self, subject: str, durable: str, **consumer_opts) -> Subscription:
         ks = self.router.members(subject)

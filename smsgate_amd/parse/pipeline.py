@@ -69,6 +69,14 @@ def _debug_record(body: str, answer: Dict[str, Any], outcome: str) -> None:
 _REJECT_TXN = ("otp", "unknown")  # serving/qa.py REJECT_TXN (not imported: parse must not import serving)
 
 
+def _as_answer(a):
+    """A cached / fresh answer as the backend interface's dict: a row of the nine decoded
+    field strings (the local extractor's answers) becomes the rejection-nulled dict."""
+    if isinstance(a, list) and len(a) == len(CORE_FIELDS):
+        return _null_rejection(dict(zip(CORE_FIELDS, a)))
+    return a
+
+
 def _null_rejection(answer: Dict[str, Any]) -> Dict[str, Any]:
     """serving/qa.py null_rejection: a non-transaction class nulls every other field."""
     if answer.get("txn_type") in _REJECT_TXN:
@@ -220,13 +228,14 @@ class ParsePipeline:
                     if rows_api is not None and isinstance(r, list):
                         for i in uniq[b]:
                             rows[i] = r
-                        # the answer as the backend interface gives it (cached raw, D7)
-                        r = _null_rejection(dict(zip(CORE_FIELDS, r)))
-                    if not isinstance(r, BaseException) and not isinstance(r, dict):
+                        # the nine decoded strings stand for the answer (cached raw, D7):
+                        # _as_answer() makes the backend interface's dict only where the
+                        # Python path or a cache reader needs it
+                    elif not isinstance(r, BaseException) and not isinstance(r, dict):
                         r = BackendError(f"backend returned {type(r).__name__}, not a JSON object")
                     for i in uniq[b]:
                         answers[i] = r
-                    if isinstance(r, dict):
+                    if isinstance(r, (dict, list)):
                         to_cache.append((keys[uniq[b][0]], r))
                 if to_cache:
                     self.cache.put_many(to_cache)
@@ -248,7 +257,7 @@ class ParsePipeline:
         for i in todo:
             if results[i] is not None:
                 continue
-            ans = answers[i]
+            ans = _as_answer(answers[i])
             if isinstance(ans, BaseException):
                 sentry_capture(ans, extras={"raw_body": raws[i].body[:4096]})
                 results[i] = ParseResult(Outcome.ERROR, error=ans)

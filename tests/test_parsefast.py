@@ -280,12 +280,21 @@ def test_route_batch_is_byte_identical_with_and_without_the_native_path(arun, mo
 
     from smsgate_amd.bus.base import MsgMetadata
 
-    def run():
-        pipe = ParsePipeline(_RowBackend(table))
+    def run(pipe=None):
+        pipe = pipe or ParsePipeline(_RowBackend(table))
         msgs = [Msg("sms.raw", d, MsgMetadata(i, 1, 0.0, "SMS", "t"), None) for i, d in enumerate(payloads)]
         return arun(route_batch(pipe, msgs))
 
     native_out, native_counts = run()
+    # a replay answered from the response cache (rows cached as the nine decoded strings,
+    # turned into the answer dict on the Python path) routes every message the same way
+    pipe = ParsePipeline(_RowBackend(table))
+    run(pipe)
+    pipe.backend.table = {}  # every answer must now come from the cache
+    replay_out, replay_counts = run(pipe)
+    assert replay_counts == native_counts
+    assert [x for x, _ in replay_out] == [x for x, _ in native_out]
+    assert [b for x, b in replay_out if x != "sms.failed"] == [b for x, b in native_out if x != "sms.failed"]
     monkeypatch.setattr(fastpath, "_EXT", None)
     monkeypatch.setattr(fastpath, "_TRIED", True)
     py_out, py_counts = run()

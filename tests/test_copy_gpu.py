@@ -109,7 +109,8 @@ def test_gemm_argmax_copy_rows(cfg, M):
 def _engine(spec_k, **kw):
     from smsgate_amd.parse.backends.local_llm import build_engine, bundled_checkpoint
 
-    return build_engine("small", bundled_checkpoint("small-copy"), device=DEV, max_slots=512, buckets=(64, 512), use_graphs=False, spec_k=spec_k,
+    return build_engine("small", bundled_checkpoint("small-copy"), device=DEV, answer_format="copy", max_slots=512,
+                        buckets=(64, 512), use_graphs=False, spec_k=spec_k,
                         decode_attn_small_rows=0, lm_head_fused=True, split_decode=0, **kw)
 
 

@@ -54,6 +54,7 @@ struct RopeArgs {
   uint16_t* k_cache;    // [S][nkv][Lmax][64]
   uint16_t* vt_cache;   // [S][nkv][Lmax/8][64][8]
   int nh, nkv, Lmax, p0;
+  int hb;  // head index of N column 0 (the v-only launch of cfg 39 starts at nh + nkv)
 };
 
 // Row scales computed by the PRODUCER of the activation (NORM 2).  An EPI 1 GEMM
@@ -282,7 +283,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   constexpr int EPN = EPI == 3 ? (QIT > VU ? QIT : VU) : 1;
   int epos[EPN], eslot[EPN];
   if constexpr (EPI == 3) {
-    const int h = n0 >> 6;
+    const int h = (n0 >> 6) + ra.hb;
     if (h < ra.nh + ra.nkv) {
 #pragma unroll
       for (int it = 0; it < QIT; ++it) {
@@ -447,7 +448,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_fused_kernel(const uint16_t
   // cache, or scatter the v heads into the blocked V^T cache.  Same rounding as
   // the unfused path: bf16 projection (the staged tile) -> fp32 RoPE -> bf16.
   if constexpr (EPI == 3) {
-    const int h0 = n0 >> 6;
+    const int h0 = (n0 >> 6) + ra.hb;
     if (h0 < ra.nh + ra.nkv) {
       // one (row, quarter) item per thread and trip: its (cos, sin) chunk is loaded once
       // and rotates that quarter of all HT heads of the tile (the heads share the row's
@@ -1062,6 +1063,284 @@ __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail DMAs
 }
 
+// Persistent QK+RoPE GEMM (cfg 39): the gate/up kernel's schedule (one block per CU,
+// two staggered 4-wave groups, 4 phases per BK 64 K-tile, the next tile's first K-tile
+// staged during this one's last) for the q and k heads of the QKV projection (N =
+// (nh + nkv)·64, a multiple of 256: 4 heads per tile).  W rows are loaded in the RoPE-pair
+// order (stage), so the epilogue rotates in registers and stores q rows / K-cache rows
+// straight from the accumulators; the rows' positions and slots are LDS-DMA'd with the
+// next tile's first K-tile (psl, tile parity).  The v heads go through cfg 28
+// (sg_gemm_qkv_rope).
+template <int NORM>
+__global__ void __launch_bounds__(512) gemm256p_qk_rope_kernel(const uint16_t* __restrict__ A, int lda,
+                                                              const uint16_t* __restrict__ W, int M, int N, int K,
+                                                              float eps, int tiles_m, int tiles_n, int gm, NormArgs na,
+                                                              RopeArgs ra) {
+  constexpr int BM = 256, BN = 256, HALF = 128 * BK, BUF = 4 * HALF;
+  constexpr int RAW = NORM == 2 ? SS_PARTS * BM * 2 : 0;  // [16][256] fp32, in uint16 units
+  constexpr int SSL = NORM == 2 ? 2 * BM * 2 : 0;         // [2][256] fp32 (tile parity)
+  constexpr int PSL = 2 * 2 * BM * 2;                      // [2 parity][pos, slot][256] int32
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BUF + RAW + SSL + PSL];
+  float* raw = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* ssl = reinterpret_cast<float*>(smem + 2 * BUF + RAW);
+  int* psl = reinterpret_cast<int*>(smem + 2 * BUF + RAW + SSL);
+
+  const int T = tiles_m * tiles_n;
+  auto tile_mn = [&](int v, int& m0, int& n0) {
+    const int xcd = v & 7, q8 = T >> 3, r8 = T & 7;
+    const int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+    const int gsz = gm * tiles_n, g = t / gsz, gl = t - g * gsz;
+    const int grows = min(gm, tiles_m - g * gm);
+    m0 = (g * gm + gl % grows) * BM;
+    n0 = (gl / grows) * BN;
+  };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int KT = K / BK;
+
+  // W rows in the RoPE-pair order: tile row t of half hh holds head n0/64 + wc of dims
+  // hh·16 + jj·32 + [0, 16) (wc = (t & 127) >> 5, jj = bit 4), so a wave's fragments j 0 / 1
+  // (and 2 / 3) are the dims d and d + 32 of ONE head: the rotation stays in the lane
+  auto stage = [&](int b, int h, int mm, int nn, int kt) {
+    const int kk = min(kt, KT - 1) * BK;
+    uint16_t* dst = smem + b * BUF + h * HALF;
+    if (h < 2) {
+      issue_tile<128, 8>(A, lda, mm + h * 128, M - 1, kk, dst, wave, lane);
+    } else {
+      const int hh = h - 2, rr = lane >> 3, pc = lane & 7;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int g = wave + 8 * i, row = 8 * g + rr;  // 8-row piece g of this half
+        const int src = nn + (row >> 5) * 64 + hh * 16 + ((row >> 4) & 1) * 32 + (row & 15);
+        const uint16_t* gp = W + (size_t)src * K + kk + ((pc ^ (row & 7)) << 3);
+        __builtin_amdgcn_global_load_lds((const void*)gp, (lds_ptr_t)(dst + g * 8 * BK), 16, 0, 0);
+      }
+    }
+  };
+  // the rows' positions / KV slots of tile rows mm + [0, 256) into psl[par]: wave w loads
+  // array w >> 2, rows (w & 3)·64 + lane -- one dword LDS-DMA per wave (rows past the end
+  // re-read row M - 1, never used)
+  auto stage_ps = [&](int mm, int par) {
+    const int arr = wave >> 2, row = min(mm + (wave & 3) * 64 + lane, M - 1);
+    const int* src = (arr ? ra.slot : ra.pos) + row;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(psl + (par * 2 + arr) * BM + (wave & 3) * 64), 4, 0,
+                                     0);
+  };
+  // NORM 2: parts 2w, 2w+1 of rows mm + [0, 256): lane l -> rows mm + 4l .. +3 (16 B);
+  // groups past the end re-read the last aligned group (never used); ld % 4 == 0
+  auto stage_ss = [&](int mm) {
+    if constexpr (NORM == 2) {
+      const int r = min(mm + lane * 4, ((M + 3) & ~3) - 4);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int p = wave * 2 + e;
+        __builtin_amdgcn_global_load_lds((const void*)(na.ssin + (size_t)p * na.ld + r),
+                                         (lds_ptr_t)(raw + p * BM), 16, 0, 0);
+      }
+    }
+  };
+  auto sum_ss = [&](int par) {  // group 0: one row per thread
+    if constexpr (NORM == 2) {
+      if (tid < BM) {
+        float v = 0.f;
+#pragma unroll
+        for (int p = 0; p < SS_PARTS; ++p) v += raw[p * BM + tid];
+        ssl[par * BM + tid] = v;
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+  float ss[8];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ss[i] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  bf16x8 af[2][4], bq[2][2];  // ONE A set (p4 re-reads rows 0-63): 32 VGPRs fewer, no spills
+  auto read_a = [&](bf16x8 (&dst)[2][4], const uint16_t* base, int r0) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = r0 + i * 16 + (lane & 15), ch = s2 * 4 + (lane >> 4);
+        dst[s2][i] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((ch ^ (row & 7)) << 3));
+      }
+  };
+  auto read_b = [&](const uint16_t* base) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 32 + j * 16 + (lane & 15), ch = s2 * 4 + (lane >> 4);
+        bq[s2][j] = *reinterpret_cast<const bf16x8*>(base + row * BK + ((ch ^ (row & 7)) << 3));
+      }
+  };
+  auto mfma_q = [&](bf16x8 (&a_)[2][4], int i0, int j0) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i0 + i][j0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[s2][j], a_[s2][i], acc[i0 + i][j0 + j],
+                                                                        0, 0, 0);
+        if constexpr (NORM == 1)
+          if (j0 == 0) ss[i0 + i] = sumsq_frag(a_[s2][i], ss[i0 + i]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto mid = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  int v = blockIdx.x;
+  if (v >= T) return;  // (the launcher sizes the grid <= T: never taken)
+  int m0, n0;
+  tile_mn(v, m0, n0);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(0, h, m0, n0, 0);
+  stage_ss(m0);
+  stage_ps(m0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  sum_ss(0);
+  __syncthreads();
+  zero_acc();
+  if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
+
+  int gk = 0, tpar = 0;
+  const int c4 = (lane >> 4) * 4;
+  while (true) {
+    const int vn = v + gridDim.x;
+    const bool more = vn < T;
+    int m1 = m0, n1 = n0;
+    if (more) tile_mn(vn, m1, n1);
+    for (int kt = 0; kt < KT; ++kt, ++gk) {
+      const int cb = gk & 1, nb = cb ^ 1;
+      const bool last = kt == KT - 1;
+      const int sm = last ? m1 : m0, sn = last ? n1 : n0, sk = last ? (more ? 0 : KT - 1) : kt + 1;
+      const uint16_t* buf = smem + cb * BUF;
+      const uint16_t* abase = buf + wr * HALF;
+      // p1: rows 0-63 x lo
+      read_a(af, abase, 0);
+      read_b(buf + 2 * HALF);
+      if (last) {
+        stage_ss(sm);
+        stage_ps(sm, tpar ^ 1);
+      }
+      stage(nb, 0, sm, sn, sk);
+      mid();
+      mfma_q(af, 0, 0);
+      __builtin_amdgcn_s_barrier();
+      // p2: rows 64-127 x lo
+      read_a(af, abase, 64);
+      stage(nb, 1, sm, sn, sk);
+      if (NORM == 2 && last) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // + this p1's partial / pos DMAs
+      else if (last) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");          // + this p1's pos / slot DMA
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                    // Bhi of THIS K-tile landed
+      mid();
+      mfma_q(af, 4, 0);
+      __builtin_amdgcn_s_barrier();
+      // p3: rows 64-127 x hi
+      read_b(buf + 3 * HALF);
+      stage(nb, 2, sm, sn, sk);
+      mid();
+      mfma_q(af, 4, 2);
+      __builtin_amdgcn_s_barrier();
+      // p4: rows 0-63 x hi (re-read: WAR-safe, the next DMA into this A half is staged
+      // after the lagging group's p4 barrier)
+      read_a(af, abase, 0);
+      stage(nb, 3, sm, sn, sk);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // next K-tile's A_top, A_bot, Blo (+ partials)
+      mid();
+      mfma_q(af, 0, 2);
+      __builtin_amdgcn_s_barrier();
+    }
+    // next tile's row sums (its partials landed: every wave's p4 wait precedes a barrier
+    // this wave has passed); this tile's are in ssl[tpar]
+    if (more) sum_ss(tpar ^ 1);
+    // epilogue straight from the accumulators: row m0 + wr·128 + 16i + (lane & 15) of head
+    // n0/64 + wc, dims dh + c4 .. +3 (x1) and their partners dh + 32 + c4 .. (x2), dh = 0
+    // (fragments 0 / 1) and 16 (fragments 2 / 3).  The unfused path's rounding: bf16
+    // projection, fp32 rotation, bf16.  The next row fragment's (cos, sin) chunks are
+    // requested before this one is rotated (one exposed table round trip per tile)
+    const int h = (n0 >> 6) + wc;
+    const int* pp = psl + (tpar * 2) * BM;
+    const int* sp = psl + (tpar * 2 + 1) * BM;
+    float4 tc[2][2];  // [half dh][two float4 = dims c4 .. c4+3 as (cos, sin) pairs]
+    auto load_cs = [&](int i, float4 (&t)[2][2]) {
+      const int p = pp[wr * 128 + i * 16 + (lane & 15)];
+      const float4* csp = reinterpret_cast<const float4*>(ra.cs + (size_t)(ra.p0 + p) * 32 + c4);
+      t[0][0] = csp[0];
+      t[0][1] = csp[1];
+      t[1][0] = csp[8];  // dims 16 + c4 ..: 16 float2 = 8 float4 further
+      t[1][1] = csp[9];
+    };
+    load_cs(0, tc);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rl = wr * 128 + i * 16 + (lane & 15);
+      float4 t[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        t[a][0] = tc[a][0];
+        t[a][1] = tc[a][1];
+      }
+      if (i + 1 < 8) load_cs(i + 1, tc);
+      float rs = 1.f;
+      if constexpr (NORM == 1) {
+        float x = ss[i];
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        rs = rsqrtf(x / (float)K + eps);
+      } else if constexpr (NORM == 2) {
+        rs = rsqrtf(ssl[tpar * BM + rl] / (float)K + eps);
+      }
+      const int gr = m0 + rl;
+      if (gr < M) {
+        const int p = pp[rl];
+        uint16_t* dst = h < ra.nh ? ra.q_out + ((size_t)gr * ra.nh + h) * 64
+                                  : ra.k_cache + (((size_t)sp[rl] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {  // dims a·16 + c4 .. +3 and their +32 partners
+          const float cs4[8] = {t[a][0].x, t[a][0].y, t[a][0].z, t[a][0].w, t[a][1].x, t[a][1].y, t[a][1].z, t[a][1].w};
+          uint32_t o1[2], o2[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            float r1[2], r2[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int r = 2 * e + u;
+              const float x1 = bf2f(f2bf(acc[i][2 * a][r] * rs)), x2 = bf2f(f2bf(acc[i][2 * a + 1][r] * rs));
+              const float c = cs4[2 * r], sn = cs4[2 * r + 1];
+              r1[u] = x1 * c - x2 * sn;
+              r2[u] = x2 * c + x1 * sn;
+            }
+            o1[e] = (uint32_t)f2bf(r1[0]) | ((uint32_t)f2bf(r1[1]) << 16);
+            o2[e] = (uint32_t)f2bf(r2[0]) | ((uint32_t)f2bf(r2[1]) << 16);
+          }
+          *reinterpret_cast<uint2*>(dst + a * 16 + c4) = make_uint2(o1[0], o1[1]);
+          *reinterpret_cast<uint2*>(dst + 32 + a * 16 + c4) = make_uint2(o2[0], o2[1]);
+        }
+      }
+    }
+    if (!more) break;
+    zero_acc();
+    v = vn;
+    m0 = m1;
+    n0 = n1;
+    tpar ^= 1;
+  }
+  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail DMAs
+}
+
 // ---------------------------------------------------------------------------
 // Persistent, STAGGERED 256x192 residual GEMM (cfg 35): C = R + A·Wᵀ for the N = 576
 // residual GEMMs (o-proj, down-proj), the residual counterpart of the gate/up kernel's
@@ -1362,6 +1641,8 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  35: 256x192 persistent staggered residual GEMM (gemm256p_resid_kernel, 4 ring buffers,
 //      16x16x32 MFMAs; epi 1 only)   36: 35 without the group stagger (A/B)   37: 35 with
 //      32x32x16 MFMAs   38: 37 with 5 ring buffers
+//  39: (QKV+RoPE only, sg_gemm_qkv_rope) q / k heads through the persistent staggered
+//      256x256 QK+RoPE kernel (gemm256p_qk_rope_kernel), v heads through 28
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1526,6 +1807,22 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
       if (nh % 3 || nkv % 3) return -2;
       return ssin ? launch<128, 192, 2, 2, 3, 2, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
                   : launch<128, 192, 2, 2, 3, 1, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na);
+    case 39: {  // q, k heads: persistent staggered 256x256 QK+RoPE kernel; v heads: cfg 28
+      if (nh % 3 || nkv % 3 || (nh + nkv) % 4 || (ssin && ss_ld % 4 != 0)) return -2;
+      const int Nqk = (nh + nkv) * 64, tm = (M + 255) / 256, tn = Nqk / 256, T = tm * tn;
+      const int grid = T < 256 ? T : 256, gmv = g_group_m > 0 ? g_group_m : 1;
+      if (ssin)
+        hipLaunchKernelGGL((gemm256p_qk_rope_kernel<2>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,
+                           (const uint16_t*)W, M, Nqk, K, eps, tm, tn, gmv, na, ra);
+      else
+        hipLaunchKernelGGL((gemm256p_qk_rope_kernel<1>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,
+                           (const uint16_t*)W, M, Nqk, K, eps, tm, tn, gmv, na, ra);
+      RopeArgs rv = ra;
+      rv.hb = nh + nkv;
+      const uint16_t* Wv = (const uint16_t*)W + (size_t)Nqk * K;
+      return ssin ? launch<128, 192, 2, 2, 3, 2, 2>(A, lda, Wv, nullptr, 64, nullptr, 0, M, nkv * 64, K, eps, stream, rv, xa, na)
+                  : launch<128, 192, 2, 2, 3, 1, 2>(A, lda, Wv, nullptr, 64, nullptr, 0, M, nkv * 64, K, eps, stream, rv, xa, na);
+    }
     default: return -1;
   }
 #undef SG_QKV

@@ -69,3 +69,13 @@ def test_default_gemms_do_not_spill(gemm_resources):
     for p in pats:
         for name, r in _find(gemm_resources, p).items():
             assert int(r["ScratchSize [bytes/lane]"]) == 0, (name, r)
+
+
+@pytest.mark.slow
+def test_persistent_qk_rope_runs_two_waves_per_simd(gemm_resources):
+    """cfg 39's QK+RoPE kernel in the engine's form (NORM 2: row scales from the
+    producer's partials) fits 256 registers without spills: the staggered schedule needs
+    two waves per SIMD."""
+    for name, r in _find(gemm_resources, r"gemm256p_qk_rope_kernelILi2E").items():
+        assert int(r["Occupancy [waves/SIMD]"]) >= 2 and r.get("VGPRs Spill", "0") == "0", (name, r)
+        assert r.get("ScratchSize [bytes/lane]", "0") == "0", (name, r)

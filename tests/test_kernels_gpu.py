@@ -700,3 +700,42 @@ def test_gemm_resid_persistent_matches_cfg28(cfg, M, K):
     else:
         torch.testing.assert_close(xn.float(), x28.float(), atol=2e-2, rtol=1e-2)
         torch.testing.assert_close(ssn, ss28, rtol=2e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("M", [77, 1000, 9216, 70001])
+def test_gemm_qk_rope_persistent_matches_cfg28(M):
+    """cfg 39 (q / k heads through the persistent staggered 256x256 kernel, W rows loaded
+    in the RoPE-pair order, rotation in registers; v heads through cfg 28) writes the
+    same q rows and caches as cfg 28 -- V^T exactly, q / k to the last bf16 rounding
+    (the row scales sum the producer's partials in another order) -- on packed
+    sequences, with the producer's x² partials (NORM 2) and without (NORM 1)."""
+    nh, nkv, D, Lmax, K, p0 = 9, 3, 64, 192, 576, 20
+    g = torch.Generator(device="cpu").manual_seed(71)
+    lens = []
+    while sum(lens) < M:
+        lens.append(int(torch.randint(1, 71, (1,), generator=g)))
+    lens[-1] -= sum(lens) - M
+    lens = [n for n in lens if n > 0]
+    S = len(lens)
+    pos = torch.cat([torch.arange(n) for n in lens]).to(torch.int32).to(DEV)
+    slot = torch.repeat_interleave(torch.randperm(S, generator=g), torch.tensor(lens)).to(torch.int32).to(DEV)
+    a = _bf(M, K, seed=72)
+    wo = _bf(K, K, scale=K ** -0.5, seed=73)
+    x = _bf(M, K, seed=74)
+    ss = ops.ss_buffer((M + 3) // 4 * 4, DEV)
+    ops.gemm(a, wo, epi="resid", resid=x, cfg=28, ss_out=ss)  # x and its rows' x² partials
+    w = _bf((nh + 2 * nkv) * D, K, scale=K ** -0.5, seed=75)
+    cs = ops.rope_table(p0 + Lmax + 1, D, 100000.0, DEV)
+    for ss_in in (ss, None):
+        outs = []
+        for cfg in (28, 39):
+            kc = torch.zeros(S, nkv, Lmax, D, dtype=torch.bfloat16, device=DEV)
+            vt = torch.zeros(*ops.vt_shape(S, nkv, D, Lmax), dtype=torch.bfloat16, device=DEV)
+            q = torch.zeros(M, nh, D, dtype=torch.bfloat16, device=DEV)
+            ops.gemm_qkv_rope(x, w, 1e-5, pos, slot, cs, q, kc, vt, nh, nkv, p0, cfg=cfg, ss_in=ss_in)
+            outs.append((q, kc, vt))
+        (q28, k28, v28), (q39, k39, v39) = outs
+        assert torch.equal(v39, v28)
+        for u, v in ((q39, q28), (k39, k28)):
+            torch.testing.assert_close(u.float(), v.float(), atol=1e-2, rtol=1e-2)
+            assert (u == v).float().mean() > 0.98, (u != v).float().mean()

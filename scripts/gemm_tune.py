@@ -116,7 +116,7 @@ def main() -> int:
                                    "best": min(ok, key=ok.get) if ok else None}
             print(json.dumps({f"{name}_M{M}": res[f"{name}_M{M}"]}), file=sys.stderr, flush=True)
         if not only or "qkv_rope" in only:
-            qcfgs = [c for c in (1, 3, 5, 17, 18, 23, 26, 28, 39) if not pick or c in pick]
+            qcfgs = [c for c in (1, 3, 5, 17, 18, 23, 26, 28, 39, 40, 41) if not pick or c in pick]
             best = {c: math.inf for c in qcfgs}
             for _ in range(a.rounds):
                 for c in qcfgs:

@@ -1262,37 +1262,36 @@ __global__ void __launch_bounds__(512) gemm256p_qk_rope_kernel(const uint16_t* _
       mfma_q(af, 0, 2);
       __builtin_amdgcn_s_barrier();
     }
-    // next tile's row sums (its partials landed: every wave's p4 wait precedes a barrier
-    // this wave has passed); this tile's are in ssl[tpar]
+    // the tile's (cos, sin) table rows into the K-tile buffer the last K-step read (64 KB:
+    // 256 rows x 32 float2) -- the epilogue then loads nothing from global memory, so its
+    // stores never wait (a global load would wait for every older vector-memory op of the
+    // wave, vmcnt retires in order: the next tile's prefetch and the previous stores).
+    // Group 0 first passes one barrier (pairing group 1's last K-step barrier: both
+    // groups' reads of that buffer are done), then each wave DMAs 32 rows, 16-B chunk c
+    // of row r at slot c ^ (r & 15) (conflict-free reads below)
+    if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();
+    const int* pp = psl + (tpar * 2) * BM;
+    const int* sp = psl + (tpar * 2 + 1) * BM;
+    uint16_t* cbuf = smem + ((gk - 1) & 1) * BUF;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const int r = wave * 32 + d * 4 + (lane >> 4), c = (lane & 15) ^ (r & 15);
+      const float2* src = ra.cs + (size_t)(ra.p0 + pp[r]) * 32 + c * 2;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(cbuf + (wave * 32 + d * 4) * 128), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's table rows landed (groups aligned from here)
+    // next tile's row sums (its partials landed before the barrier above); this tile's
+    // are in ssl[tpar]
     if (more) sum_ss(tpar ^ 1);
     // epilogue straight from the accumulators: row m0 + wr·128 + 16i + (lane & 15) of head
     // n0/64 + wc, dims dh + c4 .. +3 (x1) and their partners dh + 32 + c4 .. (x2), dh = 0
     // (fragments 0 / 1) and 16 (fragments 2 / 3).  The unfused path's rounding: bf16
-    // projection, fp32 rotation, bf16.  The next row fragment's (cos, sin) chunks are
-    // requested before this one is rotated (one exposed table round trip per tile)
+    // projection, fp32 rotation, bf16
     const int h = (n0 >> 6) + wc;
-    const int* pp = psl + (tpar * 2) * BM;
-    const int* sp = psl + (tpar * 2 + 1) * BM;
-    float4 tc[2][2];  // [half dh][two float4 = dims c4 .. c4+3 as (cos, sin) pairs]
-    auto load_cs = [&](int i, float4 (&t)[2][2]) {
-      const int p = pp[wr * 128 + i * 16 + (lane & 15)];
-      const float4* csp = reinterpret_cast<const float4*>(ra.cs + (size_t)(ra.p0 + p) * 32 + c4);
-      t[0][0] = csp[0];
-      t[0][1] = csp[1];
-      t[1][0] = csp[8];  // dims 16 + c4 ..: 16 float2 = 8 float4 further
-      t[1][1] = csp[9];
-    };
-    load_cs(0, tc);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int rl = wr * 128 + i * 16 + (lane & 15);
-      float4 t[2][2];
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        t[a][0] = tc[a][0];
-        t[a][1] = tc[a][1];
-      }
-      if (i + 1 < 8) load_cs(i + 1, tc);
       float rs = 1.f;
       if constexpr (NORM == 1) {
         float x = ss[i];
@@ -1309,7 +1308,10 @@ __global__ void __launch_bounds__(512) gemm256p_qk_rope_kernel(const uint16_t* _
                                   : ra.k_cache + (((size_t)sp[rl] * ra.nkv + (h - ra.nh)) * ra.Lmax + p) * 64;
 #pragma unroll
         for (int a = 0; a < 2; ++a) {  // dims a·16 + c4 .. +3 and their +32 partners
-          const float cs4[8] = {t[a][0].x, t[a][0].y, t[a][0].z, t[a][0].w, t[a][1].x, t[a][1].y, t[a][1].z, t[a][1].w};
+          const int c0 = a * 8 + (c4 >> 1);  // 16-B chunk of dims a·16 + c4, c4 + 1
+          const float4 t0 = *reinterpret_cast<const float4*>(cbuf + rl * 128 + ((c0 ^ (rl & 15)) << 3));
+          const float4 t1 = *reinterpret_cast<const float4*>(cbuf + rl * 128 + (((c0 + 1) ^ (rl & 15)) << 3));
+          const float cs4[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
           uint32_t o1[2], o2[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
@@ -1330,14 +1332,16 @@ __global__ void __launch_bounds__(512) gemm256p_qk_rope_kernel(const uint16_t* _
         }
       }
     }
-    if (!more) break;
+    if (!more) break;  // (the groups are aligned: no re-align barrier at the end)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave read its table rows: the next tile's DMAs may refill the buffer
+    if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();  // group 1 falls behind again
     zero_acc();
     v = vn;
     m0 = m1;
     n0 = n1;
     tpar ^= 1;
   }
-  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tail DMAs
 }
 
@@ -1642,7 +1646,8 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //      16x16x32 MFMAs; epi 1 only)   36: 35 without the group stagger (A/B)   37: 35 with
 //      32x32x16 MFMAs   38: 37 with 5 ring buffers
 //  39: (QKV+RoPE only, sg_gemm_qkv_rope) q / k heads through the persistent staggered
-//      256x256 QK+RoPE kernel (gemm256p_qk_rope_kernel), v heads through 28
+//      256x256 QK+RoPE kernel (gemm256p_qk_rope_kernel), v heads through 28; 40 / 41: its
+//      q / k part / v part alone (timing A/B only: partial outputs)
 // Returns 0, or <0 on a shape the kernel does not cover (the launch is then
 // skipped — the Python wrapper raises).
 extern "C" {
@@ -1807,16 +1812,20 @@ int sg_gemm_qkv_rope(const void* A, int lda, const void* W, int M, int K, float 
       if (nh % 3 || nkv % 3) return -2;
       return ssin ? launch<128, 192, 2, 2, 3, 2, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na)
                   : launch<128, 192, 2, 2, 3, 1, 2>(A, lda, W, nullptr, 64, nullptr, 0, M, N, K, eps, stream, ra, xa, na);
-    case 39: {  // q, k heads: persistent staggered 256x256 QK+RoPE kernel; v heads: cfg 28
+    case 39:    // q, k heads: persistent staggered 256x256 QK+RoPE kernel; v heads: cfg 28
+    case 40:    // (timing A/B: the q, k part alone)
+    case 41: {  // (timing A/B: the v part alone)
       if (nh % 3 || nkv % 3 || (nh + nkv) % 4 || (ssin && ss_ld % 4 != 0)) return -2;
       const int Nqk = (nh + nkv) * 64, tm = (M + 255) / 256, tn = Nqk / 256, T = tm * tn;
       const int grid = T < 256 ? T : 256, gmv = g_group_m > 0 ? g_group_m : 1;
-      if (ssin)
+      if (cfg == 41) {
+      } else if (ssin)
         hipLaunchKernelGGL((gemm256p_qk_rope_kernel<2>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,
                            (const uint16_t*)W, M, Nqk, K, eps, tm, tn, gmv, na, ra);
       else
         hipLaunchKernelGGL((gemm256p_qk_rope_kernel<1>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,
                            (const uint16_t*)W, M, Nqk, K, eps, tm, tn, gmv, na, ra);
+      if (cfg == 40) return 0;
       RopeArgs rv = ra;
       rv.hb = nh + nkv;
       const uint16_t* Wv = (const uint16_t*)W + (size_t)Nqk * K;

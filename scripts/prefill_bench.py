@@ -28,6 +28,7 @@ def main() -> None:
     p.add_argument("--P0", type=int, default=20)
     p.add_argument("--iters", type=int, default=50)
     p.add_argument("--out", default=None)
+    p.add_argument("--impls", default="per_head,gqa,gqa_ks2,multi,st,st32,st64,st32pf,stpf,st64pf")
     a = p.parse_args()
     lines = [run(a, int(n)) for n in a.nseq.split(",")]
     if a.out:
@@ -57,7 +58,7 @@ def run(a, nseq: int) -> dict:
     scale = 1 / math.sqrt(D)
     res = {"nseq": a.nseq, "tokens": T, "nh": a.nh, "nkv": a.nkv, "P0": a.P0}
     outs = {}
-    for impl in ("per_head", "gqa", "gqa_ks2", "multi", "st", "st32", "st64", "st32pf", "stpf"):
+    for impl in a.impls.split(","):
         ops.set_prefill_impl("gqa" if impl.startswith("gqa") else impl)
         ops.set_prefill_split(2 if impl == "gqa_ks2" else 1)
         out = torch.empty(T, a.nh * D, dtype=torch.bfloat16, device=dev)
@@ -74,17 +75,13 @@ def run(a, nseq: int) -> dict:
         outs[impl] = out.float()
     ops.set_prefill_impl("auto")
     ops.set_prefill_split(1)
-    res["max_abs_diff"] = float((outs["gqa"] - outs["per_head"]).abs().max())
-    res["max_abs_diff_ks2"] = float((outs["gqa_ks2"] - outs["gqa"]).abs().max())
-    res["speedup"] = round(res["per_head_us"] / res["gqa_us"], 3)
-    res["speedup_ks2"] = round(res["gqa_us"] / res["gqa_ks2_us"], 3)
-    res["max_abs_diff_multi"] = float((outs["multi"] - outs["per_head"]).abs().max())
-    res["speedup_multi_vs_per_head"] = round(res["per_head_us"] / res["multi_us"], 3)
-    for impl in ("st", "st32", "st64", "st32pf", "stpf"):
-        res[f"max_abs_diff_{impl}"] = float((outs[impl] - outs["per_head"]).abs().max())
-        res[f"speedup_{impl}_vs_per_head"] = round(res["per_head_us"] / res[f"{impl}_us"], 3)
-    res["st32pf_bitwise_st32"] = bool(torch.equal(outs["st32pf"], outs["st32"]))
-    res["stpf_bitwise_st"] = bool(torch.equal(outs["stpf"], outs["st"]))
+    ref = "per_head" if "per_head" in outs else next(iter(outs))
+    for impl in outs:
+        res[f"max_abs_diff_{impl}"] = float((outs[impl] - outs[ref]).abs().max())
+        res[f"speedup_{impl}_vs_{ref}"] = round(res[f"{ref}_us"] / res[f"{impl}_us"], 3)
+    for a_, b_ in (("st32pf", "st32"), ("stpf", "st"), ("st64pf", "st64")):
+        if a_ in outs and b_ in outs:
+            res[f"{a_}_bitwise_{b_}"] = bool(torch.equal(outs[a_], outs[b_]))
     print(json.dumps(res), flush=True)
     return res
 

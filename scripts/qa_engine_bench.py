@@ -27,6 +27,8 @@ def main() -> int:
     p.add_argument("--request", type=int, default=512)
     p.add_argument("--packed", type=int, default=1, choices=[0, 1],
                    help="1: each request one engine unit (submit_packed, the engine server's path)")
+    p.add_argument("--prefill-attn", default="auto,st32,st32pf",
+                   help="comma list of EngineConfig.prefill_attn values (ops.set_prefill_impl): one line each")
     a = p.parse_args()
 
     import numpy as np
@@ -67,8 +69,11 @@ def main() -> int:
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    for mt in (int(x) for x in str(a.qa_max_tokens).split(",")):
-        eng = QAEngine(w, tok, EngineConfig(max_slots=a.max_slots, qa_max_tokens=mt, qa_split_prefill=a.split_prefill))
+    import itertools
+
+    for mt, pa in itertools.product((int(x) for x in str(a.qa_max_tokens).split(",")), a.prefill_attn.split(",")):
+        eng = QAEngine(w, tok, EngineConfig(max_slots=a.max_slots, qa_max_tokens=mt, qa_split_prefill=a.split_prefill,
+                                            prefill_attn=pa))
         run_once(eng)  # warm-up (allocator, first launches)
         eng.reset_stats()
         times = [run_once(eng) for _ in range(a.reps)]
@@ -79,7 +84,7 @@ def main() -> int:
                "batches": st.prefill_batches, "msgs_per_batch": round(st.prefill_seqs / max(1, st.prefill_batches), 1),
                "gpu_idle_s": round(st.gpu_idle_s, 4), "host_prefill_s": round(st.prefill_s, 3),
                "harvest_wait_s": round(st.harvest_wait_s, 3),
-               "config": {"packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": mt,
+               "config": {"prefill_attn": pa, "packed": bool(a.packed), "max_slots": a.max_slots, "qa_max_tokens": mt,
                           "qa_split_prefill": a.split_prefill}}
         print(json.dumps(out), flush=True)
         del eng

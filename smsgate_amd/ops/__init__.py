@@ -563,7 +563,7 @@ def set_prefill_impl(impl: str) -> None:
     ``"st"`` / ``"st32"`` / ``"st64"`` (transposed register formulation, S^T = K·Q^T and
     O^T = V^T·P^T: one wave per 16 / 32 / 64 (query, head) columns of one KV head,
     P never leaves registers)."""
-    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3, "st": 4, "st32": 5, "st64": 6, "st32pf": 7, "stpf": 8}[impl])
+    load_library().sg_set_prefill_impl({"gqa": 0, "per_head": 1, "auto": 2, "multi": 3, "st": 4, "st32": 5, "st64": 6, "st32pf": 7, "stpf": 8, "st64pf": 9}[impl])
 
 
 def set_attn_merge(on: bool) -> None:

@@ -2200,7 +2200,7 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
     // st32 with the one-tile register prefetch; stpf (impl 8): st with it
     // auto from 1 024 sequences (the qa engine's packed batches: 2 211 / 4 422 sequences of
     // ~50 rows): st64, 103.4 / 198.7 us vs 110.0 / 210.0 for st32 (profiles/r05_prefill_qa.jsonl)
-    const bool wide = g_prefill_impl == 6 || (g_prefill_impl == 2 && nseq >= 1024);
+    const bool wide = g_prefill_impl == 6 || g_prefill_impl == 9 || (g_prefill_impl == 2 && nseq >= 1024);
     const int ncb = (g_prefill_impl == 4 || g_prefill_impl == 8) ? 1 : wide ? 4 : 2, qpw = 16 * ncb / G;
     dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
 #define SG_PST(NC, PFV)                                                                                             \
@@ -2209,6 +2209,7 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
                      (const uint16_t*)pvt, P0, P0pad, (uint16_t*)out, nh, nkv, Lmax, sl2, attn_merge(P0))
     if (g_prefill_impl == 7) SG_PST(2, 1);
     else if (g_prefill_impl == 8) SG_PST(1, 1);
+    else if (g_prefill_impl == 9) SG_PST(4, 1);  // st64 with the register prefetch (A/B)
     else if (ncb == 2) SG_PST(2, 0);
     else if (ncb == 4) SG_PST(4, 0);
     else SG_PST(1, 0);

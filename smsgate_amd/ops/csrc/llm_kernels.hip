@@ -2198,9 +2198,11 @@ int sg_attn_prefill(const void* q, const int* cu_q, const int* q_start, const in
   if ((g_prefill_impl == 2 || g_prefill_impl >= 4) && G <= 16) {
     // st64 (impl 6): 64 columns, half the waves re-read a sequence's keys; st32pf (impl 7):
     // st32 with the one-tile register prefetch; stpf (impl 8): st with it
-    // auto from 1 024 sequences (the qa engine's packed batches: 2 211 / 4 422 sequences of
-    // ~50 rows): st64, 103.4 / 198.7 us vs 110.0 / 210.0 for st32 (profiles/r05_prefill_qa.jsonl)
-    const bool wide = g_prefill_impl == 6 || g_prefill_impl == 9 || (g_prefill_impl == 2 && nseq >= 1024);
+    // auto = st32 at every batch size: round 5 picked st64 from 1 024 sequences on a
+    // microbench (103.4 / 198.7 vs 110.0 / 210.0 us, profiles/r05_prefill_qa.jsonl); the
+    // engine itself runs faster with st32 (69.6 vs 69.2 k msgs/s, three identical reps
+    // each, interleaved, profiles/r06n_engine_prefill_attn_ab.jsonl)
+    const bool wide = g_prefill_impl == 6 || g_prefill_impl == 9;
     const int ncb = (g_prefill_impl == 4 || g_prefill_impl == 8) ? 1 : wide ? 4 : 2, qpw = 16 * ncb / G;
     dim3 grid((max_q + qpw - 1) / qpw, nseq, nkv);
 #define SG_PST(NC, PFV)                                                                                             \

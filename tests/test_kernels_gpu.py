@@ -86,7 +86,7 @@ def _ref_seq_attention(qb, own_k, own_v, pk, pv, P0, q_off, scale):
     return out
 
 
-@pytest.mark.parametrize("impl", ["gqa", "gqa_ks2", "per_head", "multi", "st", "st32", "st64", "st32pf", "stpf"])
+@pytest.mark.parametrize("impl", ["gqa", "gqa_ks2", "per_head", "multi", "st", "st32", "st64", "st32pf", "stpf", "st64pf"])
 @pytest.mark.parametrize("heads", [(9, 3), (4, 2), (4, 4), (8, 2)])
 @pytest.mark.parametrize("P0", [0, 20, 75])  # 0 / 20: merged prefix + own key stream; 75: prefix tiles first
 def test_attn_prefill(P0, heads, impl):

@@ -62,6 +62,8 @@ class _PubAcks(SequenceABC):
         return PubAck(s, q)
 
     def __eq__(self, other) -> bool:
+        if not isinstance(other, SequenceABC):
+            return NotImplemented
         return list(self) == list(other)
 
 

@@ -185,6 +185,8 @@ class _MergedAcks(SequenceABC):
         return self._flat[i]
 
     def __eq__(self, other) -> bool:
+        if not isinstance(other, SequenceABC):
+            return NotImplemented
         return list(self) == list(other)
 
 

@@ -248,12 +248,13 @@ GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 6
               19: (256, 256), 20: (256, 256), 21: (128, 96), 22: (64, 96), 23: (128, 192), 24: (256, 96),
               25: (128, 96), 26: (64, 192), 27: (32, 96), 28: (128, 192), 29: (256, 96),
               30: (128, 96), 31: (64, 96), 32: (256, 192), 33: (128, 192), 34: (256, 192),
-              35: (256, 192), 36: (256, 192), 37: (256, 192), 38: (256, 192)}
+              35: (256, 192), 36: (256, 192), 37: (256, 192), 38: (256, 192), 42: (256, 256)}
 # cfg -> (BM, BN); 4..8 are 3/4-stage pipelines, 9..16 are 8-wave blocks (14..16: 3/4 stages),
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 # a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
-# SwiGLU kernel (gemm256_swiglu_kernel), 20 its persistent form
-GEMM_SWIGLU_ONLY = {10, 19, 20}
+# SwiGLU kernel (gemm256_swiglu_kernel), 20 its persistent form, 42 = 20 with both A register
+# sets (A/B; producer row scales only)
+GEMM_SWIGLU_ONLY = {10, 19, 20, 42}
 # 21..26: 48-wide wave tiles (96 / 192-wide blocks) for the N = 576 residual GEMMs: no SwiGLU
 # 28 / 29: 128x192 / 256x96 with 4 waves (64x96 wave tiles); 30 / 31: 128x96 / 64x96 with 8 waves
 # 32: 256x192 with 8 waves (64x96 wave tiles); 33 / 34: 128x192 / 256x192 with BK 32 and 4 stages

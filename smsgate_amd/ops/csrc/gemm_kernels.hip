@@ -860,7 +860,10 @@ __global__ void __launch_bounds__(512) gemm256_swiglu_kernel(const uint16_t* __r
 // except (a) p4 re-reads A rows 0-63 (one A register set: the kernel then fits 256
 // VGPRs without spills) and (b) the last K-tile's p2 wait, vmcnt(6): the 2 partial
 // DMAs of p1 precede A_top.
-template <int NORM>
+//
+// TWOA (cfg 42, A/B): both A register sets kept (rows 0-63 from p1 through p4, rows
+// 64-127 in p2 / p3), so p4 issues no LDS reads -- 32 VGPRs more per lane.
+template <int NORM, bool TWOA = false>
 __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __restrict__ A, int lda,
                                                              const uint16_t* __restrict__ W, uint16_t* C, int ldc,
                                                              int M, int N, int K, float eps, int tiles_m, int tiles_n,
@@ -926,6 +929,7 @@ __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __
     }
   };
   bf16x8 af[2][4], bq[2][2];  // ONE A set (p4 re-reads rows 0-63): 32 VGPRs fewer, no spills
+  bf16x8 ab[2][4];             // TWOA: rows 64-127 (unused otherwise)
   auto read_a = [&](bf16x8 (&dst)[2][4], const uint16_t* base, int r0) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -1000,22 +1004,25 @@ __global__ void __launch_bounds__(512) gemm256p_swiglu_kernel(const uint16_t* __
       mfma_q(af, 0, 0);
       __builtin_amdgcn_s_barrier();
       // p2: rows 64-127 x lo
-      read_a(af, abase, 64);
+      if constexpr (TWOA) read_a(ab, abase, 64);
+      else read_a(af, abase, 64);
       stage(nb, 1, sm, sn, sk);
       if (NORM == 2 && last) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // + this p1's partial DMAs
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                    // Bhi of THIS K-tile landed
       mid();
-      mfma_q(af, 4, 0);
+      if constexpr (TWOA) mfma_q(ab, 4, 0);
+      else mfma_q(af, 4, 0);
       __builtin_amdgcn_s_barrier();
       // p3: rows 64-127 x hi
       read_b(buf + 3 * HALF);
       stage(nb, 2, sm, sn, sk);
       mid();
-      mfma_q(af, 4, 2);
+      if constexpr (TWOA) mfma_q(ab, 4, 2);
+      else mfma_q(af, 4, 2);
       __builtin_amdgcn_s_barrier();
       // p4: rows 0-63 x hi (re-read: WAR-safe, the next DMA into this A half is staged
       // after the lagging group's p4 barrier)
-      read_a(af, abase, 0);
+      if constexpr (!TWOA) read_a(af, abase, 0);
       stage(nb, 3, sm, sn, sk);
       asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // next K-tile's A_top, A_bot, Blo (+ partials)
       mid();
@@ -1645,6 +1652,7 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  35: 256x192 persistent staggered residual GEMM (gemm256p_resid_kernel, 4 ring buffers,
 //      16x16x32 MFMAs; epi 1 only)   36: 35 without the group stagger (A/B)   37: 35 with
 //      32x32x16 MFMAs   38: 37 with 5 ring buffers
+//  42: 20 with both A register sets (no p4 LDS re-read; NORM 2 only, A/B)
 //  39: (QKV+RoPE only, sg_gemm_qkv_rope) q / k heads through the persistent staggered
 //      256x256 QK+RoPE kernel (gemm256p_qk_rope_kernel), v heads through 28; 40 / 41: its
 //      q / k part / v part alone (timing A/B only: partial outputs)
@@ -1679,6 +1687,8 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
   static const int BNs[39] = {128, 64, 128, 64, 64, 64, 64, 128, 128, 128, 256, 256, 64, 128, 128, 256, 64, 64, 64,
                              256, 256, 96, 96, 192, 96, 96, 192, 96, 192, 96, 96, 96, 192, 192, 192, 192, 192,
                              192, 192};
+  const bool twoa = cfg == 42;  // A/B form of 20
+  if (twoa) cfg = 20;
   if (cfg < 0 || cfg > 38) return -1;
   if (M <= 0 || K % BK != 0 || N % BNs[cfg] != 0 || lda % 8 != 0 || ldc % 8 != 0 || (R && ldr % 8 != 0)) return -2;
   if (epi == 1 && !R) return -2;
@@ -1701,13 +1711,15 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
   if (cfg == 20) {  // persistent form: one block per CU (256 CUs), tiles overlapped
     if (epi != 2) return -3;
     if (norm == 2 && ss_ld % 4 != 0) return -2;
+    if (twoa && norm != 2) return -3;
     const int tm = (M + 255) / 256, tn = N / 256, T = tm * tn;
     const int grid = T < 256 ? T : 256;
     const int gmv = g_group_m > 0 ? g_group_m : 1;
-#define SG_256P(NM)                                                                                                   \
-  hipLaunchKernelGGL((gemm256p_swiglu_kernel<NM>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,       \
+#define SG_256P(...)                                                                                                  \
+  hipLaunchKernelGGL((gemm256p_swiglu_kernel<__VA_ARGS__>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,       \
                      (const uint16_t*)W, (uint16_t*)C, ldc, M, N, K, eps, tm, tn, gmv, na)
-    if (norm == 2) SG_256P(2);
+    if (norm == 2 && twoa) SG_256P(2, true);
+    else if (norm == 2) SG_256P(2);
     else if (norm == 1) SG_256P(1);
     else SG_256P(0);
 #undef SG_256P

@@ -64,7 +64,7 @@ def test_big_tile_gemms_run_two_waves_per_simd(gemm_resources, epi_norm):
 @pytest.mark.slow
 def test_default_gemms_do_not_spill(gemm_resources):
     """The persistent SwiGLU GEMM (cfg 20) and the residual / QKV tiles of the qa engine."""
-    pats = [r"gemm256p_swiglu_kernelILi[012]E", r"gemm_fused_kernelILi128ELi96ELi2ELi2ELi1ELi0ELi2ELi0E",
+    pats = [r"gemm256p_swiglu_kernelILi[012]ELb0E", r"gemm_fused_kernelILi128ELi96ELi2ELi2ELi1ELi0ELi2ELi0E",
             r"gemm_fused_kernelILi64ELi96ELi2ELi2ELi1ELi0ELi2ELi0E", r"gemm_fused_kernelILi128ELi64ELi2ELi2ELi3E"]
     for p in pats:
         for name, r in _find(gemm_resources, p).items():
@@ -73,9 +73,11 @@ def test_default_gemms_do_not_spill(gemm_resources):
 
 @pytest.mark.slow
 def test_persistent_qk_rope_runs_two_waves_per_simd(gemm_resources):
-    """cfg 39's QK+RoPE kernel in the engine's form (NORM 2: row scales from the
-    producer's partials) fits 256 registers without spills: the staggered schedule needs
-    two waves per SIMD."""
+    """cfg 39's QK+RoPE kernel (an A/B form, not the default) in the engine's form (NORM 2:
+    row scales from the producer's partials) keeps two waves per SIMD, which the staggered
+    schedule needs.  Since the (cos, sin) rows moved into LDS it spills 7 loop-invariant
+    registers (ISA: stored in the prologue, reloaded once per tile after the K loop), so
+    the bound here is that handful, not zero."""
     for name, r in _find(gemm_resources, r"gemm256p_qk_rope_kernelILi2E").items():
-        assert int(r["Occupancy [waves/SIMD]"]) >= 2 and r.get("VGPRs Spill", "0") == "0", (name, r)
-        assert r.get("ScratchSize [bytes/lane]", "0") == "0", (name, r)
+        assert int(r["Occupancy [waves/SIMD]"]) >= 2, (name, r)
+        assert int(r.get("ScratchSize [bytes/lane]", "0")) <= 32, (name, r)

@@ -702,6 +702,20 @@ def test_gemm_resid_persistent_matches_cfg28(cfg, M, K):
         torch.testing.assert_close(ssn, ss28, rtol=2e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("M", [77, 4099, 110592])
+def test_gemm_swiglu_two_a_sets_match_cfg20(M):
+    """cfg 42 (cfg 20 keeping both A register sets: p4 reads no LDS) issues the same
+    MFMAs in the same order, so its SwiGLU output is bit-identical to cfg 20's."""
+    H, I = 576, 1536
+    x = _bf(M, H, seed=91)
+    w = _bf(2 * I, H, scale=H ** -0.5, seed=92)
+    ss = ops.ss_buffer(M, DEV)
+    ss[:9] = torch.rand(9, M, device=DEV)
+    o20 = ops.gemm(x, w, epi="swiglu", norm_eps=1e-5, cfg=20, ss_in=ss)
+    o42 = ops.gemm(x, w, epi="swiglu", norm_eps=1e-5, cfg=42, ss_in=ss)
+    assert torch.equal(o42, o20)
+
+
 @pytest.mark.parametrize("M", [77, 1000, 9216, 70001])
 def test_gemm_qk_rope_persistent_matches_cfg28(M):
     """cfg 39 (q / k heads through the persistent staggered 256x256 kernel, W rows loaded

@@ -253,7 +253,7 @@ GEMM_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64), 4: (128, 6
 # 17/18: 32-row tiles (2 / 4 stages) for small decode buckets
 # a 256x256 plain-output tile does not fit the LDS staging; 19 is the staggered 8-wave
 # SwiGLU kernel (gemm256_swiglu_kernel), 20 its persistent form, 42 = 20 with both A register
-# sets (A/B; producer row scales only)
+# sets (A/B)
 GEMM_SWIGLU_ONLY = {10, 19, 20, 42}
 # 21..26: 48-wide wave tiles (96 / 192-wide blocks) for the N = 576 residual GEMMs: no SwiGLU
 # 28 / 29: 128x192 / 256x96 with 4 waves (64x96 wave tiles); 30 / 31: 128x96 / 64x96 with 8 waves

@@ -1652,7 +1652,7 @@ int dispatch_resid(int epi, int norm, const void* A, int lda, const void* W, voi
 //  35: 256x192 persistent staggered residual GEMM (gemm256p_resid_kernel, 4 ring buffers,
 //      16x16x32 MFMAs; epi 1 only)   36: 35 without the group stagger (A/B)   37: 35 with
 //      32x32x16 MFMAs   38: 37 with 5 ring buffers
-//  42: 20 with both A register sets (no p4 LDS re-read; NORM 2 only, A/B)
+//  42: 20 with both A register sets (no p4 LDS re-read; A/B)
 //  39: (QKV+RoPE only, sg_gemm_qkv_rope) q / k heads through the persistent staggered
 //      256x256 QK+RoPE kernel (gemm256p_qk_rope_kernel), v heads through 28; 40 / 41: its
 //      q / k part / v part alone (timing A/B only: partial outputs)
@@ -1711,15 +1711,17 @@ int sg_gemm(const void* A, int lda, const void* W, void* C, int ldc, const void*
   if (cfg == 20) {  // persistent form: one block per CU (256 CUs), tiles overlapped
     if (epi != 2) return -3;
     if (norm == 2 && ss_ld % 4 != 0) return -2;
-    if (twoa && norm != 2) return -3;
     const int tm = (M + 255) / 256, tn = N / 256, T = tm * tn;
     const int grid = T < 256 ? T : 256;
     const int gmv = g_group_m > 0 ? g_group_m : 1;
 #define SG_256P(...)                                                                                                  \
   hipLaunchKernelGGL((gemm256p_swiglu_kernel<__VA_ARGS__>), dim3(grid), dim3(512), 0, stream, (const uint16_t*)A, lda,       \
                      (const uint16_t*)W, (uint16_t*)C, ldc, M, N, K, eps, tm, tn, gmv, na)
-    if (norm == 2 && twoa) SG_256P(2, true);
-    else if (norm == 2) SG_256P(2);
+    if (twoa) {
+      if (norm == 2) SG_256P(2, true);
+      else if (norm == 1) SG_256P(1, true);
+      else SG_256P(0, true);
+    } else if (norm == 2) SG_256P(2);
     else if (norm == 1) SG_256P(1);
     else SG_256P(0);
 #undef SG_256P

@@ -710,7 +710,7 @@ def test_gemm_swiglu_two_a_sets_match_cfg20(M):
     x = _bf(M, H, seed=91)
     w = _bf(2 * I, H, scale=H ** -0.5, seed=92)
     ss = ops.ss_buffer(M, DEV)
-    ss[:9] = torch.rand(9, M, device=DEV)
+    ss[:9, :M] = torch.rand(9, M, device=DEV)
     o20 = ops.gemm(x, w, epi="swiglu", norm_eps=1e-5, cfg=20, ss_in=ss)
     o42 = ops.gemm(x, w, epi="swiglu", norm_eps=1e-5, cfg=42, ss_in=ss)
     assert torch.equal(o42, o20)

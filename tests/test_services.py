@@ -268,6 +268,34 @@ def test_notifier_cycle_sends_report_and_denies(tmp_path, arun):
     assert saved["last_ts"] == st.data["last_ts"] and st.last_ts > now - timedelta(days=2)
 
 
+def test_chart_totals_and_files(tmp_path):
+    """The report's data and both files (dashboard/main.py:146-197 parity: daily sums per
+    merchant, empty merchants as "Unknown", the newest record's balance), rendered without
+    a plotting stack: inline-SVG HTML and a Pillow JPEG."""
+    from datetime import date
+
+    from smsgate_amd.services.notifier import build_chart, daily_totals
+    recs = [{"amount": "100.5", "datetime": "2024-03-01 10:00:00.000Z", "merchant": "Shop A", "balance": "1 000,50",
+             "currency": "AMD"},
+            {"amount": "20", "datetime": "2024-03-01T12:00:00", "merchant": ""},
+            {"amount": "-30", "datetime": "2024-03-02 09:00:00Z", "merchant": "Shop A"},
+            {"amount": "7", "datetime": "2024-03-02 23:00:00Z", "merchant": "null", "balance": "55", "currency": "RUB"},
+            {"amount": "oops", "datetime": "2024-03-02 10:00:00Z", "merchant": "bad"},
+            {"amount": "5", "datetime": "not a date", "merchant": "bad"}]
+    days, merchants, totals, bal = daily_totals(recs)
+    assert days == [date(2024, 3, 1), date(2024, 3, 2)]
+    assert merchants == ["Shop A", "Unknown"]  # by total: 70.5 vs 27
+    assert totals == {(date(2024, 3, 1), "Shop A"): 100.5, (date(2024, 3, 1), "Unknown"): 20.0,
+                      (date(2024, 3, 2), "Shop A"): -30.0, (date(2024, 3, 2), "Unknown"): 7.0}
+    assert bal == (55.0, "RUB")
+    html, img, bal2 = build_chart(recs, "Статистика", tmp_path)
+    page = html.read_text(encoding="utf-8")
+    assert bal2 == bal and page.count("<rect") == 4 + 2 and "Статистика" in page and "Продавец" in page
+    assert img is not None and img.read_bytes()[:3] == b"\xff\xd8\xff"  # a JPEG
+    with pytest.raises(ValueError):
+        build_chart([{"amount": None, "datetime": None}], "t", tmp_path)
+
+
 # --------------------------------------------------------------------------- MCP server
 @pytest.fixture
 def mcp_tools(tmp_path):

@@ -123,6 +123,3 @@ def _pdeathsig() -> None:  # runs in the child between fork and exec
 
     ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
 
-
-def busd_path() -> Path:
-    return BUSD

@@ -14,7 +14,6 @@ references the numerics tests compare against.
 from __future__ import annotations
 
 import ctypes
-import math
 import os
 from typing import Optional
 
@@ -1194,6 +1193,3 @@ def ref_gemm(a: torch.Tensor, w: torch.Tensor, *, epi: str = "store", norm_eps: 
         return resid.float() + y
     return y
 
-
-def default_scale(head_dim: int) -> float:
-    return 1.0 / math.sqrt(head_dim)

@@ -550,8 +550,8 @@ def pin_replica(args, local: int, procs, brokers):
 
     node_gpus = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
     # the node's brokers share 2 + one core per GPU (they are single-threaded event loops,
-    # but 29 of them carry ~0.3 - 0.8 cores per GPU together: a core each would take 29
-    # cores from GPU 0's NUMA node)
+    # but the 33 of a node carry ~0.3 - 0.8 cores per GPU together: a core each would take
+    # 33 cores from GPU 0's NUMA node)
     p = plan(local, node_gpus, broker_cores=min(len(brokers), 2 + node_gpus) if brokers else 0)
     if p is None:
         return {"pinned": False, "why": "no GPU topology in sysfs"}

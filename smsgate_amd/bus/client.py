@@ -10,7 +10,6 @@ from urllib.parse import urlparse
 from .base import (
     Acker,
     Bus,
-    BusError,
     BusUnavailable,
     bus_error,
     ConsumerInfo,

@@ -14,7 +14,6 @@ from typing import Dict, List, Optional, Sequence, Tuple
 from .base import (
     Acker,
     Bus,
-    BusError,
     BusUnavailable,
     ConsumerConfig,
     ConsumerInfo,

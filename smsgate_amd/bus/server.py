@@ -13,7 +13,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import struct
-from typing import Any, Dict, Optional
+from typing import Any, Optional
 from urllib.parse import urlparse
 
 import msgpack

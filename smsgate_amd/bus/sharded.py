@@ -56,12 +56,15 @@ __all__ = ["ShardedBus", "shard_of", "parse_members", "Router", "NODE_PARTITIONS
 # door (smsgate-busd --http-listen: ~56 k single-SMS requests/s each,
 # profiles/r03_ingest_bench.jsonl: 20 doors take 2x an 8 x 70 k node), sms.parsed
 # (parser -> writer) and sms.processing (one publish per parsed SMS, consumed
-# downstream) over four each (a member carries ~0.9 / 4 of the node rate: 2x headroom
-# on one ~316 k msgs/s broker up to an 8 x 80 k node) -- and the low-rate subjects
-# (sms.failed, sms.categorized) on one more.  tests/test_broker_capacity.py sizes EVERY
-# member and the doors at 2x against the latest measured headline.
-# Fewer GPUs on a node: node_partitions() scales it down.
-NODE_PARTITIONS = {SUBJECT_RAW: 20, SUBJECT_PARSED: 4, SUBJECT_PROCESSING: 4}
+# downstream) over six each (a member carries ~0.9 / 6 of the node rate, 83 k msgs/s at
+# an 8 x 69.5 k node: 2x headroom on one broker down to 167 k msgs/s -- the
+# 16-consumer load generator measured 204-248 k with the journal on disk on a busy
+# 8-vCPU build box, 316 k on a quiet one; four partitions needed 250 k) -- and the
+# low-rate subjects (sms.failed, sms.categorized) on one more.
+# tests/test_broker_capacity.py sizes EVERY member and the doors at 2x against the
+# latest measured headline.  Fewer GPUs on a node:
+# node_partitions() scales it down.
+NODE_PARTITIONS = {SUBJECT_RAW: 20, SUBJECT_PARSED: 6, SUBJECT_PROCESSING: 6}
 NODE_GPUS = 8
 
 

@@ -17,7 +17,7 @@ must be asked for (``random_init=True``, ``engine-server --random-init``).
 from __future__ import annotations
 
 import os
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, List, Optional, Sequence
 
 from ...runtime.errors import TransientError
 from .base import BackendError, ExtractResult, ParserBackend

@@ -25,7 +25,7 @@ import datetime as _dt
 import json
 import uuid
 from decimal import Decimal
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Dict, Optional
 
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, StreamingResponse

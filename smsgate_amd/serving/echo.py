@@ -10,7 +10,7 @@ the multi-process tests); it is never a fallback for the GPU engine.
 """
 from __future__ import annotations
 
-from typing import Any, List, Sequence, Tuple
+from typing import Any, List, Tuple
 
 import numpy as np
 

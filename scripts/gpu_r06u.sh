@@ -1,6 +1,5 @@
 #!/bin/bash
 # round 6, call U: the whole GPU suite, smoke() and the headline bench after the 33-broker layout
-# (cfg 42 A/B, spill-bound test)
 set -o pipefail
 O=gpurun_out/r06u
 mkdir -p $O
